@@ -1,0 +1,212 @@
+"""Typed experiment configuration: dataclasses + YAML files + Hydra-like ``key=value`` overrides.
+
+Reference: configuration is hard-coded dicts (``src/CFed/Classical_FL.py:161-173``,
+``src/QFed/testEncoder.py:64-72``) and function defaults (``src/CFed/Preprocess.py:137-138``,
+``Classical_FL.py:41,104-110``); ROADMAP plans Hydra (``ROADMAP.md:16,70``).  Hydra is not
+installed, so this module gives the same ergonomics (YAML + dotted CLI overrides) with
+dataclasses.  The reference key names are kept verbatim: ``raw_folder, processed_folder,
+digits, val_split, num_clients, partition_type, alpha, num_rounds, local_epochs,
+learning_rate, batch_size``.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+from dataclasses import dataclass, field, asdict
+from typing import Any, Optional
+
+import yaml
+
+
+@dataclass
+class DataConfig:
+    dataset: str = "synthetic"          # mnist | synthetic | iris
+    raw_folder: str = "./dataset/raw"
+    processed_folder: str = "./dataset/processed"
+    digits: tuple = (0, 1, 2)
+    val_split: float = 0.1
+    num_clients: int = 4
+    partition_type: str = "iid"         # iid | non_iid (Dirichlet)
+    alpha: float = 0.5                  # Dirichlet concentration
+    features: str = "pool"              # pool | pca | downsample | raw
+    n_features: int = 4
+    samples_per_client: int = 256       # synthetic data size per client
+    test_samples: int = 512
+
+
+@dataclass
+class ModelConfig:
+    kind: str = "vqc"                   # vqc | tinycnn
+    n_qubits: int = 4
+    n_layers: int = 2
+    n_classes: int = 3
+    feature_map: str = "ry"             # ry | rx | rz (angle encoding basis)
+    feature_scale: str = "scale"        # scale (RY(alpha*x), ROADMAP:126) | minmax (qAngle.py:36-41)
+    alpha: float = 3.141592653589793
+    entangler: str = "chain"            # chain | ring | none
+    readout_scale: float = 1.0          # initial a in logit = a<Z> + b
+    init_std: float = 0.1
+    state_dtype: str = "fp32"           # fp32 | bf16 (statevector storage between kernel passes)
+
+
+@dataclass
+class TrainConfig:
+    num_rounds: int = 30
+    local_epochs: int = 1
+    local_steps: int = 0                # if >0, overrides local_epochs with a fixed step count
+    learning_rate: float = 0.05
+    batch_size: int = 32
+    optimizer: str = "adam"             # adam | sgd | spsa
+    momentum: float = 0.9
+    grad_method: str = "adjoint"        # adjoint | param_shift | spsa | autograd
+    client_fraction: float = 1.0        # ROADMAP:35,106 client sampling
+    dropout_prob: float = 0.0           # simulated client dropouts (ROADMAP:91)
+    aggregate: str = "delta"            # delta (ROADMAP:36) | weights (Classical_FL.py:66-81)
+    wrap_angles: bool = True            # wrap angle deltas to [-pi, pi] (ROADMAP:37)
+    weighting: str = "samples"          # samples | uniform
+    eval_every: int = 1
+    seed: int = 42
+
+
+@dataclass
+class PrivacyConfig:
+    dp: bool = False
+    clip_norm: float = 1.0              # C (ROADMAP:50)
+    noise_multiplier: float = 1.0       # sigma (ROADMAP:51)
+    delta: float = 1e-5
+    secure_agg: bool = False
+    secagg_bits: int = 48               # fixed-point ring Z_{2^bits} for exact mask cancellation
+    secagg_scale: float = 2.0 ** 24
+
+
+@dataclass
+class NoiseConfig:
+    """Quantum noise model (ROADMAP.md:64-73)."""
+    kind: str = "none"                  # none | depolarizing | amplitude
+    p: float = 0.0                      # depolarizing probability per gate
+    gamma: float = 0.0                  # amplitude damping per gate
+    readout_p01: float = 0.0            # P(read 1 | 0)
+    readout_p10: float = 0.0            # P(read 0 | 1)
+    shots: int = 0                      # 0 = exact expectation
+    trajectories: int = 1
+
+
+@dataclass
+class RuntimeConfig:
+    device: str = "auto"                # auto | cpu | cuda
+    backend: str = "auto"               # auto | hip | torch
+    dist_backend: str = "auto"          # auto | nccl (RCCL) | gloo
+    checkpoint_dir: str = ""
+    checkpoint_every: int = 0
+    resume: bool = False
+    metrics_path: str = ""
+    log_every: int = 5
+    overlap_comm: bool = True
+    use_graphs: bool = False
+
+
+@dataclass
+class ExperimentConfig:
+    name: str = "qfedx"
+    data: DataConfig = field(default_factory=DataConfig)
+    model: ModelConfig = field(default_factory=ModelConfig)
+    train: TrainConfig = field(default_factory=TrainConfig)
+    privacy: PrivacyConfig = field(default_factory=PrivacyConfig)
+    noise: NoiseConfig = field(default_factory=NoiseConfig)
+    runtime: RuntimeConfig = field(default_factory=RuntimeConfig)
+
+    def to_dict(self) -> dict:
+        return asdict(self)
+
+    def to_json(self) -> str:
+        return json.dumps(self.to_dict(), sort_keys=True)
+
+
+def _coerce(value: str, target: Any):
+    if isinstance(target, bool):
+        return value.lower() in ("1", "true", "yes", "on")
+    if isinstance(target, int) and not isinstance(target, bool):
+        return int(float(value))
+    if isinstance(target, float):
+        return float(value)
+    if isinstance(target, tuple):
+        v = yaml.safe_load(value)
+        return tuple(v) if isinstance(v, (list, tuple)) else (v,)
+    if target is None:
+        return yaml.safe_load(value)
+    return value
+
+
+def _merge(dc, updates: dict):
+    for k, v in updates.items():
+        if not hasattr(dc, k):
+            raise KeyError(f"unknown config key '{k}' in {type(dc).__name__}")
+        cur = getattr(dc, k)
+        if dataclasses.is_dataclass(cur):
+            _merge(cur, v)
+        else:
+            if isinstance(cur, tuple) and isinstance(v, list):
+                v = tuple(v)
+            setattr(dc, k, v)
+    return dc
+
+
+def apply_overrides(cfg: ExperimentConfig, overrides: list[str]) -> ExperimentConfig:
+    """Apply ``section.key=value`` overrides (Hydra style). Reference flat keys resolve too."""
+    flat_alias = _flat_aliases()
+    for ov in overrides:
+        if "=" not in ov:
+            raise ValueError(f"override '{ov}' is not key=value")
+        key, value = ov.split("=", 1)
+        key = key.strip().lstrip("+")
+        if "." not in key and key in flat_alias:
+            key = flat_alias[key]
+        obj = cfg
+        parts = key.split(".")
+        for p in parts[:-1]:
+            obj = getattr(obj, p)
+        if not hasattr(obj, parts[-1]):
+            raise KeyError(f"unknown config key '{key}'")
+        setattr(obj, parts[-1], _coerce(value, getattr(obj, parts[-1])))
+    return cfg
+
+
+def _flat_aliases() -> dict:
+    out = {}
+    for sec in ("data", "model", "train", "privacy", "noise", "runtime"):
+        dc = getattr(ExperimentConfig(), sec)
+        for f in dataclasses.fields(dc):
+            out.setdefault(f.name, f"{sec}.{f.name}")
+    return out
+
+
+def load_config(path: Optional[str] = None, overrides: Optional[list[str]] = None) -> ExperimentConfig:
+    cfg = ExperimentConfig()
+    if path:
+        with open(path) as f:
+            raw = yaml.safe_load(f) or {}
+        # accept flat reference-style dicts too
+        nested: dict = {}
+        aliases = _flat_aliases()
+        for k, v in raw.items():
+            if isinstance(v, dict) and k in ("data", "model", "train", "privacy", "noise", "runtime"):
+                nested.setdefault(k, {}).update(v)
+            elif k == "name":
+                nested["name"] = v
+            elif k in aliases:
+                sec, key = aliases[k].split(".")
+                nested.setdefault(sec, {})[key] = v
+            else:
+                raise KeyError(f"unknown config key '{k}' in {path}")
+        name = nested.pop("name", None)
+        _merge(cfg, nested)
+        if name:
+            cfg.name = name
+    if overrides:
+        apply_overrides(cfg, overrides)
+    return cfg
+
+
+def save_config(cfg: ExperimentConfig, path: str) -> None:
+    with open(path, "w") as f:
+        yaml.safe_dump(json.loads(cfg.to_json()), f, sort_keys=True)

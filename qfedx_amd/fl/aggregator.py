@@ -1,0 +1,128 @@
+"""Server-side aggregation: Delta -> angle wrap -> DP clip+noise -> SecAgg mask -> weighted sum.
+
+Reference FedAvg (``Classical_FL.py:66-81``): sum_k (n_k / sum n) * theta_k over each
+state_dict key, averaging WEIGHTS.  ROADMAP (``:36-37``) wants clients to return Delta-theta with
+angle deltas wrapped to [-pi, pi].  Both are provided: ``aggregate='delta'`` (default) and
+``aggregate='weights'`` (no wrap; algebraically identical to the reference formula).
+
+Per round on each rank (SURVEY §3.2, K8/K17/K18/K20 fused on GPU):
+    local = sum_{k on this rank, fixed order} w_k * priv(wrap(theta_k - theta_g))   (+ masks)
+    global = all_reduce(local)             # one message per rank, RCCL over xGMI
+    theta_g += global[:P] / global[P]
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ..privacy.dp import clip_and_noise
+from ..privacy.secure_agg import SecureAggregator
+
+
+def wrap_angles(d: torch.Tensor) -> torch.Tensor:
+    """Wrap to [-pi, pi) (ROADMAP.md:37 periodicity of rotation angles)."""
+    return torch.remainder(d + math.pi, 2 * math.pi) - math.pi
+
+
+def federated_averaging(client_updates):
+    """Reference-compatible FedAvg over ``[(state_dict, n_samples), ...]`` (``Classical_FL.py:66-81``).
+
+    Fixed: the reference's ``+=`` of a float into ``zeros_like`` breaks on integer buffers; here
+    non-floating entries (e.g. BatchNorm counters) are taken from the first client.
+    """
+    total = sum(n for _, n in client_updates)
+    first = client_updates[0][0]
+    out = {}
+    for key, ref in first.items():
+        if not torch.is_floating_point(ref):
+            out[key] = ref.clone()
+            continue
+        acc = torch.zeros_like(ref, dtype=torch.float64)
+        for params, n in client_updates:
+            acc += (n / total) * params[key].double()
+        out[key] = acc.to(ref.dtype)
+    return out
+
+
+class Aggregator:
+    def __init__(self, n_params: int, angle_mask: Optional[torch.Tensor], device, backend: str = "torch",
+                 aggregate: str = "delta", wrap: bool = True, dp: bool = False, clip_norm: float = 1.0,
+                 noise_multiplier: float = 1.0, secure_agg: bool = False, secagg: Optional[SecureAggregator] = None,
+                 seed: int = 0):
+        self.P = n_params
+        self.device = torch.device(device)
+        self.backend = backend
+        self.aggregate = aggregate
+        self.wrap = wrap and aggregate == "delta" and angle_mask is not None
+        self.angle_mask = (angle_mask.to(self.device).bool() if angle_mask is not None
+                           else torch.zeros(n_params, dtype=torch.bool, device=self.device))
+        self.dp = dp
+        self.clip_norm = clip_norm
+        self.noise_multiplier = noise_multiplier
+        self.secure_agg = secure_agg
+        self.secagg = secagg
+        self.seed = seed
+        self.last_norms: Optional[torch.Tensor] = None
+
+    def local_reduce(self, theta_k: torch.Tensor, theta_g: torch.Tensor, weights: torch.Tensor,
+                     round_num: int, client_ids: list, participants: Optional[list] = None,
+                     dropped: Optional[list] = None) -> torch.Tensor:
+        """This rank's contribution [P+1] = [sum_k w_k priv(Delta_k) | sum_k w_k].
+
+        float64 normally; int64 ring elements (mod 2^bits, masked) under secure aggregation.
+        ``dropped`` clients (subset of participants, possibly on other ranks) had agreed masks but
+        never deliver: survivors on this rank add the orphan-mask corrections.
+        """
+        if self.backend == "hip" and not self.secure_agg:
+            from ..ops import fedavg_hip
+            out, norms = fedavg_hip.fused_local_reduce(
+                theta_k, theta_g, weights, self.angle_mask, client_ids, round_num, self.seed,
+                wrap=self.wrap, dp=self.dp, clip_norm=self.clip_norm,
+                noise_multiplier=self.noise_multiplier)
+            self.last_norms = norms
+            return out
+        delta = theta_k.double() - theta_g.double()[None, :]
+        if self.wrap:
+            delta = torch.where(self.angle_mask[None, :], wrap_angles(delta), delta)
+        if self.dp:
+            delta, norms = clip_and_noise(delta, self.clip_norm, self.noise_multiplier, self.seed,
+                                          round_num, client_ids)
+            self.last_norms = norms
+        else:
+            self.last_norms = delta.norm(dim=-1)
+        w = weights.double().to(delta.device)
+        weighted = torch.cat([delta * w[:, None], w[:, None]], -1)    # [K, P+1]
+        if not self.secure_agg:
+            out = torch.zeros(self.P + 1, dtype=torch.float64, device=delta.device)
+            for k in range(weighted.shape[0]):                         # fixed client order
+                out += weighted[k]
+            return out
+        sa = self.secagg
+        parts = list(participants if participants is not None else client_ids)
+        total = torch.zeros(self.P + 1, dtype=torch.int64, device=delta.device)
+        for k, cid in enumerate(client_ids):
+            total = torch.remainder(total + sa.mask(weighted[k], int(cid), parts, round_num), sa.modulus)
+        from ..privacy.secure_agg import prg_mask
+        for d in dropped or []:
+            for cid in client_ids:
+                m = prg_mask(sa.registry.pair_seed(int(cid), int(d)), round_num, self.P + 1, sa.bits, delta.device)
+                total = total - m if int(cid) < int(d) else total + m
+            total = torch.remainder(total, sa.modulus)
+        return total
+
+    def finalize(self, reduced: torch.Tensor) -> tuple[torch.Tensor, float]:
+        """Decode the all-reduced [P+1] vector -> (mean update [P] float64, weight sum)."""
+        if self.secure_agg:
+            from ..privacy.secure_agg import decode_fixed
+            vals = decode_fixed(reduced, self.secagg.scale, self.secagg.bits)
+        else:
+            vals = reduced.double()
+        wsum = float(vals[self.P])
+        return vals[: self.P] / max(wsum, 1e-300), wsum
+
+    def apply(self, theta_g: torch.Tensor, mean_update: torch.Tensor, server_lr: float = 1.0) -> torch.Tensor:
+        new = theta_g.double() + server_lr * mean_update.to(theta_g.device)
+        return new.to(theta_g.dtype)
+

@@ -1,0 +1,69 @@
+"""Client-batched local optimizers on flat parameter buffers [K, P] (one row per client).
+
+Reference: a fresh ``SGD(lr, momentum=0.9)`` per client per round (``Classical_FL.py:53``), so
+momentum resets every round.  ROADMAP.md:38 adds Adam and SPSA.  State is allocated per round
+(reset) by default, matching the reference; ``persistent=True`` keeps it across rounds.
+
+On GPU the update runs as one fused kernel over all clients (``qfx_adam_step`` /
+``qfx_sgdm_step`` in ``csrc/fedavg.hip``); the torch version here is the CPU path / oracle.
+Rows with ``active[k] == 0`` are left untouched (clients whose local epochs are exhausted).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+
+class BatchedOptimizer:
+    def __init__(self, kind: str, shape, device, lr: float, momentum: float = 0.9,
+                 betas=(0.9, 0.999), eps: float = 1e-8, backend: str = "torch"):
+        self.kind = kind.lower()
+        self.lr = lr
+        self.momentum = momentum
+        self.b1, self.b2 = betas
+        self.eps = eps
+        self.backend = backend
+        self.m = torch.zeros(shape, dtype=torch.float32, device=device)
+        self.v = torch.zeros(shape, dtype=torch.float32, device=device) if self.kind == "adam" else None
+        self.t = torch.zeros(shape[0], dtype=torch.float32, device=device)
+
+    def reset(self) -> None:
+        self.m.zero_()
+        if self.v is not None:
+            self.v.zero_()
+        self.t.zero_()
+
+    @torch.no_grad()
+    def step(self, params: torch.Tensor, grads: torch.Tensor, active: Optional[torch.Tensor] = None) -> None:
+        if active is None:
+            active = torch.ones(params.shape[0], device=params.device)
+        active = active.to(params.dtype)
+        if self.backend == "hip":
+            from ..ops import fedavg_hip
+            if self.kind == "adam":
+                fedavg_hip.adam_step(params, grads, self.m, self.v, self.t, active, self.lr, self.b1,
+                                     self.b2, self.eps)
+            else:
+                fedavg_hip.sgdm_step(params, grads, self.m, active, self.lr, self.momentum)
+            return
+        a = active[:, None]
+        if self.kind == "adam":
+            self.t += active
+            t = self.t.clamp(min=1.0)[:, None]
+            m_new = self.b1 * self.m + (1 - self.b1) * grads
+            v_new = self.b2 * self.v + (1 - self.b2) * grads * grads
+            self.m = torch.where(a > 0, m_new, self.m)
+            self.v = torch.where(a > 0, v_new, self.v)
+            mhat = self.m / (1 - self.b1 ** t)
+            vhat = self.v / (1 - self.b2 ** t)
+            params -= a * self.lr * mhat / (vhat.sqrt() + self.eps)
+        elif self.kind in ("sgd", "sgdm", "spsa"):
+            # torch.optim.SGD semantics: buf = mu*buf + g ; p -= lr*buf (first step buf = g)
+            first = (self.t == 0)[:, None]
+            buf = torch.where(first, grads, self.momentum * self.m + grads)
+            self.m = torch.where(a > 0, buf, self.m)
+            self.t += active
+            params -= a * self.lr * self.m
+        else:
+            raise ValueError(f"unknown optimizer '{self.kind}'")

@@ -1,0 +1,220 @@
+"""Federated round loop ("server.py", ROADMAP.md:34-39; reference ``federated_learning``,
+``Classical_FL.py:104-157``).
+
+Reference behaviour kept: round-0 evaluation, ``num_rounds`` rounds of (all clients train ->
+FedAvg -> load -> test eval), an accuracy history list, progress print every 5 rounds, return
+``{'model', 'accuracies'}``.  Redesigned for MI355X:
+
+* every rank holds an identical global parameter vector; clients are sharded over ranks and a
+  rank's participating clients train as ONE batch (no per-client Python loop);
+* client sampling (fraction q) and dropouts are keyed by (seed, round) so all ranks agree without
+  communication; dropped clients simply contribute weight 0 (SecAgg orphan masks are removed);
+* aggregation = fused local reduce on-device + ONE all-reduce of [update | weight | metrics];
+* the test set is sharded over ranks and metrics are all-reduced;
+* RDP accountant step + epsilon per round, JSONL metrics, checkpoint every K rounds, resume.
+"""
+from __future__ import annotations
+
+import json
+import math
+import time
+from typing import Optional
+
+import torch
+
+from ..parallel.dist import FusedRoundBuffer, World, all_reduce_, barrier, broadcast_, shard_clients
+from ..privacy.accountant import RDPAccountant
+from ..privacy.secure_agg import SecureAggregator
+from ..utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
+from ..utils.logging import MetricsWriter, get_logger
+from ..utils.seeding import generator, np_rng
+from ..utils.timing import PhaseTimer
+from .aggregator import Aggregator
+from .trainer import ShardStore
+
+
+def sample_participants(num_clients: int, fraction: float, seed: int, round_num: int) -> list[int]:
+    if fraction >= 1.0:
+        return list(range(num_clients))
+    m = max(1, int(round(fraction * num_clients)))
+    g = generator(seed, "sample_clients", round_num)
+    return sorted(torch.randperm(num_clients, generator=g)[:m].tolist())
+
+
+def sample_dropouts(participants: list[int], prob: float, seed: int, round_num: int) -> list[int]:
+    if prob <= 0:
+        return []
+    out = []
+    for c in participants:
+        if np_rng(seed, "client_drop", round_num, c).random() < prob:
+            out.append(c)
+    return out
+
+
+class FederatedRunner:
+    """Drives federated training for one model adapter (VQC or TinyCNN) on this rank."""
+
+    def __init__(self, cfg, adapter, data, world: World, device: torch.device, backend: str):
+        self.cfg = cfg
+        self.adapter = adapter
+        self.data = data
+        self.world = world
+        self.device = device
+        self.backend = backend
+        self.log = get_logger()
+        t, p = cfg.train, cfg.privacy
+        self.num_clients = data.num_clients
+        self.local_ids = list(data.client_ids)
+        self.store = ShardStore(data.clients, data.client_ids, device)
+        self.P = adapter.n_params
+        self.secagg = SecureAggregator(t.seed, p.secagg_bits, p.secagg_scale) if p.secure_agg else None
+        if self.secagg is not None:
+            self.secagg.register(range(self.num_clients))
+        self.aggregator = Aggregator(self.P, adapter.angle_mask(), device, backend, t.aggregate,
+                                     t.wrap_angles, p.dp, p.clip_norm, p.noise_multiplier, p.secure_agg,
+                                     self.secagg, t.seed)
+        self.accountant = RDPAccountant()
+        # test shard for this rank
+        Xt, yt = data.test
+        sl = shard_clients(int(yt.shape[0]), world.world_size, world.rank)
+        self.X_test = Xt[sl[0]: sl[-1] + 1].to(device) if sl else Xt[:0].to(device)
+        self.y_test = yt[sl[0]: sl[-1] + 1].to(device) if sl else yt[:0].to(device)
+        self.metrics = MetricsWriter(cfg.runtime.metrics_path, world.rank, cfg.to_dict())
+        self.timer = PhaseTimer(device)
+        self.start_round = 0
+        self.history: list[dict] = []
+        self.params = adapter.init_params(t.seed).to(device)
+        broadcast_(self.params, world)                      # CC1: identical theta on all ranks
+
+    # ------------------------------------------------------------------ eval
+    @torch.no_grad()
+    def evaluate(self, params: Optional[torch.Tensor] = None) -> dict:
+        params = self.params if params is None else params
+        loss_sum, correct, n = self.adapter.evaluate(params, self.X_test, self.y_test)
+        buf = torch.tensor([loss_sum, correct, n], dtype=torch.float64, device=self.device)
+        all_reduce_(buf, self.world)
+        n_tot = max(float(buf[2]), 1.0)
+        return {"test_acc": float(buf[1]) / n_tot, "test_loss": float(buf[0]) / n_tot}
+
+    # ------------------------------------------------------------------ checkpoint
+    def save(self, round_num: int) -> None:
+        rt = self.cfg.runtime
+        if rt.checkpoint_dir and self.world.is_main:
+            save_checkpoint(rt.checkpoint_dir, round_num, {
+                "global_state": self.adapter.state_dict(self.params),
+                "accountant": json.dumps(self.accountant.state_dict()),
+                "config": self.cfg.to_dict(),
+                "metrics": self.history,
+                "seed": torch.tensor(self.cfg.train.seed),
+            })
+        barrier(self.world)
+
+    def maybe_resume(self) -> None:
+        rt = self.cfg.runtime
+        if not (rt.resume and rt.checkpoint_dir):
+            return
+        path = latest_checkpoint(rt.checkpoint_dir)
+        if path is None:
+            return
+        ck = load_checkpoint(path)
+        self.params = self.adapter.from_state_dict(ck["global_state"]).to(self.device)
+        self.accountant.load_state_dict(json.loads(ck["accountant"]))
+        self.history = list(ck.get("metrics", []))
+        self.start_round = int(ck["round"])
+        self.log.info(f"resumed from {path} at round {self.start_round}")
+
+    # ------------------------------------------------------------------ main loop
+    def run_round(self, r: int) -> dict:
+        t = self.cfg.train
+        p = self.cfg.privacy
+        participants = sample_participants(self.num_clients, t.client_fraction, t.seed, r)
+        dropped = sample_dropouts(participants, t.dropout_prob, t.seed, r)
+        dropped_set = set(dropped)
+        local_part = [i for i, c in enumerate(self.local_ids) if c in set(participants)]
+        local_alive = [i for i in local_part if self.local_ids[i] not in dropped_set]
+        t0 = time.perf_counter()
+        with self.timer.phase("local_train"):
+            res = self.adapter.trainer.run_round(self.store, local_alive, self.params, r)
+        with self.timer.phase("aggregate"):
+            if local_alive:
+                if t.weighting == "uniform":
+                    w = torch.ones(len(local_alive), dtype=torch.float64)
+                else:
+                    w = res["n_samples"].double()
+                contrib = self.aggregator.local_reduce(
+                    res["params"], self.params, w.to(self.device), r,
+                    [self.local_ids[i] for i in local_alive],
+                    participants=[c for c in participants], dropped=dropped)
+            else:
+                dt = torch.int64 if p.secure_agg else torch.float64
+                contrib = torch.zeros(self.P + 1, dtype=dt, device=self.device)
+            loss_sum = res.get("loss_sum", 0.0)
+            correct = res.get("correct", 0.0)
+            metrics = torch.stack([torch.as_tensor(loss_sum, dtype=torch.float64, device=self.device),
+                                   torch.as_tensor(correct, dtype=torch.float64, device=self.device),
+                                   torch.tensor(float(res.get("samples", 0.0)), dtype=torch.float64, device=self.device),
+                                   torch.tensor(float(res.get("steps", 0)), dtype=torch.float64, device=self.device)])
+        with self.timer.phase("comm"):
+            if p.secure_agg:
+                all_reduce_(contrib, self.world)          # int64 ring elements: exact, mod later
+                all_reduce_(metrics, self.world)
+                mean_upd, wsum = self.aggregator.finalize(contrib)
+            else:
+                fb = FusedRoundBuffer(self.P, metrics.numel(), self.device)
+                buf = fb.pack(contrib[: self.P], contrib[self.P], metrics)
+                all_reduce_(buf, self.world)              # ONE collective per round (CC2+CC3)
+                red, wsum_t, metrics = fb.unpack()
+                wsum = float(wsum_t)
+                mean_upd = red / max(wsum, 1e-300)
+        if wsum > 0:
+            self.params = self.aggregator.apply(self.params, mean_upd)
+        if p.dp:
+            q = len(participants) / self.num_clients
+            self.accountant.step(q, p.noise_multiplier, 1)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        m = metrics.double().cpu().tolist()
+        rec = {"round": r + 1, "participants": len(participants), "dropped": len(dropped),
+               "train_loss": m[0] / max(m[2], 1.0) if m[2] else float("nan"),
+               "train_acc": m[1] / max(m[2], 1.0) if m[2] else float("nan"),
+               "local_steps": int(m[3]), "round_time_s": dt,
+               "local_steps_per_s": m[3] / dt if dt > 0 else 0.0,
+               "comm_bytes_per_rank": int((self.P + 1 + 4) * 8),
+               "upload_bytes": int(len(participants) - len(dropped)) * (self.P + 1) * 4}
+        if p.dp:
+            rec["epsilon"] = self.accountant.get_epsilon(p.delta)
+        return rec
+
+    def run(self) -> dict:
+        t = self.cfg.train
+        self.maybe_resume()
+        accs = []
+        if self.start_round == 0:
+            ev = self.evaluate()
+            accs.append(ev["test_acc"])
+            if self.world.is_main:
+                self.log.info(f"Round 0: Test Accuracy = {ev['test_acc']:.4f}")
+            self.metrics.log({"round": 0, **ev})
+        else:
+            accs = [h.get("test_acc") for h in self.history if "test_acc" in h]
+        t_start = time.perf_counter()
+        for r in range(self.start_round, t.num_rounds):
+            rec = self.run_round(r)
+            if (r + 1) % max(1, t.eval_every) == 0 or r + 1 == t.num_rounds:
+                rec.update(self.evaluate())
+                accs.append(rec["test_acc"])
+            self.history.append(rec)
+            self.metrics.log(rec)
+            if self.world.is_main and ((r + 1) % self.cfg.runtime.log_every == 0 or r + 1 == t.num_rounds):
+                eps = f" eps={rec['epsilon']:.3f}" if "epsilon" in rec else ""
+                self.log.info(f"Round {r + 1}: Test Accuracy = {rec.get('test_acc', float('nan')):.4f} "
+                              f"train_loss={rec['train_loss']:.4f} {rec['local_steps_per_s']:.1f} local-steps/s{eps}")
+            ck = self.cfg.runtime.checkpoint_every
+            if ck and (r + 1) % ck == 0:
+                self.save(r + 1)
+        wall = time.perf_counter() - t_start
+        self.metrics.close()
+        return {"model": self.adapter.state_dict(self.params), "params": self.params, "accuracies": accs,
+                "history": self.history, "wall_s": wall, "phases_ms": self.timer.resolve(),
+                "epsilon": self.accountant.get_epsilon(self.cfg.privacy.delta) if self.cfg.privacy.dp else None}

@@ -1,0 +1,153 @@
+"""Client-batched local training ("client.py", ROADMAP.md:34-36; reference ``client_update``,
+``Classical_FL.py:40-64``).
+
+All of a rank's participating clients train in LOCKSTEP: step s of every client is one batched
+kernel sequence over [K clients x B samples].  Clients keep their own minibatch order (Philox-keyed
+permutation per (seed, round, client, epoch)), their own optimizer state row, and their own step
+budget: with ``local_epochs`` E, client k runs E * ceil(n_k / B) steps (exactly the reference's
+``epochs x len(dataloader)``); shorter clients are masked out of later steps, and a last partial
+batch is handled by per-sample loss weights (padding rows weigh 0).  ``local_steps > 0`` instead
+fixes the step count for every client (benchmarks).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from ..utils.seeding import generator
+from .optim import BatchedOptimizer
+
+
+class ShardStore:
+    """Device-resident padded shards: X [K, Nmax, F], y [K, Nmax], counts [K]."""
+
+    def __init__(self, shards: list, client_ids: list, device, feature_fn=None):
+        self.client_ids = list(client_ids)
+        self.device = torch.device(device)
+        K = len(shards)
+        counts = [int(s[1].shape[0]) for s in shards]
+        nmax = max(counts) if counts else 0
+        feat_shape = tuple(shards[0][0].shape[1:]) if K else ()
+        X = torch.zeros((K, nmax) + feat_shape, dtype=torch.float32)
+        y = torch.zeros(K, nmax, dtype=torch.int64)
+        for k, (Xs, ys) in enumerate(shards):
+            X[k, : counts[k]] = Xs.float()
+            y[k, : counts[k]] = ys.long()
+        if feature_fn is not None:
+            X = feature_fn(X)
+        self.X = X.to(self.device)
+        self.y = y.to(self.device)
+        self.counts = torch.tensor(counts, dtype=torch.int64)
+        self.nmax = nmax
+
+    def __len__(self) -> int:
+        return len(self.client_ids)
+
+
+class BatchPlan:
+    """Per-round minibatch schedule for a set of clients (host-side index tables, keyed RNG)."""
+
+    def __init__(self, counts: torch.Tensor, client_ids: list, batch_size: int, round_num: int,
+                 seed: int, local_epochs: int = 1, local_steps: int = 0, shuffle: bool = True):
+        self.B = batch_size
+        K = len(client_ids)
+        self.steps_per_client = []
+        perms = []
+        for k, cid in enumerate(client_ids):
+            n = int(counts[k])
+            if local_steps > 0:
+                steps = local_steps
+                epochs = math.ceil(steps * batch_size / max(n, 1))
+            else:
+                steps = local_epochs * math.ceil(n / batch_size)
+                epochs = local_epochs
+            self.steps_per_client.append(steps)
+            order = []
+            for e in range(max(epochs, 1)):
+                if shuffle:
+                    order.append(torch.randperm(n, generator=generator(seed, "batch", round_num, int(cid), e)))
+                else:
+                    order.append(torch.arange(n))
+            perms.append(torch.cat(order) if order else torch.zeros(0, dtype=torch.int64))
+        self.max_steps = max(self.steps_per_client) if K else 0
+        self.local_steps = local_steps
+        # index [S, K, B] into each client's padded shard and per-sample weights [S, K, B]
+        S = self.max_steps
+        idx = torch.zeros(S, K, batch_size, dtype=torch.int64)
+        wts = torch.zeros(S, K, batch_size, dtype=torch.float32)
+        active = torch.zeros(S, K, dtype=torch.float32)
+        for k in range(K):
+            n = int(counts[k])
+            p = perms[k]
+            for s in range(self.steps_per_client[k]):
+                if local_steps > 0:
+                    sel = p[(s * batch_size) % max(len(p), 1):][:batch_size]
+                    if sel.numel() < batch_size:  # wrap around the epoch boundary
+                        sel = torch.cat([sel, p[: batch_size - sel.numel()]])
+                    valid = batch_size
+                else:
+                    ep, j = divmod(s, math.ceil(n / batch_size))
+                    sel = p[ep * n + j * batch_size: ep * n + min((j + 1) * batch_size, n)]
+                    valid = sel.numel()
+                idx[s, k, :valid] = sel[:valid]
+                wts[s, k, :valid] = 1.0 / valid
+                active[s, k] = 1.0
+        self.idx, self.wts, self.active = idx, wts, active
+
+
+class VQCClientTrainer:
+    """Runs one federated round of local training for a rank's clients (batched)."""
+
+    def __init__(self, spec, engine, train_cfg, device, backend: str = "torch"):
+        self.spec = spec
+        self.engine = engine
+        self.cfg = train_cfg
+        self.device = torch.device(device)
+        self.backend = backend
+
+    def encode(self, X: torch.Tensor) -> torch.Tensor:
+        return self.spec.encode_features(X)
+
+    def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int) -> dict:
+        """Train clients ``store[local_idx]`` from the global params; returns their params + metrics."""
+        cfg = self.cfg
+        K = len(local_idx)
+        P = theta_g.numel()
+        if K == 0:
+            return {"params": torch.zeros(0, P, device=self.device), "loss_sum": 0.0, "correct": 0.0,
+                    "samples": 0.0, "steps": 0}
+        li = torch.tensor(local_idx, dtype=torch.int64)
+        cids = [store.client_ids[i] for i in local_idx]
+        plan = BatchPlan(store.counts[li], cids, cfg.batch_size, round_num, cfg.seed,
+                         cfg.local_epochs, cfg.local_steps)
+        params = theta_g.to(self.device).float()[None, :].repeat(K, 1).contiguous()
+        opt_kind = "sgd" if cfg.optimizer == "spsa" else cfg.optimizer
+        opt = BatchedOptimizer(opt_kind, (K, P), self.device, cfg.learning_rate, cfg.momentum,
+                               backend=self.backend)
+        method = "spsa" if cfg.optimizer == "spsa" else cfg.grad_method
+        Xs = store.X[li.to(store.X.device)]
+        ys = store.y[li.to(store.y.device)]
+        idx_d = plan.idx.to(self.device)
+        wts_d = plan.wts.to(self.device)
+        act_d = plan.active.to(self.device)
+        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+        correct = torch.zeros((), dtype=torch.float64, device=self.device)
+        samples = 0.0
+        kar = torch.arange(K, device=self.device)[:, None]
+        for s in range(plan.max_steps):
+            bi = idx_d[s]
+            xb = Xs[kar, bi]                     # [K, B, F]
+            yb = ys[kar, bi]
+            xang = self.encode(xb)
+            res = self.engine.loss_and_grads(xang, yb, wts_d[s], params, method,
+                                             rng_keys=(cfg.seed, round_num, s))
+            opt.step(params, res["grad"], act_d[s])
+            nvalid = (wts_d[s] > 0).sum(-1).double() * act_d[s].double()
+            loss_sum += (res["loss"].double() * nvalid).sum()
+            correct += (res["correct"].double() * act_d[s].double()).sum()
+            samples += float((plan.wts[s] > 0).sum())
+        return {"params": params, "loss_sum": loss_sum, "correct": correct, "samples": samples,
+                "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
+                "n_samples": store.counts[li].to(torch.float64)}

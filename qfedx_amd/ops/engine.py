@@ -1,0 +1,177 @@
+"""Client-batched VQC compute engine (forward readout, loss, gradients).
+
+One call processes ALL of a rank's clients at once: inputs are shaped [K, B, ...] (K clients x B
+samples) with per-client parameters [K, P_total] - the client axis is a batch axis of the kernels,
+replacing the reference's sequential per-client Python loop (``Classical_FL.py:132-140``).
+
+Backends:
+  * ``hip``   - gfx950 pass kernels of the in-tree extension (``ops/statevec_hip.py``)
+  * ``torch`` - the portable program executor (``ops/statevec_torch.py``), CPU path + oracle
+
+Gradient methods (ROADMAP.md:23,38,130-135): ``adjoint`` (default; 1 forward + 1 reverse sweep),
+``param_shift`` (2 shifted circuits per rotation gate, batched), ``spsa`` (2 perturbed losses),
+``autograd`` (torch complex autograd; CPU cross-check only).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from ..models.vqc import VQCSpec, logits_from_expz
+from ..utils.seeding import generator
+from .statevec_torch import TorchProgram, slot_grads
+
+
+def ce_readout(expz: torch.Tensor, y: torch.Tensor, wmask: torch.Tensor, a: torch.Tensor, b: torch.Tensor):
+    """Weighted CE on logits a<Z>+b.  expz [K,B,C], y [K,B], wmask [K,B] (per-sample loss weight).
+
+    Returns loss [K], dL/dexpz [K,B,C], grad_a [K,C], grad_b [K,C], correct [K] (weighted count of
+    argmax hits, counting samples with wmask>0 as 1).
+    """
+    logits = logits_from_expz(expz, a, b)
+    logp = torch.log_softmax(logits, -1)
+    nll = -logp.gather(-1, y.unsqueeze(-1)).squeeze(-1)
+    loss = (nll * wmask).sum(-1)
+    p = logp.exp()
+    dlog = (p - F.one_hot(y, expz.shape[-1]).to(p)) * wmask.unsqueeze(-1)
+    w = dlog * a.unsqueeze(-2)
+    grad_a = (dlog * expz).sum(-2)
+    grad_b = dlog.sum(-2)
+    correct = ((logits.argmax(-1) == y) & (wmask > 0)).sum(-1).to(expz.dtype)
+    return loss, w, grad_a, grad_b, correct
+
+
+class VQCEngine:
+    def __init__(self, spec: VQCSpec, device="cpu", backend: str = "torch", state_dtype: str = "fp32"):
+        self.spec = spec
+        self.device = torch.device(device)
+        self.backend = backend
+        ops, coef = spec.program()
+        self.ops = torch.from_numpy(ops)
+        self.coef = torch.from_numpy(coef)
+        self.n_slots = spec.n_theta + spec.n_qubits
+        self.state_dtype = state_dtype
+        if backend == "torch":
+            self.prog = TorchProgram(ops, coef, spec.n_qubits, self.device)
+            self.hip = None
+        elif backend == "hip":
+            from .statevec_hip import HipProgram
+            self.hip = HipProgram(ops, coef, spec.n_qubits, spec.readout, self.device,
+                                  n_theta=spec.n_theta, state_dtype=state_dtype)
+            self.prog = TorchProgram(ops, coef, spec.n_qubits, self.device)  # for param-shift/autograd
+        else:
+            raise ValueError(f"unknown backend '{backend}'")
+
+    # ------------------------------------------------------------------ helpers
+    def _rows(self, xang: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
+        K, B, n = xang.shape
+        th = theta[:, None, :].expand(K, B, theta.shape[-1])
+        return torch.cat([th, xang.to(th.dtype)], -1).reshape(K * B, -1)
+
+    # ------------------------------------------------------------------ forward
+    @torch.no_grad()
+    def expz(self, xang: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
+        """<Z_c> for [K,B,n] encoded features and per-client theta [K,P] -> [K,B,C]."""
+        K, B, _ = xang.shape
+        if self.backend == "hip":
+            return self.hip.expz(xang, theta)
+        psi = self.prog.run(self._rows(xang, theta))
+        return self.prog.expz(psi, self.spec.readout).reshape(K, B, -1).float()
+
+    @torch.no_grad()
+    def predict(self, xang: torch.Tensor, params: torch.Tensor) -> torch.Tensor:
+        th, a, b = self.spec.split(params)
+        return logits_from_expz(self.expz(xang, th), a, b)
+
+    # ------------------------------------------------------------------ training
+    def loss_and_grads(self, xang: torch.Tensor, y: torch.Tensor, wmask: torch.Tensor,
+                       params: torch.Tensor, method: str = "adjoint", spsa_c: float = 0.1,
+                       rng_keys: tuple = (0,)) -> dict:
+        spec = self.spec
+        th, a, b = spec.split(params)
+        if method == "autograd":
+            return self._autograd(xang, y, wmask, params)
+        if self.backend == "hip" and method == "adjoint":
+            return self.hip.loss_and_grads(xang, y, wmask, params, spec)
+        K, B, _ = xang.shape
+        P = spec.n_theta
+        with torch.no_grad():
+            rows = self._rows(xang, th)
+            psi = self.prog.run(rows)
+            expz = self.prog.expz(psi, spec.readout).reshape(K, B, -1).float()
+            loss, w, ga, gb, correct = ce_readout(expz, y, wmask, a, b)
+            if method == "adjoint":
+                gg = self.prog.adjoint_grads(rows, psi, w.reshape(K * B, -1), spec.readout)
+                gs = slot_grads(gg, self.ops, self.coef, self.n_slots)[:, :P]
+                gth = gs.reshape(K, B, P).sum(1).float()
+            elif method == "param_shift":
+                gth = self._param_shift(rows, w, K, B)
+            elif method == "spsa":
+                gth = self._spsa(xang, y, wmask, params, spsa_c, rng_keys)
+            else:
+                raise ValueError(f"unknown grad method '{method}'")
+        grad = torch.cat([gth, ga, gb], -1)
+        return {"loss": loss, "grad": grad, "correct": correct, "expz": expz}
+
+    def _param_shift(self, rows: torch.Tensor, w: torch.Tensor, K: int, B: int,
+                     chunk: int = 32) -> torch.Tensor:
+        """d<O>/dangle_g = 0.5 (<O>(angle+pi/2) - <O>(angle-pi/2)) for every theta gate."""
+        prog, spec = self.prog, self.spec
+        P = spec.n_theta
+        base = prog.angles(rows)                                   # [KB, G]
+        gates = [g for g, (k, q0, q1, s) in enumerate(prog.ops_list) if 0 <= s < P]
+        gg = torch.zeros(rows.shape[0], len(prog.ops_list), dtype=base.dtype, device=rows.device)
+        wflat = w.reshape(K * B, -1).to(base.dtype)
+        for c0 in range(0, len(gates), chunk):
+            sub = gates[c0:c0 + chunk]
+            G2 = len(sub)
+            ang = base.unsqueeze(0).repeat(2 * G2, 1, 1)            # [2G2, KB, G]
+            for i, g in enumerate(sub):
+                ang[2 * i, :, g] += math.pi / 2
+                ang[2 * i + 1, :, g] -= math.pi / 2
+            ang = ang.reshape(-1, base.shape[1])
+            st = prog.initial_state(ang.shape[0])
+            for g in range(len(prog.ops_list)):
+                st = prog.apply_gate(st, g, ang[:, g])
+            z = prog.expz(st, spec.readout).reshape(G2, 2, rows.shape[0], -1)
+            dz = 0.5 * (z[:, 0] - z[:, 1])                           # [G2, KB, C]
+            for i, g in enumerate(sub):
+                gg[:, g] = (dz[i] * wflat).sum(-1)
+        gs = slot_grads(gg, self.ops, self.coef, self.n_slots)[:, :P]
+        return gs.reshape(K, B, P).sum(1).float()
+
+    def _loss_only(self, xang, y, wmask, params):
+        th, a, b = self.spec.split(params)
+        z = self.expz(xang, th)
+        return ce_readout(z, y, wmask, a, b)[0]
+
+    def _spsa(self, xang, y, wmask, params, c: float, rng_keys: tuple) -> torch.Tensor:
+        P = self.spec.n_theta
+        K = params.shape[0]
+        g = generator(*rng_keys, "spsa")
+        delta = (torch.randint(0, 2, (K, P), generator=g) * 2 - 1).to(params)
+        pad = torch.zeros(K, params.shape[1] - P, dtype=params.dtype, device=params.device)
+        d = torch.cat([delta.to(params.device), pad], -1)
+        lp = self._loss_only(xang, y, wmask, params + c * d)
+        lm = self._loss_only(xang, y, wmask, params - c * d)
+        return ((lp - lm) / (2 * c)).unsqueeze(-1) * delta.to(params.device)
+
+    def _autograd(self, xang, y, wmask, params):
+        spec = self.spec
+        K, B, _ = xang.shape
+        p = params.detach().clone().double().requires_grad_(True)
+        th, a, b = spec.split(p)
+        prog = TorchProgram(self.ops, self.coef, spec.n_qubits, params.device, torch.complex128)
+        rows = self._rows(xang.double(), th)
+        psi = prog.run(rows)
+        expz = prog.expz(psi, spec.readout).reshape(K, B, -1)
+        logits = logits_from_expz(expz, a, b)
+        nll = -torch.log_softmax(logits, -1).gather(-1, y.unsqueeze(-1)).squeeze(-1)
+        loss = (nll * wmask.double()).sum(-1)
+        loss.sum().backward()
+        correct = ((logits.argmax(-1) == y) & (wmask > 0)).sum(-1).float()
+        return {"loss": loss.detach().float(), "grad": p.grad.float(), "correct": correct,
+                "expz": expz.detach().float()}

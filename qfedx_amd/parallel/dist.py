@@ -1,0 +1,266 @@
+"""Process-group runtime: one process per GPU, RCCL over xGMI (backend "nccl" on ROCm), gloo on CPU.
+
+Reference: no collectives at all - aggregation is an in-process loop over state_dicts
+(``Classical_FL.py:66-81``) and clients run sequentially (``:132-140``); the ROADMAP plans Ray /
+MPI / Slurm (``ROADMAP.md:39,77-89``).  Design here:
+
+* clients are sharded over ranks in contiguous blocks; each GPU reduces ITS clients locally first
+  (fixed client order), so every round sends exactly one P-sized message per rank (CC2);
+* the update sum, sum of weights and the round metrics travel in ONE flat buffer -> one
+  all-reduce per round (CC2+CC3), latency-bound on xGMI (<= 0.5 MB), so fewer/larger messages;
+* ``exact`` mode all-reduces a fixed-point int64 encoding: integer sums are associative, so the
+  aggregate is bitwise identical for 1/2/4/8 ranks;
+* a dedicated comm stream + events lets the collective overlap compute (``CommStream``), and
+  ``BucketedAllReduce`` splits large models (TinyCNN, 455 KB) into layer buckets whose consumers wait
+  only on their own bucket's event (CC4);
+* ``ShardedServerState``: reduce-scatter + all-gather for a server optimizer whose state is
+  sharded P/world per rank (CC5).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class World:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+def init_distributed(device: torch.device, backend: str = "auto", timeout_s: int = 600) -> World:
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if ws <= 1:
+        return World(0, 1, 0, "none", device)
+    if backend == "auto":
+        backend = "nccl" if device.type == "cuda" else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29500")
+    if not dist.is_initialized():
+        kw = {}
+        if backend == "nccl" and device.type == "cuda":
+            kw["device_id"] = device
+        dist.init_process_group(backend=backend, rank=rank, world_size=ws,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return World(rank, ws, local, backend, device)
+
+
+def shutdown(world: World) -> None:
+    if world.distributed and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def shard_clients(num_clients: int, world_size: int, rank: int) -> list[int]:
+    """Contiguous block of client ids for ``rank`` (sizes differ by at most one)."""
+    base, rem = divmod(num_clients, world_size)
+    start = rank * base + min(rank, rem)
+    return list(range(start, start + base + (1 if rank < rem else 0)))
+
+
+def barrier(world: World) -> None:
+    if world.distributed:
+        if world.backend == "nccl":
+            dist.barrier(device_ids=[world.device.index])
+        else:
+            dist.barrier()
+
+
+def all_reduce_(t: torch.Tensor, world: World, op=None) -> torch.Tensor:
+    if world.distributed:
+        dist.all_reduce(t, op=op or dist.ReduceOp.SUM)
+    return t
+
+
+def broadcast_(t: torch.Tensor, world: World, src: int = 0) -> torch.Tensor:
+    if world.distributed:
+        dist.broadcast(t, src)
+    return t
+
+
+def all_gather_cat(t: torch.Tensor, world: World) -> torch.Tensor:
+    """All-gather variable-length 1-D tensors (e.g. per-client norms, CC6)."""
+    if not world.distributed:
+        return t
+    n = torch.tensor([t.numel()], device=t.device, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(world.world_size)]
+    dist.all_gather(sizes, n)
+    mx = int(max(int(s) for s in sizes))
+    pad = torch.zeros(mx, dtype=t.dtype, device=t.device)
+    pad[: t.numel()] = t.reshape(-1)
+    outs = [torch.zeros_like(pad) for _ in range(world.world_size)]
+    dist.all_gather(outs, pad)
+    return torch.cat([o[: int(s)] for o, s in zip(outs, sizes)])
+
+
+def max_over_ranks(x: float, world: World, device=None) -> float:
+    if not world.distributed:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device or world.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+class CommStream:
+    """Dedicated HIP stream for collectives; ``wait`` makes the compute stream consume the result."""
+
+    def __init__(self, world: World):
+        self.world = world
+        self.cuda = world.device.type == "cuda"
+        self.stream = torch.cuda.Stream(device=world.device) if self.cuda else None
+        self._event = None
+        self._work = None
+
+    def all_reduce_async(self, buf: torch.Tensor) -> None:
+        if not self.world.distributed:
+            return
+        if self.cuda:
+            ready = torch.cuda.Event()
+            ready.record()                       # buffer produced on the compute stream
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ready)
+                dist.all_reduce(buf)
+                self._event = torch.cuda.Event()
+                self._event.record(self.stream)
+            buf.record_stream(self.stream)
+        else:
+            self._work = dist.all_reduce(buf, async_op=True)
+
+    def wait(self) -> None:
+        if self._event is not None:
+            torch.cuda.current_stream().wait_event(self._event)
+            self._event = None
+        if self._work is not None:
+            self._work.wait()
+            self._work = None
+
+
+class FusedRoundBuffer:
+    """One flat buffer per round: [update sum (P) | sum of weights | metric scalars...].
+
+    ``exact=True`` packs everything as fixed-point int64 (scale 2^-frac_bits) so the all-reduce is
+    associative -> bitwise rank-count invariance.  Metrics must then be integers or fixed-point.
+    """
+
+    def __init__(self, P: int, n_metrics: int, device, exact: bool = False, frac_bits: int = 32):
+        self.P = P
+        self.n_metrics = n_metrics
+        self.exact = exact
+        self.scale = float(2 ** frac_bits)
+        dtype = torch.int64 if exact else torch.float64
+        self.buf = torch.zeros(P + 1 + n_metrics, dtype=dtype, device=device)
+
+    def pack(self, update_sum: torch.Tensor, weight_sum: torch.Tensor, metrics: torch.Tensor) -> torch.Tensor:
+        vals = torch.cat([update_sum.reshape(-1).double(), weight_sum.reshape(1).double(),
+                          metrics.reshape(-1).double()])
+        if self.exact:
+            self.buf.copy_(torch.round(vals * self.scale).to(torch.int64))
+        else:
+            self.buf.copy_(vals)
+        return self.buf
+
+    def unpack(self):
+        vals = self.buf.double() / self.scale if self.exact else self.buf
+        return vals[: self.P], vals[self.P], vals[self.P + 1:]
+
+
+class BucketedAllReduce:
+    """Layer-bucketed all-reduce of a flat parameter vector on the comm stream (CC4).
+
+    Buckets are contiguous [start, end) slices (e.g. TinyCNN layer boundaries, merged up to
+    ``bucket_bytes``); ``wait_bucket(i)`` blocks the compute stream only on bucket i.
+    """
+
+    def __init__(self, world: World, boundaries: list[int], bucket_bytes: int = 1 << 20, elem_bytes: int = 8):
+        self.world = world
+        self.buckets: list[tuple[int, int]] = []
+        acc_start = 0
+        for end in boundaries[1:]:
+            if (end - acc_start) * elem_bytes >= bucket_bytes:
+                self.buckets.append((acc_start, end))
+                acc_start = end
+        if acc_start < boundaries[-1]:
+            self.buckets.append((acc_start, boundaries[-1]))
+        self.cuda = world.device.type == "cuda"
+        self.stream = torch.cuda.Stream(device=world.device) if self.cuda else None
+        self.events: list = []
+        self.works: list = []
+
+    def launch(self, flat: torch.Tensor) -> None:
+        self.events, self.works = [], []
+        if not self.world.distributed:
+            return
+        if self.cuda:
+            ready = torch.cuda.Event()
+            ready.record()
+            with torch.cuda.stream(self.stream):
+                self.stream.wait_event(ready)
+                for s, e in self.buckets:
+                    dist.all_reduce(flat[s:e])
+                    ev = torch.cuda.Event()
+                    ev.record(self.stream)
+                    self.events.append(ev)
+            flat.record_stream(self.stream)
+        else:
+            for s, e in self.buckets:
+                self.works.append(dist.all_reduce(flat[s:e], async_op=True))
+
+    def wait_bucket(self, i: int) -> None:
+        if self.events:
+            torch.cuda.current_stream().wait_event(self.events[i])
+        elif self.works:
+            self.works[i].wait()
+
+    def wait_all(self) -> None:
+        for i in range(len(self.buckets)):
+            self.wait_bucket(i)
+
+
+class ShardedServerState:
+    """Server momentum (FedAvgM) with state sharded P/world per rank (CC5: reduce-scatter + all-gather)."""
+
+    def __init__(self, P: int, world: World, device, momentum: float = 0.9, lr: float = 1.0):
+        self.world = world
+        self.P = P
+        ws = world.world_size
+        self.chunk = (P + ws - 1) // ws
+        self.padded = self.chunk * ws
+        self.momentum = momentum
+        self.lr = lr
+        self.m = torch.zeros(self.chunk, dtype=torch.float64, device=device)
+
+    def step(self, global_params: torch.Tensor, local_update_sum: torch.Tensor, weight_total: float) -> torch.Tensor:
+        """``local_update_sum`` = this rank's weighted delta sum; returns new full params."""
+        flat = torch.zeros(self.padded, dtype=torch.float64, device=local_update_sum.device)
+        flat[: self.P] = local_update_sum.double()
+        shard = torch.zeros(self.chunk, dtype=torch.float64, device=flat.device)
+        if self.world.distributed:
+            dist.reduce_scatter_tensor(shard, flat)
+        else:
+            shard.copy_(flat)
+        avg = shard / weight_total
+        self.m.mul_(self.momentum).add_(avg)
+        upd_shard = self.lr * self.m
+        full = torch.zeros(self.padded, dtype=torch.float64, device=flat.device)
+        if self.world.distributed:
+            dist.all_gather_into_tensor(full, upd_shard)
+        else:
+            full.copy_(upd_shard)
+        return (global_params.double() + full[: self.P]).to(global_params.dtype)

@@ -1,0 +1,34 @@
+"""Device / backend selection (reference: one global ``device``, ``Classical_FL.py:19``).
+
+Each process owns exactly one GPU (``LOCAL_RANK``) - the MI355X-native scaling model is one
+process per GPU with RCCL between them.  ``backend`` chooses the statevector/CNN compute path:
+``hip`` = the in-tree gfx950 extension (mandatory on a GPU: it fails loudly if the extension
+is missing rather than silently falling back), ``torch`` = the portable reference
+implementation used on CPU and as the numerics oracle in tests.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+
+def resolve_device(spec: str = "auto") -> torch.device:
+    if spec == "cpu":
+        return torch.device("cpu")
+    if spec in ("auto", "cuda") and torch.cuda.is_available():
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        idx = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(idx)
+        return torch.device("cuda", idx)
+    if spec == "cuda":
+        raise RuntimeError("runtime.device=cuda requested but no GPU is visible")
+    return torch.device("cpu")
+
+
+def resolve_backend(spec: str, device: torch.device) -> str:
+    if spec == "auto":
+        return "hip" if device.type == "cuda" else "torch"
+    if spec == "hip" and device.type != "cuda":
+        raise RuntimeError("backend=hip requires a GPU device")
+    return spec

@@ -1,0 +1,64 @@
+"""Phase timers and profiler ranges (SURVEY §5 "Tracing / profiling").
+
+The reference has no tracing.  ``PhaseTimer`` brackets the federated phases (local-train,
+aggregate, comm, eval) with HIP events on GPU (no host sync inside the hot loop; the events
+are resolved once per report) and ``time.perf_counter`` on CPU, and wraps each phase in a
+``torch.profiler.record_function`` range so rocprofv3/roctracer and torch.profiler traces
+carry the same names.
+"""
+from __future__ import annotations
+
+import contextlib
+import time
+from collections import defaultdict
+
+import torch
+
+
+class PhaseTimer:
+    def __init__(self, device: torch.device | str = "cpu", enabled: bool = True):
+        self.device = torch.device(device)
+        self.enabled = enabled
+        self.gpu = self.device.type == "cuda"
+        self._pending: list[tuple[str, object, object]] = []
+        self.totals: dict[str, float] = defaultdict(float)
+        self.counts: dict[str, int] = defaultdict(int)
+
+    @contextlib.contextmanager
+    def phase(self, name: str):
+        if not self.enabled:
+            yield
+            return
+        with torch.profiler.record_function(f"qfedx::{name}"):
+            if self.gpu:
+                s = torch.cuda.Event(enable_timing=True)
+                e = torch.cuda.Event(enable_timing=True)
+                s.record()
+                yield
+                e.record()
+                self._pending.append((name, s, e))
+            else:
+                t0 = time.perf_counter()
+                yield
+                self.totals[name] += (time.perf_counter() - t0) * 1e3
+                self.counts[name] += 1
+
+    def resolve(self) -> dict[str, float]:
+        """Return accumulated milliseconds per phase (syncs once on GPU)."""
+        if self._pending:
+            self._pending[-1][2].synchronize()
+            for name, s, e in self._pending:
+                self.totals[name] += s.elapsed_time(e)
+                self.counts[name] += 1
+            self._pending.clear()
+        return dict(self.totals)
+
+    def reset(self) -> None:
+        self._pending.clear()
+        self.totals.clear()
+        self.counts.clear()
+
+
+def sync(device) -> None:
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize()
