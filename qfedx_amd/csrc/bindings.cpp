@@ -1,0 +1,177 @@
+// Python bindings of the qfedx_amd native runtime (pybind11 + torch tensors).
+//
+// Host planner (planner.cpp) and launchers of the gfx950 kernels (statevec.hip, train_kernels.hip,
+// cnn_kernels.hip).  Every launch goes on torch's CURRENT HIP stream, so the ops compose with
+// torch's stream semantics, ``torch.cuda.graph`` capture (hipGraph) and the comm-stream overlap of
+// the federated runtime.  Shapes are validated here, on the host, before any kernel is launched.
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <stdexcept>
+#include <vector>
+
+namespace qfx {
+std::vector<int> plan_circuit(int n, int R, int kmax, const std::vector<int>& ops_i,
+                              const std::vector<float>& coef, const std::vector<int>& readout,
+                              int n_theta, int mode, int final_flags);
+}
+
+extern "C" {
+int qfx_launch_pass(int R, int adjoint, const int* blob, int pass_off, int k, int n, float2* psi, float2* lam,
+                    const float* params, int p_stride, int spc, const float* xang, int x_stride,
+                    const float* w_read, float* out_read, float* gslab, int n_samples, int n_grad_ops,
+                    hipStream_t stream);
+int qfx_launch_readout_ce(const float* part, int tps, int C, int spc, int K, const long long* y, const float* wts,
+                          const float* params, int p_stride, int n_theta, float* expz, float* w_out, float* loss,
+                          float* correct, float* grad, int write_grad, hipStream_t st);
+int qfx_launch_readout_sum(const float* part, int tps, int C, long n_samples, float* expz, hipStream_t st);
+int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob, float* grad,
+                           int p_stride, hipStream_t st);
+int qfx_launch_adam(float* p, const float* g, float* m, float* v, float* t, const float* active, int K, int P,
+                    float lr, float b1, float b2, float eps, hipStream_t st);
+int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, const float* active, int K, int P, float lr,
+                    float mu, hipStream_t st);
+int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
+                      const double* weights, double* norms, const uint32_t* keys, int K, int P, int wrap, int dp,
+                      float clip, float sigma, double* out, hipStream_t st);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + " failed: hip error " + std::to_string(rc));
+}
+
+template <typename T>
+T* ptr(const torch::Tensor& t) { return t.defined() && t.numel() > 0 ? reinterpret_cast<T*>(t.data_ptr()) : nullptr; }
+
+void need(const torch::Tensor& t, torch::ScalarType dt, const char* name) {
+  if (!t.defined()) throw std::invalid_argument(std::string(name) + " is undefined");
+  if (t.scalar_type() != dt) throw std::invalid_argument(std::string(name) + " has wrong dtype");
+  if (!t.is_contiguous()) throw std::invalid_argument(std::string(name) + " must be contiguous");
+  if (!t.is_cuda()) throw std::invalid_argument(std::string(name) + " must be a GPU tensor");
+}
+
+torch::Tensor plan(torch::Tensor ops, torch::Tensor coef, int64_t n, int64_t R, int64_t kmax,
+                   std::vector<int64_t> readout, int64_t n_theta, int64_t mode, int64_t final_flags) {
+  auto o = ops.to(torch::kInt32).contiguous().cpu();
+  auto c = coef.to(torch::kFloat32).contiguous().cpu();
+  std::vector<int> oi(o.data_ptr<int>(), o.data_ptr<int>() + o.numel());
+  std::vector<float> cf(c.data_ptr<float>(), c.data_ptr<float>() + c.numel());
+  std::vector<int> ro(readout.begin(), readout.end());
+  auto blob = qfx::plan_circuit((int)n, (int)R, (int)kmax, oi, cf, ro, (int)n_theta, (int)mode, (int)final_flags);
+  auto out = torch::empty({(int64_t)blob.size()}, torch::kInt32);
+  std::copy(blob.begin(), blob.end(), out.data_ptr<int>());
+  return out;
+}
+
+void pass_launch(int64_t R, bool adjoint, torch::Tensor blob, int64_t pass_off, int64_t k, int64_t n,
+                 torch::Tensor psi, c10::optional<torch::Tensor> lam, torch::Tensor params, int64_t spc,
+                 torch::Tensor xang, c10::optional<torch::Tensor> w_read, c10::optional<torch::Tensor> out_read,
+                 c10::optional<torch::Tensor> gslab, int64_t n_samples, int64_t n_grad_ops) {
+  need(blob, torch::kInt32, "blob");
+  need(psi, torch::kComplexFloat, "psi");
+  need(params, torch::kFloat32, "params");
+  need(xang, torch::kFloat32, "xang");
+  if (psi.numel() < (n_samples << n)) throw std::invalid_argument("psi too small for n_samples x 2^n");
+  if (xang.size(0) < n_samples) throw std::invalid_argument("xang rows < n_samples");
+  if (params.size(0) * spc < n_samples) throw std::invalid_argument("params rows * spc < n_samples");
+  torch::Tensor lt = lam.has_value() ? *lam : torch::Tensor();
+  torch::Tensor wt = w_read.has_value() ? *w_read : torch::Tensor();
+  torch::Tensor ot = out_read.has_value() ? *out_read : torch::Tensor();
+  torch::Tensor gs = gslab.has_value() ? *gslab : torch::Tensor();
+  if (adjoint) {
+    need(lt, torch::kComplexFloat, "lam");
+    need(gs, torch::kFloat32, "gslab");
+    if (lt.numel() < psi.numel()) throw std::invalid_argument("lam smaller than psi");
+  }
+  check(qfx_launch_pass((int)R, adjoint ? 1 : 0, ptr<int>(blob), (int)pass_off, (int)k, (int)n, ptr<float2>(psi),
+                        ptr<float2>(lt), ptr<float>(params), (int)params.size(1), (int)spc, ptr<float>(xang),
+                        (int)xang.size(1), ptr<float>(wt), ptr<float>(ot), ptr<float>(gs), (int)n_samples,
+                        (int)n_grad_ops, cur_stream()),
+        "qfx_pass");
+}
+
+void readout_ce(torch::Tensor part, int64_t tps, int64_t C, int64_t spc, int64_t K, torch::Tensor y,
+                torch::Tensor wts, torch::Tensor params, int64_t n_theta, torch::Tensor expz, torch::Tensor w_out,
+                torch::Tensor loss, torch::Tensor correct, torch::Tensor grad, bool write_grad) {
+  need(part, torch::kFloat32, "part");
+  need(y, torch::kInt64, "y");
+  need(wts, torch::kFloat32, "wts");
+  need(params, torch::kFloat32, "params");
+  if (y.numel() < K * spc || wts.numel() < K * spc) throw std::invalid_argument("y/wts too small");
+  check(qfx_launch_readout_ce(ptr<float>(part), (int)tps, (int)C, (int)spc, (int)K, ptr<long long>(y),
+                              ptr<float>(wts), ptr<float>(params), (int)params.size(1), (int)n_theta,
+                              ptr<float>(expz), ptr<float>(w_out), ptr<float>(loss), ptr<float>(correct),
+                              ptr<float>(grad), write_grad ? 1 : 0, cur_stream()),
+        "qfx_readout_ce");
+}
+
+void readout_sum(torch::Tensor part, int64_t tps, int64_t C, int64_t n_samples, torch::Tensor expz) {
+  need(part, torch::kFloat32, "part");
+  need(expz, torch::kFloat32, "expz");
+  check(qfx_launch_readout_sum(ptr<float>(part), (int)tps, (int)C, (long)n_samples, ptr<float>(expz), cur_stream()),
+        "qfx_readout_sum");
+}
+
+void grad_reduce(torch::Tensor slab, int64_t tps, int64_t spc, int64_t K, int64_t G, torch::Tensor blob,
+                 torch::Tensor grad) {
+  need(slab, torch::kFloat32, "slab");
+  need(grad, torch::kFloat32, "grad");
+  if (slab.numel() < K * spc * tps * G) throw std::invalid_argument("grad slab too small");
+  check(qfx_launch_grad_reduce(ptr<float>(slab), (int)tps, (int)spc, (int)K, (int)G, ptr<int>(blob),
+                               ptr<float>(grad), (int)grad.size(1), cur_stream()),
+        "qfx_grad_reduce");
+}
+
+void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor t, torch::Tensor active,
+          double lr, double b1, double b2, double eps) {
+  for (auto* x : {&p, &g, &m, &v}) need(*x, torch::kFloat32, "adam tensor");
+  check(qfx_launch_adam(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), ptr<float>(t),
+                        ptr<float>(active), (int)p.size(0), (int)p.size(1), (float)lr, (float)b1, (float)b2,
+                        (float)eps, cur_stream()),
+        "qfx_adam");
+}
+
+void sgdm(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor t, torch::Tensor active, double lr,
+          double mu) {
+  for (auto* x : {&p, &g, &buf}) need(*x, torch::kFloat32, "sgd tensor");
+  check(qfx_launch_sgdm(ptr<float>(p), ptr<float>(g), ptr<float>(buf), ptr<float>(t), ptr<float>(active),
+                        (int)p.size(0), (int)p.size(1), (float)lr, (float)mu, cur_stream()),
+        "qfx_sgdm");
+}
+
+void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_mask, torch::Tensor weights,
+            torch::Tensor norms, torch::Tensor keys, bool wrap, bool dp, double clip, double sigma,
+            torch::Tensor out) {
+  need(theta_k, torch::kFloat32, "theta_k");
+  need(theta_g, torch::kFloat32, "theta_g");
+  need(weights, torch::kFloat64, "weights");
+  need(norms, torch::kFloat64, "norms");
+  need(out, torch::kFloat64, "out");
+  const int K = (int)theta_k.size(0), P = (int)theta_k.size(1);
+  if (out.numel() < P + 1) throw std::invalid_argument("fedavg out too small");
+  check(qfx_launch_fedavg(ptr<float>(theta_k), ptr<float>(theta_g), ptr<unsigned char>(angle_mask),
+                          ptr<double>(weights), ptr<double>(norms), ptr<uint32_t>(keys), K, P, wrap ? 1 : 0,
+                          dp ? 1 : 0, (float)clip, (float)sigma, ptr<double>(out), cur_stream()),
+        "qfx_fedavg");
+}
+
+}  // namespace
+
+void register_cnn(pybind11::module& m);
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "qfedx_amd native runtime: pass planner + gfx950 HIP kernels";
+  m.def("plan", &plan, "plan circuit passes");
+  m.def("pass_launch", &pass_launch);
+  m.def("readout_ce", &readout_ce);
+  m.def("readout_sum", &readout_sum);
+  m.def("grad_reduce", &grad_reduce);
+  m.def("adam", &adam);
+  m.def("sgdm", &sgdm);
+  m.def("fedavg", &fedavg);
+  register_cnn(m);
+}

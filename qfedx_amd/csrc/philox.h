@@ -1,0 +1,46 @@
+// Philox4x32-10 counter-based RNG (Salmon et al. 2011), device + host.
+// Bit-identical to qfedx_amd/utils/seeding.py::philox4x32 (the CPU oracle); keyed by
+// (seed, purpose, round, client) so every random stream is independent of the rank layout.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qfx {
+
+struct u32x4 { uint32_t x, y, z, w; };
+
+__host__ __device__ inline void mulhilo32(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
+  const uint64_t p = (uint64_t)a * (uint64_t)b;
+  hi = (uint32_t)(p >> 32);
+  lo = (uint32_t)p;
+}
+
+__host__ __device__ inline u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    uint32_t hi0, lo0, hi1, lo1;
+    mulhilo32(0xD2511F53u, c.x, hi0, lo0);
+    mulhilo32(0xCD9E8D57u, c.z, hi1, lo1);
+    c = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// standard normal for element e of a stream: pairs (2i, 2i+1) come from counter e/4, Box-Muller in
+// double on the (0,1] float uniforms - matches seeding.philox_normal element-for-element
+__device__ inline float philox_normal_at(uint64_t e, uint32_t k0, uint32_t k1, uint32_t stream) {
+  const uint64_t blk = e >> 2;
+  const u32x4 o = philox4x32_10({(uint32_t)blk, (uint32_t)(blk >> 32), stream, 0u}, k0, k1);
+  const bool second_pair = (e >> 1) & 1;
+  const uint32_t w1 = second_pair ? o.z : o.x;
+  const uint32_t w2 = second_pair ? o.w : o.y;
+  const float u1f = (float)(((double)w1 + 1.0) * (1.0 / 4294967296.0));
+  const float u2f = (float)(((double)w2 + 1.0) * (1.0 / 4294967296.0));
+  const double r = sqrt(-2.0 * log((double)u1f));
+  const double th = 6.283185307179586 * (double)u2f;
+  return (float)((e & 1) ? r * sin(th) : r * cos(th));
+}
+
+}  // namespace qfx

@@ -1,0 +1,299 @@
+// gfx950 kernels around the statevector passes: readout + cross-entropy (K14), adjoint gradient
+// reduction, fused client-batched Adam / SGD-momentum (K6), and the fused FedAvg local reduce with
+// angle wrap + DP clip + Philox Gaussian noise (K8 + K17 + K20).
+//
+// Reference equivalents: CrossEntropyLoss + optimizer.step in client_update
+// (src/CFed/Classical_FL.py:53-62), federated_averaging (:66-81); ROADMAP.md:36-37 (delta + wrap),
+// :50-51 (clip + Gaussian noise), :38 (Adam).
+//
+// All reductions are deterministic: fixed-order per-thread loops + LDS tree, no float atomics, so
+// results do not depend on timing or on how clients are sharded across GPUs.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "philox.h"
+#include "qfx_plan.h"
+
+namespace qfx {
+
+constexpr int CMAX = 8;
+
+// deterministic block reduction of NV values per thread (blockDim = 256)
+template <int NV>
+__device__ __forceinline__ void block_sum(float (&v)[NV], float* sm) {
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    float x = v[i];
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+    v[i] = x;
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) sm[i * 4 + w] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = sm[i * 4 + 0] + sm[i * 4 + 1] + sm[i * 4 + 2] + sm[i * 4 + 3];
+}
+
+// one block per client: <Z_c> = sum of tile partials; logits a<Z>+b; CE; dL/d<Z>; grads of a, b
+__global__ void __launch_bounds__(256) qfx_readout_ce_kernel(
+    const float* __restrict__ part, int tps, int C, int spc, const long long* __restrict__ y,
+    const float* __restrict__ wts, const float* __restrict__ params, int p_stride, int n_theta,
+    float* __restrict__ expz, float* __restrict__ w_out, float* __restrict__ loss,
+    float* __restrict__ correct, float* __restrict__ grad, int write_grad) {
+  __shared__ float sm[(2 * CMAX + 2) * 4];
+  const int k = blockIdx.x;
+  const float* a = params + (size_t)k * p_stride + n_theta;
+  const float* b = a + C;
+  float acc[2 * CMAX + 2];
+#pragma unroll
+  for (int i = 0; i < 2 * CMAX + 2; ++i) acc[i] = 0.f;
+  for (int j = threadIdx.x; j < spc; j += 256) {
+    const long s = (long)k * spc + j;
+    float z[CMAX], lg[CMAX];
+    float m = -INFINITY;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) {
+      if (c >= C) break;
+      float t = 0.f;
+      for (int u = 0; u < tps; ++u) t += part[((size_t)s * tps + u) * C + c];
+      z[c] = t;
+      lg[c] = fmaf(a[c], t, b[c]);
+      m = fmaxf(m, lg[c]);
+    }
+    float se = 0.f;
+    int am = 0;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) {
+      if (c >= C) break;
+      se += expf(lg[c] - m);
+      if (lg[c] > lg[am]) am = c;
+    }
+    const float lse = m + logf(se);
+    const int yy = (int)y[s];
+    const float ws = wts[s];
+    float ly = 0.f;
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) {
+      if (c >= C) break;
+      if (c == yy) ly = lg[c];
+      const float p = expf(lg[c] - lse);
+      const float dl = (p - (c == yy ? 1.f : 0.f)) * ws;
+      expz[(size_t)s * C + c] = z[c];
+      w_out[(size_t)s * C + c] = dl * a[c];
+      acc[c] += dl * z[c];
+      acc[CMAX + c] += dl;
+    }
+    acc[2 * CMAX] += ws * (lse - ly);
+    acc[2 * CMAX + 1] += (am == yy && ws > 0.f) ? 1.f : 0.f;
+  }
+  block_sum<2 * CMAX + 2>(acc, sm);
+  if (threadIdx.x == 0) {
+    loss[k] = acc[2 * CMAX];
+    correct[k] = acc[2 * CMAX + 1];
+    if (write_grad) {
+      float* g = grad + (size_t)k * p_stride + n_theta;
+      for (int c = 0; c < C; ++c) {
+        g[c] = acc[c];
+        g[C + c] = acc[CMAX + c];
+      }
+    }
+  }
+}
+
+// sum of tile partials only (evaluation): expz[s][c]
+__global__ void qfx_readout_sum_kernel(const float* __restrict__ part, int tps, int C, long n_samples,
+                                       float* __restrict__ expz) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_samples * C) return;
+  const long s = i / C;
+  const int c = (int)(i % C);
+  float t = 0.f;
+  for (int u = 0; u < tps; ++u) t += part[((size_t)s * tps + u) * C + c];
+  expz[i] = t;
+}
+
+// one block per client: grad[k][slot] = sum_{samples of k, tiles} sum_{gates g with slot} scale_g * slab
+__global__ void __launch_bounds__(256) qfx_grad_reduce_kernel(
+    const float* __restrict__ slab, int tps, int spc, const int* __restrict__ blob,
+    float* __restrict__ grad, int p_stride) {
+  extern __shared__ float gsum[];
+  const int k = blockIdx.x;
+  const int G = blob[HF_NGATES];
+  const int n_theta = blob[HF_NTHETA];
+  const int* gt = blob + blob[HF_GATES];
+  const long rows = (long)spc * tps;
+  const size_t row0 = (size_t)k * rows;
+  for (int g = threadIdx.x; g < G; g += 256) {
+    const int kind = gt[g * GATE_WORDS];
+    const int slot = gt[g * GATE_WORDS + 3];
+    float s = 0.f;
+    if (slot >= 0 && slot < n_theta && kind <= K_P) {
+      for (long r = 0; r < rows; ++r) s += slab[(row0 + r) * G + g];
+    }
+    gsum[g] = s;
+  }
+  __syncthreads();
+  for (int slot = threadIdx.x; slot < n_theta; slot += 256) {
+    float s = 0.f;
+    for (int g = 0; g < G; ++g) {
+      if (gt[g * GATE_WORDS + 3] == slot && gt[g * GATE_WORDS] <= K_P)
+        s = fmaf(__int_as_float(gt[g * GATE_WORDS + 4]), gsum[g], s);
+    }
+    grad[(size_t)k * p_stride + slot] = s;
+  }
+}
+
+// fused client-batched Adam: rows with active[k]==0 untouched
+__global__ void qfx_adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                float* __restrict__ v, float* __restrict__ t, const float* __restrict__ active,
+                                int K, int P, float lr, float b1, float b2, float eps) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)K * P) return;
+  const int k = (int)(i / P);
+  const float act = active[k];
+  if (act == 0.f) return;
+  const float tk = t[k] + 1.f;   // t incremented by the row-0 thread of each row after the step
+  const float gi = g[i];
+  const float mi = b1 * m[i] + (1.f - b1) * gi;
+  const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float mh = mi / (1.f - powf(b1, tk));
+  const float vh = vi / (1.f - powf(b2, tk));
+  p[i] -= lr * mh / (sqrtf(vh) + eps);
+}
+
+__global__ void qfx_step_count_kernel(float* __restrict__ t, const float* __restrict__ active, int K) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < K) t[k] += active[k];
+}
+
+// torch.optim.SGD(momentum) semantics: buf = g on the first step, else mu*buf + g; p -= lr*buf
+__global__ void qfx_sgdm_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
+                                const float* __restrict__ t, const float* __restrict__ active, int K, int P,
+                                float lr, float mu) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)K * P) return;
+  const int k = (int)(i / P);
+  if (active[k] == 0.f) return;
+  const float b = (t[k] == 0.f) ? g[i] : fmaf(mu, buf[i], g[i]);
+  buf[i] = b;
+  p[i] -= lr * b;
+}
+
+__device__ __forceinline__ double wrap_pi(double d) {
+  const double tp = 6.283185307179586;
+  double r = fmod(d + 3.141592653589793, tp);
+  if (r < 0) r += tp;
+  return r - 3.141592653589793;
+}
+
+// per-client l2 norm of the (wrapped) update, one block per client, double accumulation
+__global__ void __launch_bounds__(256) qfx_delta_norm_kernel(
+    const float* __restrict__ theta_k, const float* __restrict__ theta_g,
+    const unsigned char* __restrict__ angle_mask, int P, int wrap, double* __restrict__ norms) {
+  __shared__ double sm[4];
+  const int k = blockIdx.x;
+  double acc = 0.0;
+  for (int e = threadIdx.x; e < P; e += 256) {
+    double d = (double)theta_k[(size_t)k * P + e] - (double)theta_g[e];
+    if (wrap && angle_mask[e]) d = wrap_pi(d);
+    acc += d * d;
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) norms[k] = sqrt(sm[0] + sm[1] + sm[2] + sm[3]);
+}
+
+// out[e] = sum_k (fixed order) w_k * priv(wrap(theta_k[e] - theta_g[e])), out[P] = sum_k w_k
+__global__ void qfx_fedavg_reduce_kernel(
+    const float* __restrict__ theta_k, const float* __restrict__ theta_g,
+    const unsigned char* __restrict__ angle_mask, const double* __restrict__ weights,
+    const double* __restrict__ norms, const uint32_t* __restrict__ keys, int K, int P, int wrap,
+    int dp, float clip, float sigma, double* __restrict__ out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e == 0) {
+    double ws = 0.0;
+    for (int k = 0; k < K; ++k) ws += weights[k];
+    out[P] = ws;
+  }
+  if (e >= P) return;
+  double acc = 0.0;
+  for (int k = 0; k < K; ++k) {
+    double d = (double)theta_k[(size_t)k * P + e] - (double)theta_g[e];
+    if (wrap && angle_mask[e]) d = wrap_pi(d);
+    if (dp) {
+      const double n = norms[k];
+      const double sc = fmin(1.0, (double)clip / fmax(n, 1e-12));
+      d = d * sc;
+      if (sigma > 0.f)
+        d += (double)(sigma * clip) * (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
+    }
+    acc += weights[k] * d;
+  }
+  out[e] = acc;
+}
+
+}  // namespace qfx
+
+using namespace qfx;
+
+extern "C" int qfx_launch_readout_ce(const float* part, int tps, int C, int spc, int K, const long long* y,
+                                     const float* wts, const float* params, int p_stride, int n_theta,
+                                     float* expz, float* w_out, float* loss, float* correct, float* grad,
+                                     int write_grad, hipStream_t st) {
+  if (C > CMAX) return -2;
+  hipLaunchKernelGGL(qfx_readout_ce_kernel, dim3(K), dim3(256), 0, st, part, tps, C, spc, y, wts, params,
+                     p_stride, n_theta, expz, w_out, loss, correct, grad, write_grad);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_launch_readout_sum(const float* part, int tps, int C, long n_samples, float* expz,
+                                      hipStream_t st) {
+  const long tot = n_samples * C;
+  if (tot <= 0) return 0;
+  hipLaunchKernelGGL(qfx_readout_sum_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, part,
+                     tps, C, n_samples, expz);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob,
+                                      float* grad, int p_stride, hipStream_t st) {
+  hipLaunchKernelGGL(qfx_grad_reduce_kernel, dim3(K), dim3(256), (size_t)G * sizeof(float), st, slab, tps,
+                     spc, blob, grad, p_stride);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_launch_adam(float* p, const float* g, float* m, float* v, float* t, const float* active,
+                               int K, int P, float lr, float b1, float b2, float eps, hipStream_t st) {
+  const long tot = (long)K * P;
+  hipLaunchKernelGGL(qfx_adam_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, p, g, m, v, t,
+                     active, K, P, lr, b1, b2, eps);
+  hipLaunchKernelGGL(qfx_step_count_kernel, dim3((K + 255) / 256), dim3(256), 0, st, t, active, K);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, const float* active, int K,
+                               int P, float lr, float mu, hipStream_t st) {
+  const long tot = (long)K * P;
+  hipLaunchKernelGGL(qfx_sgdm_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, p, g, buf, t,
+                     active, K, P, lr, mu);
+  hipLaunchKernelGGL(qfx_step_count_kernel, dim3((K + 255) / 256), dim3(256), 0, st, t, active, K);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
+                                 const double* weights, double* norms, const uint32_t* keys, int K, int P,
+                                 int wrap, int dp, float clip, float sigma, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(qfx_delta_norm_kernel, dim3(K), dim3(256), 0, st, theta_k, theta_g, angle_mask, P, wrap,
+                     norms);
+  hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, st, theta_k, theta_g,
+                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out);
+  return (int)hipGetLastError();
+}

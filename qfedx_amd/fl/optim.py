@@ -45,7 +45,7 @@ class BatchedOptimizer:
                 fedavg_hip.adam_step(params, grads, self.m, self.v, self.t, active, self.lr, self.b1,
                                      self.b2, self.eps)
             else:
-                fedavg_hip.sgdm_step(params, grads, self.m, active, self.lr, self.momentum)
+                fedavg_hip.sgdm_step(params, grads, self.m, active, self.lr, self.momentum, t=self.t)
             return
         a = active[:, None]
         if self.kind == "adam":

@@ -1,0 +1,32 @@
+"""Python entry points of the fused aggregation / optimizer kernels (``csrc/train_kernels.hip``)."""
+from __future__ import annotations
+
+import torch
+
+from ..utils.seeding import philox_key
+from ._ext import ext
+
+
+def adam_step(params, grads, m, v, t, active, lr, b1, b2, eps) -> None:
+    ext().adam(params, grads.float().contiguous(), m, v, t, active.float().contiguous(), lr, b1, b2, eps)
+
+
+def sgdm_step(params, grads, buf, active, lr, mu, t=None) -> None:
+    if t is None:
+        raise ValueError("sgdm_step needs the step counter tensor")
+    ext().sgdm(params, grads.float().contiguous(), buf, t, active.float().contiguous(), lr, mu)
+
+
+def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp,
+                       clip_norm, noise_multiplier):
+    """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as float64 [P+1], plus norms [K]."""
+    K, P = theta_k.shape
+    dev = theta_k.device
+    keys = torch.tensor([w for c in client_ids for w in philox_key(seed, "dp_noise", round_num, int(c))],
+                        dtype=torch.int64).to(torch.int32).to(dev)
+    norms = torch.empty(K, dtype=torch.float64, device=dev)
+    out = torch.empty(P + 1, dtype=torch.float64, device=dev)
+    ext().fedavg(theta_k.float().contiguous(), theta_g.float().contiguous(),
+                 angle_mask.to(torch.uint8).contiguous(), weights.double().contiguous(), norms, keys,
+                 bool(wrap), bool(dp), float(clip_norm), float(noise_multiplier) if dp else 0.0, out)
+    return out, norms

@@ -1,0 +1,114 @@
+"""gfx950 statevector program: plans + workspaces + kernel launch sequences.
+
+``HipProgram`` owns three plans of one lowered circuit (built once by the native planner):
+  * ``eval``  : forward from the product state, last pass = readout partials only (no store)
+  * ``train`` : forward, last pass stores psi and readout partials
+  * ``adj``   : adjoint sweep (reverse program, psi + lambda, gradient slab)
+and the device workspaces (psi, lambda, readout partials, gradient slab) sized for the largest batch
+seen.  A local training step is then a fixed launch sequence (all on the current stream, capturable
+in a hipGraph):  train passes -> readout+CE -> adjoint passes -> gradient reduce.
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import ext
+from .plan_tools import FIN_READOUT, FIN_STORE, parse_blob
+
+KMAX = 12        # tile = 2^12 amplitudes = 256 lanes x 16 registers
+MODE_FWD_PRODUCT, MODE_FWD_LOAD, MODE_ADJ = 0, 1, 2
+
+
+def choose_R(n: int) -> int:
+    return 16 if n >= 4 else 4
+
+
+class _Plan:
+    def __init__(self, ops, coef, n, R, kmax, readout, n_theta, mode, final_flags, device):
+        C = ext()
+        blob = C.plan(torch.as_tensor(ops), torch.as_tensor(coef), n, R, kmax, list(readout), n_theta,
+                      mode, final_flags)
+        self.info = parse_blob(blob)
+        self.blob = blob.to(device)
+        self.R = R
+        self.passes = [(p["offset"], p["K"], p["NGRAD"]) for p in self.info["passes"]]
+        self.k = self.info["passes"][0]["K"]
+        self.n = n
+
+    @property
+    def tiles_per_state(self) -> int:
+        return 1 << (self.n - self.k)
+
+
+class HipProgram:
+    def __init__(self, ops, coef, n_qubits: int, readout, device, n_theta: int, state_dtype: str = "fp32",
+                 kmax: int = KMAX):
+        if state_dtype != "fp32":
+            raise NotImplementedError("bf16 statevector storage is not implemented yet")
+        self.n = n_qubits
+        self.readout = list(readout)
+        self.C = len(self.readout)
+        self.device = torch.device(device)
+        self.n_theta = n_theta
+        self.R = choose_R(n_qubits)
+        args = (ops, coef, n_qubits, self.R, kmax, self.readout, n_theta)
+        self.eval_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_READOUT, self.device)
+        self.train_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_STORE | FIN_READOUT, self.device)
+        self.adj_plan = _Plan(*args, MODE_ADJ, 0, self.device)
+        self.G = self.train_plan.info["G"]
+        self._ws = {}
+
+    # ------------------------------------------------------------------ workspaces
+    def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:
+        t = self._ws.get(name)
+        if t is None or t.numel() < numel or t.dtype != dtype:
+            t = torch.empty(numel, dtype=dtype, device=self.device)
+            self._ws[name] = t
+        return t[:numel]
+
+    def _run_passes(self, plan: _Plan, adjoint: bool, psi, lam, params, spc, xang, w_read, part, slab, S):
+        C = ext()
+        for off, k, ngrad in plan.passes:
+            C.pass_launch(plan.R, adjoint, plan.blob, off, k, self.n, psi, lam, params, spc, xang, w_read,
+                          part, slab, S, ngrad)
+
+    # ------------------------------------------------------------------ forward / eval
+    @torch.no_grad()
+    def expz(self, xang: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
+        K, B, F = xang.shape
+        S = K * B
+        x = xang.reshape(S, F).float().contiguous()
+        th = theta.float().contiguous()
+        plan = self.eval_plan
+        psi = self._buf("psi", S << self.n, torch.complex64)
+        part = self._buf("part", S * plan.tiles_per_state * self.C, torch.float32)
+        self._run_passes(plan, False, psi, None, th, B, x, None, part, None, S)
+        out = self._buf("expz", S * self.C, torch.float32)
+        ext().readout_sum(part, plan.tiles_per_state, self.C, S, out)
+        return out.reshape(K, B, self.C).clone()
+
+    # ------------------------------------------------------------------ train step
+    def loss_and_grads(self, xang, y, wmask, params, spec) -> dict:
+        K, B, F = xang.shape
+        S = K * B
+        C = ext()
+        x = xang.reshape(S, F).float().contiguous()
+        p = params.float().contiguous()
+        yy = y.reshape(S).long().contiguous()
+        ww = wmask.reshape(S).float().contiguous()
+        tr, adj = self.train_plan, self.adj_plan
+        psi = self._buf("psi", S << self.n, torch.complex64)
+        lam = self._buf("lam", S << self.n, torch.complex64)
+        part = self._buf("part", S * tr.tiles_per_state * self.C, torch.float32)
+        slab = self._buf("slab", S * adj.tiles_per_state * self.G, torch.float32)
+        expz = self._buf("expz", S * self.C, torch.float32)
+        wread = self._buf("wread", S * self.C, torch.float32)
+        loss = torch.empty(K, dtype=torch.float32, device=self.device)
+        correct = torch.empty(K, dtype=torch.float32, device=self.device)
+        grad = torch.zeros_like(p)
+        self._run_passes(tr, False, psi, None, p, B, x, None, part, None, S)
+        C.readout_ce(part, tr.tiles_per_state, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
+                     correct, grad, True)
+        self._run_passes(adj, True, psi, lam, p, B, x, wread, None, slab, S)
+        C.grad_reduce(slab, adj.tiles_per_state, B, K, self.G, adj.blob, grad)
+        return {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}
