@@ -104,7 +104,8 @@ def build(verbose: bool = False, force: bool = False) -> str:
     link_key = _hash(objs) if all(os.path.exists(o) for o in objs) else ""
     if jobs or stamps.get("__link__") != link_key or not os.path.exists(out):
         cmd = ["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
-               f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-ltorch_hip",
+               f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-ltorch_hip", "-lhiprtc",
+               "-lamdhip64",
                f"-Wl,-rpath,{tlib}"]
         _run(cmd)
         os.replace(out + ".tmp", out)

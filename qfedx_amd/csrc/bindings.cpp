@@ -8,7 +8,10 @@
 #include <torch/extension.h>
 
 #include <stdexcept>
+#include <string>
 #include <vector>
+
+namespace py = pybind11;
 
 namespace qfx {
 std::vector<int> plan_circuit(int n, int R, int kmax, const std::vector<int>& ops_i,
@@ -16,8 +19,31 @@ std::vector<int> plan_circuit(int n, int R, int kmax, const std::vector<int>& op
                               int n_theta, int mode, int final_flags);
 }
 
+namespace qfx {
+struct PassArgsHost {
+  const int* blob;
+  int pass_off;
+  void* psi;
+  void* lam;
+  const float* params;
+  int p_stride;
+  int spc;
+  const float* xang;
+  int x_stride;
+  const float* w_read;
+  float* out_read;
+  float* gslab;
+  int n_samples;
+  int n_grad;
+};
+int jit_prepare(const std::vector<int>& blob, int p, bool adjoint, const std::string& cache_dir,
+                const std::string& include_dir, const std::string& arch, std::string* key_out);
+int jit_launch(int handle, const PassArgsHost& args, hipStream_t stream);
+std::string jit_source(const std::vector<int>& blob, int p, bool adjoint);
+}  // namespace qfx
+
 extern "C" {
-int qfx_launch_pass(int R, int adjoint, const int* blob, int pass_off, int k, int n, float2* psi, float2* lam,
+int qfx_launch_pass(int R, int adjoint, const int* blob, int pass_off, int k, int n, int n_ops, int n_gates, float2* psi, float2* lam,
                     const float* params, int p_stride, int spc, const float* xang, int x_stride,
                     const float* w_read, float* out_read, float* gslab, int n_samples, int n_grad_ops,
                     hipStream_t stream);
@@ -67,7 +93,7 @@ torch::Tensor plan(torch::Tensor ops, torch::Tensor coef, int64_t n, int64_t R, 
   return out;
 }
 
-void pass_launch(int64_t R, bool adjoint, torch::Tensor blob, int64_t pass_off, int64_t k, int64_t n,
+void pass_launch(int64_t R, bool adjoint, torch::Tensor blob, int64_t pass_off, int64_t k, int64_t n, int64_t n_ops, int64_t n_gates,
                  torch::Tensor psi, c10::optional<torch::Tensor> lam, torch::Tensor params, int64_t spc,
                  torch::Tensor xang, c10::optional<torch::Tensor> w_read, c10::optional<torch::Tensor> out_read,
                  c10::optional<torch::Tensor> gslab, int64_t n_samples, int64_t n_grad_ops) {
@@ -87,7 +113,7 @@ void pass_launch(int64_t R, bool adjoint, torch::Tensor blob, int64_t pass_off, 
     need(gs, torch::kFloat32, "gslab");
     if (lt.numel() < psi.numel()) throw std::invalid_argument("lam smaller than psi");
   }
-  check(qfx_launch_pass((int)R, adjoint ? 1 : 0, ptr<int>(blob), (int)pass_off, (int)k, (int)n, ptr<float2>(psi),
+  check(qfx_launch_pass((int)R, adjoint ? 1 : 0, ptr<int>(blob), (int)pass_off, (int)k, (int)n, (int)n_ops, (int)n_gates, ptr<float2>(psi),
                         ptr<float2>(lt), ptr<float>(params), (int)params.size(1), (int)spc, ptr<float>(xang),
                         (int)xang.size(1), ptr<float>(wt), ptr<float>(ot), ptr<float>(gs), (int)n_samples,
                         (int)n_grad_ops, cur_stream()),
@@ -159,6 +185,42 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
         "qfx_fedavg");
 }
 
+std::vector<int> blob_vec(const torch::Tensor& blob) {
+  auto b = blob.to(torch::kInt32).contiguous().cpu();
+  return std::vector<int>(b.data_ptr<int>(), b.data_ptr<int>() + b.numel());
+}
+
+py::tuple jit_prepare(torch::Tensor blob, int64_t p, bool adjoint, std::string cache_dir, std::string include_dir,
+                      std::string arch) {
+  std::string key;
+  int h = qfx::jit_prepare(blob_vec(blob), (int)p, adjoint, cache_dir, include_dir, arch, &key);
+  return py::make_tuple(h, key);
+}
+
+std::string jit_source(torch::Tensor blob, int64_t p, bool adjoint) {
+  return qfx::jit_source(blob_vec(blob), (int)p, adjoint);
+}
+
+void jit_launch(int64_t handle, torch::Tensor blob, int64_t pass_off, torch::Tensor psi, c10::optional<torch::Tensor> lam,
+                torch::Tensor params, int64_t spc, torch::Tensor xang, c10::optional<torch::Tensor> w_read,
+                c10::optional<torch::Tensor> out_read, c10::optional<torch::Tensor> gslab, int64_t n_samples,
+                int64_t n_grad) {
+  need(blob, torch::kInt32, "blob");
+  need(psi, torch::kComplexFloat, "psi");
+  need(params, torch::kFloat32, "params");
+  need(xang, torch::kFloat32, "xang");
+  if (xang.size(0) < n_samples) throw std::invalid_argument("xang rows < n_samples");
+  if (params.size(0) * spc < n_samples) throw std::invalid_argument("params rows * spc < n_samples");
+  torch::Tensor lt = lam.has_value() ? *lam : torch::Tensor();
+  torch::Tensor wt = w_read.has_value() ? *w_read : torch::Tensor();
+  torch::Tensor ot = out_read.has_value() ? *out_read : torch::Tensor();
+  torch::Tensor gs = gslab.has_value() ? *gslab : torch::Tensor();
+  qfx::PassArgsHost a{ptr<int>(blob), (int)pass_off, psi.data_ptr(), lt.defined() ? lt.data_ptr() : nullptr,
+                      ptr<float>(params), (int)params.size(1), (int)spc, ptr<float>(xang), (int)xang.size(1),
+                      ptr<float>(wt), ptr<float>(ot), ptr<float>(gs), (int)n_samples, (int)n_grad};
+  check(qfx::jit_launch((int)handle, a, cur_stream()), "qfx_jit_launch");
+}
+
 }  // namespace
 
 void register_cnn(pybind11::module& m);
@@ -173,5 +235,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam", &adam);
   m.def("sgdm", &sgdm);
   m.def("fedavg", &fedavg);
+  m.def("jit_prepare", &jit_prepare, "generate + hiprtc-compile (or load cached) a circuit-specialised pass kernel");
+  m.def("jit_source", &jit_source);
+  m.def("jit_launch", &jit_launch);
   register_cnn(m);
 }

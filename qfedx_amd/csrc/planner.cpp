@@ -16,6 +16,8 @@
 //     a contiguous 128-byte line (coalesced HBM access).
 #include "qfx_plan.h"
 
+#include <cstdint>
+
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -51,6 +53,8 @@ class Planner {
   Planner(int n, int R, int kmax, const std::vector<PGate>& gates, const std::vector<int>& readout,
           int n_theta)
       : n_(n), R_(R), gates_(gates), readout_(readout), n_theta_(n_theta) {
+    if (R > 32 || R < 2) throw std::invalid_argument("R must be in [2, 32]");
+    if (n > 30) throw std::invalid_argument("at most 30 qubits per state");
     rb_ = 0;
     while ((1 << rb_) < R) ++rb_;
     if ((1 << rb_) != R) throw std::invalid_argument("R must be a power of two");
@@ -350,25 +354,89 @@ class Planner {
       }
     }
 
-    // ---- serialise ops, layouts, maps ----
-    blob[desc + PF_NOPS] = (int)ops.size();
+    // ---- lower U1/D1 on register bits into fused G1 groups, D1 elsewhere into D1T ----
+    std::vector<Op> out;
+    std::vector<std::vector<int>> glists;
+    std::vector<int> open(rb, -1);   // open group (index into out) per register bit
+    auto close_bit = [&](int phys) {
+      if (phys >= 0 && phys < rb) open[phys] = -1;
+    };
+    for (const Op& o : ops) {
+      if (o.code == OP_U1 || (o.code == OP_D1 && o.a < rb)) {
+        int p = o.a;
+        if (open[p] >= 0 && (int)glists[out[open[p]].c].size() < MAX_GROUP) {
+          glists[out[open[p]].c].push_back(o.c);
+        } else {
+          glists.push_back({o.c});
+          out.push_back({OP_G1, p, 0, (int)glists.size() - 1});
+          open[p] = (int)out.size() - 1;
+        }
+      } else if (o.code == OP_D1) {
+        out.push_back({OP_D1T, o.a, 0, o.c});
+      } else if (o.code == OP_CX) {
+        close_bit(o.a);
+        close_bit(o.b);
+        out.push_back(o);
+      } else if (o.code == OP_CZ) {
+        close_bit(o.a);
+        close_bit(o.b);
+        out.push_back(o);
+      } else {  // REMAP
+        for (int p = 0; p < rb; ++p) open[p] = -1;
+        out.push_back(o);
+      }
+    }
+
+    // ---- serialise ops, group lists, remap tables, layouts ----
+    const int R = R_;
+    auto swz = [&](uint32_t s) -> uint32_t {   // must equal the kernel-side LDS slot swizzle
+      return k >= 10 ? (s ^ ((s >> 5) & 31u)) : (k >= 6 ? (s ^ ((s >> 5) & 15u)) : s);
+    };
+    auto apply_map = [&](uint32_t x, const std::vector<int>& rows) {
+      uint32_t y = 0;
+      for (int j = 0; j < k; ++j) y |= (uint32_t)(__builtin_popcount(x & (uint32_t)rows[j]) & 1) << j;
+      return y;
+    };
+    auto treg = [&](const std::vector<int>& lay, int r) {
+      uint32_t t = 0;
+      for (int p = 0; p < rb; ++p)
+        if ((r >> p) & 1) t |= 1u << lay[p];
+      return t;
+    };
+    blob[desc + PF_NOPS] = (int)out.size();
     blob[desc + PF_OPS] = (int)blob.size();
     size_t ops_at = blob.size();
-    blob.resize(ops_at + ops.size() * OP_WORDS, 0);
-    std::vector<int> lay_off(layout_list.size()), map_off(map_list.size());
+    blob.resize(ops_at + out.size() * OP_WORDS, 0);
+    std::vector<int> lay_off(layout_list.size());
     for (size_t l = 0; l < layout_list.size(); ++l) {
       lay_off[l] = (int)blob.size();
       for (int p = 0; p < k; ++p) blob.push_back(layout_list[l][p]);
     }
-    for (size_t m = 0; m < map_list.size(); ++m) {
-      map_off[m] = (int)blob.size();
-      for (int j = 0; j < k; ++j) blob.push_back(map_list[m][j]);
+    std::vector<int> glist_off(glists.size());
+    for (size_t g = 0; g < glists.size(); ++g) {
+      glist_off[g] = (int)blob.size();
+      for (int gi : glists[g]) blob.push_back(gi);
     }
-    for (size_t i = 0; i < ops.size(); ++i) {
-      Op o = ops[i];
-      if (o.code == OP_REMAP) {
-        o.a = lay_off[o.a];
-        o.b = o.b >= 0 ? map_off[o.b] : -1;
+    int cur = 0;   // current layout index while walking the ops
+    for (size_t i = 0; i < out.size(); ++i) {
+      Op o = out[i];
+      if (o.code == OP_G1) {
+        o.b = (int)glists[o.c].size();
+        o.c = glist_off[o.c];
+      } else if (o.code == OP_REMAP) {
+        const std::vector<int>& ol = layout_list[cur];
+        const std::vector<int>& nl = layout_list[o.a];
+        std::vector<int> ident(k);
+        for (int j = 0; j < k; ++j) ident[j] = 1 << j;
+        const std::vector<int>& rows = o.b >= 0 ? map_list[o.b] : ident;
+        int tab = (int)blob.size();
+        for (int r = 0; r < R; ++r) blob.push_back((int)swz(apply_map(treg(ol, r), rows)));
+        for (int j = 0; j < tb_; ++j) blob.push_back((int)swz(apply_map(1u << ol[rb + j], rows)));
+        for (int r = 0; r < R; ++r) blob.push_back((int)swz(treg(nl, r)));
+        for (int j = 0; j < tb_; ++j) blob.push_back((int)swz(1u << nl[rb + j]));
+        cur = o.a;
+        o.b = lay_off[o.a];
+        o.a = tab;
       }
       blob[ops_at + i * OP_WORDS + 0] = o.code;
       blob[ops_at + i * OP_WORDS + 1] = o.a;
@@ -377,6 +445,22 @@ class Planner {
     }
     blob[desc + PF_LAYOUT0] = lay_off[0];
     blob[desc + PF_FINAL_LAYOUT] = lay_off.back();
+    // global amplitude offsets of registers / thread bits for the load and store layouts
+    auto gq = [&](const std::vector<int>& lay, int p) { return pb.tileq[lay[p]]; };
+    const std::vector<int>& L0 = layout_list[0];
+    const std::vector<int>& LF = layout_list.back();
+    for (int p = 0; p < k; ++p) blob[desc + PF_Q0 + p] = gq(L0, p);
+    for (int r = 0; r < R; ++r) {
+      uint32_t g0 = 0, gf = 0;
+      for (int p = 0; p < rb; ++p)
+        if ((r >> p) & 1) g0 |= 1u << gq(L0, p), gf |= 1u << gq(LF, p);
+      blob[desc + PF_GREG0 + r] = (int)g0;
+      blob[desc + PF_GREGF + r] = (int)gf;
+    }
+    for (int j = 0; j < tb_; ++j) {
+      blob[desc + PF_GTHR0 + j] = 1 << gq(L0, rb + j);
+      blob[desc + PF_GTHRF + j] = 1 << gq(LF, rb + j);
+    }
     // readout phys bits: final layout (forward readout) and initial layout (adjoint lambda)
     std::vector<int> inv0 = t2p(layout_list[0]);
     std::vector<int> invf = t2p(layout_list.back());

@@ -9,7 +9,7 @@
 // live in registers and, in the same trip, applies the pending GF(2)-linear permutation of fused
 // CNOT chains.  Diagonal gates (RZ/P/Z/S/T/CZ) act on any bit, even qubits outside the tile.
 #pragma once
-#include <stdint.h>
+// (no <stdint.h>: this header is also compiled by hiprtc)
 
 namespace qfx {
 
@@ -19,8 +19,9 @@ enum Kind : int {
   K_T = 10, K_TDG = 11, K_SX = 12, K_CX = 13, K_CZ = 14, K_SWAP = 15
 };
 
-// micro-op codes
-enum OpCode : int { OP_U1 = 1, OP_D1 = 2, OP_CX = 3, OP_CZ = 4, OP_REMAP = 5 };
+// micro-op codes (planner-internal U1/D1 are lowered to G1 groups / D1T before serialisation)
+enum OpCode : int { OP_G1 = 1, OP_D1T = 2, OP_CX = 3, OP_CZ = 4, OP_REMAP = 5, OP_U1 = 6, OP_D1 = 7 };
+constexpr int MAX_GROUP = 8;   // single-qubit gates fused into one register-bit group
 
 // pass init / final modes
 enum InitMode : int { INIT_LOAD = 0, INIT_PRODUCT = 1, INIT_PSI_LAMBDA = 2, INIT_LOAD_BOTH = 3 };
@@ -40,7 +41,12 @@ enum PassField : int {
   PF_NONTILE = 40,      // [32] non-tile qubits (ascending)
   PF_READ_PHYS = 72,    // [8]  readout qubit -> phys bit in the FINAL layout
   PF_LAM_PHYS = 80,     // [8]  readout qubit -> phys bit in the INITIAL layout (adjoint lambda init)
-  PF_SIZE = 96
+  PF_Q0 = 96,           // [24] phys bit -> qubit in the initial layout (product-state init)
+  PF_GREG0 = 120,       // [32] initial layout: global amplitude offset of register r
+  PF_GTHR0 = 152,       // [16] initial layout: global offset contributed by thread bit j
+  PF_GREGF = 168,       // [32] final layout: global offset of register r
+  PF_GTHRF = 200,       // [16] final layout: global offset of thread bit j
+  PF_SIZE = 224
 };
 
 // blob header: [0]=n_qubits [1]=n_passes [2]=n_gates [3]=gate table offset [4]=prefix offset
@@ -53,12 +59,15 @@ enum HeaderField : int {
 // gate table entry: 6 words: kind, q0, q1, slot, scale(f32 bits), offset(f32 bits)
 constexpr int GATE_WORDS = 6;
 // micro-op: 4 words: code, a, b, c
-//   U1:    a = register bit, c = gate index
-//   D1:    a = phys bit,     c = gate index
+//   G1:    a = register bit, b = gate count, c = word offset of the gate-index list (execution
+//          order; forward multiplies the 2x2s, adjoint applies inverses + gradients in list order)
+//   D1T:   a = phys bit (thread bit or non-tile qubit), c = gate index (diagonal 1q gate)
 //   CX:    a = control phys bit, b = target register bit, c = gate index
 //   CZ:    a, b = phys bits, c = gate index
-//   REMAP: a = word offset of the new layout (k phys->tile entries), b = word offset of the linear
-//          map (k row masks, new tile bit j = parity(old_tile_index & row_j)) or -1 for identity
+//   REMAP: a = word offset of the remap table [wr R][wt TB][rr R][rt TB]: LDS slot of register r /
+//          thread bit j on write (GF(2) map and XOR swizzle already applied - both are linear) and
+//          on read (new layout); slot(r, tl) = tab_r[r] ^ XOR_{j: bit j of tl} tab_t[j]
+//          b = word offset of the new layout (phys -> tile bit; bookkeeping only)
 constexpr int OP_WORDS = 4;
 
 }  // namespace qfx

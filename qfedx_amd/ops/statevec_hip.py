@@ -7,8 +7,15 @@
 and the device workspaces (psi, lambda, readout partials, gradient slab) sized for the largest batch
 seen.  A local training step is then a fixed launch sequence (all on the current stream, capturable
 in a hipGraph):  train passes -> readout+CE -> adjoint passes -> gradient reduce.
+
+Each pass runs either as a circuit-specialised kernel (generated from the plan and compiled with
+hiprtc for gfx950 by ``csrc/jit.cpp``; default) or through the ahead-of-time interpreter kernel
+(``csrc/statevec.hip``; ``QFEDX_JIT=0`` or when specialisation is unavailable).  Both execute the
+same plan and are tested against each other and the float64 oracle.
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -17,23 +24,37 @@ from .plan_tools import FIN_READOUT, FIN_STORE, parse_blob
 
 KMAX = 12        # tile = 2^12 amplitudes = 256 lanes x 16 registers
 MODE_FWD_PRODUCT, MODE_FWD_LOAD, MODE_ADJ = 0, 1, 2
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(_PKG, "csrc")
+JIT_CACHE = os.environ.get("QFEDX_JIT_CACHE", os.path.join(os.path.dirname(_PKG), "build", "jit"))
+ARCH = os.environ.get("QFEDX_ARCH", "gfx950")
 
 
 def choose_R(n: int) -> int:
     return 16 if n >= 4 else 4
 
 
+def jit_enabled() -> bool:
+    return os.environ.get("QFEDX_JIT", "1") != "0"
+
+
 class _Plan:
-    def __init__(self, ops, coef, n, R, kmax, readout, n_theta, mode, final_flags, device):
+    def __init__(self, ops, coef, n, R, kmax, readout, n_theta, mode, final_flags, device, jit: bool):
         C = ext()
         blob = C.plan(torch.as_tensor(ops), torch.as_tensor(coef), n, R, kmax, list(readout), n_theta,
                       mode, final_flags)
         self.info = parse_blob(blob)
+        self.blob_cpu = blob
         self.blob = blob.to(device)
         self.R = R
-        self.passes = [(p["offset"], p["K"], p["NGRAD"]) for p in self.info["passes"]]
+        self.adjoint = mode == MODE_ADJ
+        self.passes = [(p["offset"], p["K"], p["NGRAD"], p["NOPS"]) for p in self.info["passes"]]
         self.k = self.info["passes"][0]["K"]
         self.n = n
+        self.jit_handles = None
+        if jit:
+            self.jit_handles = [C.jit_prepare(blob, i, self.adjoint, JIT_CACHE, CSRC, ARCH)[0]
+                                for i in range(len(self.passes))]
 
     @property
     def tiles_per_state(self) -> int:
@@ -42,7 +63,7 @@ class _Plan:
 
 class HipProgram:
     def __init__(self, ops, coef, n_qubits: int, readout, device, n_theta: int, state_dtype: str = "fp32",
-                 kmax: int = KMAX):
+                 kmax: int = KMAX, jit: bool | None = None):
         if state_dtype != "fp32":
             raise NotImplementedError("bf16 statevector storage is not implemented yet")
         self.n = n_qubits
@@ -51,10 +72,11 @@ class HipProgram:
         self.device = torch.device(device)
         self.n_theta = n_theta
         self.R = choose_R(n_qubits)
+        self.jit = jit_enabled() if jit is None else jit
         args = (ops, coef, n_qubits, self.R, kmax, self.readout, n_theta)
-        self.eval_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_READOUT, self.device)
-        self.train_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_STORE | FIN_READOUT, self.device)
-        self.adj_plan = _Plan(*args, MODE_ADJ, 0, self.device)
+        self.eval_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_READOUT, self.device, self.jit)
+        self.train_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_STORE | FIN_READOUT, self.device, self.jit)
+        self.adj_plan = _Plan(*args, MODE_ADJ, 0, self.device, self.jit)
         self.G = self.train_plan.info["G"]
         self._ws = {}
 
@@ -68,9 +90,13 @@ class HipProgram:
 
     def _run_passes(self, plan: _Plan, adjoint: bool, psi, lam, params, spc, xang, w_read, part, slab, S):
         C = ext()
-        for off, k, ngrad in plan.passes:
-            C.pass_launch(plan.R, adjoint, plan.blob, off, k, self.n, psi, lam, params, spc, xang, w_read,
-                          part, slab, S, ngrad)
+        for i, (off, k, ngrad, nops) in enumerate(plan.passes):
+            if plan.jit_handles is not None:
+                C.jit_launch(plan.jit_handles[i], plan.blob, off, psi, lam, params, spc, xang, w_read, part, slab,
+                             S, ngrad)
+            else:
+                C.pass_launch(plan.R, adjoint, plan.blob, off, k, self.n, nops, plan.info["G"], psi, lam, params,
+                              spc, xang, w_read, part, slab, S, ngrad)
 
     # ------------------------------------------------------------------ forward / eval
     @torch.no_grad()

@@ -26,7 +26,9 @@ def _setup(n, L, C, K, B, seed=0, ent="chain"):
 @pytest.mark.parametrize("n,L,K,B,ent", [(2, 1, 3, 5, "chain"), (4, 2, 4, 7, "chain"), (6, 2, 2, 9, "ring"),
                                          (8, 3, 3, 4, "chain"), (12, 2, 2, 3, "ring"), (14, 2, 2, 2, "chain"),
                                          (16, 3, 2, 2, "chain")])
-def test_forward_expz_matches_torch(cuda, n, L, K, B, ent):
+@pytest.mark.parametrize("jit", ["1", "0"])
+def test_forward_expz_matches_torch(cuda, n, L, K, B, ent, jit, monkeypatch):
+    monkeypatch.setenv("QFEDX_JIT", jit)
     C = 2 if n < 3 else 3
     spec, x, y, w, params = _setup(n, L, C, K, B, ent=ent)
     ref = VQCEngine(spec, "cpu", "torch")
@@ -50,7 +52,9 @@ def test_forward_matches_float64_oracle(cuda):
 
 
 @pytest.mark.parametrize("n,L,K,B", [(3, 2, 2, 4), (4, 2, 3, 6), (8, 2, 2, 5), (13, 2, 2, 2), (16, 2, 2, 2)])
-def test_adjoint_grads_match_torch(cuda, n, L, K, B):
+@pytest.mark.parametrize("jit", ["1", "0"])
+def test_adjoint_grads_match_torch(cuda, n, L, K, B, jit, monkeypatch):
+    monkeypatch.setenv("QFEDX_JIT", jit)
     spec, x, y, w, params = _setup(n, L, 3 if n >= 3 else 2, K, B, seed=n)
     ref = VQCEngine(spec, "cpu", "torch")
     hip = VQCEngine(spec, cuda, "hip")
