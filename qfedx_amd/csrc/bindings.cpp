@@ -59,7 +59,7 @@ int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, const float*
                     float mu, hipStream_t st);
 int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
                       const double* weights, double* norms, const uint32_t* keys, int K, int P, int wrap, int dp,
-                      float clip, float sigma, double* out, hipStream_t st);
+                      float clip, float sigma, long long* out, hipStream_t st);
 }
 
 namespace {
@@ -176,12 +176,12 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
   need(theta_g, torch::kFloat32, "theta_g");
   need(weights, torch::kFloat64, "weights");
   need(norms, torch::kFloat64, "norms");
-  need(out, torch::kFloat64, "out");
+  need(out, torch::kInt64, "out");
   const int K = (int)theta_k.size(0), P = (int)theta_k.size(1);
   if (out.numel() < P + 1) throw std::invalid_argument("fedavg out too small");
   check(qfx_launch_fedavg(ptr<float>(theta_k), ptr<float>(theta_g), ptr<unsigned char>(angle_mask),
                           ptr<double>(weights), ptr<double>(norms), ptr<uint32_t>(keys), K, P, wrap ? 1 : 0,
-                          dp ? 1 : 0, (float)clip, (float)sigma, ptr<double>(out), cur_stream()),
+                          dp ? 1 : 0, (float)clip, (float)sigma, ptr<long long>(out), cur_stream()),
         "qfx_fedavg");
 }
 

@@ -211,20 +211,23 @@ __global__ void __launch_bounds__(256) qfx_delta_norm_kernel(
   if (threadIdx.x == 0) norms[k] = sqrt(sm[0] + sm[1] + sm[2] + sm[3]);
 }
 
-// out[e] = sum_k (fixed order) w_k * priv(wrap(theta_k[e] - theta_g[e])), out[P] = sum_k w_k
+// out[e] = sum_k round(2^32 * w_k * priv(wrap(theta_k[e] - theta_g[e]))), out[P] = sum_k round(2^32 w_k)
+// Each client's term is rounded to fixed point BEFORE the sum: integer addition is associative, so the
+// aggregate is bitwise identical for any sharding of clients over GPUs (and equal to the CPU path).
 __global__ void qfx_fedavg_reduce_kernel(
     const float* __restrict__ theta_k, const float* __restrict__ theta_g,
     const unsigned char* __restrict__ angle_mask, const double* __restrict__ weights,
     const double* __restrict__ norms, const uint32_t* __restrict__ keys, int K, int P, int wrap,
-    int dp, float clip, float sigma, double* __restrict__ out) {
+    int dp, float clip, float sigma, long long* __restrict__ out) {
+  const double SC = 4294967296.0;
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e == 0) {
-    double ws = 0.0;
-    for (int k = 0; k < K; ++k) ws += weights[k];
+    long long ws = 0;
+    for (int k = 0; k < K; ++k) ws += llrint(weights[k] * SC);
     out[P] = ws;
   }
   if (e >= P) return;
-  double acc = 0.0;
+  long long acc = 0;
   for (int k = 0; k < K; ++k) {
     double d = (double)theta_k[(size_t)k * P + e] - (double)theta_g[e];
     if (wrap && angle_mask[e]) d = wrap_pi(d);
@@ -233,9 +236,9 @@ __global__ void qfx_fedavg_reduce_kernel(
       const double sc = fmin(1.0, (double)clip / fmax(n, 1e-12));
       d = d * sc;
       if (sigma > 0.f)
-        d += (double)(sigma * clip) * (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
+        d += (double)sigma * (double)clip * (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
     }
-    acc += weights[k] * d;
+    acc += llrint(weights[k] * d * SC);
   }
   out[e] = acc;
 }
@@ -290,7 +293,7 @@ extern "C" int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, c
 
 extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
                                  const double* weights, double* norms, const uint32_t* keys, int K, int P,
-                                 int wrap, int dp, float clip, float sigma, double* out, hipStream_t st) {
+                                 int wrap, int dp, float clip, float sigma, long long* out, hipStream_t st) {
   hipLaunchKernelGGL(qfx_delta_norm_kernel, dim3(K), dim3(256), 0, st, theta_k, theta_g, angle_mask, P, wrap,
                      norms);
   hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, st, theta_k, theta_g,

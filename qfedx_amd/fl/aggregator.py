@@ -21,6 +21,9 @@ from ..privacy.dp import clip_and_noise
 from ..privacy.secure_agg import SecureAggregator
 
 
+EXACT_SCALE = float(2 ** 32)   # fixed-point scale of the exact (rank-count invariant) aggregation
+
+
 def wrap_angles(d: torch.Tensor) -> torch.Tensor:
     """Wrap to [-pi, pi) (ROADMAP.md:37 periodicity of rotation angles)."""
     return torch.remainder(d + math.pi, 2 * math.pi) - math.pi
@@ -95,10 +98,9 @@ class Aggregator:
         w = weights.double().to(delta.device)
         weighted = torch.cat([delta * w[:, None], w[:, None]], -1)    # [K, P+1]
         if not self.secure_agg:
-            out = torch.zeros(self.P + 1, dtype=torch.float64, device=delta.device)
-            for k in range(weighted.shape[0]):                         # fixed client order
-                out += weighted[k]
-            return out
+            # per-client fixed point BEFORE summation: integer sums are associative, so the aggregate
+            # is bitwise identical however clients are sharded over ranks
+            return torch.round(weighted * EXACT_SCALE).to(torch.int64).sum(0)
         sa = self.secagg
         parts = list(participants if participants is not None else client_ids)
         total = torch.zeros(self.P + 1, dtype=torch.int64, device=delta.device)
@@ -117,6 +119,8 @@ class Aggregator:
         if self.secure_agg:
             from ..privacy.secure_agg import decode_fixed
             vals = decode_fixed(reduced, self.secagg.scale, self.secagg.bits)
+        elif reduced.dtype == torch.int64:
+            vals = reduced.double() / EXACT_SCALE
         else:
             vals = reduced.double()
         wsum = float(vals[self.P])

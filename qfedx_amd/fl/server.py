@@ -22,14 +22,14 @@ from typing import Optional
 
 import torch
 
-from ..parallel.dist import FusedRoundBuffer, World, all_reduce_, barrier, broadcast_, shard_clients
+from ..parallel.dist import World, all_reduce_, barrier, broadcast_, shard_clients
 from ..privacy.accountant import RDPAccountant
 from ..privacy.secure_agg import SecureAggregator
 from ..utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 from ..utils.logging import MetricsWriter, get_logger
 from ..utils.seeding import generator, np_rng
 from ..utils.timing import PhaseTimer
-from .aggregator import Aggregator
+from .aggregator import EXACT_SCALE, Aggregator
 from .trainer import ShardStore
 
 
@@ -146,8 +146,7 @@ class FederatedRunner:
                     [self.local_ids[i] for i in local_alive],
                     participants=[c for c in participants], dropped=dropped)
             else:
-                dt = torch.int64 if p.secure_agg else torch.float64
-                contrib = torch.zeros(self.P + 1, dtype=dt, device=self.device)
+                contrib = torch.zeros(self.P + 1, dtype=torch.int64, device=self.device)
             loss_sum = res.get("loss_sum", 0.0)
             correct = res.get("correct", 0.0)
             metrics = torch.stack([torch.as_tensor(loss_sum, dtype=torch.float64, device=self.device),
@@ -160,12 +159,12 @@ class FederatedRunner:
                 all_reduce_(metrics, self.world)
                 mean_upd, wsum = self.aggregator.finalize(contrib)
             else:
-                fb = FusedRoundBuffer(self.P, metrics.numel(), self.device)
-                buf = fb.pack(contrib[: self.P], contrib[self.P], metrics)
-                all_reduce_(buf, self.world)              # ONE collective per round (CC2+CC3)
-                red, wsum_t, metrics = fb.unpack()
-                wsum = float(wsum_t)
-                mean_upd = red / max(wsum, 1e-300)
+                # ONE collective per round (CC2+CC3): [exact fixed-point update | weight | metrics]
+                buf = torch.cat([contrib.to(torch.int64),
+                                 torch.round(metrics.double() * EXACT_SCALE).to(torch.int64)])
+                all_reduce_(buf, self.world)
+                mean_upd, wsum = self.aggregator.finalize(buf[: self.P + 1])
+                metrics = buf[self.P + 1:].double() / EXACT_SCALE
         if wsum > 0:
             self.params = self.aggregator.apply(self.params, mean_upd)
         if p.dp:

@@ -19,13 +19,14 @@ def sgdm_step(params, grads, buf, active, lr, mu, t=None) -> None:
 
 def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp,
                        clip_norm, noise_multiplier):
-    """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as float64 [P+1], plus norms [K]."""
+    """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as exact int64 fixed point (scale 2^32)
+    [P+1] (per-client terms rounded before the sum -> rank-count invariant), plus norms [K]."""
     K, P = theta_k.shape
     dev = theta_k.device
     keys = torch.tensor([w for c in client_ids for w in philox_key(seed, "dp_noise", round_num, int(c))],
                         dtype=torch.int64).to(torch.int32).to(dev)
     norms = torch.empty(K, dtype=torch.float64, device=dev)
-    out = torch.empty(P + 1, dtype=torch.float64, device=dev)
+    out = torch.empty(P + 1, dtype=torch.int64, device=dev)
     ext().fedavg(theta_k.float().contiguous(), theta_g.float().contiguous(),
                  angle_mask.to(torch.uint8).contiguous(), weights.double().contiguous(), norms, keys,
                  bool(wrap), bool(dp), float(clip_norm), float(noise_multiplier) if dp else 0.0, out)

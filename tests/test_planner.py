@@ -1,0 +1,86 @@
+"""Native pass planner: the register-level emulator of the plan (same semantics as the gfx950 kernel,
+including the precomputed remap / address tables) must reproduce the float64 oracle for forward,
+readout and adjoint gradients, on VQCs and on random generic circuits."""
+import numpy as np
+import pytest
+import torch
+
+from qfedx_amd.models.vqc import VQCSpec
+from qfedx_amd.ops.plan_tools import emulate_adjoint, emulate_forward, parse_blob
+from qfedx_amd.ops.statevec_torch import TorchProgram
+from qfedx_amd.quantum.circuit import Circuit, ParameterVector
+from qfedx_amd.quantum.statevector import Statevector
+
+C = pytest.importorskip("qfedx_amd._qfedx_C", reason="native extension not built")
+
+
+def _plan(ops, coef, n, R, kmax, readout, n_theta, mode, fin):
+    return parse_blob(C.plan(torch.from_numpy(ops), torch.from_numpy(coef), n, R, kmax, readout, n_theta, mode, fin))
+
+
+def _check(ops, coef, n, R, kmax, readout, n_theta, vals_theta, vals_x, circ, values, tol=1e-12):
+    info = _plan(ops, coef, n, R, kmax, readout, n_theta, 0, 3)
+    psi, out = emulate_forward(info, vals_theta, vals_x)
+    sv = Statevector.from_instruction(circ, values)
+    assert np.abs(psi - sv.data).max() < tol
+    assert np.allclose(out, [sv.expectation_z(q) for q in readout], atol=tol)
+    binfo = _plan(ops, coef, n, R, kmax, readout, n_theta, 2, 0)
+    w = np.random.default_rng(1).normal(size=len(readout))
+    g = emulate_adjoint(binfo, sv.data, vals_theta, vals_x, w)
+    prog = TorchProgram(ops, coef, n, dtype=torch.complex128)
+    rows = torch.from_numpy(np.concatenate([vals_theta, vals_x]))[None]
+    gt = prog.adjoint_grads(rows, prog.run(rows), torch.from_numpy(w)[None], readout)[0].numpy()
+    mask = np.array([0 <= s < n_theta and k <= 3 for k, s in zip(ops[:, 0], ops[:, 3])])
+    assert np.abs(g[mask] - gt[mask]).max() < tol
+    return info, binfo
+
+
+@pytest.mark.parametrize("n,L,R,kmax,ent", [(2, 1, 4, 12, "chain"), (4, 2, 16, 12, "chain"), (8, 2, 4, 6, "ring"),
+                                            (9, 3, 16, 7, "chain"), (10, 2, 4, 5, "chain"), (14, 2, 16, 12, "ring"),
+                                            (16, 3, 16, 12, "chain")])
+def test_vqc_plans_exact(n, L, R, kmax, ent):
+    spec = VQCSpec(n_qubits=n, n_layers=L, n_classes=2 if n < 3 else 3, entangler=ent)
+    ops, coef = spec.program()
+    rng = np.random.default_rng(n)
+    th, x = rng.normal(size=spec.n_theta), rng.uniform(0, 3, n)
+    info, _ = _check(ops, coef, n, R, kmax, spec.readout, spec.n_theta, th, x, spec.circuit(), {"theta": th, "x": x})
+    if n == 16:   # fusion quality: 3-layer 16-qubit VQC forward in 2 passes
+        assert info["npass"] == 2
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_generic_circuits(seed):
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(6, 11))
+    th = ParameterVector("theta", 40)
+    qc = Circuit(n)
+    k = 0
+    for _ in range(60):
+        r = rng.random()
+        q = int(rng.integers(n))
+        if r < 0.35:
+            g = ["rx", "ry", "rz", "p"][int(rng.integers(4))]
+            getattr(qc, g)(float(rng.uniform(0.5, 1.5)) * th[k % 40] + float(rng.normal()), q)
+            k += 1
+        elif r < 0.55:
+            getattr(qc, ["h", "x", "y", "z", "s", "sdg", "t", "tdg", "sx"][int(rng.integers(9))])(q)
+        elif r < 0.85:
+            a, b = rng.choice(n, 2, replace=False)
+            qc.cx(int(a), int(b))
+        else:
+            a, b = rng.choice(n, 2, replace=False)
+            qc.cz(int(a), int(b))
+    ops, coef = qc.to_program({"theta": 0, "x": 40})
+    vals = rng.normal(size=40)
+    readout = [0, n - 1]
+    # gate scale/offset are stored as float32 in the program table -> ~1e-8 vs the float64 oracle
+    _check(ops, coef, n, 4, 5, readout, 40, vals, np.zeros(1), qc, {"theta": vals}, tol=1e-6)
+    _check(ops, coef, n, 16, 7, readout, 40, vals, np.zeros(1), qc, {"theta": vals}, tol=1e-6)
+
+
+def test_jit_codegen_emits_straight_line_kernel():
+    spec = VQCSpec(n_qubits=12, n_layers=2, n_classes=3)
+    ops, coef = spec.program()
+    blob = C.plan(torch.from_numpy(ops), torch.from_numpy(coef), 12, 16, 12, spec.readout, spec.n_theta, 2, 0)
+    src = C.jit_source(blob, 0, True)
+    assert "qfx_jit_pass" in src and "adj_step<R," in src and "switch" not in src

@@ -1,0 +1,108 @@
+"""DP clip+noise, pairwise-mask secure aggregation, RDP accountant, Philox determinism."""
+import math
+
+import numpy as np
+import pytest
+import torch
+from hypothesis import given, settings, strategies as st
+
+from qfedx_amd.privacy.accountant import RDPAccountant, compute_rdp, epsilon, rdp_sampled_gaussian
+from qfedx_amd.privacy.dp import clip_and_noise, clip_factors, dp_noise
+from qfedx_amd.privacy.secure_agg import SecureAggregator, decode_fixed, encode_fixed, prg_mask
+from qfedx_amd.utils.seeding import philox4x32, philox_normal, philox_key
+
+
+def test_philox_known_answers():
+    # Random123 philox4x32-10 known-answer vectors
+    z = philox4x32(torch.zeros(1, 4, dtype=torch.int64), 0, 0)[0].tolist()
+    assert [hex(v) for v in z] == ["0x6627e8d5", "0xe169c58d", "0xbc57ac4c", "0x9b00dbd8"]
+    f = philox4x32(torch.tensor([[0xFFFFFFFF] * 4]), 0xFFFFFFFF, 0xFFFFFFFF)[0].tolist()
+    assert [hex(v) for v in f] == ["0x408f276d", "0x41c83b0e", "0xa20bc7c6", "0x6d5451fd"]
+
+
+def test_philox_normal_stats_and_determinism():
+    z = philox_normal(20000, (123, 456))
+    assert abs(float(z.mean())) < 0.03 and abs(float(z.std()) - 1) < 0.03
+    assert torch.equal(z[:100], philox_normal(100, (123, 456)))
+
+
+def test_clip_bounds_norm():
+    d = torch.randn(5, 30) * 3
+    out, norms = clip_and_noise(d.double(), 1.0, 0.0, 0, 0, range(5), add_noise=False)
+    assert torch.all(out.norm(dim=1) <= 1.0 + 1e-9)
+    small = torch.full((1, 4), 0.01).double()
+    s, _ = clip_factors(small, 1.0)
+    assert float(s) == 1.0   # below the bound: untouched
+
+
+def test_noise_keyed_by_client_not_rank():
+    a = dp_noise(50, seed=3, round_num=2, client=7)
+    b = dp_noise(50, seed=3, round_num=2, client=7)
+    c = dp_noise(50, seed=3, round_num=2, client=8)
+    assert torch.equal(a, b) and not torch.equal(a, c)
+
+
+def test_dp_noise_std():
+    d = torch.zeros(400, 100, dtype=torch.float64)
+    out, _ = clip_and_noise(d, 0.5, 2.0, 1, 0, range(400))
+    assert abs(float(out.std()) - 1.0) < 0.03     # sigma * C = 1.0
+
+
+@settings(max_examples=15, deadline=None)
+@given(st.integers(2, 9), st.integers(0, 1000))
+def test_secagg_masks_cancel(k, seed):
+    """ROADMAP.md:55,61 - masked sum equals the raw sum."""
+    rng = np.random.default_rng(seed)
+    sa = SecureAggregator(seed)
+    parts = list(range(k))
+    sa.register(parts)
+    ups = [torch.from_numpy(rng.normal(size=17)) for _ in parts]
+    masked = [sa.mask(u, c, parts, round_num=3) for c, u in zip(parts, ups)]
+    total = sa.aggregate(masked, parts, round_num=3)
+    assert torch.allclose(total, sum(ups), atol=1e-5)
+    # individual masked vectors reveal nothing obvious: far from the raw encoding
+    assert not torch.equal(masked[0], encode_fixed(ups[0], sa.scale, sa.bits))
+
+
+def test_secagg_dropout_recovery():
+    sa = SecureAggregator(9)
+    parts = [0, 1, 2, 3, 4]
+    rng = np.random.default_rng(0)
+    ups = {c: torch.from_numpy(rng.normal(size=8)) for c in parts}
+    masked = {c: sa.mask(ups[c], c, parts, round_num=1) for c in parts}
+    survivors = [0, 2, 3]
+    dropped = [1, 4]
+    total = sa.aggregate([masked[c] for c in survivors], survivors, dropped, round_num=1)
+    assert torch.allclose(total, sum(ups[c] for c in survivors), atol=1e-5)
+
+
+def test_fixed_point_roundtrip_and_prg_range():
+    x = torch.tensor([-3.25, 0.0, 1e-3, 1000.5], dtype=torch.float64)
+    assert torch.allclose(decode_fixed(encode_fixed(x, 2.0 ** 24, 48), 2.0 ** 24, 48), x, atol=1e-7)
+    m = prg_mask(12345, 0, 1000, 48)
+    assert int(m.min()) >= 0 and int(m.max()) < 2 ** 48 and int(m.max()) > 2 ** 46
+
+
+def test_accountant_known_values():
+    # TF-Privacy tutorial setting (q=256/60000, sigma=1.1, 60 epochs, delta=1e-5): eps ~= 3.01 (classic)
+    steps = int(60 * 60000 / 256)
+    assert abs(epsilon(256 / 60000, 1.1, steps, 1e-5, "classic") - 3.01) < 0.02
+    assert epsilon(256 / 60000, 1.1, steps, 1e-5) < epsilon(256 / 60000, 1.1, steps, 1e-5, "classic")
+    # q = 1: RDP of the Gaussian mechanism is alpha / (2 sigma^2) exactly
+    assert math.isclose(rdp_sampled_gaussian(1.0, 2.0, 5.0), 5.0 / 8.0)
+    # integer and fractional order formulas agree
+    assert math.isclose(rdp_sampled_gaussian(0.1, 1.0, 3.0), rdp_sampled_gaussian(0.1, 1.0, 3.0 - 1e-7), rel_tol=1e-4)
+
+
+def test_accountant_monotone_and_state():
+    acc = RDPAccountant()
+    eps = []
+    for _ in range(5):
+        acc.step(0.3, 1.0)
+        eps.append(acc.get_epsilon(1e-5))
+    assert all(a < b for a, b in zip(eps, eps[1:]))
+    acc2 = RDPAccountant()
+    acc2.load_state_dict(acc.state_dict())
+    assert acc2.get_epsilon(1e-5) == eps[-1]
+    assert epsilon(0.3, 2.0, 5, 1e-5) < eps[-1]         # more noise -> less epsilon
+    assert (compute_rdp(0.3, 1.0, 5) >= 0).all()
