@@ -29,7 +29,7 @@ class DataConfig:
     partition_type: str = "iid"         # iid | non_iid (Dirichlet)
     alpha: float = 0.5                  # Dirichlet concentration
     features: str = "pool"              # pool | pca | downsample | raw
-    n_features: int = 4
+    n_features: int = 0                 # 0 = one feature per qubit (VQC angle map needs n_qubits)
     samples_per_client: int = 256       # synthetic data size per client
     test_samples: int = 512
 

@@ -233,11 +233,16 @@ __global__ void __launch_bounds__(256) qfx_pass_kernel(PassArgs A) {
   // ------------------------------------------------------------------ finalize
   const int fin = pd[PF_FINAL];
   if constexpr (ADJ) {
-    if (T > 64) {
+    if (T > 64 && gcount > 0) {
+      // a tile spans WPT = T/64 waves (2 tiles per block at T=128): sum only its own waves
       __syncthreads();
-      for (int g = tid; g < gcount; g += 256) {
-        const float sum = gacc[g * 5 + 0] + gacc[g * 5 + 1] + gacc[g * 5 + 2] + gacc[g * 5 + 3];
-        if (valid) A.gslab[(size_t)tile * G + __float_as_int(gacc[g * 5 + 4])] = sum;
+      const int WPT = T >> 6;
+      for (int e = tid; e < tiles_pb * gcount; e += 256) {
+        const int tb_ = e / gcount, g = e - tb_ * gcount;
+        float sum = 0.f;
+        for (int w = 0; w < WPT; ++w) sum += gacc[g * 5 + tb_ * WPT + w];
+        const long tile_ = (long)blockIdx.x * tiles_pb + tb_;
+        if ((tile_ >> ltps) < A.n_samples) A.gslab[(size_t)tile_ * G + __float_as_int(gacc[g * 5 + 4])] = sum;
       }
     }
   }
@@ -260,8 +265,14 @@ __global__ void __launch_bounds__(256) qfx_pass_kernel(PassArgs A) {
     }
     if (T > 64) {
       __syncthreads();
-      if (tid < C && valid)
-        A.out_read[(size_t)tile * C + tid] = red[tid * 4 + 0] + red[tid * 4 + 1] + red[tid * 4 + 2] + red[tid * 4 + 3];
+      const int WPT = T >> 6;
+      for (int e = tid; e < tiles_pb * C; e += 256) {
+        const int tb_ = e / C, c = e - tb_ * C;
+        float sum = 0.f;
+        for (int w = 0; w < WPT; ++w) sum += red[c * 4 + tb_ * WPT + w];
+        const long tile_ = (long)blockIdx.x * tiles_pb + tb_;
+        if ((tile_ >> ltps) < A.n_samples) A.out_read[(size_t)tile_ * C + c] = sum;
+      }
     }
   }
   if (fin & FIN_STORE) {

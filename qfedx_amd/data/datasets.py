@@ -112,17 +112,18 @@ def build_federated_data(cfg, clients: Optional[list[int]] = None, images: bool 
     """Dispatch on ``cfg.data.dataset`` (ExperimentConfig)."""
     d, m, t = cfg.data, cfg.model, cfg.train
     non_iid = d.partition_type.lower() != "iid"
+    nf = d.n_features if d.n_features > 0 else m.n_qubits
     if d.dataset == "synthetic":
         if images or m.kind == "tinycnn":
             return load_synthetic_images_federated(d.num_clients, m.n_classes, d.samples_per_client,
                                                    d.test_samples, d.alpha, t.seed, clients)
-        return load_synthetic_federated(d.num_clients, m.n_qubits if d.n_features <= 0 else d.n_features,
+        return load_synthetic_federated(d.num_clients, nf,
                                         m.n_classes, d.samples_per_client, d.test_samples, d.alpha,
                                         t.seed, non_iid, clients)
     if d.dataset == "iris":
         return load_iris_federated(d.num_clients, d.partition_type, d.alpha, t.seed, clients=clients)
     if d.dataset == "mnist":
         return load_mnist_federated(d.raw_folder, d.num_clients, tuple(d.digits), d.partition_type,
-                                    d.alpha, d.features, d.n_features, t.seed, d.val_split, clients,
+                                    d.alpha, d.features, nf, t.seed, d.val_split, clients,
                                     keep_images=images or m.kind == "tinycnn")
     raise ValueError(f"unknown dataset '{d.dataset}'")

@@ -1,0 +1,109 @@
+"""CFed adapter: client-batched TinyCNN local training (reference ``client_update``,
+``Classical_FL.py:40-64``; BASELINE config 4 "CFed classical-CNN path, 128 clients").
+
+Per local step all of a rank's clients run together: [K, B] minibatches (keyed shuffles), one
+batched forward/backward (grouped convs + batched GEMMs; fused gfx950 kernels on the HIP backend),
+keyed inverted-dropout masks, CE loss, then ONE fused multi-client SGD-momentum (or Adam) update of
+the flat [K, P] buffer.  Optimizer state is fresh every round, like the reference's per-round
+``optim.SGD(lr, momentum=0.9)`` (``:53``).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ..models import tinycnn as tc
+from .optim import BatchedOptimizer
+from .trainer import BatchPlan, ShardStore
+
+
+class CNNClientTrainer:
+    def __init__(self, num_classes: int, train_cfg, device, backend: str = "torch"):
+        self.C = num_classes
+        self.cfg = train_cfg
+        self.device = torch.device(device)
+        self.backend = backend
+        self._hip = None
+        if backend == "hip":
+            from ..ops.cnn_hip import HipTinyCNN
+            self._hip = HipTinyCNN(num_classes, self.device)
+
+    def loss_and_grads(self, params, xb, yb, wts, mask):
+        if self._hip is not None:
+            return self._hip.loss_and_grads(params, xb, yb, wts, mask)
+        p = params.detach().requires_grad_(True)
+        logits = tc.batched_forward(p, xb, self.C, mask)
+        nll = F.cross_entropy(logits.reshape(-1, self.C), yb.reshape(-1), reduction="none").reshape(yb.shape)
+        loss = (nll * wts).sum(-1)
+        loss.sum().backward()
+        correct = ((logits.argmax(-1) == yb) & (wts > 0)).sum(-1).float()
+        return {"loss": loss.detach(), "grad": p.grad, "correct": correct}
+
+    def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int) -> dict:
+        cfg = self.cfg
+        K = len(local_idx)
+        P = theta_g.numel()
+        if K == 0:
+            return {"params": torch.zeros(0, P, device=self.device), "loss_sum": 0.0, "correct": 0.0,
+                    "samples": 0.0, "steps": 0}
+        li = torch.tensor(local_idx, dtype=torch.int64)
+        cids = [store.client_ids[i] for i in local_idx]
+        plan = BatchPlan(store.counts[li], cids, cfg.batch_size, round_num, cfg.seed, cfg.local_epochs,
+                         cfg.local_steps)
+        params = theta_g.to(self.device).float()[None, :].repeat(K, 1).contiguous()
+        opt = BatchedOptimizer(cfg.optimizer if cfg.optimizer != "spsa" else "sgd", (K, P), self.device,
+                               cfg.learning_rate, cfg.momentum, backend=self.backend)
+        X = store.X[li.to(store.X.device)]
+        Y = store.y[li.to(store.y.device)]
+        idx_d, wts_d, act_d = plan.idx.to(self.device), plan.wts.to(self.device), plan.active.to(self.device)
+        kar = torch.arange(K, device=self.device)[:, None]
+        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+        correct = torch.zeros((), dtype=torch.float64, device=self.device)
+        samples = 0.0
+        for s in range(plan.max_steps):
+            xb = X[kar, idx_d[s]]
+            yb = Y[kar, idx_d[s]]
+            mask = tc.dropout_masks(cids, cfg.batch_size, cfg.seed, round_num, s, self.device)
+            res = self.loss_and_grads(params, xb, yb, wts_d[s], mask)
+            opt.step(params, res["grad"], act_d[s])
+            nvalid = (wts_d[s] > 0).sum(-1).double() * act_d[s].double()
+            loss_sum += (res["loss"].double() * nvalid).sum()
+            correct += (res["correct"].double() * act_d[s].double()).sum()
+            samples += float((plan.wts[s] > 0).sum())
+        return {"params": params, "loss_sum": loss_sum, "correct": correct, "samples": samples,
+                "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
+                "n_samples": store.counts[li].to(torch.float64)}
+
+
+class TinyCNNAdapter:
+    def __init__(self, cfg, device, backend: str):
+        self.C = cfg.model.n_classes
+        self.device = torch.device(device)
+        self.trainer = CNNClientTrainer(self.C, cfg.train, device, backend)
+        self.n_params = tc.n_params(self.C)
+        self.eval_batch = 1024
+
+    def init_params(self, seed: int) -> torch.Tensor:
+        return tc.init_flat(self.C, seed)
+
+    def angle_mask(self):
+        return None
+
+    def state_dict(self, params: torch.Tensor) -> dict:
+        return dict(tc.flat_to_state_dict(params.detach().cpu(), self.C))
+
+    def from_state_dict(self, sd: dict) -> torch.Tensor:
+        return tc.state_dict_to_flat(sd, self.C)
+
+    @torch.no_grad()
+    def evaluate(self, params: torch.Tensor, X: torch.Tensor, y: torch.Tensor):
+        if X.shape[0] == 0:
+            return 0.0, 0.0, 0.0
+        loss_sum = correct = 0.0
+        for s in range(0, X.shape[0], self.eval_batch):
+            xb = X[s: s + self.eval_batch].reshape(1, -1, 1, 28, 28)
+            yb = y[s: s + self.eval_batch]
+            logits = tc.batched_forward(params[None].float(), xb.float(), self.C)[0]
+            loss_sum += float(F.cross_entropy(logits, yb, reduction="sum"))
+            correct += float((logits.argmax(-1) == yb).sum())
+        return loss_sum, correct, float(X.shape[0])

@@ -110,6 +110,31 @@ class VQCClientTrainer:
     def encode(self, X: torch.Tensor) -> torch.Tensor:
         return self.spec.encode_features(X)
 
+    def _body(self, Xs, ys, theta, idx_d, wts_d, act_d, steps: int, round_num: int, method: str):
+        """Device work of one round (capturable): local steps of all clients + metrics."""
+        cfg = self.cfg
+        K = Xs.shape[0]
+        P = theta.numel()
+        params = theta.float()[None, :].repeat(K, 1).contiguous()
+        opt_kind = "sgd" if cfg.optimizer == "spsa" else cfg.optimizer
+        opt = BatchedOptimizer(opt_kind, (K, P), self.device, cfg.learning_rate, cfg.momentum,
+                               backend=self.backend)
+        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
+        correct = torch.zeros((), dtype=torch.float64, device=self.device)
+        kar = torch.arange(K, device=self.device)[:, None]
+        for s in range(steps):
+            bi = idx_d[s]
+            xb = Xs[kar, bi]                     # [K, B, F]
+            yb = ys[kar, bi]
+            xang = self.encode(xb)
+            res = self.engine.loss_and_grads(xang, yb, wts_d[s], params, method,
+                                             rng_keys=(cfg.seed, round_num, s))
+            opt.step(params, res["grad"], act_d[s])
+            nvalid = (wts_d[s] > 0).sum(-1).double() * act_d[s].double()
+            loss_sum += (res["loss"].double() * nvalid).sum()
+            correct += (res["correct"].double() * act_d[s].double()).sum()
+        return params, loss_sum, correct
+
     def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int) -> dict:
         """Train clients ``store[local_idx]`` from the global params; returns their params + metrics."""
         cfg = self.cfg
@@ -122,32 +147,61 @@ class VQCClientTrainer:
         cids = [store.client_ids[i] for i in local_idx]
         plan = BatchPlan(store.counts[li], cids, cfg.batch_size, round_num, cfg.seed,
                          cfg.local_epochs, cfg.local_steps)
-        params = theta_g.to(self.device).float()[None, :].repeat(K, 1).contiguous()
-        opt_kind = "sgd" if cfg.optimizer == "spsa" else cfg.optimizer
-        opt = BatchedOptimizer(opt_kind, (K, P), self.device, cfg.learning_rate, cfg.momentum,
-                               backend=self.backend)
         method = "spsa" if cfg.optimizer == "spsa" else cfg.grad_method
-        Xs = store.X[li.to(store.X.device)]
-        ys = store.y[li.to(store.y.device)]
-        idx_d = plan.idx.to(self.device)
-        wts_d = plan.wts.to(self.device)
-        act_d = plan.active.to(self.device)
-        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
-        correct = torch.zeros((), dtype=torch.float64, device=self.device)
-        samples = 0.0
-        kar = torch.arange(K, device=self.device)[:, None]
-        for s in range(plan.max_steps):
-            bi = idx_d[s]
-            xb = Xs[kar, bi]                     # [K, B, F]
-            yb = ys[kar, bi]
-            xang = self.encode(xb)
-            res = self.engine.loss_and_grads(xang, yb, wts_d[s], params, method,
-                                             rng_keys=(cfg.seed, round_num, s))
-            opt.step(params, res["grad"], act_d[s])
-            nvalid = (wts_d[s] > 0).sum(-1).double() * act_d[s].double()
-            loss_sum += (res["loss"].double() * nvalid).sum()
-            correct += (res["correct"].double() * act_d[s].double()).sum()
-            samples += float((plan.wts[s] > 0).sum())
-        return {"params": params, "loss_sum": loss_sum, "correct": correct, "samples": samples,
-                "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
-                "n_samples": store.counts[li].to(torch.float64)}
+        samples = float((plan.wts > 0).sum())
+        common = {"samples": samples, "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
+                  "n_samples": store.counts[li].to(torch.float64)}
+        if self.use_graph and method == "adjoint":
+            params, loss_sum, correct = self._graphed(store, local_idx, li, theta_g, plan, round_num)
+        else:
+            Xs = store.X[li.to(store.X.device)]
+            ys = store.y[li.to(store.y.device)]
+            params, loss_sum, correct = self._body(Xs, ys, theta_g.to(self.device), plan.idx.to(self.device),
+                                                   plan.wts.to(self.device), plan.active.to(self.device),
+                                                   plan.max_steps, round_num, method)
+        return {"params": params, "loss_sum": loss_sum, "correct": correct, **common}
+
+    # ------------------------------------------------------------------ hipGraph capture
+    @property
+    def use_graph(self) -> bool:
+        return self.backend == "hip" and self.device.type == "cuda" and getattr(self, "graphs", True)
+
+    def _graphed(self, store, local_idx, li, theta_g, plan, round_num):
+        """Replay the whole round as ONE hipGraph (static shapes: clients, steps, batch).
+
+        Captured once per (client set, step count); each round only refreshes the static inputs
+        (global params + this round's minibatch index tables) and replays ~15 launches per local
+        step with no host round trips.
+        """
+        key = (tuple(local_idx), plan.max_steps, plan.B)
+        cache = self.__dict__.setdefault("_graph_cache", {})
+        ent = cache.get(key)
+        if ent is None:
+            dev = self.device
+            ent = {
+                "X": store.X[li.to(store.X.device)].contiguous(),
+                "y": store.y[li.to(store.y.device)].contiguous(),
+                "theta": theta_g.to(dev).float().clone(),
+                "idx": plan.idx.to(dev).clone(), "wts": plan.wts.to(dev).clone(), "act": plan.active.to(dev).clone(),
+            }
+            args = (ent["X"], ent["y"], ent["theta"], ent["idx"], ent["wts"], ent["act"], plan.max_steps,
+                    round_num, "adjoint")
+            # the graph owns its workspaces: eager calls (evaluation) can never regrow/free them
+            ent["ws"] = {}
+            with self.engine.hip.private_workspace(ent["ws"]):
+                side = torch.cuda.Stream(device=dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(side):       # warm-up: JIT modules loaded, workspaces sized
+                    self._body(*args)
+                torch.cuda.current_stream(dev).wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    ent["out"] = self._body(*args)
+            ent["graph"] = g
+            cache[key] = ent
+        ent["theta"].copy_(theta_g.float(), non_blocking=True)
+        ent["idx"].copy_(plan.idx, non_blocking=True)
+        ent["wts"].copy_(plan.wts, non_blocking=True)
+        ent["act"].copy_(plan.active, non_blocking=True)
+        ent["graph"].replay()
+        return ent["out"]

@@ -66,6 +66,13 @@ class VQCEngine:
             raise ValueError(f"unknown backend '{backend}'")
 
     # ------------------------------------------------------------------ helpers
+    def _check(self, xang: torch.Tensor) -> None:
+        # the angle feature map reads one feature per qubit: a narrower input would make the
+        # kernels read past each sample's row
+        if xang.shape[-1] != self.spec.n_qubits:
+            raise ValueError(f"VQC needs {self.spec.n_qubits} features per sample (one per qubit), "
+                             f"got {xang.shape[-1]}; set data.n_features = model.n_qubits")
+
     def _rows(self, xang: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
         K, B, n = xang.shape
         th = theta[:, None, :].expand(K, B, theta.shape[-1])
@@ -76,6 +83,7 @@ class VQCEngine:
     def expz(self, xang: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
         """<Z_c> for [K,B,n] encoded features and per-client theta [K,P] -> [K,B,C]."""
         K, B, _ = xang.shape
+        self._check(xang)
         if self.backend == "hip":
             return self.hip.expz(xang, theta)
         psi = self.prog.run(self._rows(xang, theta))
@@ -91,6 +99,7 @@ class VQCEngine:
                        params: torch.Tensor, method: str = "adjoint", spsa_c: float = 0.1,
                        rng_keys: tuple = (0,)) -> dict:
         spec = self.spec
+        self._check(xang)
         th, a, b = spec.split(params)
         if method == "autograd":
             return self._autograd(xang, y, wmask, params)

@@ -15,6 +15,7 @@ same plan and are tested against each other and the float64 oracle.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -81,6 +82,19 @@ class HipProgram:
         self._ws = {}
 
     # ------------------------------------------------------------------ workspaces
+    @contextlib.contextmanager
+    def private_workspace(self, ws: dict):
+        """Route workspace allocations to ``ws`` (owned by a captured hipGraph).
+
+        A graph bakes buffer addresses into its kernel nodes, so its workspaces must never be
+        regrown or freed by later eager calls (e.g. an evaluation with a larger batch)."""
+        saved = self._ws
+        self._ws = ws
+        try:
+            yield ws
+        finally:
+            self._ws = saved
+
     def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:
         t = self._ws.get(name)
         if t is None or t.numel() < numel or t.dtype != dtype:
@@ -102,6 +116,8 @@ class HipProgram:
     @torch.no_grad()
     def expz(self, xang: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
         K, B, F = xang.shape
+        if F != self.n:
+            raise ValueError(f"expected {self.n} encoded features per sample, got {F}")
         S = K * B
         x = xang.reshape(S, F).float().contiguous()
         th = theta.float().contiguous()
@@ -116,6 +132,8 @@ class HipProgram:
     # ------------------------------------------------------------------ train step
     def loss_and_grads(self, xang, y, wmask, params, spec) -> dict:
         K, B, F = xang.shape
+        if F != self.n:
+            raise ValueError(f"expected {self.n} encoded features per sample, got {F}")
         S = K * B
         C = ext()
         x = xang.reshape(S, F).float().contiguous()

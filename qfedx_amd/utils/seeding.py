@@ -88,8 +88,12 @@ def philox4x32(counter: torch.Tensor, key0: int, key1: int, rounds: int = 10) ->
     implementation in ``qfedx_amd/csrc/philox.h``.
     """
     c0, c1, c2, c3 = (counter[..., i].to(torch.int64) & MASK32 for i in range(4))
-    k0 = torch.full_like(c0, key0 & MASK32)
-    k1 = torch.full_like(c0, key1 & MASK32)
+    if isinstance(key0, torch.Tensor):   # per-row keys, broadcast against the counter
+        k0 = (key0.to(torch.int64) & MASK32).expand_as(c0).clone()
+        k1 = (key1.to(torch.int64) & MASK32).expand_as(c0).clone()
+    else:
+        k0 = torch.full_like(c0, key0 & MASK32)
+        k1 = torch.full_like(c0, key1 & MASK32)
 
     def mul32(a, m):
         # a, m < 2^32: compute 64-bit product split into hi/lo using 16-bit limbs
@@ -123,6 +127,20 @@ def philox_uniform(n: int, key: tuple[int, int], stream: int = 0, offset: int = 
                        torch.full_like(idx, stream & MASK32), torch.zeros_like(idx)], -1)
     out = philox4x32(ctr, key[0], key[1]).reshape(-1)[:n]
     # (x + 1) * 2^-32 in (0, 1]; computed in float64 then rounded like the device does
+    return ((out.to(torch.float64) + 1.0) * (1.0 / 4294967296.0)).to(torch.float32)
+
+
+def philox_uniform_rows(keys: torch.Tensor, n: int, stream: int = 0) -> torch.Tensor:
+    """[K, n] uniforms, row k from key ``keys[k]`` (int64 [K, 2]); runs on keys.device (GPU ok).
+
+    Row k equals ``philox_uniform(n, tuple(keys[k]), stream)`` exactly.
+    """
+    K = keys.shape[0]
+    nblk = (n + 3) // 4
+    idx = torch.arange(nblk, dtype=torch.int64, device=keys.device)
+    ctr = torch.stack([idx & MASK32, (idx >> 32) & MASK32, torch.full_like(idx, stream & MASK32),
+                       torch.zeros_like(idx)], -1)[None].expand(K, nblk, 4)
+    out = philox4x32(ctr, keys[:, 0:1], keys[:, 1:2]).reshape(K, -1)[:, :n]
     return ((out.to(torch.float64) + 1.0) * (1.0 / 4294967296.0)).to(torch.float32)
 
 

@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU tests + bench (graphs on and off) without profiling.
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests/test_gpu_kernels.py -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py --steps 10 --warmup 3 "$@" > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; grep metric gpurun_out/bench.log
+exit $rc

@@ -24,7 +24,8 @@ def _setup(n, L, C, K, B, seed=0, ent="chain"):
 
 
 @pytest.mark.parametrize("n,L,K,B,ent", [(2, 1, 3, 5, "chain"), (4, 2, 4, 7, "chain"), (6, 2, 2, 9, "ring"),
-                                         (8, 3, 3, 4, "chain"), (12, 2, 2, 3, "ring"), (14, 2, 2, 2, "chain"),
+                                         (8, 3, 3, 4, "chain"), (10, 2, 3, 3, "chain"), (11, 2, 3, 3, "ring"),
+                                         (12, 2, 2, 3, "ring"), (14, 2, 2, 2, "chain"),
                                          (16, 3, 2, 2, "chain")])
 @pytest.mark.parametrize("jit", ["1", "0"])
 def test_forward_expz_matches_torch(cuda, n, L, K, B, ent, jit, monkeypatch):
@@ -51,7 +52,7 @@ def test_forward_matches_float64_oracle(cuda):
     assert torch.allclose(z, ref, atol=2e-5)
 
 
-@pytest.mark.parametrize("n,L,K,B", [(3, 2, 2, 4), (4, 2, 3, 6), (8, 2, 2, 5), (13, 2, 2, 2), (16, 2, 2, 2)])
+@pytest.mark.parametrize("n,L,K,B", [(3, 2, 2, 4), (4, 2, 3, 6), (8, 2, 2, 5), (10, 2, 2, 3), (11, 2, 3, 3), (13, 2, 2, 2), (16, 2, 2, 2)])
 @pytest.mark.parametrize("jit", ["1", "0"])
 def test_adjoint_grads_match_torch(cuda, n, L, K, B, jit, monkeypatch):
     monkeypatch.setenv("QFEDX_JIT", jit)
@@ -108,3 +109,38 @@ def test_fused_fedavg_reduce_matches_torch(cuda, dp):
     a = cpu.finalize(cpu.local_reduce(tk, tg, w, 4, ids))[0]
     b = gpu.finalize(gpu.local_reduce(tk.to(cuda), tg.to(cuda), w.to(cuda), 4, ids).cpu())[0]
     assert torch.allclose(a, b, atol=1e-6, rtol=1e-6), (a - b).abs().max()
+
+
+def test_graph_round_matches_eager(cuda):
+    """hipGraph-replayed local rounds produce the same global model as eager launches."""
+    from tests.test_fl import small_cfg
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.parallel.dist import init_distributed
+    outs = []
+    for graphs in (True, False):
+        cfg = small_cfg(num_rounds=3, n_qubits=6, device="cuda", backend="hip")
+        dev = torch.device("cuda", 0)
+        world = init_distributed(dev)
+        import qfedx_amd.fl.trainer as tr
+        old = tr.VQCClientTrainer.use_graph
+        tr.VQCClientTrainer.use_graph = property(lambda self, g=graphs: g)
+        try:
+            outs.append(run_experiment(cfg, world=world, device=dev, backend="hip"))
+        finally:
+            tr.VQCClientTrainer.use_graph = old
+    assert torch.equal(outs[0]["params"], outs[1]["params"])
+
+
+def test_hip_federated_run_matches_cpu(cuda):
+    from tests.test_fl import small_cfg
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.parallel.dist import init_distributed
+    # SGD: Adam would blow fp32 noise on the zero-gradient angles (last-layer RZ, unmeasured
+    # qubits) up to lr-sized steps of random sign, so those would not be comparable
+    cpu = run_experiment(small_cfg(num_rounds=2, optimizer="sgd"))
+    dev = torch.device("cuda", 0)
+    gpu = run_experiment(small_cfg(num_rounds=2, optimizer="sgd", device="cuda", backend="hip"),
+                         world=init_distributed(dev), device=dev, backend="hip")
+    assert torch.allclose(gpu["params"].cpu(), cpu["params"], atol=1e-4)
+    for hg, hc in zip(gpu["history"], cpu["history"]):
+        assert abs(hg["train_loss"] - hc["train_loss"]) < 1e-4
