@@ -80,11 +80,11 @@ def main():
             torch.cuda.synchronize()
 
     for r in range(args.warmup):
-        runner.run_round(r)
+        runner.run_round(r, sync=False)
     sync()
     t0 = time.perf_counter()
     for r in range(args.warmup, args.warmup + args.steps):
-        runner.run_round(r)
+        runner.run_round(r, sync=False)
     sync()
     dt = time.perf_counter() - t0
     dt = max_over_ranks(dt, world)

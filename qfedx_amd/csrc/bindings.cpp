@@ -43,7 +43,7 @@ std::string jit_source(const std::vector<int>& blob, int p, bool adjoint);
 }  // namespace qfx
 
 extern "C" {
-int qfx_launch_pass(int R, int adjoint, const int* blob, int pass_off, int k, int n, int n_ops, int n_gates, float2* psi, float2* lam,
+int qfx_launch_pass(int R, int adjoint, const int* blob, int pass_off, int k, int n, int n_ops, int n_gates, void* psi, void* lam,
                     const float* params, int p_stride, int spc, const float* xang, int x_stride,
                     const float* w_read, float* out_read, float* gslab, int n_samples, int n_grad_ops,
                     hipStream_t stream);

@@ -15,18 +15,31 @@ namespace qfx {
 // global memory inside the op loop (a generic pointer could alias those stores)
 typedef const __attribute__((address_space(4))) int* cint_p;
 
-struct M2 { float2 a, b, c, d; };   // [[a, b], [c, d]]
+// Complex amplitudes are native 2-wide float vectors: every complex op below is written so that the
+// gfx950 backend emits packed fp32 math (v_pk_mul_f32 / v_pk_fma_f32, two lanes of math per issue)
+// with the re/im swap and sign flips folded into op_sel / neg modifiers - a complex multiply is 2
+// packed instructions, an Im(conj(l) p) accumulation 1.
+typedef float v2f __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ float2 mk(float x, float y) { return make_float2(x, y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
-}
-__device__ __forceinline__ float2 cfma(float2 a, float2 b, float2 c) {  // a*b + c
-  return make_float2(fmaf(a.x, b.x, fmaf(-a.y, b.y, c.x)), fmaf(a.x, b.y, fmaf(a.y, b.x, c.y)));
-}
-__device__ __forceinline__ float2 conjf2(float2 a) { return make_float2(a.x, -a.y); }
-__device__ __forceinline__ float imcl(float2 l, float2 p) { return l.x * p.y - l.y * p.x; }  // Im(conj(l) p)
-__device__ __forceinline__ float recl(float2 l, float2 p) { return l.x * p.x + l.y * p.y; }  // Re(conj(l) p)
+struct M2 { v2f a, b, c, d; };   // [[a, b], [c, d]]
+
+__device__ __forceinline__ v2f mk(float x, float y) { return v2f{x, y}; }
+__device__ __forceinline__ v2f splat(float x) { return v2f{x, x}; }
+__device__ __forceinline__ v2f sw(v2f v) { return __builtin_shufflevector(v, v, 1, 0); }
+__device__ __forceinline__ v2f pfma(v2f a, v2f b, v2f c) { return __builtin_elementwise_fma(a, b, c); }
+// a * b  (put the gate-uniform factor in `a`: its splat / sign vector is hoisted out of loops)
+// (the re/im swap is applied to a fresh product, never to a state register: swaps of state registers
+// get CSE'd across gates and then materialised with v_pk_mov instead of folding into op_sel)
+__device__ __forceinline__ v2f cmul(v2f a, v2f b) { return pfma(splat(a.x), b, sw(b * mk(a.y, -a.y))); }
+// a * b + c
+__device__ __forceinline__ v2f cfma(v2f a, v2f b, v2f c) { return pfma(splat(a.x), b, sw(pfma(b, mk(a.y, -a.y), sw(c)))); }
+__device__ __forceinline__ v2f conjf2(v2f a) { return mk(a.x, -a.y); }
+__device__ __forceinline__ float imcl(v2f l, v2f p) { return l.x * p.y - l.y * p.x; }  // Im(conj(l) p)
+__device__ __forceinline__ float recl(v2f l, v2f p) { return l.x * p.x + l.y * p.y; }  // Re(conj(l) p)
+// packed accumulators: Im(conj(l) p) = acc.x - acc.y after acc = pfma(l, sw(p), acc);
+//                      Re(conj(l) p) = acc.x + acc.y after acc = pfma(l, p, acc)
+__device__ __forceinline__ v2f acc_im(v2f acc, v2f l, v2f p) { return pfma(l, sw(p), acc); }
+__device__ __forceinline__ v2f acc_re(v2f acc, v2f l, v2f p) { return pfma(l, p, acc); }
 
 __device__ __forceinline__ bool kind_is_diag(int k) {
   return k == K_RZ || k == K_P || k == K_Z || k == K_S || k == K_SDG || k == K_T || k == K_TDG;
@@ -42,7 +55,7 @@ __device__ __forceinline__ float gate_angle(cint_p gt, int gi, const float* prow
 }
 
 // (c, s) = (cos, sin) of the half angle for RX/RY/RZ, of the full angle for P
-__device__ __forceinline__ float2 gate_cs(cint_p gt, int gi, const float* prow,
+__device__ __forceinline__ v2f gate_cs(cint_p gt, int gi, const float* prow,
                                           const float* xrow, int n_theta) {
   const float ang = gate_angle(gt, gi, prow, xrow, n_theta);
   const float x = gt[gi * GATE_WORDS] == K_P ? ang : 0.5f * ang;
@@ -52,11 +65,11 @@ __device__ __forceinline__ float2 gate_cs(cint_p gt, int gi, const float* prow,
 }
 
 // full 2x2 (diagonal kinds too); inverse = conjugate transpose
-__device__ __forceinline__ M2 gate_m2(int kind, float2 cs, bool inv) {
+__device__ __forceinline__ M2 gate_m2(int kind, v2f cs, bool inv) {
   const float r2 = 0.70710678118654752f, t = 0.70710678118654752f;
   const float c = cs.x, s = cs.y;
   M2 m;
-  const float2 z = mk(0.f, 0.f), one = mk(1.f, 0.f);
+  const v2f z = mk(0.f, 0.f), one = mk(1.f, 0.f);
   switch (kind) {
     case K_RX: m = {mk(c, 0.f), mk(0.f, -s), mk(0.f, -s), mk(c, 0.f)}; break;
     case K_RY: m = {mk(c, 0.f), mk(-s, 0.f), mk(s, 0.f), mk(c, 0.f)}; break;
@@ -90,58 +103,76 @@ __device__ __forceinline__ int pbit(int p, int r, int tl, uint32_t gbase) {
   return (gbase >> (p - PHYS_NONTILE)) & 1;
 }
 
+// 2x2 complex matvec row:  m0 * x + m1 * y  in 4 packed instructions.  cmul(a, x) = a.x*x + sw(x*(a.y,-a.y)),
+// so the single re/im swap lands on a one-use temporary and folds into op_sel (a swap of x or y
+// itself would be shared by both output rows and materialised with v_pk_mov).
+__device__ __forceinline__ v2f mrow(v2f m0, v2f m1, v2f x, v2f y) {
+  const v2f t = pfma(x, mk(m0.y, -m0.y), mk(m1.y, -m1.y) * y);
+  return pfma(splat(m0.x), x, pfma(splat(m1.x), y, sw(t)));
+}
+
 template <int R, int RBT>
-__device__ __forceinline__ void m2_apply(float2 (&a)[R], const M2& m) {
+__device__ __forceinline__ void m2_apply(v2f (&a)[R], const M2& m) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (r & (1 << RBT)) continue;
     const int r1 = r | (1 << RBT);
-    const float2 x = a[r], y = a[r1];
-    a[r] = cfma(m.b, y, cmul(m.a, x));
-    a[r1] = cfma(m.d, y, cmul(m.c, x));
+    const v2f x = a[r], y = a[r1];
+    a[r] = mrow(m.a, m.b, x, y);
+    a[r1] = mrow(m.c, m.d, x, y);
   }
 }
 
-// adjoint step for one gate on register bit RBT: gradient partial, then the inverse gate on psi
-// and lambda.  CLS (compile time): 0 generic non-diagonal, 1 diagonal, 2 RX (grad X), 3 RY (grad Y),
-// 4 RZ/P (grad Z, diagonal)
+// adjoint step for one gate on register bit RBT: the inverse gate on psi and lambda, then the
+// gradient partial.  The generator (X, Y or Z) commutes with its own rotation, so
+// Im<lambda|P|psi> is the same before and after un-applying the gate; taking it from the new values
+// keeps every swapped operand single-use (foldable).  CLS (compile time): 0 generic non-diagonal,
+// 1 diagonal, 2 RX (grad X), 3 RY (grad Y), 4 RZ/P (grad Z, diagonal)
 enum { CLS_GEN = 0, CLS_DIAG = 1, CLS_RX = 2, CLS_RY = 3, CLS_RZ = 4 };
 template <int R, int RBT, int CLS>
-__device__ __forceinline__ float adj_step(float2 (&a)[R], float2 (&l)[R], const M2& mi) {
-  float acc = 0.f;
+__device__ __forceinline__ float adj_step(v2f (&a)[R], v2f (&l)[R], const M2& mi) {
+  v2f acc = mk(0.f, 0.f);
+  // gate-uniform factors, hoisted out of the register loop
+  const v2f c2 = splat(mi.a.x);
+  const v2f rxs = mk(mi.b.y, -mi.b.y);      // RX^dag off-diagonal: i*s*p = sw(p * (s, -s))
+  const v2f rys = splat(mi.b.x), rysn = splat(mi.c.x);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (r & (1 << RBT)) continue;
     const int r1 = r | (1 << RBT);
-    const float2 p0 = a[r], p1 = a[r1], l0 = l[r], l1 = l[r1];
-    if constexpr (CLS == CLS_RX) acc += imcl(l0, p1) + imcl(l1, p0);
-    if constexpr (CLS == CLS_RY) acc += recl(l1, p0) - recl(l0, p1);
-    if constexpr (CLS == CLS_RZ) acc += imcl(l0, p0) - imcl(l1, p1);
+    const v2f p0 = a[r], p1 = a[r1], l0 = l[r], l1 = l[r1];
+    v2f q0, q1, m0, m1;
     if constexpr (CLS == CLS_DIAG || CLS == CLS_RZ) {
-      a[r] = cmul(mi.a, p0);
-      a[r1] = cmul(mi.d, p1);
-      l[r] = cmul(mi.a, l0);
-      l[r1] = cmul(mi.d, l1);
-    } else if constexpr (CLS == CLS_RX) {   // RX^dag = [[c, i s], [i s, c]]: real c, imaginary off-diagonal
-      const float c = mi.a.x, s = mi.b.y;
-      a[r] = mk(fmaf(c, p0.x, -s * p1.y), fmaf(c, p0.y, s * p1.x));
-      a[r1] = mk(fmaf(c, p1.x, -s * p0.y), fmaf(c, p1.y, s * p0.x));
-      l[r] = mk(fmaf(c, l0.x, -s * l1.y), fmaf(c, l0.y, s * l1.x));
-      l[r1] = mk(fmaf(c, l1.x, -s * l0.y), fmaf(c, l1.y, s * l0.x));
+      q0 = cmul(mi.a, p0);
+      q1 = cmul(mi.d, p1);
+      m0 = cmul(mi.a, l0);
+      m1 = cmul(mi.d, l1);
+    } else if constexpr (CLS == CLS_RX) {   // RX^dag = [[c, i s], [i s, c]]
+      q0 = pfma(c2, p0, sw(p1 * rxs));
+      q1 = pfma(c2, p1, sw(p0 * rxs));
+      m0 = pfma(c2, l0, sw(l1 * rxs));
+      m1 = pfma(c2, l1, sw(l0 * rxs));
     } else if constexpr (CLS == CLS_RY) {   // RY^dag = [[c, s], [-s, c]] real
-      const float c = mi.a.x, s = mi.b.x;
-      a[r] = mk(fmaf(c, p0.x, s * p1.x), fmaf(c, p0.y, s * p1.y));
-      a[r1] = mk(fmaf(c, p1.x, mi.c.x * p0.x), fmaf(c, p1.y, mi.c.x * p0.y));
-      l[r] = mk(fmaf(c, l0.x, s * l1.x), fmaf(c, l0.y, s * l1.y));
-      l[r1] = mk(fmaf(c, l1.x, mi.c.x * l0.x), fmaf(c, l1.y, mi.c.x * l0.y));
+      q0 = pfma(c2, p0, rys * p1);
+      q1 = pfma(c2, p1, rysn * p0);
+      m0 = pfma(c2, l0, rys * l1);
+      m1 = pfma(c2, l1, rysn * l0);
     } else {
-      a[r] = cfma(mi.b, p1, cmul(mi.a, p0));
-      a[r1] = cfma(mi.d, p1, cmul(mi.c, p0));
-      l[r] = cfma(mi.b, l1, cmul(mi.a, l0));
-      l[r1] = cfma(mi.d, l1, cmul(mi.c, l0));
+      q0 = mrow(mi.a, mi.b, p0, p1);
+      q1 = mrow(mi.c, mi.d, p0, p1);
+      m0 = mrow(mi.a, mi.b, l0, l1);
+      m1 = mrow(mi.c, mi.d, l0, l1);
     }
+    a[r] = q0;
+    a[r1] = q1;
+    l[r] = m0;
+    l[r1] = m1;
+    if constexpr (CLS == CLS_RX) { acc = acc_im(acc, m0, q1); acc = acc_im(acc, m1, q0); }
+    if constexpr (CLS == CLS_RY) { acc = acc_re(acc, m1, q0); acc = acc_re(acc, -m0, q1); }
+    if constexpr (CLS == CLS_RZ) { acc = acc_im(acc, m0, q0); acc = acc_im(acc, -m1, q1); }
   }
-  return acc;
+  if constexpr (CLS == CLS_RY) return acc.x + acc.y;
+  return acc.x - acc.y;
 }
 
 #define QFX_CLS_DISPATCH(cls, RBT_, OUT)                                   \
@@ -154,17 +185,17 @@ __device__ __forceinline__ float adj_step(float2 (&a)[R], float2 (&l)[R], const 
   }
 
 template <int R, int RB, int TT, bool ADJ>
-__device__ __forceinline__ void cx_apply(float2 (&a)[R], float2 (&l)[R], int ctl, int tl, uint32_t gbase) {
+__device__ __forceinline__ void cx_apply(v2f (&a)[R], v2f (&l)[R], int ctl, int tl, uint32_t gbase) {
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     if (r & (1 << TT)) continue;
     const int r1 = r | (1 << TT);
     const bool c = pbit<RB>(ctl, r, tl, gbase);
-    const float2 x = a[r], y = a[r1];
+    const v2f x = a[r], y = a[r1];
     a[r] = c ? y : x;
     a[r1] = c ? x : y;
     if constexpr (ADJ) {
-      const float2 lx = l[r], ly = l[r1];
+      const v2f lx = l[r], ly = l[r1];
       l[r] = c ? ly : lx;
       l[r1] = c ? lx : ly;
     }
@@ -191,7 +222,7 @@ __device__ __forceinline__ uint32_t xor_bits(cint_p tab, int tb, int tl) {
 }
 
 template <int R>
-__device__ __forceinline__ void do_remap(float2 (&a)[R], float2* __restrict__ xb, cint_p tab, int tb, int tl) {
+__device__ __forceinline__ void do_remap(v2f (&a)[R], v2f* __restrict__ xb, cint_p tab, int tb, int tl) {
   cint_p wr = tab;
   cint_p wt = tab + R;
   cint_p rr = tab + R + tb;
@@ -206,7 +237,24 @@ __device__ __forceinline__ void do_remap(float2 (&a)[R], float2* __restrict__ xb
   for (int r = 0; r < R; ++r) a[r] = xb[(uint32_t)rr[r] ^ rthr];
 }
 
-// wave-level sum over the T lanes of a tile group (T power of two <= 64)
+// DPP lane permutation inside a 16-lane row (VALU, no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// sum over aligned groups of G <= 16 lanes with row-local DPP: xor 1, xor 2 (quad_perm), then the
+// half-row and row mirrors (every lane of a quad / half-row already holds the same partial sum)
+template <int G>
+__device__ __forceinline__ float row_sum(float v) {
+  if constexpr (G >= 2) v += dppf<0xB1>(v);    // quad_perm [1,0,3,2]
+  if constexpr (G >= 4) v += dppf<0x4E>(v);    // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) v += dppf<0x141>(v);   // row_half_mirror
+  if constexpr (G >= 16) v += dppf<0x140>(v);  // row_mirror
+  return v;
+}
+
+// wave-level sum over the T lanes of a tile group (T power of two <= 64), runtime T
 __device__ __forceinline__ float group_sum(float v, int T) {
   for (int o = (T < 64 ? T : 64) >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
@@ -218,12 +266,12 @@ __device__ __forceinline__ float4 prefix_vec(cint_p blob, int q, const float* pr
   cint_p gt = blob + blob[HF_GATES];
   cint_p pl = blob + blob[blob[HF_PREFIX] + q];
   const int cnt = pl[0];
-  float2 v0 = mk(1.f, 0.f), v1 = mk(0.f, 0.f);
+  v2f v0 = mk(1.f, 0.f), v1 = mk(0.f, 0.f);
   for (int i = 0; i < cnt; ++i) {
     const int gi = pl[1 + i];
     const M2 m = gate_m2(gt[gi * GATE_WORDS], gate_cs(gt, gi, prow, xrow, n_theta), false);
-    const float2 n0 = cfma(m.b, v1, cmul(m.a, v0));
-    const float2 n1 = cfma(m.d, v1, cmul(m.c, v0));
+    const v2f n0 = cfma(m.b, v1, cmul(m.a, v0));
+    const v2f n1 = cfma(m.d, v1, cmul(m.c, v0));
     v0 = n0;
     v1 = n1;
   }
@@ -233,8 +281,8 @@ __device__ __forceinline__ float4 prefix_vec(cint_p blob, int q, const float* pr
 struct PassArgs {
   const int* blob;
   int pass_off;
-  float2* psi;           // [n_samples, 2^n]
-  float2* lam;           // adjoint only
+  v2f* psi;           // [n_samples, 2^n]
+  v2f* lam;           // adjoint only
   const float* params;   // [n_clients, p_stride]
   int p_stride;
   int spc;               // samples per client (sample s uses params row s / spc)

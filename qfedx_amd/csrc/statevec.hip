@@ -55,12 +55,12 @@ __global__ void __launch_bounds__(256) qfx_pass_kernel(PassArgs A) {
     const int nn = pd[PF_NNONTILE];
     for (int j = 0; j < nn; ++j) gbase |= ((tau >> j) & 1u) << pd[PF_NONTILE + j];
   }
-  // LDS: [exchange 256R float2][readout 64 f][grad partials A.n_grad*5 f][coef tiles_pb*G float2]
+  // LDS: [exchange 256R v2f][readout 64 f][grad partials A.n_grad*5 f][coef tiles_pb*G v2f]
   //      [prefix vectors tiles_pb*n float4]; tables only when a tile spans >= one wave (T >= 64)
-  float2* xb = reinterpret_cast<float2*>(smem) + (size_t)tib * (1u << k);
-  float* red = reinterpret_cast<float*>(smem + 256 * R * sizeof(float2));
+  v2f* xb = reinterpret_cast<v2f*>(smem) + (size_t)tib * (1u << k);
+  float* red = reinterpret_cast<float*>(smem + 256 * R * sizeof(v2f));
   float* gacc = red + 64;
-  float2* ctab = reinterpret_cast<float2*>(gacc + ((A.n_grad * 5 + 3) & ~3));
+  v2f* ctab = reinterpret_cast<v2f*>(gacc + ((A.n_grad * 5 + 3) & ~3));
   float4* vtab = reinterpret_cast<float4*>(ctab + ((tiles_pb * G + 1) & ~1));
   const int init = pd[PF_INIT];
   const bool use_tab = T >= 64;
@@ -85,14 +85,14 @@ __global__ void __launch_bounds__(256) qfx_pass_kernel(PassArgs A) {
     __syncthreads();
   }
 
-  float2 a[R];
-  float2 l[R];
+  v2f a[R];
+  v2f l[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) l[r] = mk(0.f, 0.f);
 
   // ------------------------------------------------------------------ init
   if (init == INIT_PRODUCT) {
-    float2 base = mk(1.f, 0.f);
+    v2f base = mk(1.f, 0.f);
     const int nn = pd[PF_NNONTILE];
     for (int j = 0; j < nn; ++j) {
       const int q = pd[PF_NONTILE + j];
@@ -111,8 +111,8 @@ __global__ void __launch_bounds__(256) qfx_pass_kernel(PassArgs A) {
       const float4 v = use_tab ? vtab[tib * n + q] : prefix_vec(blob, q, prow, xrow, n_theta);
 #pragma unroll
       for (int r = 0; r < (1 << p); ++r) {
-        a[r | (1 << p)] = cmul(a[r], mk(v.z, v.w));
-        a[r] = cmul(a[r], mk(v.x, v.y));
+        a[r | (1 << p)] = cmul(mk(v.z, v.w), a[r]);
+        a[r] = cmul(mk(v.x, v.y), a[r]);
       }
     }
   } else {
@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(256) qfx_pass_kernel(PassArgs A) {
       const int kind = gt[oc * GATE_WORDS];
       const M2 m = gate_m2(kind, use_tab ? ctab[tib * G + oc] : gate_cs(gt, oc, prow, xrow, n_theta), ADJ);
       const int bit = pbit<RB>(oa, 0, tl, gbase);   // thread or non-tile bit: same for all registers
-      const float2 ph = bit ? m.d : m.a;
+      const v2f ph = bit ? m.d : m.a;
       if constexpr (ADJ) {
         const int slot = gt[oc * GATE_WORDS + 3];
         if (slot >= 0 && slot < n_theta && (kind == K_RZ || kind == K_P)) {
@@ -211,8 +211,8 @@ __global__ void __launch_bounds__(256) qfx_pass_kernel(PassArgs A) {
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        a[r] = cmul(a[r], ph);
-        if constexpr (ADJ) l[r] = cmul(l[r], ph);
+        a[r] = cmul(ph, a[r]);
+        if constexpr (ADJ) l[r] = cmul(ph, l[r]);
       }
     } else if (code == OP_REMAP) {
       do_remap<R>(a, xb, blob + oa, tb, tl);
@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(256) qfx_pass_kernel(PassArgs A) {
 
 // ----------------------------------------------------------------------------------- launchers
 extern "C" int qfx_launch_pass(int R, int adjoint, const int* blob, int pass_off, int k, int n, int n_ops,
-                               int n_gates, float2* psi, float2* lam, const float* params, int p_stride, int spc,
+                               int n_gates, void* psi, void* lam, const float* params, int p_stride, int spc,
                                const float* xang, int x_stride, const float* w_read, float* out_read,
                                float* gslab, int n_samples, int n_grad_ops, hipStream_t stream) {
   using namespace qfx;
@@ -303,12 +303,12 @@ extern "C" int qfx_launch_pass(int R, int adjoint, const int* blob, int pass_off
   const long tiles_total = (long)n_samples << (n - k);
   const long blocks = (tiles_total + tiles_pb - 1) / tiles_pb;
   if (blocks <= 0) return 0;
-  PassArgs A{blob, pass_off, psi, lam, params, p_stride, spc, xang, x_stride, w_read, out_read, gslab, n_samples,
+  PassArgs A{blob, pass_off, static_cast<v2f*>(psi), static_cast<v2f*>(lam), params, p_stride, spc, xang, x_stride, w_read, out_read, gslab, n_samples,
              n_grad_ops};
   const bool tab = (1 << tb) >= 64;
-  const size_t lds = 256 * (size_t)R * sizeof(float2) + 64 * sizeof(float) +
+  const size_t lds = 256 * (size_t)R * sizeof(v2f) + 64 * sizeof(float) +
                      (size_t)((n_grad_ops * 5 + 3) & ~3) * sizeof(float) +
-                     (tab ? (size_t)((tiles_pb * n_gates + 1) & ~1) * sizeof(float2) + (size_t)tiles_pb * n * sizeof(float4)
+                     (tab ? (size_t)((tiles_pb * n_gates + 1) & ~1) * sizeof(v2f) + (size_t)tiles_pb * n * sizeof(float4)
                           : 0);
   if (lds > 160 * 1024) return -4;
   dim3 grid((unsigned)blocks), block(256);

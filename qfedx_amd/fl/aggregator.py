@@ -114,8 +114,10 @@ class Aggregator:
             total = torch.remainder(total, sa.modulus)
         return total
 
-    def finalize(self, reduced: torch.Tensor) -> tuple[torch.Tensor, float]:
-        """Decode the all-reduced [P+1] vector -> (mean update [P] float64, weight sum)."""
+    def finalize(self, reduced: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """Decode the all-reduced [P+1] vector -> (mean update [P] float64, weight sum (0-d tensor)).
+
+        Stays on the device (no host read-back), so a round can be enqueued without a sync."""
         if self.secure_agg:
             from ..privacy.secure_agg import decode_fixed
             vals = decode_fixed(reduced, self.secagg.scale, self.secagg.bits)
@@ -123,10 +125,14 @@ class Aggregator:
             vals = reduced.double() / EXACT_SCALE
         else:
             vals = reduced.double()
-        wsum = float(vals[self.P])
-        return vals[: self.P] / max(wsum, 1e-300), wsum
+        wsum = vals[self.P]
+        return vals[: self.P] / wsum.clamp(min=1e-300), wsum
 
-    def apply(self, theta_g: torch.Tensor, mean_update: torch.Tensor, server_lr: float = 1.0) -> torch.Tensor:
+    def apply(self, theta_g: torch.Tensor, mean_update: torch.Tensor, server_lr: float = 1.0,
+              wsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """theta_g + lr * mean_update; a round with zero total weight (everyone dropped) keeps theta_g."""
         new = theta_g.double() + server_lr * mean_update.to(theta_g.device)
+        if wsum is not None:
+            new = torch.where(wsum.to(new.device) > 0, new, theta_g.double())
         return new.to(theta_g.dtype)
 

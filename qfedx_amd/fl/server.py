@@ -25,6 +25,7 @@ import torch
 from ..parallel.dist import World, all_reduce_, barrier, broadcast_, shard_clients
 from ..privacy.accountant import RDPAccountant
 from ..privacy.secure_agg import SecureAggregator
+from ..utils.device import h2d
 from ..utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
 from ..utils.logging import MetricsWriter, get_logger
 from ..utils.seeding import generator, np_rng
@@ -124,15 +125,20 @@ class FederatedRunner:
         self.log.info(f"resumed from {path} at round {self.start_round}")
 
     # ------------------------------------------------------------------ main loop
-    def run_round(self, r: int) -> dict:
+    def run_round(self, r: int, sync: bool = True) -> dict:
+        """One federated round.  With ``sync=False`` nothing reads device memory back: the round is
+        only enqueued (the host can build round r+1 while the GPU runs round r) and the returned
+        record holds device tensors until :meth:`resolve_record`."""
         t = self.cfg.train
         p = self.cfg.privacy
         participants = sample_participants(self.num_clients, t.client_fraction, t.seed, r)
         dropped = sample_dropouts(participants, t.dropout_prob, t.seed, r)
         dropped_set = set(dropped)
-        local_part = [i for i, c in enumerate(self.local_ids) if c in set(participants)]
+        part_set = set(participants)
+        local_part = [i for i, c in enumerate(self.local_ids) if c in part_set]
         local_alive = [i for i in local_part if self.local_ids[i] not in dropped_set]
         t0 = time.perf_counter()
+        dev = self.device
         with self.timer.phase("local_train"):
             res = self.adapter.trainer.run_round(self.store, local_alive, self.params, r)
         with self.timer.phase("aggregate"):
@@ -142,17 +148,16 @@ class FederatedRunner:
                 else:
                     w = res["n_samples"].double()
                 contrib = self.aggregator.local_reduce(
-                    res["params"], self.params, w.to(self.device), r,
+                    res["params"], self.params, h2d(w, dev), r,
                     [self.local_ids[i] for i in local_alive],
                     participants=[c for c in participants], dropped=dropped)
             else:
-                contrib = torch.zeros(self.P + 1, dtype=torch.int64, device=self.device)
-            loss_sum = res.get("loss_sum", 0.0)
-            correct = res.get("correct", 0.0)
-            metrics = torch.stack([torch.as_tensor(loss_sum, dtype=torch.float64, device=self.device),
-                                   torch.as_tensor(correct, dtype=torch.float64, device=self.device),
-                                   torch.tensor(float(res.get("samples", 0.0)), dtype=torch.float64, device=self.device),
-                                   torch.tensor(float(res.get("steps", 0)), dtype=torch.float64, device=self.device)])
+                contrib = torch.zeros(self.P + 1, dtype=torch.int64, device=dev)
+            dev_m = torch.stack([torch.as_tensor(res.get("loss_sum", 0.0), dtype=torch.float64).to(dev),
+                                 torch.as_tensor(res.get("correct", 0.0), dtype=torch.float64).to(dev)])
+            host_m = h2d(torch.tensor([float(res.get("samples", 0.0)), float(res.get("steps", 0))],
+                                      dtype=torch.float64), dev)
+            metrics = torch.cat([dev_m, host_m])
         with self.timer.phase("comm"):
             if p.secure_agg:
                 all_reduce_(contrib, self.world)          # int64 ring elements: exact, mod later
@@ -165,24 +170,28 @@ class FederatedRunner:
                 all_reduce_(buf, self.world)
                 mean_upd, wsum = self.aggregator.finalize(buf[: self.P + 1])
                 metrics = buf[self.P + 1:].double() / EXACT_SCALE
-        if wsum > 0:
-            self.params = self.aggregator.apply(self.params, mean_upd)
+        self.params = self.aggregator.apply(self.params, mean_upd, wsum=wsum)
         if p.dp:
             q = len(participants) / self.num_clients
             self.accountant.step(q, p.noise_multiplier, 1)
-        if self.device.type == "cuda":
-            torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        m = metrics.double().cpu().tolist()
         rec = {"round": r + 1, "participants": len(participants), "dropped": len(dropped),
-               "train_loss": m[0] / max(m[2], 1.0) if m[2] else float("nan"),
-               "train_acc": m[1] / max(m[2], 1.0) if m[2] else float("nan"),
-               "local_steps": int(m[3]), "round_time_s": dt,
-               "local_steps_per_s": m[3] / dt if dt > 0 else 0.0,
+               "_metrics": metrics, "_t0": t0,
                "comm_bytes_per_rank": int((self.P + 1 + 4) * 8),
                "upload_bytes": int(len(participants) - len(dropped)) * (self.P + 1) * 4}
         if p.dp:
             rec["epsilon"] = self.accountant.get_epsilon(p.delta)
+        return self.resolve_record(rec) if sync else rec
+
+    def resolve_record(self, rec: dict) -> dict:
+        """Read a round's metrics back (syncs with the device) and fill the derived fields."""
+        if "_metrics" not in rec:
+            return rec
+        m = rec.pop("_metrics").double().cpu().tolist()
+        dt = time.perf_counter() - rec.pop("_t0")
+        rec.update({"train_loss": m[0] / max(m[2], 1.0) if m[2] else float("nan"),
+                    "train_acc": m[1] / max(m[2], 1.0) if m[2] else float("nan"),
+                    "local_steps": int(round(m[3])), "round_time_s": dt,
+                    "local_steps_per_s": m[3] / dt if dt > 0 else 0.0})
         return rec
 
     def run(self) -> dict:

@@ -16,6 +16,7 @@ from typing import Optional
 
 import torch
 
+from ..utils.device import h2d
 from ..utils.seeding import generator
 from .optim import BatchedOptimizer
 
@@ -154,10 +155,11 @@ class VQCClientTrainer:
         if self.use_graph and method == "adjoint":
             params, loss_sum, correct = self._graphed(store, local_idx, li, theta_g, plan, round_num)
         else:
-            Xs = store.X[li.to(store.X.device)]
-            ys = store.y[li.to(store.y.device)]
-            params, loss_sum, correct = self._body(Xs, ys, theta_g.to(self.device), plan.idx.to(self.device),
-                                                   plan.wts.to(self.device), plan.active.to(self.device),
+            lid = h2d(li, store.X.device)
+            Xs = store.X[lid]
+            ys = store.y[lid]
+            params, loss_sum, correct = self._body(Xs, ys, theta_g.to(self.device), h2d(plan.idx, self.device),
+                                                   h2d(plan.wts, self.device), h2d(plan.active, self.device),
                                                    plan.max_steps, round_num, method)
         return {"params": params, "loss_sum": loss_sum, "correct": correct, **common}
 
@@ -199,9 +201,9 @@ class VQCClientTrainer:
                     ent["out"] = self._body(*args)
             ent["graph"] = g
             cache[key] = ent
-        ent["theta"].copy_(theta_g.float(), non_blocking=True)
-        ent["idx"].copy_(plan.idx, non_blocking=True)
-        ent["wts"].copy_(plan.wts, non_blocking=True)
-        ent["act"].copy_(plan.active, non_blocking=True)
+        ent["theta"].copy_(theta_g.float())
+        ent["idx"].copy_(h2d(plan.idx, self.device))
+        ent["wts"].copy_(h2d(plan.wts, self.device))
+        ent["act"].copy_(h2d(plan.active, self.device))
         ent["graph"].replay()
         return ent["out"]

@@ -3,6 +3,7 @@ from __future__ import annotations
 
 import torch
 
+from ..utils.device import h2d
 from ..utils.seeding import philox_key
 from ._ext import ext
 
@@ -24,7 +25,8 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
     K, P = theta_k.shape
     dev = theta_k.device
     keys = torch.tensor([w for c in client_ids for w in philox_key(seed, "dp_noise", round_num, int(c))],
-                        dtype=torch.int64).to(torch.int32).to(dev)
+                        dtype=torch.int64).to(torch.int32)
+    keys = h2d(keys, dev)
     norms = torch.empty(K, dtype=torch.float64, device=dev)
     out = torch.empty(P + 1, dtype=torch.int64, device=dev)
     ext().fedavg(theta_k.float().contiguous(), theta_g.float().contiguous(),

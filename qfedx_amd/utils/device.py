@@ -32,3 +32,16 @@ def resolve_backend(spec: str, device: torch.device) -> str:
     if spec == "hip" and device.type != "cuda":
         raise RuntimeError("backend=hip requires a GPU device")
     return spec
+
+
+def h2d(t: torch.Tensor, device) -> torch.Tensor:
+    """Host -> device copy that never stalls the host on the GPU queue.
+
+    A pageable-memory copy blocks until the stream reaches it (i.e. a hidden device sync).  Staging
+    through pinned memory makes it a true async DMA; torch's caching host allocator keeps the pinned
+    block alive until the copy has completed, so the staging buffer is never overwritten early.
+    """
+    device = torch.device(device)
+    if device.type != "cuda" or t.device.type == "cuda":
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)

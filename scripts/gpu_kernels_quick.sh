@@ -1,0 +1,13 @@
+#!/bin/bash
+# kernel numerics tests + per-pass timings + bench (no profiler)
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests/test_gpu_kernels.py -x -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/gpu_tests.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python scripts/kbench.py > gpurun_out/kbench.log 2>&1
+rc=$?; echo "kbench rc=$rc"; tail -3 gpurun_out/kbench.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python bench.py --steps 20 --warmup 3 "$@" > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; grep metric gpurun_out/bench.log
+exit $rc
