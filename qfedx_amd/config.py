@@ -102,7 +102,7 @@ class RuntimeConfig:
     metrics_path: str = ""
     log_every: int = 5
     overlap_comm: bool = True
-    use_graphs: bool = False
+    use_graphs: bool = True            # hipGraph capture of the local round (HIP backend)
 
 
 @dataclass

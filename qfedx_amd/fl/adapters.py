@@ -22,6 +22,7 @@ class VQCAdapter:
         self.device = torch.device(device)
         self.engine = VQCEngine(self.spec, device, backend, m.state_dtype)
         self.trainer = VQCClientTrainer(self.spec, self.engine, cfg.train, device, backend)
+        self.trainer.graphs = bool(getattr(cfg.runtime, "use_graphs", True))
         self.n_params = self.spec.n_params
         self.eval_batch = 4096
 
@@ -52,6 +53,16 @@ class VQCAdapter:
             loss_sum += float(loss.sum())
             correct += float(corr.sum())
         return loss_sum, correct, float(X.shape[0])
+
+
+    @torch.no_grad()
+    def logits(self, params: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+        """Test-set logits [N, C] (AUC / calibration metrics)."""
+        out = []
+        for s in range(0, X.shape[0], self.eval_batch):
+            xb = self.spec.encode_features(X[s: s + self.eval_batch][None])
+            out.append(self.engine.predict(xb, params[None, :])[0])
+        return torch.cat(out) if out else torch.zeros(0, self.spec.n_classes, device=X.device)
 
 
 def make_adapter(cfg, device, backend: str):

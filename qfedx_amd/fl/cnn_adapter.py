@@ -96,6 +96,12 @@ class TinyCNNAdapter:
         return tc.state_dict_to_flat(sd, self.C)
 
     @torch.no_grad()
+    def logits(self, params: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+        out = [tc.batched_forward(params[None].float(), X[s: s + self.eval_batch].reshape(1, -1, 1, 28, 28).float(),
+                                  self.C)[0] for s in range(0, X.shape[0], self.eval_batch)]
+        return torch.cat(out) if out else torch.zeros(0, self.C, device=X.device)
+
+    @torch.no_grad()
     def evaluate(self, params: torch.Tensor, X: torch.Tensor, y: torch.Tensor):
         if X.shape[0] == 0:
             return 0.0, 0.0, 0.0

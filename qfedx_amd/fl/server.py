@@ -22,7 +22,7 @@ from typing import Optional
 
 import torch
 
-from ..parallel.dist import World, all_reduce_, barrier, broadcast_, shard_clients
+from ..parallel.dist import World, all_gather_cat, all_reduce_, barrier, broadcast_, shard_clients
 from ..privacy.accountant import RDPAccountant
 from ..privacy.secure_agg import SecureAggregator
 from ..utils.device import h2d
@@ -96,6 +96,26 @@ class FederatedRunner:
         all_reduce_(buf, self.world)
         n_tot = max(float(buf[2]), 1.0)
         return {"test_acc": float(buf[1]) / n_tot, "test_loss": float(buf[0]) / n_tot}
+
+    @torch.no_grad()
+    def test_auc(self, params: Optional[torch.Tensor] = None) -> float:
+        """Macro one-vs-rest ROC AUC on the full (rank-sharded, gathered) test set (ROADMAP:112)."""
+        if not hasattr(self.adapter, "logits"):
+            return float("nan")
+        params = self.params if params is None else params
+        lg = self.adapter.logits(params, self.X_test).float()
+        C = self.cfg.model.n_classes
+        probs = all_gather_cat(torch.softmax(lg, -1).reshape(-1), self.world).reshape(-1, C).cpu().numpy()
+        ys = all_gather_cat(self.y_test.to(lg.device).double(), self.world).cpu().numpy().astype(int)
+        try:
+            from sklearn.metrics import roc_auc_score
+            if C == 2:
+                return float(roc_auc_score(ys, probs[:, 1]))
+            if len(set(ys.tolist())) < C:
+                return float("nan")
+            return float(roc_auc_score(ys, probs, multi_class="ovr", average="macro"))
+        except Exception:
+            return float("nan")
 
     # ------------------------------------------------------------------ checkpoint
     def save(self, round_num: int) -> None:
@@ -222,7 +242,11 @@ class FederatedRunner:
             if ck and (r + 1) % ck == 0:
                 self.save(r + 1)
         wall = time.perf_counter() - t_start
+        auc = self.test_auc()
+        if self.world.is_main:
+            self.metrics.log({"final": True, "test_auc": auc, "wall_s": wall})
         self.metrics.close()
         return {"model": self.adapter.state_dict(self.params), "params": self.params, "accuracies": accs,
+                "auc": auc,
                 "history": self.history, "wall_s": wall, "phases_ms": self.timer.resolve(),
                 "epsilon": self.accountant.get_epsilon(self.cfg.privacy.delta) if self.cfg.privacy.dp else None}

@@ -135,4 +135,6 @@ def test_metrics_jsonl(tmp_path):
     path = str(tmp_path / "m.jsonl")
     run_experiment(small_cfg(num_rounds=2, metrics_path=path))
     recs = read_jsonl(path)
-    assert recs[0]["event"] == "config" and recs[-1]["round"] == 2 and "test_acc" in recs[-1]
+    rounds = [r for r in recs if "round" in r]
+    assert recs[0]["event"] == "config" and rounds[-1]["round"] == 2 and "test_acc" in rounds[-1]
+    assert recs[-1].get("final") and 0.0 <= recs[-1]["test_auc"] <= 1.0
