@@ -49,7 +49,11 @@ int qfx_launch_pass(int R, int adjoint, const int* blob, int pass_off, int k, in
                     hipStream_t stream);
 int qfx_launch_readout_ce(const float* part, int tps, int C, int spc, int K, const long long* y, const float* wts,
                           const float* params, int p_stride, int n_theta, float* expz, float* w_out, float* loss,
-                          float* correct, float* grad, int write_grad, hipStream_t st);
+                          float* correct, float* grad, int write_grad, float p01, float p10, int shots,
+                          const long long* keys, unsigned stream, hipStream_t st);
+int qfx_launch_readout_noise(float* expz, int C, int spc, long n_samples, float p01, float p10, int shots,
+                             const long long* keys, unsigned stream, hipStream_t st);
+int qfx_launch_philox_uniform(const long long* keys, int K, long n, unsigned stream, float* out, hipStream_t st);
 int qfx_launch_readout_sum(const float* part, int tps, int C, long n_samples, float* expz, hipStream_t st);
 int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob, float* grad,
                            int p_stride, hipStream_t st);
@@ -122,7 +126,8 @@ void pass_launch(int64_t R, bool adjoint, torch::Tensor blob, int64_t pass_off, 
 
 void readout_ce(torch::Tensor part, int64_t tps, int64_t C, int64_t spc, int64_t K, torch::Tensor y,
                 torch::Tensor wts, torch::Tensor params, int64_t n_theta, torch::Tensor expz, torch::Tensor w_out,
-                torch::Tensor loss, torch::Tensor correct, torch::Tensor grad, bool write_grad) {
+                torch::Tensor loss, torch::Tensor correct, torch::Tensor grad, bool write_grad, double p01,
+                double p10, int64_t shots, torch::Tensor keys, int64_t stream) {
   need(part, torch::kFloat32, "part");
   need(y, torch::kInt64, "y");
   need(wts, torch::kFloat32, "wts");
@@ -131,8 +136,28 @@ void readout_ce(torch::Tensor part, int64_t tps, int64_t C, int64_t spc, int64_t
   check(qfx_launch_readout_ce(ptr<float>(part), (int)tps, (int)C, (int)spc, (int)K, ptr<long long>(y),
                               ptr<float>(wts), ptr<float>(params), (int)params.size(1), (int)n_theta,
                               ptr<float>(expz), ptr<float>(w_out), ptr<float>(loss), ptr<float>(correct),
-                              ptr<float>(grad), write_grad ? 1 : 0, cur_stream()),
+                              ptr<float>(grad), write_grad ? 1 : 0, (float)p01, (float)p10, (int)shots,
+                              keys.numel() ? ptr<long long>(keys) : nullptr, (unsigned)stream, cur_stream()),
         "qfx_readout_ce");
+}
+
+void readout_noise(torch::Tensor expz, int64_t C, int64_t spc, int64_t n_samples, double p01, double p10,
+                   int64_t shots, torch::Tensor keys, int64_t stream) {
+  need(expz, torch::kFloat32, "expz");
+  if (shots > 0) need(keys, torch::kInt64, "keys");
+  check(qfx_launch_readout_noise(ptr<float>(expz), (int)C, (int)spc, (long)n_samples, (float)p01, (float)p10,
+                                 (int)shots, keys.numel() ? ptr<long long>(keys) : nullptr, (unsigned)stream,
+                                 cur_stream()),
+        "qfx_readout_noise");
+}
+
+void philox_uniform(torch::Tensor keys, int64_t n, int64_t stream, torch::Tensor out) {
+  need(keys, torch::kInt64, "keys");
+  need(out, torch::kFloat32, "out");
+  if (out.numel() < keys.size(0) * n) throw std::invalid_argument("philox_uniform: out too small");
+  check(qfx_launch_philox_uniform(ptr<long long>(keys), (int)keys.size(0), (long)n, (unsigned)stream,
+                                  ptr<float>(out), cur_stream()),
+        "qfx_philox_uniform");
 }
 
 void readout_sum(torch::Tensor part, int64_t tps, int64_t C, int64_t n_samples, torch::Tensor expz) {
@@ -231,6 +256,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pass_launch", &pass_launch);
   m.def("readout_ce", &readout_ce);
   m.def("readout_sum", &readout_sum);
+  m.def("readout_noise", &readout_noise);
+  m.def("philox_uniform", &philox_uniform);
   m.def("grad_reduce", &grad_reduce);
   m.def("adam", &adam);
   m.def("sgdm", &sgdm);

@@ -35,7 +35,7 @@ static inline bool is_diag(int k) {
   return k == K_RZ || k == K_P || k == K_Z || k == K_S || k == K_SDG || k == K_T || k == K_TDG ||
          k == K_CZ;
 }
-static inline bool is_1q(int k) { return k <= K_SX; }
+static inline bool is_1q(int k) { return k <= K_SX || k == K_PAULI; }
 
 static int f2i(float f) {
   int i;

@@ -58,6 +58,7 @@ __device__ __forceinline__ float gate_angle(cint_p gt, int gi, const float* prow
 __device__ __forceinline__ v2f gate_cs(cint_p gt, int gi, const float* prow,
                                           const float* xrow, int n_theta) {
   const float ang = gate_angle(gt, gi, prow, xrow, n_theta);
+  if (gt[gi * GATE_WORDS] == K_PAULI) return mk(ang, 0.f);   // Pauli index, no trig
   const float x = gt[gi * GATE_WORDS] == K_P ? ang : 0.5f * ang;
   float s, c;
   sincosf(x, &s, &c);
@@ -84,6 +85,13 @@ __device__ __forceinline__ M2 gate_m2(int kind, v2f cs, bool inv) {
     case K_T: m = {one, z, z, mk(t, t)}; break;
     case K_TDG: m = {one, z, z, mk(t, -t)}; break;
     case K_SX: m = {mk(.5f, .5f), mk(.5f, -.5f), mk(.5f, -.5f), mk(.5f, .5f)}; break;
+    case K_PAULI: {   // trajectory Pauli: 0 I, 1 X, 2 Y, 3 Z (Hermitian: its own inverse)
+      const int pc = (int)(c + 0.5f);
+      if (pc == 1) m = {z, one, one, z};
+      else if (pc == 2) m = {z, mk(0.f, -1.f), mk(0.f, 1.f), z};
+      else if (pc == 3) m = {one, z, z, mk(-1.f, 0.f)};
+      else m = {one, z, z, one};
+    } break;
     default: m = {one, z, z, one}; break;
   }
   if (inv) m = {conjf2(m.a), conjf2(m.c), conjf2(m.b), conjf2(m.d)};

@@ -16,7 +16,9 @@ namespace qfx {
 // gate kinds (quantum/circuit.py KIND)
 enum Kind : int {
   K_RX = 0, K_RY = 1, K_RZ = 2, K_P = 3, K_H = 4, K_X = 5, K_Y = 6, K_Z = 7, K_S = 8, K_SDG = 9,
-  K_T = 10, K_TDG = 11, K_SX = 12, K_CX = 13, K_CZ = 14, K_SWAP = 15
+  K_T = 10, K_TDG = 11, K_SX = 12, K_CX = 13, K_CZ = 14, K_SWAP = 15,
+  // stochastic Pauli (noise trajectories): the slot value selects I/X/Y/Z (0..3) per sample
+  K_PAULI = 18
 };
 
 // micro-op codes (planner-internal U1/D1 are lowered to G1 groups / D1T before serialisation)

@@ -19,6 +19,14 @@ namespace qfx {
 
 constexpr int CMAX = 8;
 
+// readout noise model (K19): confusion probabilities + shot count + per-client Philox keys
+struct ReadoutNoise {
+  float p01, p10;            // P(read 1 | 0), P(read 0 | 1)
+  int shots;                 // 0 = exact expectation
+  const long long* keys;     // [K, 2] per-client Philox key words (shots > 0)
+  unsigned stream;           // Philox stream (local step)
+};
+
 // deterministic block reduction of NV values per thread (blockDim = 256)
 template <int NV>
 __device__ __forceinline__ void block_sum(float (&v)[NV], float* sm) {
@@ -44,9 +52,12 @@ __global__ void __launch_bounds__(256) qfx_readout_ce_kernel(
     const float* __restrict__ part, int tps, int C, int spc, const long long* __restrict__ y,
     const float* __restrict__ wts, const float* __restrict__ params, int p_stride, int n_theta,
     float* __restrict__ expz, float* __restrict__ w_out, float* __restrict__ loss,
-    float* __restrict__ correct, float* __restrict__ grad, int write_grad) {
+    float* __restrict__ correct, float* __restrict__ grad, int write_grad, ReadoutNoise nz) {
   __shared__ float sm[(2 * CMAX + 2) * 4];
   const int k = blockIdx.x;
+  const bool noisy = nz.p01 != 0.f || nz.p10 != 0.f || nz.shots > 0;
+  const uint32_t k0 = nz.keys ? (uint32_t)nz.keys[2 * k] : 0u, k1 = nz.keys ? (uint32_t)nz.keys[2 * k + 1] : 0u;
+  const float gscale = 1.f - nz.p01 - nz.p10;   // straight-through d<Z>_noisy / d<Z>
   const float* a = params + (size_t)k * p_stride + n_theta;
   const float* b = a + C;
   float acc[2 * CMAX + 2];
@@ -61,6 +72,7 @@ __global__ void __launch_bounds__(256) qfx_readout_ce_kernel(
       if (c >= C) break;
       float t = 0.f;
       for (int u = 0; u < tps; ++u) t += part[((size_t)s * tps + u) * C + c];
+      if (noisy) t = noisy_z(t, nz.p01, nz.p10, nz.shots, k0, k1, nz.stream, ((uint64_t)j * C + c) * (uint64_t)nz.shots);
       z[c] = t;
       lg[c] = fmaf(a[c], t, b[c]);
       m = fmaxf(m, lg[c]);
@@ -84,7 +96,7 @@ __global__ void __launch_bounds__(256) qfx_readout_ce_kernel(
       const float p = expf(lg[c] - lse);
       const float dl = (p - (c == yy ? 1.f : 0.f)) * ws;
       expz[(size_t)s * C + c] = z[c];
-      w_out[(size_t)s * C + c] = dl * a[c];
+      w_out[(size_t)s * C + c] = dl * a[c] * gscale;
       acc[c] += dl * z[c];
       acc[CMAX + c] += dl;
     }
@@ -103,6 +115,26 @@ __global__ void __launch_bounds__(256) qfx_readout_ce_kernel(
       }
     }
   }
+}
+
+// readout noise on exact expectations expz [K * spc, C] in place (evaluation path)
+__global__ void qfx_readout_noise_kernel(float* __restrict__ expz, int C, int spc, long n_samples, ReadoutNoise nz) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_samples * C) return;
+  const long s = i / C;
+  const int c = (int)(i % C);
+  const long k = s / spc, j = s - k * spc;
+  const uint32_t k0 = nz.keys ? (uint32_t)nz.keys[2 * k] : 0u, k1 = nz.keys ? (uint32_t)nz.keys[2 * k + 1] : 0u;
+  expz[i] = noisy_z(expz[i], nz.p01, nz.p10, nz.shots, k0, k1, nz.stream, ((uint64_t)j * C + c) * (uint64_t)nz.shots);
+}
+
+// Philox uniforms (0,1]: out[k][e] for e < n from key keys[k] and the given stream (noise trajectories)
+__global__ void qfx_philox_uniform_kernel(const long long* __restrict__ keys, long n, unsigned stream,
+                                          float* __restrict__ out) {
+  const int k = blockIdx.y;
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  out[(size_t)k * n + e] = philox_uniform_at((uint64_t)e, (uint32_t)keys[2 * k], (uint32_t)keys[2 * k + 1], stream);
 }
 
 // sum of tile partials only (evaluation): expz[s][c]
@@ -250,10 +282,30 @@ using namespace qfx;
 extern "C" int qfx_launch_readout_ce(const float* part, int tps, int C, int spc, int K, const long long* y,
                                      const float* wts, const float* params, int p_stride, int n_theta,
                                      float* expz, float* w_out, float* loss, float* correct, float* grad,
-                                     int write_grad, hipStream_t st) {
+                                     int write_grad, float p01, float p10, int shots, const long long* keys,
+                                     unsigned stream, hipStream_t st) {
   if (C > CMAX) return -2;
+  ReadoutNoise nz{p01, p10, shots, keys, stream};
   hipLaunchKernelGGL(qfx_readout_ce_kernel, dim3(K), dim3(256), 0, st, part, tps, C, spc, y, wts, params,
-                     p_stride, n_theta, expz, w_out, loss, correct, grad, write_grad);
+                     p_stride, n_theta, expz, w_out, loss, correct, grad, write_grad, nz);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_launch_readout_noise(float* expz, int C, int spc, long n_samples, float p01, float p10,
+                                        int shots, const long long* keys, unsigned stream, hipStream_t st) {
+  const long tot = n_samples * C;
+  if (tot <= 0) return 0;
+  ReadoutNoise nz{p01, p10, shots, keys, stream};
+  hipLaunchKernelGGL(qfx_readout_noise_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, expz, C, spc,
+                     n_samples, nz);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_launch_philox_uniform(const long long* keys, int K, long n, unsigned stream, float* out,
+                                         hipStream_t st) {
+  if (K <= 0 || n <= 0) return 0;
+  hipLaunchKernelGGL(qfx_philox_uniform_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)K), dim3(256), 0, st,
+                     keys, n, stream, out);
   return (int)hipGetLastError();
 }
 

@@ -10,17 +10,20 @@ from __future__ import annotations
 import torch
 
 from ..models.vqc import VQCSpec
-from ..ops.engine import VQCEngine, ce_readout
+from ..quantum.noise import NoiseModel
+from ..ops.engine import VQCEngine
 from .trainer import VQCClientTrainer
 
 
 class VQCAdapter:
     def __init__(self, cfg, device, backend: str):
         m = cfg.model
+        self.noise = NoiseModel.from_config(getattr(cfg, "noise", None), cfg.train.seed)
         self.spec = VQCSpec(m.n_qubits, m.n_layers, m.n_classes, m.feature_map, m.feature_scale,
-                            m.alpha, m.entangler, None, m.readout_scale, m.init_std)
+                            m.alpha, m.entangler, None, m.readout_scale, m.init_std,
+                            noisy=self.noise is not None and self.noise.gate_noise)
         self.device = torch.device(device)
-        self.engine = VQCEngine(self.spec, device, backend, m.state_dtype)
+        self.engine = VQCEngine(self.spec, device, backend, m.state_dtype, noise=self.noise)
         self.trainer = VQCClientTrainer(self.spec, self.engine, cfg.train, device, backend)
         self.trainer.graphs = bool(getattr(cfg.runtime, "use_graphs", True))
         self.n_params = self.spec.n_params
@@ -38,30 +41,32 @@ class VQCAdapter:
     def from_state_dict(self, sd: dict) -> torch.Tensor:
         return self.spec.from_state_dict(sd)
 
+    def _eval_logits(self, params: torch.Tensor, X: torch.Tensor, chunk: int) -> torch.Tensor:
+        xang = self.spec.encode_features(X[None])
+        ro_keys = None
+        if self.noise is not None:     # noisy device: one keyed trajectory per test sample, noisy readout
+            xang = self.engine.augment(xang, self.noise.client_keys("noise_eval", chunk, [0], X.device), 0)
+            ro_keys = self.noise.client_keys("shots_eval", chunk, [0], X.device)
+        return self.engine.predict(xang, params[None, :], ro_keys, 0)[0]
+
     @torch.no_grad()
     def evaluate(self, params: torch.Tensor, X: torch.Tensor, y: torch.Tensor):
         if X.shape[0] == 0:
             return 0.0, 0.0, 0.0
-        th, a, b = self.spec.split(params[None, :])
-        loss_sum = 0.0
-        correct = 0.0
-        for s in range(0, X.shape[0], self.eval_batch):
-            xb = X[s: s + self.eval_batch][None]
-            yb = y[s: s + self.eval_batch][None]
-            z = self.engine.expz(self.spec.encode_features(xb), th)
-            loss, _, _, _, corr = ce_readout(z, yb, torch.ones_like(yb, dtype=z.dtype), a, b)
-            loss_sum += float(loss.sum())
-            correct += float(corr.sum())
-        return loss_sum, correct, float(X.shape[0])
-
+        loss_sum = torch.zeros((), dtype=torch.float64, device=X.device)
+        correct = torch.zeros((), dtype=torch.float64, device=X.device)
+        for i, s in enumerate(range(0, X.shape[0], self.eval_batch)):
+            lg = self._eval_logits(params, X[s: s + self.eval_batch], i)
+            yb = y[s: s + self.eval_batch]
+            loss_sum += torch.nn.functional.cross_entropy(lg.float(), yb, reduction="sum").double()
+            correct += (lg.argmax(-1) == yb).sum().double()
+        return float(loss_sum), float(correct), float(X.shape[0])
 
     @torch.no_grad()
     def logits(self, params: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
         """Test-set logits [N, C] (AUC / calibration metrics)."""
-        out = []
-        for s in range(0, X.shape[0], self.eval_batch):
-            xb = self.spec.encode_features(X[s: s + self.eval_batch][None])
-            out.append(self.engine.predict(xb, params[None, :])[0])
+        out = [self._eval_logits(params, X[s: s + self.eval_batch], i)
+               for i, s in enumerate(range(0, X.shape[0], self.eval_batch))]
         return torch.cat(out) if out else torch.zeros(0, self.spec.n_classes, device=X.device)
 
 

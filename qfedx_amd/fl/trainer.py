@@ -111,9 +111,15 @@ class VQCClientTrainer:
     def encode(self, X: torch.Tensor) -> torch.Tensor:
         return self.spec.encode_features(X)
 
-    def _body(self, Xs, ys, theta, idx_d, wts_d, act_d, steps: int, round_num: int, method: str):
-        """Device work of one round (capturable): local steps of all clients + metrics."""
+    def _body(self, Xs, ys, theta, idx_d, wts_d, act_d, steps: int, round_num: int, method: str,
+              traj_keys=None, ro_keys=None):
+        """Device work of one round (capturable): local steps of all clients + metrics.
+
+        With a noise model, every sample runs ``trajectories`` Pauli-trajectory replicas (loss weights
+        split evenly) and the readout is confused / shot-sampled, all keyed per client and step."""
         cfg = self.cfg
+        noise = self.engine.noise
+        T = noise.trajectories if (noise is not None and noise.gate_noise) else 1
         K = Xs.shape[0]
         P = theta.numel()
         params = theta.float()[None, :].repeat(K, 1).contiguous()
@@ -125,11 +131,15 @@ class VQCClientTrainer:
         kar = torch.arange(K, device=self.device)[:, None]
         for s in range(steps):
             bi = idx_d[s]
+            ws = wts_d[s]
+            if T > 1:
+                bi = bi.repeat(1, T)
+                ws = ws.repeat(1, T) / T
             xb = Xs[kar, bi]                     # [K, B, F]
             yb = ys[kar, bi]
-            xang = self.encode(xb)
-            res = self.engine.loss_and_grads(xang, yb, wts_d[s], params, method,
-                                             rng_keys=(cfg.seed, round_num, s))
+            xang = self.engine.augment(self.encode(xb), traj_keys, s)
+            res = self.engine.loss_and_grads(xang, yb, ws, params, method, rng_keys=(cfg.seed, round_num, s),
+                                             readout_keys=ro_keys, step=s)
             opt.step(params, res["grad"], act_d[s])
             nvalid = (wts_d[s] > 0).sum(-1).double() * act_d[s].double()
             loss_sum += (res["loss"].double() * nvalid).sum()
@@ -152,7 +162,12 @@ class VQCClientTrainer:
         samples = float((plan.wts > 0).sum())
         common = {"samples": samples, "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
                   "n_samples": store.counts[li].to(torch.float64)}
-        if self.use_graph and method == "adjoint":
+        noise = self.engine.noise
+        traj_keys = ro_keys = None
+        if noise is not None:
+            traj_keys = noise.client_keys("noise_traj", round_num, cids, self.device)
+            ro_keys = noise.client_keys("shots", round_num, cids, self.device)
+        if self.use_graph and method == "adjoint" and noise is None:
             params, loss_sum, correct = self._graphed(store, local_idx, li, theta_g, plan, round_num)
         else:
             lid = h2d(li, store.X.device)
@@ -160,7 +175,7 @@ class VQCClientTrainer:
             ys = store.y[lid]
             params, loss_sum, correct = self._body(Xs, ys, theta_g.to(self.device), h2d(plan.idx, self.device),
                                                    h2d(plan.wts, self.device), h2d(plan.active, self.device),
-                                                   plan.max_steps, round_num, method)
+                                                   plan.max_steps, round_num, method, traj_keys, ro_keys)
         return {"params": params, "loss_sum": loss_sum, "correct": correct, **common}
 
     # ------------------------------------------------------------------ hipGraph capture

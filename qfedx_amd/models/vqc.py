@@ -37,6 +37,7 @@ class VQCSpec:
     readout: Optional[list] = None    # readout qubits, default first n_classes
     readout_scale: float = 1.0
     init_std: float = 0.1
+    noisy: bool = False               # insert noise-trajectory Pauli ops after every gate (NoiseConfig)
 
     def __post_init__(self):
         if self.readout is None:
@@ -58,30 +59,59 @@ class VQCSpec:
     def n_features(self) -> int:
         return self.n_qubits
 
+    @property
+    def n_noise_ops(self) -> int:
+        """Pauli trajectory ops: one per qubit touched by each gate (feature map, rotations, CNOTs)."""
+        if not self.noisy:
+            return 0
+        n = self.n_qubits
+        ent = (n - 1) + (1 if self.entangler == "ring" and n > 2 else 0) if self.entangler in ("chain", "ring") else 0
+        return n + self.n_layers * (2 * n + 2 * ent)
+
+    @property
+    def x_width(self) -> int:
+        """Per-sample x-slot row: encoded features, then the Pauli selectors of the trajectory."""
+        return self.n_features + self.n_noise_ops
+
     def circuit(self) -> Circuit:
         n = self.n_qubits
         x = ParameterVector("x", n)
         th = ParameterVector("theta", self.n_theta)
+        nz = ParameterVector("noise", max(self.n_noise_ops, 1))
         qc = Circuit(n, name=f"VQC_{n}q_{self.n_layers}L")
+        j = [0]
+
+        def noise(*qs):
+            if self.noisy:
+                for q in qs:
+                    qc.pauli(nz[j[0]], q)
+                    j[0] += 1
+
         fm = self.feature_map.lower()
         for q in range(n):
             getattr(qc, fm if fm in ("rx", "ry", "rz") else "ry")(x[q], q)
+            noise(q)
         k = 0
         for _ in range(self.n_layers):
             for q in range(n):
                 qc.rx(th[k], q)
+                noise(q)
                 qc.rz(th[k + 1], q)
+                noise(q)
                 k += 2
             if self.entangler in ("chain", "ring"):
                 for q in range(n - 1):
                     qc.cx(q, q + 1)
+                    noise(q, q + 1)
                 if self.entangler == "ring" and n > 2:
                     qc.cx(n - 1, 0)
+                    noise(n - 1, 0)
+        assert j[0] == self.n_noise_ops
         return qc
 
     def program(self):
-        """(ops, coef) with slots [theta (n_theta) | x (n)]."""
-        return self.circuit().to_program({"theta": 0, "x": self.n_theta})
+        """(ops, coef) with slots [theta (n_theta) | x (n) | noise selectors (n_noise_ops)]."""
+        return self.circuit().to_program({"theta": 0, "x": self.n_theta, "noise": self.n_theta + self.n_features})
 
     def encode_features(self, x: torch.Tensor) -> torch.Tensor:
         """Raw features [.., n] -> encoding angles fed to the x slots (gate scale is 1)."""

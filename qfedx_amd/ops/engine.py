@@ -45,14 +45,16 @@ def ce_readout(expz: torch.Tensor, y: torch.Tensor, wmask: torch.Tensor, a: torc
 
 
 class VQCEngine:
-    def __init__(self, spec: VQCSpec, device="cpu", backend: str = "torch", state_dtype: str = "fp32"):
+    def __init__(self, spec: VQCSpec, device="cpu", backend: str = "torch", state_dtype: str = "fp32",
+                 noise=None):
         self.spec = spec
+        self.noise = noise          # quantum.noise.NoiseModel or None
         self.device = torch.device(device)
         self.backend = backend
         ops, coef = spec.program()
         self.ops = torch.from_numpy(ops)
         self.coef = torch.from_numpy(coef)
-        self.n_slots = spec.n_theta + spec.n_qubits
+        self.n_slots = spec.n_theta + spec.x_width
         self.state_dtype = state_dtype
         if backend == "torch":
             self.prog = TorchProgram(ops, coef, spec.n_qubits, self.device)
@@ -60,7 +62,7 @@ class VQCEngine:
         elif backend == "hip":
             from .statevec_hip import HipProgram
             self.hip = HipProgram(ops, coef, spec.n_qubits, spec.readout, self.device,
-                                  n_theta=spec.n_theta, state_dtype=state_dtype)
+                                  n_theta=spec.n_theta, state_dtype=state_dtype, x_width=spec.x_width)
             self.prog = TorchProgram(ops, coef, spec.n_qubits, self.device)  # for param-shift/autograd
         else:
             raise ValueError(f"unknown backend '{backend}'")
@@ -69,9 +71,23 @@ class VQCEngine:
     def _check(self, xang: torch.Tensor) -> None:
         # the angle feature map reads one feature per qubit: a narrower input would make the
         # kernels read past each sample's row
-        if xang.shape[-1] != self.spec.n_qubits:
-            raise ValueError(f"VQC needs {self.spec.n_qubits} features per sample (one per qubit), "
+        if xang.shape[-1] != self.spec.x_width:
+            raise ValueError(f"VQC needs {self.spec.n_qubits} features per sample (one per qubit)"
+                             f"{' + %d noise selectors' % self.spec.n_noise_ops if self.spec.noisy else ''}, "
                              f"got {xang.shape[-1]}; set data.n_features = model.n_qubits")
+
+    def augment(self, xang: torch.Tensor, keys: Optional[torch.Tensor], step: int) -> torch.Tensor:
+        """Append this step's noise-trajectory Pauli selectors to the encoded features [K, B, n]."""
+        if not self.spec.noisy:
+            return xang
+        K, B, _ = xang.shape
+        sel = self.noise.pauli_columns(keys, B, self.spec.n_noise_ops, step).to(xang)
+        return torch.cat([xang, sel], -1)
+
+    def _readout(self, expz, keys, step):
+        if self.noise is None or not self.noise.readout_noise:
+            return expz
+        return self.noise.apply_readout(expz, keys, step)
 
     def _rows(self, xang: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
         K, B, n = xang.shape
@@ -80,44 +96,60 @@ class VQCEngine:
 
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
-    def expz(self, xang: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
-        """<Z_c> for [K,B,n] encoded features and per-client theta [K,P] -> [K,B,C]."""
+    def expz(self, xang: torch.Tensor, theta: torch.Tensor, readout_keys: Optional[torch.Tensor] = None,
+             step: int = 0) -> torch.Tensor:
+        """<Z_c> for [K,B,x_width] encoded features and per-client theta [K,P] -> [K,B,C] (with the
+        readout noise model applied when one is configured)."""
         K, B, _ = xang.shape
         self._check(xang)
         if self.backend == "hip":
-            return self.hip.expz(xang, theta)
+            nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
+            return self.hip.expz(xang, theta, nz, readout_keys, step)
         psi = self.prog.run(self._rows(xang, theta))
-        return self.prog.expz(psi, self.spec.readout).reshape(K, B, -1).float()
+        z = self.prog.expz(psi, self.spec.readout).reshape(K, B, -1).float()
+        return self._readout(z, readout_keys, step)
 
     @torch.no_grad()
-    def predict(self, xang: torch.Tensor, params: torch.Tensor) -> torch.Tensor:
+    def predict(self, xang: torch.Tensor, params: torch.Tensor, readout_keys=None, step: int = 0) -> torch.Tensor:
         th, a, b = self.spec.split(params)
-        return logits_from_expz(self.expz(xang, th), a, b)
+        return logits_from_expz(self.expz(xang, th, readout_keys, step), a, b)
 
     # ------------------------------------------------------------------ training
     def loss_and_grads(self, xang: torch.Tensor, y: torch.Tensor, wmask: torch.Tensor,
                        params: torch.Tensor, method: str = "adjoint", spsa_c: float = 0.1,
-                       rng_keys: tuple = (0,)) -> dict:
+                       rng_keys: tuple = (0,), readout_keys: Optional[torch.Tensor] = None,
+                       step: int = 0) -> dict:
         spec = self.spec
         self._check(xang)
         th, a, b = spec.split(params)
         if method == "autograd":
             return self._autograd(xang, y, wmask, params)
         if self.backend == "hip" and method == "adjoint":
-            return self.hip.loss_and_grads(xang, y, wmask, params, spec)
+            nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
+            return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step)
         K, B, _ = xang.shape
         P = spec.n_theta
         with torch.no_grad():
-            rows = self._rows(xang, th)
-            psi = self.prog.run(rows)
-            expz = self.prog.expz(psi, spec.readout).reshape(K, B, -1).float()
+            rows = psi = None
+            if method == "adjoint":          # torch backend: keep psi for the reverse sweep
+                rows = self._rows(xang, th)
+                psi = self.prog.run(rows)
+                expz = self._readout(self.prog.expz(psi, spec.readout).reshape(K, B, -1).float(), readout_keys, step)
+            else:                            # HIP or torch forward, readout noise applied
+                expz = self.expz(xang, th, readout_keys, step)
             loss, w, ga, gb, correct = ce_readout(expz, y, wmask, a, b)
             if method == "adjoint":
+                if self.noise is not None:   # straight-through d<Z>_noisy / d<Z> for the exact adjoint
+                    w = w * (1.0 - self.noise.p01 - self.noise.p10)
                 gg = self.prog.adjoint_grads(rows, psi, w.reshape(K * B, -1), spec.readout)
                 gs = slot_grads(gg, self.ops, self.coef, self.n_slots)[:, :P]
                 gth = gs.reshape(K, B, P).sum(1).float()
             elif method == "param_shift":
-                gth = self._param_shift(rows, w, K, B)
+                # shifted expectations carry the readout channel themselves: w = dL/d<Z>_noisy unscaled
+                if self._simple_shift_slots():
+                    gth = self.param_shift_batched(xang, params, w, readout_keys, step)
+                else:
+                    gth = self._param_shift(self._rows(xang, th), w, K, B)
             elif method == "spsa":
                 gth = self._spsa(xang, y, wmask, params, spsa_c, rng_keys)
             else:
@@ -151,6 +183,64 @@ class VQCEngine:
                 gg[:, g] = (dz[i] * wflat).sum(-1)
         gs = slot_grads(gg, self.ops, self.coef, self.n_slots)[:, :P]
         return gs.reshape(K, B, P).sum(1).float()
+
+    # ------------------------------------------------------------------ batched parameter shift
+    def _simple_shift_slots(self) -> bool:
+        """True when every theta slot drives exactly one RX/RY/RZ gate with unit scale, so shifting the
+        slot by +-pi/2 IS the gate's parameter shift (then shifts batch as parameter rows)."""
+        if getattr(self, "_simple", None) is None:
+            P = self.spec.n_theta
+            seen = {}
+            ok = True
+            for (kind, q0, q1, slot), (sc, off) in zip(self.ops.tolist(), self.coef.tolist()):
+                if 0 <= slot < P:
+                    ok &= kind in (0, 1, 2) and abs(sc - 1.0) < 1e-12
+                    seen[slot] = seen.get(slot, 0) + 1
+            self._simple = bool(ok and all(v == 1 for v in seen.values()) and len(seen) == P)
+        return self._simple
+
+    def state_budget_bytes(self) -> int:
+        if getattr(self, "_budget", None) is None:
+            if self.device.type == "cuda":
+                free, _ = torch.cuda.mem_get_info(self.device)
+                self._budget = int(0.4 * free)
+            else:
+                self._budget = 1 << 31
+        return self._budget
+
+    def param_shift_batched(self, xang: torch.Tensor, params: torch.Tensor, w: torch.Tensor,
+                            readout_keys: Optional[torch.Tensor] = None, step: int = 0) -> torch.Tensor:
+        """dL/dtheta by the parameter-shift rule (ROADMAP.md:23,130-135).
+
+        Every (client k, slot j, sign) is one parameter row theta_k +- pi/2 e_j over the client's B
+        samples: the rows are one forward batch (the HIP eval kernels see them as ordinary samples),
+        chunked so that the live statevectors fit ``state_budget_bytes``.  With a readout noise model
+        each shifted evaluation is confused / shot-sampled from its own keyed stream, so the
+        estimator is the finite-shot hardware estimator.  w = dL/d<Z> [K,B,C].  -> [K, n_theta]
+        """
+        K, B, F = xang.shape
+        P = self.spec.n_theta
+        R = 2 * P
+        state_bytes = (1 << self.spec.n_qubits) * 8
+        rows_per_chunk = max(1, min(K * R, self.state_budget_bytes() // max(1, B * state_bytes)))
+        contrib_all = torch.zeros(K * R, dtype=torch.float64, device=params.device)
+        half_pi = math.pi / 2
+        for r0 in range(0, K * R, rows_per_chunk):
+            r = torch.arange(r0, min(K * R, r0 + rows_per_chunk), device=params.device)
+            k, j = r // R, r % R
+            slot, sign = j // 2, 1.0 - 2.0 * (j % 2).to(params.dtype)
+            th = params[k, :P].clone()
+            th[torch.arange(len(r), device=th.device), slot] += sign * half_pi
+            keys = None
+            if readout_keys is not None:
+                # independent stream per shifted evaluation: mix the row index into the client key
+                keys = readout_keys[k].clone()
+                keys[:, 0] = (keys[:, 0] ^ ((j + 1) * 0x9E3779B9)) & 0xFFFFFFFF
+                keys[:, 1] = (keys[:, 1] + (j + 1) * 0x85EBCA6B) & 0xFFFFFFFF
+            z = self.expz(xang[k], th, keys, step).double()                       # [rows, B, C]
+            contrib_all[r] = (z * w[k].double()).sum((1, 2)) * (0.5 * sign.double())   # [rows]
+        # row r = (k, slot, sign): fixed-order pair sum (no atomics -> deterministic)
+        return contrib_all.view(K, P, 2).sum(-1).float()
 
     def _loss_only(self, xang, y, wmask, params):
         th, a, b = self.spec.split(params)

@@ -26,6 +26,7 @@ PF = dict(K=0, TB=1, INIT=2, FINAL=3, NOPS=4, OPS=5, LAYOUT0=6, NGRAD=7, NNONTIL
           GREGF=168, GTHRF=200)
 HF = dict(N=0, NPASS=1, NGATES=2, GATES=3, PREFIX=4, R=5, NREAD=6, NTHETA=7, PASSES=8)
 K_RX, K_RY, K_RZ, K_P, K_H, K_X, K_Y, K_Z, K_S, K_SDG, K_T, K_TDG, K_SX, K_CX, K_CZ = range(15)
+K_PAULI = 18
 DIAG = {K_RZ, K_P, K_Z, K_S, K_SDG, K_T, K_TDG}
 
 
@@ -82,6 +83,9 @@ def parse_blob(blob) -> dict:
 
 
 def _m2(kind: int, ang: float, inv: bool) -> np.ndarray:
+    if kind == K_PAULI:
+        m = [np.eye(2), np.array([[0, 1], [1, 0]]), np.array([[0, -1j], [1j, 0]]), np.diag([1, -1])][int(round(ang))]
+        return np.asarray(m, dtype=complex)
     c, s = math.cos(ang / 2), math.sin(ang / 2)
     t = complex(math.cos(math.pi / 4), math.sin(math.pi / 4))
     table = {

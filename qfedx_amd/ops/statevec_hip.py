@@ -31,6 +31,17 @@ JIT_CACHE = os.environ.get("QFEDX_JIT_CACHE", os.path.join(os.path.dirname(_PKG)
 ARCH = os.environ.get("QFEDX_ARCH", "gfx950")
 
 
+_NO_KEYS = torch.zeros(0, dtype=torch.int64)
+
+
+def _keys(keys, noise) -> torch.Tensor:
+    if noise.shots > 0:
+        if keys is None:
+            raise ValueError("shot sampling needs per-client Philox keys")
+        return keys.contiguous()
+    return _NO_KEYS
+
+
 def choose_R(n: int) -> int:
     return 16 if n >= 4 else 4
 
@@ -64,7 +75,7 @@ class _Plan:
 
 class HipProgram:
     def __init__(self, ops, coef, n_qubits: int, readout, device, n_theta: int, state_dtype: str = "fp32",
-                 kmax: int = KMAX, jit: bool | None = None):
+                 kmax: int = KMAX, jit: bool | None = None, x_width: int | None = None):
         if state_dtype != "fp32":
             raise NotImplementedError("bf16 statevector storage is not implemented yet")
         self.n = n_qubits
@@ -72,6 +83,7 @@ class HipProgram:
         self.C = len(self.readout)
         self.device = torch.device(device)
         self.n_theta = n_theta
+        self.x_width = n_qubits if x_width is None else x_width
         self.R = choose_R(n_qubits)
         self.jit = jit_enabled() if jit is None else jit
         args = (ops, coef, n_qubits, self.R, kmax, self.readout, n_theta)
@@ -114,10 +126,10 @@ class HipProgram:
 
     # ------------------------------------------------------------------ forward / eval
     @torch.no_grad()
-    def expz(self, xang: torch.Tensor, theta: torch.Tensor) -> torch.Tensor:
+    def expz(self, xang: torch.Tensor, theta: torch.Tensor, noise=None, keys=None, step: int = 0) -> torch.Tensor:
         K, B, F = xang.shape
-        if F != self.n:
-            raise ValueError(f"expected {self.n} encoded features per sample, got {F}")
+        if F != self.x_width:
+            raise ValueError(f"expected {self.x_width} x-slot values per sample, got {F}")
         S = K * B
         x = xang.reshape(S, F).float().contiguous()
         th = theta.float().contiguous()
@@ -127,13 +139,16 @@ class HipProgram:
         self._run_passes(plan, False, psi, None, th, B, x, None, part, None, S)
         out = self._buf("expz", S * self.C, torch.float32)
         ext().readout_sum(part, plan.tiles_per_state, self.C, S, out)
+        if noise is not None:
+            ext().readout_noise(out, self.C, B, S, noise.p01, noise.p10, noise.shots, _keys(keys, noise),
+                                int(step))
         return out.reshape(K, B, self.C).clone()
 
     # ------------------------------------------------------------------ train step
-    def loss_and_grads(self, xang, y, wmask, params, spec) -> dict:
+    def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0) -> dict:
         K, B, F = xang.shape
-        if F != self.n:
-            raise ValueError(f"expected {self.n} encoded features per sample, got {F}")
+        if F != self.x_width:
+            raise ValueError(f"expected {self.x_width} x-slot values per sample, got {F}")
         S = K * B
         C = ext()
         x = xang.reshape(S, F).float().contiguous()
@@ -151,8 +166,12 @@ class HipProgram:
         correct = torch.empty(K, dtype=torch.float32, device=self.device)
         grad = torch.zeros_like(p)
         self._run_passes(tr, False, psi, None, p, B, x, None, part, None, S)
-        C.readout_ce(part, tr.tiles_per_state, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
-                     correct, grad, True)
+        if noise is None:
+            C.readout_ce(part, tr.tiles_per_state, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
+                         correct, grad, True, 0.0, 0.0, 0, _NO_KEYS, 0)
+        else:
+            C.readout_ce(part, tr.tiles_per_state, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
+                         correct, grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
         self._run_passes(adj, True, psi, lam, p, B, x, wread, None, slab, S)
         C.grad_reduce(slab, adj.tiles_per_state, B, K, self.G, adj.blob, grad)
         return {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}

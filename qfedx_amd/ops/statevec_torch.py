@@ -25,6 +25,7 @@ from ..quantum.circuit import KIND
 RX, RY, RZ, P = KIND["rx"], KIND["ry"], KIND["rz"], KIND["p"]
 H, X, Y, Z, S, SDG, T, TDG, SX = (KIND[k] for k in ("h", "x", "y", "z", "s", "sdg", "t", "tdg", "sx"))
 CX, CZ = KIND["cx"], KIND["cz"]
+PAULI = KIND["pauli"]
 
 _R2 = 1.0 / math.sqrt(2.0)
 
@@ -72,6 +73,10 @@ def _u1(kind: int, ang: torch.Tensor, dtype) -> tuple:
         return one, zero, zero, one * complex(math.cos(math.pi / 4), -math.sin(math.pi / 4))
     if kind == SX:
         return one * (0.5 + 0.5j), one * (0.5 - 0.5j), one * (0.5 - 0.5j), one * (0.5 + 0.5j)
+    if kind == PAULI:   # per-sample trajectory Pauli, value 0/1/2/3 = I/X/Y/Z
+        ch = torch.round(ang).long()
+        i_, x_, y_, z_ = ((ch == v).to(dtype) for v in range(4))
+        return i_ + z_, x_ - 1j * y_, x_ + 1j * y_, i_ - z_
     raise ValueError(f"not a 1-qubit kind: {kind}")
 
 

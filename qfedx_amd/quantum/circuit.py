@@ -19,6 +19,7 @@ import numpy as np
 KIND = {
     "rx": 0, "ry": 1, "rz": 2, "p": 3, "h": 4, "x": 5, "y": 6, "z": 7, "s": 8, "sdg": 9,
     "t": 10, "tdg": 11, "sx": 12, "cx": 13, "cz": 14, "swap": 15, "unitary": 16, "initialize": 17,
+    "pauli": 18,   # noise-trajectory Pauli: the (per-sample) parameter value 0/1/2/3 selects I/X/Y/Z
 }
 PARAMETRIC = {"rx", "ry", "rz", "p"}
 TWO_QUBIT = {"cx", "cz", "swap"}
@@ -139,6 +140,7 @@ class Circuit:
     def t(self, q: int): return self.append("t", (q,))
     def tdg(self, q: int): return self.append("tdg", (q,))
     def sx(self, q: int): return self.append("sx", (q,))
+    def pauli(self, sel: Angle, q: int): return self.append("pauli", (q,), sel)
     def cx(self, c: int, t: int): return self.append("cx", (c, t))
     cnot = cx
     def cz(self, a: int, b: int): return self.append("cz", (a, b))
@@ -299,6 +301,9 @@ def gate_matrix(name: str, angle: float = 0.0) -> np.ndarray:
         return np.array([[np.exp(-0.5j * angle), 0], [0, np.exp(0.5j * angle)]])
     if name == "p":
         return np.array([[1, 0], [0, np.exp(1j * angle)]])
+    if name == "pauli":
+        return [np.eye(2), np.array([[0, 1], [1, 0]]), np.array([[0, -1j], [1j, 0]]),
+                np.diag([1, -1])][int(round(angle))].astype(np.complex128)
     r2 = 1 / math.sqrt(2)
     fixed = {
         "h": np.array([[r2, r2], [r2, -r2]], dtype=np.complex128),
