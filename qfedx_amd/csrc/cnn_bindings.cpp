@@ -1,4 +1,100 @@
-// Bindings of the client-batched TinyCNN kernels (cnn_kernels.hip).
+// Bindings of the client-batched TinyCNN kernels (cnn_kernels.hip).  All launches go on torch's current
+// HIP stream (composable with graphs / stream semantics like the statevector ops).
+#include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
-void register_cnn(pybind11::module& m) { (void)m; }
+#include <cstdint>
+#include <stdexcept>
+#include <vector>
+
+extern "C" {
+int qfx_cnn_mfma_probe(const float* A, const float* B, float* D, int K, hipStream_t st);
+int qfx_cnn_forward(const float* X, const float* params, int P, int K, int B, const int* off4, float* pool1,
+                    uint8_t* am1, float* pool2, uint8_t* am2, hipStream_t st);
+int qfx_cnn_backward(const float* X, const float* params, int P, int K, int B, const int* off4, const float* pool1,
+                     const uint8_t* am1, const float* pool2, const uint8_t* am2, const float* dP2, float* part,
+                     float* grad, hipStream_t st);
+int qfx_cnn_head(const float* h1, const float* mask, const float* params, int P, int off_w, int off_b, int C, int K,
+                 int B, const long long* y, const float* wts, float* dh1, float* dlog, float* loss, float* correct,
+                 float* grad, hipStream_t st);
+int qfx_cnn_partial_size();
+int qfx_cnn_bwd_groups(int B);
+}
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+template <typename T>
+T* dptr(const torch::Tensor& t, torch::ScalarType dt, const char* name, int64_t min_numel) {
+  if (!t.defined() || t.scalar_type() != dt || !t.is_contiguous() || !t.is_cuda())
+    throw std::invalid_argument(std::string("cnn: bad tensor ") + name);
+  if (t.numel() < min_numel) throw std::invalid_argument(std::string("cnn: tensor too small: ") + name);
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+
+void check(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + " failed: " + std::to_string(rc));
+}
+
+constexpr int64_t IMG = 28 * 28, POOL1 = 16 * 14 * 14, POOL2 = 32 * 7 * 7;
+
+void mfma_probe(torch::Tensor A, torch::Tensor B, torch::Tensor D, int64_t K) {
+  check(qfx_cnn_mfma_probe(dptr<float>(A, torch::kFloat32, "A", 16 * K), dptr<float>(B, torch::kFloat32, "B", 16 * K),
+                           dptr<float>(D, torch::kFloat32, "D", 256), (int)K, stream()),
+        "mfma_probe");
+}
+
+void forward(torch::Tensor X, torch::Tensor params, int64_t K, int64_t B, std::vector<int64_t> off, torch::Tensor pool1,
+             torch::Tensor am1, torch::Tensor pool2, torch::Tensor am2) {
+  const int64_t S = K * B;
+  const int P = (int)params.size(1);
+  if (params.size(0) < K || off.size() != 4) throw std::invalid_argument("cnn_forward: params/off");
+  std::vector<int> o(off.begin(), off.end());
+  check(qfx_cnn_forward(dptr<float>(X, torch::kFloat32, "X", S * IMG), dptr<float>(params, torch::kFloat32, "params", K * P),
+                        P, (int)K, (int)B, o.data(), dptr<float>(pool1, torch::kFloat32, "pool1", S * POOL1),
+                        dptr<uint8_t>(am1, torch::kUInt8, "am1", S * POOL1), dptr<float>(pool2, torch::kFloat32, "pool2", S * POOL2),
+                        dptr<uint8_t>(am2, torch::kUInt8, "am2", S * POOL2), stream()),
+        "cnn_forward");
+}
+
+void backward(torch::Tensor X, torch::Tensor params, int64_t K, int64_t B, std::vector<int64_t> off, torch::Tensor pool1,
+              torch::Tensor am1, torch::Tensor pool2, torch::Tensor am2, torch::Tensor dP2, torch::Tensor part,
+              torch::Tensor grad) {
+  const int64_t S = K * B;
+  const int P = (int)params.size(1);
+  std::vector<int> o(off.begin(), off.end());
+  const int64_t G = qfx_cnn_bwd_groups((int)B);
+  check(qfx_cnn_backward(dptr<float>(X, torch::kFloat32, "X", S * IMG), dptr<float>(params, torch::kFloat32, "params", K * P),
+                         P, (int)K, (int)B, o.data(), dptr<float>(pool1, torch::kFloat32, "pool1", S * POOL1),
+                         dptr<uint8_t>(am1, torch::kUInt8, "am1", S * POOL1), dptr<float>(pool2, torch::kFloat32, "pool2", S * POOL2),
+                         dptr<uint8_t>(am2, torch::kUInt8, "am2", S * POOL2), dptr<float>(dP2, torch::kFloat32, "dP2", S * POOL2),
+                         dptr<float>(part, torch::kFloat32, "part", K * G * qfx_cnn_partial_size()),
+                         dptr<float>(grad, torch::kFloat32, "grad", K * P), stream()),
+        "cnn_backward");
+}
+
+void head(torch::Tensor h1, torch::Tensor mask, torch::Tensor params, int64_t off_w, int64_t off_b, int64_t C, int64_t K,
+          int64_t B, torch::Tensor y, torch::Tensor wts, torch::Tensor dh1, torch::Tensor dlog, torch::Tensor loss,
+          torch::Tensor correct, torch::Tensor grad) {
+  const int64_t S = K * B;
+  const int P = (int)params.size(1);
+  check(qfx_cnn_head(dptr<float>(h1, torch::kFloat32, "h1", S * 64), dptr<float>(mask, torch::kFloat32, "mask", S * 64),
+                     dptr<float>(params, torch::kFloat32, "params", K * P), P, (int)off_w, (int)off_b, (int)C, (int)K,
+                     (int)B, dptr<long long>(y, torch::kInt64, "y", S), dptr<float>(wts, torch::kFloat32, "wts", S),
+                     dptr<float>(dh1, torch::kFloat32, "dh1", S * 64), dptr<float>(dlog, torch::kFloat32, "dlog", S * 16),
+                     dptr<float>(loss, torch::kFloat32, "loss", K), dptr<float>(correct, torch::kFloat32, "correct", K),
+                     dptr<float>(grad, torch::kFloat32, "grad", K * P), stream()),
+        "cnn_head");
+}
+
+}  // namespace
+
+void register_cnn(pybind11::module& m) {
+  m.def("cnn_mfma_probe", &mfma_probe);
+  m.def("cnn_forward", &forward, "fused conv1/conv2 + bias + ReLU + maxpool (MFMA implicit GEMM)");
+  m.def("cnn_backward", &backward, "conv stack backward -> deterministic per-client weight/bias grads");
+  m.def("cnn_head", &head, "ReLU + dropout + fc2 + weighted CE fwd/bwd per client");
+  m.def("cnn_partial_size", []() { return qfx_cnn_partial_size(); });
+  m.def("cnn_bwd_groups", [](int64_t B) { return qfx_cnn_bwd_groups((int)B); });
+}

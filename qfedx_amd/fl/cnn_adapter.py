@@ -95,21 +95,27 @@ class TinyCNNAdapter:
     def from_state_dict(self, sd: dict) -> torch.Tensor:
         return tc.state_dict_to_flat(sd, self.C)
 
+    def _fwd(self, params: torch.Tensor, xb: torch.Tensor) -> torch.Tensor:
+        x = xb.reshape(1, -1, 1, 28, 28).float()
+        hip = self.trainer._hip
+        if hip is not None:
+            return hip.logits(params[None].float(), x)[0]
+        return tc.batched_forward(params[None].float(), x, self.C)[0]
+
     @torch.no_grad()
     def logits(self, params: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
-        out = [tc.batched_forward(params[None].float(), X[s: s + self.eval_batch].reshape(1, -1, 1, 28, 28).float(),
-                                  self.C)[0] for s in range(0, X.shape[0], self.eval_batch)]
+        out = [self._fwd(params, X[s: s + self.eval_batch]) for s in range(0, X.shape[0], self.eval_batch)]
         return torch.cat(out) if out else torch.zeros(0, self.C, device=X.device)
 
     @torch.no_grad()
     def evaluate(self, params: torch.Tensor, X: torch.Tensor, y: torch.Tensor):
         if X.shape[0] == 0:
             return 0.0, 0.0, 0.0
-        loss_sum = correct = 0.0
-        for s in range(0, X.shape[0], self.eval_batch):
-            xb = X[s: s + self.eval_batch].reshape(1, -1, 1, 28, 28)
+        loss_sum = torch.zeros((), dtype=torch.float64, device=X.device)
+        correct = torch.zeros((), dtype=torch.float64, device=X.device)
+        for s in range(0, X.shape[0], self.eval_batch):       # no per-batch host sync (reference :100)
+            logits = self._fwd(params, X[s: s + self.eval_batch])
             yb = y[s: s + self.eval_batch]
-            logits = tc.batched_forward(params[None].float(), xb.float(), self.C)[0]
-            loss_sum += float(F.cross_entropy(logits, yb, reduction="sum"))
-            correct += float((logits.argmax(-1) == yb).sum())
-        return loss_sum, correct, float(X.shape[0])
+            loss_sum += F.cross_entropy(logits, yb, reduction="sum").double()
+            correct += (logits.argmax(-1) == yb).sum().double()
+        return float(loss_sum), float(correct), float(X.shape[0])

@@ -1,0 +1,102 @@
+"""GPU numerics of the client-batched TinyCNN kernels vs plain PyTorch fp32 (grouped conv / autograd)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from qfedx_amd.models import tinycnn as tc
+
+pytestmark = pytest.mark.gpu
+
+
+def test_mfma_16x16x4_layout(cuda):
+    from qfedx_amd.ops._ext import ext
+    g = torch.Generator().manual_seed(0)
+    A = torch.randn(16, 12, generator=g)
+    B = torch.randn(12, 16, generator=g)
+    D = torch.empty(256, device=cuda)
+    ext().cnn_mfma_probe(A.to(cuda).contiguous(), B.to(cuda).contiguous(), D, 12)
+    assert torch.allclose(D.view(16, 16).cpu(), A @ B, atol=1e-4)
+
+
+def _batch(K, B, C=3, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    params = torch.stack([tc.init_flat(C, seed + k) for k in range(K)])
+    params += 0.02 * torch.randn(params.shape, generator=g)
+    X = torch.rand(K, B, 1, 28, 28, generator=g)
+    X[X < 0.6] = 0.0                       # MNIST-like sparsity
+    y = torch.randint(0, C, (K, B), generator=g)
+    w = torch.full((K, B), 1.0 / B)
+    mask = (torch.rand(K, B, 64, generator=g) >= 0.5).float() * 2.0
+    return params, X, y, w, mask
+
+
+@pytest.mark.parametrize("K,B", [(1, 1), (3, 5), (4, 32)])
+def test_conv_forward_matches_torch(cuda, K, B):
+    from qfedx_amd.ops.cnn_hip import HipTinyCNN
+    params, X, y, w, mask = _batch(K, B)
+    hip = HipTinyCNN(3, cuda)
+    _, pool1, am1, pool2, am2 = hip.conv_forward(params.to(cuda), X.to(cuda))
+    v = tc.views(params)
+    h = X.reshape(K, B, 28, 28).transpose(0, 1)
+    c1 = F.conv2d(h, v["conv1.weight"].reshape(K * 16, 1, 5, 5), v["conv1.bias"].reshape(-1), padding=2, groups=K)
+    p1 = F.max_pool2d(F.relu(c1), 2)
+    c2 = F.conv2d(p1, v["conv2.weight"].reshape(K * 32, 16, 5, 5), v["conv2.bias"].reshape(-1), padding=2, groups=K)
+    p2 = F.max_pool2d(F.relu(c2), 2)
+    ref1 = p1.reshape(B, K, 16 * 196).transpose(0, 1).reshape(K * B, -1)
+    ref2 = p2.reshape(B, K, 32 * 49).transpose(0, 1).reshape(K * B, -1)
+    assert torch.allclose(pool1.cpu(), ref1, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(pool2.cpu(), ref2, atol=1e-4, rtol=1e-4)
+    lg = hip.logits(params.to(cuda), X.to(cuda)).cpu()
+    assert torch.allclose(lg, tc.batched_forward(params, X, 3), atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("K,B,C", [(2, 3, 3), (3, 32, 3), (2, 7, 10)])
+def test_loss_and_grads_match_autograd(cuda, K, B, C):
+    from qfedx_amd.ops.cnn_hip import HipTinyCNN
+    params, X, y, w, mask = _batch(K, B, C, seed=K + B)
+    hip = HipTinyCNN(C, cuda)
+    r = hip.loss_and_grads(params.to(cuda), X.to(cuda), y.to(cuda), w.to(cuda), mask.to(cuda))
+    p = params.clone().requires_grad_(True)
+    logits = tc.batched_forward(p, X, C, mask)
+    nll = F.cross_entropy(logits.reshape(-1, C), y.reshape(-1), reduction="none").reshape(K, B)
+    loss = (nll * w).sum(-1)
+    loss.sum().backward()
+    assert torch.allclose(r["loss"].cpu(), loss.detach(), atol=1e-4, rtol=1e-4)
+    g = r["grad"].cpu()
+    bounds = tc.layer_boundaries(C)
+    for name, a, b in zip(tc.param_shapes(C), bounds[:-1], bounds[1:]):
+        ref = p.grad[:, a:b]
+        err = (g[:, a:b] - ref).abs().max().item()
+        scale = ref.abs().max().item() + 1e-6
+        assert err <= 2e-3 * scale + 1e-6, (name, err, scale)
+    acc = ((logits.argmax(-1) == y) & (w > 0)).sum(-1).float()
+    assert torch.equal(r["correct"].cpu(), acc)
+
+
+def test_cfed_federated_run_hip_matches_cpu(cuda):
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.config import ExperimentConfig
+    from qfedx_amd.parallel.dist import init_distributed
+
+    def cfg(dev, backend):
+        c = ExperimentConfig()
+        c.model.kind = "tinycnn"
+        c.data.num_clients = 4
+        c.data.samples_per_client = 64
+        c.data.test_samples = 128
+        c.train.num_rounds = 2
+        c.train.optimizer = "sgd"
+        c.train.learning_rate = 0.05
+        c.train.batch_size = 16
+        c.train.aggregate = "weights"
+        c.train.wrap_angles = False
+        c.runtime.device = dev
+        c.runtime.backend = backend
+        c.runtime.log_every = 100
+        return c
+
+    cpu = run_experiment(cfg("cpu", "torch"))
+    dev = torch.device("cuda", 0)
+    gpu = run_experiment(cfg("cuda", "hip"), world=init_distributed(dev), device=dev, backend="hip")
+    assert torch.allclose(gpu["params"].cpu(), cpu["params"], atol=2e-4, rtol=1e-3)
+    assert abs(gpu["accuracies"][-1] - cpu["accuracies"][-1]) < 0.02
