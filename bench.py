@@ -22,6 +22,36 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+def timed_rounds(cfg, device, backend, world, warmup: int, steps: int):
+    """Build this rank's runner, run ``warmup`` untimed rounds, then time exactly ``steps`` rounds
+    bracketed by barrier + device sync on both sides; returns (runner, max-over-ranks seconds)."""
+    import torch
+    from qfedx_amd.data.datasets import build_federated_data
+    from qfedx_amd.fl.adapters import make_adapter
+    from qfedx_amd.fl.server import FederatedRunner
+    from qfedx_amd.parallel.dist import barrier, max_over_ranks, shard_clients
+
+    my = shard_clients(cfg.data.num_clients, world.world_size, world.rank)
+    data = build_federated_data(cfg, clients=my)
+    adapter = make_adapter(cfg, device, backend)
+    runner = FederatedRunner(cfg, adapter, data, world, device, backend)
+
+    def sync():
+        barrier(world)
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+
+    for r in range(warmup):
+        runner.run_round(r, sync=False)
+    sync()
+    t0 = time.perf_counter()
+    for r in range(warmup, warmup + steps):
+        runner.run_round(r, sync=False)
+    sync()
+    dt = time.perf_counter() - t0
+    return runner, max_over_ranks(dt, world)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -41,10 +71,7 @@ def main():
     import torch
     from qfedx_amd.config import ExperimentConfig
     from qfedx_amd.api import setup
-    from qfedx_amd.data.datasets import build_federated_data
-    from qfedx_amd.fl.adapters import make_adapter
-    from qfedx_amd.fl.server import FederatedRunner
-    from qfedx_amd.parallel.dist import barrier, max_over_ranks, shard_clients, shutdown
+    from qfedx_amd.parallel.dist import shutdown
 
     cfg = ExperimentConfig(name="bench")
     cfg.data.dataset = "synthetic"
@@ -69,25 +96,7 @@ def main():
     cfg.runtime.backend = args.backend
     cfg.runtime.device = args.device
     device, backend, world = setup(cfg)
-    my = shard_clients(cfg.data.num_clients, world.world_size, world.rank)
-    data = build_federated_data(cfg, clients=my)
-    adapter = make_adapter(cfg, device, backend)
-    runner = FederatedRunner(cfg, adapter, data, world, device, backend)
-
-    def sync():
-        barrier(world)
-        if device.type == "cuda":
-            torch.cuda.synchronize()
-
-    for r in range(args.warmup):
-        runner.run_round(r, sync=False)
-    sync()
-    t0 = time.perf_counter()
-    for r in range(args.warmup, args.warmup + args.steps):
-        runner.run_round(r, sync=False)
-    sync()
-    dt = time.perf_counter() - t0
-    dt = max_over_ranks(dt, world)
+    runner, dt = timed_rounds(cfg, device, backend, world, args.warmup, args.steps)
     ev = runner.evaluate()
     local_steps_total = args.clients * args.local_steps * args.steps
     value = local_steps_total / dt

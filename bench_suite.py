@@ -1,0 +1,93 @@
+"""Benchmarks of the other BASELINE.json configs (bench.py is the headline 16q x 64-client VQC).
+
+    python bench_suite.py --config cfed128 --steps 10 --warmup 2
+    torchrun --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench_suite.py --config vqc20q_dp64
+
+One step = one federated round of the named config (every participating client runs its local steps,
+fused local reduce, one all-reduce, global update).  Prints one JSON line (rank 0) in bench.py's
+format; ``vs_baseline`` is set where BASELINE.md has a measured reference number (CFed: 258 client
+local-steps/s for the reference TinyCNN ``client_update`` on an 8-vCPU host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SUITE = {
+    # name: (config file, overrides, metric label, reference client-local-steps/s or None)
+    "cfed128": ("configs/baseline4_cfed_128clients.yaml", ["train.local_steps=1"],
+                "client local-steps/sec (CFed TinyCNN x 128 clients, batch 32)", 258.0),
+    "cfed128_epoch": ("configs/baseline4_cfed_128clients.yaml", [],
+                      "client local-steps/sec (CFed TinyCNN x 128 clients, 1 local epoch)", 258.0),
+    "vqc20q_dp64": ("configs/baseline3_20q_dp_64clients.yaml", [],
+                    "client local-steps/sec (20-qubit VQC x 64 non-IID clients, DP)", None),
+    "vqc24q_ps256": ("configs/baseline5_24q_256clients_paramshift_shots.yaml", [],
+                     "client local-steps/sec (24-qubit VQC x 256 clients, param-shift + shots)", None),
+    "vqc16q_bf16_8": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1"],
+                      "client local-steps/sec (16-qubit VQC bf16 state x 8 clients)", None),
+    "vqc16q_64": ("configs/headline_16q_64clients.yaml", [],
+                  "client local-steps/sec (16-qubit VQC x 64 clients federated rounds)", None),
+    "vqc4q_2_cpu": ("configs/baseline1_4q_2clients_cpu.yaml", ["train.local_steps=1"],
+                    "client local-steps/sec (4-qubit VQC x 2 clients, CPU gloo)", None),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfed128", choices=sorted(SUITE))
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("overrides", nargs="*")
+    args = ap.parse_args()
+
+    from bench import timed_rounds
+    from qfedx_amd.api import setup
+    from qfedx_amd.config import load_config
+    from qfedx_amd.parallel.dist import shutdown
+
+    path, ov, metric, ref = SUITE[args.config]
+    cfg = load_config(os.path.join(ROOT, path), ov + list(args.overrides))
+    device, backend, world = setup(cfg)
+    runner, dt = timed_rounds(cfg, device, backend, world, args.warmup, args.steps)
+    t = cfg.train
+    hist_steps = None
+    # local steps actually run per round (all clients): epochs x ceil(n/B), or the fixed step count
+    if t.local_steps > 0:
+        per_round = int(round(cfg.data.num_clients * t.client_fraction)) * t.local_steps
+    else:
+        import math
+        per_round = sum(t.local_epochs * math.ceil(int(n) / t.batch_size) for n in runner.store.counts)
+        per_round = int(per_round * world.world_size)   # store holds this rank's clients
+    value = per_round * args.steps / dt
+    ev = runner.evaluate()
+    if world.is_main:
+        kind = cfg.model.kind
+        rec = {
+            "metric": metric, "value": round(value, 3), "unit": "client local-steps/s",
+            "n_gpus": world.world_size, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": round(value / ref, 2) if ref else None,
+            "dtype": "bf16-state/fp32-compute" if cfg.model.state_dtype == "bf16" else "fp32",
+            "data": "synthetic non-IID client shards, random init", "rounds_per_sec": round(args.steps / dt, 4),
+            "samples_per_sec": round(value * t.batch_size, 1), "backend": backend,
+            "test_acc_after": round(ev["test_acc"], 4),
+            "config": {"name": cfg.name, "model": kind if kind != "vqc" else
+                       f"vqc-{cfg.model.n_qubits}q-{cfg.model.n_layers}L",
+                       "global_batch": cfg.data.num_clients * t.batch_size,
+                       "seq_len": cfg.model.n_qubits if kind == "vqc" else 784,
+                       "parallelism": f"client-parallel dp{world.world_size}", "n_clients": cfg.data.num_clients,
+                       "grad": t.grad_method, "optimizer": t.optimizer, "dp": cfg.privacy.dp,
+                       "shots": cfg.noise.shots},
+        }
+        print(json.dumps(rec), flush=True)
+    shutdown(world)
+
+
+if __name__ == "__main__":
+    main()

@@ -184,20 +184,23 @@ class VQCClientTrainer:
         return self.backend == "hip" and self.device.type == "cuda" and getattr(self, "graphs", True)
 
     def _graphed(self, store, local_idx, li, theta_g, plan, round_num):
-        """Replay the whole round as ONE hipGraph (static shapes: clients, steps, batch).
+        """Replay the whole round as ONE hipGraph (static shapes: #clients, steps, batch).
 
-        Captured once per (client set, step count); each round only refreshes the static inputs
-        (global params + this round's minibatch index tables) and replays ~15 launches per local
-        step with no host round trips.
+        Captured once per SHAPE, not per client set: the round's client shards are gathered on the
+        device into static buffers (client sampling changes the set every round), together with the
+        global params and the minibatch index tables; then ~15 launches per local step replay with no
+        host round trips.  A small LRU bounds the number of live graphs.
         """
-        key = (tuple(local_idx), plan.max_steps, plan.B)
+        K = len(local_idx)
+        key = (K, plan.max_steps, plan.B, store.nmax)
         cache = self.__dict__.setdefault("_graph_cache", {})
-        ent = cache.get(key)
+        dev = self.device
+        lid = h2d(li, store.X.device)
+        ent = cache.pop(key, None)
         if ent is None:
-            dev = self.device
             ent = {
-                "X": store.X[li.to(store.X.device)].contiguous(),
-                "y": store.y[li.to(store.y.device)].contiguous(),
+                "X": store.X[lid].contiguous(),
+                "y": store.y[lid].contiguous(),
                 "theta": theta_g.to(dev).float().clone(),
                 "idx": plan.idx.to(dev).clone(), "wts": plan.wts.to(dev).clone(), "act": plan.active.to(dev).clone(),
             }
@@ -215,7 +218,12 @@ class VQCClientTrainer:
                 with torch.cuda.graph(g):
                     ent["out"] = self._body(*args)
             ent["graph"] = g
-            cache[key] = ent
+            while len(cache) >= 4:                  # LRU: drop the oldest shape
+                cache.pop(next(iter(cache)))
+        else:
+            torch.index_select(store.X, 0, lid, out=ent["X"])
+            torch.index_select(store.y, 0, lid, out=ent["y"])
+        cache[key] = ent                            # most recently used last
         ent["theta"].copy_(theta_g.float())
         ent["idx"].copy_(h2d(plan.idx, self.device))
         ent["wts"].copy_(h2d(plan.wts, self.device))

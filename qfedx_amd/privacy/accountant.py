@@ -10,6 +10,7 @@ State is tiny (orders + accumulated rdp) and checkpointable.
 """
 from __future__ import annotations
 
+import functools
 import math
 from typing import Iterable, Optional
 
@@ -90,8 +91,17 @@ def rdp_sampled_gaussian(q: float, sigma: float, alpha: float) -> float:
     return _log_a_frac(q, sigma, alpha) / (alpha - 1)
 
 
+@functools.lru_cache(maxsize=256)
+def _rdp_curve(q: float, sigma: float, orders: tuple) -> np.ndarray:
+    # one step of the sampled Gaussian at every order: depends only on (q, sigma), so a training run
+    # (fixed q, sigma every round) evaluates the series once instead of once per round
+    out = np.array([rdp_sampled_gaussian(q, sigma, a) for a in orders])
+    out.setflags(write=False)
+    return out
+
+
 def compute_rdp(q: float, sigma: float, steps: int, orders: Iterable[float] = DEFAULT_ORDERS) -> np.ndarray:
-    return np.array([rdp_sampled_gaussian(q, sigma, a) * steps for a in orders])
+    return _rdp_curve(float(q), float(sigma), tuple(float(a) for a in orders)) * steps
 
 
 def eps_from_rdp(orders, rdp, delta: float, conversion: str = "improved") -> tuple[float, float]:
