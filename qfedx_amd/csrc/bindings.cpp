@@ -37,9 +37,10 @@ struct PassArgsHost {
   int n_grad;
 };
 int jit_prepare(const std::vector<int>& blob, int p, bool adjoint, const std::string& cache_dir,
-                const std::string& include_dir, const std::string& arch, std::string* key_out);
+                const std::string& include_dir, const std::string& arch, std::string* key_out, bool bf16);
 int jit_launch(int handle, const PassArgsHost& args, hipStream_t stream);
-std::string jit_source(const std::vector<int>& blob, int p, bool adjoint);
+std::string jit_source(const std::vector<int>& blob, int p, bool adjoint, bool bf16);
+long jit_state_bytes(int handle, bool* bf16);
 }  // namespace qfx
 
 extern "C" {
@@ -216,14 +217,14 @@ std::vector<int> blob_vec(const torch::Tensor& blob) {
 }
 
 py::tuple jit_prepare(torch::Tensor blob, int64_t p, bool adjoint, std::string cache_dir, std::string include_dir,
-                      std::string arch) {
+                      std::string arch, bool bf16) {
   std::string key;
-  int h = qfx::jit_prepare(blob_vec(blob), (int)p, adjoint, cache_dir, include_dir, arch, &key);
+  int h = qfx::jit_prepare(blob_vec(blob), (int)p, adjoint, cache_dir, include_dir, arch, &key, bf16);
   return py::make_tuple(h, key);
 }
 
-std::string jit_source(torch::Tensor blob, int64_t p, bool adjoint) {
-  return qfx::jit_source(blob_vec(blob), (int)p, adjoint);
+std::string jit_source(torch::Tensor blob, int64_t p, bool adjoint, bool bf16) {
+  return qfx::jit_source(blob_vec(blob), (int)p, adjoint, bf16);
 }
 
 void jit_launch(int64_t handle, torch::Tensor blob, int64_t pass_off, torch::Tensor psi, c10::optional<torch::Tensor> lam,
@@ -231,7 +232,14 @@ void jit_launch(int64_t handle, torch::Tensor blob, int64_t pass_off, torch::Ten
                 c10::optional<torch::Tensor> out_read, c10::optional<torch::Tensor> gslab, int64_t n_samples,
                 int64_t n_grad) {
   need(blob, torch::kInt32, "blob");
-  need(psi, torch::kComplexFloat, "psi");
+  bool bf16 = false;
+  const long sbytes = qfx::jit_state_bytes((int)handle, &bf16);
+  if (sbytes < 0) throw std::invalid_argument("jit_launch: bad kernel handle");
+  need(psi, bf16 ? torch::kInt32 : torch::kComplexFloat, "psi (int32 = packed bf16x2 state)");
+  // the kernel indexes [n_samples, 2^n] amplitudes: refuse buffers that would be overrun
+  if ((long)(psi.numel() * psi.element_size()) < sbytes * n_samples) throw std::invalid_argument("psi too small");
+  if (lam.has_value() && (long)(lam->numel() * lam->element_size()) < sbytes * n_samples)
+    throw std::invalid_argument("lam too small");
   need(params, torch::kFloat32, "params");
   need(xang, torch::kFloat32, "xang");
   if (xang.size(0) < n_samples) throw std::invalid_argument("xang rows < n_samples");
@@ -262,8 +270,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam", &adam);
   m.def("sgdm", &sgdm);
   m.def("fedavg", &fedavg);
-  m.def("jit_prepare", &jit_prepare, "generate + hiprtc-compile (or load cached) a circuit-specialised pass kernel");
-  m.def("jit_source", &jit_source);
+  m.def("jit_prepare", &jit_prepare, "generate + hiprtc-compile (or load cached) a circuit-specialised pass kernel",
+        py::arg("blob"), py::arg("p"), py::arg("adjoint"), py::arg("cache_dir"), py::arg("include_dir"),
+        py::arg("arch"), py::arg("bf16") = false);
+  m.def("jit_source", &jit_source, py::arg("blob"), py::arg("p"), py::arg("adjoint"), py::arg("bf16") = false);
   m.def("jit_launch", &jit_launch);
   register_cnn(m);
 }

@@ -67,7 +67,7 @@ struct JitSpec {
 };
 
 // Generate the kernel source for pass `p` of `blob`.
-JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint) {
+JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf16) {
   const int n = blob[HF_N], R = blob[HF_R], G = blob[HF_NGATES], n_theta = blob[HF_NTHETA];
   int RB = 0;
   while ((1 << RB) < R) ++RB;
@@ -123,8 +123,19 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint) {
     return e.str();
   };
 
+  // state loads / stores: complex64, or packed bf16x2 (state_dtype=bf16)
+  auto ld = [&](const std::string& arr, const std::string& idx) -> std::string {
+    if (bf16) return "unpack_bf16x2(reinterpret_cast<const uint32_t*>(A." + arr + ")[" + idx + "])";
+    return "A." + arr + "[" + idx + "]";
+  };
+  auto st = [&](const std::string& arr, const std::string& idx, const std::string& v) -> std::string {
+    if (bf16) return "reinterpret_cast<uint32_t*>(A." + arr + ")[" + idx + "] = pack_bf16x2(" + v + ")";
+    return "A." + arr + "[" + idx + "] = " + v;
+  };
+
   std::ostringstream s;
-  s << "// generated by qfedx_amd/csrc/jit.cpp - pass " << p << (adjoint ? " (adjoint)" : " (forward)") << "\n";
+  s << "// generated by qfedx_amd/csrc/jit.cpp - pass " << p << (adjoint ? " (adjoint)" : " (forward)")
+    << (bf16 ? " bf16 state" : "") << "\n";
   s << "#include \"qfx_device.h\"\n";
   // occupancy target (waves per SIMD) for the register allocator: QFEDX_JIT_WAVES[_ADJ|_FWD] (0 = compiler
   // default).  Part of the generated source, hence of the code-object cache key.
@@ -219,9 +230,9 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint) {
     s << "  {\n    const uint32_t gthr = " << xor_expr(pd + PF_GTHR0, tb) << ";\n";
     s << "    if (valid) {\n";
     for (int r = 0; r < R; ++r) {
-      s << "      a[" << r << "] = A.psi[sbase + gbase + (gthr | " << (uint32_t)pd[PF_GREG0 + r] << "u)];\n";
+      s << "      a[" << r << "] = " << ld("psi", "sbase + gbase + (gthr | " + std::to_string((uint32_t)pd[PF_GREG0 + r]) + "u)") << ";\n";
       if (adjoint && init == INIT_LOAD_BOTH)
-        s << "      l[" << r << "] = A.lam[sbase + gbase + (gthr | " << (uint32_t)pd[PF_GREG0 + r] << "u)];\n";
+        s << "      l[" << r << "] = " << ld("lam", "sbase + gbase + (gthr | " + std::to_string((uint32_t)pd[PF_GREG0 + r]) + "u)") << ";\n";
     }
     s << "    }\n  }\n";
     if (adjoint && init == INIT_PSI_LAMBDA) {
@@ -348,8 +359,9 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint) {
   if (fin & FIN_STORE) {
     s << "  {\n    const uint32_t gthr = " << xor_expr(pd + PF_GTHRF, tb) << ";\n    if (valid) {\n";
     for (int r = 0; r < R; ++r) {
-      s << "      A.psi[sbase + gbase + (gthr | " << (uint32_t)pd[PF_GREGF + r] << "u)] = a[" << r << "];\n";
-      if (adjoint) s << "      A.lam[sbase + gbase + (gthr | " << (uint32_t)pd[PF_GREGF + r] << "u)] = l[" << r << "];\n";
+      const std::string idx = "sbase + gbase + (gthr | " + std::to_string((uint32_t)pd[PF_GREGF + r]) + "u)";
+      s << "      " << st("psi", idx, "a[" + std::to_string(r) + "]") << ";\n";
+      if (adjoint) s << "      " << st("lam", idx, "l[" + std::to_string(r) + "]") << ";\n";
     }
     s << "    }\n  }\n";
   }
@@ -395,6 +407,7 @@ struct JitEntry {
   hipFunction_t fn = nullptr;
   size_t lds = 0;
   int tiles_pb = 1, k = 0, n = 0;
+  bool bf16 = false;
   std::string key;
 };
 
@@ -409,8 +422,8 @@ static bool file_exists(const std::string& p) {
 
 // Generate + compile (or load from the disk cache) pass p; returns a handle.  No GPU needed.
 int jit_prepare(const std::vector<int>& blob, int p, bool adjoint, const std::string& cache_dir,
-                const std::string& include_dir, const std::string& arch, std::string* key_out) {
-  JitSpec spec = codegen_pass(blob, p, adjoint);
+                const std::string& include_dir, const std::string& arch, std::string* key_out, bool bf16) {
+  JitSpec spec = codegen_pass(blob, p, adjoint, bf16);
   std::string header;
   {
     std::ifstream f(include_dir + "/qfx_device.h");
@@ -432,6 +445,7 @@ int jit_prepare(const std::vector<int>& blob, int p, bool adjoint, const std::st
   e->tiles_pb = spec.tiles_pb;
   e->k = spec.k;
   e->n = spec.n;
+  e->bf16 = bf16;
   e->key = key;
   const std::string path = cache_dir + "/" + key + ".co";
   if (!cache_dir.empty() && file_exists(path)) {
@@ -458,7 +472,9 @@ int jit_prepare(const std::vector<int>& blob, int p, bool adjoint, const std::st
   return h;
 }
 
-std::string jit_source(const std::vector<int>& blob, int p, bool adjoint) { return codegen_pass(blob, p, adjoint).source; }
+std::string jit_source(const std::vector<int>& blob, int p, bool adjoint, bool bf16) {
+  return codegen_pass(blob, p, adjoint, bf16).source;
+}
 
 struct PassArgsHost {   // must match qfx::PassArgs in qfx_device.h
   const int* blob;
@@ -476,6 +492,15 @@ struct PassArgsHost {   // must match qfx::PassArgs in qfx_device.h
   int n_samples;
   int n_grad;
 };
+
+// bytes of one sample's statevector in the kernel's storage format (-1: bad handle)
+long jit_state_bytes(int handle, bool* bf16) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (handle < 0 || handle >= (int)g_entries.size()) return -1;
+  const JitEntry* e = g_entries[handle].get();
+  if (bf16) *bf16 = e->bf16;
+  return (1L << e->n) * (e->bf16 ? 4L : 8L);
+}
 
 int jit_launch(int handle, const PassArgsHost& args, hipStream_t stream) {
   JitEntry* e;

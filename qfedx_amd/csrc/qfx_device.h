@@ -33,6 +33,17 @@ __device__ __forceinline__ v2f pfma(v2f a, v2f b, v2f c) { return __builtin_elem
 __device__ __forceinline__ v2f cmul(v2f a, v2f b) { return pfma(splat(a.x), b, sw(b * mk(a.y, -a.y))); }
 // a * b + c
 __device__ __forceinline__ v2f cfma(v2f a, v2f b, v2f c) { return pfma(splat(a.x), b, sw(pfma(b, mk(a.y, -a.y), sw(c)))); }
+// bf16 statevector storage (state_dtype=bf16): one amplitude = bf16 re | bf16 im << 16 in 32 bits;
+// compute stays fp32, stores round to nearest even
+__device__ __forceinline__ v2f unpack_bf16x2(uint32_t u) {
+  return mk(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+}
+__device__ __forceinline__ uint32_t bf16_rne(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(v2f v) { return bf16_rne(v.x) | (bf16_rne(v.y) << 16); }
 __device__ __forceinline__ v2f conjf2(v2f a) { return mk(a.x, -a.y); }
 __device__ __forceinline__ float imcl(v2f l, v2f p) { return l.x * p.y - l.y * p.x; }  // Im(conj(l) p)
 __device__ __forceinline__ float recl(v2f l, v2f p) { return l.x * p.x + l.y * p.y; }  // Re(conj(l) p)

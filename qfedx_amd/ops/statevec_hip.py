@@ -51,7 +51,8 @@ def jit_enabled() -> bool:
 
 
 class _Plan:
-    def __init__(self, ops, coef, n, R, kmax, readout, n_theta, mode, final_flags, device, jit: bool):
+    def __init__(self, ops, coef, n, R, kmax, readout, n_theta, mode, final_flags, device, jit: bool,
+                 bf16: bool = False):
         C = ext()
         blob = C.plan(torch.as_tensor(ops), torch.as_tensor(coef), n, R, kmax, list(readout), n_theta,
                       mode, final_flags)
@@ -65,7 +66,7 @@ class _Plan:
         self.n = n
         self.jit_handles = None
         if jit:
-            self.jit_handles = [C.jit_prepare(blob, i, self.adjoint, JIT_CACHE, CSRC, ARCH)[0]
+            self.jit_handles = [C.jit_prepare(blob, i, self.adjoint, JIT_CACHE, CSRC, ARCH, bf16)[0]
                                 for i in range(len(self.passes))]
 
     @property
@@ -76,8 +77,9 @@ class _Plan:
 class HipProgram:
     def __init__(self, ops, coef, n_qubits: int, readout, device, n_theta: int, state_dtype: str = "fp32",
                  kmax: int = KMAX, jit: bool | None = None, x_width: int | None = None):
-        if state_dtype != "fp32":
-            raise NotImplementedError("bf16 statevector storage is not implemented yet")
+        if state_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"state_dtype must be fp32 or bf16, got {state_dtype!r}")
+        self.bf16 = state_dtype == "bf16"
         self.n = n_qubits
         self.readout = list(readout)
         self.C = len(self.readout)
@@ -86,10 +88,15 @@ class HipProgram:
         self.x_width = n_qubits if x_width is None else x_width
         self.R = choose_R(n_qubits)
         self.jit = jit_enabled() if jit is None else jit
+        if self.bf16 and not self.jit:
+            raise RuntimeError("bf16 statevector storage needs the circuit-specialised (JIT) kernels; "
+                               "unset QFEDX_JIT=0")
         args = (ops, coef, n_qubits, self.R, kmax, self.readout, n_theta)
-        self.eval_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_READOUT, self.device, self.jit)
-        self.train_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_STORE | FIN_READOUT, self.device, self.jit)
-        self.adj_plan = _Plan(*args, MODE_ADJ, 0, self.device, self.jit)
+        self.eval_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_READOUT, self.device, self.jit, self.bf16)
+        self.train_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_STORE | FIN_READOUT, self.device, self.jit, self.bf16)
+        self.adj_plan = _Plan(*args, MODE_ADJ, 0, self.device, self.jit, self.bf16)
+        # statevector storage between passes: complex64, or packed bf16 (re, im) in one int32
+        self.state_torch_dtype = torch.int32 if self.bf16 else torch.complex64
         self.G = self.train_plan.info["G"]
         self._ws = {}
 
@@ -134,7 +141,7 @@ class HipProgram:
         x = xang.reshape(S, F).float().contiguous()
         th = theta.float().contiguous()
         plan = self.eval_plan
-        psi = self._buf("psi", S << self.n, torch.complex64)
+        psi = self._buf("psi", S << self.n, self.state_torch_dtype)
         part = self._buf("part", S * plan.tiles_per_state * self.C, torch.float32)
         self._run_passes(plan, False, psi, None, th, B, x, None, part, None, S)
         out = self._buf("expz", S * self.C, torch.float32)
@@ -156,8 +163,8 @@ class HipProgram:
         yy = y.reshape(S).long().contiguous()
         ww = wmask.reshape(S).float().contiguous()
         tr, adj = self.train_plan, self.adj_plan
-        psi = self._buf("psi", S << self.n, torch.complex64)
-        lam = self._buf("lam", S << self.n, torch.complex64)
+        psi = self._buf("psi", S << self.n, self.state_torch_dtype)
+        lam = self._buf("lam", S << self.n, self.state_torch_dtype)
         part = self._buf("part", S * tr.tiles_per_state * self.C, torch.float32)
         slab = self._buf("slab", S * adj.tiles_per_state * self.G, torch.float32)
         expz = self._buf("expz", S * self.C, torch.float32)

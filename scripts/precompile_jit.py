@@ -15,6 +15,8 @@ CONFIGS = [  # (n, L, C, entangler, noisy)
     (11, 2, 3, "chain", False), (11, 2, 3, "ring", False), (12, 2, 3, "ring", False), (13, 2, 3, "chain", False),
     (14, 2, 3, "chain", False), (16, 2, 3, "chain", False), (16, 3, 3, "chain", True),
     (4, 2, 3, "chain", True), (7, 2, 3, "chain", True), (12, 2, 3, "chain", True), (3, 1, 2, "chain", True),
+    (16, 3, 3, "chain", False, True), (6, 2, 3, "chain", False, True), (13, 2, 3, "chain", False, True),
+    (20, 2, 3, "chain", False, True),
 ]
 
 
@@ -23,7 +25,8 @@ def build(cfg):
     from qfedx_amd.models.vqc import VQCSpec
     from qfedx_amd.ops import statevec_hip as sh
     from qfedx_amd.ops._ext import ext
-    n, L, ncls, ent, noisy = cfg
+    n, L, ncls, ent, noisy = cfg[:5]
+    bf16 = bool(cfg[5]) if len(cfg) > 5 else False
     C = ext()
     t0 = time.time()
     spec = VQCSpec(n, L, ncls, entangler=ent, noisy=noisy)
@@ -33,8 +36,8 @@ def build(cfg):
         blob = C.plan(torch.from_numpy(ops), torch.from_numpy(coef), n, R, sh.KMAX, spec.readout,
                       spec.n_theta, mode, fin)
         for p in range(int(blob[1])):
-            C.jit_prepare(blob, p, mode == 2, sh.JIT_CACHE, sh.CSRC, sh.ARCH)
-    return f"n={n} L={L} C={ncls} {ent}{' noisy' if noisy else ''}: ok ({time.time() - t0:.1f}s)"
+            C.jit_prepare(blob, p, mode == 2, sh.JIT_CACHE, sh.CSRC, sh.ARCH, bf16)
+    return f"n={n} L={L} C={ncls} {ent}{' noisy' if noisy else ''}{' bf16' if bf16 else ''}: ok ({time.time() - t0:.1f}s)"
 
 
 def main():

@@ -146,3 +146,22 @@ def test_hip_federated_run_matches_cpu(cuda):
     assert torch.allclose(gpu["params"].cpu(), cpu["params"], atol=1e-4)
     for hg, hc in zip(gpu["history"], cpu["history"]):
         assert abs(hg["train_loss"] - hc["train_loss"]) < 1e-4
+
+
+@pytest.mark.parametrize("n,L", [(6, 2), (13, 2), (16, 3)])
+def test_bf16_state_storage_close_to_fp32(cuda, n, L):
+    """state_dtype=bf16: packed bf16 amplitudes between passes (fp32 compute) stay close to fp32."""
+    spec, x, y, w, params = _setup(n, L, 3, 2, 8, seed=4)
+    f32 = VQCEngine(spec, cuda, "hip", "fp32")
+    b16 = VQCEngine(spec, cuda, "hip", "bf16")
+    xa = spec.encode_features(x).to(cuda)
+    th = spec.split(params)[0].to(cuda)
+    z32, z16 = f32.expz(xa, th), b16.expz(xa, th)
+    assert (z32 - z16).abs().max().item() < 2e-2
+    r32 = f32.loss_and_grads(xa, y.to(cuda), w.to(cuda), params.to(cuda), "adjoint")
+    r16 = b16.loss_and_grads(xa, y.to(cuda), w.to(cuda), params.to(cuda), "adjoint")
+    assert torch.allclose(r32["loss"], r16["loss"], atol=2e-2, rtol=2e-2)
+    g32, g16 = r32["grad"], r16["grad"]
+    rel = (g32 - g16).norm() / g32.norm()
+    assert rel.item() < 0.05, rel.item()
+    assert b16.hip._ws["psi"].dtype == torch.int32          # 4 bytes per amplitude
