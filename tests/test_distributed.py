@@ -56,3 +56,22 @@ def test_gloo_three_ranks_uneven_shards(tmp_path):
     single = run_experiment(small_cfg(**kw))
     three = _run(3, kw, tmp_path)
     assert torch.allclose(three["params"], single["params"], atol=1e-6)
+
+
+def test_gloo_four_ranks_bitwise_rank_invariant(tmp_path):
+    """Exact fixed-point aggregation: 4 ranks reproduce the single-process model BITWISE
+    (SURVEY §7.3 item 10), including client sampling and DP noise keyed by client."""
+    from qfedx_amd.api import run_experiment
+    kw = dict(num_rounds=3, num_clients=8, client_fraction=0.75, dp=True, noise_multiplier=0.3)
+    single = run_experiment(small_cfg(**kw))
+    four = _run(4, kw, tmp_path)
+    assert torch.equal(four["params"], single["params"])
+
+
+def test_cfed_two_ranks_match_single_process(tmp_path):
+    from qfedx_amd.api import run_experiment
+    kw = {"model.kind": "tinycnn", "num_rounds": 2, "num_clients": 4, "samples_per_client": 32, "batch_size": 16,
+          "optimizer": "sgd", "learning_rate": 0.05, "test_samples": 64}
+    single = run_experiment(small_cfg(**kw))
+    two = _run(2, kw, tmp_path)
+    assert torch.allclose(two["params"], single["params"], atol=1e-6)

@@ -138,3 +138,27 @@ def test_metrics_jsonl(tmp_path):
     rounds = [r for r in recs if "round" in r]
     assert recs[0]["event"] == "config" and rounds[-1]["round"] == 2 and "test_acc" in rounds[-1]
     assert recs[-1].get("final") and 0.0 <= recs[-1]["test_auc"] <= 1.0
+
+
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=30, deadline=None)
+@given(st.integers(2, 9), st.integers(0, 2 ** 31 - 1), st.integers(1, 8))
+def test_exact_aggregation_permutation_and_split_invariant(K, seed, split):
+    """Fixed-point FedAvg: the aggregate is bitwise identical for any client order and any split of
+    the clients over ranks (the property that makes results independent of the GPU count)."""
+    g = torch.Generator().manual_seed(seed)
+    P = 17
+    tg = torch.randn(P, generator=g)
+    tk = tg + torch.randn(K, P, generator=g) * 0.3
+    w = torch.rand(K, generator=g, dtype=torch.float64) * 10 + 0.1
+    ids = list(range(K))
+    agg = Aggregator(P, torch.ones(P), "cpu", wrap=True)
+    full = agg.local_reduce(tk, tg, w, 0, ids)
+    perm = torch.randperm(K, generator=g)
+    permuted = agg.local_reduce(tk[perm], tg, w[perm], 0, [ids[i] for i in perm.tolist()])
+    cut = split % K
+    parts = agg.local_reduce(tk[:cut], tg, w[:cut], 0, ids[:cut]) if cut else torch.zeros_like(full)
+    parts = parts + agg.local_reduce(tk[cut:], tg, w[cut:], 0, ids[cut:])
+    assert torch.equal(full, permuted) and torch.equal(full, parts)
