@@ -57,7 +57,8 @@ int qfx_launch_readout_noise(float* expz, int C, int spc, long n_samples, float 
 int qfx_launch_philox_uniform(const long long* keys, int K, long n, unsigned stream, float* out, hipStream_t st);
 int qfx_launch_readout_sum(const float* part, int tps, int C, long n_samples, float* expz, hipStream_t st);
 int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob, float* grad,
-                           int p_stride, hipStream_t st);
+                           int p_stride, float* gpart, hipStream_t st);
+int qfx_grad_split(int tps, int spc);
 int qfx_launch_adam(float* p, const float* g, float* m, float* v, float* t, const float* active, int K, int P,
                     float lr, float b1, float b2, float eps, hipStream_t st);
 int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, const float* active, int K, int P, float lr,
@@ -168,13 +169,17 @@ void readout_sum(torch::Tensor part, int64_t tps, int64_t C, int64_t n_samples, 
         "qfx_readout_sum");
 }
 
+int64_t grad_split(int64_t tps, int64_t spc) { return qfx_grad_split((int)tps, (int)spc); }
+
 void grad_reduce(torch::Tensor slab, int64_t tps, int64_t spc, int64_t K, int64_t G, torch::Tensor blob,
-                 torch::Tensor grad) {
+                 torch::Tensor grad, torch::Tensor gpart) {
   need(slab, torch::kFloat32, "slab");
   need(grad, torch::kFloat32, "grad");
+  need(gpart, torch::kFloat32, "gpart");
   if (slab.numel() < K * spc * tps * G) throw std::invalid_argument("grad slab too small");
+  if (gpart.numel() < K * grad_split(tps, spc) * G) throw std::invalid_argument("gpart too small");
   check(qfx_launch_grad_reduce(ptr<float>(slab), (int)tps, (int)spc, (int)K, (int)G, ptr<int>(blob),
-                               ptr<float>(grad), (int)grad.size(1), cur_stream()),
+                               ptr<float>(grad), (int)grad.size(1), ptr<float>(gpart), cur_stream()),
         "qfx_grad_reduce");
 }
 
@@ -267,6 +272,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("readout_noise", &readout_noise);
   m.def("philox_uniform", &philox_uniform);
   m.def("grad_reduce", &grad_reduce);
+  m.def("grad_split", &grad_split);
   m.def("adam", &adam);
   m.def("sgdm", &sgdm);
   m.def("fedavg", &fedavg);

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstdio>
@@ -104,6 +105,16 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
   }
   const int NG = std::max<int>(1, (int)used.size());
   const int NGR = (int)grad_gates.size();
+  // forward fused 1-qubit groups: with one tile per wave or more (T >= 64) their 2x2 products are
+  // tile-uniform, so they are built once per tile in LDS (gtab) instead of by every lane
+  std::vector<std::vector<int>> fgroups;
+  if (!adjoint)
+    for (int i = 0; i < nops; ++i) {
+      const int* o = ops + i * OP_WORDS;
+      if (o[0] == OP_G1) fgroups.emplace_back(blob.begin() + o[3], blob.begin() + o[3] + o[2]);
+    }
+  const int NG1 = (int)fgroups.size();
+  const bool use_gtab = use_tab && NG1 > 0;
 
   auto pbit_expr = [&](int phys, const std::string& r) -> std::string {
     if (phys < RB) return "((" + r + " >> " + std::to_string(phys) + ") & 1)";
@@ -173,7 +184,8 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
   s << "  float* gacc = red + 128;\n";
   s << "  v2f* ctab = reinterpret_cast<v2f*>(gacc + " << gacc_words << ");\n";
   s << "  float4* vtab = reinterpret_cast<float4*>(ctab + " << ((TPB * NG + 1) & ~1) << ");\n";
-  s << "  (void)xb; (void)red; (void)gacc; (void)ctab; (void)vtab;\n";
+  s << "  M2* gtab = reinterpret_cast<M2*>(vtab + " << TPB * n << ");\n";
+  s << "  (void)xb; (void)red; (void)gacc; (void)ctab; (void)vtab; (void)gtab;\n";
   if (use_tab) {
     s << "  {\n    const long tile0 = (long)blockIdx.x * TPB;\n";
     s << "    static constexpr int USED[" << NG << "] = {";
@@ -191,7 +203,23 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
       s << "      vtab[e] = prefix_vec((cint_p)(A.blob), q, A.params + (size_t)(sm / A.spc) * A.p_stride, A.xang + (size_t)sm * A.x_stride, "
         << n_theta << ");\n    }\n";
     }
-    s << "    __syncthreads();\n  }\n";
+    s << "    __syncthreads();\n";
+    if (use_gtab) {
+      s << "    for (int e = tid; e < TPB * " << NG1 << "; e += 256) {\n";
+      s << "      const int tb_ = e / " << NG1 << ", i = e - tb_ * " << NG1 << ";\n";
+      s << "      M2 m;\n      switch (i) {\n";
+      for (int gi = 0; gi < NG1; ++gi) {
+        const auto& gl = fgroups[gi];
+        auto csx = [&](int g) { return "ctab[tb_ * " + std::to_string(NG) + " + " + std::to_string(slot_of[g]) + "]"; };
+        s << "        case " << gi << ": m = gate_m2(" << kind_name(gkind(gl[0])) << ", " << csx(gl[0]) << ", false);";
+        for (size_t j = 1; j < gl.size(); ++j)
+          s << " m = m2mul(gate_m2(" << kind_name(gkind(gl[j])) << ", " << csx(gl[j]) << ", false), m);";
+        s << " break;\n";
+      }
+      s << "        default: m = gate_m2(K_X, mk(0.f, 0.f), false); break;\n      }\n";
+      s << "      gtab[e] = m;\n    }\n    __syncthreads();\n";
+    }
+    s << "  }\n";
   }
   s << "  v2f a[R];\n  v2f l[R];\n";
   s << "#pragma unroll\n  for (int r = 0; r < R; ++r) { a[r] = mk(0.f, 0.f); l[r] = mk(0.f, 0.f); }\n";
@@ -251,6 +279,7 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
 
   // ---------------------------------------------------------------- ops
   int gi_local = 0;
+  int g1_idx = 0;
   auto emit_grad = [&](int g, const std::string& part) {
     // row-local DPP sum; tiles wider than a 16-lane row park one partial per row in LDS and
     // are summed once at the end of the kernel
@@ -264,7 +293,9 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
     const int code = o[0], oa = o[1], ob = o[2], oc = o[3];
     if (code == OP_G1) {
       std::vector<int> gl(blob.begin() + oc, blob.begin() + oc + ob);
-      if (!adjoint) {
+      if (!adjoint && use_gtab) {
+        s << "  { const M2 m = gtab[tib * " << NG1 << " + " << g1_idx++ << "]; m2_apply<R, " << oa << ">(a, m); }\n";
+      } else if (!adjoint) {
         s << "  { M2 m = gate_m2(" << kind_name(gkind(gl[0])) << ", " << cs(gl[0]) << ", false);\n";
         for (size_t j = 1; j < gl.size(); ++j)
           s << "    m = m2mul(gate_m2(" << kind_name(gkind(gl[j])) << ", " << cs(gl[j]) << ", false), m);\n";
@@ -302,12 +333,35 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
       const int* rt = tab + 2 * R + tb;
       s << "  { const uint32_t wthr = " << xor_expr(wt, tb) << ";\n";
       s << "    const uint32_t rthr = " << xor_expr(rt, tb) << ";\n";
+      // slot(r) = C_r ^ thr where thr only has bits in M = OR of the thread contributions: bits of C_r
+      // outside M are ADDED (disjoint), so they become ds immediate offsets; one XOR per distinct
+      // (C_r & M) pattern builds a base pointer instead of one XOR + shift-add per access
+      auto bases = [&](const int* tc, const int* tt, const char* thr, const char* pre) {
+        uint32_t M = 0;
+        for (int j = 0; j < tb; ++j) M |= (uint32_t)tt[j];
+        std::vector<std::pair<uint32_t, std::string>> ref(R);
+        std::vector<uint32_t> seen;
+        for (int r = 0; r < R; ++r) {
+          const uint32_t lo = (uint32_t)tc[r] & M, hi = (uint32_t)tc[r] & ~M;
+          size_t id = std::find(seen.begin(), seen.end(), lo) - seen.begin();
+          if (id == seen.size()) {
+            seen.push_back(lo);
+            s << "    v2f* " << pre << id << " = xb + (" << lo << "u ^ " << thr << ");\n";
+          }
+          ref[r] = {hi, std::string(pre) + std::to_string(id)};
+        }
+        return ref;
+      };
+      const auto wref = bases(wr, wt, "wthr", "wb");
+      const auto rref = bases(rr, rt, "rthr", "rb");
       const char* arrs[2] = {"a", "l"};
       for (int st = 0; st < (adjoint ? 2 : 1); ++st) {
         s << "    __syncthreads();\n";
-        for (int r = 0; r < R; ++r) s << "    xb[" << (uint32_t)wr[r] << "u ^ wthr] = " << arrs[st] << "[" << r << "];\n";
+        for (int r = 0; r < R; ++r)
+          s << "    " << wref[r].second << "[" << wref[r].first << "u] = " << arrs[st] << "[" << r << "];\n";
         s << "    __syncthreads();\n";
-        for (int r = 0; r < R; ++r) s << "    " << arrs[st] << "[" << r << "] = xb[" << (uint32_t)rr[r] << "u ^ rthr];\n";
+        for (int r = 0; r < R; ++r)
+          s << "    " << arrs[st] << "[" << r << "] = " << rref[r].second << "[" << rref[r].first << "u];\n";
       }
       s << "  }\n";
     } else if (code == OP_CX) {
@@ -373,7 +427,8 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
   spec.k = k;
   spec.n = n;
   spec.lds = 256 * (size_t)R * 8 + 128 * 4 + (size_t)gacc_words * 4 +
-             (use_tab ? (size_t)((TPB * NG + 1) & ~1) * 8 + (size_t)TPB * n * 16 : 0);
+             (use_tab ? (size_t)((TPB * NG + 1) & ~1) * 8 + (size_t)TPB * n * 16 : 0) +
+             (use_gtab ? (size_t)TPB * NG1 * 32 : 0);
   return spec;
 }
 

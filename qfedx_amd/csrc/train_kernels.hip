@@ -149,24 +149,43 @@ __global__ void qfx_readout_sum_kernel(const float* __restrict__ part, int tps, 
   expz[i] = t;
 }
 
-// one block per client: grad[k][slot] = sum_{samples of k, tiles} sum_{gates g with slot} scale_g * slab
-__global__ void __launch_bounds__(256) qfx_grad_reduce_kernel(
-    const float* __restrict__ slab, int tps, int spc, const int* __restrict__ blob,
-    float* __restrict__ grad, int p_stride) {
+// gradient reduction, stage 1: gpart[k][rs][g] = sum of slab rows of client k in row-split rs, for 64
+// gates per block (threads: 64 gates x 4 row lanes, coalesced over gates), fixed-order LDS combine
+constexpr int GR_SPLIT_MAX = 16;
+__global__ void __launch_bounds__(256) qfx_grad_partial_kernel(const float* __restrict__ slab, long rows, int G,
+                                                               int RS, float* __restrict__ gpart) {
+  __shared__ float sm[256];
+  const int k = blockIdx.x, rs = blockIdx.z;
+  const int gl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int g = blockIdx.y * 64 + gl;
+  const long chunk = (rows + RS - 1) / RS;
+  const long r0 = (long)rs * chunk, r1 = min(rows, r0 + chunk);
+  float acc = 0.f;
+  if (g < G) {
+    const float* base = slab + (size_t)k * rows * G + g;
+    for (long r = r0 + rl; r < r1; r += 4) acc += base[(size_t)r * G];
+  }
+  sm[threadIdx.x] = acc;
+  __syncthreads();
+  if (rl == 0 && g < G) gpart[((size_t)k * RS + rs) * G + g] = sm[gl] + sm[64 + gl] + sm[128 + gl] + sm[192 + gl];
+}
+
+// stage 2, one block per client: gsum[g] = sum_rs gpart (fixed order) for gradient gates, then
+// grad[k][slot] = sum_{gates g of slot} scale_g * gsum[g]
+__global__ void __launch_bounds__(256) qfx_grad_slots_kernel(const float* __restrict__ gpart, int RS,
+                                                             const int* __restrict__ blob, float* __restrict__ grad,
+                                                             int p_stride) {
   extern __shared__ float gsum[];
   const int k = blockIdx.x;
   const int G = blob[HF_NGATES];
   const int n_theta = blob[HF_NTHETA];
   const int* gt = blob + blob[HF_GATES];
-  const long rows = (long)spc * tps;
-  const size_t row0 = (size_t)k * rows;
   for (int g = threadIdx.x; g < G; g += 256) {
     const int kind = gt[g * GATE_WORDS];
     const int slot = gt[g * GATE_WORDS + 3];
     float s = 0.f;
-    if (slot >= 0 && slot < n_theta && kind <= K_P) {
-      for (long r = 0; r < rows; ++r) s += slab[(row0 + r) * G + g];
-    }
+    if (slot >= 0 && slot < n_theta && kind <= K_P)
+      for (int r = 0; r < RS; ++r) s += gpart[((size_t)k * RS + r) * G + g];
     gsum[g] = s;
   }
   __syncthreads();
@@ -318,10 +337,19 @@ extern "C" int qfx_launch_readout_sum(const float* part, int tps, int C, long n_
   return (int)hipGetLastError();
 }
 
+// rows per client = spc * tps; the row split keeps >= ~64 rows per block and the grid >= a few hundred blocks
+extern "C" int qfx_grad_split(int tps, int spc) {
+  const long rows = (long)tps * spc;
+  return (int)max(1L, min((long)GR_SPLIT_MAX, rows / 64));
+}
+
 extern "C" int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob,
-                                      float* grad, int p_stride, hipStream_t st) {
-  hipLaunchKernelGGL(qfx_grad_reduce_kernel, dim3(K), dim3(256), (size_t)G * sizeof(float), st, slab, tps,
-                     spc, blob, grad, p_stride);
+                                      float* grad, int p_stride, float* gpart, hipStream_t st) {
+  const long rows = (long)tps * spc;
+  const int RS = qfx_grad_split(tps, spc);
+  hipLaunchKernelGGL(qfx_grad_partial_kernel, dim3(K, (G + 63) / 64, RS), dim3(256), 0, st, slab, rows, G, RS, gpart);
+  hipLaunchKernelGGL(qfx_grad_slots_kernel, dim3(K), dim3(256), (size_t)G * sizeof(float), st, gpart, RS, blob, grad,
+                     p_stride);
   return (int)hipGetLastError();
 }
 

@@ -180,5 +180,6 @@ class HipProgram:
             C.readout_ce(part, tr.tiles_per_state, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
                          correct, grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
         self._run_passes(adj, True, psi, lam, p, B, x, wread, None, slab, S)
-        C.grad_reduce(slab, adj.tiles_per_state, B, K, self.G, adj.blob, grad)
+        gpart = self._buf("gpart", K * C.grad_split(adj.tiles_per_state, B) * self.G, torch.float32)
+        C.grad_reduce(slab, adj.tiles_per_state, B, K, self.G, adj.blob, grad, gpart)
         return {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}
