@@ -59,6 +59,9 @@ int qfx_launch_readout_sum(const float* part, int tps, int C, long n_samples, fl
 int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob, float* grad,
                            int p_stride, float* gpart, hipStream_t st);
 int qfx_grad_split(int tps, int spc);
+int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct, const float* nvalid,
+                          const float* act, int n, double samples, double steps, hipStream_t st);
+int qfx_launch_round_apply(const long long* buf, int P, float* theta, double lr, double* out, hipStream_t st);
 int qfx_launch_adam(float* p, const float* g, float* m, float* v, float* t, const float* active, int K, int P,
                     float lr, float b1, float b2, float eps, hipStream_t st);
 int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, const float* active, int K, int P, float lr,
@@ -171,6 +174,27 @@ void readout_sum(torch::Tensor part, int64_t tps, int64_t C, int64_t n_samples, 
 
 int64_t grad_split(int64_t tps, int64_t spc) { return qfx_grad_split((int)tps, (int)spc); }
 
+void round_pack(torch::Tensor buf, int64_t P, torch::Tensor loss, torch::Tensor correct, torch::Tensor nvalid,
+                torch::Tensor act, double samples, double steps) {
+  need(buf, torch::kInt64, "buf");
+  for (auto* x : {&loss, &correct, &nvalid, &act}) need(*x, torch::kFloat32, "round_pack metric");
+  const int64_t n = loss.numel();
+  if (buf.numel() < P + 5 || correct.numel() < n || nvalid.numel() < n || act.numel() < n)
+    throw std::invalid_argument("round_pack: sizes");
+  check(qfx_launch_round_pack(ptr<long long>(buf), (int)P, ptr<float>(loss), ptr<float>(correct), ptr<float>(nvalid),
+                              ptr<float>(act), (int)n, samples, steps, cur_stream()),
+        "qfx_round_pack");
+}
+
+void round_apply(torch::Tensor buf, int64_t P, torch::Tensor theta, double lr, torch::Tensor out) {
+  need(buf, torch::kInt64, "buf");
+  need(theta, torch::kFloat32, "theta");
+  need(out, torch::kFloat64, "out");
+  if (buf.numel() < P + 5 || theta.numel() < P || out.numel() < 5) throw std::invalid_argument("round_apply: sizes");
+  check(qfx_launch_round_apply(ptr<long long>(buf), (int)P, ptr<float>(theta), lr, ptr<double>(out), cur_stream()),
+        "qfx_round_apply");
+}
+
 void grad_reduce(torch::Tensor slab, int64_t tps, int64_t spc, int64_t K, int64_t G, torch::Tensor blob,
                  torch::Tensor grad, torch::Tensor gpart) {
   need(slab, torch::kFloat32, "slab");
@@ -273,6 +297,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("philox_uniform", &philox_uniform);
   m.def("grad_reduce", &grad_reduce);
   m.def("grad_split", &grad_split);
+  m.def("round_pack", &round_pack);
+  m.def("round_apply", &round_apply);
   m.def("adam", &adam);
   m.def("sgdm", &sgdm);
   m.def("fedavg", &fedavg);

@@ -294,9 +294,59 @@ __global__ void qfx_fedavg_reduce_kernel(
   out[e] = acc;
 }
 
+// round epilogue 1: metrics -> exact fixed point in the all-reduce buffer tail, fixed summation order
+//   buf[P+1..P+4] = round(2^32 * [sum loss*nvalid, sum correct*act, samples, steps])
+__global__ void qfx_round_pack_kernel(long long* __restrict__ buf, int P, const float* __restrict__ loss,
+                                      const float* __restrict__ correct, const float* __restrict__ nvalid,
+                                      const float* __restrict__ act, int n, double samples, double steps) {
+  if (threadIdx.x != 0) return;
+  double ls = 0.0, cs = 0.0;
+  for (int i = 0; i < n; ++i) {
+    ls += (double)loss[i] * (double)nvalid[i];
+    cs += (double)correct[i] * (double)act[i];
+  }
+  const double SC = 4294967296.0;
+  buf[P + 1] = llrint(ls * SC);
+  buf[P + 2] = llrint(cs * SC);
+  buf[P + 3] = llrint(samples * SC);
+  buf[P + 4] = llrint(steps * SC);
+}
+
+// round epilogue 2 (after the all-reduce): theta += lr * (sum w Delta) / (sum w) in float64, rounded to
+// fp32 - the same operations as Aggregator.finalize + apply; rounds with zero total weight keep theta.
+//   out[0..3] = metrics, out[4] = weight sum
+__global__ void qfx_round_apply_kernel(const long long* __restrict__ buf, int P, float* __restrict__ theta, double lr,
+                                       double* __restrict__ out) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const double SC = 4294967296.0;
+  const double wsum = (double)buf[P] / SC;
+  if (e < P) {
+    const double mean = ((double)buf[e] / SC) / fmax(wsum, 1e-300);
+    const double th = (double)theta[e];
+    theta[e] = wsum > 0.0 ? (float)(th + lr * mean) : (float)th;
+  } else if (e < P + 5) {
+    const int j = (int)(e - P);
+    out[j] = j < 4 ? (double)buf[P + 1 + j] / SC : wsum;
+  }
+}
+
 }  // namespace qfx
 
 using namespace qfx;
+
+extern "C" int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct,
+                                     const float* nvalid, const float* act, int n, double samples, double steps,
+                                     hipStream_t st) {
+  hipLaunchKernelGGL(qfx_round_pack_kernel, dim3(1), dim3(64), 0, st, buf, P, loss, correct, nvalid, act, n, samples,
+                     steps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_launch_round_apply(const long long* buf, int P, float* theta, double lr, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(qfx_round_apply_kernel, dim3((unsigned)((P + 5 + 255) / 256)), dim3(256), 0, st, buf, P, theta,
+                     lr, out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int qfx_launch_readout_ce(const float* part, int tps, int C, int spc, int K, const long long* y,
                                      const float* wts, const float* params, int p_stride, int n_theta,

@@ -14,6 +14,7 @@ import torch.nn.functional as F
 
 from ..models import tinycnn as tc
 from .optim import BatchedOptimizer
+from ..utils.device import PackedUpload
 from .trainer import BatchPlan, ShardStore
 
 
@@ -40,39 +41,42 @@ class CNNClientTrainer:
         return {"loss": loss.detach(), "grad": p.grad, "correct": correct}
 
     def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int) -> dict:
+        """Same contract as ``VQCClientTrainer.run_round`` (per-step [S,K] loss/correct round buffers)."""
         cfg = self.cfg
         K = len(local_idx)
         P = theta_g.numel()
         if K == 0:
-            return {"params": torch.zeros(0, P, device=self.device), "loss_sum": 0.0, "correct": 0.0,
-                    "samples": 0.0, "steps": 0}
+            z = torch.zeros(0, 0, device=self.device)
+            return {"params": torch.zeros(0, P, device=self.device), "loss": z, "correct": z, "nvalid": z, "act": z,
+                    "lid": torch.zeros(0, dtype=torch.int64, device=self.device), "samples": 0.0, "steps": 0,
+                    "client_ids": [], "n_samples": torch.zeros(0, dtype=torch.float64)}
         li = torch.tensor(local_idx, dtype=torch.int64)
         cids = [store.client_ids[i] for i in local_idx]
         plan = BatchPlan(store.counts[li], cids, cfg.batch_size, round_num, cfg.seed, cfg.local_epochs,
                          cfg.local_steps)
+        nvalid = (plan.wts > 0).sum(-1).float() * plan.active
+        dv = PackedUpload({"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active,
+                           "nvalid": nvalid}).to_device(self.device)
         params = theta_g.to(self.device).float()[None, :].repeat(K, 1).contiguous()
         opt = BatchedOptimizer(cfg.optimizer if cfg.optimizer != "spsa" else "sgd", (K, P), self.device,
                                cfg.learning_rate, cfg.momentum, backend=self.backend)
-        X = store.X[li.to(store.X.device)]
-        Y = store.y[li.to(store.y.device)]
-        idx_d, wts_d, act_d = plan.idx.to(self.device), plan.wts.to(self.device), plan.active.to(self.device)
+        X = store.X[dv["lid"]]
+        Y = store.y[dv["lid"]]
         kar = torch.arange(K, device=self.device)[:, None]
-        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
-        correct = torch.zeros((), dtype=torch.float64, device=self.device)
-        samples = 0.0
-        for s in range(plan.max_steps):
-            xb = X[kar, idx_d[s]]
-            yb = Y[kar, idx_d[s]]
+        S = plan.max_steps
+        loss_all = torch.empty(S, K, dtype=torch.float32, device=self.device)
+        correct_all = torch.empty(S, K, dtype=torch.float32, device=self.device)
+        for s in range(S):
+            xb = X[kar, dv["idx"][s]]
+            yb = Y[kar, dv["idx"][s]]
             mask = tc.dropout_masks(cids, cfg.batch_size, cfg.seed, round_num, s, self.device)
-            res = self.loss_and_grads(params, xb, yb, wts_d[s], mask)
-            opt.step(params, res["grad"], act_d[s])
-            nvalid = (wts_d[s] > 0).sum(-1).double() * act_d[s].double()
-            loss_sum += (res["loss"].double() * nvalid).sum()
-            correct += (res["correct"].double() * act_d[s].double()).sum()
-            samples += float((plan.wts[s] > 0).sum())
-        return {"params": params, "loss_sum": loss_sum, "correct": correct, "samples": samples,
-                "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
-                "n_samples": store.counts[li].to(torch.float64)}
+            res = self.loss_and_grads(params, xb, yb, dv["wts"][s], mask)
+            opt.step(params, res["grad"], dv["act"][s])
+            loss_all[s].copy_(res["loss"])
+            correct_all[s].copy_(res["correct"])
+        return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
+                "lid": dv["lid"], "samples": float(nvalid.sum()), "steps": int(sum(plan.steps_per_client)),
+                "client_ids": cids, "n_samples": store.counts[li].to(torch.float64)}
 
 
 class TinyCNNAdapter:

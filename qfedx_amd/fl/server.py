@@ -159,38 +159,64 @@ class FederatedRunner:
         local_alive = [i for i in local_part if self.local_ids[i] not in dropped_set]
         t0 = time.perf_counter()
         dev = self.device
+        P = self.P
         with self.timer.phase("local_train"):
             res = self.adapter.trainer.run_round(self.store, local_alive, self.params, r)
+        ids = [self.local_ids[i] for i in local_alive]
+        fast = self.backend == "hip" and not p.secure_agg
         with self.timer.phase("aggregate"):
-            if local_alive:
-                if t.weighting == "uniform":
-                    w = torch.ones(len(local_alive), dtype=torch.float64)
-                else:
-                    w = res["n_samples"].double()
-                contrib = self.aggregator.local_reduce(
-                    res["params"], self.params, h2d(w, dev), r,
-                    [self.local_ids[i] for i in local_alive],
-                    participants=[c for c in participants], dropped=dropped)
+            if t.weighting == "uniform":
+                w = torch.ones(len(local_alive), dtype=torch.float64, device=dev)
             else:
-                contrib = torch.zeros(self.P + 1, dtype=torch.int64, device=dev)
-            dev_m = torch.stack([torch.as_tensor(res.get("loss_sum", 0.0), dtype=torch.float64).to(dev),
-                                 torch.as_tensor(res.get("correct", 0.0), dtype=torch.float64).to(dev)])
-            host_m = h2d(torch.tensor([float(res.get("samples", 0.0)), float(res.get("steps", 0))],
-                                      dtype=torch.float64), dev)
-            metrics = torch.cat([dev_m, host_m])
+                if getattr(self, "_counts_dev", None) is None:
+                    self._counts_dev = self.store.counts.to(torch.float64).to(dev)
+                w = self._counts_dev[res["lid"]]
+            if fast:
+                # round epilogue on the device: fused local reduce writes the head of the all-reduce
+                # buffer, one kernel appends the fixed-point metrics (no host values, no extra copies)
+                if getattr(self, "_round_buf", None) is None:
+                    self._round_buf = torch.zeros(P + 5, dtype=torch.int64, device=dev)
+                buf = self._round_buf
+                if local_alive:
+                    self.aggregator.local_reduce(res["params"], self.params, w, r, ids, participants=participants,
+                                                 dropped=dropped, out=buf[: P + 1])
+                    from ..ops._ext import ext
+                    ext().round_pack(buf, P, res["loss"].reshape(-1), res["correct"].reshape(-1),
+                                     res["nvalid"].reshape(-1), res["act"].reshape(-1), float(res["samples"]),
+                                     float(res["steps"]))
+                else:
+                    buf.zero_()
+            else:
+                if local_alive:
+                    contrib = self.aggregator.local_reduce(res["params"], self.params, w, r, ids,
+                                                           participants=participants, dropped=dropped)
+                else:
+                    contrib = torch.zeros(P + 1, dtype=torch.int64, device=dev)
+                loss_sum = (res["loss"].double() * res["nvalid"].double()).sum()
+                correct = (res["correct"].double() * res["act"].double()).sum()
+                host_m = h2d(torch.tensor([float(res.get("samples", 0.0)), float(res.get("steps", 0))],
+                                          dtype=torch.float64), dev)
+                metrics = torch.cat([torch.stack([loss_sum, correct]).to(dev), host_m])
         with self.timer.phase("comm"):
-            if p.secure_agg:
+            if fast:
+                all_reduce_(buf, self.world)              # ONE collective per round (CC2+CC3)
+                out = torch.empty(5, dtype=torch.float64, device=dev)
+                from ..ops._ext import ext
+                ext().round_apply(buf, P, self.params, 1.0, out)   # finalize + apply, in place
+                metrics = out[:4]
+            elif p.secure_agg:
                 all_reduce_(contrib, self.world)          # int64 ring elements: exact, mod later
                 all_reduce_(metrics, self.world)
                 mean_upd, wsum = self.aggregator.finalize(contrib)
+                self.params = self.aggregator.apply(self.params, mean_upd, wsum=wsum)
             else:
                 # ONE collective per round (CC2+CC3): [exact fixed-point update | weight | metrics]
                 buf = torch.cat([contrib.to(torch.int64),
                                  torch.round(metrics.double() * EXACT_SCALE).to(torch.int64)])
                 all_reduce_(buf, self.world)
-                mean_upd, wsum = self.aggregator.finalize(buf[: self.P + 1])
-                metrics = buf[self.P + 1:].double() / EXACT_SCALE
-        self.params = self.aggregator.apply(self.params, mean_upd, wsum=wsum)
+                mean_upd, wsum = self.aggregator.finalize(buf[: P + 1])
+                metrics = buf[P + 1:].double() / EXACT_SCALE
+                self.params = self.aggregator.apply(self.params, mean_upd, wsum=wsum)
         if p.dp:
             q = len(participants) / self.num_clients
             self.accountant.step(q, p.noise_multiplier, 1)

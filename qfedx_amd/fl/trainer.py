@@ -16,7 +16,7 @@ from typing import Optional
 
 import torch
 
-from ..utils.device import h2d
+from ..utils.device import PackedUpload, h2d
 from ..utils.seeding import generator
 from .optim import BatchedOptimizer
 
@@ -113,10 +113,13 @@ class VQCClientTrainer:
 
     def _body(self, Xs, ys, theta, idx_d, wts_d, act_d, steps: int, round_num: int, method: str,
               traj_keys=None, ro_keys=None):
-        """Device work of one round (capturable): local steps of all clients + metrics.
+        """Device work of one round (capturable): local steps of all clients.
 
-        With a noise model, every sample runs ``trajectories`` Pauli-trajectory replicas (loss weights
-        split evenly) and the readout is confused / shot-sampled, all keyed per client and step."""
+        Returns (params [K,P], loss [S,K], correct [S,K]): per-step, per-client weighted loss and hit
+        counts are written straight into round buffers by the readout kernel (no per-step metric ops);
+        the round epilogue reduces them.  With a noise model, every sample runs ``trajectories``
+        Pauli-trajectory replicas (loss weights split evenly) and the readout is confused /
+        shot-sampled, all keyed per client and step."""
         cfg = self.cfg
         noise = self.engine.noise
         T = noise.trajectories if (noise is not None and noise.gate_noise) else 1
@@ -126,8 +129,8 @@ class VQCClientTrainer:
         opt_kind = "sgd" if cfg.optimizer == "spsa" else cfg.optimizer
         opt = BatchedOptimizer(opt_kind, (K, P), self.device, cfg.learning_rate, cfg.momentum,
                                backend=self.backend)
-        loss_sum = torch.zeros((), dtype=torch.float64, device=self.device)
-        correct = torch.zeros((), dtype=torch.float64, device=self.device)
+        loss_all = torch.empty(steps, K, dtype=torch.float32, device=self.device)
+        correct_all = torch.empty(steps, K, dtype=torch.float32, device=self.device)
         kar = torch.arange(K, device=self.device)[:, None]
         for s in range(steps):
             bi = idx_d[s]
@@ -139,73 +142,77 @@ class VQCClientTrainer:
             yb = ys[kar, bi]
             xang = self.engine.augment(self.encode(xb), traj_keys, s)
             res = self.engine.loss_and_grads(xang, yb, ws, params, method, rng_keys=(cfg.seed, round_num, s),
-                                             readout_keys=ro_keys, step=s)
+                                             readout_keys=ro_keys, step=s, out_loss=loss_all[s],
+                                             out_correct=correct_all[s])
             opt.step(params, res["grad"], act_d[s])
-            nvalid = (wts_d[s] > 0).sum(-1).double() * act_d[s].double()
-            loss_sum += (res["loss"].double() * nvalid).sum()
-            correct += (res["correct"].double() * act_d[s].double()).sum()
-        return params, loss_sum, correct
+        return params, loss_all, correct_all
 
     def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int) -> dict:
-        """Train clients ``store[local_idx]`` from the global params; returns their params + metrics."""
+        """Train clients ``store[local_idx]`` from the global params.
+
+        Returns device tensors: ``params`` [K,P], ``loss`` / ``correct`` [S,K] per step, ``nvalid`` /
+        ``act`` [S,K] (valid samples / active flag per client and step), ``lid`` [K] (store slots), plus
+        host scalars ``samples`` / ``steps`` and ``n_samples`` (cpu, for weighting)."""
         cfg = self.cfg
         K = len(local_idx)
         P = theta_g.numel()
         if K == 0:
-            return {"params": torch.zeros(0, P, device=self.device), "loss_sum": 0.0, "correct": 0.0,
-                    "samples": 0.0, "steps": 0}
+            z = torch.zeros(0, 0, device=self.device)
+            return {"params": torch.zeros(0, P, device=self.device), "loss": z, "correct": z, "nvalid": z, "act": z,
+                    "lid": torch.zeros(0, dtype=torch.int64, device=self.device), "samples": 0.0, "steps": 0,
+                    "client_ids": [], "n_samples": torch.zeros(0, dtype=torch.float64)}
         li = torch.tensor(local_idx, dtype=torch.int64)
         cids = [store.client_ids[i] for i in local_idx]
         plan = BatchPlan(store.counts[li], cids, cfg.batch_size, round_num, cfg.seed,
                          cfg.local_epochs, cfg.local_steps)
         method = "spsa" if cfg.optimizer == "spsa" else cfg.grad_method
-        samples = float((plan.wts > 0).sum())
-        common = {"samples": samples, "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
+        nvalid = (plan.wts > 0).sum(-1).float() * plan.active
+        common = {"samples": float(nvalid.sum()), "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
                   "n_samples": store.counts[li].to(torch.float64)}
+        up = PackedUpload({"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid})
         noise = self.engine.noise
         traj_keys = ro_keys = None
         if noise is not None:
             traj_keys = noise.client_keys("noise_traj", round_num, cids, self.device)
             ro_keys = noise.client_keys("shots", round_num, cids, self.device)
         if self.use_graph and method == "adjoint" and noise is None:
-            params, loss_sum, correct = self._graphed(store, local_idx, li, theta_g, plan, round_num)
+            params, loss_all, correct_all, dv = self._graphed(store, up, theta_g, plan, round_num)
         else:
-            lid = h2d(li, store.X.device)
-            Xs = store.X[lid]
-            ys = store.y[lid]
-            params, loss_sum, correct = self._body(Xs, ys, theta_g.to(self.device), h2d(plan.idx, self.device),
-                                                   h2d(plan.wts, self.device), h2d(plan.active, self.device),
-                                                   plan.max_steps, round_num, method, traj_keys, ro_keys)
-        return {"params": params, "loss_sum": loss_sum, "correct": correct, **common}
+            dv = up.to_device(self.device)
+            Xs = store.X[dv["lid"]]
+            ys = store.y[dv["lid"]]
+            params, loss_all, correct_all = self._body(Xs, ys, theta_g.to(self.device), dv["idx"], dv["wts"], dv["act"],
+                                                       plan.max_steps, round_num, method, traj_keys, ro_keys)
+        return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
+                "lid": dv["lid"], **common}
 
     # ------------------------------------------------------------------ hipGraph capture
     @property
     def use_graph(self) -> bool:
         return self.backend == "hip" and self.device.type == "cuda" and getattr(self, "graphs", True)
 
-    def _graphed(self, store, local_idx, li, theta_g, plan, round_num):
+    def _graphed(self, store, up, theta_g, plan, round_num):
         """Replay the whole round as ONE hipGraph (static shapes: #clients, steps, batch).
 
-        Captured once per SHAPE, not per client set: the round's client shards are gathered on the
-        device into static buffers (client sampling changes the set every round), together with the
-        global params and the minibatch index tables; then ~15 launches per local step replay with no
+        Captured once per SHAPE, not per client set: each round ONE async copy refreshes the packed
+        static input buffer (client slots, minibatch indices, loss weights, step masks), the round's
+        client shards are gathered on the device into static buffers (client sampling changes the set
+        every round), the global params are copied in, and ~15 launches per local step replay with no
         host round trips.  A small LRU bounds the number of live graphs.
         """
-        K = len(local_idx)
+        K = up.layout[0][4][0]
         key = (K, plan.max_steps, plan.B, store.nmax)
         cache = self.__dict__.setdefault("_graph_cache", {})
         dev = self.device
-        lid = h2d(li, store.X.device)
         ent = cache.pop(key, None)
         if ent is None:
-            ent = {
-                "X": store.X[lid].contiguous(),
-                "y": store.y[lid].contiguous(),
-                "theta": theta_g.to(dev).float().clone(),
-                "idx": plan.idx.to(dev).clone(), "wts": plan.wts.to(dev).clone(), "act": plan.active.to(dev).clone(),
-            }
-            args = (ent["X"], ent["y"], ent["theta"], ent["idx"], ent["wts"], ent["act"], plan.max_steps,
-                    round_num, "adjoint")
+            pack = torch.empty(up.nbytes, dtype=torch.uint8, device=dev)
+            dv = up.to_device(dev, pack)
+            ent = {"pack": pack, "dv": dv,
+                   "X": store.X[dv["lid"]].contiguous(), "y": store.y[dv["lid"]].contiguous(),
+                   "theta": theta_g.to(dev).float().clone()}
+            args = (ent["X"], ent["y"], ent["theta"], dv["idx"], dv["wts"], dv["act"], plan.max_steps, round_num,
+                    "adjoint")
             # the graph owns its workspaces: eager calls (evaluation) can never regrow/free them
             ent["ws"] = {}
             with self.engine.hip.private_workspace(ent["ws"]):
@@ -221,12 +228,10 @@ class VQCClientTrainer:
             while len(cache) >= 4:                  # LRU: drop the oldest shape
                 cache.pop(next(iter(cache)))
         else:
-            torch.index_select(store.X, 0, lid, out=ent["X"])
-            torch.index_select(store.y, 0, lid, out=ent["y"])
+            dv = up.to_device(dev, ent["pack"])     # one H2D copy for all the round's tables
+            torch.index_select(store.X, 0, dv["lid"], out=ent["X"])
+            torch.index_select(store.y, 0, dv["lid"], out=ent["y"])
         cache[key] = ent                            # most recently used last
         ent["theta"].copy_(theta_g.float())
-        ent["idx"].copy_(h2d(plan.idx, self.device))
-        ent["wts"].copy_(h2d(plan.wts, self.device))
-        ent["act"].copy_(h2d(plan.active, self.device))
         ent["graph"].replay()
-        return ent["out"]
+        return (*ent["out"], ent["dv"])

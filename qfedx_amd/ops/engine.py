@@ -118,15 +118,29 @@ class VQCEngine:
     def loss_and_grads(self, xang: torch.Tensor, y: torch.Tensor, wmask: torch.Tensor,
                        params: torch.Tensor, method: str = "adjoint", spsa_c: float = 0.1,
                        rng_keys: tuple = (0,), readout_keys: Optional[torch.Tensor] = None,
-                       step: int = 0) -> dict:
+                       step: int = 0, out_loss: Optional[torch.Tensor] = None,
+                       out_correct: Optional[torch.Tensor] = None) -> dict:
+        """Loss [K], gradient [K,P], correct [K] for [K,B] minibatches.  ``out_loss`` / ``out_correct``
+        (optional [K] views, e.g. rows of a round buffer) receive the loss / hit counts in place."""
         spec = self.spec
         self._check(xang)
+        if self.backend == "hip" and method == "adjoint":
+            nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
+            return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step, out_loss, out_correct)
+        res = self._loss_and_grads(xang, y, wmask, params, method, spsa_c, rng_keys, readout_keys, step)
+        if out_loss is not None:
+            out_loss.copy_(res["loss"])
+            res["loss"] = out_loss
+        if out_correct is not None:
+            out_correct.copy_(res["correct"])
+            res["correct"] = out_correct
+        return res
+
+    def _loss_and_grads(self, xang, y, wmask, params, method, spsa_c, rng_keys, readout_keys, step) -> dict:
+        spec = self.spec
         th, a, b = spec.split(params)
         if method == "autograd":
             return self._autograd(xang, y, wmask, params)
-        if self.backend == "hip" and method == "adjoint":
-            nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
-            return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step)
         K, B, _ = xang.shape
         P = spec.n_theta
         with torch.no_grad():

@@ -18,18 +18,29 @@ def sgdm_step(params, grads, buf, active, lr, mu, t=None) -> None:
     ext().sgdm(params, grads.float().contiguous(), buf, t, active.float().contiguous(), lr, mu)
 
 
-def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp,
-                       clip_norm, noise_multiplier):
+_NO_KEYS = {}
+
+
+def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp, clip_norm,
+                       noise_multiplier, out=None):
     """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as exact int64 fixed point (scale 2^32)
-    [P+1] (per-client terms rounded before the sum -> rank-count invariant), plus norms [K]."""
+    [P+1] (per-client terms rounded before the sum -> rank-count invariant), plus norms [K].
+    ``angle_mask`` uint8 [P] on the device; ``out`` an optional int64 [P+1] destination (e.g. the head
+    of the round's all-reduce buffer).  DP noise keys are only built / uploaded when DP is on."""
     K, P = theta_k.shape
     dev = theta_k.device
-    keys = torch.tensor([w for c in client_ids for w in philox_key(seed, "dp_noise", round_num, int(c))],
-                        dtype=torch.int64).to(torch.int32)
-    keys = h2d(keys, dev)
+    if dp:
+        keys = torch.tensor([w for c in client_ids for w in philox_key(seed, "dp_noise", round_num, int(c))],
+                            dtype=torch.int64).to(torch.int32)
+        keys = h2d(keys, dev)
+    else:
+        keys = _NO_KEYS.setdefault(dev, torch.zeros(0, dtype=torch.int32, device=dev))
     norms = torch.empty(K, dtype=torch.float64, device=dev)
-    out = torch.empty(P + 1, dtype=torch.int64, device=dev)
-    ext().fedavg(theta_k.float().contiguous(), theta_g.float().contiguous(),
-                 angle_mask.to(torch.uint8).contiguous(), weights.double().contiguous(), norms, keys,
-                 bool(wrap), bool(dp), float(clip_norm), float(noise_multiplier) if dp else 0.0, out)
+    if out is None:
+        out = torch.empty(P + 1, dtype=torch.int64, device=dev)
+    if angle_mask.dtype != torch.uint8:
+        angle_mask = angle_mask.to(torch.uint8)
+    ext().fedavg(theta_k.float().contiguous(), theta_g.float().contiguous(), angle_mask.contiguous(),
+                 weights.double().contiguous(), norms, keys, bool(wrap), bool(dp), float(clip_norm),
+                 float(noise_multiplier) if dp else 0.0, out)
     return out, norms

@@ -152,7 +152,8 @@ class HipProgram:
         return out.reshape(K, B, self.C).clone()
 
     # ------------------------------------------------------------------ train step
-    def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0) -> dict:
+    def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
+                       out_correct=None) -> dict:
         K, B, F = xang.shape
         if F != self.x_width:
             raise ValueError(f"expected {self.x_width} x-slot values per sample, got {F}")
@@ -169,8 +170,8 @@ class HipProgram:
         slab = self._buf("slab", S * adj.tiles_per_state * self.G, torch.float32)
         expz = self._buf("expz", S * self.C, torch.float32)
         wread = self._buf("wread", S * self.C, torch.float32)
-        loss = torch.empty(K, dtype=torch.float32, device=self.device)
-        correct = torch.empty(K, dtype=torch.float32, device=self.device)
+        loss = torch.empty(K, dtype=torch.float32, device=self.device) if out_loss is None else out_loss
+        correct = torch.empty(K, dtype=torch.float32, device=self.device) if out_correct is None else out_correct
         grad = torch.zeros_like(p)
         self._run_passes(tr, False, psi, None, p, B, x, None, part, None, S)
         if noise is None:
