@@ -54,9 +54,9 @@ def test_federated_learning_shapes_and_learning():
     assert out["accuracies"][-1] > out["accuracies"][0]
 
 
-def test_encoder_demo_runs_on_synthetic_image():
+def test_encoder_demo_runs_on_synthetic_image(tmp_path):
     img = synthetic_digit_images(np.array([2]), 3)[0]
-    res = testEncoder.main(image=img, verbose=False)
+    res = testEncoder.main(image=img, verbose=False, results_folder=str(tmp_path))
     assert res["downsampled"].shape == (4, 4)
     assert len(res["amplitudes"]) == 8
     assert res["amplitude_circuit"].name == "AmplitudeEncode"
