@@ -62,6 +62,7 @@ int qfx_grad_split(int tps, int spc);
 int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct, const float* nvalid,
                           const float* act, int n, double samples, double steps, hipStream_t st);
 int qfx_launch_round_apply(const long long* buf, int P, float* theta, double lr, double* out, hipStream_t st);
+int qfx_fedavg_norm_scratch(int K, int P);
 int qfx_launch_adam(float* p, const float* g, float* m, float* v, float* t, const float* active, int K, int P,
                     float lr, float b1, float b2, float eps, hipStream_t st);
 int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, const float* active, int K, int P, float lr,
@@ -234,6 +235,8 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
   need(out, torch::kInt64, "out");
   const int K = (int)theta_k.size(0), P = (int)theta_k.size(1);
   if (out.numel() < P + 1) throw std::invalid_argument("fedavg out too small");
+  if (norms.numel() < qfx_fedavg_norm_scratch(K, P)) throw std::invalid_argument("fedavg norms scratch too small");
+  if (dp && keys.numel() < 2 * K) throw std::invalid_argument("fedavg: DP needs 2 key words per client");
   check(qfx_launch_fedavg(ptr<float>(theta_k), ptr<float>(theta_g), ptr<unsigned char>(angle_mask),
                           ptr<double>(weights), ptr<double>(norms), ptr<uint32_t>(keys), K, P, wrap ? 1 : 0,
                           dp ? 1 : 0, (float)clip, (float)sigma, ptr<long long>(out), cur_stream()),
@@ -298,6 +301,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_reduce", &grad_reduce);
   m.def("grad_split", &grad_split);
   m.def("round_pack", &round_pack);
+  m.def("fedavg_norm_scratch", [](int64_t K, int64_t P) { return qfx_fedavg_norm_scratch((int)K, (int)P); });
   m.def("round_apply", &round_apply);
   m.def("adam", &adam);
   m.def("sgdm", &sgdm);

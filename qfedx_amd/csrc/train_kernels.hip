@@ -244,14 +244,17 @@ __device__ __forceinline__ double wrap_pi(double d) {
   return r - 3.141592653589793;
 }
 
-// per-client l2 norm of the (wrapped) update, one block per client, double accumulation
-__global__ void __launch_bounds__(256) qfx_delta_norm_kernel(
+// per-client l2 norm of the (wrapped) update for DP clipping: stage 1, grid (client, chunk of
+// NORM_CHUNK params) -> partial sums of squares in double (fixed-order wave + LDS combine)
+constexpr int NORM_CHUNK = 8192;
+__global__ void __launch_bounds__(256) qfx_delta_norm_partial_kernel(
     const float* __restrict__ theta_k, const float* __restrict__ theta_g,
-    const unsigned char* __restrict__ angle_mask, int P, int wrap, double* __restrict__ norms) {
+    const unsigned char* __restrict__ angle_mask, int P, int wrap, double* __restrict__ partial) {
   __shared__ double sm[4];
-  const int k = blockIdx.x;
+  const int k = blockIdx.x, c = blockIdx.y;
+  const int e0 = c * NORM_CHUNK, e1 = min(P, e0 + NORM_CHUNK);
   double acc = 0.0;
-  for (int e = threadIdx.x; e < P; e += 256) {
+  for (int e = e0 + threadIdx.x; e < e1; e += 256) {
     double d = (double)theta_k[(size_t)k * P + e] - (double)theta_g[e];
     if (wrap && angle_mask[e]) d = wrap_pi(d);
     acc += d * d;
@@ -259,7 +262,16 @@ __global__ void __launch_bounds__(256) qfx_delta_norm_kernel(
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) norms[k] = sqrt(sm[0] + sm[1] + sm[2] + sm[3]);
+  if (threadIdx.x == 0) partial[(size_t)k * gridDim.y + c] = sm[0] + sm[1] + sm[2] + sm[3];
+}
+
+// stage 2: norms[k] = sqrt(sum_c partial[k][c]) in chunk order
+__global__ void qfx_delta_norm_final_kernel(const double* __restrict__ partial, int nc, int K, double* __restrict__ norms) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  double s = 0.0;
+  for (int c = 0; c < nc; ++c) s += partial[(size_t)k * nc + c];
+  norms[k] = sqrt(s);
 }
 
 // out[e] = sum_k round(2^32 * w_k * priv(wrap(theta_k[e] - theta_g[e]))), out[P] = sum_k round(2^32 w_k)
@@ -333,6 +345,8 @@ __global__ void qfx_round_apply_kernel(const long long* __restrict__ buf, int P,
 }  // namespace qfx
 
 using namespace qfx;
+
+extern "C" int qfx_fedavg_norm_scratch(int K, int P) { return K * (1 + (P + NORM_CHUNK - 1) / NORM_CHUNK); }
 
 extern "C" int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct,
                                      const float* nvalid, const float* act, int n, double samples, double steps,
@@ -424,8 +438,13 @@ extern "C" int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, c
 extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
                                  const double* weights, double* norms, const uint32_t* keys, int K, int P,
                                  int wrap, int dp, float clip, float sigma, long long* out, hipStream_t st) {
-  hipLaunchKernelGGL(qfx_delta_norm_kernel, dim3(K), dim3(256), 0, st, theta_k, theta_g, angle_mask, P, wrap,
-                     norms);
+  if (dp) {   // clipping needs the per-client norms; without DP they are not computed
+    const int nc = (P + NORM_CHUNK - 1) / NORM_CHUNK;
+    double* partial = norms + K;   // scratch tail of the norms buffer: K * nc doubles
+    hipLaunchKernelGGL(qfx_delta_norm_partial_kernel, dim3(K, nc), dim3(256), 0, st, theta_k, theta_g, angle_mask, P,
+                       wrap, partial);
+    hipLaunchKernelGGL(qfx_delta_norm_final_kernel, dim3((K + 63) / 64), dim3(64), 0, st, partial, nc, K, norms);
+  }
   hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, st, theta_k, theta_g,
                      angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out);
   return (int)hipGetLastError();

@@ -35,7 +35,7 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
         keys = h2d(keys, dev)
     else:
         keys = _NO_KEYS.setdefault(dev, torch.zeros(0, dtype=torch.int32, device=dev))
-    norms = torch.empty(K, dtype=torch.float64, device=dev)
+    norms = torch.empty(ext().fedavg_norm_scratch(K, P), dtype=torch.float64, device=dev)   # [K] + scratch
     if out is None:
         out = torch.empty(P + 1, dtype=torch.int64, device=dev)
     if angle_mask.dtype != torch.uint8:
@@ -43,4 +43,4 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
     ext().fedavg(theta_k.float().contiguous(), theta_g.float().contiguous(), angle_mask.contiguous(),
                  weights.double().contiguous(), norms, keys, bool(wrap), bool(dp), float(clip_norm),
                  float(noise_multiplier) if dp else 0.0, out)
-    return out, norms
+    return out, (norms[:K] if dp else None)
