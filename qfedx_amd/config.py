@@ -64,6 +64,9 @@ class TrainConfig:
     aggregate: str = "delta"            # delta (ROADMAP:36) | weights (Classical_FL.py:66-81)
     wrap_angles: bool = True            # wrap angle deltas to [-pi, pi] (ROADMAP:37)
     weighting: str = "samples"          # samples | uniform
+    server_optimizer: str = "fedavg"    # fedavg | momentum (FedAvgM) | adam (FedAdam); state sharded over ranks
+    server_lr: float = 1.0
+    server_momentum: float = 0.9
     eval_every: int = 1
     seed: int = 42
 

@@ -22,7 +22,8 @@ from typing import Optional
 
 import torch
 
-from ..parallel.dist import World, all_gather_cat, all_reduce_, barrier, broadcast_, shard_clients
+from ..parallel.dist import (ShardedServerState, World, all_gather_cat, all_reduce_, barrier, broadcast_,
+                             shard_clients)
 from ..privacy.accountant import RDPAccountant
 from ..privacy.secure_agg import SecureAggregator
 from ..utils.device import h2d
@@ -84,6 +85,12 @@ class FederatedRunner:
         self.timer = PhaseTimer(device)
         self.start_round = 0
         self.history: list[dict] = []
+        self.server_opt = None
+        if t.server_optimizer != "fedavg" or t.server_lr != 1.0:
+            if p.secure_agg:
+                raise ValueError("server_optimizer needs plain (non-SecAgg) aggregation of the update sums")
+            self.server_opt = ShardedServerState(self.P, world, device, t.server_optimizer, t.server_lr,
+                                                 t.server_momentum)
         self.params = adapter.init_params(t.seed).to(device)
         broadcast_(self.params, world)                      # CC1: identical theta on all ranks
 
@@ -163,7 +170,7 @@ class FederatedRunner:
         with self.timer.phase("local_train"):
             res = self.adapter.trainer.run_round(self.store, local_alive, self.params, r)
         ids = [self.local_ids[i] for i in local_alive]
-        fast = self.backend == "hip" and not p.secure_agg
+        fast = self.backend == "hip" and not p.secure_agg and self.server_opt is None
         with self.timer.phase("aggregate"):
             if t.weighting == "uniform":
                 w = torch.ones(len(local_alive), dtype=torch.float64, device=dev)
@@ -204,6 +211,15 @@ class FederatedRunner:
                 from ..ops._ext import ext
                 ext().round_apply(buf, P, self.params, 1.0, out)   # finalize + apply, in place
                 metrics = out[:4]
+            elif self.server_opt is not None:
+                # server optimizer (CC5): small all-reduce of [weight | metrics]; the update sums are
+                # reduce-scattered inside the sharded step and the new params all-gathered
+                tail = torch.cat([contrib[P:P + 1].to(torch.int64),
+                                  torch.round(metrics.double() * EXACT_SCALE).to(torch.int64)])
+                all_reduce_(tail, self.world)
+                wsum = tail[0].double() / EXACT_SCALE
+                metrics = tail[1:].double() / EXACT_SCALE
+                self.params = self.server_opt.step(self.params, contrib[:P].to(torch.int64), wsum)
             elif p.secure_agg:
                 all_reduce_(contrib, self.world)          # int64 ring elements: exact, mod later
                 all_reduce_(metrics, self.world)

@@ -233,34 +233,83 @@ class BucketedAllReduce:
             self.wait_bucket(i)
 
 
-class ShardedServerState:
-    """Server momentum (FedAvgM) with state sharded P/world per rank (CC5: reduce-scatter + all-gather)."""
+def reduce_scatter_(full: torch.Tensor, world: World) -> torch.Tensor:
+    """Sum ``full`` [world * chunk] over ranks and return this rank's chunk (CC5).  gloo has no
+    reduce-scatter: there it is an all-reduce + slice (same result, CPU test path)."""
+    ws = world.world_size
+    chunk = full.numel() // ws
+    if not world.distributed:
+        return full[:chunk].clone()
+    if world.backend == "gloo":
+        buf = full.clone()
+        dist.all_reduce(buf)
+        return buf[world.rank * chunk: (world.rank + 1) * chunk].clone()
+    out = torch.empty(chunk, dtype=full.dtype, device=full.device)
+    dist.reduce_scatter_tensor(out, full.contiguous())
+    return out
 
-    def __init__(self, P: int, world: World, device, momentum: float = 0.9, lr: float = 1.0):
+
+def all_gather_(shard: torch.Tensor, world: World) -> torch.Tensor:
+    """Concatenate every rank's equally sized ``shard`` (CC5)."""
+    if not world.distributed:
+        return shard.clone()
+    out = torch.empty(shard.numel() * world.world_size, dtype=shard.dtype, device=shard.device)
+    if world.backend == "gloo":
+        parts = [torch.empty_like(shard) for _ in range(world.world_size)]
+        dist.all_gather(parts, shard.contiguous())
+        return torch.cat(parts)
+    dist.all_gather_into_tensor(out, shard.contiguous())
+    return out
+
+
+class ShardedServerState:
+    """Server-side optimizer over the aggregated update with its state sharded P/world per rank (CC5).
+
+    ``kind``: ``fedavg`` (theta += lr * mean update), ``momentum`` (FedAvgM, v = beta v + d) or ``adam``
+    (FedAdam, Reddi et al. 2021: m, v moments, tau adaptivity).  The input is the EXACT int64 fixed-point
+    sum of the clients' weighted updates (scale 2^32): it is reduce-scattered (integer sums are
+    associative -> rank-count invariant), each rank steps its slice in float64, and the new parameter
+    slices are all-gathered.
+    """
+
+    def __init__(self, P: int, world: World, device, kind: str = "momentum", lr: float = 1.0,
+                 momentum: float = 0.9, betas=(0.9, 0.99), tau: float = 1e-3, scale: float = 2.0 ** 32):
         self.world = world
         self.P = P
         ws = world.world_size
         self.chunk = (P + ws - 1) // ws
         self.padded = self.chunk * ws
-        self.momentum = momentum
+        self.kind = kind
         self.lr = lr
+        self.momentum = momentum
+        self.b1, self.b2 = betas
+        self.tau = tau
+        self.scale = scale
+        self.t = 0
         self.m = torch.zeros(self.chunk, dtype=torch.float64, device=device)
+        self.v = torch.zeros(self.chunk, dtype=torch.float64, device=device) if kind == "adam" else None
 
-    def step(self, global_params: torch.Tensor, local_update_sum: torch.Tensor, weight_total: float) -> torch.Tensor:
-        """``local_update_sum`` = this rank's weighted delta sum; returns new full params."""
-        flat = torch.zeros(self.padded, dtype=torch.float64, device=local_update_sum.device)
-        flat[: self.P] = local_update_sum.double()
-        shard = torch.zeros(self.chunk, dtype=torch.float64, device=flat.device)
-        if self.world.distributed:
-            dist.reduce_scatter_tensor(shard, flat)
+    def step(self, global_params: torch.Tensor, update_sum_fixed: torch.Tensor, wsum: torch.Tensor) -> torch.Tensor:
+        """``update_sum_fixed``: this rank's int64 [P] fixed-point weighted update sum; ``wsum``: the
+        all-reduced weight total (0-d tensor).  Returns the new full parameter vector."""
+        dev = update_sum_fixed.device
+        flat = torch.zeros(self.padded, dtype=torch.int64, device=dev)
+        flat[: self.P] = update_sum_fixed
+        shard = reduce_scatter_(flat, self.world).double() / self.scale
+        d = shard / wsum.to(dev).double().clamp(min=1e-300)
+        self.t += 1
+        if self.kind == "momentum":
+            self.m.mul_(self.momentum).add_(d)
+            step = self.lr * self.m
+        elif self.kind == "adam":
+            self.m.mul_(self.b1).add_((1 - self.b1) * d)
+            self.v.mul_(self.b2).add_((1 - self.b2) * d * d)
+            step = self.lr * self.m / (self.v.sqrt() + self.tau)
         else:
-            shard.copy_(flat)
-        avg = shard / weight_total
-        self.m.mul_(self.momentum).add_(avg)
-        upd_shard = self.lr * self.m
-        full = torch.zeros(self.padded, dtype=torch.float64, device=flat.device)
-        if self.world.distributed:
-            dist.all_gather_into_tensor(full, upd_shard)
-        else:
-            full.copy_(upd_shard)
+            step = self.lr * d
+        step = torch.where(wsum.to(dev) > 0, step, torch.zeros_like(step))
+        full = all_gather_(step, self.world)
         return (global_params.double() + full[: self.P]).to(global_params.dtype)
+
+    def state_dict(self) -> dict:
+        return {"t": self.t, "m": self.m.cpu(), "v": None if self.v is None else self.v.cpu()}

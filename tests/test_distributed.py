@@ -75,3 +75,12 @@ def test_cfed_two_ranks_match_single_process(tmp_path):
     single = run_experiment(small_cfg(**kw))
     two = _run(2, kw, tmp_path)
     assert torch.allclose(two["params"], single["params"], atol=1e-6)
+
+
+def test_gloo_two_ranks_sharded_server_adam(tmp_path):
+    """FedAdam with its state sharded over ranks (reduce-scatter + all-gather) == single process."""
+    from qfedx_amd.api import run_experiment
+    kw = dict(num_rounds=3, server_optimizer="adam", server_lr=0.3)
+    single = run_experiment(small_cfg(**kw))
+    two = _run(2, kw, tmp_path)
+    assert torch.equal(two["params"], single["params"])

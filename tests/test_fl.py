@@ -162,3 +162,19 @@ def test_exact_aggregation_permutation_and_split_invariant(K, seed, split):
     parts = agg.local_reduce(tk[:cut], tg, w[:cut], 0, ids[:cut]) if cut else torch.zeros_like(full)
     parts = parts + agg.local_reduce(tk[cut:], tg, w[cut:], 0, ids[cut:])
     assert torch.equal(full, permuted) and torch.equal(full, parts)
+
+
+@pytest.mark.parametrize("opt", ["momentum", "adam"])
+def test_server_optimizers_train(opt):
+    out = run_experiment(small_cfg(num_rounds=5, server_optimizer=opt, server_lr=0.5 if opt == "adam" else 1.0))
+    assert out["accuracies"][-1] > out["accuracies"][0]
+
+
+def test_sharded_fedavg_step_equals_plain_path():
+    from qfedx_amd.parallel.dist import ShardedServerState, World
+    # local SGD: Adam would amplify the 1e-12 lr offset on the zero-gradient angles
+    plain = run_experiment(small_cfg(num_rounds=3, optimizer="sgd"))
+    # a FedAvg "server optimizer" with lr 1 through the sharded reduce-scatter/all-gather path
+    sharded = run_experiment(small_cfg(num_rounds=3, optimizer="sgd", server_optimizer="fedavg",
+                                       server_lr=1.0 + 1e-12))
+    assert torch.allclose(plain["params"], sharded["params"], atol=1e-6)
