@@ -81,6 +81,22 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
   auto gkind = [&](int g) { return gt[g * GATE_WORDS]; };
   auto gslot = [&](int g) { return gt[g * GATE_WORDS + 3]; };
   auto is_grad = [&](int g) { return adjoint && gslot(g) >= 0 && gslot(g) < n_theta && gkind(g) <= K_P; };
+  // adjoint: is the gate's inverse needed by a live gate earlier in the circuit (processed later)?
+  // (same liveness as the planner, which already dropped the dead gates)
+  std::vector<char> need_inv(G, 1);
+  if (adjoint) {
+    std::vector<char> has_live(n, 0);
+    for (int g = 0; g < G; ++g) {
+      const int kd = gkind(g), q0 = gt[g * GATE_WORDS + 1], q1 = gt[g * GATE_WORDS + 2];
+      const bool two = kd == K_CX || kd == K_CZ;
+      const bool nd = has_live[q0] || (two && has_live[q1]);
+      need_inv[g] = nd;
+      if (is_grad(g) || nd) {
+        has_live[q0] = 1;
+        if (two) has_live[q1] = 1;
+      }
+    }
+  }
 
   // gates referenced by this pass (coefficient table entries)
   std::vector<int> used, slot_of(G, -1);
@@ -306,6 +322,12 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
           const char* cls = is_grad(g) ? (kd == K_RX ? "CLS_RX" : kd == K_RY ? "CLS_RY" : "CLS_RZ")
                                        : (is_diag_kind(kd) ? "CLS_DIAG" : kd == K_RX ? "CLS_RX"
                                                                         : kd == K_RY ? "CLS_RY" : "CLS_GEN");
+          if (is_grad(g) && !need_inv[g]) {   // gradient only: nothing processed later needs the inverse
+            s << "  { const float part = adj_grad_only<R, " << oa << ", " << cls << ">(a, l);\n";
+            emit_grad(g, "part");
+            s << "  }\n";
+            continue;
+          }
           s << "  { const M2 mi = gate_m2(" << kind_name(kd) << ", " << cs(g) << ", true);\n";
           s << "    const float part = adj_step<R, " << oa << ", " << cls << ">(a, l, mi); (void)part;\n";
           if (is_grad(g)) emit_grad(g, "part");
@@ -323,8 +345,10 @@ JitSpec codegen_pass(const std::vector<int>& blob, int p, bool adjoint, bool bf1
         s << "    part = bit ? -part : part;\n";
         emit_grad(oc, "part");
       }
-      s << "#pragma unroll\n    for (int r = 0; r < R; ++r) { a[r] = cmul(ph, a[r]);"
-        << (adjoint ? " l[r] = cmul(ph, l[r]);" : "") << " }\n  }\n";
+      if (adjoint && !need_inv[oc]) s << "  }\n";   // phase not needed by anything processed later
+      else
+        s << "#pragma unroll\n    for (int r = 0; r < R; ++r) { a[r] = cmul(ph, a[r]);"
+          << (adjoint ? " l[r] = cmul(ph, l[r]);" : "") << " }\n  }\n";
     } else if (code == OP_REMAP) {
       const int* tab = blob.data() + oa;
       const int* wr = tab;

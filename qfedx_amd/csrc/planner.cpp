@@ -77,8 +77,13 @@ class Planner {
     std::vector<std::vector<int>> prefix(n_);
     std::vector<int> body;
     if (mode == 2) {
+      // adjoint sweep = reverse circuit order.  A gate's inverse is only needed if some gate EARLIER in
+      // the circuit (processed later) on one of its qubits is live (a gradient gate, or a gate whose
+      // inverse is needed): gates that are neither are dead work (e.g. the feature map) and dropped.
+      const std::vector<char> live = adjoint_liveness(nullptr);
       std::reverse(order.begin(), order.end());
-      body = order;
+      for (int gi : order)
+        if (live[gi]) body.push_back(gi);
     } else if (mode == 0) {
       std::vector<char> ent(n_, 0);
       for (int gi : order) {
@@ -177,6 +182,26 @@ class Planner {
   }
 
  private:
+  // live[g] (grad gate or inverse needed) and, optionally, need_inverse[g], in circuit order
+  std::vector<char> adjoint_liveness(std::vector<char>* need_inverse) const {
+    const int G = (int)gates_.size();
+    std::vector<char> live(G, 0), need(G, 0), has_live(n_, 0);
+    for (int g = 0; g < G; ++g) {
+      const PGate& x = gates_[g];
+      const bool two = !is_1q(x.kind);
+      const bool nd = has_live[x.q0] || (two && has_live[x.q1]);
+      const bool grad = x.slot >= 0 && x.slot < n_theta_ && x.kind <= K_P;
+      need[g] = nd;
+      live[g] = grad || nd;
+      if (live[g]) {
+        has_live[x.q0] = 1;
+        if (two) has_live[x.q1] = 1;
+      }
+    }
+    if (need_inverse) *need_inverse = need;
+    return live;
+  }
+
   int n_, R_, rb_, k_, tb_, coal_, n_theta_;
   std::vector<PGate> gates_;
   std::vector<int> readout_;

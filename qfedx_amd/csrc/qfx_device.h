@@ -194,6 +194,24 @@ __device__ __forceinline__ float adj_step(v2f (&a)[R], v2f (&l)[R], const M2& mi
   return acc.x - acc.y;
 }
 
+// gradient only (the gate's inverse is not needed by anything processed later): Im<lambda|P|psi> on
+// the current values - equal to the post-inverse value because the generator commutes with its gate
+template <int R, int RBT, int CLS>
+__device__ __forceinline__ float adj_grad_only(const v2f (&a)[R], const v2f (&l)[R]) {
+  v2f acc = mk(0.f, 0.f);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (r & (1 << RBT)) continue;
+    const int r1 = r | (1 << RBT);
+    const v2f p0 = a[r], p1 = a[r1], l0 = l[r], l1 = l[r1];
+    if constexpr (CLS == CLS_RX) { acc = acc_im(acc, l0, p1); acc = acc_im(acc, l1, p0); }
+    if constexpr (CLS == CLS_RY) { acc = acc_re(acc, l1, p0); acc = acc_re(acc, -l0, p1); }
+    if constexpr (CLS == CLS_RZ) { acc = acc_im(acc, l0, p0); acc = acc_im(acc, -l1, p1); }
+  }
+  if constexpr (CLS == CLS_RY) return acc.x + acc.y;
+  return acc.x - acc.y;
+}
+
 #define QFX_CLS_DISPATCH(cls, RBT_, OUT)                                   \
   switch (cls) {                                                         \
     case CLS_GEN: OUT = adj_step<R, RBT_, CLS_GEN>(a, l, mi); break;      \
