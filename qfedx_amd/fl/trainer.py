@@ -12,12 +12,14 @@ fixes the step count for every client (benchmarks).
 from __future__ import annotations
 
 import math
+
+import numpy as np
 from typing import Optional
 
 import torch
 
 from ..utils.device import PackedUpload, h2d
-from ..utils.seeding import generator
+from ..utils.seeding import philox4x32, philox_key, philox_uniform_rows
 from .optim import BatchedOptimizer
 
 
@@ -48,54 +50,62 @@ class ShardStore:
 
 
 class BatchPlan:
-    """Per-round minibatch schedule for a set of clients (host-side index tables, keyed RNG)."""
+    """Per-round minibatch schedule for a set of clients (host-side index tables, keyed RNG).
+
+    Vectorised over clients: one round key, per-client Philox keys derived from it by client id, keyed
+    uniforms [K, epochs, n_max] -> argsort = every client's epoch permutations at once; the [S, K, B]
+    index / weight / active tables are built with tensor ops (no per-client Python loop).  Keyed by
+    (seed, round, client id, epoch) only -> identical however clients are sharded over ranks.
+    """
 
     def __init__(self, counts: torch.Tensor, client_ids: list, batch_size: int, round_num: int,
                  seed: int, local_epochs: int = 1, local_steps: int = 0, shuffle: bool = True):
-        self.B = batch_size
+        B = self.B = batch_size
         K = len(client_ids)
-        self.steps_per_client = []
-        perms = []
-        for k, cid in enumerate(client_ids):
-            n = int(counts[k])
-            if local_steps > 0:
-                steps = local_steps
-                epochs = math.ceil(steps * batch_size / max(n, 1))
-            else:
-                steps = local_epochs * math.ceil(n / batch_size)
-                epochs = local_epochs
-            self.steps_per_client.append(steps)
-            order = []
-            for e in range(max(epochs, 1)):
-                if shuffle:
-                    order.append(torch.randperm(n, generator=generator(seed, "batch", round_num, int(cid), e)))
-                else:
-                    order.append(torch.arange(n))
-            perms.append(torch.cat(order) if order else torch.zeros(0, dtype=torch.int64))
-        self.max_steps = max(self.steps_per_client) if K else 0
+        n = counts.to(torch.int64).reshape(-1)
+        nb = (n + B - 1) // B                                   # batches per epoch
+        if local_steps > 0:
+            steps = torch.full((K,), local_steps, dtype=torch.int64)
+            epochs = (steps * B + n.clamp(min=1) - 1) // n.clamp(min=1)
+        else:
+            steps = local_epochs * nb
+            epochs = torch.full((K,), local_epochs, dtype=torch.int64)
+        self.steps_per_client = steps.tolist()
+        self.max_steps = int(steps.max()) if K else 0
         self.local_steps = local_steps
-        # index [S, K, B] into each client's padded shard and per-sample weights [S, K, B]
-        S = self.max_steps
-        idx = torch.zeros(S, K, batch_size, dtype=torch.int64)
-        wts = torch.zeros(S, K, batch_size, dtype=torch.float32)
-        active = torch.zeros(S, K, dtype=torch.float32)
-        for k in range(K):
-            n = int(counts[k])
-            p = perms[k]
-            for s in range(self.steps_per_client[k]):
-                if local_steps > 0:
-                    sel = p[(s * batch_size) % max(len(p), 1):][:batch_size]
-                    if sel.numel() < batch_size:  # wrap around the epoch boundary
-                        sel = torch.cat([sel, p[: batch_size - sel.numel()]])
-                    valid = batch_size
-                else:
-                    ep, j = divmod(s, math.ceil(n / batch_size))
-                    sel = p[ep * n + j * batch_size: ep * n + min((j + 1) * batch_size, n)]
-                    valid = sel.numel()
-                idx[s, k, :valid] = sel[:valid]
-                wts[s, k, :valid] = 1.0 / valid
-                active[s, k] = 1.0
-        self.idx, self.wts, self.active = idx, wts, active
+        S, E, N = self.max_steps, max(int(epochs.max()) if K else 1, 1), max(int(n.max()) if K else 1, 1)
+        if shuffle and K:
+            rk = philox_key(seed, "batch", round_num)
+            ids = torch.tensor([int(c) for c in client_ids], dtype=torch.int64)
+            ctr = torch.stack([ids & 0xFFFFFFFF, ids >> 32, torch.zeros_like(ids), torch.zeros_like(ids)], -1)
+            keys = philox4x32(ctr, rk[0], rk[1])[:, :2]          # per-client key = Philox(round key, client id)
+            u = philox_uniform_rows(keys, E * N).reshape(K, E, N)
+            u = torch.where(torch.arange(N)[None, None, :] < n[:, None, None], u, torch.full_like(u, 2.0))
+            perm = torch.argsort(u, dim=-1)                       # [K, E, N]: first n_k entries permute 0..n_k-1
+        else:
+            perm = torch.arange(N).expand(K, E, N)
+        s_ = torch.arange(S)[:, None, None]                       # [S, 1, 1]
+        t_ = torch.arange(B)[None, None, :]                       # [1, 1, B]
+        nk = n[None, :, None].clamp(min=1)
+        kk = torch.arange(K)[None, :, None]
+        if local_steps > 0:                                       # fixed steps: walk the epoch order cyclically
+            pos = (s_ * B + t_) % (epochs[None, :, None] * nk)
+            ep, i = pos // nk, pos % nk
+            valid = torch.ones(S, K, B, dtype=torch.bool)
+        else:                                                     # epochs x ceil(n/B) steps, last batch partial
+            ep, jb = s_ // nb[None, :, None].clamp(min=1), s_ % nb[None, :, None].clamp(min=1)
+            i = jb * B + t_
+            valid = i < n[None, :, None]
+            i = torch.where(valid, i, torch.zeros_like(i))
+        active = (torch.arange(S)[:, None] < steps[None, :])      # [S, K]
+        valid = valid & active[:, :, None]
+        lin = (kk * E + ep.clamp(max=E - 1)) * N + i               # broadcast -> [S, K, B] linear indices
+        # numpy gather: torch's OpenMP take on a few thousand elements can stall for tens of ms
+        idx = torch.from_numpy(np.take(perm.contiguous().numpy(), lin.expand(S, K, B).contiguous().numpy()))
+        cnt = valid.sum(-1, keepdim=True).clamp(min=1)
+        self.idx = torch.where(valid, idx, torch.zeros_like(idx))
+        self.wts = valid.float() / cnt.float()
+        self.active = active.float()
 
 
 class VQCClientTrainer:

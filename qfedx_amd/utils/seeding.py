@@ -81,12 +81,41 @@ def philox_key(root: int, *keys: int | str) -> tuple[int, int]:
 # Philox4x32-10, vectorised in torch int64 (CPU oracle of csrc/philox.h)
 # ---------------------------------------------------------------------------
 
+def _philox4x32_np(c: np.ndarray, k0, k1, rounds: int = 10) -> np.ndarray:
+    """numpy uint64 Philox4x32: the product of two 32-bit words is exact in uint64 (no limb split)."""
+    m = np.uint64(MASK32)
+    c0, c1, c2, c3 = (c[..., i].astype(np.uint64) & m for i in range(4))
+    k0 = np.broadcast_to(np.asarray(k0, dtype=np.uint64) & m, c0.shape).copy()
+    k1 = np.broadcast_to(np.asarray(k1, dtype=np.uint64) & m, c0.shape).copy()
+    M0, M1 = np.uint64(PHILOX_M0), np.uint64(PHILOX_M1)
+    W0, W1 = np.uint64(PHILOX_W0), np.uint64(PHILOX_W1)
+    s32 = np.uint64(32)
+    for _ in range(rounds):
+        p0 = c0 * M0
+        p1 = c2 * M1
+        c0, c1, c2, c3 = ((p1 >> s32) ^ c1 ^ k0) & m, p1 & m, ((p0 >> s32) ^ c3 ^ k1) & m, p0 & m
+        k0 = (k0 + W0) & m
+        k1 = (k1 + W1) & m
+    return np.stack([c0, c1, c2, c3], axis=-1)
+
+
 def philox4x32(counter: torch.Tensor, key0: int, key1: int, rounds: int = 10) -> torch.Tensor:
     """Philox4x32 on an int64 tensor ``counter[..., 4]`` of 32-bit words.
 
     Returns int64 tensor [..., 4] of 32-bit outputs.  Bit-identical to the device
-    implementation in ``qfedx_amd/csrc/philox.h``.
+    implementation in ``qfedx_amd/csrc/philox.h``.  CPU tensors use the numpy uint64 path; device
+    tensors a limb-split int64 torch path (both tested against the known-answer vectors).
     """
+    if counter.device.type == "cpu":
+        k0 = key0.numpy() if isinstance(key0, torch.Tensor) else key0
+        k1 = key1.numpy() if isinstance(key1, torch.Tensor) else key1
+        out = _philox4x32_np(counter.to(torch.int64).numpy(), k0, k1, rounds)
+        return torch.from_numpy(out.astype(np.int64))
+    return _philox4x32_torch(counter, key0, key1, rounds)
+
+
+def _philox4x32_torch(counter: torch.Tensor, key0, key1, rounds: int = 10) -> torch.Tensor:
+    """int64 torch Philox (16-bit limb products: no uint64 multiply in torch), any device."""
     c0, c1, c2, c3 = (counter[..., i].to(torch.int64) & MASK32 for i in range(4))
     if isinstance(key0, torch.Tensor):   # per-row keys, broadcast against the counter
         k0 = (key0.to(torch.int64) & MASK32).expand_as(c0).clone()

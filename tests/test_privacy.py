@@ -106,3 +106,12 @@ def test_accountant_monotone_and_state():
     assert acc2.get_epsilon(1e-5) == eps[-1]
     assert epsilon(0.3, 2.0, 5, 1e-5) < eps[-1]         # more noise -> less epsilon
     assert (compute_rdp(0.3, 1.0, 5) >= 0).all()
+
+
+def test_philox_numpy_and_torch_paths_bitwise():
+    from qfedx_amd.utils.seeding import _philox4x32_torch, philox4x32
+    g = torch.Generator().manual_seed(3)
+    ctr = torch.randint(0, 2 ** 32, (777, 4), generator=g, dtype=torch.int64)
+    keys = torch.randint(0, 2 ** 32, (777, 2), generator=g, dtype=torch.int64)
+    assert torch.equal(philox4x32(ctr, 0xDEADBEEF, 0x12345678), _philox4x32_torch(ctr, 0xDEADBEEF, 0x12345678))
+    assert torch.equal(philox4x32(ctr, keys[:, 0], keys[:, 1]), _philox4x32_torch(ctr, keys[:, 0], keys[:, 1]))
