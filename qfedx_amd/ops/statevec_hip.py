@@ -92,6 +92,7 @@ class HipProgram:
             raise RuntimeError("bf16 statevector storage needs the circuit-specialised (JIT) kernels; "
                                "unset QFEDX_JIT=0")
         args = (ops, coef, n_qubits, self.R, kmax, self.readout, n_theta)
+        self._plan_args = (ops, coef, kmax)
         self.eval_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_READOUT, self.device, self.jit, self.bf16)
         self.train_plan = _Plan(*args, MODE_FWD_PRODUCT, FIN_STORE | FIN_READOUT, self.device, self.jit, self.bf16)
         self.adj_plan = _Plan(*args, MODE_ADJ, 0, self.device, self.jit, self.bf16)
@@ -150,6 +151,69 @@ class HipProgram:
             ext().readout_noise(out, self.C, B, S, noise.p01, noise.p10, noise.shots, _keys(keys, noise),
                                 int(step))
         return out.reshape(K, B, self.C).clone()
+
+    # ------------------------------------------------------------------ generic simulation
+    def _load_plan(self, fin: int) -> _Plan:
+        """Plan that starts from a caller-provided state (amplitude encoding / initialize)."""
+        cache = self.__dict__.setdefault("_load_plans", {})
+        if fin not in cache:
+            cache[fin] = _Plan(self._plan_args[0], self._plan_args[1], self.n, self.R, self._plan_args[2],
+                               self.readout, self.n_theta, MODE_FWD_LOAD, fin, self.device, self.jit, self.bf16)
+        return cache[fin]
+
+    def _state_in(self, psi: torch.Tensor, init: torch.Tensor) -> None:
+        if self.bf16:
+            raise NotImplementedError("initial states are loaded in complex64 storage only")
+        psi.view(init.shape[0], -1).copy_(init.to(torch.complex64))
+
+    @torch.no_grad()
+    def statevector(self, xang: torch.Tensor, theta: torch.Tensor, init: torch.Tensor | None = None):
+        """Final states [S, 2^n] complex64 (logical amplitude order) and <Z_readout> [S, C]."""
+        K, B, F = xang.shape
+        S = K * B
+        x = xang.reshape(S, F).float().contiguous()
+        th = theta.float().contiguous()
+        plan = self.train_plan if init is None else self._load_plan(FIN_STORE | FIN_READOUT)
+        psi = self._buf("psi", S << self.n, self.state_torch_dtype)
+        part = self._buf("part", S * plan.tiles_per_state * self.C, torch.float32)
+        if init is not None:
+            self._state_in(psi, init)
+        self._run_passes(plan, False, psi, None, th, B, x, None, part, None, S)
+        z = self._buf("expz", S * self.C, torch.float32)
+        ext().readout_sum(part, plan.tiles_per_state, self.C, S, z)
+        state = psi.view(S, -1)
+        if self.bf16:   # unpack (re, im) bf16 pairs
+            u = state.view(torch.int32)
+            re = (u << 16).view(torch.float32)
+            im = (u & -65536).view(torch.float32)
+            state = torch.complex(re, im)
+        return state.clone(), z.view(S, self.C).clone()
+
+    @torch.no_grad()
+    def vjp(self, xang: torch.Tensor, theta: torch.Tensor, w: torch.Tensor, init: torch.Tensor | None = None):
+        """Adjoint VJP of sum_c w[s, c] <Z_c>_s: returns (<Z> [S, C], d/dtheta [K, n_theta] summed over the
+        B samples of each parameter row)."""
+        K, B, F = xang.shape
+        S = K * B
+        C = ext()
+        x = xang.reshape(S, F).float().contiguous()
+        th = theta.float().contiguous()
+        tr, adj = (self.train_plan if init is None else self._load_plan(FIN_STORE | FIN_READOUT)), self.adj_plan
+        psi = self._buf("psi", S << self.n, self.state_torch_dtype)
+        lam = self._buf("lam", S << self.n, self.state_torch_dtype)
+        part = self._buf("part", S * tr.tiles_per_state * self.C, torch.float32)
+        slab = self._buf("slab", S * adj.tiles_per_state * self.G, torch.float32)
+        if init is not None:
+            self._state_in(psi, init)
+        self._run_passes(tr, False, psi, None, th, B, x, None, part, None, S)
+        z = self._buf("expz", S * self.C, torch.float32)
+        C.readout_sum(part, tr.tiles_per_state, self.C, S, z)
+        wr = w.reshape(S, self.C).float().contiguous()
+        self._run_passes(adj, True, psi, lam, th, B, x, wr, None, slab, S)
+        grad = torch.zeros(K, th.shape[1], dtype=torch.float32, device=self.device)
+        gpart = self._buf("gpart", K * C.grad_split(adj.tiles_per_state, B) * self.G, torch.float32)
+        C.grad_reduce(slab, adj.tiles_per_state, B, K, self.G, adj.blob, grad, gpart)
+        return z.view(S, self.C).clone(), grad[:, : self.n_theta]
 
     # ------------------------------------------------------------------ train step
     def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
