@@ -29,7 +29,7 @@ class DataConfig:
     partition_type: str = "iid"         # iid | non_iid (Dirichlet)
     alpha: float = 0.5                  # Dirichlet concentration
     features: str = "pool"              # pool | pca | downsample | raw
-    n_features: int = 0                 # 0 = one feature per qubit (VQC angle map needs n_qubits)
+    n_features: int = 0                 # 0 = one per qubit (angle map) / 2^n_qubits (amplitude encoding)
     samples_per_client: int = 256       # synthetic data size per client
     test_samples: int = 512
 
@@ -40,7 +40,7 @@ class ModelConfig:
     n_qubits: int = 4
     n_layers: int = 2
     n_classes: int = 3
-    feature_map: str = "ry"             # ry | rx | rz (angle encoding basis)
+    feature_map: str = "ry"             # ry | rx | rz (angle encoding basis) | amplitude (2^n features = state)
     feature_scale: str = "scale"        # scale (RY(alpha*x), ROADMAP:126) | minmax (qAngle.py:36-41)
     alpha: float = 3.141592653589793
     entangler: str = "chain"            # chain | ring | none

@@ -112,7 +112,8 @@ def build_federated_data(cfg, clients: Optional[list[int]] = None, images: bool 
     """Dispatch on ``cfg.data.dataset`` (ExperimentConfig)."""
     d, m, t = cfg.data, cfg.model, cfg.train
     non_iid = d.partition_type.lower() != "iid"
-    nf = d.n_features if d.n_features > 0 else m.n_qubits
+    amp = getattr(m, "kind", "vqc") == "vqc" and str(getattr(m, "feature_map", "")).lower() == "amplitude"
+    nf = d.n_features if d.n_features > 0 else ((1 << m.n_qubits) if amp else m.n_qubits)
     if d.dataset == "synthetic":
         if images or m.kind == "tinycnn":
             return load_synthetic_images_federated(d.num_clients, m.n_classes, d.samples_per_client,

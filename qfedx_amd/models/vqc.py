@@ -56,8 +56,18 @@ class VQCSpec:
         return self.n_theta + 2 * self.n_classes
 
     @property
+    def amplitude(self) -> bool:
+        """feature_map='amplitude': the 2^n features ARE the (normalised) initial state (reference
+        ``amplitude_encode``, qAmplitude.py:25-41) instead of an RY(alpha x) angle map."""
+        return self.feature_map.lower() == "amplitude"
+
+    @property
     def n_features(self) -> int:
-        return self.n_qubits
+        return (1 << self.n_qubits) if self.amplitude else self.n_qubits
+
+    @property
+    def n_x_slots(self) -> int:
+        return 0 if self.amplitude else self.n_qubits
 
     @property
     def n_noise_ops(self) -> int:
@@ -66,12 +76,13 @@ class VQCSpec:
             return 0
         n = self.n_qubits
         ent = (n - 1) + (1 if self.entangler == "ring" and n > 2 else 0) if self.entangler in ("chain", "ring") else 0
-        return n + self.n_layers * (2 * n + 2 * ent)
+        return (0 if self.amplitude else n) + self.n_layers * (2 * n + 2 * ent)
 
     @property
     def x_width(self) -> int:
-        """Per-sample x-slot row: encoded features, then the Pauli selectors of the trajectory."""
-        return self.n_features + self.n_noise_ops
+        """Per-sample x-slot row: encoded angles, then the Pauli selectors of the trajectory (at least one
+        column: an amplitude-encoded model without noise carries a dummy)."""
+        return max(1, self.n_x_slots + self.n_noise_ops)
 
     def circuit(self) -> Circuit:
         n = self.n_qubits
@@ -88,9 +99,10 @@ class VQCSpec:
                     j[0] += 1
 
         fm = self.feature_map.lower()
-        for q in range(n):
-            getattr(qc, fm if fm in ("rx", "ry", "rz") else "ry")(x[q], q)
-            noise(q)
+        if not self.amplitude:
+            for q in range(n):
+                getattr(qc, fm if fm in ("rx", "ry", "rz") else "ry")(x[q], q)
+                noise(q)
         k = 0
         for _ in range(self.n_layers):
             for q in range(n):
@@ -111,12 +123,26 @@ class VQCSpec:
 
     def program(self):
         """(ops, coef) with slots [theta (n_theta) | x (n) | noise selectors (n_noise_ops)]."""
-        return self.circuit().to_program({"theta": 0, "x": self.n_theta, "noise": self.n_theta + self.n_features})
+        return self.circuit().to_program({"theta": 0, "x": self.n_theta, "noise": self.n_theta + self.n_x_slots})
 
     def encode_features(self, x: torch.Tensor) -> torch.Tensor:
-        """Raw features [.., n] -> encoding angles fed to the x slots (gate scale is 1)."""
+        """Raw features [.., n] -> encoding angles fed to the x slots (gate scale is 1).  Amplitude
+        encoding has no x slots: a dummy column (or nothing, when noise selectors follow)."""
+        if self.amplitude:
+            return x.new_zeros(*x.shape[:-1], 0 if self.noisy else 1)
         from ..data.features import angle_scale
         return angle_scale(x, self.feature_scale, self.alpha)
+
+    def initial_states(self, x: torch.Tensor) -> Optional[torch.Tensor]:
+        """Amplitude encoding: features [.., <= 2^n] -> normalised complex64 states [.., 2^n] (zero vector ->
+        uniform state, reference normalize_for_amplitude); None for angle encodings."""
+        if not self.amplitude:
+            return None
+        from ..quantum.encoders import amplitude_states
+        N = 1 << self.n_qubits
+        if x.shape[-1] < N:
+            x = torch.cat([x, x.new_zeros(*x.shape[:-1], N - x.shape[-1])], -1)
+        return amplitude_states(x[..., :N]).to(torch.complex64)
 
     def init_params(self, seed: int = 0) -> torch.Tensor:
         g = generator(seed, "init", 0)

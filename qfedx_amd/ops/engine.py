@@ -68,7 +68,17 @@ class VQCEngine:
             raise ValueError(f"unknown backend '{backend}'")
 
     # ------------------------------------------------------------------ helpers
-    def _check(self, xang: torch.Tensor) -> None:
+    def _init_rows(self, init: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        """[K,B,2^n] initial states -> [K*B, 2^n] in the torch executor's dtype (None passes through)."""
+        return None if init is None else init.reshape(-1, init.shape[-1]).to(self.prog.dtype)
+
+    def _check(self, xang: torch.Tensor, init: Optional[torch.Tensor] = None) -> None:
+        if self.spec.amplitude:
+            if init is None or init.shape[:-1] != xang.shape[:-1] or init.shape[-1] != (1 << self.spec.n_qubits):
+                raise ValueError("amplitude-encoded VQC needs init states [K, B, 2^n] "
+                                 "(VQCSpec.initial_states of the raw features)")
+        elif init is not None:
+            raise ValueError("initial states are only used by feature_map='amplitude'")
         # the angle feature map reads one feature per qubit: a narrower input would make the
         # kernels read past each sample's row
         if xang.shape[-1] != self.spec.x_width:
@@ -97,37 +107,41 @@ class VQCEngine:
     # ------------------------------------------------------------------ forward
     @torch.no_grad()
     def expz(self, xang: torch.Tensor, theta: torch.Tensor, readout_keys: Optional[torch.Tensor] = None,
-             step: int = 0) -> torch.Tensor:
+             step: int = 0, init: Optional[torch.Tensor] = None) -> torch.Tensor:
         """<Z_c> for [K,B,x_width] encoded features and per-client theta [K,P] -> [K,B,C] (with the
-        readout noise model applied when one is configured)."""
+        readout noise model applied when one is configured).  ``init`` [K,B,2^n]: amplitude-encoded
+        initial states (``VQCSpec.initial_states``)."""
         K, B, _ = xang.shape
-        self._check(xang)
+        self._check(xang, init)
         if self.backend == "hip":
             nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
-            return self.hip.expz(xang, theta, nz, readout_keys, step)
-        psi = self.prog.run(self._rows(xang, theta))
+            return self.hip.expz(xang, theta, nz, readout_keys, step, init)
+        psi = self.prog.run(self._rows(xang, theta), state=self._init_rows(init))
         z = self.prog.expz(psi, self.spec.readout).reshape(K, B, -1).float()
         return self._readout(z, readout_keys, step)
 
     @torch.no_grad()
-    def predict(self, xang: torch.Tensor, params: torch.Tensor, readout_keys=None, step: int = 0) -> torch.Tensor:
+    def predict(self, xang: torch.Tensor, params: torch.Tensor, readout_keys=None, step: int = 0,
+                init: Optional[torch.Tensor] = None) -> torch.Tensor:
         th, a, b = self.spec.split(params)
-        return logits_from_expz(self.expz(xang, th, readout_keys, step), a, b)
+        return logits_from_expz(self.expz(xang, th, readout_keys, step, init), a, b)
 
     # ------------------------------------------------------------------ training
     def loss_and_grads(self, xang: torch.Tensor, y: torch.Tensor, wmask: torch.Tensor,
                        params: torch.Tensor, method: str = "adjoint", spsa_c: float = 0.1,
                        rng_keys: tuple = (0,), readout_keys: Optional[torch.Tensor] = None,
                        step: int = 0, out_loss: Optional[torch.Tensor] = None,
-                       out_correct: Optional[torch.Tensor] = None) -> dict:
+                       out_correct: Optional[torch.Tensor] = None, init: Optional[torch.Tensor] = None) -> dict:
         """Loss [K], gradient [K,P], correct [K] for [K,B] minibatches.  ``out_loss`` / ``out_correct``
-        (optional [K] views, e.g. rows of a round buffer) receive the loss / hit counts in place."""
+        (optional [K] views, e.g. rows of a round buffer) receive the loss / hit counts in place.
+        ``init`` [K,B,2^n] = amplitude-encoded initial states (None for angle encodings)."""
         spec = self.spec
-        self._check(xang)
+        self._check(xang, init)
         if self.backend == "hip" and method == "adjoint":
             nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
-            return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step, out_loss, out_correct)
-        res = self._loss_and_grads(xang, y, wmask, params, method, spsa_c, rng_keys, readout_keys, step)
+            return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step, out_loss,
+                                           out_correct, init)
+        res = self._loss_and_grads(xang, y, wmask, params, method, spsa_c, rng_keys, readout_keys, step, init)
         if out_loss is not None:
             out_loss.copy_(res["loss"])
             res["loss"] = out_loss
@@ -136,21 +150,22 @@ class VQCEngine:
             res["correct"] = out_correct
         return res
 
-    def _loss_and_grads(self, xang, y, wmask, params, method, spsa_c, rng_keys, readout_keys, step) -> dict:
+    def _loss_and_grads(self, xang, y, wmask, params, method, spsa_c, rng_keys, readout_keys, step,
+                        init=None) -> dict:
         spec = self.spec
         th, a, b = spec.split(params)
         if method == "autograd":
-            return self._autograd(xang, y, wmask, params)
+            return self._autograd(xang, y, wmask, params, init)
         K, B, _ = xang.shape
         P = spec.n_theta
         with torch.no_grad():
             rows = psi = None
             if method == "adjoint":          # torch backend: keep psi for the reverse sweep
                 rows = self._rows(xang, th)
-                psi = self.prog.run(rows)
+                psi = self.prog.run(rows, state=self._init_rows(init))
                 expz = self._readout(self.prog.expz(psi, spec.readout).reshape(K, B, -1).float(), readout_keys, step)
             else:                            # HIP or torch forward, readout noise applied
-                expz = self.expz(xang, th, readout_keys, step)
+                expz = self.expz(xang, th, readout_keys, step, init)
             loss, w, ga, gb, correct = ce_readout(expz, y, wmask, a, b)
             if method == "adjoint":
                 if self.noise is not None:   # straight-through d<Z>_noisy / d<Z> for the exact adjoint
@@ -161,18 +176,18 @@ class VQCEngine:
             elif method == "param_shift":
                 # shifted expectations carry the readout channel themselves: w = dL/d<Z>_noisy unscaled
                 if self._simple_shift_slots():
-                    gth = self.param_shift_batched(xang, params, w, readout_keys, step)
+                    gth = self.param_shift_batched(xang, params, w, readout_keys, step, init)
                 else:
-                    gth = self._param_shift(self._rows(xang, th), w, K, B)
+                    gth = self._param_shift(self._rows(xang, th), w, K, B, init=init)
             elif method == "spsa":
-                gth = self._spsa(xang, y, wmask, params, spsa_c, rng_keys)
+                gth = self._spsa(xang, y, wmask, params, spsa_c, rng_keys, init)
             else:
                 raise ValueError(f"unknown grad method '{method}'")
         grad = torch.cat([gth, ga, gb], -1)
         return {"loss": loss, "grad": grad, "correct": correct, "expz": expz}
 
     def _param_shift(self, rows: torch.Tensor, w: torch.Tensor, K: int, B: int,
-                     chunk: int = 32) -> torch.Tensor:
+                     chunk: int = 32, init: Optional[torch.Tensor] = None) -> torch.Tensor:
         """d<O>/dangle_g = 0.5 (<O>(angle+pi/2) - <O>(angle-pi/2)) for every theta gate."""
         prog, spec = self.prog, self.spec
         P = spec.n_theta
@@ -188,7 +203,10 @@ class VQCEngine:
                 ang[2 * i, :, g] += math.pi / 2
                 ang[2 * i + 1, :, g] -= math.pi / 2
             ang = ang.reshape(-1, base.shape[1])
-            st = prog.initial_state(ang.shape[0])
+            if init is None:
+                st = prog.initial_state(ang.shape[0])
+            else:
+                st = self._init_rows(init).repeat(2 * G2, 1)
             for g in range(len(prog.ops_list)):
                 st = prog.apply_gate(st, g, ang[:, g])
             z = prog.expz(st, spec.readout).reshape(G2, 2, rows.shape[0], -1)
@@ -223,7 +241,8 @@ class VQCEngine:
         return self._budget
 
     def param_shift_batched(self, xang: torch.Tensor, params: torch.Tensor, w: torch.Tensor,
-                            readout_keys: Optional[torch.Tensor] = None, step: int = 0) -> torch.Tensor:
+                            readout_keys: Optional[torch.Tensor] = None, step: int = 0,
+                            init: Optional[torch.Tensor] = None) -> torch.Tensor:
         """dL/dtheta by the parameter-shift rule (ROADMAP.md:23,130-135).
 
         Every (client k, slot j, sign) is one parameter row theta_k +- pi/2 e_j over the client's B
@@ -251,35 +270,35 @@ class VQCEngine:
                 keys = readout_keys[k].clone()
                 keys[:, 0] = (keys[:, 0] ^ ((j + 1) * 0x9E3779B9)) & 0xFFFFFFFF
                 keys[:, 1] = (keys[:, 1] + (j + 1) * 0x85EBCA6B) & 0xFFFFFFFF
-            z = self.expz(xang[k], th, keys, step).double()                       # [rows, B, C]
+            z = self.expz(xang[k], th, keys, step, None if init is None else init[k]).double()                       # [rows, B, C]
             contrib_all[r] = (z * w[k].double()).sum((1, 2)) * (0.5 * sign.double())   # [rows]
         # row r = (k, slot, sign): fixed-order pair sum (no atomics -> deterministic)
         return contrib_all.view(K, P, 2).sum(-1).float()
 
-    def _loss_only(self, xang, y, wmask, params):
+    def _loss_only(self, xang, y, wmask, params, init=None):
         th, a, b = self.spec.split(params)
-        z = self.expz(xang, th)
+        z = self.expz(xang, th, init=init)
         return ce_readout(z, y, wmask, a, b)[0]
 
-    def _spsa(self, xang, y, wmask, params, c: float, rng_keys: tuple) -> torch.Tensor:
+    def _spsa(self, xang, y, wmask, params, c: float, rng_keys: tuple, init=None) -> torch.Tensor:
         P = self.spec.n_theta
         K = params.shape[0]
         g = generator(*rng_keys, "spsa")
         delta = (torch.randint(0, 2, (K, P), generator=g) * 2 - 1).to(params)
         pad = torch.zeros(K, params.shape[1] - P, dtype=params.dtype, device=params.device)
         d = torch.cat([delta.to(params.device), pad], -1)
-        lp = self._loss_only(xang, y, wmask, params + c * d)
-        lm = self._loss_only(xang, y, wmask, params - c * d)
+        lp = self._loss_only(xang, y, wmask, params + c * d, init)
+        lm = self._loss_only(xang, y, wmask, params - c * d, init)
         return ((lp - lm) / (2 * c)).unsqueeze(-1) * delta.to(params.device)
 
-    def _autograd(self, xang, y, wmask, params):
+    def _autograd(self, xang, y, wmask, params, init=None):
         spec = self.spec
         K, B, _ = xang.shape
         p = params.detach().clone().double().requires_grad_(True)
         th, a, b = spec.split(p)
         prog = TorchProgram(self.ops, self.coef, spec.n_qubits, params.device, torch.complex128)
         rows = self._rows(xang.double(), th)
-        psi = prog.run(rows)
+        psi = prog.run(rows, state=None if init is None else init.reshape(K * B, -1).to(prog.dtype))
         expz = prog.expz(psi, spec.readout).reshape(K, B, -1)
         logits = logits_from_expz(expz, a, b)
         nll = -torch.log_softmax(logits, -1).gather(-1, y.unsqueeze(-1)).squeeze(-1)

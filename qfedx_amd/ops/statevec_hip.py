@@ -134,16 +134,19 @@ class HipProgram:
 
     # ------------------------------------------------------------------ forward / eval
     @torch.no_grad()
-    def expz(self, xang: torch.Tensor, theta: torch.Tensor, noise=None, keys=None, step: int = 0) -> torch.Tensor:
+    def expz(self, xang: torch.Tensor, theta: torch.Tensor, noise=None, keys=None, step: int = 0,
+             init: torch.Tensor | None = None) -> torch.Tensor:
         K, B, F = xang.shape
         if F != self.x_width:
             raise ValueError(f"expected {self.x_width} x-slot values per sample, got {F}")
         S = K * B
         x = xang.reshape(S, F).float().contiguous()
         th = theta.float().contiguous()
-        plan = self.eval_plan
+        plan = self.eval_plan if init is None else self._load_plan(FIN_READOUT)
         psi = self._buf("psi", S << self.n, self.state_torch_dtype)
         part = self._buf("part", S * plan.tiles_per_state * self.C, torch.float32)
+        if init is not None:
+            self._state_in(psi, init.reshape(S, -1))
         self._run_passes(plan, False, psi, None, th, B, x, None, part, None, S)
         out = self._buf("expz", S * self.C, torch.float32)
         ext().readout_sum(part, plan.tiles_per_state, self.C, S, out)
@@ -217,7 +220,9 @@ class HipProgram:
 
     # ------------------------------------------------------------------ train step
     def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
-                       out_correct=None) -> dict:
+                       out_correct=None, init: torch.Tensor | None = None) -> dict:
+        """One adjoint training step; ``init`` [K, B, 2^n] (amplitude encoding) starts the circuit from
+        the given states through the planner's load-from-state forward plan."""
         K, B, F = xang.shape
         if F != self.x_width:
             raise ValueError(f"expected {self.x_width} x-slot values per sample, got {F}")
@@ -227,12 +232,15 @@ class HipProgram:
         p = params.float().contiguous()
         yy = y.reshape(S).long().contiguous()
         ww = wmask.reshape(S).float().contiguous()
-        tr, adj = self.train_plan, self.adj_plan
+        tr = self.train_plan if init is None else self._load_plan(FIN_STORE | FIN_READOUT)
+        adj = self.adj_plan
         psi = self._buf("psi", S << self.n, self.state_torch_dtype)
         lam = self._buf("lam", S << self.n, self.state_torch_dtype)
         part = self._buf("part", S * tr.tiles_per_state * self.C, torch.float32)
         slab = self._buf("slab", S * adj.tiles_per_state * self.G, torch.float32)
         expz = self._buf("expz", S * self.C, torch.float32)
+        if init is not None:
+            self._state_in(psi, init.reshape(S, -1))
         wread = self._buf("wread", S * self.C, torch.float32)
         loss = torch.empty(K, dtype=torch.float32, device=self.device) if out_loss is None else out_loss
         correct = torch.empty(K, dtype=torch.float32, device=self.device) if out_correct is None else out_correct
