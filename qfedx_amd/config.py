@@ -103,6 +103,8 @@ class RuntimeConfig:
     checkpoint_every: int = 0
     resume: bool = False
     metrics_path: str = ""
+    tracking_dir: str = ""              # MLflow file-store root (e.g. ./mlruns); "" = off
+    experiment: str = ""                # tracking experiment name ("" = config name)
     log_every: int = 5
     overlap_comm: bool = True
     use_graphs: bool = True            # hipGraph capture of the local round (HIP backend)

@@ -81,7 +81,8 @@ class FederatedRunner:
         sl = shard_clients(int(yt.shape[0]), world.world_size, world.rank)
         self.X_test = Xt[sl[0]: sl[-1] + 1].to(device) if sl else Xt[:0].to(device)
         self.y_test = yt[sl[0]: sl[-1] + 1].to(device) if sl else yt[:0].to(device)
-        self.metrics = MetricsWriter(cfg.runtime.metrics_path, world.rank, cfg.to_dict())
+        self.metrics = MetricsWriter(cfg.runtime.metrics_path, world.rank, cfg.to_dict(), cfg.runtime.tracking_dir,
+                                     cfg.runtime.experiment or cfg.name)
         self.timer = PhaseTimer(device)
         self.start_round = 0
         self.history: list[dict] = []
@@ -128,13 +129,14 @@ class FederatedRunner:
     def save(self, round_num: int) -> None:
         rt = self.cfg.runtime
         if rt.checkpoint_dir and self.world.is_main:
-            save_checkpoint(rt.checkpoint_dir, round_num, {
+            path = save_checkpoint(rt.checkpoint_dir, round_num, {
                 "global_state": self.adapter.state_dict(self.params),
                 "accountant": json.dumps(self.accountant.state_dict()),
                 "config": self.cfg.to_dict(),
                 "metrics": self.history,
                 "seed": torch.tensor(self.cfg.train.seed),
             })
+            self.metrics.tracker.log_artifact(path, "checkpoints")
         barrier(self.world)
 
     def maybe_resume(self) -> None:

@@ -52,3 +52,29 @@ def test_cli_run_prints_summary(capsys):
     line = [l for l in capsys.readouterr().out.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     assert len(out["accuracies"]) == 2 and out["backend"] == "torch"
+
+
+def test_mlflow_file_store_tracking(tmp_path):
+    """ROADMAP.md:92-93: per-experiment config, metrics, checkpoints and artifacts in the MLflow file-store
+    layout (written without the mlflow package)."""
+    import glob
+    import os
+    import yaml
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.utils.tracking import FINISHED, read_metric
+    from tests.test_fl import small_cfg
+    root = tmp_path / "mlruns"
+    run_experiment(small_cfg(num_rounds=3, tracking_dir=str(root), experiment="unit", checkpoint_every=1,
+                             checkpoint_dir=str(tmp_path / "ck")))
+    exp = glob.glob(str(root / "*" / "meta.yaml"))
+    assert len(exp) == 1 and yaml.safe_load(open(exp[0]))["name"] == "unit"
+    runs = [d for d in glob.glob(str(root / "*" / "*")) if os.path.isdir(d)]
+    assert len(runs) == 1
+    run = runs[0]
+    meta = yaml.safe_load(open(os.path.join(run, "meta.yaml")))
+    assert meta["status"] == FINISHED and meta["end_time"] >= meta["start_time"]
+    assert open(os.path.join(run, "params", "train.num_rounds")).read() == "3"
+    acc = read_metric(run, "test_acc")
+    assert [s for _, _, s in acc] == [0, 1, 2, 3] and all(0.0 <= v <= 1.0 for _, v, _ in acc)
+    assert len(glob.glob(os.path.join(run, "artifacts", "checkpoints", "round_*.pt"))) == 3
+    assert yaml.safe_load(open(os.path.join(run, "artifacts", "config.yaml")))["train"]["num_rounds"] == 3
