@@ -56,6 +56,9 @@ int qfx_launch_readout_noise(float* expz, int C, int spc, long n_samples, float 
                              const long long* keys, unsigned stream, hipStream_t st);
 int qfx_launch_philox_uniform(const long long* keys, int K, long n, unsigned stream, float* out, hipStream_t st);
 int qfx_launch_readout_sum(const float* part, int tps, int C, long n_samples, float* expz, hipStream_t st);
+int qfx_amp_scratch(long F);
+int qfx_launch_amp_init(const float* x, long F, long ld, int n_samples, int n, double* part, void* psi, int bf16,
+                        hipStream_t stream);
 int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob, float* grad,
                            int p_stride, float* gpart, hipStream_t st);
 int qfx_grad_split(int tps, int spc);
@@ -165,6 +168,26 @@ void philox_uniform(torch::Tensor keys, int64_t n, int64_t stream, torch::Tensor
                                   ptr<float>(out), cur_stream()),
         "qfx_philox_uniform");
 }
+
+// amplitude encoding straight into pass storage: x [S, F] fp32 (row stride ld), psi complex64 [S, 2^n] or
+// int32 [S, 2^n] (packed bf16x2)
+void amp_init(torch::Tensor x, int64_t n, torch::Tensor part, torch::Tensor psi) {
+  need(x, torch::kFloat32, "x");
+  need(part, torch::kFloat64, "part");
+  if (x.dim() != 2 || x.stride(1) != 1) throw std::invalid_argument("amp_init: x must be [S, F] with unit inner stride");
+  const int64_t S = x.size(0), F = x.size(1);
+  if (n < 1 || n > 34 || F > (int64_t(1) << n)) throw std::invalid_argument("amp_init: need F <= 2^n");
+  const bool bf16 = psi.scalar_type() == torch::kInt32;
+  if (!bf16 && psi.scalar_type() != torch::kComplexFloat)
+    throw std::invalid_argument("amp_init: psi must be complex64 or int32 (bf16x2)");
+  if (!psi.is_contiguous() || psi.numel() < (S << n)) throw std::invalid_argument("amp_init: psi too small");
+  if (part.numel() < S * qfx_amp_scratch((long)F)) throw std::invalid_argument("amp_init: scratch too small");
+  check(qfx_launch_amp_init(ptr<float>(x), (long)F, (long)x.stride(0), (int)S, (int)n, ptr<double>(part),
+                            psi.data_ptr(), bf16 ? 1 : 0, cur_stream()),
+        "qfx_amp_init");
+}
+
+int64_t amp_scratch(int64_t F) { return qfx_amp_scratch((long)F); }
 
 void readout_sum(torch::Tensor part, int64_t tps, int64_t C, int64_t n_samples, torch::Tensor expz) {
   need(part, torch::kFloat32, "part");
@@ -296,6 +319,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pass_launch", &pass_launch);
   m.def("readout_ce", &readout_ce);
   m.def("readout_sum", &readout_sum);
+  m.def("amp_init", &amp_init);
+  m.def("amp_scratch", &amp_scratch);
   m.def("readout_noise", &readout_noise);
   m.def("philox_uniform", &philox_uniform);
   m.def("grad_reduce", &grad_reduce);

@@ -319,3 +319,79 @@ extern "C" int qfx_launch_pass(int R, int adjoint, const int* blob, int pass_off
 #undef QFX_L
   return (int)hipGetLastError();
 }
+
+// ----------------------------------------------------------------------------------- amplitude encoding (K9)
+// Raw features x[s, 0:F] (F <= N = 2^n, zero-padded) -> normalised state psi[s, 0:N] in logical order:
+// psi = x / ||x||_2 (float64 norm), a zero row -> the uniform state 1/sqrt(N) (reference
+// normalize_for_amplitude, qAmplitude.py:11-22).  Two deterministic stages: per-(chunk, sample) float64
+// partial sums of squares, then a write pass whose blocks first reduce their sample's partials in fixed
+// order.  The state is written directly in the pass storage format (complex64 or packed bf16x2).
+constexpr int AMP_CHUNK = 4096;
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) qfx_amp_norm_kernel(const float* __restrict__ x, long F, long ld, int nch,
+                                                          double* __restrict__ part) {
+  __shared__ double sm[4];
+  const long s = blockIdx.y;
+  const long beg = (long)blockIdx.x * AMP_CHUNK, end = beg + AMP_CHUNK < F ? beg + AMP_CHUNK : F;
+  const float* row = x + s * ld;
+  double acc = 0.0;
+  for (long i = beg + threadIdx.x; i < end; i += 256) {
+    const double v = row[i];
+    acc += v * v;
+  }
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[s * nch + blockIdx.x] = (sm[0] + sm[1]) + (sm[2] + sm[3]);
+}
+
+template <bool BF16>
+__global__ void __launch_bounds__(256) qfx_amp_write_kernel(const float* __restrict__ x, long F, long ld, int nch,
+                                                           const double* __restrict__ part, long N,
+                                                           void* __restrict__ psi) {
+  __shared__ double sm[4];
+  const long s = blockIdx.y;
+  double acc = 0.0;
+  for (int c = threadIdx.x; c < nch; c += 256) acc += part[s * nch + c];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  const double nrm2 = (sm[0] + sm[1]) + (sm[2] + sm[3]);
+  const bool zero = !(nrm2 > 0.0);
+  const double inv = zero ? 0.0 : 1.0 / sqrt(nrm2);
+  const float uni = (float)(1.0 / sqrt((double)N));
+  const float* row = x + s * ld;
+  const long beg = (long)blockIdx.x * AMP_CHUNK;
+  for (long i = beg + threadIdx.x; i < beg + AMP_CHUNK && i < N; i += 256) {
+    const float a = zero ? uni : (i < F ? (float)((double)row[i] * inv) : 0.0f);
+    if constexpr (BF16) {
+      static_cast<uint32_t*>(psi)[s * N + i] = qfx::pack_bf16x2(qfx::mk(a, 0.0f));
+    } else {
+      static_cast<float2*>(psi)[s * N + i] = make_float2(a, 0.0f);
+    }
+  }
+}
+
+extern "C" int qfx_amp_scratch(long F) { return (int)((F + AMP_CHUNK - 1) / AMP_CHUNK); }
+
+extern "C" int qfx_launch_amp_init(const float* x, long F, long ld, int n_samples, int n, double* part, void* psi,
+                                   int bf16, hipStream_t stream) {
+  const long N = 1L << n;
+  if (F > N || F <= 0 || ld < F || n_samples <= 0) return -2;
+  const int nch = (int)((F + AMP_CHUNK - 1) / AMP_CHUNK);
+  const unsigned wch = (unsigned)((N + AMP_CHUNK - 1) / AMP_CHUNK);
+  hipLaunchKernelGGL(qfx_amp_norm_kernel, dim3((unsigned)nch, (unsigned)n_samples), dim3(256), 0, stream, x, F, ld,
+                     nch, part);
+  if (bf16)
+    hipLaunchKernelGGL(qfx_amp_write_kernel<true>, dim3(wch, (unsigned)n_samples), dim3(256), 0, stream, x, F, ld, nch,
+                       part, N, psi);
+  else
+    hipLaunchKernelGGL(qfx_amp_write_kernel<false>, dim3(wch, (unsigned)n_samples), dim3(256), 0, stream, x, F, ld,
+                       nch, part, N, psi);
+  return (int)hipGetLastError();
+}

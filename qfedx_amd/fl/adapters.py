@@ -47,7 +47,7 @@ class VQCAdapter:
         if self.noise is not None:     # noisy device: one keyed trajectory per test sample, noisy readout
             xang = self.engine.augment(xang, self.noise.client_keys("noise_eval", chunk, [0], X.device), 0)
             ro_keys = self.noise.client_keys("shots_eval", chunk, [0], X.device)
-        return self.engine.predict(xang, params[None, :], ro_keys, 0, self.spec.initial_states(X[None]))[0]
+        return self.engine.predict(xang, params[None, :], ro_keys, 0, X[None] if self.spec.amplitude else None)[0]
 
     @torch.no_grad()
     def evaluate(self, params: torch.Tensor, X: torch.Tensor, y: torch.Tensor):

@@ -153,7 +153,7 @@ class VQCClientTrainer:
             xang = self.engine.augment(self.encode(xb), traj_keys, s)
             res = self.engine.loss_and_grads(xang, yb, ws, params, method, rng_keys=(cfg.seed, round_num, s),
                                              readout_keys=ro_keys, step=s, out_loss=loss_all[s],
-                                             out_correct=correct_all[s], init=self.spec.initial_states(xb))
+                                             out_correct=correct_all[s], init=xb if self.spec.amplitude else None)
             opt.step(params, res["grad"], act_d[s])
         return params, loss_all, correct_all
 

@@ -68,15 +68,25 @@ class VQCEngine:
             raise ValueError(f"unknown backend '{backend}'")
 
     # ------------------------------------------------------------------ helpers
+    def _states(self, init: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+        """Initial states [.., 2^n] complex: real ``init`` holds raw amplitudes (encoded here, on the HIP
+        backend by the device kernel instead); complex ``init`` is used as given."""
+        if init is None or init.is_complex():
+            return init
+        return self.spec.initial_states(init)
+
     def _init_rows(self, init: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
-        """[K,B,2^n] initial states -> [K*B, 2^n] in the torch executor's dtype (None passes through)."""
-        return None if init is None else init.reshape(-1, init.shape[-1]).to(self.prog.dtype)
+        """[K,B,..] initial states -> [K*B, 2^n] in the torch executor's dtype (None passes through)."""
+        st = self._states(init)
+        return None if st is None else st.reshape(-1, st.shape[-1]).to(self.prog.dtype)
 
     def _check(self, xang: torch.Tensor, init: Optional[torch.Tensor] = None) -> None:
         if self.spec.amplitude:
-            if init is None or init.shape[:-1] != xang.shape[:-1] or init.shape[-1] != (1 << self.spec.n_qubits):
-                raise ValueError("amplitude-encoded VQC needs init states [K, B, 2^n] "
-                                 "(VQCSpec.initial_states of the raw features)")
+            N = 1 << self.spec.n_qubits
+            if (init is None or init.shape[:-1] != xang.shape[:-1]
+                    or (init.shape[-1] != N if init.is_complex() else init.shape[-1] > N)):
+                raise ValueError("amplitude-encoded VQC needs init [K, B, <=2^n] raw amplitudes (or complex "
+                                 "states [K, B, 2^n])")
         elif init is not None:
             raise ValueError("initial states are only used by feature_map='amplitude'")
         # the angle feature map reads one feature per qubit: a narrower input would make the
@@ -109,8 +119,8 @@ class VQCEngine:
     def expz(self, xang: torch.Tensor, theta: torch.Tensor, readout_keys: Optional[torch.Tensor] = None,
              step: int = 0, init: Optional[torch.Tensor] = None) -> torch.Tensor:
         """<Z_c> for [K,B,x_width] encoded features and per-client theta [K,P] -> [K,B,C] (with the
-        readout noise model applied when one is configured).  ``init`` [K,B,2^n]: amplitude-encoded
-        initial states (``VQCSpec.initial_states``)."""
+        readout noise model applied when one is configured).  ``init`` (amplitude encoding): raw
+        amplitudes [K,B,F<=2^n] (normalised on device) or complex initial states [K,B,2^n]."""
         K, B, _ = xang.shape
         self._check(xang, init)
         if self.backend == "hip":
@@ -134,7 +144,7 @@ class VQCEngine:
                        out_correct: Optional[torch.Tensor] = None, init: Optional[torch.Tensor] = None) -> dict:
         """Loss [K], gradient [K,P], correct [K] for [K,B] minibatches.  ``out_loss`` / ``out_correct``
         (optional [K] views, e.g. rows of a round buffer) receive the loss / hit counts in place.
-        ``init`` [K,B,2^n] = amplitude-encoded initial states (None for angle encodings)."""
+        ``init`` = raw amplitudes [K,B,F<=2^n] or complex states (amplitude encoding; None otherwise)."""
         spec = self.spec
         self._check(xang, init)
         if self.backend == "hip" and method == "adjoint":
@@ -298,7 +308,8 @@ class VQCEngine:
         th, a, b = spec.split(p)
         prog = TorchProgram(self.ops, self.coef, spec.n_qubits, params.device, torch.complex128)
         rows = self._rows(xang.double(), th)
-        psi = prog.run(rows, state=None if init is None else init.reshape(K * B, -1).to(prog.dtype))
+        st = self._states(init)
+        psi = prog.run(rows, state=None if st is None else st.reshape(K * B, -1).to(prog.dtype))
         expz = prog.expz(psi, spec.readout).reshape(K, B, -1)
         logits = logits_from_expz(expz, a, b)
         nll = -torch.log_softmax(logits, -1).gather(-1, y.unsqueeze(-1)).squeeze(-1)

@@ -165,9 +165,18 @@ class HipProgram:
         return cache[fin]
 
     def _state_in(self, psi: torch.Tensor, init: torch.Tensor) -> None:
-        if self.bf16:
-            raise NotImplementedError("initial states are loaded in complex64 storage only")
-        psi.view(init.shape[0], -1).copy_(init.to(torch.complex64))
+        """Initial states into the pass workspace.  Real ``init`` [S, F <= 2^n] = raw amplitudes, encoded
+        on device (zero-pad, float64 L2 normalisation, zero row -> uniform) straight into the
+        storage format; complex ``init`` [S, 2^n] = states used as given (complex64 storage)."""
+        if init.is_complex():
+            if self.bf16:
+                raise NotImplementedError("explicit complex initial states need complex64 storage; pass real "
+                                          "amplitudes to encode them on device")
+            psi.view(init.shape[0], -1).copy_(init.to(torch.complex64))
+            return
+        x = init.reshape(init.shape[0], -1).float().contiguous()
+        part = self._buf("amp_part", x.shape[0] * ext().amp_scratch(x.shape[1]), torch.float64)
+        ext().amp_init(x, self.n, part, psi)
 
     @torch.no_grad()
     def statevector(self, xang: torch.Tensor, theta: torch.Tensor, init: torch.Tensor | None = None):

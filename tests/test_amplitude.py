@@ -92,3 +92,14 @@ def test_amplitude_federated_run_cpu():
     out = run_experiment(small_cfg(num_rounds=3, feature_map="amplitude", n_qubits=3))
     assert np.isfinite(out["accuracies"][-1])
     assert out["history"][-1]["train_loss"] < out["history"][0]["train_loss"] + 1e-6
+
+
+def test_amplitude_raw_init_equals_states():
+    spec, x, y, w, params = _amp_setup(n=4, seed=5)
+    eng = VQCEngine(spec, "cpu", "torch")
+    xa = spec.encode_features(x)
+    a = eng.loss_and_grads(xa, y, w, params, "adjoint", init=x)
+    b = eng.loss_and_grads(xa, y, w, params, "adjoint", init=spec.initial_states(x))
+    assert torch.equal(a["grad"], b["grad"]) and torch.equal(a["loss"], b["loss"])
+    with pytest.raises(ValueError):
+        eng.loss_and_grads(xa, y, w, params, "adjoint", init=torch.rand(2, 5, 17))   # > 2^n raw amplitudes

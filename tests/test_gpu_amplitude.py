@@ -47,3 +47,39 @@ def test_amplitude_federated_hip_matches_cpu(cuda):
             tr.VQCClientTrainer.use_graph = old
     assert torch.equal(outs[0]["params"], outs[1]["params"])
     assert torch.allclose(outs[0]["params"].cpu(), cpu["params"], atol=1e-4)
+
+
+@pytest.mark.parametrize("n,F", [(4, 16), (4, 11), (13, 8192), (14, 5000), (20, 1 << 20)])
+def test_amp_init_kernel_matches_torch(cuda, n, F):
+    """K9: device amplitude encoding (float64 norm, zero-pad, zero row -> uniform) == torch reference,
+    written straight into complex64 and packed-bf16 pass storage."""
+    from qfedx_amd.ops._ext import ext
+    from qfedx_amd.quantum.encoders import amplitude_states
+    S = 3
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(S, F, generator=g)
+    x[1] = 0.0                                                  # zero row -> uniform state
+    N = 1 << n
+    ref = amplitude_states(torch.cat([x, x.new_zeros(S, N - F)], 1))
+    xc = x.to(cuda)
+    part = torch.empty(S * ext().amp_scratch(F), dtype=torch.float64, device=cuda)
+    psi = torch.empty(S * N, dtype=torch.complex64, device=cuda)
+    ext().amp_init(xc, n, part, psi)
+    assert torch.allclose(psi.view(S, N).cpu(), ref, atol=1e-7, rtol=1e-6)
+    packed = torch.empty(S * N, dtype=torch.int32, device=cuda)
+    ext().amp_init(xc, n, part, packed)
+    re = (packed.view(S, N) << 16).view(torch.float32).cpu()
+    assert torch.allclose(re, ref.real, atol=1e-6, rtol=1e-2)
+    assert torch.equal(re, ref.real.to(torch.bfloat16).float())   # RNE rounding like torch
+
+
+def test_amplitude_raw_features_bf16_storage(cuda):
+    spec, x, y, w, params = _amp_setup(12, 2, 3, 2, 4, seed=7)
+    xc = x.to(cuda)
+    f32 = VQCEngine(spec, cuda, "hip", "fp32").expz(spec.encode_features(xc), spec.split(params.to(cuda))[0],
+                                                     init=xc)
+    b16 = VQCEngine(spec, cuda, "hip", "bf16").expz(spec.encode_features(xc), spec.split(params.to(cuda))[0],
+                                                     init=xc)
+    ref = VQCEngine(spec, "cpu", "torch").expz(spec.encode_features(x), spec.split(params)[0], init=x)
+    assert torch.allclose(f32.cpu(), ref, atol=2e-5)
+    assert (b16.cpu() - ref).abs().max() < 2e-2
