@@ -66,10 +66,15 @@ int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float*
                           const float* act, int n, double samples, double steps, hipStream_t st);
 int qfx_launch_round_apply(const long long* buf, int P, float* theta, double lr, double* out, hipStream_t st);
 int qfx_fedavg_norm_scratch(int K, int P);
-int qfx_launch_adam(float* p, const float* g, float* m, float* v, float* t, const float* active, int K, int P,
-                    float lr, float b1, float b2, float eps, hipStream_t st);
-int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, const float* active, int K, int P, float lr,
-                    float mu, hipStream_t st);
+int qfx_launch_adam(float* p, const float* g, float* m, float* v, const float* t_in, float* t_out,
+                    const float* active, int K, int P, float lr, float b1, float b2, float eps, hipStream_t st);
+int qfx_launch_sgdm(float* p, const float* g, float* buf, const float* t_in, float* t_out, const float* active,
+                    int K, int P, float lr, float mu, hipStream_t st);
+int qfx_launch_round_init(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
+                          hipStream_t st);
+int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx, int K,
+                            int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride, long long* yo,
+                            hipStream_t st);
 int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
                       const double* weights, double* norms, const uint32_t* keys, int K, int P, int wrap, int dp,
                       float clip, float sigma, long long* out, hipStream_t st);
@@ -231,21 +236,72 @@ void grad_reduce(torch::Tensor slab, int64_t tps, int64_t spc, int64_t K, int64_
         "qfx_grad_reduce");
 }
 
-void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor t, torch::Tensor active,
-          double lr, double b1, double b2, double eps) {
+void check_counters(const torch::Tensor& p, const torch::Tensor& t_in, const torch::Tensor& t_out,
+                    const torch::Tensor& active) {
+  for (auto* x : {&t_in, &t_out, &active}) need(*x, torch::kFloat32, "optimizer counter/mask");
+  if (t_in.numel() < p.size(0) || t_out.numel() < p.size(0) || active.numel() < p.size(0))
+    throw std::invalid_argument("optimizer: counters / mask need one entry per client row");
+  if (t_in.data_ptr() == t_out.data_ptr()) throw std::invalid_argument("optimizer: t_in and t_out must differ");
+}
+
+void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, torch::Tensor t_in, torch::Tensor t_out,
+          torch::Tensor active, double lr, double b1, double b2, double eps) {
   for (auto* x : {&p, &g, &m, &v}) need(*x, torch::kFloat32, "adam tensor");
-  check(qfx_launch_adam(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), ptr<float>(t),
-                        ptr<float>(active), (int)p.size(0), (int)p.size(1), (float)lr, (float)b1, (float)b2,
-                        (float)eps, cur_stream()),
+  check_counters(p, t_in, t_out, active);
+  check(qfx_launch_adam(ptr<float>(p), ptr<float>(g), ptr<float>(m), ptr<float>(v), ptr<float>(t_in),
+                        ptr<float>(t_out), ptr<float>(active), (int)p.size(0), (int)p.size(1), (float)lr, (float)b1,
+                        (float)b2, (float)eps, cur_stream()),
         "qfx_adam");
 }
 
-void sgdm(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor t, torch::Tensor active, double lr,
-          double mu) {
+void sgdm(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor t_in, torch::Tensor t_out,
+          torch::Tensor active, double lr, double mu) {
   for (auto* x : {&p, &g, &buf}) need(*x, torch::kFloat32, "sgd tensor");
-  check(qfx_launch_sgdm(ptr<float>(p), ptr<float>(g), ptr<float>(buf), ptr<float>(t), ptr<float>(active),
-                        (int)p.size(0), (int)p.size(1), (float)lr, (float)mu, cur_stream()),
+  check_counters(p, t_in, t_out, active);
+  check(qfx_launch_sgdm(ptr<float>(p), ptr<float>(g), ptr<float>(buf), ptr<float>(t_in), ptr<float>(t_out),
+                        ptr<float>(active), (int)p.size(0), (int)p.size(1), (float)lr, (float)mu, cur_stream()),
         "qfx_sgdm");
+}
+
+// params[k, :] = theta; optional m, v (same shape) and t (any length) zeroed
+void round_init(torch::Tensor theta, torch::Tensor params, c10::optional<torch::Tensor> m,
+                c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> t) {
+  need(theta, torch::kFloat32, "theta");
+  need(params, torch::kFloat32, "params");
+  const int64_t K = params.size(0), P = params.size(1);
+  if (theta.numel() != P) throw std::invalid_argument("round_init: theta size != params row");
+  torch::Tensor mt = m ? *m : torch::Tensor(), vt = v ? *v : torch::Tensor(), tt = t ? *t : torch::Tensor();
+  for (auto* x : {&mt, &vt})
+    if (x->defined()) {
+      need(*x, torch::kFloat32, "round_init state");
+      if (x->numel() != K * P) throw std::invalid_argument("round_init: state shape");
+    }
+  if (tt.defined()) need(tt, torch::kFloat32, "round_init t");
+  check(qfx_launch_round_init(ptr<float>(theta), (int)K, (int)P, ptr<float>(params), ptr<float>(mt), ptr<float>(vt),
+                              ptr<float>(tt), tt.defined() ? (int)tt.numel() : 0, cur_stream()),
+        "qfx_round_init");
+}
+
+// X [Nc, nmax, F] fp32, Y [Nc, nmax] int64, lid [K] int64, idx [K, B] int64 (rows < nmax, checked by the
+// planner on the host) -> x_out rows of stride x_stride (first F columns), y_out [K*B]
+void batch_gather(torch::Tensor X, torch::Tensor Y, torch::Tensor lid, torch::Tensor idx, int64_t mode, double alpha,
+                  torch::Tensor x_out, torch::Tensor y_out) {
+  need(X, torch::kFloat32, "X");
+  need(Y, torch::kInt64, "Y");
+  need(lid, torch::kInt64, "lid");
+  need(idx, torch::kInt64, "idx");
+  need(x_out, torch::kFloat32, "x_out");
+  need(y_out, torch::kInt64, "y_out");
+  if (X.dim() != 3 || Y.dim() != 2 || idx.dim() != 2 || Y.size(1) != X.size(1))
+    throw std::invalid_argument("batch_gather: shapes");
+  const int64_t K = idx.size(0), B = idx.size(1), F = X.size(2);
+  if (lid.numel() != K || x_out.dim() != 3 || x_out.size(0) != K || x_out.size(1) != B || x_out.size(2) < F ||
+      !x_out.is_contiguous() || y_out.numel() < K * B || mode < 0 || mode > 2)
+    throw std::invalid_argument("batch_gather: output shapes / mode");
+  check(qfx_launch_batch_gather(ptr<float>(X), ptr<long long>(Y), ptr<long long>(lid), ptr<long long>(idx), (int)K,
+                                (int)B, (long)X.size(1), (int)F, (int)mode, (float)alpha, ptr<float>(x_out),
+                                (int)x_out.size(2), ptr<long long>(y_out), cur_stream()),
+        "qfx_batch_gather");
 }
 
 void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_mask, torch::Tensor weights,
@@ -320,6 +376,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("readout_ce", &readout_ce);
   m.def("readout_sum", &readout_sum);
   m.def("amp_init", &amp_init);
+  m.def("round_init", &round_init);
+  m.def("batch_gather", &batch_gather);
   m.def("amp_scratch", &amp_scratch);
   m.def("readout_noise", &readout_noise);
   m.def("philox_uniform", &philox_uniform);

@@ -200,15 +200,19 @@ __global__ void __launch_bounds__(256) qfx_grad_slots_kernel(const float* __rest
 }
 
 // fused client-batched Adam: rows with active[k]==0 untouched
+// The per-client step counter ping-pongs between two buffers (t_in read by the whole row, t_out = t_in +
+// active written by the row's first element), so no separate counter launch is needed.
 __global__ void qfx_adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                                float* __restrict__ v, float* __restrict__ t, const float* __restrict__ active,
-                                int K, int P, float lr, float b1, float b2, float eps) {
+                                float* __restrict__ v, const float* __restrict__ t_in, float* __restrict__ t_out,
+                                const float* __restrict__ active, int K, int P, float lr, float b1, float b2,
+                                float eps) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)K * P) return;
   const int k = (int)(i / P);
   const float act = active[k];
+  const float tk = t_in[k] + act;
+  if (i == (long)k * P) t_out[k] = tk;
   if (act == 0.f) return;
-  const float tk = t[k] + 1.f;   // t incremented by the row-0 thread of each row after the step
   const float gi = g[i];
   const float mi = b1 * m[i] + (1.f - b1) * gi;
   const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
@@ -219,20 +223,17 @@ __global__ void qfx_adam_kernel(float* __restrict__ p, const float* __restrict__
   p[i] -= lr * mh / (sqrtf(vh) + eps);
 }
 
-__global__ void qfx_step_count_kernel(float* __restrict__ t, const float* __restrict__ active, int K) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < K) t[k] += active[k];
-}
-
 // torch.optim.SGD(momentum) semantics: buf = g on the first step, else mu*buf + g; p -= lr*buf
 __global__ void qfx_sgdm_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
-                                const float* __restrict__ t, const float* __restrict__ active, int K, int P,
-                                float lr, float mu) {
+                                const float* __restrict__ t_in, float* __restrict__ t_out,
+                                const float* __restrict__ active, int K, int P, float lr, float mu) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)K * P) return;
   const int k = (int)(i / P);
-  if (active[k] == 0.f) return;
-  const float b = (t[k] == 0.f) ? g[i] : fmaf(mu, buf[i], g[i]);
+  const float act = active[k];
+  if (i == (long)k * P) t_out[k] = t_in[k] + act;
+  if (act == 0.f) return;
+  const float b = (t_in[k] == 0.f) ? g[i] : fmaf(mu, buf[i], g[i]);
   buf[i] = b;
   p[i] -= lr * b;
 }
@@ -417,21 +418,98 @@ extern "C" int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_launch_adam(float* p, const float* g, float* m, float* v, float* t, const float* active,
-                               int K, int P, float lr, float b1, float b2, float eps, hipStream_t st) {
+extern "C" int qfx_launch_adam(float* p, const float* g, float* m, float* v, const float* t_in, float* t_out,
+                               const float* active, int K, int P, float lr, float b1, float b2, float eps,
+                               hipStream_t st) {
   const long tot = (long)K * P;
-  hipLaunchKernelGGL(qfx_adam_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, p, g, m, v, t,
-                     active, K, P, lr, b1, b2, eps);
-  hipLaunchKernelGGL(qfx_step_count_kernel, dim3((K + 255) / 256), dim3(256), 0, st, t, active, K);
+  hipLaunchKernelGGL(qfx_adam_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, p, g, m, v, t_in,
+                     t_out, active, K, P, lr, b1, b2, eps);
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_launch_sgdm(float* p, const float* g, float* buf, float* t, const float* active, int K,
-                               int P, float lr, float mu, hipStream_t st) {
+extern "C" int qfx_launch_sgdm(float* p, const float* g, float* buf, const float* t_in, float* t_out,
+                               const float* active, int K, int P, float lr, float mu, hipStream_t st) {
   const long tot = (long)K * P;
-  hipLaunchKernelGGL(qfx_sgdm_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, p, g, buf, t,
-                     active, K, P, lr, mu);
-  hipLaunchKernelGGL(qfx_step_count_kernel, dim3((K + 255) / 256), dim3(256), 0, st, t, active, K);
+  hipLaunchKernelGGL(qfx_sgdm_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, p, g, buf, t_in,
+                     t_out, active, K, P, lr, mu);
+  return (int)hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------------- round prologue
+// local round start: every client row starts from the global params; optimizer moments / counters zeroed
+__global__ void qfx_round_init_kernel(const float* __restrict__ theta, int K, int P, float* __restrict__ params,
+                                      float* __restrict__ m, float* __restrict__ v, float* __restrict__ t, int nt) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (long)K * P) {
+    params[i] = theta[i % P];
+    if (m) m[i] = 0.f;
+    if (v) v[i] = 0.f;
+  }
+  if (t && i < nt) t[i] = 0.f;
+}
+
+extern "C" int qfx_launch_round_init(const float* theta, int K, int P, float* params, float* m, float* v, float* t,
+                                     int nt, hipStream_t st) {
+  const long tot = (long)K * P > nt ? (long)K * P : nt;
+  hipLaunchKernelGGL(qfx_round_init_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, theta, K, P,
+                     params, m, v, t, nt);
+  return (int)hipGetLastError();
+}
+
+// per-step minibatch gather + feature encoding, one block per sample s = k*B + b:
+//   x_out[s, 0:F] = enc(X[lid[k], idx[s], 0:F]),  y_out[s] = Y[lid[k], idx[s]]
+// enc: 0 = alpha * x (ROADMAP RY(alpha x)), 1 = per-sample min-max -> pi * x^ (qAngle.py:36-41; constant
+// rows -> 0), 2 = raw copy (amplitude encoding: normalised later by the state-load kernel)
+__global__ void __launch_bounds__(256) qfx_batch_gather_kernel(
+    const float* __restrict__ X, const long long* __restrict__ Y, const long long* __restrict__ lid,
+    const long long* __restrict__ idx, int B, long nmax, int F, int mode, float alpha, float* __restrict__ xo,
+    int x_stride, long long* __restrict__ yo) {
+  __shared__ float smn[4], smx[4];
+  const long s = blockIdx.x;
+  const long row = lid[s / B] * nmax + idx[s];
+  const float* xr = X + row * F;
+  float* out = xo + s * (long)x_stride;
+  if (threadIdx.x == 0) yo[s] = Y[row];
+  if (mode == 1) {
+    float mn = INFINITY, mx = -INFINITY;
+    for (int f = threadIdx.x; f < F; f += blockDim.x) {
+      const float v = xr[f];
+      mn = fminf(mn, v);
+      mx = fmaxf(mx, v);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      mn = fminf(mn, __shfl_xor(mn, o, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    }
+    const int nw = blockDim.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      smn[threadIdx.x >> 6] = mn;
+      smx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    mn = smn[0];
+    mx = smx[0];
+    for (int w = 1; w < nw; ++w) {
+      mn = fminf(mn, smn[w]);
+      mx = fmaxf(mx, smx[w]);
+    }
+    const float rng = mx - mn;
+    const float pi_f = 3.14159265358979323846f;
+    for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = rng > 0.f ? ((xr[f] - mn) / rng) * pi_f : 0.f;
+  } else if (mode == 0) {
+    for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = alpha * xr[f];
+  } else {
+    for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = xr[f];
+  }
+}
+
+extern "C" int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx,
+                                       int K, int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride,
+                                       long long* yo, hipStream_t st) {
+  if (K <= 0 || B <= 0) return 0;
+  const int threads = F > 64 ? 256 : 64;
+  hipLaunchKernelGGL(qfx_batch_gather_kernel, dim3((unsigned)((long)K * B)), dim3(threads), 0, st, X, Y, lid, idx, B,
+                     nmax, F, mode, alpha, xo, x_stride, yo);
   return (int)hipGetLastError();
 }
 

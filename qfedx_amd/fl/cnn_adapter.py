@@ -55,20 +55,34 @@ class CNNClientTrainer:
         plan = BatchPlan(store.counts[li], cids, cfg.batch_size, round_num, cfg.seed, cfg.local_epochs,
                          cfg.local_steps)
         nvalid = (plan.wts > 0).sum(-1).float() * plan.active
+        if plan.idx.numel() and int(plan.idx.max()) >= max(1, store.nmax):
+            raise RuntimeError("minibatch plan indexes past the client store")
         dv = PackedUpload({"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active,
                            "nvalid": nvalid}).to_device(self.device)
-        params = theta_g.to(self.device).float()[None, :].repeat(K, 1).contiguous()
+        params = torch.empty(K, P, dtype=torch.float32, device=self.device)
         opt = BatchedOptimizer(cfg.optimizer if cfg.optimizer != "spsa" else "sgd", (K, P), self.device,
-                               cfg.learning_rate, cfg.momentum, backend=self.backend)
-        X = store.X[dv["lid"]]
-        Y = store.y[dv["lid"]]
-        kar = torch.arange(K, device=self.device)[:, None]
+                               cfg.learning_rate, cfg.momentum, backend=self.backend, zero_init=False)
+        opt.init_round(params, theta_g.to(self.device).float())
         S = plan.max_steps
         loss_all = torch.empty(S, K, dtype=torch.float32, device=self.device)
         correct_all = torch.empty(S, K, dtype=torch.float32, device=self.device)
+        fused = self.backend == "hip" and store.X.is_cuda
+        if fused:   # minibatches gathered straight from the device store by slot (no per-round shard copy)
+            from ..ops._ext import ext
+            img = tuple(store.X.shape[2:])
+            Xf = store.X.view(store.X.shape[0], store.X.shape[1], -1)
+            B = plan.B
+            xbuf = torch.empty(K, B, Xf.shape[-1], dtype=torch.float32, device=self.device)
+            ybuf = torch.empty(K * B, dtype=torch.int64, device=self.device)
+        else:
+            rows = dv["lid"][:, None]
         for s in range(S):
-            xb = X[kar, dv["idx"][s]]
-            yb = Y[kar, dv["idx"][s]]
+            if fused:
+                ext().batch_gather(Xf, store.y, dv["lid"], dv["idx"][s], 2, 1.0, xbuf, ybuf)
+                xb, yb = xbuf.view(K, B, *img), ybuf.view(K, B)
+            else:
+                xb = store.X[rows, dv["idx"][s]]
+                yb = store.y[rows, dv["idx"][s]]
             mask = tc.dropout_masks(cids, cfg.batch_size, cfg.seed, round_num, s, self.device)
             res = self.loss_and_grads(params, xb, yb, dv["wts"][s], mask)
             opt.step(params, res["grad"], dv["act"][s])

@@ -4,8 +4,9 @@ Reference: a fresh ``SGD(lr, momentum=0.9)`` per client per round (``Classical_F
 momentum resets every round.  ROADMAP.md:38 adds Adam and SPSA.  State is allocated per round
 (reset) by default, matching the reference; ``persistent=True`` keeps it across rounds.
 
-On GPU the update runs as one fused kernel over all clients (``qfx_adam_step`` /
-``qfx_sgdm_step`` in ``csrc/fedavg.hip``); the torch version here is the CPU path / oracle.
+On GPU the update runs as one fused kernel over all clients (``qfx_adam_kernel`` /
+``qfx_sgdm_kernel`` in ``csrc/train_kernels.hip``; the per-client step counter ping-pongs between two
+buffers so the counter update needs no launch of its own); the torch version is the CPU path / oracle.
 Rows with ``active[k] == 0`` are left untouched (clients whose local epochs are exhausted).
 """
 from __future__ import annotations
@@ -17,39 +18,64 @@ import torch
 
 class BatchedOptimizer:
     def __init__(self, kind: str, shape, device, lr: float, momentum: float = 0.9,
-                 betas=(0.9, 0.999), eps: float = 1e-8, backend: str = "torch"):
+                 betas=(0.9, 0.999), eps: float = 1e-8, backend: str = "torch", zero_init: bool = True):
         self.kind = kind.lower()
         self.lr = lr
         self.momentum = momentum
         self.b1, self.b2 = betas
         self.eps = eps
         self.backend = backend
-        self.m = torch.zeros(shape, dtype=torch.float32, device=device)
-        self.v = torch.zeros(shape, dtype=torch.float32, device=device) if self.kind == "adam" else None
-        self.t = torch.zeros(shape[0], dtype=torch.float32, device=device)
+        # zero_init=False: the state is left unset until init_round() (the round prologue kernel zeroes it)
+        alloc = torch.zeros if zero_init else torch.empty
+        self.m = alloc(shape, dtype=torch.float32, device=device)
+        self.v = alloc(shape, dtype=torch.float32, device=device) if self.kind == "adam" else None
+        self._t = alloc(2, shape[0], dtype=torch.float32, device=device)
+        self._phase = 0
+        self._fresh = zero_init
+
+    @property
+    def t(self) -> torch.Tensor:
+        return self._t[self._phase]
 
     def reset(self) -> None:
         self.m.zero_()
         if self.v is not None:
             self.v.zero_()
-        self.t.zero_()
+        self._t.zero_()
+        self._phase = 0
+        self._fresh = True
+
+    def init_round(self, params: torch.Tensor, theta: torch.Tensor) -> None:
+        """params[k] = theta for every client row and the optimizer state reset (HIP: one kernel)."""
+        if self.backend == "hip":
+            from ..ops._ext import ext
+            ext().round_init(theta.float().contiguous(), params, self.m, self.v, self._t)
+            self._phase = 0
+            self._fresh = True
+            return
+        params.copy_(theta[None, :].expand_as(params))
+        self.reset()
 
     @torch.no_grad()
     def step(self, params: torch.Tensor, grads: torch.Tensor, active: Optional[torch.Tensor] = None) -> None:
         if active is None:
             active = torch.ones(params.shape[0], device=params.device)
         active = active.to(params.dtype)
+        if not self._fresh:
+            raise RuntimeError("BatchedOptimizer(zero_init=False): call init_round() or reset() first")
         if self.backend == "hip":
             from ..ops import fedavg_hip
+            t_in, t_out = self._t[self._phase], self._t[1 - self._phase]
             if self.kind == "adam":
-                fedavg_hip.adam_step(params, grads, self.m, self.v, self.t, active, self.lr, self.b1,
+                fedavg_hip.adam_step(params, grads, self.m, self.v, t_in, t_out, active, self.lr, self.b1,
                                      self.b2, self.eps)
             else:
-                fedavg_hip.sgdm_step(params, grads, self.m, active, self.lr, self.momentum, t=self.t)
+                fedavg_hip.sgdm_step(params, grads, self.m, t_in, t_out, active, self.lr, self.momentum)
+            self._phase ^= 1
             return
         a = active[:, None]
         if self.kind == "adam":
-            self.t += active
+            self._t[self._phase] += active
             t = self.t.clamp(min=1.0)[:, None]
             m_new = self.b1 * self.m + (1 - self.b1) * grads
             v_new = self.b2 * self.v + (1 - self.b2) * grads * grads
@@ -63,7 +89,7 @@ class BatchedOptimizer:
             first = (self.t == 0)[:, None]
             buf = torch.where(first, grads, self.momentum * self.m + grads)
             self.m = torch.where(a > 0, buf, self.m)
-            self.t += active
+            self._t[self._phase] += active
             params -= a * self.lr * self.m
         else:
             raise ValueError(f"unknown optimizer '{self.kind}'")

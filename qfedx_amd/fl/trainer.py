@@ -121,39 +121,62 @@ class VQCClientTrainer:
     def encode(self, X: torch.Tensor) -> torch.Tensor:
         return self.spec.encode_features(X)
 
-    def _body(self, Xs, ys, theta, idx_d, wts_d, act_d, steps: int, round_num: int, method: str,
+    def _body(self, X, Y, lid, theta, idx_d, wts_d, act_d, steps: int, round_num: int, method: str,
               traj_keys=None, ro_keys=None):
         """Device work of one round (capturable): local steps of all clients.
+
+        ``X`` [Nc, Nmax, F] / ``Y`` [Nc, Nmax] are the whole device-resident client store and ``lid`` [K]
+        the round's store slots: on HIP each step's minibatch is gathered and angle-encoded straight from
+        the store by one kernel (no per-round copy of the clients' shards), the round starts with one
+        params/optimizer-state init kernel.
 
         Returns (params [K,P], loss [S,K], correct [S,K]): per-step, per-client weighted loss and hit
         counts are written straight into round buffers by the readout kernel (no per-step metric ops);
         the round epilogue reduces them.  With a noise model, every sample runs ``trajectories``
         Pauli-trajectory replicas (loss weights split evenly) and the readout is confused /
         shot-sampled, all keyed per client and step."""
-        cfg = self.cfg
+        cfg, spec = self.cfg, self.spec
         noise = self.engine.noise
         T = noise.trajectories if (noise is not None and noise.gate_noise) else 1
-        K = Xs.shape[0]
+        K = lid.shape[0]
         P = theta.numel()
-        params = theta.float()[None, :].repeat(K, 1).contiguous()
+        params = torch.empty(K, P, dtype=torch.float32, device=self.device)
         opt_kind = "sgd" if cfg.optimizer == "spsa" else cfg.optimizer
         opt = BatchedOptimizer(opt_kind, (K, P), self.device, cfg.learning_rate, cfg.momentum,
-                               backend=self.backend)
+                               backend=self.backend, zero_init=False)
+        opt.init_round(params, theta.float())
         loss_all = torch.empty(steps, K, dtype=torch.float32, device=self.device)
         correct_all = torch.empty(steps, K, dtype=torch.float32, device=self.device)
-        kar = torch.arange(K, device=self.device)[:, None]
+        BT = idx_d.shape[-1] * T
+        fused = self.backend == "hip" and X.is_cuda
+        if fused:
+            from ..ops._ext import ext
+            mode = 2 if spec.amplitude else (1 if spec.feature_scale == "minmax" else 0)
+            xbuf = torch.empty(K, BT, X.shape[-1], dtype=torch.float32, device=self.device)
+            ybuf = torch.empty(K * BT, dtype=torch.int64, device=self.device)
+            dummy = torch.zeros(K, BT, 0 if spec.noisy else 1, device=self.device) if spec.amplitude else None
+        else:
+            rows = lid[:, None]
         for s in range(steps):
             bi = idx_d[s]
             ws = wts_d[s]
             if T > 1:
                 bi = bi.repeat(1, T)
                 ws = ws.repeat(1, T) / T
-            xb = Xs[kar, bi]                     # [K, B, F]
-            yb = ys[kar, bi]
-            xang = self.engine.augment(self.encode(xb), traj_keys, s)
+            if fused:
+                ext().batch_gather(X, Y, lid, bi.contiguous(), mode, float(spec.alpha), xbuf, ybuf)
+                yb = ybuf.view(K, BT)
+                init = xbuf if spec.amplitude else None
+                xang = dummy if spec.amplitude else xbuf
+            else:
+                xb = X[rows, bi]                     # [K, B, F]
+                yb = Y[rows, bi]
+                init = xb if spec.amplitude else None
+                xang = self.encode(xb)
+            xang = self.engine.augment(xang, traj_keys, s)
             res = self.engine.loss_and_grads(xang, yb, ws, params, method, rng_keys=(cfg.seed, round_num, s),
                                              readout_keys=ro_keys, step=s, out_loss=loss_all[s],
-                                             out_correct=correct_all[s], init=xb if self.spec.amplitude else None)
+                                             out_correct=correct_all[s], init=init)
             opt.step(params, res["grad"], act_d[s])
         return params, loss_all, correct_all
 
@@ -179,6 +202,8 @@ class VQCClientTrainer:
         nvalid = (plan.wts > 0).sum(-1).float() * plan.active
         common = {"samples": float(nvalid.sum()), "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
                   "n_samples": store.counts[li].to(torch.float64)}
+        if plan.idx.numel() and int(plan.idx.max()) >= max(1, store.nmax):   # the gather kernel trusts the table
+            raise RuntimeError("minibatch plan indexes past the client store")
         up = PackedUpload({"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid})
         noise = self.engine.noise
         traj_keys = ro_keys = None
@@ -189,10 +214,9 @@ class VQCClientTrainer:
             params, loss_all, correct_all, dv = self._graphed(store, up, theta_g, plan, round_num)
         else:
             dv = up.to_device(self.device)
-            Xs = store.X[dv["lid"]]
-            ys = store.y[dv["lid"]]
-            params, loss_all, correct_all = self._body(Xs, ys, theta_g.to(self.device), dv["idx"], dv["wts"], dv["act"],
-                                                       plan.max_steps, round_num, method, traj_keys, ro_keys)
+            params, loss_all, correct_all = self._body(store.X, store.y, dv["lid"], theta_g.to(self.device), dv["idx"],
+                                                       dv["wts"], dv["act"], plan.max_steps, round_num, method,
+                                                       traj_keys, ro_keys)
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
                 "lid": dv["lid"], **common}
 
@@ -205,24 +229,21 @@ class VQCClientTrainer:
         """Replay the whole round as ONE hipGraph (static shapes: #clients, steps, batch).
 
         Captured once per SHAPE, not per client set: each round ONE async copy refreshes the packed
-        static input buffer (client slots, minibatch indices, loss weights, step masks), the round's
-        client shards are gathered on the device into static buffers (client sampling changes the set
-        every round), the global params are copied in, and ~15 launches per local step replay with no
-        host round trips.  A small LRU bounds the number of live graphs.
+        static input buffer (client slots, minibatch indices, loss weights, step masks), the global params
+        are copied in, and the captured launches gather every step's minibatches from the (static) client
+        store by slot, so client sampling reuses the graph.  A small LRU bounds the number of live graphs.
         """
         K = up.layout[0][4][0]
-        key = (K, plan.max_steps, plan.B, store.nmax)
+        key = (K, plan.max_steps, plan.B, store.nmax, store.X.data_ptr())
         cache = self.__dict__.setdefault("_graph_cache", {})
         dev = self.device
         ent = cache.pop(key, None)
         if ent is None:
             pack = torch.empty(up.nbytes, dtype=torch.uint8, device=dev)
             dv = up.to_device(dev, pack)
-            ent = {"pack": pack, "dv": dv,
-                   "X": store.X[dv["lid"]].contiguous(), "y": store.y[dv["lid"]].contiguous(),
-                   "theta": theta_g.to(dev).float().clone()}
-            args = (ent["X"], ent["y"], ent["theta"], dv["idx"], dv["wts"], dv["act"], plan.max_steps, round_num,
-                    "adjoint")
+            ent = {"pack": pack, "dv": dv, "theta": theta_g.to(dev).float().clone()}
+            args = (store.X, store.y, dv["lid"], ent["theta"], dv["idx"], dv["wts"], dv["act"], plan.max_steps,
+                    round_num, "adjoint")
             # the graph owns its workspaces: eager calls (evaluation) can never regrow/free them
             ent["ws"] = {}
             with self.engine.hip.private_workspace(ent["ws"]):
@@ -239,8 +260,6 @@ class VQCClientTrainer:
                 cache.pop(next(iter(cache)))
         else:
             dv = up.to_device(dev, ent["pack"])     # one H2D copy for all the round's tables
-            torch.index_select(store.X, 0, dv["lid"], out=ent["X"])
-            torch.index_select(store.y, 0, dv["lid"], out=ent["y"])
         cache[key] = ent                            # most recently used last
         ent["theta"].copy_(theta_g.float())
         ent["graph"].replay()

@@ -8,14 +8,13 @@ from ..utils.seeding import philox_key
 from ._ext import ext
 
 
-def adam_step(params, grads, m, v, t, active, lr, b1, b2, eps) -> None:
-    ext().adam(params, grads.float().contiguous(), m, v, t, active.float().contiguous(), lr, b1, b2, eps)
+def adam_step(params, grads, m, v, t_in, t_out, active, lr, b1, b2, eps) -> None:
+    """Fused client-batched Adam; step counters read from ``t_in``, ``t_in + active`` written to ``t_out``."""
+    ext().adam(params, grads.float().contiguous(), m, v, t_in, t_out, active.float().contiguous(), lr, b1, b2, eps)
 
 
-def sgdm_step(params, grads, buf, active, lr, mu, t=None) -> None:
-    if t is None:
-        raise ValueError("sgdm_step needs the step counter tensor")
-    ext().sgdm(params, grads.float().contiguous(), buf, t, active.float().contiguous(), lr, mu)
+def sgdm_step(params, grads, buf, t_in, t_out, active, lr, mu) -> None:
+    ext().sgdm(params, grads.float().contiguous(), buf, t_in, t_out, active.float().contiguous(), lr, mu)
 
 
 _NO_KEYS = {}

@@ -253,7 +253,7 @@ class HipProgram:
         wread = self._buf("wread", S * self.C, torch.float32)
         loss = torch.empty(K, dtype=torch.float32, device=self.device) if out_loss is None else out_loss
         correct = torch.empty(K, dtype=torch.float32, device=self.device) if out_correct is None else out_correct
-        grad = torch.zeros_like(p)
+        grad = torch.empty_like(p)      # every entry written: theta slots by grad_reduce, a/b by readout_ce
         self._run_passes(tr, False, psi, None, p, B, x, None, part, None, S)
         if noise is None:
             C.readout_ce(part, tr.tiles_per_state, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,

@@ -165,3 +165,43 @@ def test_bf16_state_storage_close_to_fp32(cuda, n, L):
     rel = (g32 - g16).norm() / g32.norm()
     assert rel.item() < 0.05, rel.item()
     assert b16.hip._ws["psi"].dtype == torch.int32          # 4 bytes per amplitude
+
+
+@pytest.mark.parametrize("mode,F", [(0, 16), (1, 16), (1, 300), (2, 784)])
+def test_batch_gather_matches_torch(cuda, mode, F):
+    """Fused per-step minibatch gather + encoding == torch indexing + angle_scale (bitwise)."""
+    from qfedx_amd.data.features import angle_scale
+    from qfedx_amd.ops._ext import ext
+    g = torch.Generator().manual_seed(F)
+    Nc, nmax, K, B = 7, 40, 4, 9
+    X = torch.randn(Nc, nmax, F, generator=g)
+    X[2, 3] = 0.5                                   # constant row -> minmax gives zeros
+    Y = torch.randint(0, 5, (Nc, nmax), generator=g)
+    lid = torch.tensor([5, 2, 0, 6])
+    idx = torch.randint(0, nmax, (K, B), generator=g)
+    idx[1, 0] = 3
+    xo = torch.empty(K, B, F, device=cuda)
+    yo = torch.empty(K * B, dtype=torch.int64, device=cuda)
+    ext().batch_gather(X.to(cuda), Y.to(cuda), lid.to(cuda), idx.to(cuda), mode, 2.5, xo, yo)
+    xb = X[lid[:, None], idx]
+    ref = {0: lambda: angle_scale(xb, "scale", 2.5), 1: lambda: angle_scale(xb, "minmax"), 2: lambda: xb}[mode]()
+    assert torch.equal(xo.cpu(), ref)
+    assert torch.equal(yo.cpu().view(K, B), Y[lid[:, None], idx])
+
+
+def test_round_init_and_counter_pingpong(cuda):
+    from qfedx_amd.fl.optim import BatchedOptimizer
+    K, P = 5, 37
+    theta = torch.randn(P)
+    act = [torch.tensor([1., 1., 0., 1., 1.]), torch.tensor([1., 0., 0., 1., 1.]), torch.tensor([1., 0., 0., 0., 1.])]
+    g = [torch.randn(K, P) for _ in range(3)]
+    outs = []
+    for dev, backend in (("cpu", "torch"), (cuda, "hip")):
+        p = torch.empty(K, P, device=dev)
+        opt = BatchedOptimizer("adam", (K, P), dev, 0.05, backend=backend)
+        opt.init_round(p, theta.to(dev))
+        for s in range(3):
+            opt.step(p, g[s].to(dev), act[s].to(dev))
+        outs.append((p.cpu(), opt.t.cpu()))
+    assert torch.allclose(outs[0][0], outs[1][0], atol=1e-6)
+    assert torch.equal(outs[0][1], outs[1][1]) and outs[1][1].tolist() == [3, 1, 0, 2, 3]
