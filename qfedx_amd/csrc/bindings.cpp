@@ -59,7 +59,8 @@ int qfx_launch_readout_sum(const float* part, int tps, int C, long n_samples, fl
 int qfx_amp_scratch(long F);
 int qfx_launch_amp_init(const float* x, long F, long ld, int n_samples, int n, double* part, void* psi, int bf16,
                         hipStream_t stream);
-int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob, float* grad,
+int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob, const int* csr,
+                           float* grad,
                            int p_stride, float* gpart, hipStream_t st);
 int qfx_grad_split(int tps, int spc);
 int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct, const float* nvalid,
@@ -78,6 +79,11 @@ int qfx_launch_batch_gather(const float* X, const long long* Y, const long long*
 int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
                       const double* weights, double* norms, const uint32_t* keys, int K, int P, int wrap, int dp,
                       float clip, float sigma, long long* out, hipStream_t st);
+}
+
+namespace qfx_runtime {
+std::vector<torch::Tensor> batch_plan(torch::Tensor counts, torch::Tensor client_ids, int64_t B, int64_t rk0,
+                                      int64_t rk1, int64_t local_epochs, int64_t local_steps, bool shuffle);
 }
 
 namespace {
@@ -224,15 +230,17 @@ void round_apply(torch::Tensor buf, int64_t P, torch::Tensor theta, double lr, t
         "qfx_round_apply");
 }
 
+// csr: int32 [n_theta + 1 + n_entries] slot -> gradient-gate CSR (ops/statevec_hip.py slot_csr)
 void grad_reduce(torch::Tensor slab, int64_t tps, int64_t spc, int64_t K, int64_t G, torch::Tensor blob,
-                 torch::Tensor grad, torch::Tensor gpart) {
+                 torch::Tensor csr, torch::Tensor grad, torch::Tensor gpart) {
   need(slab, torch::kFloat32, "slab");
+  need(csr, torch::kInt32, "csr");
   need(grad, torch::kFloat32, "grad");
   need(gpart, torch::kFloat32, "gpart");
   if (slab.numel() < K * spc * tps * G) throw std::invalid_argument("grad slab too small");
   if (gpart.numel() < K * grad_split(tps, spc) * G) throw std::invalid_argument("gpart too small");
   check(qfx_launch_grad_reduce(ptr<float>(slab), (int)tps, (int)spc, (int)K, (int)G, ptr<int>(blob),
-                               ptr<float>(grad), (int)grad.size(1), ptr<float>(gpart), cur_stream()),
+                               ptr<int>(csr), ptr<float>(grad), (int)grad.size(1), ptr<float>(gpart), cur_stream()),
         "qfx_grad_reduce");
 }
 
@@ -377,6 +385,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("readout_sum", &readout_sum);
   m.def("amp_init", &amp_init);
   m.def("round_init", &round_init);
+  m.def("batch_plan", &qfx_runtime::batch_plan);
   m.def("batch_gather", &batch_gather);
   m.def("amp_scratch", &amp_scratch);
   m.def("readout_noise", &readout_noise);

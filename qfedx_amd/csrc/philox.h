@@ -5,28 +5,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "philox_core.h"
+
 namespace qfx {
-
-struct u32x4 { uint32_t x, y, z, w; };
-
-__host__ __device__ inline void mulhilo32(uint32_t a, uint32_t b, uint32_t& hi, uint32_t& lo) {
-  const uint64_t p = (uint64_t)a * (uint64_t)b;
-  hi = (uint32_t)(p >> 32);
-  lo = (uint32_t)p;
-}
-
-__host__ __device__ inline u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    uint32_t hi0, lo0, hi1, lo1;
-    mulhilo32(0xD2511F53u, c.x, hi0, lo0);
-    mulhilo32(0xCD9E8D57u, c.z, hi1, lo1);
-    c = {hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
-    k0 += 0x9E3779B9u;
-    k1 += 0xBB67AE85u;
-  }
-  return c;
-}
 
 // standard normal for element e of a stream: pairs (2i, 2i+1) come from counter e/4, Box-Muller in
 // double on the (0,1] float uniforms - matches seeding.philox_normal element-for-element

@@ -47,6 +47,25 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* sm) {
   for (int i = 0; i < NV; ++i) v[i] = sm[i * 4 + 0] + sm[i * 4 + 1] + sm[i * 4 + 2] + sm[i * 4 + 3];
 }
 
+// zs[c] = sum_u part[s][u][c] in tile order.  Loads are issued in batches of 8 tiles (predicated) so
+// their latencies overlap instead of serialising one dependent load per tile.
+__device__ __forceinline__ void tile_sums(const float* __restrict__ part, long s, int tps, int C, float (&zs)[CMAX]) {
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) zs[c] = 0.f;
+  const float* base = part + (size_t)s * tps * C;
+  for (int u0 = 0; u0 < tps; u0 += 8) {
+    float v[8][CMAX];
+#pragma unroll
+    for (int du = 0; du < 8; ++du)
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) v[du][c] = (u0 + du < tps && c < C) ? base[(size_t)(u0 + du) * C + c] : 0.f;
+#pragma unroll
+    for (int du = 0; du < 8; ++du)
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) zs[c] += v[du][c];
+  }
+}
+
 // one block per client: <Z_c> = sum of tile partials; logits a<Z>+b; CE; dL/d<Z>; grads of a, b
 __global__ void __launch_bounds__(256) qfx_readout_ce_kernel(
     const float* __restrict__ part, int tps, int C, int spc, const long long* __restrict__ y,
@@ -67,11 +86,12 @@ __global__ void __launch_bounds__(256) qfx_readout_ce_kernel(
     const long s = (long)k * spc + j;
     float z[CMAX], lg[CMAX];
     float m = -INFINITY;
+    float zs[CMAX];
+    tile_sums(part, s, tps, C, zs);
 #pragma unroll
     for (int c = 0; c < CMAX; ++c) {
       if (c >= C) break;
-      float t = 0.f;
-      for (int u = 0; u < tps; ++u) t += part[((size_t)s * tps + u) * C + c];
+      float t = zs[c];
       if (noisy) t = noisy_z(t, nz.p01, nz.p10, nz.shots, k0, k1, nz.stream, ((uint64_t)j * C + c) * (uint64_t)nz.shots);
       z[c] = t;
       lg[c] = fmaf(a[c], t, b[c]);
@@ -144,8 +164,15 @@ __global__ void qfx_readout_sum_kernel(const float* __restrict__ part, int tps, 
   if (i >= n_samples * C) return;
   const long s = i / C;
   const int c = (int)(i % C);
+  const float* base = part + (size_t)s * tps * C + c;
   float t = 0.f;
-  for (int u = 0; u < tps; ++u) t += part[((size_t)s * tps + u) * C + c];
+  for (int u0 = 0; u0 < tps; u0 += 8) {   // 8 loads in flight, summed in tile order
+    float v[8];
+#pragma unroll
+    for (int du = 0; du < 8; ++du) v[du] = u0 + du < tps ? base[(size_t)(u0 + du) * C] : 0.f;
+#pragma unroll
+    for (int du = 0; du < 8; ++du) t += v[du];
+  }
   expz[i] = t;
 }
 
@@ -161,9 +188,18 @@ __global__ void __launch_bounds__(256) qfx_grad_partial_kernel(const float* __re
   const long chunk = (rows + RS - 1) / RS;
   const long r0 = (long)rs * chunk, r1 = min(rows, r0 + chunk);
   float acc = 0.f;
-  if (g < G) {
+  if (g < G) {   // rows r0+rl, +4, +8, ...: four loads in flight per iteration, summed in row order
     const float* base = slab + (size_t)k * rows * G + g;
-    for (long r = r0 + rl; r < r1; r += 4) acc += base[(size_t)r * G];
+    for (long r = r0 + rl; r < r1; r += 16) {
+      const float v0 = base[(size_t)r * G];
+      const float v1 = r + 4 < r1 ? base[(size_t)(r + 4) * G] : 0.f;
+      const float v2 = r + 8 < r1 ? base[(size_t)(r + 8) * G] : 0.f;
+      const float v3 = r + 12 < r1 ? base[(size_t)(r + 12) * G] : 0.f;
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
   }
   sm[threadIdx.x] = acc;
   __syncthreads();
@@ -171,29 +207,39 @@ __global__ void __launch_bounds__(256) qfx_grad_partial_kernel(const float* __re
 }
 
 // stage 2, one block per client: gsum[g] = sum_rs gpart (fixed order) for gradient gates, then
-// grad[k][slot] = sum_{gates g of slot} scale_g * gsum[g]
+// grad[k][slot] = sum_{gates g of slot} scale_g * gsum[g] in gate order, walking the host-built slot -> gate
+// CSR (csr[0..n_theta] offsets, then gate ids) so each slot touches only its own gates.
 __global__ void __launch_bounds__(256) qfx_grad_slots_kernel(const float* __restrict__ gpart, int RS,
-                                                             const int* __restrict__ blob, float* __restrict__ grad,
+                                                             const int* __restrict__ blob,
+                                                             const int* __restrict__ csr, float* __restrict__ grad,
                                                              int p_stride) {
-  extern __shared__ float gsum[];
+  extern __shared__ float gsh[];
   const int k = blockIdx.x;
   const int G = blob[HF_NGATES];
   const int n_theta = blob[HF_NTHETA];
   const int* gt = blob + blob[HF_GATES];
+  float* gsum = gsh;
+  float* gscale = gsh + G;
   for (int g = threadIdx.x; g < G; g += 256) {
     const int kind = gt[g * GATE_WORDS];
     const int slot = gt[g * GATE_WORDS + 3];
+    const bool use = slot >= 0 && slot < n_theta && kind <= K_P;
+    float v[GR_SPLIT_MAX];
+#pragma unroll
+    for (int r = 0; r < GR_SPLIT_MAX; ++r) v[r] = (use && r < RS) ? gpart[((size_t)k * RS + r) * G + g] : 0.f;
     float s = 0.f;
-    if (slot >= 0 && slot < n_theta && kind <= K_P)
-      for (int r = 0; r < RS; ++r) s += gpart[((size_t)k * RS + r) * G + g];
+#pragma unroll
+    for (int r = 0; r < GR_SPLIT_MAX; ++r) s += v[r];
     gsum[g] = s;
+    gscale[g] = __int_as_float(gt[g * GATE_WORDS + 4]);
   }
   __syncthreads();
   for (int slot = threadIdx.x; slot < n_theta; slot += 256) {
     float s = 0.f;
-    for (int g = 0; g < G; ++g) {
-      if (gt[g * GATE_WORDS + 3] == slot && gt[g * GATE_WORDS] <= K_P)
-        s = fmaf(__int_as_float(gt[g * GATE_WORDS + 4]), gsum[g], s);
+    const int e1 = csr[slot + 1];
+    for (int e = csr[slot]; e < e1; ++e) {
+      const int g = csr[n_theta + 1 + e];
+      s = fmaf(gscale[g], gsum[g], s);
     }
     grad[(size_t)k * p_stride + slot] = s;
   }
@@ -409,11 +455,12 @@ extern "C" int qfx_grad_split(int tps, int spc) {
 }
 
 extern "C" int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, const int* blob,
-                                      float* grad, int p_stride, float* gpart, hipStream_t st) {
+                                      const int* csr, float* grad, int p_stride, float* gpart, hipStream_t st) {
   const long rows = (long)tps * spc;
   const int RS = qfx_grad_split(tps, spc);
+  if ((size_t)G * 8 > 64 * 1024) return -5;   // LDS gate sums + scales of the slot stage
   hipLaunchKernelGGL(qfx_grad_partial_kernel, dim3(K, (G + 63) / 64, RS), dim3(256), 0, st, slab, rows, G, RS, gpart);
-  hipLaunchKernelGGL(qfx_grad_slots_kernel, dim3(K), dim3(256), (size_t)G * sizeof(float), st, gpart, RS, blob, grad,
+  hipLaunchKernelGGL(qfx_grad_slots_kernel, dim3(K), dim3(256), (size_t)G * 8, st, gpart, RS, blob, csr, grad,
                      p_stride);
   return (int)hipGetLastError();
 }

@@ -58,7 +58,7 @@ class CNNClientTrainer:
         if plan.idx.numel() and int(plan.idx.max()) >= max(1, store.nmax):
             raise RuntimeError("minibatch plan indexes past the client store")
         dv = PackedUpload({"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active,
-                           "nvalid": nvalid}).to_device(self.device)
+                           "nvalid": nvalid, "w": store.counts[li].to(torch.float64)}).to_device(self.device)
         params = torch.empty(K, P, dtype=torch.float32, device=self.device)
         opt = BatchedOptimizer(cfg.optimizer if cfg.optimizer != "spsa" else "sgd", (K, P), self.device,
                                cfg.learning_rate, cfg.momentum, backend=self.backend, zero_init=False)
@@ -89,7 +89,7 @@ class CNNClientTrainer:
             loss_all[s].copy_(res["loss"])
             correct_all[s].copy_(res["correct"])
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
-                "lid": dv["lid"], "samples": float(nvalid.sum()), "steps": int(sum(plan.steps_per_client)),
+                "lid": dv["lid"], "weights": dv["w"], "samples": float(nvalid.sum()), "steps": int(sum(plan.steps_per_client)),
                 "client_ids": cids, "n_samples": store.counts[li].to(torch.float64)}
 
 

@@ -176,6 +176,8 @@ class FederatedRunner:
         with self.timer.phase("aggregate"):
             if t.weighting == "uniform":
                 w = torch.ones(len(local_alive), dtype=torch.float64, device=dev)
+            elif "weights" in res:            # uploaded with the round's tables (no gather launch)
+                w = res["weights"]
             else:
                 if getattr(self, "_counts_dev", None) is None:
                     self._counts_dev = self.store.counts.to(torch.float64).to(dev)

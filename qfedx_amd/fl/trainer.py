@@ -19,7 +19,7 @@ from typing import Optional
 import torch
 
 from ..utils.device import PackedUpload, h2d
-from ..utils.seeding import philox4x32, philox_key, philox_uniform_rows
+from ..utils.seeding import _philox4x32_np, philox4x32, philox_key
 from .optim import BatchedOptimizer
 
 
@@ -52,15 +52,30 @@ class ShardStore:
 class BatchPlan:
     """Per-round minibatch schedule for a set of clients (host-side index tables, keyed RNG).
 
-    Vectorised over clients: one round key, per-client Philox keys derived from it by client id, keyed
-    uniforms [K, epochs, n_max] -> argsort = every client's epoch permutations at once; the [S, K, B]
-    index / weight / active tables are built with tensor ops (no per-client Python loop).  Keyed by
-    (seed, round, client id, epoch) only -> identical however clients are sharded over ranks.
+    Built by the native round scheduler (``csrc/runtime.cpp``: per-client Philox keys from one round key,
+    keyed partial Fisher-Yates epoch orders, [S, K, B] index / weight / active tables) in microseconds; ``_plan_torch`` is the vectorised torch oracle / fallback.  Keyed by (seed, round,
+    client id, epoch) only -> identical however clients are sharded over ranks.
     """
 
     def __init__(self, counts: torch.Tensor, client_ids: list, batch_size: int, round_num: int,
-                 seed: int, local_epochs: int = 1, local_steps: int = 0, shuffle: bool = True):
-        B = self.B = batch_size
+                 seed: int, local_epochs: int = 1, local_steps: int = 0, shuffle: bool = True,
+                 native: bool | None = None):
+        self.B = batch_size
+        self.local_steps = local_steps
+        C = _native_runtime() if native is not False else None
+        if native and C is None:
+            raise RuntimeError("native round scheduler requested but the extension is not built")
+        rk = philox_key(seed, "batch", round_num) if shuffle else (0, 0)
+        if C is not None:
+            ids = torch.tensor([int(c) for c in client_ids], dtype=torch.int64)
+            self.idx, self.wts, self.active, steps = C.batch_plan(counts.reshape(-1), ids, batch_size, rk[0], rk[1],
+                                                                  local_epochs, local_steps, shuffle)
+            self.steps_per_client = steps.tolist()
+            self.max_steps = int(self.idx.shape[0])
+        else:
+            self._plan_torch(counts, client_ids, batch_size, rk, local_epochs, local_steps, shuffle)
+
+    def _plan_torch(self, counts, client_ids, B, rk, local_epochs, local_steps, shuffle):
         K = len(client_ids)
         n = counts.to(torch.int64).reshape(-1)
         nb = (n + B - 1) // B                                   # batches per epoch
@@ -72,18 +87,30 @@ class BatchPlan:
             epochs = torch.full((K,), local_epochs, dtype=torch.int64)
         self.steps_per_client = steps.tolist()
         self.max_steps = int(steps.max()) if K else 0
-        self.local_steps = local_steps
         S, E, N = self.max_steps, max(int(epochs.max()) if K else 1, 1), max(int(n.max()) if K else 1, 1)
+        perm = np.tile(np.arange(N, dtype=np.int64), (K, E, 1))
         if shuffle and K:
-            rk = philox_key(seed, "batch", round_num)
             ids = torch.tensor([int(c) for c in client_ids], dtype=torch.int64)
             ctr = torch.stack([ids & 0xFFFFFFFF, ids >> 32, torch.zeros_like(ids), torch.zeros_like(ids)], -1)
-            keys = philox4x32(ctr, rk[0], rk[1])[:, :2]          # per-client key = Philox(round key, client id)
-            u = philox_uniform_rows(keys, E * N).reshape(K, E, N)
-            u = torch.where(torch.arange(N)[None, None, :] < n[:, None, None], u, torch.full_like(u, 2.0))
-            perm = torch.argsort(u, dim=-1)                       # [K, E, N]: first n_k entries permute 0..n_k-1
-        else:
-            perm = torch.arange(N).expand(K, E, N)
+            keys = philox4x32(ctr, rk[0], rk[1])[:, :2].numpy()  # per-client key = Philox(round key, client id)
+            nblk = (E * N + 3) // 4
+            blk = np.arange(nblk, dtype=np.int64)
+            c = np.stack([blk & 0xFFFFFFFF, blk >> 32, np.zeros_like(blk), np.zeros_like(blk)], -1)[None]
+            w = _philox4x32_np(np.broadcast_to(c, (K, nblk, 4)), keys[:, 0:1], keys[:, 1:2])
+            w = w.reshape(K, -1)[:, :E * N].reshape(K, E, N)      # raw words of elements e*N + j
+            nn = n.numpy()[:, None]
+            used = (steps.numpy() * B if local_steps > 0 else epochs.numpy() * np.maximum(n.numpy(), 1))[:, None]
+            m = np.minimum(nn, used - np.arange(E)[None, :] * np.maximum(nn, 1))      # [K, E] prefix drawn
+            jmax = np.minimum(m, nn - 1)
+            kk_, ee_ = np.meshgrid(np.arange(K), np.arange(E), indexing="ij")
+            for j in range(int(jmax.max()) if jmax.size else 0):   # partial Fisher-Yates, Lemire multiply-shift
+                act = j < jmax
+                span = np.maximum(nn - j, 0).astype(np.uint64)
+                r = np.where(act, j + ((w[:, :, j] * span) >> np.uint64(32)).astype(np.int64), j)
+                a, bvals = perm[:, :, j].copy(), perm[kk_, ee_, r]
+                perm[:, :, j] = bvals
+                perm[kk_, ee_, r] = a
+        perm = torch.from_numpy(perm)
         s_ = torch.arange(S)[:, None, None]                       # [S, 1, 1]
         t_ = torch.arange(B)[None, None, :]                       # [1, 1, B]
         nk = n[None, :, None].clamp(min=1)
@@ -106,6 +133,19 @@ class BatchPlan:
         self.idx = torch.where(valid, idx, torch.zeros_like(idx))
         self.wts = valid.float() / cnt.float()
         self.active = active.float()
+
+
+_NATIVE = []
+
+
+def _native_runtime():
+    if not _NATIVE:
+        try:
+            from .. import _qfedx_C as C
+            _NATIVE.append(C if hasattr(C, "batch_plan") else None)
+        except ImportError:
+            _NATIVE.append(None)
+    return _NATIVE[0]
 
 
 class VQCClientTrainer:
@@ -204,7 +244,8 @@ class VQCClientTrainer:
                   "n_samples": store.counts[li].to(torch.float64)}
         if plan.idx.numel() and int(plan.idx.max()) >= max(1, store.nmax):   # the gather kernel trusts the table
             raise RuntimeError("minibatch plan indexes past the client store")
-        up = PackedUpload({"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid})
+        up = PackedUpload({"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid,
+                           "w": store.counts[li].to(torch.float64)})   # FedAvg sample-count weights
         noise = self.engine.noise
         traj_keys = ro_keys = None
         if noise is not None:
@@ -218,7 +259,7 @@ class VQCClientTrainer:
                                                        dv["wts"], dv["act"], plan.max_steps, round_num, method,
                                                        traj_keys, ro_keys)
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
-                "lid": dv["lid"], **common}
+                "lid": dv["lid"], "weights": dv["w"], **common}
 
     # ------------------------------------------------------------------ hipGraph capture
     @property

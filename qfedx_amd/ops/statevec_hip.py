@@ -50,6 +50,20 @@ def jit_enabled() -> bool:
     return os.environ.get("QFEDX_JIT", "1") != "0"
 
 
+def slot_csr(info: dict, n_theta: int) -> torch.Tensor:
+    """slot -> gradient-gate CSR of a plan: int32 [offsets (n_theta + 1) | gate ids], gates in plan order
+    (the order the device sums them in)."""
+    lists = [[] for _ in range(n_theta)]
+    for g, e in enumerate(info["gates"]):
+        if 0 <= e["slot"] < n_theta and e["kind"] <= 3:          # rx / ry / rz / p carry gradients
+            lists[e["slot"]].append(g)
+    offs, ent = [0], []
+    for lst in lists:
+        ent += lst
+        offs.append(len(ent))
+    return torch.tensor(offs + ent, dtype=torch.int32)
+
+
 class _Plan:
     def __init__(self, ops, coef, n, R, kmax, readout, n_theta, mode, final_flags, device, jit: bool,
                  bf16: bool = False):
@@ -64,6 +78,7 @@ class _Plan:
         self.passes = [(p["offset"], p["K"], p["NGRAD"], p["NOPS"]) for p in self.info["passes"]]
         self.k = self.info["passes"][0]["K"]
         self.n = n
+        self.csr = slot_csr(self.info, n_theta).to(device) if self.adjoint else None
         self.jit_handles = None
         if jit:
             self.jit_handles = [C.jit_prepare(blob, i, self.adjoint, JIT_CACHE, CSRC, ARCH, bf16)[0]
@@ -224,7 +239,7 @@ class HipProgram:
         self._run_passes(adj, True, psi, lam, th, B, x, wr, None, slab, S)
         grad = torch.zeros(K, th.shape[1], dtype=torch.float32, device=self.device)
         gpart = self._buf("gpart", K * C.grad_split(adj.tiles_per_state, B) * self.G, torch.float32)
-        C.grad_reduce(slab, adj.tiles_per_state, B, K, self.G, adj.blob, grad, gpart)
+        C.grad_reduce(slab, adj.tiles_per_state, B, K, self.G, adj.blob, adj.csr, grad, gpart)
         return z.view(S, self.C).clone(), grad[:, : self.n_theta]
 
     # ------------------------------------------------------------------ train step
@@ -263,5 +278,5 @@ class HipProgram:
                          correct, grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
         self._run_passes(adj, True, psi, lam, p, B, x, wread, None, slab, S)
         gpart = self._buf("gpart", K * C.grad_split(adj.tiles_per_state, B) * self.G, torch.float32)
-        C.grad_reduce(slab, adj.tiles_per_state, B, K, self.G, adj.blob, grad, gpart)
+        C.grad_reduce(slab, adj.tiles_per_state, B, K, self.G, adj.blob, adj.csr, grad, gpart)
         return {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}

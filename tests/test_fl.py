@@ -166,8 +166,8 @@ def test_exact_aggregation_permutation_and_split_invariant(K, seed, split):
 
 @pytest.mark.parametrize("opt", ["momentum", "adam"])
 def test_server_optimizers_train(opt):
-    out = run_experiment(small_cfg(num_rounds=5, server_optimizer=opt, server_lr=0.5 if opt == "adam" else 1.0))
-    assert out["accuracies"][-1] > out["accuracies"][0]
+    out = run_experiment(small_cfg(num_rounds=5, server_optimizer=opt, server_lr=0.1 if opt == "adam" else 1.0))
+    assert max(out["accuracies"][1:]) > out["accuracies"][0] + 0.05
 
 
 def test_sharded_fedavg_step_equals_plain_path():
@@ -178,3 +178,17 @@ def test_sharded_fedavg_step_equals_plain_path():
     sharded = run_experiment(small_cfg(num_rounds=3, optimizer="sgd", server_optimizer="fedavg",
                                        server_lr=1.0 + 1e-12))
     assert torch.allclose(plain["params"], sharded["params"], atol=1e-6)
+
+
+@pytest.mark.parametrize("local_epochs,local_steps,shuffle", [(1, 0, True), (3, 0, True), (2, 0, False),
+                                                                (1, 7, True), (1, 40, True)])
+def test_native_batch_plan_matches_torch_oracle(local_epochs, local_steps, shuffle):
+    """csrc/runtime.cpp builds the same keyed plan tables as the torch oracle (bitwise)."""
+    pytest.importorskip("qfedx_amd._qfedx_C", reason="native extension not built")
+    counts = torch.tensor([0, 1, 5, 33, 64, 17, 100, 31])
+    ids = [3, 17, 2, 40, 1 << 33, 9, 11, 5]
+    for r in (0, 7):
+        a = BatchPlan(counts, ids, 16, r, 1234, local_epochs, local_steps, shuffle, native=True)
+        b = BatchPlan(counts, ids, 16, r, 1234, local_epochs, local_steps, shuffle, native=False)
+        assert a.steps_per_client == b.steps_per_client and a.max_steps == b.max_steps
+        assert torch.equal(a.idx, b.idx) and torch.equal(a.wts, b.wts) and torch.equal(a.active, b.active)
