@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--dp", action="store_true")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--engine", default="valu", choices=["mfma", "valu"],
+                    help="mfma: fp16-state MFMA group-unitary engine (ops/hea_mfma.py); valu: fp32 pass engine")
     args = ap.parse_args()
 
     import torch
@@ -85,6 +87,7 @@ def main():
     cfg.model.n_layers = args.layers
     cfg.model.n_classes = args.classes
     cfg.model.readout_scale = 3.0
+    cfg.model.state_dtype = "mfma" if args.engine == "mfma" else "fp32"
     cfg.train.batch_size = args.batch
     cfg.train.local_steps = args.local_steps
     cfg.train.learning_rate = 0.05
@@ -113,7 +116,8 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": "fp16-state/fp32-accumulate (MFMA)" if args.engine == "mfma" else "fp32",
+            "engine": args.engine,
             "data": "synthetic non-IID (Dirichlet alpha=0.5) client shards, random-init VQC",
             "rounds_per_sec": round(rounds_per_s, 4),
             "samples_per_sec": round(value * args.batch, 1),

@@ -46,7 +46,7 @@ class ModelConfig:
     entangler: str = "chain"            # chain | ring | none
     readout_scale: float = 1.0          # initial a in logit = a<Z> + b
     init_std: float = 0.1
-    state_dtype: str = "fp32"           # fp32 | bf16 (statevector storage between kernel passes)
+    state_dtype: str = "fp32"           # fp32 | bf16 (VALU pass engine storage) | mfma (fp16 MFMA engine)
 
 
 @dataclass

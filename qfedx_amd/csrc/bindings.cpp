@@ -376,6 +376,7 @@ void jit_launch(int64_t handle, torch::Tensor blob, int64_t pass_off, torch::Ten
 }  // namespace
 
 void register_cnn(pybind11::module& m);
+void register_hea(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "qfedx_amd native runtime: pass planner + gfx950 HIP kernels";
@@ -404,4 +405,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("jit_source", &jit_source, py::arg("blob"), py::arg("p"), py::arg("adjoint"), py::arg("bf16") = false);
   m.def("jit_launch", &jit_launch);
   register_cnn(m);
+  register_hea(m);
 }

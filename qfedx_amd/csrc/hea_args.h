@@ -1,0 +1,29 @@
+// Launch arguments of the MFMA statevector pass kernel (csrc/hea_mfma.hip); shared by the host
+// bindings (csrc/hea_bindings.cpp) so both sides agree on the layout.
+#pragma once
+#include <cstdint>
+
+struct HeaPassArgs {
+  const int* ops;            // [nops][128] op records (hea_plan.py)
+  const int* fidx;           // [nops] unitary fragment index (slot * 4 + 0 | 2) or -1
+  int nops;
+  int n, t, c, lo, hi, n_tiles;   // tile = memory bits [0, c) u [lo, hi), 2^(n - t) tiles per sample
+  int gen, load_lam, store_psi, store_lam;
+  int spc, C, n_theta, p_stride, feature;
+  float scale;               // stored amplitudes = scale * true amplitudes (fp16 range)
+  const uint32_t* psi_in;    // fp16 (re, im) states [S][2^n]
+  uint32_t* psi_out;
+  const uint32_t* lam_in;
+  uint32_t* lam_out;
+  const float* xang;         // [S][x_stride] feature angles
+  int x_stride;
+  const float* params;       // [K][p_stride]
+  const void* frags;         // uint4 unitary fragments (hea_frag_kernel)
+  int n_slots;
+  const float* wread;        // [S][C] dL/d<Z_c>
+  float* part;               // [S][n_tiles][C] readout partials
+  float* gslab;              // [S][slab_tiles][n_theta] gradient partials
+  int slab_tiles;
+  int hrow[5];
+  long long* dbg;            // optional phase timestamps (s_memtime) of workgroups < 8, [8][64]               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
+};

@@ -1,0 +1,161 @@
+// Bindings of the MFMA statevector engine (hea_mfma.hip).  Every launch goes on torch's current HIP
+// stream (composes with hipGraph capture).  Buffer extents are checked here against the geometry the
+// kernel will index with, so a bad plan or a short buffer is a Python exception, never a GPU fault.
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "hea_args.h"
+
+extern "C" {
+int qfx_hea_pass(int adjoint, const HeaPassArgs* args, int n_samples, hipStream_t st);
+int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
+                  hipStream_t st);
+int qfx_hea_grad_reduce(const float* gslab, int slab_tiles, const int* owner_tiles, int n_theta, int spc, int K,
+                        float* grad, int p_stride, hipStream_t st);
+int qfx_hea_args_size();
+}
+
+namespace {
+
+hipStream_t cur() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void need(bool ok, const std::string& msg) {
+  if (!ok) throw std::invalid_argument("hea: " + msg);
+}
+
+template <typename T>
+T* dp(const torch::Tensor& t, torch::ScalarType dt, const char* name, int64_t min_numel) {
+  if (min_numel == 0 && (!t.defined() || t.numel() == 0)) return nullptr;
+  need(t.defined() && t.is_cuda() && t.is_contiguous() && t.scalar_type() == dt, std::string(name) +
+       ": expected a contiguous CUDA tensor of the right dtype");
+  need(t.numel() >= min_numel, std::string(name) + ": buffer too small (" + std::to_string(t.numel()) + " < " +
+       std::to_string(min_numel) + ")");
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+
+void check(int rc, const char* what) {
+  if (rc != 0) throw std::runtime_error(std::string(what) + " failed: " + std::to_string(rc));
+}
+
+// geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
+//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows)]
+void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<int64_t> geom, double scale, torch::Tensor psi_in,
+              torch::Tensor psi_out, torch::Tensor lam_in, torch::Tensor lam_out, torch::Tensor xang,
+              torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
+              torch::Tensor gslab, torch::Tensor dbg) {
+  need(geom.size() == 25, "geometry vector must have 25 entries");
+  HeaPassArgs a{};
+  a.n = (int)geom[0];
+  a.t = (int)geom[1];
+  a.c = (int)geom[2];
+  a.lo = (int)geom[3];
+  a.hi = (int)geom[4];
+  a.n_tiles = (int)geom[5];
+  a.gen = (int)geom[6];
+  a.load_lam = (int)geom[7];
+  a.store_psi = (int)geom[8];
+  a.store_lam = (int)geom[9];
+  a.spc = (int)geom[10];
+  a.C = (int)geom[11];
+  a.n_theta = (int)geom[12];
+  a.p_stride = (int)geom[13];
+  a.feature = (int)geom[14];
+  const int64_t S = geom[15];
+  a.x_stride = (int)geom[16];
+  a.n_slots = (int)geom[17];
+  a.slab_tiles = (int)geom[18];
+  const int64_t K = geom[19];
+  a.scale = (float)scale;
+  a.dbg = dbg.defined() && dbg.numel() >= 8 * 64 ? dp<long long>(dbg, torch::kInt64, "dbg", 8 * 64) : nullptr;
+  for (int b = 0; b < 5; ++b) {
+    a.hrow[b] = (int)geom[20 + b];
+    need(a.hrow[b] >= 0 && a.hrow[b] < (1 << (a.t - 5)), "swizzle row reads past the tile bits");
+  }
+  need(a.n >= 8 && a.n <= 30 && a.t >= 8 && a.t <= 14 && a.t <= a.n, "qubit / tile size out of range");
+  need(a.c >= 2 && a.c <= a.lo && a.lo <= a.hi && a.hi <= a.n && a.c + a.hi - a.lo == a.t, "bad tile layout");
+  need(a.n_tiles == (1 << (a.n - a.t)), "n_tiles must be 2^(n - t)");
+  need(a.spc > 0 && S == K * a.spc, "samples must be K x spc");
+  need(a.C >= 1 && a.C <= 8, "1..8 readout classes");
+  need(a.n_theta >= 2 * a.n, "theta count below one layer");
+  need(a.p_stride >= a.n_theta, "param stride too small");
+  need(ops.dim() == 2 && ops.size(1) == 128 && ops.scalar_type() == torch::kInt32 && ops.is_cuda(),
+       "ops must be int32 [nops, 128] on the device");
+  a.nops = (int)ops.size(0);
+  a.ops = dp<int>(ops, torch::kInt32, "ops", 0);
+  a.fidx = a.nops ? dp<int>(fidx, torch::kInt32, "fidx", a.nops) : nullptr;
+  const int64_t states = S << a.n;
+  a.psi_in = a.gen ? nullptr : dp<uint32_t>(psi_in, torch::kInt32, "psi_in", states);
+  a.psi_out = a.store_psi ? dp<uint32_t>(psi_out, torch::kInt32, "psi_out", states) : nullptr;
+  a.lam_in = (adjoint && a.load_lam) ? dp<uint32_t>(lam_in, torch::kInt32, "lam_in", states) : nullptr;
+  a.lam_out = (adjoint && a.store_lam) ? dp<uint32_t>(lam_out, torch::kInt32, "lam_out", states) : nullptr;
+  need(a.x_stride >= a.n, "x stride must cover n feature angles");
+  a.xang = dp<float>(xang, torch::kFloat32, "xang", S * a.x_stride);
+  a.params = dp<float>(params, torch::kFloat32, "params", K * a.p_stride);
+  a.frags = a.n_slots ? (const void*)dp<int32_t>(frags, torch::kInt32, "frags", K * a.n_slots * 4 * 128 * 4) : nullptr;
+  a.wread = adjoint ? dp<float>(wread, torch::kFloat32, "wread", S * a.C) : nullptr;
+  a.part = dp<float>(part, torch::kFloat32, "part", 0);
+  if (a.part) need(part.numel() >= S * a.n_tiles * a.C, "part buffer too small");
+  a.gslab = adjoint ? dp<float>(gslab, torch::kFloat32, "gslab", S * a.slab_tiles * a.n_theta) : nullptr;
+  need(!adjoint || a.slab_tiles >= a.n_tiles, "gradient slab has fewer tiles than the pass");
+  need(!a.gen || a.n <= 32, "product-state generation supports <= 32 qubits");
+  check(qfx_hea_pass(adjoint ? 1 : 0, &a, (int)S, cur()), "qfx_hea_pass");
+}
+
+// Validate a pass program once (host copy) when it is built: slot / gradient-slot ranges and op kinds.
+void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64_t n_theta, bool adjoint, int64_t t) {
+  need(fidx.scalar_type() == torch::kInt32 && !fidx.is_cuda() && fidx.numel() == ops.size(0),
+       "fidx must be a host int32 [nops] tensor");
+  const int* fi = fidx.data_ptr<int>();
+  for (int64_t o = 0; o < ops.size(0); ++o) need(fi[o] >= -1 && fi[o] < 4 * n_slots, "fragment index out of range");
+  need(ops.dim() == 2 && ops.size(1) == 128 && ops.scalar_type() == torch::kInt32 && !ops.is_cuda() &&
+       ops.is_contiguous(), "ops must be a contiguous host int32 [nops, 128] tensor");
+  const int* ow = ops.data_ptr<int>();
+  for (int64_t o = 0; o < ops.size(0); ++o) {
+    const int* w = ow + o * 128;
+    const int code = w[0];
+    need(code >= 1 && code <= 8, "unknown op code");
+    need(adjoint || code == 1 || code == 7, "adjoint op in a forward pass");
+    if (code <= 3 || code == 8) need(w[1] >= 0 && w[1] < n_slots, "op names a missing unitary slot");
+    if (code <= 5 || code == 8) {
+      need(w[2] >= 0 && w[2] <= 4, "group size out of range");
+      for (int j = 0; j < w[2]; ++j)
+        need(w[12 + j] >= 0 && w[12 + j] < n_theta && w[16 + j] >= 0 && w[16 + j] < n_theta,
+             "gradient slot out of range");
+      for (int i = 20; i < 100; ++i) need(w[i] >= 0 && w[i] < (1 << t), "tile address out of range");
+    }
+    if (code == 6 || code == 7) need(w[2] >= 1 && w[2] <= 8, "observable count out of range");
+  }
+}
+
+void hea_frags(torch::Tensor params, int64_t p_stride, torch::Tensor slot_tab, int64_t n_slots, int64_t K,
+               torch::Tensor frags) {
+  need(slot_tab.scalar_type() == torch::kInt32 && slot_tab.numel() >= n_slots * 9, "slot table [n_slots, 9] int32");
+  check(qfx_hea_frags(dp<float>(params, torch::kFloat32, "params", K * p_stride), (int)p_stride,
+                      dp<int>(slot_tab, torch::kInt32, "slot_tab", n_slots * 9), (int)n_slots, (int)K,
+                      dp<int32_t>(frags, torch::kInt32, "frags", K * n_slots * 4 * 128 * 4), cur()),
+        "qfx_hea_frags");
+}
+
+void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, torch::Tensor owner_tiles, int64_t n_theta, int64_t spc,
+                     int64_t K, torch::Tensor grad, int64_t p_stride) {
+  check(qfx_hea_grad_reduce(dp<float>(gslab, torch::kFloat32, "gslab", K * spc * slab_tiles * n_theta),
+                            (int)slab_tiles, dp<int>(owner_tiles, torch::kInt32, "owner_tiles", n_theta),
+                            (int)n_theta, (int)spc, (int)K, dp<float>(grad, torch::kFloat32, "grad", K * p_stride),
+                            (int)p_stride, cur()),
+        "qfx_hea_grad_reduce");
+}
+
+}  // namespace
+
+void register_hea(pybind11::module& m) {
+  m.def("hea_pass", &hea_pass);
+  m.def("hea_frags", &hea_frags);
+  m.def("hea_check_ops", &hea_check_ops);
+  m.def("hea_grad_reduce", &hea_grad_reduce);
+  m.def("hea_args_size", []() { return qfx_hea_args_size(); });
+}

@@ -1,0 +1,647 @@
+// MFMA statevector engine for the hardware-efficient VQC (plan: qfedx_amd/ops/hea_plan.py).
+//
+// One workgroup owns one LDS tile of 2^t amplitudes of one sample (t <= 14; fp16 (re, im) packed in a
+// u32 = 64 KB per state).  A pass = [product-state generation | tile load] -> op list -> [store],
+// where every rotation op is a 16 x 16 complex unitary on a 4-dim GF(2) subspace of the tile:
+//
+//     Y[m', col] = sum_m U[m', m] X[m, col]        (columns = cosets of the subspace, 2^(t-4) of them)
+//
+// executed as v_mfma_f32_16x16x32_f16 with the complex matrix in its real 32 x 32 embedding (two
+// 16-row blocks, K = 32 = 16 amplitudes x (re, im)) and split hi + lo in fp16 so the unitary is exact
+// to ~2^-22 (the state itself is fp16 between ops, fp32 inside the MFMA).  Column c of a block maps to
+// tile address  y'(c) ^ OFF[m ^ b(c)]  with y' a deposit of c into the non-pivot bits and b(c) the
+// logical bits of y' in the op's CNOT frame (parities with the frame's row masks) - the CNOT chains are
+// never executed, only folded into this addressing.
+//
+// Adjoint ops: gradient cross matrix N[b][a] = sum_col psi[b] conj(lam[a]) as two MFMAs per 16 columns
+// (A = psi, B = lam and i*lam), reduced over waves in LDS; each qubit's 2x2 partial trace of N gives
+// d/dtheta = Im(e^-i.phi n10 + e^i.phi n01) and d/dphi = Im(n00 - n11) (RZ(phi) RX(theta) rotation).
+// Per-workgroup gradient partials go to a slab that hea_grad_reduce sums in a fixed order.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hea_args.h"
+
+namespace hea {
+
+constexpr int OPW = 128;
+enum { OP_APPLY = 1, OP_UNAPPLY_PSI = 2, OP_UNAPPLY_LAM = 3, OP_GRAD = 4, OP_GRAD_L1 = 5, OP_OBS = 6, OP_READOUT = 7,
+       OP_BACK = 8 };
+enum { W_CODE = 0, W_SLOT = 1, W_NREAL = 2, W_FLAGS = 3, W_RFULL = 4, W_RT = 8, W_TH = 12, W_PH = 16, W_OFF = 20,
+       W_BL = 36, W_BH = 68 };
+constexpr int F_BACK_PSI = 1;
+constexpr int TMAX = 14;
+constexpr int NT_FWD = 512;    // forward: 8 waves, 64 KB LDS -> 2 workgroups per CU
+constexpr int NT_ADJ = 1024;   // adjoint: 16 waves, 128 KB LDS (psi + lambda) -> 1 workgroup per CU
+constexpr int CMAX = 8;
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+
+using PassArgs = HeaPassArgs;
+
+__device__ __forceinline__ uint32_t pack_h2(float re, float im) {
+  half2v h = {(_Float16)re, (_Float16)im};
+  return __builtin_bit_cast(uint32_t, h);
+}
+
+__device__ __forceinline__ float2 unpack_h2(uint32_t u) {
+  half2v h = __builtin_bit_cast(half2v, u);
+  return make_float2((float)h.x, (float)h.y);
+}
+
+__device__ __forceinline__ int par(uint32_t x) { return __builtin_popcount(x) & 1; }
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+
+__device__ __forceinline__ f4 mfma(uint4 a, uint4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), c, 0,
+                                                 0, 0);
+}
+
+// memory index of tile position tau
+__device__ __forceinline__ uint32_t mem_of(uint32_t tau, const PassArgs& a, uint32_t fixed) {
+  const uint32_t cm = (1u << a.c) - 1u;
+  return (tau & cm) | ((tau >> a.c) << a.lo) | fixed;
+}
+
+// LDS swizzle h(x) (5 bank bits) of the high tile bits x = tau >> 5
+__device__ __forceinline__ uint32_t swz(const PassArgs& a, uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 5; ++b) r |= (uint32_t)par((uint32_t)a.hrow[b] & x) << b;
+  return r;
+}
+
+// out[j] = in[j ^ r]: a 16-byte quad whose dwords the swizzle permutes inside their aligned quad
+__device__ __forceinline__ uint4 quad_perm(uint4 v, uint32_t r) {
+  if (r & 1u) v = make_uint4(v.y, v.x, v.w, v.z);
+  if (r & 2u) v = make_uint4(v.z, v.w, v.x, v.y);
+  return v;
+}
+
+// Global [mem order] <-> LDS [swizzled] tile copies: quad q = 4 (tid + NT i) of the tile sits at LDS dword
+// (q ^ h) & ~3 with its dwords permuted by h & 3, h = h(q >> 5) = h(tid >> 3) ^ h(4 NT / 32 * i).  All of a
+// thread's global loads are issued before its LDS writes.
+template <int NT>
+__device__ __forceinline__ void load_tile(const PassArgs& a, const uint32_t* src, uint32_t* dst, int tid, int T,
+                                          uint32_t h_q, uint32_t fixed) {
+  constexpr int MQ = (1 << TMAX) / (4 * NT);
+  uint4 v[MQ];
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) v[i] = *(const uint4*)&src[mem_of(q, a, fixed)];
+  }
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) {
+      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+      *(uint4*)&dst[(q ^ h) & ~3u] = quad_perm(v[i], h & 3u);
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, const uint32_t* src, int tid, int T,
+                                           uint32_t h_q, uint32_t fixed) {
+  constexpr int MQ = (1 << TMAX) / (4 * NT);
+  uint4 v[MQ];
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) {
+      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+      v[i] = quad_perm(*(const uint4*)&src[(q ^ h) & ~3u], h & 3u);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
+  }
+}
+
+// RZ(ph) RX(th) F(x)|0> for a layer-1 qubit
+__device__ void l1_factor(float x, float th, float ph, int feature, float2* w) {
+  float sa, ca;
+  __sincosf(0.5f * x, &sa, &ca);
+  float2 v0, v1;
+  if (feature == 1) {          // rx
+    v0 = make_float2(ca, 0.f);
+    v1 = make_float2(0.f, -sa);
+  } else if (feature == 2) {   // rz
+    v0 = make_float2(ca, -sa);
+    v1 = make_float2(0.f, 0.f);
+  } else {                     // ry
+    v0 = make_float2(ca, 0.f);
+    v1 = make_float2(sa, 0.f);
+  }
+  float s, c;
+  __sincosf(0.5f * th, &s, &c);
+  // RX: w0 = c v0 - i s v1 ; w1 = -i s v0 + c v1      (-i z = (z.y, -z.x))
+  float2 w0 = make_float2(c * v0.x + s * v1.y, c * v0.y - s * v1.x);
+  float2 w1 = make_float2(c * v1.x + s * v0.y, c * v1.y - s * v0.x);
+  float sp, cp;
+  __sincosf(0.5f * ph, &sp, &cp);
+  w[0] = cmul(w0, make_float2(cp, -sp));
+  w[1] = cmul(w1, make_float2(cp, sp));
+}
+
+// LDS image: one dword array, psi at byte 0 and lambda at byte LAM_OFF (adjoint), every amplitude
+// addressed by BYTE offset = 4 * sigma(tau); all table entries combine by XOR, so a target's tile base
+// (0 / LAM_OFF, bit 16) is XORed into the lane's constant offsets once per op and each access is one XOR.
+constexpr uint32_t LAM_OFF = 4u << TMAX;
+
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* tile, uint32_t byte) {
+  return *(const uint32_t*)((const char*)tile + byte);
+}
+__device__ __forceinline__ void lds_st(uint32_t* tile, uint32_t byte, uint32_t v) {
+  *(uint32_t*)((char*)tile + byte) = v;
+}
+
+
+// Y = U X on the op's column blocks for NX targets (tile byte bases tb[x]) sharing the addressing.  Lane
+// (g4, cl) owns column cl of a 16-column block: it reads amplitudes m = 4 g4 .. 4 g4 + 3 (B operand,
+// k = 2m + re/im) and writes rows m' = 2 g4, 2 g4 + 1, 8 + 2 g4, 9 + 2 g4 of the two 16-row output blocks.
+// A wave's blocks are blk = wave + NW i (i < nbw <= MAXB, fully unrolled): (blk & 1) = (wave & 1), so the
+// block bases are BL[lane] ^ BH[blk >> 1] precomputed in registers.  Blocks go in pairs (independent MFMA
+// chains) and the next pair's operands are read before the current pair is written (disjoint blocks).
+template <int NX, int NW>
+__device__ __forceinline__ void group_apply(uint32_t* tile, const uint32_t* tb, const uint4* F, const int* opw,
+                                            uint32_t fo, int lane, int wave, int nbw) {
+  constexpr int MAXB = (1 << (TMAX - 8)) / NW;   // column blocks per wave per op (t = 14: 64 blocks)
+  const int g4 = lane >> 4, cl = lane & 15;
+  uint32_t oin[NX][4], oout[NX][4];
+#pragma unroll
+  for (int x = 0; x < NX; ++x) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) oin[x][jj] = (((uint32_t)opw[W_OFF + 4 * g4 + jj] ^ fo) << 2) ^ tb[x];
+    oout[x][0] = (((uint32_t)opw[W_OFF + 2 * g4] ^ fo) << 2) ^ tb[x];
+    oout[x][1] = (((uint32_t)opw[W_OFF + 2 * g4 + 1] ^ fo) << 2) ^ tb[x];
+    oout[x][2] = (((uint32_t)opw[W_OFF + 8 + 2 * g4] ^ fo) << 2) ^ tb[x];
+    oout[x][3] = (((uint32_t)opw[W_OFF + 9 + 2 * g4] ^ fo) << 2) ^ tb[x];
+  }
+  const uint32_t bl = (uint32_t)opw[W_BL + (wave & 1) * 16 + cl];
+  uint32_t base[MAXB];
+#pragma unroll
+  for (int i = 0; i < MAXB; ++i) base[i] = (bl ^ (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)]) << 2;
+  auto load = [&](uint32_t b, int x) -> uint4 {
+    return make_uint4(lds_ld(tile, b ^ oin[x][0]), lds_ld(tile, b ^ oin[x][1]), lds_ld(tile, b ^ oin[x][2]),
+                      lds_ld(tile, b ^ oin[x][3]));
+  };
+  auto compute_store = [&](uint32_t b, const uint4& X, int x) {
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    f4 d0 = mfma(F[0], X, z), d1 = mfma(F[1], X, z);
+    d0 = mfma(F[2], X, d0);
+    d1 = mfma(F[3], X, d1);
+    lds_st(tile, b ^ oout[x][0], pack_h2(d0[0], d0[1]));
+    lds_st(tile, b ^ oout[x][1], pack_h2(d0[2], d0[3]));
+    lds_st(tile, b ^ oout[x][2], pack_h2(d1[0], d1[1]));
+    lds_st(tile, b ^ oout[x][3], pack_h2(d1[2], d1[3]));
+  };
+  if (nbw <= 0) return;
+  uint4 B0[NX], B1[NX];
+#pragma unroll
+  for (int x = 0; x < NX; ++x) {
+    B0[x] = load(base[0], x);
+    if (nbw > 1) B1[x] = load(base[1], x);
+  }
+#pragma unroll
+  for (int p = 0; p < MAXB; p += 2) {
+    if (p >= nbw) break;
+    uint4 C0[NX], C1[NX];
+    constexpr bool PREFETCH = NX == 1 || NW <= 8;   // the two-target form at 16 waves stays within 128 VGPRs
+    if (PREFETCH && p + 2 < MAXB && p + 2 < nbw) {
+#pragma unroll
+      for (int x = 0; x < NX; ++x) {
+        C0[x] = load(base[p + 2 < MAXB ? p + 2 : 0], x);
+        if (p + 3 < nbw) C1[x] = load(base[p + 3 < MAXB ? p + 3 : 0], x);
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < NX; ++x) {
+      compute_store(base[p], B0[x], x);
+      if (p + 1 < nbw) compute_store(base[p + 1 < MAXB ? p + 1 : 0], B1[x], x);
+    }
+    if (PREFETCH) {
+#pragma unroll
+      for (int x = 0; x < NX; ++x) {
+        B0[x] = C0[x];
+        B1[x] = C1[x];
+      }
+    } else if (p + 2 < MAXB && p + 2 < nbw) {
+#pragma unroll
+      for (int x = 0; x < NX; ++x) {
+        B0[x] = load(base[p + 2 < MAXB ? p + 2 : 0], x);
+        if (p + 3 < nbw) B1[x] = load(base[p + 3 < MAXB ? p + 3 : 0], x);
+      }
+    }
+  }
+}
+
+// Gradient cross matrix N[b][a] += sum_col psi[b][col] conj(lam[a][col]) over the op's column blocks:
+// K = 16 columns x (re, im), lane (g4, cl) reads amplitude m = cl of columns 4 g4 .. 4 g4 + 3; accR / accI
+// end up holding N[4 g4 + i][cl] (real / imaginary).
+template <int NW>
+__device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw, uint32_t fo, int lane, int wave,
+                                            int nbw, f4& accR, f4& accI) {
+  constexpr int MAXB = (1 << (TMAX - 8)) / NW;
+  const int g4 = lane >> 4, cl = lane & 15;
+  const uint32_t om = (uint32_t)opw[W_OFF + cl] ^ fo;
+  uint32_t gb[4];
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) gb[jj] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + jj] ^ om) << 2;
+#pragma unroll
+  for (int i = 0; i < MAXB; ++i) {
+    if (i >= nbw) break;
+    const uint32_t bh = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << 2;
+    uint32_t pv[4], lv[4];
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      pv[jj] = lds_ld(tile, gb[jj] ^ bh);
+      lv[jj] = lds_ld(tile, gb[jj] ^ bh ^ LAM_OFF);
+    }
+    const uint4 A = make_uint4(pv[0], pv[1], pv[2], pv[3]);
+    const uint4 Br = make_uint4(lv[0], lv[1], lv[2], lv[3]);
+    // i*lam: (re, im) -> (-im, re)
+    const uint4 Bi = make_uint4((lv[0] >> 16 ^ 0x8000u) | (lv[0] << 16), (lv[1] >> 16 ^ 0x8000u) | (lv[1] << 16),
+                                (lv[2] >> 16 ^ 0x8000u) | (lv[2] << 16), (lv[3] >> 16 ^ 0x8000u) | (lv[3] << 16));
+    accR = mfma(A, Br, accR);
+    accI = mfma(A, Bi, accI);
+  }
+}
+
+__device__ __forceinline__ void load_frags(const PassArgs& a, int k, int fi, int lane, uint4* F) {
+  if (fi < 0) return;
+  const uint4* fr = (const uint4*)a.frags + ((size_t)k * a.n_slots * 4 + fi) * 128;
+  F[0] = fr[lane];
+  F[1] = fr[64 + lane];
+  F[2] = fr[128 + lane];
+  F[3] = fr[192 + lane];
+}
+
+template <bool ADJ>
+__global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArgs a) {
+  constexpr int NT = ADJ ? NT_ADJ : NT_FWD, NW = NT / 64;
+  __shared__ uint32_t tile[(ADJ ? 2 : 1) << TMAX];     // psi | lambda (fp16 re, im), swizzled
+  __shared__ int opw[OPW];
+  __shared__ float red[NW * CMAX];
+  __shared__ unsigned long long red64[ADJ ? 512 : 1];   // gradient cross matrix, 2^-20 fixed point
+  __shared__ float2 wv[32][2];
+  __shared__ float2 tabA[128];
+  __shared__ float2 tabB[128];
+  __shared__ float rsc[CMAX + 2];
+  uint32_t* psi_t = tile;
+  uint32_t* lam_t = tile + (ADJ ? (1 << TMAX) : 0);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s = blockIdx.x / a.n_tiles, tile_id = blockIdx.x % a.n_tiles;
+  const int k = s / a.spc;
+  const int T = 1 << a.t;
+  const size_t N = (size_t)1 << a.n;
+  const int w1 = a.lo - a.c;
+  const uint32_t fixed = ((uint32_t)(tile_id & ((1 << w1) - 1)) << a.c) | ((uint32_t)(tile_id >> w1) << a.hi);
+  const float* prm = a.params + (size_t)k * a.p_stride;
+  // swizzle / parity decomposition: word w = tid + NT i  ->  f(w >> 5) = f(tid >> 5) ^ f(16 i)  (h linear)
+  const uint32_t h_w = swz(a, (uint32_t)tid >> 5);        // for words tid + NT i
+  long long* dbg = (a.dbg && blockIdx.x < 8) ? a.dbg + blockIdx.x * 64 : nullptr;
+  int ndbg = 0;
+#define HEA_MARK()                                              \
+  do {                                                          \
+    if (dbg && tid == 0 && ndbg < 64) dbg[ndbg] = (long long)__builtin_readcyclecounter(); \
+    ++ndbg;                                                     \
+  } while (0)
+  HEA_MARK();
+  const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
+
+  // ---------------------------------------------------------------- initial psi tile
+  if (a.gen) {
+    if (tid < a.n) {
+      float2 w[2];
+      l1_factor(a.xang[(size_t)s * a.x_stride + tid], prm[2 * tid], prm[2 * tid + 1], a.feature, w);
+      wv[tid][0] = w[0];
+      wv[tid][1] = w[1];
+    }
+    __syncthreads();
+    HEA_MARK();
+    const int ta = a.t >> 1, tb = a.t - ta;
+    if (tid < (1 << ta)) {                          // threads [0, 2^ta): low-half products
+      const int i = tid;
+      float2 v = make_float2(1.f, 0.f);
+      for (int j = 0; j < ta; ++j) {
+        const int mb = j < a.c ? j : a.lo + j - a.c;
+        v = cmul(v, wv[mb][(i >> j) & 1]);
+      }
+      tabA[i] = v;
+    } else if (tid >= 256 && tid < 256 + (1 << tb)) {   // threads [256, 256 + 2^tb): high half x fixed bits
+      const int i = tid - 256;
+      float2 v = make_float2(a.scale, 0.f);
+      for (int q = 0; q < a.n; ++q) {
+        const bool in_tile = q < a.c || (q >= a.lo && q < a.hi);
+        if (!in_tile) v = cmul(v, wv[q][(fixed >> q) & 1]);
+      }
+      for (int j = 0; j < tb; ++j) {
+        const int tj = ta + j;
+        const int mb = tj < a.c ? tj : a.lo + tj - a.c;
+        v = cmul(v, wv[mb][(i >> j) & 1]);
+      }
+      tabB[i] = v;
+    }
+    __syncthreads();
+    HEA_MARK();
+    const uint32_t am = (1u << ta) - 1u;
+    const int iters = (T + NT - 1) / NT;
+#pragma unroll 4
+    for (int i = 0; i < iters; ++i) {       // LDS dword w holds amplitude tau = sigma(w)
+      const uint32_t w = (uint32_t)(tid + NT * i);
+      const uint32_t tau = w ^ h_w ^ swz(a, (uint32_t)(NT >> 5) * i);
+      if (w < (uint32_t)T) {
+        const float2 v = cmul(tabA[tau & am], tabB[tau >> ta]);
+        psi_t[w] = pack_h2(v.x, v.y);
+      }
+    }
+  } else {
+    load_tile<NT>(a, a.psi_in + (size_t)s * N, psi_t, tid, T, h_q, fixed);
+  }
+  if (ADJ) {
+    if (a.load_lam) {
+      load_tile<NT>(a, a.lam_in + (size_t)s * N, lam_t, tid, T, h_q, fixed);
+    }
+    if (tid == 0) {
+      float rho = 0.f;
+      for (int c = 0; c < a.C; ++c) rho = fmaxf(rho, fabsf(a.wread[(size_t)s * a.C + c]));
+      if (rho == 0.f) rho = 1.f;
+      for (int c = 0; c < a.C; ++c) rsc[c] = a.wread[(size_t)s * a.C + c] / rho;
+      rsc[CMAX] = rho / (a.scale * a.scale);
+    }
+  }
+
+  // ---------------------------------------------------------------- op list
+  if (ADJ)
+    for (int e = tid; e < 512; e += NT) red64[e] = 0ull;
+  const int ncol = T >> 4, nblk = ncol >> 4;
+  const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
+  // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op)
+  int nxt = (tid < OPW && a.nops > 0) ? a.ops[tid] : 0;
+  uint4 FN[4] = {};
+  if (a.nops > 0) load_frags(a, k, a.fidx[0], lane, FN);
+  __syncthreads();
+  HEA_MARK();
+  for (int o = 0; o < a.nops; ++o) {
+    __syncthreads();
+    HEA_MARK();
+    if (tid < OPW) opw[tid] = nxt;
+    const uint4 F[4] = {FN[0], FN[1], FN[2], FN[3]};
+    __syncthreads();
+    if (o + 1 < a.nops) {
+      if (tid < OPW) nxt = a.ops[(size_t)(o + 1) * OPW + tid];
+      load_frags(a, k, a.fidx[o + 1], lane, FN);
+    }
+    const int code = opw[W_CODE];
+    const int nreal = opw[W_NREAL];
+    if (code == OP_APPLY || code == OP_UNAPPLY_PSI || code == OP_UNAPPLY_LAM || code == OP_BACK ||
+        code == OP_GRAD || code == OP_GRAD_L1) {
+      int fpb = 0;
+      for (int j = 0; j < nreal; ++j) fpb |= par(fixed & (uint32_t)opw[W_RFULL + j]) << j;
+      const uint32_t fo = (uint32_t)opw[W_OFF + fpb];
+      const uint32_t tbp[1] = {0u}, tbl[1] = {LAM_OFF}, tbb[2] = {LAM_OFF, 0u};
+      if (code == OP_APPLY || code == OP_UNAPPLY_PSI) {
+        group_apply<1, NW>(tile, tbp, F, opw, fo, lane, wave, nbw);
+      } else if (ADJ && code == OP_UNAPPLY_LAM) {
+        group_apply<1, NW>(tile, tbl, F, opw, fo, lane, wave, nbw);
+      } else if (ADJ) {   // OP_BACK / OP_GRAD / OP_GRAD_L1
+        f4 accR = {0.f, 0.f, 0.f, 0.f}, accI = {0.f, 0.f, 0.f, 0.f};
+        group_cross<NW>(tile, opw, fo, lane, wave, nbw, accR, accI);
+        if (code == OP_BACK) {
+          if (opw[W_FLAGS] & F_BACK_PSI)
+            group_apply<2, NW>(tile, tbb, F, opw, fo, lane, wave, nbw);
+          else
+            group_apply<1, NW>(tile, tbl, F, opw, fo, lane, wave, nbw);
+        }
+        // Cross-wave sum of N in 2^-20 fixed point with 64-bit LDS atomics: integer addition is associative, so
+        // the sum is bitwise independent of the order the waves arrive in.  Only entries with b ^ a in
+        // {0, e_j} enter a partial trace; lane (g4, cl) holds N[4 g4 + i][cl].
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15;
+          if (__builtin_popcount(bb ^ aa) <= 1) {
+            const int e = bb * 16 + aa;
+            atomicAdd(&red64[e], (unsigned long long)(long long)((double)accR[i] * 1048576.0));
+            atomicAdd(&red64[256 + e], (unsigned long long)(long long)((double)accI[i] * 1048576.0));
+          }
+        }
+        __syncthreads();
+        if (wave == 0) {   // partial traces: lane (j, y, x, comp) sums N[b][a], b_j = y, a_j = x, b ^ a in {0, e_j}
+          const int j = (lane >> 3) & 3, y = (lane >> 2) & 1, x = (lane >> 1) & 1, comp = lane & 1;
+          double v = 0.0;
+          if (lane < 32 && j < nreal) {
+            const int lowm = (1 << j) - 1;
+            for (int o8 = 0; o8 < 8; ++o8) {    // the other three bits of b
+              const int bb = ((o8 & ~lowm) << 1) | (o8 & lowm) | (y << j);
+              const int aa = (bb & ~(1 << j)) | (x << j);
+              v += (double)(long long)red64[comp * 256 + bb * 16 + aa];
+            }
+          }
+          const float pv = (float)(v * (1.0 / 1048576.0));
+          // lane 8j + k holds pt[k] = n[y][x].(re, im) with k = 4y + 2x + comp
+          const int jj = lane >> 1;
+          const float p1 = __shfl(pv, 8 * jj + 1, 64), p2 = __shfl(pv, 8 * jj + 2, 64);
+          const float p3 = __shfl(pv, 8 * jj + 3, 64), p4 = __shfl(pv, 8 * jj + 4, 64);
+          const float p5 = __shfl(pv, 8 * jj + 5, 64), p7 = __shfl(pv, 8 * jj + 7, 64);
+          for (int e = lane; e < 512; e += 64) red64[e] = 0ull;     // ready for the next gradient op
+          if (lane < 2 * nreal) {
+            float* gs = a.gslab + ((size_t)s * a.slab_tiles + tile_id) * a.n_theta;
+            if ((lane & 1) == 0) {               // d/dtheta = Im(e^{-i ph} n10 + e^{i ph} n01)
+              float sp, cp;
+              __sincosf(prm[opw[W_PH + jj]], &sp, &cp);
+              gs[opw[W_TH + jj]] = ((cp * p5 - sp * p4) + (cp * p3 + sp * p2)) * rsc[CMAX];
+            } else {                             // d/dphi = Im(n00 - n11)
+              gs[opw[W_PH + jj]] = (p1 - p7) * rsc[CMAX];
+            }
+          }
+        }
+      }
+    } else if (ADJ && code == OP_OBS) {
+      // sign_c(w) = parity(w & O'_c) ^ parity(fixed & O_c) = per-thread part ^ per-iteration (uniform) part
+      uint32_t om[CMAX], sgn0 = 0;
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) {
+        om[c] = c < a.C ? (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_OFF + c]) : 0u;
+        const uint32_t of = c < a.C ? (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_RFULL + 2 * c]) : 0u;
+        sgn0 |= (uint32_t)(par((uint32_t)tid & om[c]) ^ par(fixed & of)) << c;
+      }
+      const int iters = (T + NT - 1) / NT;
+#pragma unroll 4
+      for (int i = 0; i < iters; ++i) {
+        const int w = tid + NT * i;
+        if (w >= T) continue;
+        float fsum = 0.f;
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c) {
+          if (c < a.C) {
+            const uint32_t sg = ((sgn0 >> c) & 1u) ^ (uint32_t)par((uint32_t)(NT * i) & om[c]);
+            fsum += sg ? -rsc[c] : rsc[c];
+          }
+        }
+        const float2 v = unpack_h2(psi_t[w]);
+        lam_t[w] = pack_h2(fsum * v.x, fsum * v.y);
+      }
+    } else if (code == OP_READOUT) {
+      uint32_t om[CMAX], sgn0 = 0;
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) {
+        om[c] = c < a.C ? (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_OFF + c]) : 0u;
+        const uint32_t of = c < a.C ? (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_RFULL + 2 * c]) : 0u;
+        sgn0 |= (uint32_t)(par((uint32_t)tid & om[c]) ^ par(fixed & of)) << c;
+      }
+      float acc[CMAX];
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) acc[c] = 0.f;
+      const int iters = (T + NT - 1) / NT;
+#pragma unroll 4
+      for (int i = 0; i < iters; ++i) {
+        const int w = tid + NT * i;
+        if (w >= T) continue;
+        const float2 v = unpack_h2(psi_t[w]);
+        const float p = v.x * v.x + v.y * v.y;
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c) {
+          if (c < a.C) {
+            const uint32_t sg = ((sgn0 >> c) & 1u) ^ (uint32_t)par((uint32_t)(NT * i) & om[c]);
+            acc[c] += sg ? -p : p;
+          }
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) {
+        if (c < a.C) {
+          float v = acc[c];
+          for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+          if (lane == 0) red[wave * CMAX + c] = v;
+        }
+      }
+      __syncthreads();
+      if (tid < a.C) {
+        float v = 0.f;
+        for (int w = 0; w < NW; ++w) v += red[w * CMAX + tid];
+        a.part[((size_t)s * a.n_tiles + tile_id) * a.C + tid] = v / (a.scale * a.scale);
+      }
+    }
+  }
+  __syncthreads();
+  HEA_MARK();
+  if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
+  if (ADJ && a.store_lam) store_tile<NT>(a, a.lam_out + (size_t)s * N, lam_t, tid, T, h_q, fixed);
+  __syncthreads();
+  HEA_MARK();
+#undef HEA_MARK
+}
+
+// Unitary fragments: per (client, slot) U and U^H in the real 32 x 32 embedding, laid out as the MFMA
+// A operand of v_mfma_f32_16x16x32_f16 (lane l: row 16h + (l & 15), k = 8 (l >> 4) .. +7), hi and lo fp16.
+// frags[((k * n_slots + slot) * 4 + f) * 128 + h * 64 + lane], f = 0 U hi, 1 U lo, 2 U^H hi, 3 U^H lo.
+__global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__ params, int p_stride,
+                                                       const int* __restrict__ slot_tab, int n_slots,
+                                                       uint4* __restrict__ frags) {
+  const int slot = blockIdx.x, k = blockIdx.y;
+  const int t = threadIdx.x, dag = t >> 7, h = (t >> 6) & 1, lane = t & 63;
+  const int* st = slot_tab + slot * 9;
+  const int nreal = st[0];
+  const float* prm = params + (size_t)k * p_stride;
+  float2 u[4][2][2];
+  for (int j = 0; j < 4; ++j) {
+    if (j < nreal) {
+      float s, c, sp, cp;
+      __sincosf(0.5f * prm[st[1 + j]], &s, &c);
+      __sincosf(0.5f * prm[st[5 + j]], &sp, &cp);
+      // RZ(ph) RX(th) = [[e- c, -i e- s], [-i e+ s, e+ c]],  e-+ = cp -+ i sp
+      u[j][0][0] = make_float2(cp * c, -sp * c);
+      u[j][0][1] = make_float2(-sp * s, -cp * s);
+      u[j][1][0] = make_float2(sp * s, -cp * s);
+      u[j][1][1] = make_float2(cp * c, sp * c);
+    } else {
+      u[j][0][0] = make_float2(1.f, 0.f);
+      u[j][0][1] = make_float2(0.f, 0.f);
+      u[j][1][0] = make_float2(0.f, 0.f);
+      u[j][1][1] = make_float2(1.f, 0.f);
+    }
+  }
+  const int r = 16 * h + (lane & 15);
+  _Float16 hi[8], lo[8];
+  for (int jj = 0; jj < 8; ++jj) {
+    const int kk = 8 * (lane >> 4) + jj;
+    const int mp = r >> 1, cr = r & 1, m = kk >> 1, ck = kk & 1;
+    const int row = dag ? m : mp, colm = dag ? mp : m;   // U^H[mp][m] = conj(U[m][mp])
+    float2 v = make_float2(1.f, 0.f);
+    for (int j = 0; j < 4; ++j) v = cmul(v, u[j][(row >> j) & 1][(colm >> j) & 1]);
+    if (dag) v.y = -v.y;
+    const float val = cr == 0 ? (ck == 0 ? v.x : -v.y) : (ck == 0 ? v.y : v.x);
+    hi[jj] = (_Float16)val;
+    lo[jj] = (_Float16)(val - (float)hi[jj]);
+  }
+  uint4 H, Lw;
+  uint32_t* hp = (uint32_t*)&H;
+  uint32_t* lp = (uint32_t*)&Lw;
+  for (int i = 0; i < 4; ++i) {
+    half2v a2 = {hi[2 * i], hi[2 * i + 1]}, b2 = {lo[2 * i], lo[2 * i + 1]};
+    hp[i] = __builtin_bit_cast(uint32_t, a2);
+    lp[i] = __builtin_bit_cast(uint32_t, b2);
+  }
+  uint4* base = frags + ((size_t)(k * n_slots + slot) * 4 + 2 * dag) * 128;
+  base[h * 64 + lane] = H;
+  base[128 + h * 64 + lane] = Lw;
+}
+
+// grad[k][j] = sum over the client's samples and the owner pass' tiles of the slab (fixed order)
+__global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const float* __restrict__ gslab, int slab_tiles,
+                                                              const int* __restrict__ owner_tiles, int n_theta,
+                                                              int spc, float* __restrict__ grad, int p_stride) {
+  const int k = blockIdx.x;
+  for (int j = threadIdx.x; j < n_theta; j += 256) {
+    const int nt = owner_tiles[j];
+    float acc = 0.f;
+    for (int s = k * spc; s < (k + 1) * spc; ++s)
+      for (int t = 0; t < nt; ++t) acc += gslab[((size_t)s * slab_tiles + t) * n_theta + j];
+    grad[(size_t)k * p_stride + j] = acc;
+  }
+}
+
+}  // namespace hea
+
+extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_samples, hipStream_t st) {
+  const hea::PassArgs& a = *args;
+  if (a.t > hea::TMAX || a.t < 8 || a.C > hea::CMAX || a.n > 30 || a.c < 2) return -2;
+  const unsigned grid = (unsigned)(n_samples * a.n_tiles);
+  if (grid == 0) return 0;
+  if (adjoint)
+    hipLaunchKernelGGL(hea::hea_pass_kernel<true>, dim3(grid), dim3(hea::NT_ADJ), 0, st, a);
+  else
+    hipLaunchKernelGGL(hea::hea_pass_kernel<false>, dim3(grid), dim3(hea::NT_FWD), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
+                             hipStream_t st) {
+  if (n_slots == 0 || K == 0) return 0;
+  hipLaunchKernelGGL(hea::hea_frag_kernel, dim3(n_slots, K), dim3(256), 0, st, params, p_stride, slot_tab, n_slots,
+                     (uint4*)frags);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_hea_grad_reduce(const float* gslab, int slab_tiles, const int* owner_tiles, int n_theta, int spc,
+                                   int K, float* grad, int p_stride, hipStream_t st) {
+  if (K == 0) return 0;
+  hipLaunchKernelGGL(hea::hea_grad_reduce_kernel, dim3(K), dim3(256), 0, st, gslab, slab_tiles, owner_tiles, n_theta,
+                     spc, grad, p_stride);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_hea_args_size() { return (int)sizeof(hea::PassArgs); }

@@ -59,6 +59,11 @@ class VQCEngine:
         if backend == "torch":
             self.prog = TorchProgram(ops, coef, spec.n_qubits, self.device)
             self.hip = None
+        elif backend == "hip" and state_dtype in ("mfma", "fp16"):
+            # fp16 states + MFMA group unitaries (ops/hea_mfma.py) for the hardware-efficient ansatz
+            from .hea_mfma import HeaMfmaProgram
+            self.hip = HeaMfmaProgram(spec, self.device)
+            self.prog = TorchProgram(ops, coef, spec.n_qubits, self.device)
         elif backend == "hip":
             from .statevec_hip import HipProgram
             self.hip = HipProgram(ops, coef, spec.n_qubits, spec.readout, self.device,

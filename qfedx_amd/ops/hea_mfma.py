@@ -1,0 +1,244 @@
+"""MFMA statevector engine for the hardware-efficient VQC (host side).
+
+``HeaMfmaProgram`` runs the pass plans of ``ops/hea_plan.py`` on the gfx950 kernels of
+``csrc/hea_mfma.hip``: per local step
+
+    hea_frags (per-client 16 x 16 group unitaries -> MFMA A fragments, hi + lo fp16)
+    forward passes  (product state generated in-tile; intermediate pass outputs stored as fp16 (re, im))
+    readout_ce      (shared with the VALU engine: <Z>, CE loss, dL/d<Z>, a/b gradients)
+    adjoint passes  (reverse pass order; per-workgroup gradient partials)
+    hea_grad_reduce (fixed-order sum over each client's samples and tiles)
+
+It exposes the subset of ``HipProgram``'s interface the engine / trainer use (``expz``, ``vjp``,
+``loss_and_grads``, ``private_workspace``), so ``VQCEngine(..., backend="hip", state_dtype="mfma")``
+swaps it in for circuits ``hea_plan.eligible`` accepts.  Amplitudes are stored as fp16 scaled by
+2^(n/2) (unit-magnitude typical values); MFMAs accumulate in fp32 and the unitaries carry a hi/lo fp16
+split, so the only rounding is the fp16 state between ops (~2^-12 relative per op).
+"""
+from __future__ import annotations
+
+import contextlib
+
+import numpy as np
+import torch
+
+from ._ext import ext
+from .hea_plan import TILE_BITS, build_plan, eligible, pass_programs
+
+_FEATURE = {"ry": 0, "rx": 1, "rz": 2}
+
+
+def _frag_index(ops: np.ndarray) -> torch.Tensor:
+    """Per op the unitary fragment it multiplies by (slot * 4 + 0: U, + 2: U^H) or -1 (prefetch table)."""
+    from .hea_plan import OP_APPLY, OP_BACK, OP_UNAPPLY_LAM, OP_UNAPPLY_PSI, W_CODE, W_SLOT
+    out = np.full(len(ops), -1, dtype=np.int32)
+    for i, w in enumerate(ops):
+        code = int(w[W_CODE])
+        if code == OP_APPLY:
+            out[i] = 4 * int(w[W_SLOT])
+        elif code in (OP_UNAPPLY_PSI, OP_UNAPPLY_LAM, OP_BACK):
+            out[i] = 4 * int(w[W_SLOT]) + 2
+    return torch.from_numpy(out)
+_NO_KEYS = torch.zeros(0, dtype=torch.int64)
+_NODBG = torch.zeros(0, dtype=torch.int64)     # no phase timestamps
+
+
+class HeaMfmaProgram:
+    def __init__(self, spec, device, tile_bits: int = TILE_BITS):
+        if not eligible(spec):
+            raise ValueError("the MFMA engine covers angle-encoded RX/RZ + CNOT-chain VQCs with 8..30 qubits, "
+                             "no gate noise and <= 8 classes")
+        self.spec = spec
+        self.n = spec.n_qubits
+        self.C = spec.n_classes
+        self.n_theta = spec.n_theta
+        self.device = torch.device(device)
+        self.plan = build_plan(self.n, spec.n_layers, spec.readout, spec.entangler == "chain", spec.feature_map,
+                               tile_bits)
+        C = ext()
+        self.n_slots = self.plan.n_slots
+        self.passes = []
+        for p, fwd, adj in pass_programs(self.plan):
+            f = torch.from_numpy(fwd.astype(np.int32)).contiguous()
+            a = torch.from_numpy(adj.astype(np.int32)).contiguous()
+            ff, fa = _frag_index(fwd), _frag_index(adj)
+            C.hea_check_ops(f, ff, self.n_slots, self.n_theta, False, p.t)
+            C.hea_check_ops(a, fa, self.n_slots, self.n_theta, True, p.t)
+            self.passes.append((p, (f.to(self.device), ff.to(self.device)), (a.to(self.device), fa.to(self.device))))
+        slot_tab = np.zeros((max(self.n_slots, 1), 9), dtype=np.int32)
+        owner = np.zeros(self.n_theta, dtype=np.int32)
+        for p in self.plan.passes:
+            nt = 1 << (self.n - p.t)
+            for g in p.groups:
+                slot_tab[g.slot, 0] = len(g.qubits)
+                for j, q in enumerate(g.qubits):
+                    slot_tab[g.slot, 1 + j] = self.plan.theta_slot(g.layer, q)
+                    slot_tab[g.slot, 5 + j] = self.plan.theta_slot(g.layer, q) + 1
+            for g in p.groups + p.l1:
+                for q in g.qubits:
+                    owner[self.plan.theta_slot(g.layer, q)] = nt
+                    owner[self.plan.theta_slot(g.layer, q) + 1] = nt
+        if (owner == 0).any():
+            raise RuntimeError("a parameter has no owning pass")
+        self.slot_tab = torch.from_numpy(slot_tab).to(self.device)
+        self.owner_tiles = torch.from_numpy(owner).to(self.device)
+        self.slab_tiles = max(1 << (self.n - p.t) for p in self.plan.passes)
+        self.scale = float(1 << (self.n // 2))
+        self.feature = _FEATURE[spec.feature_map.lower()]
+        self._ws = {}
+
+    # ------------------------------------------------------------------ workspaces
+    @contextlib.contextmanager
+    def private_workspace(self, ws: dict):
+        """Route workspace allocations to ``ws`` (owned by a captured hipGraph)."""
+        saved = self._ws
+        self._ws = ws
+        try:
+            yield ws
+        finally:
+            self._ws = saved
+
+    def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:
+        t = self._ws.get(name)
+        if t is None or t.numel() < numel or t.dtype != dtype:
+            t = torch.empty(numel, dtype=dtype, device=self.device)
+            self._ws[name] = t
+        return t[:numel]
+
+    @property
+    def n_passes(self) -> int:
+        return len(self.passes)
+
+    @property
+    def tiles_last(self) -> int:
+        return 1 << (self.n - self.passes[-1][0].t)
+
+    def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K):
+        return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
+                int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
+                self.slab_tiles, K] + [int(h) for h in p.H]
+
+    def _frags(self, params: torch.Tensor, K: int) -> torch.Tensor:
+        fr = self._buf("frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
+        if self.n_slots:
+            ext().hea_frags(params, params.shape[1], self.slot_tab, self.n_slots, K, fr)
+        return fr
+
+    def _forward(self, x, params, fr, K, B, part, store_last: bool = False):
+        """Forward passes; returns the stored pass outputs (all of them with ``store_last``: the adjoint
+        starts each pass from its output)."""
+        C = ext()
+        S = K * B
+        N = S << self.n
+        stored = []
+        empty = torch.empty(0, dtype=torch.int32, device=self.device)
+        fempty = torch.empty(0, dtype=torch.float32, device=self.device)
+        J = self.n_passes
+        for j, (p, fwd, _) in enumerate(self.passes):
+            keep = j < J - 1 or store_last
+            out = self._buf(f"psi{j}", N, torch.int32) if keep else empty
+            psi_in = stored[-1] if j > 0 else empty
+            geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K)
+            C.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
+                       part if j == J - 1 else fempty, fempty, _NODBG)
+            if keep:
+                stored.append(out)
+        return stored
+
+    def _adjoint(self, x, params, fr, K, B, stored, wread, gslab):
+        C = ext()
+        S = K * B
+        N = S << self.n
+        empty = torch.empty(0, dtype=torch.int32, device=self.device)
+        fempty = torch.empty(0, dtype=torch.float32, device=self.device)
+        J = self.n_passes
+        lam_in = empty
+        for j in range(J - 1, -1, -1):
+            p, _, adj = self.passes[j]
+            lam_out = self._buf(f"lam{j % 2}", N, torch.int32) if j > 0 else empty
+            geom = self._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, x.shape[1], K)
+            C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
+                       params, fr, wread, fempty, gslab, _NODBG)
+            lam_in = lam_out
+
+    def _prep(self, xang, params):
+        K, B, F = xang.shape
+        if F < self.n:
+            raise ValueError(f"expected >= {self.n} feature angles per sample, got {F}")
+        x = xang.reshape(K * B, F).float().contiguous()
+        p = params.float().contiguous()
+        if p.shape[0] != K:
+            raise ValueError("one parameter row per client expected")
+        return x, p, K, B
+
+    # ------------------------------------------------------------------ forward / eval
+    @torch.no_grad()
+    def expz(self, xang: torch.Tensor, theta: torch.Tensor, noise=None, keys=None, step: int = 0,
+             init: torch.Tensor | None = None) -> torch.Tensor:
+        if init is not None:
+            raise ValueError("the MFMA engine starts from the angle feature map (no initial states)")
+        x, th, K, B = self._prep(xang, theta)
+        if th.shape[1] < self.n_theta + 2 * self.C:    # pad theta-only rows to the kernel's param stride
+            th = torch.cat([th, th.new_zeros(K, self.n_theta + 2 * self.C - th.shape[1])], 1)
+        S = K * B
+        fr = self._frags(th, K)
+        part = self._buf("part", S * self.tiles_last * self.C, torch.float32)
+        self._forward(x, th, fr, K, B, part)
+        out = self._buf("expz", S * self.C, torch.float32)
+        ext().readout_sum(part, self.tiles_last, self.C, S, out)
+        if noise is not None:
+            from .statevec_hip import _keys
+            ext().readout_noise(out, self.C, B, S, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
+        return out.reshape(K, B, self.C).clone()
+
+    @torch.no_grad()
+    def vjp(self, xang: torch.Tensor, theta: torch.Tensor, w: torch.Tensor, init: torch.Tensor | None = None):
+        """Adjoint VJP of sum_c w[s, c] <Z_c>_s -> (<Z> [S, C], d/dtheta [K, n_theta])."""
+        if init is not None:
+            raise ValueError("the MFMA engine starts from the angle feature map (no initial states)")
+        x, th, K, B = self._prep(xang, theta)
+        if th.shape[1] < self.n_theta + 2 * self.C:
+            th = torch.cat([th, th.new_zeros(K, self.n_theta + 2 * self.C - th.shape[1])], 1)
+        S = K * B
+        fr = self._frags(th, K)
+        part = self._buf("part", S * self.tiles_last * self.C, torch.float32)
+        stored = self._forward(x, th, fr, K, B, part, store_last=True)
+        z = self._buf("expz", S * self.C, torch.float32)
+        ext().readout_sum(part, self.tiles_last, self.C, S, z)
+        wr = w.reshape(S, self.C).float().contiguous()
+        gslab = self._buf("gslab", S * self.slab_tiles * self.n_theta, torch.float32)
+        self._adjoint(x, th, fr, K, B, stored, wr, gslab)
+        grad = torch.zeros(K, th.shape[1], dtype=torch.float32, device=self.device)
+        ext().hea_grad_reduce(gslab, self.slab_tiles, self.owner_tiles, self.n_theta, B, K, grad, th.shape[1])
+        return z.view(S, self.C).clone(), grad[:, : self.n_theta]
+
+    # ------------------------------------------------------------------ train step
+    def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
+                       out_correct=None, init: torch.Tensor | None = None) -> dict:
+        """One adjoint training step (same contract as ``HipProgram.loss_and_grads``)."""
+        if init is not None:
+            raise ValueError("the MFMA engine starts from the angle feature map (no initial states)")
+        x, p, K, B = self._prep(xang, params)
+        S = K * B
+        C = ext()
+        yy = y.reshape(S).long().contiguous()
+        ww = wmask.reshape(S).float().contiguous()
+        fr = self._frags(p, K)
+        part = self._buf("part", S * self.tiles_last * self.C, torch.float32)
+        expz = self._buf("expz", S * self.C, torch.float32)
+        wread = self._buf("wread", S * self.C, torch.float32)
+        gslab = self._buf("gslab", S * self.slab_tiles * self.n_theta, torch.float32)
+        loss = torch.empty(K, dtype=torch.float32, device=self.device) if out_loss is None else out_loss
+        correct = torch.empty(K, dtype=torch.float32, device=self.device) if out_correct is None else out_correct
+        grad = torch.empty_like(p)
+        stored = self._forward(x, p, fr, K, B, part, store_last=True)
+        if noise is None:
+            C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss, correct,
+                         grad, True, 0.0, 0.0, 0, _NO_KEYS, 0)
+        else:
+            from .statevec_hip import _keys
+            C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss, correct,
+                         grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
+        self._adjoint(x, p, fr, K, B, stored, wread, gslab)
+        C.hea_grad_reduce(gslab, self.slab_tiles, self.owner_tiles, self.n_theta, B, K, grad, p.shape[1])
+        return {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}

@@ -1,0 +1,685 @@
+"""Pass planner for the MFMA statevector engine of the hardware-efficient VQC (``models/vqc.py``).
+
+The flagship circuit (ROADMAP.md:20-23, 125-128) is
+
+    RY(x_q) feature map -> L x [ RX(theta_lq) RZ(phi_lq) on every qubit ; CNOT chain q -> q+1 ] -> <Z_c>
+
+and this module turns it into a short sequence of LDS-tile passes whose work is dense 16 x 16 complex
+GEMMs (MFMA, ``csrc/hea_mfma.hip``) instead of per-gate VALU sweeps:
+
+* **Frames instead of permutations.**  A CNOT chain maps basis index y -> P y with P the prefix-XOR
+  matrix over GF(2).  Nothing is moved: after k chains memory index y holds logical index z = P^k y,
+  so a rotation on logical qubit q pairs memory indices y and y ^ P^-k e_q (a 1..k+1-bit mask) and its
+  logical bit is parity(y & row_q(P^k)).  The readout <Z_c> after the last chain is the diagonal sign
+  (-1)^parity(y & row_c(P^L)).
+* **Layer 1 is closed form.**  RZ RX RY(x)|0> on every qubit is a product state, generated directly
+  into the tile (no gate pass); its gradients come from 2 x 2 cross matrices.
+* **4-qubit groups.**  Rotations of one layer commute, so the qubits of a layer are grouped by four;
+  each group is one 16 x 16 complex unitary (tensor product of RZ.RX) acting on a 4-dim GF(2)
+  subspace of the tile: Y[m', col] = sum_m U[m', m] X[m, col] - an MFMA GEMM over columns = cosets.
+* **Staircase passes.**  A pass loads 2^t amplitudes (t = 14: fp16 (re, im) = 64 KB LDS, two states
+  for the adjoint = 128 KB) spanning memory bits [0, c) u [lo, hi) and applies every group whose
+  memory support lies in the tile and whose earlier-layer dependencies are done.  16 qubits x 3 layers
+  needs 2 passes.
+* **Adjoint.**  The forward stores every pass output (fp16); the reverse of pass j loads pass j's output
+  and lambda and walks back: gradient cross matrix N = sum_col psi lambda^H per group (MFMA), then U^H
+  on lambda and psi (no forward recompute).
+  A layer-1 qubit's 2 x 2 cross matrix is measured in the first pass whose tile holds its bit (every
+  earlier pass avoids that bit, and unitaries on other bits preserve the partial inner product).
+
+Everything here is host-side planning (runs once per circuit shape).  ``emulate`` executes a plan
+tile by tile with exactly the kernel's addressing tables in float64 numpy: it is the oracle the CPU
+tests hold against a dense simulation, and the HIP kernel is tested against both.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+GROUP = 4                  # qubits per fused group (16-dim complex unitary -> K = 32 real MFMA)
+TILE_BITS = 14             # 2^14 fp16 complex amplitudes = 64 KB of LDS per state
+MIN_CONTIG = 5             # contiguous low bits in a strided tile (32 amplitudes = 128 B)
+
+# op codes (kept in sync with csrc/hea_mfma.hip)
+OP_APPLY, OP_UNAPPLY_PSI, OP_UNAPPLY_LAM, OP_GRAD, OP_GRAD_L1, OP_OBS, OP_READOUT, OP_BACK = 1, 2, 3, 4, 5, 6, 7, 8
+OP_WORDS = 128
+W_CODE, W_SLOT, W_NREAL, W_FLAGS, W_RFULL, W_RT, W_TH, W_PH, W_OFF, W_BL, W_BH = 0, 1, 2, 3, 4, 8, 12, 16, 20, 36, 68
+F_BACK_PSI = 1             # OP_BACK also un-applies the group on psi (still needed further back)
+MAX_CLASSES = 8
+BANK_BITS = 5              # ds_read_b32 / ds_write_b32: bank = dword address % 32 per 32-lane half
+
+
+def parity(x: int) -> int:
+    return bin(x).count("1") & 1
+
+
+def frame_vec(q: int, k: int, n: int) -> int:
+    """Memory mask P^-k e_q that a rotation on logical qubit q pairs after k CNOT chains."""
+    v = 1 << q
+    full = (1 << n) - 1
+    for _ in range(k):
+        v = (v ^ (v << 1)) & full
+    return v
+
+
+def frame_rows(k: int, n: int) -> list:
+    """Row masks of P^k: logical bit q of memory index y is parity(y & R[q])."""
+    R = [1 << q for q in range(n)]
+    for _ in range(k):
+        acc, new = 0, []
+        for q in range(n):
+            acc ^= R[q]
+            new.append(acc)
+        R = new
+    return R
+
+
+@dataclass
+class Group:
+    layer: int                 # 1 = closed-form layer (gradient only), >= 2 rotation layer
+    qubits: list               # logical qubits (<= 4)
+    frame: int                 # CNOT chains before this layer
+    slot: int = -1             # unitary fragment slot (rotation groups)
+
+    def vecs(self, n):
+        return [frame_vec(q, self.frame, n) for q in self.qubits]
+
+    def support(self, n):
+        s = 0
+        for v in self.vecs(n):
+            s |= v
+        return s
+
+
+@dataclass
+class Pass:
+    c: int
+    lo: int
+    hi: int
+    groups: list = field(default_factory=list)      # rotation groups, forward order
+    l1: list = field(default_factory=list)          # layer-1 gradient groups (measured at the pass input)
+    H: list = field(default_factory=lambda: [0] * BANK_BITS)   # LDS swizzle rows (see sigma)
+    cols: dict = field(default_factory=dict)        # per group: the 4 non-pivot bits that feed MFMA columns
+
+    @property
+    def bits(self) -> list:
+        return list(range(self.c)) + list(range(self.lo, self.hi))
+
+    @property
+    def t(self) -> int:
+        return self.c + self.hi - self.lo
+
+    def mask(self) -> int:
+        m = 0
+        for b in self.bits:
+            m |= 1 << b
+        return m
+
+    def to_tile(self, mem_mask: int) -> int:
+        out = 0
+        for i, b in enumerate(self.bits):
+            if (mem_mask >> b) & 1:
+                out |= 1 << i
+        return out
+
+    def fixed(self, tile_id: int, n: int) -> int:
+        """Memory bits that are constant over tile ``tile_id`` (bits outside the tile)."""
+        w1 = self.lo - self.c
+        f1 = tile_id & ((1 << w1) - 1)
+        f2 = tile_id >> w1
+        return (f1 << self.c) | (f2 << self.hi)
+
+    def mem_index(self, tau: np.ndarray, tile_id: int, n: int) -> np.ndarray:
+        lo_part = tau & ((1 << self.c) - 1)
+        hi_part = tau >> self.c
+        return lo_part | (hi_part << self.lo) | self.fixed(tile_id, n)
+
+
+@dataclass
+class HEAPlan:
+    n: int
+    L: int
+    C: int
+    readout: list
+    chain: bool
+    feature: str
+    t: int
+    passes: list
+    n_slots: int                 # rotation groups (unitary fragments per client)
+
+    @property
+    def n_theta(self) -> int:
+        return 2 * self.n * self.L
+
+    def layer_frame(self, layer: int) -> int:
+        return (layer - 1) if self.chain else 0
+
+    @property
+    def obs_masks(self) -> list:
+        R = frame_rows(self.L if self.chain else 0, self.n)
+        return [R[q] for q in self.readout]
+
+    def theta_slot(self, layer: int, q: int) -> int:
+        return 2 * ((layer - 1) * self.n + q)
+
+
+def eligible(spec) -> bool:
+    """Circuits this engine covers: angle feature map, RX/RZ layers, chain (or no) entangler, no noise."""
+    return (not spec.amplitude and not spec.noisy and spec.entangler in ("chain", "none")
+            and spec.feature_map.lower() in ("rx", "ry", "rz") and spec.n_qubits >= 8
+            and spec.n_qubits <= 30 and spec.n_classes <= MAX_CLASSES)
+
+
+def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
+               tile_bits: int = TILE_BITS, swizzle: bool = True) -> HEAPlan:
+    t = min(tile_bits, n)
+    if t < GROUP + 4:
+        raise ValueError("the MFMA engine needs at least 8 tile qubits (16 columns per MFMA block)")
+    frame = (lambda layer: layer - 1) if chain else (lambda layer: 0)
+    sup = {}
+    for layer in range(2, L + 1):
+        for q in range(n):
+            sup[(layer, q)] = frame_vec(q, frame(layer), n)
+    preds = {}
+    for (layer, q), s in sup.items():
+        preds[(layer, q)] = [(layer - 1, p) for p in range(n) if layer > 2 and (sup[(layer - 1, p)] & s)]
+    remaining = sorted(sup, key=lambda o: (o[0], o[1]))
+    done = set()
+    passes = []
+    while True:
+        if not passes:
+            p = Pass(t, t, t) if n > t else Pass(n, n, n)
+        else:
+            mc = min(MIN_CONTIG, max(2, t - 6))
+            low = lambda o: min(b for b in range(n) if (sup[o] >> b) & 1)
+            lo_all = min(low(o) for o in remaining)      # one pass for everything left, if it fits
+            ready = [o for o in remaining if all(d in done for d in preds[o])]
+            lo_min = lo_all if t - (n - lo_all) >= mc else min(low(o) for o in ready)
+            w = n - lo_min
+            if t - w >= mc:
+                p = Pass(t - w, lo_min, n)
+            else:
+                base = max(lo_min, mc)
+                p = Pass(mc, base, min(n, base + t - mc))
+        tm = p.mask()
+        taken = []
+        for o in remaining:
+            if (sup[o] & ~tm) == 0 and all(d in done or d in taken for d in preds[o]):
+                taken.append(o)
+        if not taken and remaining:
+            raise RuntimeError(f"pass planner stuck at {len(passes)} passes (n={n}, L={L}, t={t})")
+        for o in taken:
+            done.add(o)
+        remaining = [o for o in remaining if o not in done]
+        by_layer = {}
+        for (layer, q) in taken:
+            by_layer.setdefault(layer, []).append(q)
+        for layer in sorted(by_layer):
+            qs = sorted(by_layer[layer])
+            for i in range(0, len(qs), GROUP):
+                p.groups.append(Group(layer, qs[i:i + GROUP], frame(layer)))
+        passes.append(p)
+        if not remaining:
+            break
+        if len(passes) > 16:
+            raise RuntimeError("pass planner did not converge")
+    # every qubit's bit must sit in some tile (layer-1 gradients): add group-free passes for the rest
+    covered = 0
+    for p in passes:
+        covered |= p.mask()
+    while covered != (1 << n) - 1:
+        top = (1 << n) - 1 & ~covered
+        lo = max(top.bit_length() - (t - MIN_CONTIG), min(b for b in range(n) if (top >> b) & 1))
+        lo = max(lo, MIN_CONTIG)
+        p = Pass(t - (min(n, lo + t - MIN_CONTIG) - lo), lo, min(n, lo + t - MIN_CONTIG))
+        passes.append(p)
+        covered |= p.mask()
+    # layer-1 gradient groups: first pass whose tile holds the qubit's bit
+    owner = {}
+    for q in range(n):
+        for j, p in enumerate(passes):
+            if (p.mask() >> q) & 1:
+                owner[q] = j
+                break
+    for j, p in enumerate(passes):
+        qs = [q for q in range(n) if owner[q] == j]
+        for i in range(0, len(qs), GROUP):
+            p.l1.append(Group(1, qs[i:i + GROUP], 0))
+    slot = 0
+    for p in passes:
+        for g in p.groups:
+            g.slot = slot
+            slot += 1
+    plan = HEAPlan(n, L, len(readout), list(readout), chain, feature, t, passes, slot)
+    if swizzle:
+        for j, p in enumerate(passes):
+            layout_pass(plan, p, seed=j)
+    return plan
+
+
+# ---------------------------------------------------------------------------------------- op tables
+def _neutral_pads(vt: list, rt: list, t: int, need: int) -> list:
+    """``need`` tile vectors independent of ``vt`` whose logical parity against every ``rt`` mask is 0."""
+    def sig(v):
+        return tuple(parity(v & r) for r in rt)
+    basis = []          # GF(2) elimination of vt + chosen pads
+
+    def independent(v):
+        x = v
+        for b in basis:
+            x = min(x, x ^ b)
+        return x != 0
+
+    def add(v):
+        x = v
+        for b in basis:
+            x = min(x, x ^ b)
+        basis.append(x)
+        basis.sort(reverse=True)
+
+    for v in vt:
+        add(v)
+    pads = []
+    cands = [1 << i for i in range(t)]
+    by_sig = {}
+    for e in cands:
+        by_sig.setdefault(sig(e), []).append(e)
+    pool = list(by_sig.get(tuple(0 for _ in rt), []))
+    for s, es in by_sig.items():
+        if any(s):
+            pool += [es[0] ^ e for e in es[1:]]
+    for v in pool:
+        if len(pads) == need:
+            break
+        if independent(v):
+            add(v)
+            pads.append(v)
+    if len(pads) < need:
+        raise RuntimeError("could not pad a group to 4 qubits inside the tile")
+    return pads
+
+
+def _pivots(vecs: list) -> list:
+    """Distinct pivot bit per vector after GF(2) elimination (rows stay the original span)."""
+    rows = []
+    piv = []
+    for v in vecs:
+        x = v
+        for pb, r in zip(piv, rows):
+            if (x >> pb) & 1:
+                x ^= r
+        if x == 0:
+            raise RuntimeError("dependent group vectors")
+        pb = x.bit_length() - 1
+        # keep earlier rows reduced w.r.t. the new pivot
+        for i in range(len(rows)):
+            if (rows[i] >> pb) & 1:
+                rows[i] ^= x
+        rows.append(x)
+        piv.append(pb)
+    return piv
+
+
+# ---------------------------------------------------------------------------------------- LDS layout
+# The tile lives in LDS at dword sigma(tau) = tau ^ h(tau >> 5), h linear (rows H), an involution that
+# only rewrites the 5 bank bits.  It is linear over GF(2), so every XOR-composed table entry is stored
+# already swizzled.  Per pass H and per group the 4 non-pivot bits that become the 16 MFMA columns of
+# a block are searched so that the 32 lanes of each half-wave hit 32 distinct banks in all three
+# access patterns of a group op: apply reads (columns x m-bit 2), apply writes (columns x m-bit 1) and
+# cross-matrix reads (m bits 0..3 x column bit 2).
+def _hmul(H, x: int) -> int:
+    r = 0
+    for b, row in enumerate(H):
+        r |= parity(row & x) << b
+    return r
+
+
+def sigma(H, tau: int) -> int:
+    return tau ^ _hmul(H, tau >> BANK_BITS)
+
+
+def _bank(H, v: int) -> int:
+    return (v & ((1 << BANK_BITS) - 1)) ^ _hmul(H, v >> BANK_BITS)
+
+
+def _rank(vals) -> int:
+    basis = []
+    for v in vals:
+        x = v
+        for b in basis:
+            x = min(x, x ^ b)
+        if x:
+            basis.append(x)
+            basis.sort(reverse=True)
+    return len(basis)
+
+
+def _group_geom(plan: HEAPlan, p: Pass, g: Group):
+    """Tile-local group vectors (padded to 4), row masks, non-pivot bits and their column directions."""
+    n, t = plan.n, p.t
+    R = frame_rows(g.frame, n)
+    vt = [p.to_tile(v) for v in g.vecs(n)]
+    for v, vm in zip(vt, g.vecs(n)):
+        if p.to_tile(vm) != v or (vm & ~p.mask()):
+            raise RuntimeError("group support leaves the tile")
+    rfull = [R[q] for q in g.qubits]
+    rt = [p.to_tile(r) for r in rfull]
+    allv = vt + _neutral_pads(vt, rt, t, GROUP - len(g.qubits))
+    off = [0] * 16
+    for m in range(16):
+        for j in range(GROUP):
+            if (m >> j) & 1:
+                off[m] ^= allv[j]
+    piv = set(_pivots(allv))
+    nonpiv = [b for b in range(t) if b not in piv]
+
+    def bits(y):
+        b = 0
+        for j in range(len(g.qubits)):
+            b |= parity(y & rt[j]) << j
+        return b
+
+    dirs = {b: (1 << b) ^ off[bits(1 << b)] for b in nonpiv}
+    return allv, rfull, rt, off, nonpiv, bits, dirs
+
+
+def _best_cols(H, allv, dirs):
+    """(score, (c0, c1, c2, c3)): column bits maximising conflict-free access patterns (3 = all)."""
+    bv = [_bank(H, v) for v in allv]
+    bd = {b: _bank(H, d) for b, d in dirs.items()}
+    best = (-1, None)
+    import itertools
+    for combo in itertools.combinations(sorted(dirs), 4):
+        cb = [bd[b] for b in combo]
+        sa = int(_rank(cb + [bv[2]]) == 5)
+        sw = int(_rank(cb + [bv[1]]) == 5)
+        for c2 in combo:
+            sg = int(_rank(bv + [bd[c2]]) == 5)
+            sc = sa + sw + sg
+            if sc > best[0]:
+                rest = [b for b in combo if b != c2]
+                best = (sc, (rest[0], rest[1], c2, rest[2]))
+                if sc == 3:
+                    return best
+    return best
+
+
+def layout_pass(plan: HEAPlan, p: Pass, seed: int = 0, tries: int = 48) -> None:
+    """Pick the pass' LDS swizzle rows H and every group's column bits (bank-conflict search)."""
+    groups = p.groups + p.l1
+    geoms = [_group_geom(plan, p, g) for g in groups]
+    hb = max(p.t - BANK_BITS, 0)
+    rng = np.random.default_rng(1234 + seed)
+    best = None
+    for i in range(tries):
+        H = [0] * BANK_BITS if i == 0 else [int(x) for x in rng.integers(0, 1 << hb, BANK_BITS)] if hb else [0] * 5
+        cols, score = [], 0
+        for allv, _, _, _, _, _, dirs in geoms:
+            sc, c = _best_cols(H, allv, dirs)
+            cols.append(c)
+            score += sc
+        if best is None or score > best[0]:
+            best = (score, H, cols)
+        if score == 3 * len(groups):
+            break
+    p.H = best[1]
+    p.cols = {(g.layer, tuple(g.qubits)): c for g, c in zip(groups, best[2])}
+
+
+def group_table(plan: HEAPlan, p: Pass, g: Group, code: int, flags: int = 0) -> np.ndarray:
+    """One op record: frame row masks, XOR offsets OFF[m], column bases and parameter slots.
+
+    Column c's coset representative with logical group bits 0 is y'(c) ^ OFF[bits(y'(c)) ^ fp], y' the
+    deposit of c into the non-pivot tile bits, bits() its logical group bits from the tile-local row
+    masks and fp those of the tile's fixed memory bits.  Everything but OFF[fp] is tile independent,
+    and deposit and parity are linear, so the table stores per 5-bit half of c the pre-XORed base
+    BL[c & 31] / BH[c >> 5] = d ^ OFF[bits(d)]:  addr(c, m) = BL ^ BH ^ OFF[fp] ^ OFF[m]  (all swizzled).
+    The first four deposit bits are the pass layout's column bits for this group (bank-conflict free)."""
+    n, t = plan.n, p.t
+    w = np.zeros(OP_WORDS, dtype=np.int64)
+    w[W_CODE] = code
+    w[W_SLOT] = g.slot
+    w[W_FLAGS] = flags
+    nreal = len(g.qubits)
+    w[W_NREAL] = nreal
+    allv, rfull, rt, off, nonpiv, bits, _ = _group_geom(plan, p, g)
+    first = list(p.cols.get((g.layer, tuple(g.qubits))) or nonpiv[:4])
+    order = first + [b for b in nonpiv if b not in first]
+    assert len(order) == t - GROUP
+    for j in range(GROUP):
+        w[W_RFULL + j] = rfull[j] if j < nreal else 0
+        w[W_RT + j] = rt[j] if j < nreal else 0
+        w[W_TH + j] = plan.theta_slot(g.layer, g.qubits[j]) if j < nreal else -1
+        w[W_PH + j] = plan.theta_slot(g.layer, g.qubits[j]) + 1 if j < nreal else -1
+    for m in range(16):
+        w[W_OFF + m] = sigma(p.H, off[m])
+    for i in range(32):
+        lo = hi = 0
+        for j in range(5):
+            if (i >> j) & 1:
+                if j < len(order):
+                    lo |= 1 << order[j]
+                if 5 + j < len(order):
+                    hi |= 1 << order[5 + j]
+        w[W_BL + i] = sigma(p.H, lo ^ off[bits(lo)])
+        w[W_BH + i] = sigma(p.H, hi ^ off[bits(hi)])
+    return w
+
+
+def obs_table(plan: HEAPlan, p: Pass, code: int) -> np.ndarray:
+    w = np.zeros(OP_WORDS, dtype=np.int64)
+    w[W_CODE] = code
+    w[W_NREAL] = plan.C
+    for c, m in enumerate(plan.obs_masks):
+        w[W_RFULL + 2 * c] = m                  # 8 words: full masks (two words per class slot)
+        ot = p.to_tile(m)                       # parity(sigma(w) & ot) = parity(w & ot')
+        ht = 0
+        for b in range(BANK_BITS):
+            if (ot >> b) & 1:
+                ht ^= p.H[b]
+        w[W_OFF + c] = ot ^ (ht << BANK_BITS)
+    return w
+
+
+def pass_programs(plan: HEAPlan):
+    """Forward and adjoint op lists per pass: list of (Pass, fwd_ops [k, OP_WORDS], adj_ops)."""
+    out = []
+    J = len(plan.passes)
+    for j, p in enumerate(plan.passes):
+        fwd = [group_table(plan, p, g, OP_APPLY) for g in p.groups]
+        if j == J - 1:
+            fwd.append(obs_table(plan, p, OP_READOUT))
+        # the adjoint of pass j starts from pass j's stored OUTPUT (no recompute) and walks back
+        adj = [obs_table(plan, p, OP_OBS)] if j == J - 1 else []
+        rev = list(reversed(p.groups))
+        for i, g in enumerate(rev):
+            # gradient cross matrix + U^H on lambda (and on psi while it is still needed further back)
+            psi_needed = i < len(rev) - 1 or bool(p.l1)
+            adj.append(group_table(plan, p, g, OP_BACK, F_BACK_PSI if psi_needed else 0))
+        for g in p.l1:
+            adj.append(group_table(plan, p, g, OP_GRAD_L1))
+        out.append((p, np.stack(fwd) if fwd else np.zeros((0, OP_WORDS), np.int64),
+                    np.stack(adj) if adj else np.zeros((0, OP_WORDS), np.int64)))
+    return out
+
+
+# ---------------------------------------------------------------------------------------- numerics
+def rot_u(theta, phi):
+    """RZ(phi) RX(theta) as [..., 2, 2] complex."""
+    c, s = np.cos(theta / 2), np.sin(theta / 2)
+    em, ep = np.exp(-0.5j * phi), np.exp(0.5j * phi)
+    u = np.empty(np.shape(theta) + (2, 2), dtype=np.complex128)
+    u[..., 0, 0] = em * c
+    u[..., 0, 1] = -1j * em * s
+    u[..., 1, 0] = -1j * ep * s
+    u[..., 1, 1] = ep * c
+    return u
+
+
+def feature_vec(x, basis: str):
+    """F(x)|0> for the feature rotation."""
+    a = np.asarray(x, dtype=np.float64) / 2
+    v = np.zeros(np.shape(a) + (2,), dtype=np.complex128)
+    b = basis.lower()
+    if b == "rx":
+        v[..., 0], v[..., 1] = np.cos(a), -1j * np.sin(a)
+    elif b == "rz":
+        v[..., 0] = np.exp(-1j * a)
+    else:
+        v[..., 0], v[..., 1] = np.cos(a), np.sin(a)
+    return v
+
+
+def group_unitary(theta: np.ndarray, nreal: int, th_slots, ph_slots) -> np.ndarray:
+    """16 x 16 unitary U[m', m] = prod_j u_j[m'_j, m_j] (pads: identity) for one client's params."""
+    U = np.ones((16, 16), dtype=np.complex128)
+    mp = np.arange(16)[:, None]
+    mm = np.arange(16)[None, :]
+    for j in range(GROUP):
+        bj_p, bj = (mp >> j) & 1, (mm >> j) & 1
+        if j < nreal:
+            u = rot_u(theta[th_slots[j]], theta[ph_slots[j]])
+            U = U * u[bj_p, bj]
+        else:
+            U = U * (bj_p == bj)
+    return U
+
+
+def _addr(w, t, fixed):
+    """[ncol, 16] tile addresses of (column, group coordinate m), computed as the kernel does."""
+    col = np.arange(1 << (t - GROUP))
+    fp = 0
+    for j in range(int(w[W_NREAL])):
+        fp |= parity(fixed & int(w[W_RFULL + j])) << j
+    off = w[W_OFF:W_OFF + 16]
+    base = w[W_BL + (col & 31)] ^ w[W_BH + (col >> 5)] ^ off[fp]
+    return base[:, None] ^ off[None, :]
+
+
+def _grad(w, ps, lm, th, gk, gfac):
+    """Cross matrix N[b][a] = sum_col psi[b] conj(lam[a]); per qubit 2 x 2 partial trace -> d/dtheta, d/dphi."""
+    N = ps.T @ lm.conj()
+    for jq in range(int(w[W_NREAL])):
+        nn = np.zeros((2, 2), dtype=np.complex128)
+        for bb in range(16):
+            for aa in range(16):
+                if ((bb ^ aa) & ~(1 << jq)) == 0:
+                    nn[(bb >> jq) & 1, (aa >> jq) & 1] += N[bb, aa]
+        sth, sph = int(w[W_TH + jq]), int(w[W_PH + jq])
+        ph = th[sph]
+        gk[sth] += (np.exp(-1j * ph) * nn[1, 0] + np.exp(1j * ph) * nn[0, 1]).imag * gfac
+        gk[sph] += (nn[0, 0] - nn[1, 1]).imag * gfac
+
+
+def _signs(w, t, fixed, C):
+    tau = np.arange(1 << t)
+    out = []
+    for c in range(C):
+        m_t, m_f = int(w[W_OFF + c]), int(w[W_RFULL + 2 * c])
+        par = np.array([parity(int(x) & m_t) for x in tau]) ^ parity(fixed & m_f)
+        out.append(1.0 - 2.0 * par)
+    return np.stack(out)     # [C, 2^t]
+
+
+def _round16(z):
+    return (z.real.astype(np.float16).astype(np.float64) + 1j * z.imag.astype(np.float16).astype(np.float64))
+
+
+def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp16: bool = False):
+    """Tile-exact execution of ``plan`` with the kernel's tables.
+
+    xang [K, B, n] encoded feature angles, params [K, P] (theta first), wread [K, B, C] = dL/d<Z_c>.
+    Returns expz [K, B, C] and (if wread is given) theta gradients [K, n_theta] summed over samples.
+    ``fp16`` rounds the stored amplitudes to half precision after every op (kernel storage format).
+    """
+    n, t = plan.n, plan.t
+    K, B, _ = xang.shape
+    progs = pass_programs(plan)
+    rnd = _round16 if fp16 else (lambda z: z)
+    scale = float(1 << (n // 2))
+    expz = np.zeros((K, B, plan.C))
+    grads = np.zeros((K, plan.n_theta))
+    for k in range(K):
+        th = params[k].astype(np.float64)
+        Us = {}
+        for p in plan.passes:
+            for g in p.groups:
+                w = group_table(plan, p, g, OP_APPLY)
+                Us[g.slot] = group_unitary(th, len(g.qubits), w[W_TH:W_TH + 4], w[W_PH:W_PH + 4])
+        for b in range(B):
+            wv = [rot_u(th[plan.theta_slot(1, q)], th[plan.theta_slot(1, q) + 1]) @ feature_vec(xang[k, b, q], plan.feature)
+                  for q in range(n)]
+            idx = np.arange(1 << n)
+            psi0 = np.full(1 << n, scale, dtype=np.complex128)
+            for q in range(n):
+                psi0 = psi0 * np.array(wv[q])[(idx >> q) & 1]
+            psi0 = rnd(psi0)
+            stored = [psi0]
+            # forward passes
+            psi = psi0.copy()
+            for j, (p, fwd, _) in enumerate(progs):
+                out = psi.copy()
+                sg_w = np.array([sigma(p.H, int(x)) for x in range(1 << p.t)])
+                for tid in range(1 << (n - p.t)):
+                    tau = np.arange(1 << p.t)
+                    mem = p.mem_index(tau, tid, n)
+                    fixed = p.fixed(tid, n)
+                    tile = np.empty(1 << p.t, dtype=np.complex128)
+                    tile[sg_w] = psi[mem]                     # LDS dword sigma(tau) holds amplitude tau
+                    for w in fwd:
+                        if w[W_CODE] == OP_APPLY:
+                            a = _addr(w, p.t, fixed)
+                            tile[a] = rnd((Us[int(w[W_SLOT])] @ tile[a].T).T)
+                        elif w[W_CODE] == OP_READOUT:
+                            sg = _signs(w, p.t, fixed, plan.C)
+                            expz[k, b] += sg @ (np.abs(tile) ** 2) / scale ** 2
+                    out[mem] = tile[sg_w]
+                psi = out
+                stored.append(psi.copy())
+            if wread is None:
+                continue
+            r = wread[k, b].astype(np.float64)
+            rho = np.max(np.abs(r)) if np.max(np.abs(r)) > 0 else 1.0
+            rr = r / rho
+            gfac = rho / scale ** 2
+            lam = None
+            for j in range(len(progs) - 1, -1, -1):
+                p, _, adj = progs[j]
+                psi_in = stored[j + 1]                    # output of forward pass j
+                lam_out = np.zeros(1 << n, dtype=np.complex128)
+                sg_w = np.array([sigma(p.H, int(x)) for x in range(1 << p.t)])
+                for tid in range(1 << (n - p.t)):
+                    tau = np.arange(1 << p.t)
+                    mem = p.mem_index(tau, tid, n)
+                    fixed = p.fixed(tid, n)
+                    ps = np.empty(1 << p.t, dtype=np.complex128)
+                    ps[sg_w] = psi_in[mem]
+                    lm = np.zeros_like(ps)
+                    if lam is not None:
+                        lm[sg_w] = lam[mem]
+                    for w in adj:
+                        code = int(w[W_CODE])
+                        if code == OP_OBS:
+                            sg = _signs(w, p.t, fixed, plan.C)
+                            lm = rnd((rr @ sg) * ps)
+                            continue
+                        a = _addr(w, p.t, fixed)
+                        if code == OP_BACK:
+                            _grad(w, ps[a], lm[a], th, grads[k], gfac)
+                            Uh = Us[int(w[W_SLOT])].conj().T
+                            lm[a] = rnd((Uh @ lm[a].T).T)
+                            if int(w[W_FLAGS]) & F_BACK_PSI:
+                                ps[a] = rnd((Uh @ ps[a].T).T)
+                        elif code == OP_APPLY:
+                            ps[a] = rnd((Us[int(w[W_SLOT])] @ ps[a].T).T)
+                        elif code == OP_UNAPPLY_PSI:
+                            ps[a] = rnd((Us[int(w[W_SLOT])].conj().T @ ps[a].T).T)
+                        elif code == OP_UNAPPLY_LAM:
+                            lm[a] = rnd((Us[int(w[W_SLOT])].conj().T @ lm[a].T).T)
+                        else:   # OP_GRAD / OP_GRAD_L1
+                            _grad(w, ps[a], lm[a], th, grads[k], gfac)
+                    lam_out[mem] = lm[sg_w]
+                lam = lam_out
+    return expz, grads

@@ -1,0 +1,81 @@
+"""CPU tests of the MFMA-engine pass planner: tile-exact emulation with the kernel's addressing tables
+vs a dense float64 simulation (expectations and adjoint gradients), plan structure, table invariants."""
+import numpy as np
+import pytest
+import torch
+
+from qfedx_amd.models.vqc import VQCSpec
+from qfedx_amd.ops import hea_plan as hp
+from qfedx_amd.ops.statevec_torch import TorchProgram, slot_grads
+
+
+def _dense(spec, xang, params, wread):
+    ops, coef = spec.program()
+    prog = TorchProgram(ops, coef, spec.n_qubits, dtype=torch.complex128)
+    K, B, n = xang.shape
+    P = spec.n_theta
+    rows = torch.cat([params[:, None, :P].expand(K, B, P), xang], -1).reshape(K * B, -1)
+    psi = prog.run(rows)
+    ez = prog.expz(psi, spec.readout).reshape(K, B, -1)
+    g = prog.adjoint_grads(rows, psi, wread.reshape(K * B, -1), spec.readout)
+    return ez.numpy(), slot_grads(g, prog.ops, prog.coef, rows.shape[1])[:, :P].reshape(K, B, P).sum(1).numpy()
+
+
+@pytest.mark.parametrize("n,L,t,chain,feat", [(8, 2, 8, True, "ry"), (10, 3, 8, True, "ry"), (10, 3, 14, True, "rx"),
+                                              (11, 2, 8, False, "ry"), (12, 4, 9, True, "ry"), (9, 1, 8, True, "rz")])
+def test_emulated_plan_matches_dense(n, L, t, chain, feat):
+    spec = VQCSpec(n, L, 3, feature_map=feat, entangler="chain" if chain else "none")
+    plan = hp.build_plan(n, L, spec.readout, chain, feat, tile_bits=t)
+    g = torch.Generator().manual_seed(n * 10 + L)
+    x = torch.rand(2, 2, n, generator=g, dtype=torch.float64) * 3
+    params = torch.randn(2, spec.n_params, generator=g, dtype=torch.float64)
+    wr = torch.randn(2, 2, 3, generator=g, dtype=torch.float64)
+    ez, gr = _dense(spec, x, params, wr)
+    ez2, gr2 = hp.emulate(plan, x.numpy(), params.numpy(), wr.numpy())
+    np.testing.assert_allclose(ez2, ez, atol=1e-12)
+    np.testing.assert_allclose(gr2, gr, atol=1e-12)
+    ez3, gr3 = hp.emulate(plan, x.numpy(), params.numpy(), wr.numpy(), fp16=True)   # kernel storage format
+    np.testing.assert_allclose(ez3, ez, atol=2e-3)
+    np.testing.assert_allclose(gr3, gr, atol=3e-3 * max(1.0, np.abs(gr).max()))
+
+
+@pytest.mark.parametrize("n,L,passes", [(16, 3, 2), (16, 2, 2), (20, 2, 2), (20, 3, 2), (24, 2, 3), (12, 3, 1)])
+def test_plan_shapes(n, L, passes):
+    plan = hp.build_plan(n, L, [0, 1, 2])
+    assert len(plan.passes) == passes
+    # every rotation (layer >= 2, qubit) lands in exactly one group, every qubit's layer-1 gradient once
+    seen = sorted((g.layer, q) for p in plan.passes for g in p.groups for q in g.qubits)
+    assert seen == sorted((layer, q) for layer in range(2, L + 1) for q in range(n))
+    l1 = sorted(q for p in plan.passes for g in p.l1 for q in g.qubits)
+    assert l1 == list(range(n))
+    for p in plan.passes:
+        assert p.t <= hp.TILE_BITS and p.c >= 2
+        for g in p.groups:
+            assert g.support(n) & ~p.mask() == 0
+
+
+def test_group_tables_cover_tile_once():
+    """(column, m) -> y'(col) ^ OFF[m ^ b] is a bijection onto the tile for every op and tile."""
+    plan = hp.build_plan(16, 3, [0, 1, 2])
+    for p in plan.passes:
+        for g in p.groups + p.l1:
+            w = hp.group_table(plan, p, g, hp.OP_APPLY)
+            for tid in (0, (1 << (16 - p.t)) - 1):
+                a = hp._addr(w, p.t, p.fixed(tid, 16))
+                assert np.array_equal(np.sort(a.ravel()), np.arange(1 << p.t))
+
+
+def test_frame_algebra():
+    n = 12
+    for k in range(4):
+        R = hp.frame_rows(k, n)
+        for q in range(n):
+            v = hp.frame_vec(q, k, n)
+            assert [hp.parity(v & R[j]) for j in range(n)] == [int(j == q) for j in range(n)]
+
+
+def test_eligibility():
+    assert hp.eligible(VQCSpec(16, 3, 3))
+    assert not hp.eligible(VQCSpec(16, 3, 3, entangler="ring"))
+    assert not hp.eligible(VQCSpec(4, 2, 3))
+    assert not hp.eligible(VQCSpec(8, 2, 3, feature_map="amplitude"))
