@@ -24,6 +24,6 @@ struct HeaPassArgs {
   float* part;               // [S][n_tiles][C] readout partials
   float* gslab;              // [S][slab_tiles][n_theta] gradient partials
   int slab_tiles;
-  int hrow[5];
-  long long* dbg;            // optional phase timestamps (s_memtime) of workgroups < 8, [8][64]               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
+  int hrow[5];               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
+  long long* dbg;            // optional phase timestamps (s_memtime) of workgroups < 8, [8][64]
 };

@@ -86,6 +86,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   need(ops.dim() == 2 && ops.size(1) == 128 && ops.scalar_type() == torch::kInt32 && ops.is_cuda(),
        "ops must be int32 [nops, 128] on the device");
   a.nops = (int)ops.size(0);
+  need(a.nops <= 128, "at most 128 ops per pass program");
   a.ops = dp<int>(ops, torch::kInt32, "ops", 0);
   a.fidx = a.nops ? dp<int>(fidx, torch::kInt32, "fidx", a.nops) : nullptr;
   const int64_t states = S << a.n;

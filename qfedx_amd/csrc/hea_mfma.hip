@@ -35,6 +35,7 @@ constexpr int TMAX = 14;
 constexpr int NT_FWD = 512;    // forward: 8 waves, 64 KB LDS -> 2 workgroups per CU
 constexpr int NT_ADJ = 1024;   // adjoint: 16 waves, 128 KB LDS (psi + lambda) -> 1 workgroup per CU
 constexpr int CMAX = 8;
+constexpr int MAXOPS = 128;    // ops per pass program (host-checked)
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
@@ -54,6 +55,12 @@ __device__ __forceinline__ float2 unpack_h2(uint32_t u) {
 }
 
 __device__ __forceinline__ int par(uint32_t x) { return __builtin_popcount(x) & 1; }
+
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup fence and so also drains every
+// outstanding GLOBAL load (vmcnt(0)) - including the next op's prefetched record and unitary fragments.
+// Cross-wave data here only moves through LDS, so completing this wave's LDS (and scalar) operations before
+// the s_barrier is sufficient; global results (gslab, stored tiles) are never read back inside the kernel.
+__device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -292,6 +299,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
   constexpr int NT = ADJ ? NT_ADJ : NT_FWD, NW = NT / 64;
   __shared__ uint32_t tile[(ADJ ? 2 : 1) << TMAX];     // psi | lambda (fp16 re, im), swizzled
   __shared__ int opw[OPW];
+  __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
   __shared__ float red[NW * CMAX];
   __shared__ unsigned long long red64[ADJ ? 512 : 1];   // gradient cross matrix, 2^-20 fixed point
   __shared__ float2 wv[32][2];
@@ -330,7 +338,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
       wv[tid][0] = w[0];
       wv[tid][1] = w[1];
     }
-    __syncthreads();
+    lds_barrier();
     HEA_MARK();
     const int ta = a.t >> 1, tb = a.t - ta;
     if (tid < (1 << ta)) {                          // threads [0, 2^ta): low-half products
@@ -355,7 +363,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
       }
       tabB[i] = v;
     }
-    __syncthreads();
+    lds_barrier();
     HEA_MARK();
     const uint32_t am = (1u << ta) - 1u;
     const int iters = (T + NT - 1) / NT;
@@ -390,20 +398,21 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
   const int ncol = T >> 4, nblk = ncol >> 4;
   const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
   // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op)
+  if (tid < a.nops) fidx_s[tid] = a.fidx[tid];   // LDS copy: the prefetch below never waits on a global load
   int nxt = (tid < OPW && a.nops > 0) ? a.ops[tid] : 0;
   uint4 FN[4] = {};
   if (a.nops > 0) load_frags(a, k, a.fidx[0], lane, FN);
-  __syncthreads();
+  lds_barrier();
   HEA_MARK();
   for (int o = 0; o < a.nops; ++o) {
-    __syncthreads();
+    lds_barrier();
     HEA_MARK();
     if (tid < OPW) opw[tid] = nxt;
     const uint4 F[4] = {FN[0], FN[1], FN[2], FN[3]};
-    __syncthreads();
+    lds_barrier();
     if (o + 1 < a.nops) {
       if (tid < OPW) nxt = a.ops[(size_t)(o + 1) * OPW + tid];
-      load_frags(a, k, a.fidx[o + 1], lane, FN);
+      load_frags(a, k, fidx_s[o + 1], lane, FN);
     }
     const int code = opw[W_CODE];
     const int nreal = opw[W_NREAL];
@@ -438,7 +447,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
             atomicAdd(&red64[256 + e], (unsigned long long)(long long)((double)accI[i] * 1048576.0));
           }
         }
-        __syncthreads();
+        lds_barrier();
         if (wave == 0) {   // partial traces: lane (j, y, x, comp) sums N[b][a], b_j = y, a_j = x, b ^ a in {0, e_j}
           const int j = (lane >> 3) & 3, y = (lane >> 2) & 1, x = (lane >> 1) & 1, comp = lane & 1;
           double v = 0.0;
@@ -528,7 +537,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
           if (lane == 0) red[wave * CMAX + c] = v;
         }
       }
-      __syncthreads();
+      lds_barrier();
       if (tid < a.C) {
         float v = 0.f;
         for (int w = 0; w < NW; ++w) v += red[w * CMAX + tid];
@@ -536,11 +545,11 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   HEA_MARK();
   if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
   if (ADJ && a.store_lam) store_tile<NT>(a, a.lam_out + (size_t)s * N, lam_t, tid, T, h_q, fixed);
-  __syncthreads();
+  lds_barrier();
   HEA_MARK();
 #undef HEA_MARK
 }

@@ -66,6 +66,12 @@ def main():
     run("load_only", False, p1, f1[:0], fi1[:0], False, False, False, False)
     run("load_readout", False, p1, f1[-1:].contiguous(), fi1[-1:].contiguous(), False, False, False, False)
     run("load_3apply_readout", False, p1, f1, fi1, False, False, False, False)
+    nop = torch.zeros(64, 128, dtype=torch.int32, device=dev)
+    nop[:, 0] = 9                                   # unknown code: the kernel only does the per-op bookkeeping
+    nopf = torch.full((64,), -1, dtype=torch.int32, device=dev)
+    run("gen_store_64nop", False, p0, nop, nopf, True, False, True, False)
+    nopf2 = fi0[:1].repeat(64).contiguous()
+    run("gen_store_64nop_frag", False, p0, nop, nopf2, True, False, True, False)
     run("adj1_full", True, p1, a1, ai1, False, False, False, True)
     run("adj0_full", True, p0, a0, ai0, False, True, False, False)
     run("adj0_1back", True, p0, a0[:1].contiguous(), ai0[:1].contiguous(), False, True, False, False)
