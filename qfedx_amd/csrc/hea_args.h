@@ -22,8 +22,9 @@ struct HeaPassArgs {
   int n_slots;
   const float* wread;        // [S][C] dL/d<Z_c>
   float* part;               // [S][n_tiles][C] readout partials
-  float* gslab;              // [S][slab_tiles][n_theta] gradient partials
+  long long* gslab;          // [S][slab_tiles][n_gradops][32] 2^-32 fixed-point partial traces
   int slab_tiles;
+  int n_gradops;
   int hrow[5];               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
   long long* dbg;            // optional phase timestamps (s_memtime) of workgroups < 8, [8][64]
 };

@@ -15,8 +15,8 @@ extern "C" {
 int qfx_hea_pass(int adjoint, const HeaPassArgs* args, int n_samples, hipStream_t st);
 int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                   hipStream_t st);
-int qfx_hea_grad_reduce(const float* gslab, int slab_tiles, const int* owner_tiles, int n_theta, int spc, int K,
-                        float* grad, int p_stride, hipStream_t st);
+int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc, int K,
+                        const float* params, float* grad, int p_stride, hipStream_t st);
 int qfx_hea_args_size();
 }
 
@@ -43,12 +43,12 @@ void check(int rc, const char* what) {
 }
 
 // geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
-//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows)]
+//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops]
 void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<int64_t> geom, double scale, torch::Tensor psi_in,
               torch::Tensor psi_out, torch::Tensor lam_in, torch::Tensor lam_out, torch::Tensor xang,
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
               torch::Tensor gslab, torch::Tensor dbg) {
-  need(geom.size() == 25, "geometry vector must have 25 entries");
+  need(geom.size() == 26, "geometry vector must have 26 entries");
   HeaPassArgs a{};
   a.n = (int)geom[0];
   a.t = (int)geom[1];
@@ -70,6 +70,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.n_slots = (int)geom[17];
   a.slab_tiles = (int)geom[18];
   const int64_t K = geom[19];
+  a.n_gradops = (int)geom[25];
   a.scale = (float)scale;
   a.dbg = dbg.defined() && dbg.numel() >= 8 * 64 ? dp<long long>(dbg, torch::kInt64, "dbg", 8 * 64) : nullptr;
   for (int b = 0; b < 5; ++b) {
@@ -101,14 +102,15 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.wread = adjoint ? dp<float>(wread, torch::kFloat32, "wread", S * a.C) : nullptr;
   a.part = dp<float>(part, torch::kFloat32, "part", 0);
   if (a.part) need(part.numel() >= S * a.n_tiles * a.C, "part buffer too small");
-  a.gslab = adjoint ? dp<float>(gslab, torch::kFloat32, "gslab", S * a.slab_tiles * a.n_theta) : nullptr;
+  a.gslab = adjoint ? dp<long long>(gslab, torch::kInt64, "gslab", S * a.slab_tiles * a.n_gradops * 32) : nullptr;
   need(!adjoint || a.slab_tiles >= a.n_tiles, "gradient slab has fewer tiles than the pass");
   need(!a.gen || a.n <= 32, "product-state generation supports <= 32 qubits");
   check(qfx_hea_pass(adjoint ? 1 : 0, &a, (int)S, cur()), "qfx_hea_pass");
 }
 
 // Validate a pass program once (host copy) when it is built: slot / gradient-slot ranges and op kinds.
-void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64_t n_theta, bool adjoint, int64_t t) {
+void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64_t n_theta, bool adjoint, int64_t t,
+                   int64_t n_gradops) {
   need(fidx.scalar_type() == torch::kInt32 && !fidx.is_cuda() && fidx.numel() == ops.size(0),
        "fidx must be a host int32 [nops] tensor");
   const int* fi = fidx.data_ptr<int>();
@@ -128,6 +130,7 @@ void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64
         need(w[12 + j] >= 0 && w[12 + j] < n_theta && w[16 + j] >= 0 && w[16 + j] < n_theta,
              "gradient slot out of range");
       for (int i = 20; i < 100; ++i) need(w[i] >= 0 && w[i] < (1 << t), "tile address out of range");
+      if (code >= 4 && code != 6 && code != 7) need(w[100] >= 0 && w[100] < n_gradops, "gradient op index out of range");
     }
     if (code == 6 || code == 7) need(w[2] >= 1 && w[2] <= 8, "observable count out of range");
   }
@@ -142,12 +145,12 @@ void hea_frags(torch::Tensor params, int64_t p_stride, torch::Tensor slot_tab, i
         "qfx_hea_frags");
 }
 
-void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, torch::Tensor owner_tiles, int64_t n_theta, int64_t spc,
-                     int64_t K, torch::Tensor grad, int64_t p_stride) {
-  check(qfx_hea_grad_reduce(dp<float>(gslab, torch::kFloat32, "gslab", K * spc * slab_tiles * n_theta),
-                            (int)slab_tiles, dp<int>(owner_tiles, torch::kInt32, "owner_tiles", n_theta),
-                            (int)n_theta, (int)spc, (int)K, dp<float>(grad, torch::kFloat32, "grad", K * p_stride),
-                            (int)p_stride, cur()),
+void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops, torch::Tensor gmeta, int64_t spc,
+                     int64_t K, torch::Tensor params, torch::Tensor grad, int64_t p_stride) {
+  check(qfx_hea_grad_reduce(dp<long long>(gslab, torch::kInt64, "gslab", K * spc * slab_tiles * n_gradops * 32),
+                            (int)slab_tiles, (int)n_gradops, dp<int>(gmeta, torch::kInt32, "gmeta", n_gradops * 10),
+                            (int)spc, (int)K, dp<float>(params, torch::kFloat32, "params", K * p_stride),
+                            dp<float>(grad, torch::kFloat32, "grad", K * p_stride), (int)p_stride, cur()),
         "qfx_hea_grad_reduce");
 }
 

@@ -29,7 +29,8 @@ constexpr int OPW = 128;
 enum { OP_APPLY = 1, OP_UNAPPLY_PSI = 2, OP_UNAPPLY_LAM = 3, OP_GRAD = 4, OP_GRAD_L1 = 5, OP_OBS = 6, OP_READOUT = 7,
        OP_BACK = 8 };
 enum { W_CODE = 0, W_SLOT = 1, W_NREAL = 2, W_FLAGS = 3, W_RFULL = 4, W_RT = 8, W_TH = 12, W_PH = 16, W_OFF = 20,
-       W_BL = 36, W_BH = 68 };
+       W_BL = 36, W_BH = 68, W_GIDX = 100 };
+constexpr double FIX = 4294967296.0;   // 2^32: fixed point of the scaled gradient partial traces
 constexpr int F_BACK_PSI = 1;
 constexpr int TMAX = 14;
 constexpr int NT_FWD = 512;    // forward: 8 waves, 64 KB LDS -> 2 workgroups per CU
@@ -435,47 +436,37 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
           else
             group_apply<1, NW>(tile, tbl, F, opw, fo, lane, wave, nbw);
         }
-        // Cross-wave sum of N in 2^-20 fixed point with 64-bit LDS atomics: integer addition is associative, so
-        // the sum is bitwise independent of the order the waves arrive in.  Only entries with b ^ a in
-        // {0, e_j} enter a partial trace; lane (g4, cl) holds N[4 g4 + i][cl].
+        // Cross-wave sum of N, pre-scaled by the sample's rho / scale^2, in 2^-32 fixed point with 64-bit LDS
+        // atomics: integer addition is associative, so the sums are bitwise independent of the order the waves
+        // (and, in hea_grad_reduce, the samples and tiles) arrive in.  Only entries with b ^ a in {0, e_j}
+        // enter a partial trace; lane (g4, cl) holds N[4 g4 + i][cl].
+        const double sc = (double)rsc[CMAX] * FIX;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15;
           if (__builtin_popcount(bb ^ aa) <= 1) {
             const int e = bb * 16 + aa;
-            atomicAdd(&red64[e], (unsigned long long)(long long)((double)accR[i] * 1048576.0));
-            atomicAdd(&red64[256 + e], (unsigned long long)(long long)((double)accI[i] * 1048576.0));
+            atomicAdd(&red64[e], (unsigned long long)__double2ll_rn((double)accR[i] * sc));
+            atomicAdd(&red64[256 + e], (unsigned long long)__double2ll_rn((double)accI[i] * sc));
           }
         }
         lds_barrier();
-        if (wave == 0) {   // partial traces: lane (j, y, x, comp) sums N[b][a], b_j = y, a_j = x, b ^ a in {0, e_j}
-          const int j = (lane >> 3) & 3, y = (lane >> 2) & 1, x = (lane >> 1) & 1, comp = lane & 1;
-          double v = 0.0;
-          if (lane < 32 && j < nreal) {
-            const int lowm = (1 << j) - 1;
-            for (int o8 = 0; o8 < 8; ++o8) {    // the other three bits of b
-              const int bb = ((o8 & ~lowm) << 1) | (o8 & lowm) | (y << j);
-              const int aa = (bb & ~(1 << j)) | (x << j);
-              v += (double)(long long)red64[comp * 256 + bb * 16 + aa];
+        if (wave == 0) {   // partial traces: lane (j, y, x, comp) = sum of N[b][a], b_j = y, a_j = x, b ^ a in {0, e_j}
+          if (lane < 32) {
+            const int j = lane >> 3, y = (lane >> 2) & 1, x = (lane >> 1) & 1, comp = lane & 1;
+            unsigned long long v = 0ull;
+            if (j < nreal) {
+              const int lowm = (1 << j) - 1;
+#pragma unroll
+              for (int o8 = 0; o8 < 8; ++o8) {    // the other three bits of b
+                const int bb = ((o8 & ~lowm) << 1) | (o8 & lowm) | (y << j);
+                const int aa = (bb & ~(1 << j)) | (x << j);
+                v += red64[comp * 256 + bb * 16 + aa];
+              }
             }
+            a.gslab[(((size_t)s * a.slab_tiles + tile_id) * a.n_gradops + opw[W_GIDX]) * 32 + lane] = (long long)v;
           }
-          const float pv = (float)(v * (1.0 / 1048576.0));
-          // lane 8j + k holds pt[k] = n[y][x].(re, im) with k = 4y + 2x + comp
-          const int jj = lane >> 1;
-          const float p1 = __shfl(pv, 8 * jj + 1, 64), p2 = __shfl(pv, 8 * jj + 2, 64);
-          const float p3 = __shfl(pv, 8 * jj + 3, 64), p4 = __shfl(pv, 8 * jj + 4, 64);
-          const float p5 = __shfl(pv, 8 * jj + 5, 64), p7 = __shfl(pv, 8 * jj + 7, 64);
           for (int e = lane; e < 512; e += 64) red64[e] = 0ull;     // ready for the next gradient op
-          if (lane < 2 * nreal) {
-            float* gs = a.gslab + ((size_t)s * a.slab_tiles + tile_id) * a.n_theta;
-            if ((lane & 1) == 0) {               // d/dtheta = Im(e^{-i ph} n10 + e^{i ph} n01)
-              float sp, cp;
-              __sincosf(prm[opw[W_PH + jj]], &sp, &cp);
-              gs[opw[W_TH + jj]] = ((cp * p5 - sp * p4) + (cp * p3 + sp * p2)) * rsc[CMAX];
-            } else {                             // d/dphi = Im(n00 - n11)
-              gs[opw[W_PH + jj]] = (p1 - p7) * rsc[CMAX];
-            }
-          }
         }
       }
     } else if (ADJ && code == OP_OBS) {
@@ -609,17 +600,31 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
   base[128 + h * 64 + lane] = Lw;
 }
 
-// grad[k][j] = sum over the client's samples and the owner pass' tiles of the slab (fixed order)
-__global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const float* __restrict__ gslab, int slab_tiles,
-                                                              const int* __restrict__ owner_tiles, int n_theta,
-                                                              int spc, float* __restrict__ grad, int p_stride) {
-  const int k = blockIdx.x;
-  for (int j = threadIdx.x; j < n_theta; j += 256) {
-    const int nt = owner_tiles[j];
-    float acc = 0.f;
+// Per client and gradient op: exact int64 sums of the 32 partial-trace slots over the client's samples and
+// the op's tiles, then per real qubit j (slots 8j + 4y + 2x + comp = n_j[y][x].(re, im))
+//   d/dtheta = Im(e^{-i phi} n10 + e^{i phi} n01),   d/dphi = Im(n00 - n11).
+__global__ void __launch_bounds__(64) hea_grad_reduce_kernel(const long long* __restrict__ gslab, int slab_tiles,
+                                                             int n_gradops, const int* __restrict__ gmeta, int spc,
+                                                             const float* __restrict__ params,
+                                                             float* __restrict__ grad, int p_stride) {
+  const int k = blockIdx.x, g = blockIdx.y, lane = threadIdx.x;
+  const int* m = gmeta + g * 10;
+  const int nt = m[0], nreal = m[1];
+  __shared__ double pt[32];
+  if (lane < 32) {
+    long long acc = 0;
     for (int s = k * spc; s < (k + 1) * spc; ++s)
-      for (int t = 0; t < nt; ++t) acc += gslab[((size_t)s * slab_tiles + t) * n_theta + j];
-    grad[(size_t)k * p_stride + j] = acc;
+      for (int t = 0; t < nt; ++t) acc += gslab[(((size_t)s * slab_tiles + t) * n_gradops + g) * 32 + lane];
+    pt[lane] = (double)acc / FIX;
+  }
+  __syncthreads();
+  if (lane < nreal) {
+    const double* p = pt + 8 * lane;
+    const float* prm = params + (size_t)k * p_stride;
+    const double ph = prm[m[6 + lane]];
+    const double cp = cos(ph), sp = sin(ph);
+    grad[(size_t)k * p_stride + m[2 + lane]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
+    grad[(size_t)k * p_stride + m[6 + lane]] = (float)(p[1] - p[7]);
   }
 }
 
@@ -645,11 +650,11 @@ extern "C" int qfx_hea_frags(const float* params, int p_stride, const int* slot_
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_hea_grad_reduce(const float* gslab, int slab_tiles, const int* owner_tiles, int n_theta, int spc,
-                                   int K, float* grad, int p_stride, hipStream_t st) {
-  if (K == 0) return 0;
-  hipLaunchKernelGGL(hea::hea_grad_reduce_kernel, dim3(K), dim3(256), 0, st, gslab, slab_tiles, owner_tiles, n_theta,
-                     spc, grad, p_stride);
+extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc,
+                                   int K, const float* params, float* grad, int p_stride, hipStream_t st) {
+  if (K == 0 || n_gradops == 0) return 0;
+  hipLaunchKernelGGL(hea::hea_grad_reduce_kernel, dim3(K, n_gradops), dim3(64), 0, st, gslab, slab_tiles, n_gradops,
+                     gmeta, spc, params, grad, p_stride);
   return (int)hipGetLastError();
 }
 

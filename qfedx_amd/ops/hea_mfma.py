@@ -58,12 +58,15 @@ class HeaMfmaProgram:
         C = ext()
         self.n_slots = self.plan.n_slots
         self.passes = []
-        for p, fwd, adj in pass_programs(self.plan):
+        gmeta = []
+        progs = pass_programs(self.plan, gmeta)
+        self.n_gradops = len(gmeta)
+        for p, fwd, adj in progs:
             f = torch.from_numpy(fwd.astype(np.int32)).contiguous()
             a = torch.from_numpy(adj.astype(np.int32)).contiguous()
             ff, fa = _frag_index(fwd), _frag_index(adj)
-            C.hea_check_ops(f, ff, self.n_slots, self.n_theta, False, p.t)
-            C.hea_check_ops(a, fa, self.n_slots, self.n_theta, True, p.t)
+            C.hea_check_ops(f, ff, self.n_slots, self.n_theta, False, p.t, self.n_gradops)
+            C.hea_check_ops(a, fa, self.n_slots, self.n_theta, True, p.t, self.n_gradops)
             self.passes.append((p, (f.to(self.device), ff.to(self.device)), (a.to(self.device), fa.to(self.device))))
         slot_tab = np.zeros((max(self.n_slots, 1), 9), dtype=np.int32)
         owner = np.zeros(self.n_theta, dtype=np.int32)
@@ -81,7 +84,7 @@ class HeaMfmaProgram:
         if (owner == 0).any():
             raise RuntimeError("a parameter has no owning pass")
         self.slot_tab = torch.from_numpy(slot_tab).to(self.device)
-        self.owner_tiles = torch.from_numpy(owner).to(self.device)
+        self.gmeta = torch.tensor(gmeta, dtype=torch.int32).reshape(-1).to(self.device)
         self.slab_tiles = max(1 << (self.n - p.t) for p in self.plan.passes)
         self.scale = float(1 << (self.n // 2))
         self.feature = _FEATURE[spec.feature_map.lower()]
@@ -116,7 +119,7 @@ class HeaMfmaProgram:
     def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K):
         return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
                 int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
-                self.slab_tiles, K] + [int(h) for h in p.H]
+                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops]
 
     def _frags(self, params: torch.Tensor, K: int) -> torch.Tensor:
         fr = self._buf("frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
@@ -206,10 +209,10 @@ class HeaMfmaProgram:
         z = self._buf("expz", S * self.C, torch.float32)
         ext().readout_sum(part, self.tiles_last, self.C, S, z)
         wr = w.reshape(S, self.C).float().contiguous()
-        gslab = self._buf("gslab", S * self.slab_tiles * self.n_theta, torch.float32)
+        gslab = self._buf("gslab", S * self.slab_tiles * self.n_gradops * 32, torch.int64)
         self._adjoint(x, th, fr, K, B, stored, wr, gslab)
         grad = torch.zeros(K, th.shape[1], dtype=torch.float32, device=self.device)
-        ext().hea_grad_reduce(gslab, self.slab_tiles, self.owner_tiles, self.n_theta, B, K, grad, th.shape[1])
+        ext().hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, th, grad, th.shape[1])
         return z.view(S, self.C).clone(), grad[:, : self.n_theta]
 
     # ------------------------------------------------------------------ train step
@@ -227,7 +230,7 @@ class HeaMfmaProgram:
         part = self._buf("part", S * self.tiles_last * self.C, torch.float32)
         expz = self._buf("expz", S * self.C, torch.float32)
         wread = self._buf("wread", S * self.C, torch.float32)
-        gslab = self._buf("gslab", S * self.slab_tiles * self.n_theta, torch.float32)
+        gslab = self._buf("gslab", S * self.slab_tiles * self.n_gradops * 32, torch.int64)
         loss = torch.empty(K, dtype=torch.float32, device=self.device) if out_loss is None else out_loss
         correct = torch.empty(K, dtype=torch.float32, device=self.device) if out_correct is None else out_correct
         grad = torch.empty_like(p)
@@ -240,5 +243,5 @@ class HeaMfmaProgram:
             C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss, correct,
                          grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
         self._adjoint(x, p, fr, K, B, stored, wread, gslab)
-        C.hea_grad_reduce(gslab, self.slab_tiles, self.owner_tiles, self.n_theta, B, K, grad, p.shape[1])
+        C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1])
         return {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}

@@ -47,6 +47,7 @@ OP_APPLY, OP_UNAPPLY_PSI, OP_UNAPPLY_LAM, OP_GRAD, OP_GRAD_L1, OP_OBS, OP_READOU
 OP_WORDS = 128
 W_CODE, W_SLOT, W_NREAL, W_FLAGS, W_RFULL, W_RT, W_TH, W_PH, W_OFF, W_BL, W_BH = 0, 1, 2, 3, 4, 8, 12, 16, 20, 36, 68
 F_BACK_PSI = 1             # OP_BACK also un-applies the group on psi (still needed further back)
+W_GIDX = 100               # gradient ops: global index of the op's partial-trace record in the slab
 MAX_CLASSES = 8
 BANK_BITS = 5              # ds_read_b32 / ds_write_b32: bank = dword address % 32 per 32-lane half
 
@@ -483,9 +484,12 @@ def obs_table(plan: HEAPlan, p: Pass, code: int) -> np.ndarray:
     return w
 
 
-def pass_programs(plan: HEAPlan):
-    """Forward and adjoint op lists per pass: list of (Pass, fwd_ops [k, OP_WORDS], adj_ops)."""
+def pass_programs(plan: HEAPlan, meta: list | None = None):
+    """Forward and adjoint op lists per pass: list of (Pass, fwd_ops [k, OP_WORDS], adj_ops).  ``meta``
+    (optional list) receives one row per gradient op: [tiles of its pass, nreal, theta slots x4, phi slots x4]."""
     out = []
+    gidx = [0]
+    gmeta = meta if meta is not None else []
     J = len(plan.passes)
     for j, p in enumerate(plan.passes):
         fwd = [group_table(plan, p, g, OP_APPLY) for g in p.groups]
@@ -500,6 +504,12 @@ def pass_programs(plan: HEAPlan):
             adj.append(group_table(plan, p, g, OP_BACK, F_BACK_PSI if psi_needed else 0))
         for g in p.l1:
             adj.append(group_table(plan, p, g, OP_GRAD_L1))
+        for w in adj:
+            if w[W_CODE] in (OP_BACK, OP_GRAD, OP_GRAD_L1):
+                w[W_GIDX] = gidx[0]
+                gmeta.append([1 << (plan.n - p.t), int(w[W_NREAL])] + [int(v) for v in w[W_TH:W_TH + 4]] +
+                             [int(v) for v in w[W_PH:W_PH + 4]])
+                gidx[0] += 1
         out.append((p, np.stack(fwd) if fwd else np.zeros((0, OP_WORDS), np.int64),
                     np.stack(adj) if adj else np.zeros((0, OP_WORDS), np.int64)))
     return out

@@ -27,7 +27,7 @@ def main():
     buf2 = torch.zeros(N, dtype=torch.int32, device=dev)
     lam = torch.zeros(N, dtype=torch.int32, device=dev)
     part = torch.zeros(S * 64 * 3, device=dev)
-    gslab = torch.zeros(S * prog.slab_tiles * prog.n_theta, device=dev)
+    gslab = torch.zeros(S * prog.slab_tiles * prog.n_gradops * 32, dtype=torch.int64, device=dev)
     wread = torch.randn(S, 3, device=dev) / B
     empty = torch.empty(0, dtype=torch.int32, device=dev)
     fempty = torch.empty(0, dtype=torch.float32, device=dev)

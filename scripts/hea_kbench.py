@@ -53,7 +53,7 @@ def main():
     part = prog._buf("part", S * prog.tiles_last * prog.C, torch.float32)
     stored = prog._forward(xx, params, fr, K, B, part, store_last=True)
     wread = torch.randn(S, prog.C, device=dev) / B
-    gslab = prog._buf("gslab", S * prog.slab_tiles * prog.n_theta, torch.float32)
+    gslab = prog._buf("gslab", S * prog.slab_tiles * prog.n_gradops * 32, torch.int64)
     empty = torch.empty(0, dtype=torch.int32, device=dev)
     fempty = torch.empty(0, dtype=torch.float32, device=dev)
     J = prog.n_passes
@@ -90,7 +90,7 @@ def main():
         timeit(lambda: C.hea_pass(True, adj[0], adj[1], geom, prog.scale, stored[j], empty, lin, lout,
                                   xx, params, fr, wread, fempty, gslab, _NODBG), f"adj{j}", nb)
     grad = torch.zeros(K, params.shape[1], device=dev)
-    timeit(lambda: C.hea_grad_reduce(gslab, prog.slab_tiles, prog.owner_tiles, prog.n_theta, B, K, grad,
+    timeit(lambda: C.hea_grad_reduce(gslab, prog.slab_tiles, prog.n_gradops, prog.gmeta, B, K, params, grad,
                                      params.shape[1]), "grad_reduce", 0)
     print(json.dumps(res), flush=True)
 
