@@ -118,6 +118,10 @@ void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64
   need(ops.dim() == 2 && ops.size(1) == 128 && ops.scalar_type() == torch::kInt32 && !ops.is_cuda() &&
        ops.is_contiguous(), "ops must be a contiguous host int32 [nops, 128] tensor");
   const int* ow = ops.data_ptr<int>();
+  int ngrad = 0;
+  for (int64_t o = 0; o < ops.size(0); ++o) ngrad += (ow[o * 128] == 4 || ow[o * 128] == 5 || ow[o * 128] == 8);
+  need(ngrad <= 12, "at most 12 gradient ops per pass program");
+  need(ops.size(0) <= 128, "at most 128 ops per pass program");
   for (int64_t o = 0; o < ops.size(0); ++o) {
     const int* w = ow + o * 128;
     const int code = w[0];

@@ -37,6 +37,7 @@ constexpr int NT_FWD = 512;    // forward: 8 waves, 64 KB LDS -> 2 workgroups pe
 constexpr int NT_ADJ = 1024;   // adjoint: 16 waves, 128 KB LDS (psi + lambda) -> 1 workgroup per CU
 constexpr int CMAX = 8;
 constexpr int MAXOPS = 128;    // ops per pass program (host-checked)
+constexpr int MAXGRAD = 12;    // gradient ops per pass program (host-checked)
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
@@ -302,7 +303,11 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
   __shared__ int opw[OPW];
   __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
   __shared__ float red[NW * CMAX];
-  __shared__ unsigned long long red64[ADJ ? 512 : 1];   // gradient cross matrix, 2^-20 fixed point
+  // per gradient op of the pass: the 80 cross-matrix entries a partial trace can use (b = a, and b = a ^ e_j),
+  // x (re, im), in 2^-32 fixed point; turned into partial traces once, at the end of the pass
+  __shared__ unsigned long long red64[ADJ ? MAXGRAD * 160 : 1];
+  __shared__ int gops[ADJ ? MAXGRAD * 2 : 1];            // (slab index, nreal) of the pass' gradient ops
+  int ngrad = 0;
   __shared__ float2 wv[32][2];
   __shared__ float2 tabA[128];
   __shared__ float2 tabB[128];
@@ -395,7 +400,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
 
   // ---------------------------------------------------------------- op list
   if (ADJ)
-    for (int e = tid; e < 512; e += NT) red64[e] = 0ull;
+    for (int e = tid; e < MAXGRAD * 160; e += NT) red64[e] = 0ull;
   const int ncol = T >> 4, nblk = ncol >> 4;
   const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
   // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op)
@@ -436,38 +441,27 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
           else
             group_apply<1, NW>(tile, tbl, F, opw, fo, lane, wave, nbw);
         }
-        // Cross-wave sum of N, pre-scaled by the sample's rho / scale^2, in 2^-32 fixed point with 64-bit LDS
-        // atomics: integer addition is associative, so the sums are bitwise independent of the order the waves
-        // (and, in hea_grad_reduce, the samples and tiles) arrive in.  Only entries with b ^ a in {0, e_j}
-        // enter a partial trace; lane (g4, cl) holds N[4 g4 + i][cl].
+        // Cross-wave sum of the partial-trace entries of N, pre-scaled by the sample's rho / scale^2, in 2^-32
+        // fixed point with 64-bit LDS atomics into this op's own region (no barrier, no tail: the regions are
+        // reduced to partial traces once at the end of the pass).  Integer addition is associative, so the sums
+        // are bitwise independent of the order the waves (and, in hea_grad_reduce, samples and tiles) arrive.
+        // Lane (g4, cl) holds N[4 g4 + i][cl]; entry slot: b == a -> b, b ^ a == e_j -> 16 + 16 j + b.
         const double sc = (double)rsc[CMAX] * FIX;
+        unsigned long long* rg = red64 + ngrad * 160;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15;
-          if (__builtin_popcount(bb ^ aa) <= 1) {
-            const int e = bb * 16 + aa;
-            atomicAdd(&red64[e], (unsigned long long)__double2ll_rn((double)accR[i] * sc));
-            atomicAdd(&red64[256 + e], (unsigned long long)__double2ll_rn((double)accI[i] * sc));
+          const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15, d = bb ^ aa;
+          if (__builtin_popcount(d) <= 1) {
+            const int e = d == 0 ? (int)bb : 16 + 16 * (__builtin_ctz(d)) + (int)bb;
+            atomicAdd(&rg[e], (unsigned long long)__double2ll_rn((double)accR[i] * sc));
+            atomicAdd(&rg[80 + e], (unsigned long long)__double2ll_rn((double)accI[i] * sc));
           }
         }
-        lds_barrier();
-        if (wave == 0) {   // partial traces: lane (j, y, x, comp) = sum of N[b][a], b_j = y, a_j = x, b ^ a in {0, e_j}
-          if (lane < 32) {
-            const int j = lane >> 3, y = (lane >> 2) & 1, x = (lane >> 1) & 1, comp = lane & 1;
-            unsigned long long v = 0ull;
-            if (j < nreal) {
-              const int lowm = (1 << j) - 1;
-#pragma unroll
-              for (int o8 = 0; o8 < 8; ++o8) {    // the other three bits of b
-                const int bb = ((o8 & ~lowm) << 1) | (o8 & lowm) | (y << j);
-                const int aa = (bb & ~(1 << j)) | (x << j);
-                v += red64[comp * 256 + bb * 16 + aa];
-              }
-            }
-            a.gslab[(((size_t)s * a.slab_tiles + tile_id) * a.n_gradops + opw[W_GIDX]) * 32 + lane] = (long long)v;
-          }
-          for (int e = lane; e < 512; e += 64) red64[e] = 0ull;     // ready for the next gradient op
+        if (tid == 0) {
+          gops[2 * ngrad] = opw[W_GIDX];
+          gops[2 * ngrad + 1] = nreal;
         }
+        ++ngrad;
       }
     } else if (ADJ && code == OP_OBS) {
       // sign_c(w) = parity(w & O'_c) ^ parity(fixed & O_c) = per-thread part ^ per-iteration (uniform) part
@@ -538,6 +532,21 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
   }
   lds_barrier();
   HEA_MARK();
+  if (ADJ) {   // partial traces: thread (op, j, y, x, comp) sums the 8 entries with b_j = y, a_j = x
+    for (int e = tid; e < ngrad * 32; e += NT) {
+      const int g = e >> 5, r = e & 31, j = r >> 3, y = (r >> 2) & 1, x = (r >> 1) & 1, comp = r & 1;
+      const unsigned long long* rg = red64 + g * 160 + comp * 80;
+      unsigned long long v = 0ull;
+      if (j < gops[2 * g + 1]) {
+        const int lowm = (1 << j) - 1;
+        for (int o8 = 0; o8 < 8; ++o8) {    // the other three bits of b
+          const int bb = ((o8 & ~lowm) << 1) | (o8 & lowm) | (y << j);
+          v += rg[x == y ? bb : 16 + 16 * j + bb];
+        }
+      }
+      a.gslab[(((size_t)s * a.slab_tiles + tile_id) * a.n_gradops + gops[2 * g]) * 32 + r] = (long long)v;
+    }
+  }
   if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
   if (ADJ && a.store_lam) store_tile<NT>(a, a.lam_out + (size_t)s * N, lam_t, tid, T, h_q, fixed);
   lds_barrier();
