@@ -66,7 +66,7 @@ def main():
     ap.add_argument("--dp", action="store_true")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--device", default="auto")
-    ap.add_argument("--engine", default="valu", choices=["mfma", "valu"],
+    ap.add_argument("--engine", default="mfma", choices=["mfma", "valu"],
                     help="mfma: fp16-state MFMA group-unitary engine (ops/hea_mfma.py); valu: fp32 pass engine")
     args = ap.parse_args()
 

@@ -32,6 +32,10 @@ SUITE = {
                       "client local-steps/sec (16-qubit VQC bf16 state x 8 clients)", None),
     "vqc16q_64": ("configs/headline_16q_64clients.yaml", [],
                   "client local-steps/sec (16-qubit VQC x 64 clients federated rounds)", None),
+    "vqc16q_64_mfma": ("configs/headline_16q_64clients.yaml", ["model.state_dtype=mfma"],
+                       "client local-steps/sec (16-qubit VQC x 64 clients, fp16 MFMA engine)", None),
+    "vqc20q_dp64_mfma": ("configs/baseline3_20q_dp_64clients.yaml", ["model.state_dtype=mfma"],
+                         "client local-steps/sec (20-qubit VQC x 64 non-IID clients, DP, fp16 MFMA engine)", None),
     "vqc4q_2_cpu": ("configs/baseline1_4q_2clients_cpu.yaml", ["train.local_steps=1"],
                     "client local-steps/sec (4-qubit VQC x 2 clients, CPU gloo)", None),
 }
@@ -73,7 +77,8 @@ def main():
             "n_gpus": world.world_size, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(value / ref, 2) if ref else None,
-            "dtype": "bf16-state/fp32-compute" if cfg.model.state_dtype == "bf16" else "fp32",
+            "dtype": {"bf16": "bf16-state/fp32-compute", "mfma": "fp16-state/fp32-accumulate (MFMA)",
+                      "fp16": "fp16-state/fp32-accumulate (MFMA)"}.get(cfg.model.state_dtype, "fp32"),
             "data": "synthetic non-IID client shards, random init", "rounds_per_sec": round(args.steps / dt, 4),
             "samples_per_sec": round(value * t.batch_size, 1), "backend": backend,
             "test_acc_after": round(ev["test_acc"], 4),
