@@ -337,7 +337,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
 
   // ---------------------------------------------------------------- initial psi tile
-  if (a.gen) {
+  if (!ADJ && a.gen) {              // adjoint passes always start from stored outputs
     if (tid < a.n) {
       float2 w[2];
       l1_factor(a.xang[(size_t)s * a.x_stride + tid], prm[2 * tid], prm[2 * tid + 1], a.feature, w);
@@ -372,14 +372,23 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
     lds_barrier();
     HEA_MARK();
     const uint32_t am = (1u << ta) - 1u;
-    const int iters = (T + NT - 1) / NT;
-#pragma unroll 4
-    for (int i = 0; i < iters; ++i) {       // LDS dword w holds amplitude tau = sigma(w)
-      const uint32_t w = (uint32_t)(tid + NT * i);
-      const uint32_t tau = w ^ h_w ^ swz(a, (uint32_t)(NT >> 5) * i);
-      if (w < (uint32_t)T) {
-        const float2 v = cmul(tabA[tau & am], tabB[tau >> ta]);
-        psi_t[w] = pack_h2(v.x, v.y);
+    // quad q = tid + NT i holds LDS words 4q .. 4q+3 = amplitudes tau_e = (4q + e) ^ h, h = h(q >> 3);
+    // the swizzle only flips bits < 5 and ta >= 4, so the four words share one high-half factor
+    constexpr int QI = (1 << TMAX) / (4 * NT);
+#pragma unroll
+    for (int i = 0; i < QI; ++i) {
+      const uint32_t q = (uint32_t)(tid + NT * i);
+      if (4 * q < (uint32_t)T) {
+        const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+        const float2 vb = tabB[((4 * q) ^ h) >> ta];          // same high half for the whole quad
+        uint4 out;
+        uint32_t* ow = (uint32_t*)&out;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float2 v = cmul(tabA[((4 * q + e) ^ h) & am], vb);
+          ow[e] = pack_h2(v.x, v.y);
+        }
+        *(uint4*)&psi_t[4 * q] = out;
       }
     }
   } else {

@@ -9,7 +9,8 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# QFX_PKG_ROOT: import the package from another built tree (scripts/ab_kbench.sh)
+sys.path.insert(0, os.environ.get("QFX_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
