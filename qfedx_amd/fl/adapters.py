@@ -23,9 +23,15 @@ class VQCAdapter:
                             m.alpha, m.entangler, None, m.readout_scale, m.init_std,
                             noisy=self.noise is not None and self.noise.gate_noise)
         self.device = torch.device(device)
-        self.engine = VQCEngine(self.spec, device, backend, m.state_dtype, noise=self.noise)
+        sim = getattr(m, "simulator", "statevector")
+        if sim not in ("statevector", "mps"):
+            raise ValueError(f"model.simulator must be statevector or mps, got '{sim}'")
+        # the circuit engine follows model.simulator; optimizer / aggregation kernels follow the runtime backend
+        self.engine = VQCEngine(self.spec, device, "mps" if sim == "mps" else backend, m.state_dtype,
+                                noise=self.noise, mps_chi=int(getattr(m, "mps_chi", 64)))
         self.trainer = VQCClientTrainer(self.spec, self.engine, cfg.train, device, backend)
-        self.trainer.graphs = bool(getattr(cfg.runtime, "use_graphs", True))
+        # QR/SVD recompression is data dependent: the MPS round runs eagerly, not as a captured graph
+        self.trainer.graphs = bool(getattr(cfg.runtime, "use_graphs", True)) and sim != "mps"
         self.n_params = self.spec.n_params
         self.eval_batch = 4096
 

@@ -7,6 +7,9 @@ replacing the reference's sequential per-client Python loop (``Classical_FL.py:1
 Backends:
   * ``hip``   - gfx950 pass kernels of the in-tree extension (``ops/statevec_hip.py``)
   * ``torch`` - the portable program executor (``ops/statevec_torch.py``), CPU path + oracle
+  * ``mps``   - batched matrix-product-state network (``quantum/mps.py``) for qubit counts past
+                statevector memory (ROADMAP.md:85-87); ``adjoint`` = reverse-mode AD through the exact
+                network, or parameter shift when the bond bound exceeds ``mps_chi``
 
 Gradient methods (ROADMAP.md:23,38,130-135): ``adjoint`` (default; 1 forward + 1 reverse sweep),
 ``param_shift`` (2 shifted circuits per rotation gate, batched), ``spsa`` (2 perturbed losses),
@@ -46,7 +49,7 @@ def ce_readout(expz: torch.Tensor, y: torch.Tensor, wmask: torch.Tensor, a: torc
 
 class VQCEngine:
     def __init__(self, spec: VQCSpec, device="cpu", backend: str = "torch", state_dtype: str = "fp32",
-                 noise=None):
+                 noise=None, mps_chi: int = 64):
         self.spec = spec
         self.noise = noise          # quantum.noise.NoiseModel or None
         self.device = torch.device(device)
@@ -58,6 +61,12 @@ class VQCEngine:
         self.state_dtype = state_dtype
         if backend == "torch":
             self.prog = TorchProgram(ops, coef, spec.n_qubits, self.device)
+            self.hip = None
+        elif backend == "mps":
+            from ..quantum.mps import MPSProgram
+            if spec.amplitude and spec.n_qubits > 26:
+                raise ValueError("amplitude-encoded initial states need a dense 2^n vector (n <= 26 with mps)")
+            self.prog = MPSProgram(ops, coef, spec.n_qubits, self.device, chi_max=mps_chi)
             self.hip = None
         elif backend == "hip" and state_dtype in ("mfma", "fp16"):
             # fp16 states + MFMA group unitaries (ops/hea_mfma.py) for the hardware-efficient ansatz
@@ -169,6 +178,8 @@ class VQCEngine:
                         init=None) -> dict:
         spec = self.spec
         th, a, b = spec.split(params)
+        if method == "autograd" and self.backend == "mps":
+            method = "adjoint"               # the MPS adjoint IS reverse-mode AD through the network
         if method == "autograd":
             return self._autograd(xang, y, wmask, params, init)
         K, B, _ = xang.shape
@@ -185,7 +196,11 @@ class VQCEngine:
             if method == "adjoint":
                 if self.noise is not None:   # straight-through d<Z>_noisy / d<Z> for the exact adjoint
                     w = w * (1.0 - self.noise.p01 - self.noise.p10)
-                gg = self.prog.adjoint_grads(rows, psi, w.reshape(K * B, -1), spec.readout)
+                if self.backend == "mps":
+                    gg = self.prog.adjoint_grads(rows, psi, w.reshape(K * B, -1), spec.readout,
+                                                 init=self._init_rows(init))
+                else:
+                    gg = self.prog.adjoint_grads(rows, psi, w.reshape(K * B, -1), spec.readout)
                 gs = slot_grads(gg, self.ops, self.coef, self.n_slots)[:, :P]
                 gth = gs.reshape(K, B, P).sum(1).float()
             elif method == "param_shift":
@@ -269,7 +284,8 @@ class VQCEngine:
         K, B, F = xang.shape
         P = self.spec.n_theta
         R = 2 * P
-        state_bytes = (1 << self.spec.n_qubits) * 8
+        state_bytes = (self.spec.n_qubits * 2 * 8 * self.prog.chi_max ** 2 if self.backend == "mps"
+                       else (1 << self.spec.n_qubits) * 8)
         rows_per_chunk = max(1, min(K * R, self.state_budget_bytes() // max(1, B * state_bytes)))
         contrib_all = torch.zeros(K * R, dtype=torch.float64, device=params.device)
         half_pi = math.pi / 2

@@ -4,6 +4,7 @@
     psi, z = sim.run(values)                     # values [S, n_slots] -> states [S, 2^n], <Z_c> [S, C]
     z, g = sim.vjp(values, w)                    # adjoint VJP of sum_c w[s,c] <Z_c>_s -> dL/dvalues [S, n_slots]
     psi, z = sim.run(values, initial_state=amp)  # start from given (e.g. amplitude-encoded) states
+    sim = Simulator(circuit, readout=[0], backend="mps", chi_max=64)   # tensor network: run() returns an MPS
 
 ``values`` is one parameter row per circuit instance: the concatenation of the circuit's parameter
 vectors in ``slots`` order (default: order of first appearance).  On a GPU the circuit is planned by the
@@ -22,7 +23,7 @@ from .circuit import Circuit
 
 class Simulator:
     def __init__(self, circuit: Circuit, readout: Optional[list] = None, device="cpu", backend: str = "auto",
-                 slots: Optional[list] = None, state_dtype: str = "fp32"):
+                 slots: Optional[list] = None, state_dtype: str = "fp32", chi_max: int = 64):
         self.circuit = circuit
         self.n = circuit.n_qubits
         self.readout = list(range(min(self.n, 1))) if readout is None else list(readout)
@@ -46,7 +47,10 @@ class Simulator:
         self.n_slots = max(off, 1)
         ops, coef = circuit.to_program(self.slot_of)
         self.ops, self.coef = ops, coef
-        if backend == "hip":
+        if backend == "mps":
+            from .mps import MPSProgram
+            self.prog = MPSProgram(ops, coef, self.n, self.device, chi_max=chi_max)
+        elif backend == "hip":
             from ..ops.statevec_hip import HipProgram
             # every slot is a parameter row entry (n_theta = n_slots); the per-sample x row is a dummy
             self.prog = HipProgram(ops, coef, self.n, self.readout, self.device, n_theta=self.n_slots,
@@ -64,10 +68,14 @@ class Simulator:
         return v.contiguous()
 
     def run(self, values, initial_state: Optional[torch.Tensor] = None):
-        """-> (states [S, 2^n] complex64, <Z_readout> [S, C] float32)."""
+        """-> (states [S, 2^n] complex64, <Z_readout> [S, C] float32); with backend="mps" the states are
+        returned as a ``quantum.mps.MPS`` batch."""
         v = self._rows(values)
         S = v.shape[0]
         init = None if initial_state is None else torch.as_tensor(initial_state).to(self.device, torch.complex64)
+        if self.backend == "mps":
+            st = self.prog.run(v, state=init)
+            return st, self.prog.expz(st, self.readout).float()
         if self.backend == "hip":
             x = torch.zeros(S, 1, 1, device=self.device)
             return self.prog.statevector(x, v, init)
@@ -88,6 +96,12 @@ class Simulator:
             x = torch.zeros(S, 1, 1, device=self.device)
             return self.prog.vjp(x, v, w, init)
         from ..ops.statevec_torch import slot_grads
+        if self.backend == "mps":
+            st = self.prog.run(v, state=init)
+            z = self.prog.expz(st, self.readout).float()
+            gg = self.prog.adjoint_grads(v, st, w, self.readout, init=init)
+            g = slot_grads(gg, torch.from_numpy(self.ops), torch.from_numpy(self.coef), self.n_slots).float()
+            return z, g
         vd = v.double()
         psi = self.prog.run(vd, state=None if init is None else init.to(self.prog.dtype))
         z = self.prog.expz(psi, self.readout).float()
