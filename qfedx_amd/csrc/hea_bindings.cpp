@@ -92,6 +92,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.fidx = a.nops ? dp<int>(fidx, torch::kInt32, "fidx", a.nops) : nullptr;
   const int64_t states = S << a.n;
   a.psi_in = a.gen ? nullptr : dp<uint32_t>(psi_in, torch::kInt32, "psi_in", states);
+  need(!(adjoint && a.store_psi), "adjoint passes store lambda only");
   a.psi_out = a.store_psi ? dp<uint32_t>(psi_out, torch::kInt32, "psi_out", states) : nullptr;
   a.lam_in = (adjoint && a.load_lam) ? dp<uint32_t>(lam_in, torch::kInt32, "lam_in", states) : nullptr;
   a.lam_out = (adjoint && a.store_lam) ? dp<uint32_t>(lam_out, torch::kInt32, "lam_out", states) : nullptr;

@@ -38,6 +38,15 @@ constexpr int NT_ADJ = 1024;   // adjoint: 16 waves, 128 KB LDS (psi + lambda) -
 constexpr int CMAX = 8;
 constexpr int MAXOPS = 128;    // ops per pass program (host-checked)
 constexpr int MAXGRAD = 12;    // gradient ops per pass program (host-checked)
+// Per gradient op, 80 cross-matrix entries e = 16 k + b (k = 0: b == a, k = 1 + j: b ^ a = e_j) x (re, im) as
+// u64 LDS atomics.  A half-wave's active lanes add entries {b + 16 k} with b in {i, i + 4}: unskewed they all
+// sit on one bank pair (5-way conflicts); slot(e) = e + s(k), s = 0, 1, 2, 3, 8, spreads them over distinct
+// 8-byte bank pairs (b + s(k) distinct mod 16).
+constexpr int RIM = 88, RSTR = 2 * RIM;
+__device__ __forceinline__ int red_slot(int e) {
+  const int k = e >> 4;
+  return e + (k < 4 ? k : 8);
+}
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
@@ -137,6 +146,57 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
   }
 }
 
+// Interleaved adjoint image (word 2w = psi, 2w + 1 = lambda of swizzled amplitude w): a quad's psi and
+// lambda dwords go to LDS as two 16-byte pair runs.  Without a lambda input the lambda words are zeroed (the
+// observable op writes them).
+template <int NT>
+__device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* psrc, const uint32_t* lsrc,
+                                             uint32_t* tile, int tid, int T, uint32_t h_q, uint32_t fixed) {
+  constexpr int MQ = (1 << TMAX) / (4 * NT);
+  uint4 v[MQ], l[MQ];
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) {
+      v[i] = *(const uint4*)&psrc[mem_of(q, a, fixed)];
+      l[i] = lsrc ? *(const uint4*)&lsrc[mem_of(q, a, fixed)] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) {
+      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+      const uint4 pv = quad_perm(v[i], h & 3u), lv = quad_perm(l[i], h & 3u);
+      const uint32_t w0 = 2u * ((q ^ h) & ~3u);
+      *(uint4*)&tile[w0] = make_uint4(pv.x, lv.x, pv.y, lv.y);
+      *(uint4*)&tile[w0 + 4] = make_uint4(pv.z, lv.z, pv.w, lv.w);
+    }
+  }
+}
+
+template <int NT>
+__device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, const uint32_t* tile, int tid, int T,
+                                             uint32_t h_q, uint32_t fixed) {
+  constexpr int MQ = (1 << TMAX) / (4 * NT);
+  uint4 v[MQ];
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) {
+      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+      const uint32_t w0 = 2u * ((q ^ h) & ~3u);
+      const uint4 a0 = *(const uint4*)&tile[w0], a1 = *(const uint4*)&tile[w0 + 4];
+      v[i] = quad_perm(make_uint4(a0.y, a0.w, a1.y, a1.w), h & 3u);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
+  }
+}
+
 // RZ(ph) RX(th) F(x)|0> for a layer-1 qubit
 __device__ void l1_factor(float x, float th, float ph, int feature, float2* w) {
   float sa, ca;
@@ -163,10 +223,19 @@ __device__ void l1_factor(float x, float th, float ph, int feature, float2* w) {
   w[1] = cmul(w1, make_float2(cp, sp));
 }
 
-// LDS image: one dword array, psi at byte 0 and lambda at byte LAM_OFF (adjoint), every amplitude
-// addressed by BYTE offset = 4 * sigma(tau); all table entries combine by XOR, so a target's tile base
-// (0 / LAM_OFF, bit 16) is XORed into the lane's constant offsets once per op and each access is one XOR.
-constexpr uint32_t LAM_OFF = 4u << TMAX;
+// LDS images, addressed by BYTE offsets that combine by XOR (each access is one XOR of per-lane constants):
+//   forward: psi only, amplitude tau at byte 4 sigma(tau);
+//   adjoint: psi and lambda interleaved, amplitude tau at bytes 8 sigma(tau) (psi) and 8 sigma(tau) + 4
+//   (lambda).  Every adjoint access touches psi and lambda at the same amplitude, so they move as 8-byte
+//   ds_read_b64 / ds_write_b64 pairs: twice the bytes of ds_read_b32 in the same LDS cycles, and one
+//   6-cycle store instead of two 4-cycle ones.  The b64 read bank is (byte / 4) mod 64 per 32 lanes, i.e.
+//   the pair index sigma(tau) mod 32, so the planner's conflict-free b32 swizzle stays conflict free.
+__device__ __forceinline__ uint2 lds_ld2(const uint32_t* tile, uint32_t byte) {
+  return *(const uint2*)((const char*)tile + byte);
+}
+__device__ __forceinline__ void lds_st2(uint32_t* tile, uint32_t byte, uint2 v) {
+  *(uint2*)((char*)tile + byte) = v;
+}
 
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t* tile, uint32_t byte) {
   return *(const uint32_t*)((const char*)tile + byte);
@@ -182,63 +251,82 @@ __device__ __forceinline__ void lds_st(uint32_t* tile, uint32_t byte, uint32_t v
 // A wave's blocks are blk = wave + NW i (i < nbw <= MAXB, fully unrolled): (blk & 1) = (wave & 1), so the
 // block bases are BL[lane] ^ BH[blk >> 1] precomputed in registers.  Blocks go in pairs (independent MFMA
 // chains) and the next pair's operands are read before the current pair is written (disjoint blocks).
-template <int NX, int NW>
-__device__ __forceinline__ void group_apply(uint32_t* tile, const uint32_t* tb, const uint4* F, const int* opw,
-                                            uint32_t fo, int lane, int wave, int nbw) {
+//   IL = false: forward psi image, NX = 1.
+//   IL = true : interleaved adjoint image; NX = 2 applies U to psi and lambda (one b64 read / write per
+//               amplitude pair), NX = 1 to component SEL only (pairs read, single dwords written).
+template <int NX, int NW, bool IL, int SEL>
+__device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, const int* opw, uint32_t fo, int lane,
+                                            int wave, int nbw) {
   constexpr int MAXB = (1 << (TMAX - 8)) / NW;   // column blocks per wave per op (t = 14: 64 blocks)
+  constexpr int SH = IL ? 3 : 2;
+  static_assert(IL || NX == 1, "the forward image holds psi only");
   const int g4 = lane >> 4, cl = lane & 15;
-  uint32_t oin[NX][4], oout[NX][4];
+  uint32_t oin[4], oout[4];
 #pragma unroll
-  for (int x = 0; x < NX; ++x) {
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) oin[x][jj] = (((uint32_t)opw[W_OFF + 4 * g4 + jj] ^ fo) << 2) ^ tb[x];
-    oout[x][0] = (((uint32_t)opw[W_OFF + 2 * g4] ^ fo) << 2) ^ tb[x];
-    oout[x][1] = (((uint32_t)opw[W_OFF + 2 * g4 + 1] ^ fo) << 2) ^ tb[x];
-    oout[x][2] = (((uint32_t)opw[W_OFF + 8 + 2 * g4] ^ fo) << 2) ^ tb[x];
-    oout[x][3] = (((uint32_t)opw[W_OFF + 9 + 2 * g4] ^ fo) << 2) ^ tb[x];
-  }
+  for (int jj = 0; jj < 4; ++jj) oin[jj] = ((uint32_t)opw[W_OFF + 4 * g4 + jj] ^ fo) << SH;
+  oout[0] = ((uint32_t)opw[W_OFF + 2 * g4] ^ fo) << SH;
+  oout[1] = ((uint32_t)opw[W_OFF + 2 * g4 + 1] ^ fo) << SH;
+  oout[2] = ((uint32_t)opw[W_OFF + 8 + 2 * g4] ^ fo) << SH;
+  oout[3] = ((uint32_t)opw[W_OFF + 9 + 2 * g4] ^ fo) << SH;
   const uint32_t bl = (uint32_t)opw[W_BL + (wave & 1) * 16 + cl];
   uint32_t base[MAXB];
 #pragma unroll
-  for (int i = 0; i < MAXB; ++i) base[i] = (bl ^ (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)]) << 2;
-  auto load = [&](uint32_t b, int x) -> uint4 {
-    return make_uint4(lds_ld(tile, b ^ oin[x][0]), lds_ld(tile, b ^ oin[x][1]), lds_ld(tile, b ^ oin[x][2]),
-                      lds_ld(tile, b ^ oin[x][3]));
+  for (int i = 0; i < MAXB; ++i) base[i] = (bl ^ (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)]) << SH;
+  auto load = [&](uint32_t b, uint4* X) {
+    if constexpr (!IL) {
+      X[0] = make_uint4(lds_ld(tile, b ^ oin[0]), lds_ld(tile, b ^ oin[1]), lds_ld(tile, b ^ oin[2]),
+                        lds_ld(tile, b ^ oin[3]));
+    } else {
+      const uint2 p0 = lds_ld2(tile, b ^ oin[0]), p1 = lds_ld2(tile, b ^ oin[1]), p2 = lds_ld2(tile, b ^ oin[2]),
+                  p3 = lds_ld2(tile, b ^ oin[3]);
+      if constexpr (NX == 2) {
+        X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
+        X[1] = make_uint4(p0.y, p1.y, p2.y, p3.y);
+      } else if constexpr (SEL == 0) {
+        X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
+      } else {
+        X[0] = make_uint4(p0.y, p1.y, p2.y, p3.y);
+      }
+    }
   };
-  auto compute_store = [&](uint32_t b, const uint4& X, int x) {
+  auto compute_store = [&](uint32_t b, const uint4* X) {
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    f4 d0 = mfma(F[0], X, z), d1 = mfma(F[1], X, z);
-    d0 = mfma(F[2], X, d0);
-    d1 = mfma(F[3], X, d1);
-    lds_st(tile, b ^ oout[x][0], pack_h2(d0[0], d0[1]));
-    lds_st(tile, b ^ oout[x][1], pack_h2(d0[2], d0[3]));
-    lds_st(tile, b ^ oout[x][2], pack_h2(d1[0], d1[1]));
-    lds_st(tile, b ^ oout[x][3], pack_h2(d1[2], d1[3]));
+    f4 d0[NX], d1[NX];
+#pragma unroll
+    for (int x = 0; x < NX; ++x) {
+      d0[x] = mfma(F[0], X[x], z);
+      d1[x] = mfma(F[1], X[x], z);
+      d0[x] = mfma(F[2], X[x], d0[x]);
+      d1[x] = mfma(F[3], X[x], d1[x]);
+    }
+    if constexpr (IL && NX == 2) {
+      lds_st2(tile, b ^ oout[0], make_uint2(pack_h2(d0[0][0], d0[0][1]), pack_h2(d0[1][0], d0[1][1])));
+      lds_st2(tile, b ^ oout[1], make_uint2(pack_h2(d0[0][2], d0[0][3]), pack_h2(d0[1][2], d0[1][3])));
+      lds_st2(tile, b ^ oout[2], make_uint2(pack_h2(d1[0][0], d1[0][1]), pack_h2(d1[1][0], d1[1][1])));
+      lds_st2(tile, b ^ oout[3], make_uint2(pack_h2(d1[0][2], d1[0][3]), pack_h2(d1[1][2], d1[1][3])));
+    } else {
+      constexpr uint32_t tb = IL ? 4u * SEL : 0u;
+      lds_st(tile, b ^ oout[0] ^ tb, pack_h2(d0[0][0], d0[0][1]));
+      lds_st(tile, b ^ oout[1] ^ tb, pack_h2(d0[0][2], d0[0][3]));
+      lds_st(tile, b ^ oout[2] ^ tb, pack_h2(d1[0][0], d1[0][1]));
+      lds_st(tile, b ^ oout[3] ^ tb, pack_h2(d1[0][2], d1[0][3]));
+    }
   };
   if (nbw <= 0) return;
   uint4 B0[NX], B1[NX];
-#pragma unroll
-  for (int x = 0; x < NX; ++x) {
-    B0[x] = load(base[0], x);
-    if (nbw > 1) B1[x] = load(base[1], x);
-  }
+  load(base[0], B0);
+  if (nbw > 1) load(base[1], B1);
+  constexpr bool PREFETCH = NX == 1 || NW <= 8;   // the two-target form at 16 waves stays within 128 VGPRs
 #pragma unroll
   for (int p = 0; p < MAXB; p += 2) {
     if (p >= nbw) break;
     uint4 C0[NX], C1[NX];
-    constexpr bool PREFETCH = NX == 1 || NW <= 8;   // the two-target form at 16 waves stays within 128 VGPRs
     if (PREFETCH && p + 2 < MAXB && p + 2 < nbw) {
-#pragma unroll
-      for (int x = 0; x < NX; ++x) {
-        C0[x] = load(base[p + 2 < MAXB ? p + 2 : 0], x);
-        if (p + 3 < nbw) C1[x] = load(base[p + 3 < MAXB ? p + 3 : 0], x);
-      }
+      load(base[p + 2 < MAXB ? p + 2 : 0], C0);
+      if (p + 3 < nbw) load(base[p + 3 < MAXB ? p + 3 : 0], C1);
     }
-#pragma unroll
-    for (int x = 0; x < NX; ++x) {
-      compute_store(base[p], B0[x], x);
-      if (p + 1 < nbw) compute_store(base[p + 1 < MAXB ? p + 1 : 0], B1[x], x);
-    }
+    compute_store(base[p], B0);
+    if (p + 1 < nbw) compute_store(base[p + 1 < MAXB ? p + 1 : 0], B1);
     if (PREFETCH) {
 #pragma unroll
       for (int x = 0; x < NX; ++x) {
@@ -246,11 +334,8 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint32_t* tb, 
         B1[x] = C1[x];
       }
     } else if (p + 2 < MAXB && p + 2 < nbw) {
-#pragma unroll
-      for (int x = 0; x < NX; ++x) {
-        B0[x] = load(base[p + 2 < MAXB ? p + 2 : 0], x);
-        if (p + 3 < nbw) B1[x] = load(base[p + 3 < MAXB ? p + 3 : 0], x);
-      }
+      load(base[p + 2 < MAXB ? p + 2 : 0], B0);
+      if (p + 3 < nbw) load(base[p + 3 < MAXB ? p + 3 : 0], B1);
     }
   }
 }
@@ -266,16 +351,17 @@ __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw
   const uint32_t om = (uint32_t)opw[W_OFF + cl] ^ fo;
   uint32_t gb[4];
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) gb[jj] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + jj] ^ om) << 2;
+  for (int jj = 0; jj < 4; ++jj) gb[jj] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + jj] ^ om) << 3;
 #pragma unroll
   for (int i = 0; i < MAXB; ++i) {
     if (i >= nbw) break;
-    const uint32_t bh = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << 2;
+    const uint32_t bh = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << 3;
     uint32_t pv[4], lv[4];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-      pv[jj] = lds_ld(tile, gb[jj] ^ bh);
-      lv[jj] = lds_ld(tile, gb[jj] ^ bh ^ LAM_OFF);
+    for (int jj = 0; jj < 4; ++jj) {            // (psi, lambda) of one amplitude: one b64 read
+      const uint2 v = lds_ld2(tile, gb[jj] ^ bh);
+      pv[jj] = v.x;
+      lv[jj] = v.y;
     }
     const uint4 A = make_uint4(pv[0], pv[1], pv[2], pv[3]);
     const uint4 Br = make_uint4(lv[0], lv[1], lv[2], lv[3]);
@@ -299,21 +385,21 @@ __device__ __forceinline__ void load_frags(const PassArgs& a, int k, int fi, int
 template <bool ADJ>
 __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArgs a) {
   constexpr int NT = ADJ ? NT_ADJ : NT_FWD, NW = NT / 64;
-  __shared__ uint32_t tile[(ADJ ? 2 : 1) << TMAX];     // psi | lambda (fp16 re, im), swizzled
-  __shared__ int opw[OPW];
+  // psi, or (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
+  __shared__ __attribute__((aligned(16))) uint32_t tile[(ADJ ? 2 : 1) << TMAX];
+  __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
   __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
   __shared__ float red[NW * CMAX];
   // per gradient op of the pass: the 80 cross-matrix entries a partial trace can use (b = a, and b = a ^ e_j),
   // x (re, im), in 2^-32 fixed point; turned into partial traces once, at the end of the pass
-  __shared__ unsigned long long red64[ADJ ? MAXGRAD * 160 : 1];
+  __shared__ unsigned long long red64[ADJ ? MAXGRAD * RSTR : 1];
   __shared__ int gops[ADJ ? MAXGRAD * 2 : 1];            // (slab index, nreal) of the pass' gradient ops
   int ngrad = 0;
   __shared__ float2 wv[32][2];
   __shared__ float2 tabA[128];
   __shared__ float2 tabB[128];
   __shared__ float rsc[CMAX + 2];
-  uint32_t* psi_t = tile;
-  uint32_t* lam_t = tile + (ADJ ? (1 << TMAX) : 0);
+  uint32_t* psi_t = tile;                                // forward image
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -391,13 +477,13 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
         *(uint4*)&psi_t[4 * q] = out;
       }
     }
+  } else if (ADJ) {
+    load_tile_il<NT>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
+                     h_q, fixed);
   } else {
     load_tile<NT>(a, a.psi_in + (size_t)s * N, psi_t, tid, T, h_q, fixed);
   }
   if (ADJ) {
-    if (a.load_lam) {
-      load_tile<NT>(a, a.lam_in + (size_t)s * N, lam_t, tid, T, h_q, fixed);
-    }
     if (tid == 0) {
       float rho = 0.f;
       for (int c = 0; c < a.C; ++c) rho = fmaxf(rho, fabsf(a.wread[(size_t)s * a.C + c]));
@@ -409,24 +495,27 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
 
   // ---------------------------------------------------------------- op list
   if (ADJ)
-    for (int e = tid; e < MAXGRAD * 160; e += NT) red64[e] = 0ull;
+    for (int e = tid; e < MAXGRAD * RSTR; e += NT) red64[e] = 0ull;
   const int ncol = T >> 4, nblk = ncol >> 4;
   const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
   // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op)
   if (tid < a.nops) fidx_s[tid] = a.fidx[tid];   // LDS copy: the prefetch below never waits on a global load
-  int nxt = (tid < OPW && a.nops > 0) ? a.ops[tid] : 0;
+  if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
+  int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
   uint4 FN[4] = {};
   if (a.nops > 0) load_frags(a, k, a.fidx[0], lane, FN);
   lds_barrier();
   HEA_MARK();
   for (int o = 0; o < a.nops; ++o) {
+    // op o's record was written during op o - 1; the other buffer was last read by op o - 1, which every
+    // wave has finished at this barrier, so op o + 1's record is written into it right away
     lds_barrier();
     HEA_MARK();
-    if (tid < OPW) opw[tid] = nxt;
+    const int* opw = opw2[o & 1];
     const uint4 F[4] = {FN[0], FN[1], FN[2], FN[3]};
-    lds_barrier();
     if (o + 1 < a.nops) {
-      if (tid < OPW) nxt = a.ops[(size_t)(o + 1) * OPW + tid];
+      if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
+      if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
       load_frags(a, k, fidx_s[o + 1], lane, FN);
     }
     const int code = opw[W_CODE];
@@ -436,19 +525,18 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
       int fpb = 0;
       for (int j = 0; j < nreal; ++j) fpb |= par(fixed & (uint32_t)opw[W_RFULL + j]) << j;
       const uint32_t fo = (uint32_t)opw[W_OFF + fpb];
-      const uint32_t tbp[1] = {0u}, tbl[1] = {LAM_OFF}, tbb[2] = {LAM_OFF, 0u};
       if (code == OP_APPLY || code == OP_UNAPPLY_PSI) {
-        group_apply<1, NW>(tile, tbp, F, opw, fo, lane, wave, nbw);
+        group_apply<1, NW, ADJ, 0>(tile, F, opw, fo, lane, wave, nbw);
       } else if (ADJ && code == OP_UNAPPLY_LAM) {
-        group_apply<1, NW>(tile, tbl, F, opw, fo, lane, wave, nbw);
+        group_apply<1, NW, true, 1>(tile, F, opw, fo, lane, wave, nbw);
       } else if (ADJ) {   // OP_BACK / OP_GRAD / OP_GRAD_L1
         f4 accR = {0.f, 0.f, 0.f, 0.f}, accI = {0.f, 0.f, 0.f, 0.f};
         group_cross<NW>(tile, opw, fo, lane, wave, nbw, accR, accI);
         if (code == OP_BACK) {
           if (opw[W_FLAGS] & F_BACK_PSI)
-            group_apply<2, NW>(tile, tbb, F, opw, fo, lane, wave, nbw);
+            group_apply<2, NW, true, 0>(tile, F, opw, fo, lane, wave, nbw);
           else
-            group_apply<1, NW>(tile, tbl, F, opw, fo, lane, wave, nbw);
+            group_apply<1, NW, true, 1>(tile, F, opw, fo, lane, wave, nbw);
         }
         // Cross-wave sum of the partial-trace entries of N, pre-scaled by the sample's rho / scale^2, in 2^-32
         // fixed point with 64-bit LDS atomics into this op's own region (no barrier, no tail: the regions are
@@ -456,14 +544,14 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
         // are bitwise independent of the order the waves (and, in hea_grad_reduce, samples and tiles) arrive.
         // Lane (g4, cl) holds N[4 g4 + i][cl]; entry slot: b == a -> b, b ^ a == e_j -> 16 + 16 j + b.
         const double sc = (double)rsc[CMAX] * FIX;
-        unsigned long long* rg = red64 + ngrad * 160;
+        unsigned long long* rg = red64 + ngrad * RSTR;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15, d = bb ^ aa;
           if (__builtin_popcount(d) <= 1) {
             const int e = d == 0 ? (int)bb : 16 + 16 * (__builtin_ctz(d)) + (int)bb;
-            atomicAdd(&rg[e], (unsigned long long)__double2ll_rn((double)accR[i] * sc));
-            atomicAdd(&rg[80 + e], (unsigned long long)__double2ll_rn((double)accI[i] * sc));
+            atomicAdd(&rg[red_slot(e)], (unsigned long long)__double2ll_rn((double)accR[i] * sc));
+            atomicAdd(&rg[RIM + red_slot(e)], (unsigned long long)__double2ll_rn((double)accI[i] * sc));
           }
         }
         if (tid == 0) {
@@ -494,10 +582,12 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
             fsum += sg ? -rsc[c] : rsc[c];
           }
         }
-        const float2 v = unpack_h2(psi_t[w]);
-        lam_t[w] = pack_h2(fsum * v.x, fsum * v.y);
+        uint2 pl = *(const uint2*)&tile[2 * w];   // (psi, lambda) pair of word w
+        const float2 v = unpack_h2(pl.x);
+        pl.y = pack_h2(fsum * v.x, fsum * v.y);
+        *(uint2*)&tile[2 * w] = pl;
       }
-    } else if (code == OP_READOUT) {
+    } else if (!ADJ && code == OP_READOUT) {
       uint32_t om[CMAX], sgn0 = 0;
 #pragma unroll
       for (int c = 0; c < CMAX; ++c) {
@@ -544,20 +634,20 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
   if (ADJ) {   // partial traces: thread (op, j, y, x, comp) sums the 8 entries with b_j = y, a_j = x
     for (int e = tid; e < ngrad * 32; e += NT) {
       const int g = e >> 5, r = e & 31, j = r >> 3, y = (r >> 2) & 1, x = (r >> 1) & 1, comp = r & 1;
-      const unsigned long long* rg = red64 + g * 160 + comp * 80;
+      const unsigned long long* rg = red64 + g * RSTR + comp * RIM;
       unsigned long long v = 0ull;
       if (j < gops[2 * g + 1]) {
         const int lowm = (1 << j) - 1;
         for (int o8 = 0; o8 < 8; ++o8) {    // the other three bits of b
           const int bb = ((o8 & ~lowm) << 1) | (o8 & lowm) | (y << j);
-          v += rg[x == y ? bb : 16 + 16 * j + bb];
+          v += rg[red_slot(x == y ? bb : 16 + 16 * j + bb)];
         }
       }
       a.gslab[(((size_t)s * a.slab_tiles + tile_id) * a.n_gradops + gops[2 * g]) * 32 + r] = (long long)v;
     }
   }
-  if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
-  if (ADJ && a.store_lam) store_tile<NT>(a, a.lam_out + (size_t)s * N, lam_t, tid, T, h_q, fixed);
+  if (!ADJ && a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
+  if (ADJ && a.store_lam) store_lam_il<NT>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
   lds_barrier();
   HEA_MARK();
 #undef HEA_MARK

