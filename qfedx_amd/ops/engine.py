@@ -186,6 +186,18 @@ class VQCEngine:
         P = spec.n_theta
         with torch.no_grad():
             rows = psi = None
+            if (method == "adjoint" and self.backend == "mps" and self.prog.autograd_ok and init is None):
+                # one recorded MPS contraction: readout now, reverse-mode pull-back of dL/d<Z> below
+                rows = self._rows(xang, th)
+                zt, back = self.prog.expz_vjp(rows, spec.readout)
+                expz = self._readout(zt.reshape(K, B, -1).float(), readout_keys, step)
+                loss, w, ga, gb, correct = ce_readout(expz, y, wmask, a, b)
+                if self.noise is not None:
+                    w = w * (1.0 - self.noise.p01 - self.noise.p10)
+                gg = back(w.reshape(K * B, -1))
+                gs = slot_grads(gg, self.ops, self.coef, self.n_slots)[:, :P]
+                gth = gs.reshape(K, B, P).sum(1).float()
+                return {"loss": loss, "grad": torch.cat([gth, ga, gb], -1), "correct": correct, "expz": expz}
             if method == "adjoint":          # torch backend: keep psi for the reverse sweep
                 rows = self._rows(xang, th)
                 psi = self.prog.run(rows, state=self._init_rows(init))

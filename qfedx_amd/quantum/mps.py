@@ -41,9 +41,11 @@ from typing import List, Optional
 import torch
 
 from ..ops.statevec_torch import CX, CZ, PAULI, RX, RY, RZ, P, _u1, gate_angles
+from .circuit import gate_matrix, KIND
 
 _U_OF = {CX: ((0, 1), (1, 0)), CZ: ((1, 0), (0, -1))}
 _SUPPORTED = set(range(13)) | {PAULI, CX, CZ}      # every 1-qubit kind of the IR, CX, CZ (SWAP lowers to CX)
+_NAME = {v: k for k, v in KIND.items()}
 
 
 class MPS:
@@ -163,7 +165,6 @@ class MPSProgram:
         self.raw_bond = 1 << max(raw, default=0)
         self.exact = self.exact_bond <= self.chi_max          # no singular value is ever dropped
         self.autograd_ok = self.raw_bond <= self.chi_max      # no recompression at all: pure einsum network
-        self._ad = False
 
     # ------------------------------------------------------------------ interface of TorchProgram
     def initial_state(self, B: int) -> MPS:
@@ -178,23 +179,78 @@ class MPSProgram:
         return MPS.from_dense(state.to(self.device, self.dtype), self.chi_max, self.cutoff)
 
     def run(self, params: torch.Tensor, state=None, ang: Optional[torch.Tensor] = None) -> MPS:
+        """Whole program: every 1-qubit gate matrix is built at once ([B, G, 2, 2], a few vectorised ops per
+        gate kind), runs of 1-qubit gates on a qubit are multiplied together and contracted into its site
+        only when a two-qubit gate needs it (or at the end), so the MPS sees ~one contraction per qubit and
+        layer plus the two-qubit MPOs."""
         ang = self.angles(params) if ang is None else ang
         st = self.initial_state(ang.shape[0]) if state is None else self._as_mps(state)
-        for g in range(len(self.ops_list)):
-            st = self.apply_gate(st, g, ang[:, g])
+        M = self._gate_mats(ang)
+        pend = {}
+
+        def flush(q):
+            m = pend.pop(q, None)
+            if m is not None:
+                t = list(st.tensors)
+                t[q] = torch.einsum("bij,bljr->blir", m, t[q])
+                return MPS(t, st.trunc_err, st.n_trunc)
+            return st
+
+        for g, (kind, q0, q1, _) in enumerate(self.ops_list):
+            if kind in (CX, CZ):
+                st = flush(q0)
+                st = flush(q1)
+                st = self._two(st, q0, q1, kind)
+            else:
+                m = M[:, g]
+                pend[q0] = m if q0 not in pend else torch.matmul(m, pend[q0])
+        for q in list(pend):
+            st = flush(q)
         return st
+
+    def _gate_mats(self, ang: torch.Tensor) -> torch.Tensor:
+        """[B, G, 2, 2] matrices of the program's 1-qubit gates (identity at two-qubit gates)."""
+        B, G = ang.shape
+        dt, dev = self.dtype, ang.device
+        if not hasattr(self, "_kind_idx"):
+            groups = {}
+            for g, (kind, _, _, _) in enumerate(self.ops_list):
+                if kind not in (CX, CZ):
+                    groups.setdefault(kind, []).append(g)
+            self._kind_idx = {k: torch.tensor(v, dtype=torch.long) for k, v in groups.items()}
+        M = torch.zeros(B, G, 2, 2, dtype=dt, device=dev)
+        for kind, idx in self._kind_idx.items():
+            idx = idx.to(dev)
+            a = ang[:, idx].to(self.rdtype)
+            if kind in (RX, RY, RZ, P, PAULI):
+                c, sn = torch.cos(a / 2).to(dt), torch.sin(a / 2).to(dt)
+                if kind == RX:
+                    m = torch.stack([torch.stack([c, -1j * sn], -1), torch.stack([-1j * sn, c], -1)], -2)
+                elif kind == RY:
+                    m = torch.stack([torch.stack([c, -sn], -1), torch.stack([sn, c], -1)], -2)
+                elif kind == RZ:
+                    em, ep = torch.exp(-0.5j * a.to(dt)), torch.exp(0.5j * a.to(dt))
+                    z = torch.zeros_like(em)
+                    m = torch.stack([torch.stack([em, z], -1), torch.stack([z, ep], -1)], -2)
+                elif kind == P:
+                    one, e = torch.ones_like(c), torch.exp(1j * a.to(dt))
+                    z = torch.zeros_like(e)
+                    m = torch.stack([torch.stack([one, z], -1), torch.stack([z, e], -1)], -2)
+                else:   # per-sample trajectory Pauli 0/1/2/3 = I/X/Y/Z
+                    ch = torch.round(a).long()
+                    i_, x_, y_, z_ = ((ch == v).to(dt) for v in range(4))
+                    m = torch.stack([torch.stack([i_ + z_, x_ - 1j * y_], -1),
+                                     torch.stack([x_ + 1j * y_, i_ - z_], -1)], -2)
+            else:
+                m = torch.as_tensor(gate_matrix(_NAME[kind]), dtype=dt, device=dev).expand(B, len(idx), 2, 2)
+            M[:, idx] = m
+        return M
 
     def apply_gate(self, st, g: int, ang: torch.Tensor, inverse: bool = False) -> MPS:
         st = self._as_mps(st)
         kind, q0, q1, _ = self.ops_list[g]
         if kind in (CX, CZ):
-            st = self._controlled(st, q0, q1, kind)
-            b = st.bonds()
-            # over chi_max: truncate.  Over a cut's Schmidt cap: lossless trim (skipped while differentiating
-            # so that the autograd graph holds no QR/SVD)
-            if max(b, default=1) > self.chi_max or (not self._ad and any(x > c for x, c in zip(b, self.cap))):
-                st = self.compress(st)
-            return st
+            return self._two(st, q0, q1, kind)
         u = _u1(kind, ang.to(self.rdtype), self.dtype)
         if inverse:
             u = (u[0].conj(), u[2].conj(), u[1].conj(), u[3].conj())
@@ -202,6 +258,16 @@ class MPSProgram:
         t = list(st.tensors)
         t[q0] = torch.einsum("bij,bljr->blir", m, t[q0])
         return MPS(t, st.trunc_err, st.n_trunc)
+
+    def _two(self, st: MPS, q0: int, q1: int, kind: int) -> MPS:
+        st = self._controlled(st, q0, q1, kind)
+        b = st.bonds()
+        # over chi_max: truncate.  Programs whose raw MPO bond fits chi_max are never recompressed: their
+        # forward stays a pure einsum network (no QR/SVD, no host syncs, differentiable); otherwise bonds
+        # above a cut's Schmidt cap are trimmed losslessly in the same sweep that truncates
+        if max(b, default=1) > self.chi_max or (not self.autograd_ok and any(x > c for x, c in zip(b, self.cap))):
+            st = self.compress(st)
+        return st
 
     # ------------------------------------------------------------------ two-qubit gates as bond-2 MPOs
     def _controlled(self, st: MPS, c: int, t_: int, kind: int) -> MPS:
@@ -284,18 +350,26 @@ class MPSProgram:
         when the bond bound fits ``chi_max``; parameter shift otherwise."""
         if not self.autograd_ok or init is not None:
             return self.param_shift_grads(params, w, readout, init=init)
-        self._ad = True
-        try:
-            with torch.enable_grad():
-                ang = self.angles(params).detach().requires_grad_(True)
-                st = self.run(params, ang=ang)
-                z = self.expz(st, readout)
-                (z * w.to(z.dtype)).sum().backward()
-        finally:
-            self._ad = False
-        g = ang.grad
-        mask = torch.tensor([s >= 0 and k in (RX, RY, RZ, P) for k, _, _, s in self.ops_list], device=g.device)
-        return torch.where(mask, g, torch.zeros_like(g))
+        return self.expz_vjp(params, readout)[1](w)
+
+    def expz_vjp(self, params: torch.Tensor, readout):
+        """One recorded forward: -> (<Z> [B, C] detached, back(w) -> dL/d(angle_g) [B, G]).  A training step
+        computes dL/d<Z> from the returned readout and pulls it back through the same network, so the MPS
+        is contracted once per step (requires ``autograd_ok``: no QR/SVD in the graph)."""
+        if not self.autograd_ok:
+            raise RuntimeError("expz_vjp needs a program whose raw MPO bond fits chi_max")
+        with torch.enable_grad():
+            ang = self.angles(params).detach().requires_grad_(True)
+            z = self.expz(self.run(params, ang=ang), readout)
+
+        def back(w: torch.Tensor) -> torch.Tensor:
+            z.backward(w.to(z.dtype))
+            g = ang.grad
+            mask = torch.tensor([s >= 0 and k in (RX, RY, RZ, P) for k, _, _, s in self.ops_list],
+                                device=g.device)
+            return torch.where(mask, g, torch.zeros_like(g))
+
+        return z.detach(), back
 
     @torch.no_grad()
     def param_shift_grads(self, params: torch.Tensor, w: torch.Tensor, readout, chunk: int = 16,
