@@ -329,7 +329,8 @@ def _pivots(vecs: list) -> list:
 # already swizzled.  Per pass H and per group the 4 non-pivot bits that become the 16 MFMA columns of
 # a block are searched so that the 32 lanes of each half-wave hit 32 distinct banks in all three
 # access patterns of a group op: apply reads (columns x m-bit 2), apply writes (columns x m-bit 1) and
-# cross-matrix reads (m bits 0..3 x column bit 2).
+# cross-matrix reads (m bits 0..3 x column bit 2), and so that the adjoint's b64 pair stores (16-lane
+# groups) hit distinct bank pairs.
 def _hmul(H, x: int) -> int:
     r = 0
     for b, row in enumerate(H):
@@ -386,8 +387,14 @@ def _group_geom(plan: HEAPlan, p: Pass, g: Group):
     return allv, rfull, rt, off, nonpiv, bits, dirs
 
 
+FULL_SCORE = 4
+
+
 def _best_cols(H, allv, dirs):
-    """(score, (c0, c1, c2, c3)): column bits maximising conflict-free access patterns (3 = all)."""
+    """(score, (c0, c1, c2, c3)): column bits maximising conflict-free access patterns (FULL_SCORE = all):
+    apply reads, forward b32 apply writes, cross-matrix reads, and the adjoint's ds_write_b64 pair stores,
+    whose lane groups are 16 contiguous lanes (one row, 16 columns) with bank (byte / 4) mod 32, i.e. the
+    16 columns need distinct swizzled pair indices mod 16."""
     bv = [_bank(H, v) for v in allv]
     bd = {b: _bank(H, d) for b, d in dirs.items()}
     best = (-1, None)
@@ -396,13 +403,14 @@ def _best_cols(H, allv, dirs):
         cb = [bd[b] for b in combo]
         sa = int(_rank(cb + [bv[2]]) == 5)
         sw = int(_rank(cb + [bv[1]]) == 5)
+        s16 = int(_rank([x & 15 for x in cb]) == 4)
         for c2 in combo:
             sg = int(_rank(bv + [bd[c2]]) == 5)
-            sc = sa + sw + sg
+            sc = sa + sw + sg + s16
             if sc > best[0]:
                 rest = [b for b in combo if b != c2]
                 best = (sc, (rest[0], rest[1], c2, rest[2]))
-                if sc == 3:
+                if sc == FULL_SCORE:
                     return best
     return best
 
@@ -423,7 +431,7 @@ def layout_pass(plan: HEAPlan, p: Pass, seed: int = 0, tries: int = 48) -> None:
             score += sc
         if best is None or score > best[0]:
             best = (score, H, cols)
-        if score == 3 * len(groups):
+        if score == FULL_SCORE * len(groups):
             break
     p.H = best[1]
     p.cols = {(g.layer, tuple(g.qubits)): c for g, c in zip(groups, best[2])}
