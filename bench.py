@@ -52,29 +52,9 @@ def timed_rounds(cfg, device, backend, world, warmup: int, steps: int):
     return runner, max_over_ranks(dt, world)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--qubits", type=int, default=16)
-    ap.add_argument("--layers", type=int, default=3)
-    ap.add_argument("--clients", type=int, default=64)
-    ap.add_argument("--batch", type=int, default=32)
-    ap.add_argument("--local-steps", type=int, default=1)
-    ap.add_argument("--classes", type=int, default=3)
-    ap.add_argument("--dp", action="store_true")
-    ap.add_argument("--backend", default="auto")
-    ap.add_argument("--device", default="auto")
-    ap.add_argument("--engine", default="mfma", choices=["mfma", "valu"],
-                    help="mfma: fp16-state MFMA group-unitary engine (ops/hea_mfma.py); valu: fp32 pass engine")
-    args = ap.parse_args()
-
-    import torch
+def make_config(args):
+    """The bench's experiment config (BASELINE.json headline: 16-qubit VQC x 64 clients, synthetic non-IID)."""
     from qfedx_amd.config import ExperimentConfig
-    from qfedx_amd.api import setup
-    from qfedx_amd.parallel.dist import shutdown
-
     cfg = ExperimentConfig(name="bench")
     cfg.data.dataset = "synthetic"
     cfg.data.num_clients = args.clients
@@ -98,6 +78,32 @@ def main():
     cfg.privacy.noise_multiplier = 1.0
     cfg.runtime.backend = args.backend
     cfg.runtime.device = args.device
+    return cfg
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--qubits", type=int, default=16)
+    ap.add_argument("--layers", type=int, default=3)
+    ap.add_argument("--clients", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--local-steps", type=int, default=1)
+    ap.add_argument("--classes", type=int, default=3)
+    ap.add_argument("--dp", action="store_true")
+    ap.add_argument("--backend", default="auto")
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--engine", default="mfma", choices=["mfma", "valu"],
+                    help="mfma: fp16-state MFMA group-unitary engine (ops/hea_mfma.py); valu: fp32 pass engine")
+    args = ap.parse_args()
+
+    import torch
+    from qfedx_amd.api import setup
+    from qfedx_amd.parallel.dist import shutdown
+
+    cfg = make_config(args)
     device, backend, world = setup(cfg)
     runner, dt = timed_rounds(cfg, device, backend, world, args.warmup, args.steps)
     ev = runner.evaluate()

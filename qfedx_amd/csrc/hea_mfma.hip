@@ -711,28 +711,46 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
 // Per client and gradient op: exact int64 sums of the 32 partial-trace slots over the client's samples and
 // the op's tiles, then per real qubit j (slots 8j + 4y + 2x + comp = n_j[y][x].(re, im))
 //   d/dtheta = Im(e^{-i phi} n10 + e^{i phi} n01),   d/dphi = Im(n00 - n11).
-__global__ void __launch_bounds__(64) hea_grad_reduce_kernel(const long long* __restrict__ gslab, int slab_tiles,
-                                                             int n_gradops, const int* __restrict__ gmeta, int spc,
-                                                             const float* __restrict__ params,
-                                                             float* __restrict__ grad, int p_stride) {
-  const int k = blockIdx.x, g = blockIdx.y, lane = threadIdx.x;
+__global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* __restrict__ gslab, int slab_tiles,
+                                                              int n_gradops, const int* __restrict__ gmeta, int spc,
+                                                              const float* __restrict__ params,
+                                                              float* __restrict__ grad, int p_stride) {
+  // 8 groups of 32 lanes split the client's (sample, tile) rows; 4 independent loads in flight per lane; the
+  // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
+  const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
   const int* m = gmeta + g * 10;
   const int nt = m[0], nreal = m[1];
+  const int R = spc * nt;
+  __shared__ long long part[8][32];
   __shared__ double pt[32];
-  if (lane < 32) {
-    long long acc = 0;
-    for (int s = k * spc; s < (k + 1) * spc; ++s)
-      for (int t = 0; t < nt; ++t) acc += gslab[(((size_t)s * slab_tiles + t) * n_gradops + g) * 32 + lane];
-    pt[lane] = (double)acc / FIX;
+  long long acc[4] = {0, 0, 0, 0};
+  auto row = [&](int r) -> long long {
+    const int s = k * spc + r / nt, t = r % nt;
+    return gslab[(((size_t)s * slab_tiles + t) * n_gradops + g) * 32 + lane];
+  };
+  int r = grp;
+  for (; r + 24 < R; r += 32) {
+    acc[0] += row(r);
+    acc[1] += row(r + 8);
+    acc[2] += row(r + 16);
+    acc[3] += row(r + 24);
+  }
+  for (; r < R; r += 8) acc[0] += row(r);
+  part[grp][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (tid < 32) {
+    long long v = 0;
+    for (int j = 0; j < 8; ++j) v += part[j][tid];
+    pt[tid] = (double)v / FIX;
   }
   __syncthreads();
-  if (lane < nreal) {
-    const double* p = pt + 8 * lane;
+  if (tid < nreal) {
+    const double* p = pt + 8 * tid;
     const float* prm = params + (size_t)k * p_stride;
-    const double ph = prm[m[6 + lane]];
+    const double ph = prm[m[6 + tid]];
     const double cp = cos(ph), sp = sin(ph);
-    grad[(size_t)k * p_stride + m[2 + lane]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
-    grad[(size_t)k * p_stride + m[6 + lane]] = (float)(p[1] - p[7]);
+    grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
+    grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
   }
 }
 
@@ -761,7 +779,7 @@ extern "C" int qfx_hea_frags(const float* params, int p_stride, const int* slot_
 extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc,
                                    int K, const float* params, float* grad, int p_stride, hipStream_t st) {
   if (K == 0 || n_gradops == 0) return 0;
-  hipLaunchKernelGGL(hea::hea_grad_reduce_kernel, dim3(K, n_gradops), dim3(64), 0, st, gslab, slab_tiles, n_gradops,
+  hipLaunchKernelGGL(hea::hea_grad_reduce_kernel, dim3(K, n_gradops), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
                      gmeta, spc, params, grad, p_stride);
   return (int)hipGetLastError();
 }
