@@ -1,5 +1,9 @@
 """In-tree build of the native extension ``qfedx_amd._qfedx_C`` for gfx950 (MI355X).
 
+``QFEDX_DEBUG=1`` (or ``python -m qfedx_amd._build --debug``) builds the separate debug extension
+``qfedx_amd._qfedx_C_debug`` with device-side bounds checks (``csrc/qfx_check.h``) into ``build/qfx_debug``;
+``QFEDX_DEBUG=1`` at run time makes ``ops/_ext.py`` load it instead of the release one.
+
 Device code (``csrc/*.hip``) is compiled by ``hipcc --offload-arch=gfx950``; host bindings
 (``csrc/*.cpp``: planner + pybind11/torch glue) by g++ against torch's headers; everything is linked
 by hipcc into one shared object next to this file, so it travels with the repo snapshot to the GPU
@@ -19,14 +23,19 @@ import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-BUILD = os.path.join(HERE, "..", "build", "qfx")
-EXT_NAME = "_qfedx_C"
 ARCH = os.environ.get("QFEDX_ARCH", "gfx950")
 
 
-def ext_path() -> str:
+def _mode(debug):
+    if debug is None:
+        debug = os.environ.get("QFEDX_DEBUG", "0") == "1"
+    return (os.path.join(HERE, "..", "build", "qfx_debug" if debug else "qfx"),
+            "_qfedx_C_debug" if debug else "_qfedx_C", bool(debug))
+
+
+def ext_path(debug=None) -> str:
     suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
-    return os.path.join(HERE, EXT_NAME + suffix)
+    return os.path.join(HERE, _mode(debug)[1] + suffix)
 
 
 def _torch_paths():
@@ -55,8 +64,10 @@ def _run(cmd):
     return r
 
 
-def build(verbose: bool = False, force: bool = False) -> str:
+def build(verbose: bool = False, force: bool = False, debug=None) -> str:
+    BUILD, EXT_NAME, dbg = _mode(debug)
     os.makedirs(BUILD, exist_ok=True)
+    checks = ["-DQFX_DEVICE_CHECKS=1"] if dbg else []
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     hips = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     cpps = sorted(glob.glob(os.path.join(CSRC, "*.cpp")))
@@ -78,14 +89,14 @@ def build(verbose: bool = False, force: bool = False) -> str:
         objs.append(obj)
         if stamps.get(obj) != key or not os.path.exists(obj):
             cmd = ["hipcc", "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
-                   "-munsafe-fp-atomics", "-I", CSRC, src, "-o", obj]
+                   "-munsafe-fp-atomics", *checks, "-I", CSRC, src, "-o", obj]
             jobs.append((obj, key, cmd))
     for src in cpps:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         key = _hash([src]) + hh + str(abi)
         objs.append(obj)
         if stamps.get(obj) != key or not os.path.exists(obj):
-            cmd = ["g++", "-c", "-fPIC", "-O2", "-std=c++17", *common_defs,
+            cmd = ["g++", "-c", "-fPIC", "-O2", "-std=c++17", *common_defs, *checks,
                    f"-DTORCH_EXTENSION_NAME={EXT_NAME}", "-DTORCH_API_INCLUDE_EXTENSION_H",
                    *[f"-I{p}" for p in inc], f"-I{py_inc}", f"-I{pybind11.get_include()}", "-I", CSRC,
                    src, "-o", obj]
@@ -100,7 +111,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
                 stamps[obj] = key
                 if verbose:
                     print("compiled", os.path.basename(obj))
-    out = ext_path()
+    out = ext_path(dbg)
     link_key = _hash(objs) if all(os.path.exists(o) for o in objs) else ""
     if jobs or stamps.get("__link__") != link_key or not os.path.exists(out):
         cmd = ["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
@@ -118,5 +129,5 @@ def build(verbose: bool = False, force: bool = False) -> str:
 
 
 if __name__ == "__main__":
-    p = build(verbose=True, force="--force" in sys.argv)
+    p = build(verbose=True, force="--force" in sys.argv, debug=True if "--debug" in sys.argv else None)
     print(p)

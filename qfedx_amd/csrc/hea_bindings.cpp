@@ -18,6 +18,7 @@ int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_
 int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc, int K,
                         const float* params, float* grad, int p_stride, hipStream_t st);
 int qfx_hea_args_size();
+int qfx_hea_check_status(hipStream_t st);
 }
 
 namespace {
@@ -40,6 +41,12 @@ T* dp(const torch::Tensor& t, torch::ScalarType dt, const char* name, int64_t mi
 
 void check(int rc, const char* what) {
   if (rc != 0) throw std::runtime_error(std::string(what) + " failed: " + std::to_string(rc));
+#if defined(QFX_DEVICE_CHECKS) && QFX_DEVICE_CHECKS
+  // debug build: every launch is followed by a read of the device-check status word
+  const int line = qfx_hea_check_status(cur());
+  if (line != 0)
+    throw std::runtime_error(std::string(what) + ": device check failed at hea_mfma.hip:" + std::to_string(line));
+#endif
 }
 
 // geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
@@ -167,4 +174,6 @@ void register_hea(pybind11::module& m) {
   m.def("hea_check_ops", &hea_check_ops);
   m.def("hea_grad_reduce", &hea_grad_reduce);
   m.def("hea_args_size", []() { return qfx_hea_args_size(); });
+  // -1: release build (no device checks); 0: no failure since the last read; else the failing source line
+  m.def("hea_check_status", []() { return qfx_hea_check_status(cur()); });
 }

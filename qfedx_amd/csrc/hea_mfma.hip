@@ -22,6 +22,11 @@
 #include <cstdint>
 
 #include "hea_args.h"
+#include "qfx_check.h"
+
+#if QFX_CHECKS_ON
+__device__ unsigned int qfx_check_word = 0;
+#endif
 
 namespace hea {
 
@@ -520,6 +525,24 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
     }
     const int code = opw[W_CODE];
     const int nreal = opw[W_NREAL];
+#if QFX_CHECKS_ON
+    QFX_DCHECK(code >= OP_APPLY && code <= OP_BACK);
+    if (code != OP_OBS && code != OP_READOUT) {
+      QFX_DCHECK(nreal >= 0 && nreal <= 4);
+      QFX_DCHECK((uint32_t)opw[W_OFF + (lane & 15)] < (uint32_t)T);
+      QFX_DCHECK((uint32_t)opw[W_BL + (lane & 31)] < (uint32_t)T);
+      QFX_DCHECK((uint32_t)opw[W_BH + (lane & 31)] < (uint32_t)T);
+      // -1 = no unitary (cross-matrix-only gradient ops); every op that applies one names a fragment
+      QFX_DCHECK(fidx_s[o] >= -1 && fidx_s[o] < 4 * a.n_slots);
+      QFX_DCHECK(fidx_s[o] >= 0 || code == OP_GRAD || code == OP_GRAD_L1);
+      if (ADJ && code != OP_APPLY && code != OP_UNAPPLY_PSI && code != OP_UNAPPLY_LAM) {
+        QFX_DCHECK(opw[W_GIDX] >= 0 && opw[W_GIDX] < a.n_gradops);
+        QFX_DCHECK(ngrad < MAXGRAD);
+      }
+    } else {
+      QFX_DCHECK(nreal >= 1 && nreal <= a.C);
+    }
+#endif
     if (code == OP_APPLY || code == OP_UNAPPLY_PSI || code == OP_UNAPPLY_LAM || code == OP_BACK ||
         code == OP_GRAD || code == OP_GRAD_L1) {
       int fpb = 0;
@@ -631,6 +654,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
   }
   lds_barrier();
   HEA_MARK();
+  QFX_DCHECK(!ADJ || tile_id < a.slab_tiles);
   if (ADJ) {   // partial traces: thread (op, j, y, x, comp) sums the 8 entries with b_j = y, a_j = x
     for (int e = tid; e < ngrad * 32; e += NT) {
       const int g = e >> 5, r = e & 31, j = r >> 3, y = (r >> 2) & 1, x = (r >> 1) & 1, comp = r & 1;
@@ -785,3 +809,18 @@ extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n
 }
 
 extern "C" int qfx_hea_args_size() { return (int)sizeof(hea::PassArgs); }
+
+// Debug build: synchronise the stream and return (and clear) the first failed device-check line, 0 if none;
+// -1 in the release build (no checks compiled).
+extern "C" int qfx_hea_check_status(hipStream_t st) {
+#if QFX_CHECKS_ON
+  if (hipStreamSynchronize(st) != hipSuccess) return -2;
+  unsigned int v = 0, z = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(qfx_check_word), sizeof(v)) != hipSuccess) return -2;
+  if (v && hipMemcpyToSymbol(HIP_SYMBOL(qfx_check_word), &z, sizeof(z)) != hipSuccess) return -2;
+  return (int)v;
+#else
+  (void)st;
+  return -1;
+#endif
+}
