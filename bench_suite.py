@@ -36,6 +36,8 @@ SUITE = {
                        "client local-steps/sec (16-qubit VQC x 64 clients, fp16 MFMA engine)", None),
     "vqc20q_dp64_mfma": ("configs/baseline3_20q_dp_64clients.yaml", ["model.state_dtype=mfma"],
                          "client local-steps/sec (20-qubit VQC x 64 non-IID clients, DP, fp16 MFMA engine)", None),
+    "vqc48q_mps64": ("configs/mps_48q_64clients.yaml", [],
+                     "client local-steps/sec (48-qubit VQC x 64 clients, MPS tensor-network backend)", None),
     "vqc4q_2_cpu": ("configs/baseline1_4q_2clients_cpu.yaml", ["train.local_steps=1"],
                     "client local-steps/sec (4-qubit VQC x 2 clients, CPU gloo)", None),
 }
