@@ -24,13 +24,13 @@ SUITE = {
                 "client local-steps/sec (CFed TinyCNN x 128 clients, batch 32)", 258.0),
     "cfed128_epoch": ("configs/baseline4_cfed_128clients.yaml", [],
                       "client local-steps/sec (CFed TinyCNN x 128 clients, 1 local epoch)", 258.0),
-    "vqc20q_dp64": ("configs/baseline3_20q_dp_64clients.yaml", [],
+    "vqc20q_dp64": ("configs/baseline3_20q_dp_64clients.yaml", ["model.state_dtype=fp32"],
                     "client local-steps/sec (20-qubit VQC x 64 non-IID clients, DP)", None),
-    "vqc24q_ps256": ("configs/baseline5_24q_256clients_paramshift_shots.yaml", [],
+    "vqc24q_ps256": ("configs/baseline5_24q_256clients_paramshift_shots.yaml", ["model.state_dtype=fp32"],
                      "client local-steps/sec (24-qubit VQC x 256 clients, param-shift + shots)", None),
     "vqc16q_bf16_8": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1"],
                       "client local-steps/sec (16-qubit VQC bf16 state x 8 clients)", None),
-    "vqc16q_64": ("configs/headline_16q_64clients.yaml", [],
+    "vqc16q_64": ("configs/headline_16q_64clients.yaml", ["model.state_dtype=fp32"],
                   "client local-steps/sec (16-qubit VQC x 64 clients federated rounds)", None),
     "vqc16q_64_mfma": ("configs/headline_16q_64clients.yaml", ["model.state_dtype=mfma"],
                        "client local-steps/sec (16-qubit VQC x 64 clients, fp16 MFMA engine)", None),
@@ -80,7 +80,8 @@ def main():
             "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(value / ref, 2) if ref else None,
             "dtype": {"bf16": "bf16-state/fp32-compute", "mfma": "fp16-state/fp32-accumulate (MFMA)",
-                      "fp16": "fp16-state/fp32-accumulate (MFMA)"}.get(cfg.model.state_dtype, "fp32"),
+                      "fp16": "fp16-state/fp32-accumulate (MFMA)"}.get(
+                          getattr(runner.adapter, "state_dtype", cfg.model.state_dtype), "fp32"),
             "data": "synthetic non-IID client shards, random init", "rounds_per_sec": round(args.steps / dt, 4),
             "samples_per_sec": round(value * t.batch_size, 1), "backend": backend,
             "test_acc_after": round(ev["test_acc"], 4),

@@ -46,7 +46,8 @@ class ModelConfig:
     entangler: str = "chain"            # chain | ring | none
     readout_scale: float = 1.0          # initial a in logit = a<Z> + b
     init_std: float = 0.1
-    state_dtype: str = "fp32"           # fp32 | bf16 (VALU pass engine storage) | mfma (fp16 MFMA engine)
+    state_dtype: str = "auto"           # auto (mfma when eligible on HIP, else fp32) | fp32 | bf16 (VALU pass
+                                        # engine storage) | mfma (fp16 MFMA engine, hardware-efficient ansatz)
     simulator: str = "statevector"      # statevector | mps (tensor network past statevector memory)
     mps_chi: int = 64                   # MPS bond-dimension cap (exact while the circuit's bound fits)
 

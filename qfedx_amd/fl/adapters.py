@@ -15,6 +15,18 @@ from ..ops.engine import VQCEngine
 from .trainer import VQCClientTrainer
 
 
+def resolve_state_dtype(state_dtype: str, spec, backend: str, noise) -> str:
+    """``auto``: the fp16 MFMA engine (ops/hea_mfma.py) on the HIP backend for the specs it covers (CNOT-chain
+    or no entangler, angle features, >= 8 qubits, no noise model), the fp32 VALU pass engine otherwise."""
+    if state_dtype != "auto":
+        return state_dtype
+    if backend == "hip" and noise is None:
+        from ..ops.hea_plan import eligible
+        if eligible(spec):
+            return "mfma"
+    return "fp32"
+
+
 class VQCAdapter:
     def __init__(self, cfg, device, backend: str):
         m = cfg.model
@@ -27,7 +39,8 @@ class VQCAdapter:
         if sim not in ("statevector", "mps"):
             raise ValueError(f"model.simulator must be statevector or mps, got '{sim}'")
         # the circuit engine follows model.simulator; optimizer / aggregation kernels follow the runtime backend
-        self.engine = VQCEngine(self.spec, device, "mps" if sim == "mps" else backend, m.state_dtype,
+        self.state_dtype = resolve_state_dtype(m.state_dtype, self.spec, backend, self.noise)
+        self.engine = VQCEngine(self.spec, device, "mps" if sim == "mps" else backend, self.state_dtype,
                                 noise=self.noise, mps_chi=int(getattr(m, "mps_chi", 64)))
         self.trainer = VQCClientTrainer(self.spec, self.engine, cfg.train, device, backend)
         # QR/SVD recompression is data dependent: the MPS round runs eagerly, not as a captured graph
