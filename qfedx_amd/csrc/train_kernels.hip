@@ -324,33 +324,47 @@ __global__ void qfx_delta_norm_final_kernel(const double* __restrict__ partial, 
 // out[e] = sum_k round(2^32 * w_k * priv(wrap(theta_k[e] - theta_g[e]))), out[P] = sum_k round(2^32 w_k)
 // Each client's term is rounded to fixed point BEFORE the sum: integer addition is associative, so the
 // aggregate is bitwise identical for any sharding of clients over GPUs (and equal to the CPU path).
-__global__ void qfx_fedavg_reduce_kernel(
+constexpr int FA_E = 32, FA_G = 8;   // fedavg reduce: parameters per block x client groups per block
+__global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
     const float* __restrict__ theta_k, const float* __restrict__ theta_g,
     const unsigned char* __restrict__ angle_mask, const double* __restrict__ weights,
     const double* __restrict__ norms, const uint32_t* __restrict__ keys, int K, int P, int wrap,
     int dp, float clip, float sigma, long long* __restrict__ out) {
+  // thread (group g, lane el): parameter e = block * FA_E + el, clients k = g, g + FA_G, ...; the FA_G integer
+  // partials are combined in LDS (exact, so the split changes no bit of the result)
+  __shared__ long long part[FA_G][FA_E];
   const double SC = 4294967296.0;
-  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e == 0) {
+  const int el = threadIdx.x % FA_E, grp = threadIdx.x / FA_E;
+  const long e = (long)blockIdx.x * FA_E + el;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     long long ws = 0;
     for (int k = 0; k < K; ++k) ws += llrint(weights[k] * SC);
     out[P] = ws;
   }
-  if (e >= P) return;
   long long acc = 0;
-  for (int k = 0; k < K; ++k) {
-    double d = (double)theta_k[(size_t)k * P + e] - (double)theta_g[e];
-    if (wrap && angle_mask[e]) d = wrap_pi(d);
-    if (dp) {
-      const double n = norms[k];
-      const double sc = fmin(1.0, (double)clip / fmax(n, 1e-12));
-      d = d * sc;
-      if (sigma > 0.f)
-        d += (double)sigma * (double)clip * (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
+  if (e < P) {
+    const double tg = (double)theta_g[e];
+    const bool wr = wrap && angle_mask[e];
+    for (int k = grp; k < K; k += FA_G) {
+      double d = (double)theta_k[(size_t)k * P + e] - tg;
+      if (wr) d = wrap_pi(d);
+      if (dp) {
+        const double n = norms[k];
+        const double sc = fmin(1.0, (double)clip / fmax(n, 1e-12));
+        d = d * sc;
+        if (sigma > 0.f)
+          d += (double)sigma * (double)clip * (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
+      }
+      acc += llrint(weights[k] * d * SC);
     }
-    acc += llrint(weights[k] * d * SC);
   }
-  out[e] = acc;
+  part[grp][el] = acc;
+  __syncthreads();
+  if (grp == 0 && e < P) {
+    long long v = 0;
+    for (int j = 0; j < FA_G; ++j) v += part[j][el];
+    out[e] = v;
+  }
 }
 
 // round epilogue 1: metrics -> exact fixed point in the all-reduce buffer tail, fixed summation order
@@ -570,7 +584,7 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                        wrap, partial);
     hipLaunchKernelGGL(qfx_delta_norm_final_kernel, dim3((K + 63) / 64), dim3(64), 0, st, partial, nc, K, norms);
   }
-  hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, st, theta_k, theta_g,
+  hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3((P + FA_E - 1) / FA_E), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
                      angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out);
   return (int)hipGetLastError();
 }
