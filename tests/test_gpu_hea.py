@@ -88,3 +88,24 @@ def test_hea_expz_eval_matches_dense_20q(cuda):
     np.testing.assert_allclose(gr.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
     z2 = prog.expz(x.to(cuda), params[:, : spec.n_theta].to(cuda))
     np.testing.assert_allclose(z2.cpu().numpy(), z.cpu().reshape(K, B, -1).numpy(), atol=1e-6)
+
+
+def test_hea_24q_three_passes_match_valu_engine(cuda):
+    """24 qubits: a three-pass plan (2^14-amplitude tiles, 1024 tiles per sample in the first pass) against
+    the fp32 VALU pass engine on the same inputs (a float64 dense oracle is too slow at this size)."""
+    spec = VQCSpec(24, 2, 3, readout_scale=2.0)
+    prog = HeaMfmaProgram(spec, cuda)
+    assert prog.n_passes == 3
+    K, B = 2, 2
+    x, params, wr = _inputs(spec, K, B, seed=7)
+    ref = VQCEngine(spec, cuda, "hip")
+    xx, th, ww = x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda)
+    z_ref = ref.expz(xx, th)
+    y = torch.randint(0, 3, (K, B), generator=torch.Generator().manual_seed(1)).to(cuda)
+    w = torch.full((K, B), 1.0 / B, device=cuda)
+    g_ref = ref.loss_and_grads(xx, y, w, params.to(cuda))["grad"]
+    z, _ = prog.vjp(xx, th, ww)
+    g = VQCEngine(spec, cuda, "hip", "mfma").loss_and_grads(xx, y, w, params.to(cuda))["grad"]
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(z.cpu().reshape(K, B, -1).numpy(), z_ref.cpu().numpy(), atol=3e-3)
+    np.testing.assert_allclose(g.cpu().numpy(), g_ref.cpu().numpy(), atol=3e-3)
