@@ -28,6 +28,9 @@ SUITE = {
                     "client local-steps/sec (20-qubit VQC x 64 non-IID clients, DP)", None),
     "vqc24q_ps256": ("configs/baseline5_24q_256clients_paramshift_shots.yaml", ["model.state_dtype=fp32"],
                      "client local-steps/sec (24-qubit VQC x 256 clients, param-shift + shots)", None),
+    "vqc24q_ps256_mfma": ("configs/baseline5_24q_256clients_paramshift_shots.yaml", ["model.state_dtype=mfma"],
+                          "client local-steps/sec (24-qubit VQC x 256 clients, param-shift + shots, fp16 MFMA engine)",
+                          None),
     "vqc16q_bf16_8": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1"],
                       "client local-steps/sec (16-qubit VQC bf16 state x 8 clients)", None),
     "vqc16q_64": ("configs/headline_16q_64clients.yaml", ["model.state_dtype=fp32"],

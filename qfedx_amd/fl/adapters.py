@@ -17,10 +17,11 @@ from .trainer import VQCClientTrainer
 
 def resolve_state_dtype(state_dtype: str, spec, backend: str, noise) -> str:
     """``auto``: the fp16 MFMA engine (ops/hea_mfma.py) on the HIP backend for the specs it covers (CNOT-chain
-    or no entangler, angle features, >= 8 qubits, no noise model), the fp32 VALU pass engine otherwise."""
+    or no entangler, angle features, >= 8 qubits, no gate noise; readout confusion and shots are applied by its
+    readout kernels), the fp32 VALU pass engine otherwise."""
     if state_dtype != "auto":
         return state_dtype
-    if backend == "hip" and noise is None:
+    if backend == "hip" and (noise is None or not noise.gate_noise):
         from ..ops.hea_plan import eligible
         if eligible(spec):
             return "mfma"
