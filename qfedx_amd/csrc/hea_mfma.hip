@@ -321,7 +321,7 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
   uint4 B0[NX], B1[NX];
   load(base[0], B0);
   if (nbw > 1) load(base[1], B1);
-  constexpr bool PREFETCH = NX == 1 || NW <= 8;   // the two-target form at 16 waves stays within 128 VGPRs
+  constexpr bool PREFETCH = true;
 #pragma unroll
   for (int p = 0; p < MAXB; p += 2) {
     if (p >= nbw) break;
@@ -378,13 +378,19 @@ __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw
   }
 }
 
-__device__ __forceinline__ void load_frags(const PassArgs& a, int k, int fi, int lane, uint4* F) {
-  if (fi < 0) return;
+// An op's unitary fragments (4 x 64 lanes x 16 B = 4 KB, contiguous in global memory) go to an LDS slot by
+// direct global -> LDS DMA (global_load_lds_dwordx4, 1 KB per wave-instruction, waves 0..3), issued one op
+// ahead: no VGPRs are held for the prefetch.  The LDS base of a wave-instruction is wave-uniform (M0); the
+// DMA is complete once the issuing wave has passed s_waitcnt vmcnt(0) (lds_barrier_dma).
+__device__ __forceinline__ void dma_frags(const PassArgs& a, int k, int fi, int tid, int wave, uint4* slot) {
+  if (fi < 0 || wave >= 4) return;
   const uint4* fr = (const uint4*)a.frags + ((size_t)k * a.n_slots * 4 + fi) * 128;
-  F[0] = fr[lane];
-  F[1] = fr[64 + lane];
-  F[2] = fr[128 + lane];
-  F[3] = fr[192 + lane];
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(fr + tid),
+                                   (__attribute__((address_space(3))) void*)(slot + 64 * wave), 16, 0, 0);
+}
+
+__device__ __forceinline__ void lds_barrier_dma() {
+  __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 template <bool ADJ>
@@ -394,6 +400,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
   __shared__ __attribute__((aligned(16))) uint32_t tile[(ADJ ? 2 : 1) << TMAX];
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
   __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
+  __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];   // op unitary fragments, double buffered
   __shared__ float red[NW * CMAX];
   // per gradient op of the pass: the 80 cross-matrix entries a partial trace can use (b = a, and b = a ^ e_j),
   // x (re, im), in 2^-32 fixed point; turned into partial traces once, at the end of the pass
@@ -507,21 +514,24 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
   if (tid < a.nops) fidx_s[tid] = a.fidx[tid];   // LDS copy: the prefetch below never waits on a global load
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
-  uint4 FN[4] = {};
-  if (a.nops > 0) load_frags(a, k, a.fidx[0], lane, FN);
-  lds_barrier();
+  if (a.nops > 0) dma_frags(a, k, a.fidx[0], tid, wave, frag_s[0]);
+  lds_barrier_dma();
   HEA_MARK();
   for (int o = 0; o < a.nops; ++o) {
-    // op o's record was written during op o - 1; the other buffer was last read by op o - 1, which every
-    // wave has finished at this barrier, so op o + 1's record is written into it right away
-    lds_barrier();
+    // op o's record and fragments were written during op o - 1; the other buffers were last read at the
+    // start of op o - 1, which every wave has finished at this barrier, so op o + 1's go there right away
+    lds_barrier_dma();
     HEA_MARK();
     const int* opw = opw2[o & 1];
-    const uint4 F[4] = {FN[0], FN[1], FN[2], FN[3]};
+    uint4 F[4];
+    if (fidx_s[o] >= 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) F[i] = frag_s[o & 1][64 * i + lane];
+    }
     if (o + 1 < a.nops) {
       if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
       if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
-      load_frags(a, k, fidx_s[o + 1], lane, FN);
+      dma_frags(a, k, fidx_s[o + 1], tid, wave, frag_s[(o + 1) & 1]);
     }
     const int code = opw[W_CODE];
     const int nreal = opw[W_NREAL];
