@@ -174,7 +174,18 @@ def eligible(spec) -> bool:
 
 
 def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
-               tile_bits: int = TILE_BITS, swizzle: bool = True) -> HEAPlan:
+               tile_bits: int = TILE_BITS, swizzle: bool = True, trim=None) -> HEAPlan:
+    """Plan the passes.  ``trim=None`` builds both the greedy plan (every ready rotation joins the current
+    pass) and the trimmed plan (a non-final pass defers each layer's ragged tail so its groups are full
+    4-qubit unitaries) and keeps the one with fewer passes, then fewer group ops: for 16q x 3L the trimmed
+    plan runs 8 group ops instead of 10 in the same two passes."""
+    if trim is None:
+        cands = [build_plan(n, L, readout, chain, feature, tile_bits, False, tr) for tr in (False, True)]
+        best = min(cands, key=lambda pl: (len(pl.passes), sum(len(p.groups) for p in pl.passes), not trim))
+        if swizzle:
+            for j, p in enumerate(best.passes):
+                layout_pass(best, p, seed=j)
+        return best
     t = min(tile_bits, n)
     if t < GROUP + 4:
         raise ValueError("the MFMA engine needs at least 8 tile qubits (16 columns per MFMA block)")
@@ -209,6 +220,8 @@ def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
         for o in remaining:
             if (sup[o] & ~tm) == 0 and all(d in done or d in taken for d in preds[o]):
                 taken.append(o)
+        if trim and len(taken) < len(remaining):
+            taken = _trim_ragged(taken, preds)
         if not taken and remaining:
             raise RuntimeError(f"pass planner stuck at {len(passes)} passes (n={n}, L={L}, t={t})")
         for o in taken:
@@ -258,6 +271,31 @@ def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
         for j, p in enumerate(passes):
             layout_pass(plan, p, seed=j)
     return plan
+
+
+def _trim_ragged(taken: list, preds: dict) -> list:
+    """Drop each layer's highest rotations until every layer's count is a multiple of GROUP, together with
+    every taken rotation that depends on a dropped one.  Falls back to ``taken`` if nothing would be left."""
+    keep = list(taken)
+    while True:
+        by_layer = {}
+        for o in keep:
+            by_layer.setdefault(o[0], []).append(o)
+        drop = set()
+        for layer, os_ in by_layer.items():
+            r = len(os_) % GROUP
+            if r:
+                drop.update(sorted(os_, key=lambda o: o[1])[-r:])
+        if not drop:
+            return keep if keep else list(taken)
+        changed = True
+        while changed:
+            changed = False
+            for o in keep:
+                if o not in drop and any(d in drop for d in preds[o]):
+                    drop.add(o)
+                    changed = True
+        keep = [o for o in keep if o not in drop]
 
 
 # ---------------------------------------------------------------------------------------- op tables

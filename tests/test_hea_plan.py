@@ -22,7 +22,9 @@ def _dense(spec, xang, params, wread):
 
 
 @pytest.mark.parametrize("n,L,t,chain,feat", [(8, 2, 8, True, "ry"), (10, 3, 8, True, "ry"), (10, 3, 14, True, "rx"),
-                                              (11, 2, 8, False, "ry"), (12, 4, 9, True, "ry"), (9, 1, 8, True, "rz")])
+                                              (11, 2, 8, False, "ry"), (12, 4, 9, True, "ry"), (9, 1, 8, True, "rz"),
+                                              # trimmed plans (ragged layer tails deferred to a later pass)
+                                              (11, 2, 10, True, "ry"), (13, 3, 9, True, "ry")])
 def test_emulated_plan_matches_dense(n, L, t, chain, feat):
     spec = VQCSpec(n, L, 3, feature_map=feat, entangler="chain" if chain else "none")
     plan = hp.build_plan(n, L, spec.readout, chain, feat, tile_bits=t)
@@ -79,3 +81,26 @@ def test_eligibility():
     assert not hp.eligible(VQCSpec(16, 3, 3, entangler="ring"))
     assert not hp.eligible(VQCSpec(4, 2, 3))
     assert not hp.eligible(VQCSpec(8, 2, 3, feature_map="amplitude"))
+
+
+def test_trimmed_plan_full_groups():
+    """16q x 3L: deferring layer tails gives 8 full group ops (greedy: 10) in the same 2 passes, and the
+    LDS swizzle search still reaches the conflict-free score for every group of every pass."""
+    greedy = hp.build_plan(16, 3, [0, 1, 2], trim=False)
+    plan = hp.build_plan(16, 3, [0, 1, 2])
+    assert len(plan.passes) == len(greedy.passes) == 2
+    assert sum(len(p.groups) for p in plan.passes) == 8 < sum(len(p.groups) for p in greedy.passes)
+    assert all(len(g.qubits) == hp.GROUP for p in plan.passes for g in p.groups)
+    for n, L in [(11, 2), (13, 3)]:
+        t = 10 if n == 11 else 9
+        a = hp.build_plan(n, L, [0, 1, 2], tile_bits=t, trim=False)
+        b = hp.build_plan(n, L, [0, 1, 2], tile_bits=t)
+        assert len(b.passes) == len(a.passes)
+        assert sum(len(p.groups) for p in b.passes) < sum(len(p.groups) for p in a.passes)
+    for p in plan.passes:
+        groups = p.groups + p.l1
+        total = 0
+        for g in groups:
+            allv, dirs = hp._group_geom(plan, p, g)[0], hp._group_geom(plan, p, g)[6]
+            total += hp._best_cols(p.H, allv, dirs)[0]
+        assert total == hp.FULL_SCORE * len(groups)
