@@ -34,6 +34,7 @@ tests hold against a dense simulation, and the HIP kernel is tested against both
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -179,6 +180,8 @@ def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
     pass) and the trimmed plan (a non-final pass defers each layer's ragged tail so its groups are full
     4-qubit unitaries) and keeps the one with fewer passes, then fewer group ops: for 16q x 3L the trimmed
     plan runs 8 group ops instead of 10 in the same two passes."""
+    if trim is None and os.environ.get("QFEDX_HEA_TRIM", "auto") in ("0", "1"):   # A/B timing override
+        trim = os.environ["QFEDX_HEA_TRIM"] == "1"
     if trim is None:
         cands = [build_plan(n, L, readout, chain, feature, tile_bits, False, tr) for tr in (False, True)]
         best = min(cands, key=lambda pl: (len(pl.passes), sum(len(p.groups) for p in pl.passes), not trim))
