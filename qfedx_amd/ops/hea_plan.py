@@ -183,8 +183,18 @@ def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
     if trim is None and os.environ.get("QFEDX_HEA_TRIM", "auto") in ("0", "1"):   # A/B timing override
         trim = os.environ["QFEDX_HEA_TRIM"] == "1"
     if trim is None:
-        cands = [build_plan(n, L, readout, chain, feature, tile_bits, False, tr) for tr in (False, True)]
-        best = min(cands, key=lambda pl: (len(pl.passes), sum(len(p.groups) for p in pl.passes), not trim))
+        # candidates: no trimming, trimming everywhere, and per-layer trimming of the first (product-state)
+        # pass with the later passes greedy or trimmed; ties keep the earlier candidate
+        opts = [False, True]
+        for m in range(1, 1 << max(L - 1, 0)):
+            opts += [(m << 2,), (m << 2, -1)]
+        cands = []
+        for tr in opts:
+            try:
+                cands.append(build_plan(n, L, readout, chain, feature, tile_bits, False, tr))
+            except RuntimeError:
+                continue
+        best = min(cands, key=lambda pl: (len(pl.passes), sum(len(p.groups) for p in pl.passes)))
         if swizzle:
             for j, p in enumerate(best.passes):
                 layout_pass(best, p, seed=j)
@@ -223,8 +233,13 @@ def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
         for o in remaining:
             if (sup[o] & ~tm) == 0 and all(d in done or d in taken for d in preds[o]):
                 taken.append(o)
-        if trim and len(taken) < len(remaining):
-            taken = _trim_ragged(taken, preds)
+        if isinstance(trim, tuple):         # per-pass layer masks (bit l = trim layer l; -1 = all layers)
+            j = len(passes)
+            layers = trim[j] if j < len(trim) else (-1 if trim[-1] == -1 else 0)
+        else:
+            layers = -1 if trim else 0
+        if layers and len(taken) < len(remaining):
+            taken = _trim_ragged(taken, preds, layers)
         if not taken and remaining:
             raise RuntimeError(f"pass planner stuck at {len(passes)} passes (n={n}, L={L}, t={t})")
         for o in taken:
@@ -276,9 +291,10 @@ def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
     return plan
 
 
-def _trim_ragged(taken: list, preds: dict) -> list:
-    """Drop each layer's highest rotations until every layer's count is a multiple of GROUP, together with
-    every taken rotation that depends on a dropped one.  Falls back to ``taken`` if nothing would be left."""
+def _trim_ragged(taken: list, preds: dict, layers: int = -1) -> list:
+    """Drop the highest rotations of each layer in the bitmask ``layers`` until its count is a multiple of
+    GROUP, together with every taken rotation that depends on a dropped one.  Falls back to ``taken`` if
+    nothing would be left."""
     keep = list(taken)
     while True:
         by_layer = {}
@@ -287,7 +303,7 @@ def _trim_ragged(taken: list, preds: dict) -> list:
         drop = set()
         for layer, os_ in by_layer.items():
             r = len(os_) % GROUP
-            if r:
+            if r and (layers >> layer) & 1:
                 drop.update(sorted(os_, key=lambda o: o[1])[-r:])
         if not drop:
             return keep if keep else list(taken)

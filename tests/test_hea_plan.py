@@ -24,7 +24,9 @@ def _dense(spec, xang, params, wread):
 @pytest.mark.parametrize("n,L,t,chain,feat", [(8, 2, 8, True, "ry"), (10, 3, 8, True, "ry"), (10, 3, 14, True, "rx"),
                                               (11, 2, 8, False, "ry"), (12, 4, 9, True, "ry"), (9, 1, 8, True, "rz"),
                                               # trimmed plans (ragged layer tails deferred to a later pass)
-                                              (11, 2, 10, True, "ry"), (13, 3, 9, True, "ry")])
+                                              (11, 2, 10, True, "ry"), (13, 3, 9, True, "ry"),
+                                              # per-layer trimming of the first pass (10q: 7 -> 6 ops)
+                                              (12, 3, 10, True, "ry"), (9, 4, 8, True, "rz")])
 def test_emulated_plan_matches_dense(n, L, t, chain, feat):
     spec = VQCSpec(n, L, 3, feature_map=feat, entangler="chain" if chain else "none")
     plan = hp.build_plan(n, L, spec.readout, chain, feat, tile_bits=t)
@@ -91,8 +93,9 @@ def test_trimmed_plan_full_groups():
     assert len(plan.passes) == len(greedy.passes) == 2
     assert sum(len(p.groups) for p in plan.passes) == 8 < sum(len(p.groups) for p in greedy.passes)
     assert all(len(g.qubits) == hp.GROUP for p in plan.passes for g in p.groups)
-    for n, L in [(11, 2), (13, 3)]:
-        t = 10 if n == 11 else 9
+    p20 = hp.build_plan(20, 2, [0, 1, 2], swizzle=False)       # the 20q DP suite config: 6 -> 5 ops
+    assert len(p20.passes) == 2 and sum(len(p.groups) for p in p20.passes) == 5
+    for n, L, t in [(11, 2, 10), (13, 3, 9), (10, 3, 8), (12, 3, 10)]:
         a = hp.build_plan(n, L, [0, 1, 2], tile_bits=t, trim=False)
         b = hp.build_plan(n, L, [0, 1, 2], tile_bits=t)
         assert len(b.passes) == len(a.passes)
