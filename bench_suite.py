@@ -84,7 +84,8 @@ def main():
             "vs_baseline": round(value / ref, 2) if ref else None,
             "dtype": {"bf16": "bf16-state/fp32-compute", "mfma": "fp16-state/fp32-accumulate (MFMA)",
                       "fp16": "fp16-state/fp32-accumulate (MFMA)"}.get(
-                          getattr(runner.adapter, "state_dtype", cfg.model.state_dtype), "fp32"),
+                          getattr(runner.adapter, "state_dtype", cfg.model.state_dtype)
+                          if backend == "hip" else "fp32", "fp32"),   # the MFMA/bf16 engines exist only on HIP
             "data": "synthetic non-IID client shards, random init", "rounds_per_sec": round(args.steps / dt, 4),
             "samples_per_sec": round(value * t.batch_size, 1), "backend": backend,
             "test_acc_after": round(ev["test_acc"], 4),
