@@ -33,6 +33,7 @@ tests hold against a dense simulation, and the HIP kernel is tested against both
 """
 from __future__ import annotations
 
+import copy
 import math
 import os
 from dataclasses import dataclass, field
@@ -174,6 +175,9 @@ def eligible(spec) -> bool:
             and spec.n_qubits <= 30 and spec.n_classes <= MAX_CLASSES)
 
 
+_PLAN_CACHE: dict = {}
+
+
 def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
                tile_bits: int = TILE_BITS, swizzle: bool = True, trim=None) -> HEAPlan:
     """Plan the passes.  ``trim=None`` builds both the greedy plan (every ready rotation joins the current
@@ -182,6 +186,9 @@ def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
     plan runs 8 group ops instead of 10 in the same two passes."""
     if trim is None and os.environ.get("QFEDX_HEA_TRIM", "auto") in ("0", "1"):   # A/B timing override
         trim = os.environ["QFEDX_HEA_TRIM"] == "1"
+    key = (n, L, tuple(readout), chain, feature, tile_bits, swizzle)
+    if trim is None and key in _PLAN_CACHE:          # the candidate search runs once per circuit shape
+        return copy.deepcopy(_PLAN_CACHE[key])
     if trim is None:
         # candidates: no trimming, trimming everywhere, and per-layer trimming of the first (product-state)
         # pass with the later passes greedy or trimmed; ties keep the earlier candidate
@@ -198,6 +205,7 @@ def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
         if swizzle:
             for j, p in enumerate(best.passes):
                 layout_pass(best, p, seed=j)
+        _PLAN_CACHE[key] = copy.deepcopy(best)
         return best
     t = min(tile_bits, n)
     if t < GROUP + 4:
