@@ -81,6 +81,27 @@ def make_config(args):
     return cfg
 
 
+def relaunch_if_needed(gpus: int) -> None:
+    """``--gpus N`` must match the launched world.  Started without a launcher (no WORLD_SIZE) and N > 1,
+    re-run this command under ``torch.distributed.run`` (one rank per GPU, 127.0.0.1 rendezvous) as a
+    CHILD process - nothing here has touched the GPU yet - and exit with its status."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if gpus <= 1:
+            return
+        import socket
+        import subprocess
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+               "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(sys.argv[0]), *sys.argv[1:]]
+        sys.exit(subprocess.call(cmd))
+    if int(ws) != gpus:
+        sys.exit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}; launch one rank per GPU "
+                 f"(torch.distributed.run --nproc-per-node {gpus}) or pass --gpus {ws}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,6 +119,7 @@ def main():
     ap.add_argument("--engine", default="mfma", choices=["mfma", "valu"],
                     help="mfma: fp16-state MFMA group-unitary engine (ops/hea_mfma.py); valu: fp32 pass engine")
     args = ap.parse_args()
+    relaunch_if_needed(args.gpus)
 
     import torch
     from qfedx_amd.api import setup

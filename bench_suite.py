@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("overrides", nargs="*")
     args = ap.parse_args()
+    from bench import relaunch_if_needed
+    relaunch_if_needed(args.gpus)
 
     from bench import timed_rounds
     from qfedx_amd.api import setup

@@ -63,6 +63,7 @@ class TrainConfig:
     momentum: float = 0.9
     grad_method: str = "adjoint"        # adjoint | param_shift | spsa | autograd
     client_fraction: float = 1.0        # ROADMAP:35,106 client sampling
+    sampling: str = "auto"              # auto (poisson under DP, else fixed) | fixed (m = round(q N)) | poisson
     dropout_prob: float = 0.0           # simulated client dropouts (ROADMAP:91)
     aggregate: str = "delta"            # delta (ROADMAP:36) | weights (Classical_FL.py:66-81)
     wrap_angles: bool = True            # wrap angle deltas to [-pi, pi] (ROADMAP:37)
@@ -83,6 +84,9 @@ class PrivacyConfig:
     secure_agg: bool = False
     secagg_bits: int = 48               # fixed-point ring Z_{2^bits} for exact mask cancellation
     secagg_scale: float = 2.0 ** 24
+    # testing/debug only: key DP noise and DP client sampling by the PUBLIC train.seed (reproducible
+    # across runs and rank counts) instead of a per-run secret - voids the DP guarantee
+    deterministic_noise: bool = False
 
 
 @dataclass

@@ -20,11 +20,13 @@ import math
 import time
 from typing import Optional
 
+import numpy as np
 import torch
 
 from ..parallel.dist import (ShardedServerState, World, all_gather_cat, all_reduce_, barrier, broadcast_,
                              shard_clients)
 from ..privacy.accountant import RDPAccountant
+from ..privacy.dp import draw_noise_seed
 from ..privacy.secure_agg import SecureAggregator
 from ..utils.device import h2d
 from ..utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
@@ -35,9 +37,19 @@ from .aggregator import EXACT_SCALE, Aggregator
 from .trainer import ShardStore
 
 
-def sample_participants(num_clients: int, fraction: float, seed: int, round_num: int) -> list[int]:
+def sample_participants(num_clients: int, fraction: float, seed: int, round_num: int,
+                        poisson: bool = False) -> list[int]:
+    """Clients taking part in round ``round_num`` (ROADMAP.md:35,106), keyed by (seed, round) so every
+    rank draws the same set without communication.
+
+    ``poisson=False``: a fixed-size subset of m = round(q N) drawn without replacement.
+    ``poisson=True``: every client independently with probability q (the set may be empty) - the
+    sampling the subsampled-Gaussian RDP bound of ``privacy/accountant.py`` assumes."""
     if fraction >= 1.0:
         return list(range(num_clients))
+    if poisson:
+        u = np_rng(seed, "sample_clients_poisson", round_num).random(num_clients)
+        return [int(c) for c in np.flatnonzero(u < fraction)]
     m = max(1, int(round(fraction * num_clients)))
     g = generator(seed, "sample_clients", round_num)
     return sorted(torch.randperm(num_clients, generator=g)[:m].tolist())
@@ -69,12 +81,22 @@ class FederatedRunner:
         self.local_ids = list(data.client_ids)
         self.store = ShardStore(data.clients, data.client_ids, device)
         self.P = adapter.n_params
-        self.secagg = SecureAggregator(t.seed, p.secagg_bits, p.secagg_scale) if p.secure_agg else None
-        if self.secagg is not None:
-            self.secagg.register(range(self.num_clients))
+        # DP noise + DP client sampling key: a per-run secret (rank 0's OS randomness, broadcast, never
+        # persisted or logged); the public train.seed only under privacy.deterministic_noise
+        self.noise_seed = draw_noise_seed(world, p.deterministic_noise, t.seed) if p.dp else t.seed
+        sampling = t.sampling if t.sampling != "auto" else ("poisson" if p.dp else "fixed")
+        if sampling not in ("fixed", "poisson"):
+            raise ValueError(f"train.sampling must be auto | fixed | poisson, got {t.sampling!r}")
+        self.poisson = sampling == "poisson"
+        self.secagg = None
+        if p.secure_agg:
+            # each client's DH secret comes from OS randomness on the rank hosting it; only public keys
+            # are exchanged (all-gather), so no process holds another rank's client secrets
+            self.secagg = SecureAggregator(None, p.secagg_bits, p.secagg_scale)
+            self.secagg.setup(self.local_ids, world)
         self.aggregator = Aggregator(self.P, adapter.angle_mask(), device, backend, t.aggregate,
                                      t.wrap_angles, p.dp, p.clip_norm, p.noise_multiplier, p.secure_agg,
-                                     self.secagg, t.seed)
+                                     self.secagg, self.noise_seed)
         self.accountant = RDPAccountant()
         # test shard for this rank
         Xt, yt = data.test
@@ -128,14 +150,21 @@ class FederatedRunner:
     # ------------------------------------------------------------------ checkpoint
     def save(self, round_num: int) -> None:
         rt = self.cfg.runtime
-        if rt.checkpoint_dir and self.world.is_main:
-            path = save_checkpoint(rt.checkpoint_dir, round_num, {
+        if not rt.checkpoint_dir:
+            return
+        # the sharded server-optimizer moments are gathered on every rank (collective) before rank 0 writes
+        server_state = self.server_opt.state_dict() if self.server_opt is not None else None
+        if self.world.is_main:
+            payload = {
                 "global_state": self.adapter.state_dict(self.params),
                 "accountant": json.dumps(self.accountant.state_dict()),
                 "config": self.cfg.to_dict(),
                 "metrics": self.history,
-                "seed": torch.tensor(self.cfg.train.seed),
-            })
+                "seed": torch.tensor(self.cfg.train.seed),   # public root seed (DP noise uses a run secret)
+            }
+            if server_state is not None:
+                payload["server_state"] = server_state
+            path = save_checkpoint(rt.checkpoint_dir, round_num, payload)
             self.metrics.tracker.log_artifact(path, "checkpoints")
         barrier(self.world)
 
@@ -150,6 +179,11 @@ class FederatedRunner:
         self.params = self.adapter.from_state_dict(ck["global_state"]).to(self.device)
         self.accountant.load_state_dict(json.loads(ck["accountant"]))
         self.history = list(ck.get("metrics", []))
+        if self.server_opt is not None:
+            if "server_state" not in ck:
+                raise ValueError(f"{path} has no server_state but train.server_optimizer="
+                                 f"{self.cfg.train.server_optimizer!r} needs its moments to resume")
+            self.server_opt.load_state_dict(ck["server_state"])
         self.start_round = int(ck["round"])
         self.log.info(f"resumed from {path} at round {self.start_round}")
 
@@ -160,7 +194,9 @@ class FederatedRunner:
         record holds device tensors until :meth:`resolve_record`."""
         t = self.cfg.train
         p = self.cfg.privacy
-        participants = sample_participants(self.num_clients, t.client_fraction, t.seed, r)
+        # under DP the participant set is part of the mechanism: keyed by the secret like the noise
+        participants = sample_participants(self.num_clients, t.client_fraction,
+                                           self.noise_seed if p.dp else t.seed, r, self.poisson)
         dropped = sample_dropouts(participants, t.dropout_prob, t.seed, r)
         dropped_set = set(dropped)
         part_set = set(participants)
@@ -238,7 +274,9 @@ class FederatedRunner:
                 metrics = buf[P + 1:].double() / EXACT_SCALE
                 self.params = self.aggregator.apply(self.params, mean_upd, wsum=wsum)
         if p.dp:
-            q = len(participants) / self.num_clients
+            # the subsampled-Gaussian RDP bound holds for Poisson sampling at rate q; a fixed-size subset
+            # drawn without replacement is accounted conservatively with no amplification (q = 1)
+            q = min(1.0, t.client_fraction) if self.poisson else 1.0
             self.accountant.step(q, p.noise_multiplier, 1)
         rec = {"round": r + 1, "participants": len(participants), "dropped": len(dropped),
                "_metrics": metrics, "_t0": t0,

@@ -312,4 +312,25 @@ class ShardedServerState:
         return (global_params.double() + full[: self.P]).to(global_params.dtype)
 
     def state_dict(self) -> dict:
-        return {"t": self.t, "m": self.m.cpu(), "v": None if self.v is None else self.v.cpu()}
+        """Full (un-sharded) optimizer state, identical on every rank.  COLLECTIVE: every rank calls it
+        (the moment shards are all-gathered), so the checkpoint resumes at any world size."""
+        def full(x):
+            return all_gather_(x, self.world)[: self.P].cpu()
+        empty = torch.zeros(0, dtype=torch.float64)
+        return {"kind": self.kind, "t": torch.tensor(self.t, dtype=torch.int64), "m": full(self.m),
+                "v": full(self.v) if self.v is not None else empty}
+
+    def load_state_dict(self, sd: dict) -> None:
+        """Restore from :meth:`state_dict` (any saving world size): this rank keeps its own P/world slice."""
+        if sd.get("kind", self.kind) != self.kind:
+            raise ValueError(f"checkpoint server optimizer {sd.get('kind')!r} != configured {self.kind!r}")
+        self.t = int(sd["t"])
+        lo = self.world.rank * self.chunk
+
+        def shard(x):
+            pad = torch.zeros(self.padded, dtype=torch.float64)
+            pad[: self.P] = x.double().reshape(-1)[: self.P]
+            return pad[lo: lo + self.chunk].to(self.m.device)
+        self.m = shard(sd["m"])
+        if self.v is not None:
+            self.v = shard(sd["v"])

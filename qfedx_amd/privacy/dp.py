@@ -1,14 +1,35 @@
 """Per-client DP: clip the update to l2 norm C, add N(0, sigma^2 C^2 I) (ROADMAP.md:47,50-51).
 
-Noise is drawn from Philox4x32-10 keyed by (seed, 'dp_noise', round, client) - counter-based, so
-a client's noise is the same whichever rank (and however many ranks) processes it; the gfx950
-fused aggregation kernel (``csrc/fedavg.hip``) draws the identical stream on device.
+Noise is drawn from Philox4x32-10 keyed by (noise_seed, 'dp_noise', round, client) - counter-based,
+so a client's noise is the same whichever rank (and however many ranks) processes it; the gfx950
+fused aggregation kernel (``csrc/train_kernels.hip``) draws the identical stream on device.
+
+``noise_seed`` is a per-run SECRET (:func:`draw_noise_seed`): 63 bits of OS randomness drawn on
+rank 0 and broadcast, held in memory only - never written to the config, metrics, tracking store
+or checkpoints.  Keying the noise by the public ``train.seed`` would let anyone holding the config
+and successive released models regenerate and subtract it, voiding the accountant's epsilon; that
+mode exists only behind ``privacy.deterministic_noise`` (tests of rank-count invariance / resume).
 """
 from __future__ import annotations
+
+import secrets
 
 import torch
 
 from ..utils.seeding import philox_key, philox_normal
+
+
+def draw_noise_seed(world, deterministic: bool = False, public_seed: int = 0) -> int:
+    """Root key of the DP noise and DP client-sampling streams, identical on every rank.
+
+    ``deterministic=True`` returns ``public_seed`` (reproducible; NOT private)."""
+    if deterministic:
+        return int(public_seed)
+    from ..parallel.dist import broadcast_
+    s = secrets.randbits(63) if world.is_main else 0
+    t = torch.tensor([s], dtype=torch.int64, device=world.device)
+    broadcast_(t, world)
+    return int(t.item())
 
 
 def clip_factors(deltas: torch.Tensor, clip_norm: float) -> tuple[torch.Tensor, torch.Tensor]:

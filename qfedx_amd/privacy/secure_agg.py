@@ -2,8 +2,12 @@
 exchange API simulating DH key agreement at registration).
 
 Protocol (Bonawitz et al. style, single round, honest-but-curious server):
-  * registration: each client draws a secret ``sk_i`` and publishes ``pk_i = g^sk_i mod p``; a pair
-    seed is ``s_ij = H(g^(sk_i sk_j) mod p)`` - both ends derive it, the server cannot.
+  * registration: each client draws a secret ``sk_i`` from OS randomness (``secrets``), held only by
+    the rank hosting that client, and publishes ``pk_i = g^sk_i mod p``; ranks exchange public keys
+    only (``SecureAggregator.setup``: one all-gather).  A pair seed is ``s_ij = H(g^(sk_i sk_j) mod p)``
+    - both ends derive it; the aggregate (server side) sees public keys and masked sums only.
+    Passing an integer ``session_seed`` instead derives every secret from it (reproducible simulation
+    for tests - whoever knows the seed can unmask, so it is not a confidentiality setting).
   * masking: the update is encoded in the fixed-point ring Z_{2^bits} (default 2^48, scale 2^24), then client i
     adds ``+PRG(s_ij, round)`` for every peer j>i and ``-PRG(s_ij, round)`` for j<i.
   * aggregation: masked vectors are summed mod 2^bits - pair masks cancel EXACTLY (integer ring,
@@ -17,6 +21,7 @@ HIP aggregation kernel uses on device.
 from __future__ import annotations
 
 import hashlib
+import secrets
 from typing import Iterable, Optional
 
 import torch
@@ -36,24 +41,37 @@ def _hash_int(*vals: int) -> int:
 
 
 class KeyRegistry:
-    """Simulated Diffie-Hellman key agreement (registration phase)."""
+    """Simulated Diffie-Hellman key agreement (registration phase).
 
-    def __init__(self, session_seed: int):
+    Holds the secret keys of the clients registered HERE and the public keys of every client."""
+
+    def __init__(self, session_seed: Optional[int] = None):
         self.session_seed = session_seed
         self._sk: dict[int, int] = {}
         self.public: dict[int, int] = {}
 
     def register(self, client: int) -> int:
-        sk = derive_seed(self.session_seed, "secagg", 0xD4, client) % (_P - 2) + 1
+        if self.session_seed is None:
+            sk = secrets.randbelow(_P - 2) + 1
+        else:
+            sk = derive_seed(self.session_seed, "secagg", 0xD4, client) % (_P - 2) + 1
         self._sk[client] = sk
         self.public[client] = pow(_G, sk, _P)
         return self.public[client]
 
+    def add_public(self, client: int, pk: int) -> None:
+        if client not in self._sk:
+            self.public[client] = int(pk)
+
     def pair_seed(self, me: int, peer: int) -> int:
         """Computed by client ``me`` from its own secret and the peer's public key."""
         if me not in self._sk:
+            if self.session_seed is None:
+                raise KeyError(f"client {me}'s secret key is not held by this process")
             self.register(me)
         if peer not in self.public:
+            if self.session_seed is None:
+                raise KeyError(f"no public key registered for client {peer}")
             self.register(peer)
         shared = pow(self.public[peer], self._sk[me], _P)
         return _hash_int(shared)
@@ -91,7 +109,7 @@ def decode_fixed(v: torch.Tensor, scale: float, bits: int = 48) -> torch.Tensor:
 
 
 class SecureAggregator:
-    def __init__(self, session_seed: int, bits: int = 48, scale: float = 2.0 ** 24):
+    def __init__(self, session_seed: Optional[int] = None, bits: int = 48, scale: float = 2.0 ** 24):
         self.registry = KeyRegistry(session_seed)
         self.bits = bits
         self.scale = scale
@@ -100,6 +118,19 @@ class SecureAggregator:
     def register(self, clients: Iterable[int]) -> None:
         for c in clients:
             self.registry.register(int(c))
+
+    def setup(self, local_clients: Iterable[int], world) -> None:
+        """Register this rank's clients (secrets stay here) and all-gather every client's public key:
+        rows [client, pk words 0..3] (127-bit keys as four 32-bit words)."""
+        from ..parallel.dist import all_gather_cat
+        rows = []
+        for c in local_clients:
+            pk = self.registry.register(int(c))
+            rows.append([int(c)] + [(pk >> (32 * i)) & 0xFFFFFFFF for i in range(4)])
+        t = torch.tensor(rows, dtype=torch.int64).reshape(-1).to(world.device)
+        allrows = all_gather_cat(t, world).cpu().reshape(-1, 5).tolist()
+        for c, *w in allrows:
+            self.registry.add_public(int(c), sum(int(x) << (32 * i) for i, x in enumerate(w)))
 
     def client_mask(self, client: int, participants: Iterable[int], round_num: int, P: int,
                     device="cpu") -> torch.Tensor:

@@ -51,3 +51,17 @@ def test_bench_two_ranks_gloo():
                  "--gpus", "2"] + SMALL)
     assert len(recs) == 1, "only rank 0 prints"
     _check(recs[0], 2)
+
+
+def test_bench_self_launches_ranks_for_gpus_flag():
+    """``python bench.py --gpus 2`` without a launcher spawns torch.distributed.run itself."""
+    recs = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"] + SMALL)
+    assert len(recs) == 1
+    _check(recs[0], 2)
+
+
+def test_bench_rejects_mismatched_world():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"] + SMALL, cwd="/tmp",
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr

@@ -41,7 +41,7 @@ def _run(world, kw, tmp_path):
 
 
 @pytest.mark.parametrize("kw", [dict(num_rounds=3), dict(num_rounds=2, dp=True, secure_agg=True, dropout_prob=0.3,
-                                                         client_fraction=0.75)])
+                                                         client_fraction=0.75, deterministic_noise=True)])
 def test_gloo_two_ranks_match_single_process(tmp_path, kw):
     from qfedx_amd.api import run_experiment
     single = run_experiment(small_cfg(**kw))
@@ -62,7 +62,8 @@ def test_gloo_four_ranks_bitwise_rank_invariant(tmp_path):
     """Exact fixed-point aggregation: 4 ranks reproduce the single-process model BITWISE
     (SURVEY §7.3 item 10), including client sampling and DP noise keyed by client."""
     from qfedx_amd.api import run_experiment
-    kw = dict(num_rounds=3, num_clients=8, client_fraction=0.75, dp=True, noise_multiplier=0.3)
+    kw = dict(num_rounds=3, num_clients=8, client_fraction=0.75, dp=True, noise_multiplier=0.3,
+              deterministic_noise=True)
     single = run_experiment(small_cfg(**kw))
     four = _run(4, kw, tmp_path)
     assert torch.equal(four["params"], single["params"])
@@ -84,3 +85,15 @@ def test_gloo_two_ranks_sharded_server_adam(tmp_path):
     single = run_experiment(small_cfg(**kw))
     two = _run(2, kw, tmp_path)
     assert torch.equal(two["params"], single["params"])
+
+
+def test_sharded_server_state_checkpoint_resumes_at_other_world_size(tmp_path):
+    """FedAdam moments sharded over 2 ranks are gathered into the checkpoint; a single process resumes
+    from it and matches the uninterrupted run bitwise (server_state in checkpoints)."""
+    from qfedx_amd.api import run_experiment
+    srv = dict(server_optimizer="adam", server_lr=0.3)
+    full = run_experiment(small_cfg(num_rounds=4, **srv))
+    ck = str(tmp_path / "ck")
+    _run(2, dict(num_rounds=2, checkpoint_every=1, checkpoint_dir=ck, **srv), tmp_path)
+    resumed = run_experiment(small_cfg(num_rounds=4, checkpoint_every=1, checkpoint_dir=ck, resume=True, **srv))
+    assert torch.equal(resumed["params"], full["params"])

@@ -105,15 +105,60 @@ def test_gradient_methods_train(method, opt):
     assert np.isfinite(out["accuracies"][-1])
 
 
-def test_checkpoint_resume_matches_uninterrupted(tmp_path):
-    full = run_experiment(small_cfg(num_rounds=4))
-    cfg = small_cfg(num_rounds=2, checkpoint_every=1, checkpoint_dir=str(tmp_path / "ck"))
+@pytest.mark.parametrize("server", [{}, {"server_optimizer": "momentum", "server_lr": 0.5},
+                                    {"server_optimizer": "adam", "server_lr": 0.3}])
+def test_checkpoint_resume_matches_uninterrupted(tmp_path, server):
+    """Resume reproduces the uninterrupted run, including the server optimizer's moments."""
+    full = run_experiment(small_cfg(num_rounds=4, **server))
+    cfg = small_cfg(num_rounds=2, checkpoint_every=1, checkpoint_dir=str(tmp_path / "ck"), **server)
     run_experiment(cfg)
-    cfg2 = small_cfg(num_rounds=4, checkpoint_every=1, checkpoint_dir=str(tmp_path / "ck"), resume=True)
+    cfg2 = small_cfg(num_rounds=4, checkpoint_every=1, checkpoint_dir=str(tmp_path / "ck"), resume=True, **server)
     resumed = run_experiment(cfg2)
-    assert torch.allclose(full["params"], resumed["params"], atol=1e-6)
+    assert torch.equal(full["params"], resumed["params"])
     ck = torch.load(sorted((tmp_path / "ck").glob("round_*.pt"))[-1], weights_only=True)
     assert set(ck["global_state"]) == {"theta", "readout.a", "readout.b"}
+    if server:
+        st = ck["server_state"]
+        assert st["kind"] == server["server_optimizer"] and int(st["t"]) == 4
+        assert st["m"].shape == (full["params"].numel(),) and st["m"].abs().sum() > 0
+    else:
+        assert "server_state" not in ck
+
+
+def test_resume_refuses_checkpoint_without_server_state(tmp_path):
+    run_experiment(small_cfg(num_rounds=1, checkpoint_every=1, checkpoint_dir=str(tmp_path / "ck")))
+    with pytest.raises(ValueError, match="server_state"):
+        run_experiment(small_cfg(num_rounds=2, checkpoint_every=1, checkpoint_dir=str(tmp_path / "ck"),
+                                 resume=True, server_optimizer="adam"))
+
+
+def test_dp_noise_is_keyed_by_a_run_secret(tmp_path):
+    """DP noise is not reproducible from the public config/checkpoint: two runs with the same
+    train.seed differ, and nothing written to disk holds the key; deterministic_noise=True restores
+    reproducibility for tests."""
+    kw = dict(num_rounds=2, dp=True, noise_multiplier=0.5)
+    a = run_experiment(small_cfg(**kw, checkpoint_every=1, checkpoint_dir=str(tmp_path / "a"),
+                                 metrics_path=str(tmp_path / "m.jsonl")))
+    b = run_experiment(small_cfg(**kw))
+    assert not torch.equal(a["params"], b["params"])
+    c = run_experiment(small_cfg(**kw, deterministic_noise=True))
+    d = run_experiment(small_cfg(**kw, deterministic_noise=True))
+    assert torch.equal(c["params"], d["params"])
+    ck = torch.load(sorted((tmp_path / "a").glob("round_*.pt"))[-1], weights_only=True)
+    assert not any("noise" in k for k in ck) and "noise_seed" not in open(tmp_path / "m.jsonl").read()
+
+
+def test_poisson_sampling_under_dp():
+    sizes = [len(sample_participants(200, 0.1, 7, r, poisson=True)) for r in range(200)]
+    assert 17 < float(np.mean(sizes)) < 23 and len(set(sizes)) > 5        # Bernoulli(q), variable size
+    assert sample_participants(200, 0.1, 7, 3, poisson=True) == sample_participants(200, 0.1, 7, 3, poisson=True)
+    # DP defaults to Poisson and accounts at q = client_fraction; fixed-size sampling is accounted with q = 1
+    pois = run_experiment(small_cfg(num_rounds=2, dp=True, client_fraction=0.5, num_clients=8))
+    fixed = run_experiment(small_cfg(num_rounds=2, dp=True, client_fraction=0.5, num_clients=8, sampling="fixed"))
+    from qfedx_amd.privacy.accountant import epsilon
+    assert pois["epsilon"] == pytest.approx(epsilon(0.5, 1.0, 2, 1e-5), rel=1e-9)
+    assert fixed["epsilon"] == pytest.approx(epsilon(1.0, 1.0, 2, 1e-5), rel=1e-9)
+    assert fixed["epsilon"] > pois["epsilon"]
 
 
 def test_config_yaml_and_overrides(tmp_path):

@@ -115,3 +115,37 @@ def test_philox_numpy_and_torch_paths_bitwise():
     keys = torch.randint(0, 2 ** 32, (777, 2), generator=g, dtype=torch.int64)
     assert torch.equal(philox4x32(ctr, 0xDEADBEEF, 0x12345678), _philox4x32_torch(ctr, 0xDEADBEEF, 0x12345678))
     assert torch.equal(philox4x32(ctr, keys[:, 0], keys[:, 1]), _philox4x32_torch(ctr, keys[:, 0], keys[:, 1]))
+
+
+def test_secagg_secrets_are_local_and_random():
+    """Client DH secrets come from OS randomness and stay with their rank; only public keys are shared
+    (ADVICE r1).  Two registries model two ranks: masks still cancel across them."""
+    from qfedx_amd.parallel.dist import World
+    a, b = SecureAggregator(None), SecureAggregator(None)
+    a.setup([0, 1], World())
+    b.setup([2, 3], World())
+    for c in (0, 1):
+        b.registry.add_public(c, a.registry.public[c])
+    for c in (2, 3):
+        a.registry.add_public(c, b.registry.public[c])
+    assert set(a.registry._sk) == {0, 1} and set(b.registry._sk) == {2, 3}
+    with pytest.raises(KeyError):
+        a.registry.pair_seed(2, 0)                 # rank a cannot act as client 2
+    assert a.registry.pair_seed(0, 3) == b.registry.pair_seed(3, 0)
+    parts = [0, 1, 2, 3]
+    rng = np.random.default_rng(1)
+    ups = {c: torch.from_numpy(rng.normal(size=9)) for c in parts}
+    masked = [a.mask(ups[c], c, parts, 2) for c in (0, 1)] + [b.mask(ups[c], c, parts, 2) for c in (2, 3)]
+    total = torch.zeros_like(masked[0])
+    for m in masked:
+        total = torch.remainder(total + m, a.modulus)
+    assert torch.allclose(decode_fixed(total, a.scale, a.bits), sum(ups.values()), atol=1e-5)
+    # fresh randomness: a second registry for the same client gets a different key
+    assert SecureAggregator(None).registry.register(0) != a.registry.public[0]
+
+
+def test_noise_seed_secret_vs_deterministic():
+    from qfedx_amd.parallel.dist import World
+    from qfedx_amd.privacy.dp import draw_noise_seed
+    assert draw_noise_seed(World(), True, 42) == 42
+    assert draw_noise_seed(World()) != draw_noise_seed(World())
