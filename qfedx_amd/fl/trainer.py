@@ -135,6 +135,35 @@ class BatchPlan:
         self.active = active.float()
 
 
+def graph_bucket(k: int, k_max: int) -> int:
+    """Captured client count for ``k`` participating clients: the next power of two up to 8, then the next
+    multiple of 8, capped at the rank's client count ``k_max``.  Under Poisson client sampling the per-round
+    count varies (Binomial(N, q)); bucketing keeps the number of distinct hipGraph shapes small, so rounds
+    replay a cached graph instead of re-capturing (at the cost of < 8 idle client rows)."""
+    if k <= 0:
+        return 0
+    b = 1 << (k - 1).bit_length() if k <= 8 else -(-k // 8) * 8
+    return max(k, min(b, k_max))
+
+
+def _pad_clients(tabs: dict, kp: int) -> dict:
+    """Extend a round's client tables to ``kp`` clients with inactive rows: store slot of client 0, minibatch
+    index 0, loss weight 0, step mask 0, FedAvg weight 0 (the optimizer leaves them untouched, the readout
+    writes zero loss / hits for them)."""
+    K = tabs["lid"].shape[0]
+    if kp <= K:
+        return tabs
+    n = kp - K
+    out = dict(tabs)
+    out["lid"] = torch.cat([tabs["lid"], tabs["lid"][:1].expand(n)])
+    out["idx"] = torch.cat([tabs["idx"], torch.zeros_like(tabs["idx"][:, :1]).expand(-1, n, -1)], 1)
+    out["wts"] = torch.cat([tabs["wts"], torch.zeros_like(tabs["wts"][:, :1]).expand(-1, n, -1)], 1)
+    out["act"] = torch.cat([tabs["act"], torch.zeros_like(tabs["act"][:, :1]).expand(-1, n)], 1)
+    out["nvalid"] = torch.cat([tabs["nvalid"], torch.zeros_like(tabs["nvalid"][:, :1]).expand(-1, n)], 1)
+    out["w"] = torch.cat([tabs["w"], torch.zeros(n, dtype=tabs["w"].dtype)])
+    return out
+
+
 _NATIVE = []
 
 
@@ -244,15 +273,23 @@ class VQCClientTrainer:
                   "n_samples": store.counts[li].to(torch.float64)}
         if plan.idx.numel() and int(plan.idx.max()) >= max(1, store.nmax):   # the gather kernel trusts the table
             raise RuntimeError("minibatch plan indexes past the client store")
-        up = PackedUpload({"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid,
-                           "w": store.counts[li].to(torch.float64)})   # FedAvg sample-count weights
         noise = self.engine.noise
+        graphed = self.use_graph and method == "adjoint" and noise is None
+        tabs = {"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid,
+                "w": store.counts[li].to(torch.float64)}   # FedAvg sample-count weights
+        if graphed:
+            tabs = _pad_clients(tabs, graph_bucket(K, len(store)))
+        up = PackedUpload(tabs)
         traj_keys = ro_keys = None
         if noise is not None:
             traj_keys = noise.client_keys("noise_traj", round_num, cids, self.device)
             ro_keys = noise.client_keys("shots", round_num, cids, self.device)
-        if self.use_graph and method == "adjoint" and noise is None:
+        if graphed:
             params, loss_all, correct_all, dv = self._graphed(store, up, theta_g, plan, round_num)
+            # padding clients (inactive, weight 0) only fill the captured shape: the FedAvg reduce sees the
+            # K real rows; their [S, Kpad] metric columns are all zero
+            params = params[:K]
+            dv = dict(dv, w=dv["w"][:K], lid=dv["lid"][:K])
         else:
             dv = up.to_device(self.device)
             params, loss_all, correct_all = self._body(store.X, store.y, dv["lid"], theta_g.to(self.device), dv["idx"],

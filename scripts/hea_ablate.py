@@ -74,6 +74,8 @@ def main():
     run("gen_store_64nop_frag", False, p0, nop, nopf2, True, False, True, False)
     run("adj1_full", True, p1, a1, ai1, False, False, False, True)
     run("adj0_full", True, p0, a0, ai0, False, True, False, False)
+    run("adj0_load_only", True, p0, a0[:0].contiguous(), ai0[:0].contiguous(), False, True, False, False)
+    run("adj0_load_store", True, p0, a0[:0].contiguous(), ai0[:0].contiguous(), False, True, False, True)
     run("adj0_1back", True, p0, a0[:1].contiguous(), ai0[:1].contiguous(), False, True, False, False)
     run("adj0_4back", True, p0, a0[:4].contiguous(), ai0[:4].contiguous(), False, True, False, False)
     print(json.dumps(res), flush=True)

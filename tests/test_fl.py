@@ -237,3 +237,22 @@ def test_native_batch_plan_matches_torch_oracle(local_epochs, local_steps, shuff
         b = BatchPlan(counts, ids, 16, r, 1234, local_epochs, local_steps, shuffle, native=False)
         assert a.steps_per_client == b.steps_per_client and a.max_steps == b.max_steps
         assert torch.equal(a.idx, b.idx) and torch.equal(a.wts, b.wts) and torch.equal(a.active, b.active)
+
+
+def test_graph_bucket_and_client_padding():
+    """Poisson client sampling varies the per-rank client count; the hipGraph path pads to a few buckets
+    with inactive weight-0 rows (trainer.graph_bucket / _pad_clients)."""
+    from qfedx_amd.fl.trainer import _pad_clients, graph_bucket
+    assert [graph_bucket(k, 64) for k in (1, 2, 3, 5, 8, 9, 16, 17, 31)] == [1, 2, 4, 8, 8, 16, 16, 24, 32]
+    assert graph_bucket(5, 6) == 6 and graph_bucket(7, 7) == 7 and graph_bucket(0, 4) == 0
+    assert len({graph_bucket(k, 64) for k in range(20, 45)}) == 4      # Binomial(64, .5) bulk -> 4 shapes
+    S, K, B = 2, 3, 4
+    tabs = {"lid": torch.tensor([5, 1, 2]), "idx": torch.randint(0, 9, (S, K, B)), "wts": torch.rand(S, K, B),
+            "act": torch.ones(S, K), "nvalid": torch.full((S, K), 4.0), "w": torch.tensor([3.0, 4.0, 5.0]).double()}
+    out = _pad_clients(tabs, 8)
+    assert out["lid"].tolist() == [5, 1, 2, 5, 5, 5, 5, 5]
+    assert out["idx"].shape == (S, 8, B) and torch.equal(out["idx"][:, :K], tabs["idx"])
+    for key in ("wts", "act", "nvalid"):
+        assert torch.equal(out[key][:, :K], tabs[key]) and not out[key][:, K:].any()
+    assert out["w"].tolist() == [3.0, 4.0, 5.0, 0, 0, 0, 0, 0] and out["w"].dtype == torch.float64
+    assert _pad_clients(tabs, 3) is tabs

@@ -111,16 +111,18 @@ def test_fused_fedavg_reduce_matches_torch(cuda, dp):
     assert torch.allclose(a, b, atol=1e-6, rtol=1e-6), (a - b).abs().max()
 
 
-@pytest.mark.parametrize("fraction", [1.0, 0.5])
-def test_graph_round_matches_eager(cuda, fraction):
+@pytest.mark.parametrize("fraction,sampling", [(1.0, "fixed"), (0.5, "fixed"), (0.5, "poisson")])
+def test_graph_round_matches_eager(cuda, fraction, sampling):
     """hipGraph-replayed local rounds produce the same global model as eager launches (with client
-    sampling the set changes every round while the captured shape is reused)."""
+    sampling the set changes every round while the captured shape is reused; under Poisson sampling the
+    client count changes too and the graph runs padded to its bucket, trainer.graph_bucket)."""
     from tests.test_fl import small_cfg
     from qfedx_amd.api import run_experiment
     from qfedx_amd.parallel.dist import init_distributed
     outs = []
     for graphs in (True, False):
-        cfg = small_cfg(num_rounds=4, n_qubits=6, device="cuda", backend="hip", client_fraction=fraction)
+        cfg = small_cfg(num_rounds=6, n_qubits=6, device="cuda", backend="hip", client_fraction=fraction,
+                        sampling=sampling, num_clients=7)
         dev = torch.device("cuda", 0)
         world = init_distributed(dev)
         import qfedx_amd.fl.trainer as tr
