@@ -389,12 +389,152 @@ __device__ __forceinline__ void dma_frags(const PassArgs& a, int k, int fi, int 
                                    (__attribute__((address_space(3))) void*)(slot + 64 * wave), 16, 0, 0);
 }
 
+// Readout / observable ops walk the tile words w = tid + NT i (i < T / NT).  The sign of class c at word w is
+// parity(w & om[c]) ^ parity(fixed & of[c]): a per-thread part (tid bits) and a wave-uniform part (NT i bits,
+// scalar).  The words are read in chunks of RCH with every read of a chunk issued before the first use (one
+// LDS wait per chunk instead of one per word), and NC, the class count, is a template parameter so the class
+// loop has no per-word branches.  Reads are never predicated (a predicated read serialises on the mask
+// register): words past the tile wrap to in-bounds addresses and their contributions are masked.
+constexpr int RCH = 8;
+
+// Per-op class sign state, kept small in scalar registers (this kernel runs at the SGPR limit, and the class
+// masks are dead after setup): words w = tid + NT (i0 + j), i0 = k CH a chunk start, j < CH, have the sign
+//   parity(tid & om_c) ^ parity(fixed & of_c)   per lane    -> bit c of sgn0 (VGPR)
+// ^ parity(NT k CH & om_c)                       per chunk   -> bit k NC + c of fu (one SGPR)
+// ^ parity(NT j & om_c)                          per word    -> bit j NC + c of jb (two SGPRs)
+// The word part becomes a +-1 table in registers (0 for words past a partial tile) while NC x CH <= 32.
+template <int NC, int CH>
+struct ClassSigns {
+  static constexpr bool TAB = NC * CH <= 32;
+  uint32_t sgn0;
+  uint32_t fu;
+  uint64_t jb;
+  int iters;
+  float f[TAB ? CH : 1][TAB ? NC : 1];
+  __device__ __forceinline__ bool flip(int c, int k) const { return (((sgn0 >> c) ^ (fu >> (k * NC + c))) & 1u) != 0u; }
+  __device__ __forceinline__ float mul(float x, int j, int c) const {
+    if constexpr (TAB) return x * f[j][c];
+    return j < iters ? (((jb >> (j * NC + c)) & 1u) ? -x : x) : 0.f;
+  }
+};
+
+template <int NC, int NT, int CH>
+__device__ __forceinline__ ClassSigns<NC, CH> class_signs(const int* opw, int tid, uint32_t fixed, int iters) {
+  constexpr int QI = (1 << TMAX) / NT;
+  static_assert((QI / CH) * NC <= 32 && CH * NC <= 64, "class sign masks must fit one / two dwords");
+  ClassSigns<NC, CH> cs;
+  cs.sgn0 = 0;
+  cs.fu = 0;
+  cs.jb = 0;
+  cs.iters = iters;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const uint32_t om = (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_OFF + c]);
+    const uint32_t of = (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_RFULL + 2 * c]);
+    cs.sgn0 |= (uint32_t)(par((uint32_t)tid & om) ^ par(fixed & of)) << c;
+#pragma unroll
+    for (int k = 0; k < QI / CH; ++k) cs.fu |= (uint32_t)par((uint32_t)(NT * CH * k) & om) << (k * NC + c);
+#pragma unroll
+    for (int j = 0; j < CH; ++j) cs.jb |= (uint64_t)par((uint32_t)(NT * j) & om) << (j * NC + c);
+  }
+  if constexpr (ClassSigns<NC, CH>::TAB) {
+#pragma unroll
+    for (int j = 0; j < CH; ++j)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) cs.f[j][c] = j < iters ? (((cs.jb >> (j * NC + c)) & 1u) ? -1.f : 1.f) : 0.f;
+  }
+  return cs;
+}
+
+// <Z_c> partial sums of the tile (forward image: one fp16 (re, im) word per amplitude).
+template <int NC, int NT>
+__device__ __forceinline__ void readout_op(const uint32_t* psi_t, const PassArgs& a, const int* opw, int tid,
+                                           int lane, int wave, int T, uint32_t fixed, float* red, size_t pidx) {
+  constexpr int QI = (1 << TMAX) / NT, NW = NT / 64;
+  constexpr int CH = QI < RCH ? QI : RCH;
+  const int iters = T >= NT ? T / NT : 1;
+  const ClassSigns<NC, CH> cs = class_signs<NC, NT, CH>(opw, tid, fixed, iters);
+  float acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = 0.f;
+#pragma unroll 1
+  for (int i0 = 0; i0 < QI; i0 += CH) {
+    if (i0 >= iters) break;
+    uint32_t v[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) v[j] = psi_t[(tid + NT * (i0 + j)) & (T - 1)];   // in bounds; masked by the sign table
+    float sum[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) sum[c] = 0.f;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const float2 f = unpack_h2(v[j]);
+      const float p = f.x * f.x + f.y * f.y;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) sum[c] += cs.mul(p, j, c);
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] += cs.flip(c, i0 / CH) ? -sum[c] : sum[c];
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float v = tid < T ? acc[c] : 0.f;     // T < NT: lanes past the tile read wrapped words
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[wave * CMAX + c] = v;
+  }
+  lds_barrier();
+  if (tid < a.C) {
+    float v = 0.f;
+    for (int w = 0; w < NW; ++w) v += red[w * CMAX + tid];
+    a.part[pidx + tid] = v / (a.scale * a.scale);
+  }
+}
+
+// Adjoint seed lambda = sum_c r_c Z_c psi on the interleaved image (word 2w = psi, 2w + 1 = lambda).
+template <int NC, int NT>
+__device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, int T, uint32_t fixed,
+                                       const float* rsc_s) {
+  constexpr int QI = (1 << TMAX) / NT;
+  constexpr int CH = QI < RCH ? QI : RCH;
+  const int iters = T >= NT ? T / NT : 1;
+  const ClassSigns<NC, CH> cs = class_signs<NC, NT, CH>(opw, tid, fixed, iters);
+  float r[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) r[c] = rsc_s[c];
+#pragma unroll 1
+  for (int i0 = 0; i0 < QI; i0 += CH) {
+    if (i0 >= iters) break;
+    uint32_t v[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) v[j] = tile[2 * ((tid + NT * (i0 + j)) & (T - 1))];   // in bounds; writes masked
+    float rr[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) rr[c] = cs.flip(c, i0 / CH) ? -r[c] : r[c];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      float fsum = 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) fsum += cs.mul(rr[c], j, c);
+      const float2 f = unpack_h2(v[j]);
+      const int w = tid + NT * (i0 + j);
+      if (i0 + j < iters && w < T) tile[2 * w + 1] = pack_h2(fsum * f.x, fsum * f.y);
+    }
+  }
+}
+
+// Class-count specialisations of the pass kernel: NCK >= C classes (1, 2, 3, 4 or 8).  Classes C..NCK-1 are
+// inert padding (zero observable masks, zero adjoint weights, no readout output).  One kernel per count, not a
+// switch inside one kernel: the arms of such a switch keep their uniform values live across the op loop and
+// push this kernel, which runs at the SGPR limit, into spilling scalars inside the group-op loops.
+__host__ __device__ constexpr int class_kernel(int C) { return C <= 4 ? C : 8; }
+
 __device__ __forceinline__ void lds_barrier_dma() {
   __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <bool ADJ>
-__global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArgs a) {
+// minimum waves per SIMD: forward 2 workgroups x 8 waves, adjoint 1 x 16 -> 4 (<= 128 VGPRs)
+template <bool ADJ, int NCK>
+__global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD, 4) hea_pass_kernel(PassArgs a) {
   constexpr int NT = ADJ ? NT_ADJ : NT_FWD, NW = NT / 64;
   // psi, or (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
   __shared__ __attribute__((aligned(16))) uint32_t tile[(ADJ ? 2 : 1) << TMAX];
@@ -500,7 +640,7 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
       float rho = 0.f;
       for (int c = 0; c < a.C; ++c) rho = fmaxf(rho, fabsf(a.wread[(size_t)s * a.C + c]));
       if (rho == 0.f) rho = 1.f;
-      for (int c = 0; c < a.C; ++c) rsc[c] = a.wread[(size_t)s * a.C + c] / rho;
+      for (int c = 0; c < NCK; ++c) rsc[c] = c < a.C ? a.wread[(size_t)s * a.C + c] / rho : 0.f;
       rsc[CMAX] = rho / (a.scale * a.scale);
     }
   }
@@ -594,72 +734,10 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD) hea_pass_kernel(PassArg
         ++ngrad;
       }
     } else if (ADJ && code == OP_OBS) {
-      // sign_c(w) = parity(w & O'_c) ^ parity(fixed & O_c) = per-thread part ^ per-iteration (uniform) part
-      uint32_t om[CMAX], sgn0 = 0;
-#pragma unroll
-      for (int c = 0; c < CMAX; ++c) {
-        om[c] = c < a.C ? (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_OFF + c]) : 0u;
-        const uint32_t of = c < a.C ? (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_RFULL + 2 * c]) : 0u;
-        sgn0 |= (uint32_t)(par((uint32_t)tid & om[c]) ^ par(fixed & of)) << c;
-      }
-      const int iters = (T + NT - 1) / NT;
-#pragma unroll 4
-      for (int i = 0; i < iters; ++i) {
-        const int w = tid + NT * i;
-        if (w >= T) continue;
-        float fsum = 0.f;
-#pragma unroll
-        for (int c = 0; c < CMAX; ++c) {
-          if (c < a.C) {
-            const uint32_t sg = ((sgn0 >> c) & 1u) ^ (uint32_t)par((uint32_t)(NT * i) & om[c]);
-            fsum += sg ? -rsc[c] : rsc[c];
-          }
-        }
-        uint2 pl = *(const uint2*)&tile[2 * w];   // (psi, lambda) pair of word w
-        const float2 v = unpack_h2(pl.x);
-        pl.y = pack_h2(fsum * v.x, fsum * v.y);
-        *(uint2*)&tile[2 * w] = pl;
-      }
+      obs_op<NCK, NT>(tile, opw, tid, T, fixed, rsc);
     } else if (!ADJ && code == OP_READOUT) {
-      uint32_t om[CMAX], sgn0 = 0;
-#pragma unroll
-      for (int c = 0; c < CMAX; ++c) {
-        om[c] = c < a.C ? (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_OFF + c]) : 0u;
-        const uint32_t of = c < a.C ? (uint32_t)__builtin_amdgcn_readfirstlane(opw[W_RFULL + 2 * c]) : 0u;
-        sgn0 |= (uint32_t)(par((uint32_t)tid & om[c]) ^ par(fixed & of)) << c;
-      }
-      float acc[CMAX];
-#pragma unroll
-      for (int c = 0; c < CMAX; ++c) acc[c] = 0.f;
-      const int iters = (T + NT - 1) / NT;
-#pragma unroll 4
-      for (int i = 0; i < iters; ++i) {
-        const int w = tid + NT * i;
-        if (w >= T) continue;
-        const float2 v = unpack_h2(psi_t[w]);
-        const float p = v.x * v.x + v.y * v.y;
-#pragma unroll
-        for (int c = 0; c < CMAX; ++c) {
-          if (c < a.C) {
-            const uint32_t sg = ((sgn0 >> c) & 1u) ^ (uint32_t)par((uint32_t)(NT * i) & om[c]);
-            acc[c] += sg ? -p : p;
-          }
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < CMAX; ++c) {
-        if (c < a.C) {
-          float v = acc[c];
-          for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-          if (lane == 0) red[wave * CMAX + c] = v;
-        }
-      }
-      lds_barrier();
-      if (tid < a.C) {
-        float v = 0.f;
-        for (int w = 0; w < NW; ++w) v += red[w * CMAX + tid];
-        a.part[((size_t)s * a.n_tiles + tile_id) * a.C + tid] = v / (a.scale * a.scale);
-      }
+      const size_t pidx = ((size_t)s * a.n_tiles + tile_id) * a.C;
+      readout_op<NCK, NT>(psi_t, a, opw, tid, lane, wave, T, fixed, red, pidx);
     }
   }
   lds_barrier();
@@ -795,10 +873,21 @@ extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_sample
   if (a.t > hea::TMAX || a.t < 8 || a.C > hea::CMAX || a.n > 30 || a.c < 2) return -2;
   const unsigned grid = (unsigned)(n_samples * a.n_tiles);
   if (grid == 0) return 0;
-  if (adjoint)
-    hipLaunchKernelGGL(hea::hea_pass_kernel<true>, dim3(grid), dim3(hea::NT_ADJ), 0, st, a);
-  else
-    hipLaunchKernelGGL(hea::hea_pass_kernel<false>, dim3(grid), dim3(hea::NT_FWD), 0, st, a);
+#define HEA_LAUNCH(NCK)                                                                                     \
+  do {                                                                                                     \
+    if (adjoint)                                                                                           \
+      hipLaunchKernelGGL((hea::hea_pass_kernel<true, NCK>), dim3(grid), dim3(hea::NT_ADJ), 0, st, a);      \
+    else                                                                                                   \
+      hipLaunchKernelGGL((hea::hea_pass_kernel<false, NCK>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);     \
+  } while (0)
+  switch (hea::class_kernel(a.C)) {
+    case 1: HEA_LAUNCH(1); break;
+    case 2: HEA_LAUNCH(2); break;
+    case 3: HEA_LAUNCH(3); break;
+    case 4: HEA_LAUNCH(4); break;
+    default: HEA_LAUNCH(8); break;
+  }
+#undef HEA_LAUNCH
   return (int)hipGetLastError();
 }
 

@@ -109,3 +109,18 @@ def test_hea_24q_three_passes_match_valu_engine(cuda):
     torch.cuda.synchronize()
     np.testing.assert_allclose(z.cpu().reshape(K, B, -1).numpy(), z_ref.cpu().numpy(), atol=3e-3)
     np.testing.assert_allclose(g.cpu().numpy(), g_ref.cpu().numpy(), atol=3e-3)
+
+
+@pytest.mark.parametrize("C,tile", [(2, 14), (4, 8), (5, 14), (8, 9), (8, 14)])
+def test_hea_class_counts_match_dense(cuda, C, tile):
+    """Readout / observable ops are specialised per class count (register sign tables up to 4 classes,
+    scalar bit masks above; tiles smaller than a workgroup's word stride at tile_bits 8)."""
+    spec = VQCSpec(10, 2, C)
+    prog = HeaMfmaProgram(spec, cuda, tile_bits=tile)
+    K, B = 2, 3
+    x, params, wr = _inputs(spec, K, B, seed=C)
+    ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
+    z, g = prog.vjp(x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(z.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
+    np.testing.assert_allclose(g.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
