@@ -72,6 +72,16 @@ __device__ __forceinline__ float2 unpack_h2(uint32_t u) {
 
 __device__ __forceinline__ int par(uint32_t x) { return __builtin_popcount(x) & 1; }
 
+// round(y) as int64 in single precision (|y| < 2^62): the rounded value splits exactly into 2^32 hi + lo with
+// lo in [0, 2^32).  Seven fp32 VALU ops instead of the fp64 multiply / round / split chain (the gradient
+// partials are fixed point at 2^-32 of their scale; fp32 keeps 24 of their bits, the fp16 state ~11).
+__device__ __forceinline__ long long fix64(float y) {
+  const float r = __builtin_rintf(y);
+  const float hf = __builtin_floorf(r * 0x1p-32f);
+  const float lf = __builtin_fmaf(hf, -0x1p32f, r);
+  return (long long)(((unsigned long long)(unsigned int)(int)hf << 32) | (unsigned long long)(unsigned int)lf);
+}
+
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup fence and so also drains every
 // outstanding GLOBAL load (vmcnt(0)) - including the next op's prefetched record and unitary fragments.
 // Cross-wave data here only moves through LDS, so completing this wave's LDS (and scalar) operations before
@@ -384,9 +394,15 @@ __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw
 // DMA is complete once the issuing wave has passed s_waitcnt vmcnt(0) (lds_barrier_dma).
 __device__ __forceinline__ void dma_frags(const PassArgs& a, int k, int fi, int tid, int wave, uint4* slot) {
   if (fi < 0 || wave >= 4) return;
-  const uint4* fr = (const uint4*)a.frags + ((size_t)k * a.n_slots * 4 + fi) * 128;
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(fr + tid),
-                                   (__attribute__((address_space(3))) void*)(slot + 64 * wave), 16, 0, 0);
+  const uint4* fr = (const uint4*)a.frags + ((size_t)k * a.n_slots * 4 + fi) * 128 + tid;
+  // Issued as inline asm: the compiler's wait-count pass cannot tell which LDS bytes a builtin DMA writes (no
+  // alias scopes reach codegen), so it waited for the DMA before the op's first LDS store or atomic and exposed
+  // the fragment latency in every op.  The slot is only read after lds_barrier_dma's vmcnt(0) + barrier, and a
+  // vector-memory op unknown to the pass can only make its other waits longer, never shorter.
+  const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)(slot + 64 * wave);
+  __asm__ volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(fr),
+                   "s"(__builtin_amdgcn_readfirstlane(lds))
+                   : "memory", "m0");
 }
 
 // Readout / observable ops walk the tile words w = tid + NT i (i < T / NT).  The sign of class c at word w is
@@ -716,15 +732,15 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD, 4) hea_pass_kernel(Pass
         // reduced to partial traces once at the end of the pass).  Integer addition is associative, so the sums
         // are bitwise independent of the order the waves (and, in hea_grad_reduce, samples and tiles) arrive.
         // Lane (g4, cl) holds N[4 g4 + i][cl]; entry slot: b == a -> b, b ^ a == e_j -> 16 + 16 j + b.
-        const double sc = (double)rsc[CMAX] * FIX;
+        const float sc = (float)((double)rsc[CMAX] * FIX);
         unsigned long long* rg = red64 + ngrad * RSTR;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15, d = bb ^ aa;
           if (__builtin_popcount(d) <= 1) {
             const int e = d == 0 ? (int)bb : 16 + 16 * (__builtin_ctz(d)) + (int)bb;
-            atomicAdd(&rg[red_slot(e)], (unsigned long long)__double2ll_rn((double)accR[i] * sc));
-            atomicAdd(&rg[RIM + red_slot(e)], (unsigned long long)__double2ll_rn((double)accI[i] * sc));
+            atomicAdd(&rg[red_slot(e)], (unsigned long long)fix64(accR[i] * sc));
+            atomicAdd(&rg[RIM + red_slot(e)], (unsigned long long)fix64(accI[i] * sc));
           }
         }
         if (tid == 0) {
