@@ -78,6 +78,7 @@ def make_config(args):
     cfg.privacy.noise_multiplier = 1.0
     cfg.runtime.backend = args.backend
     cfg.runtime.device = args.device
+    cfg.runtime.dist_backend = getattr(args, "dist_backend", "auto")
     return cfg
 
 
@@ -116,6 +117,9 @@ def main():
     ap.add_argument("--dp", action="store_true")
     ap.add_argument("--backend", default="auto")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="process-group backend (auto: nccl = RCCL on GPUs, gloo on CPU); gloo on GPUs lets "
+                         "several ranks share one GPU in tests")
     ap.add_argument("--engine", default="mfma", choices=["mfma", "valu"],
                     help="mfma: fp16-state MFMA group-unitary engine (ops/hea_mfma.py); valu: fp32 pass engine")
     args = ap.parse_args()
