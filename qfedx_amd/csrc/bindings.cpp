@@ -64,7 +64,7 @@ int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, co
                            int p_stride, float* gpart, hipStream_t st);
 int qfx_grad_split(int tps, int spc);
 int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct, const float* nvalid,
-                          const float* act, int n, double samples, double steps, hipStream_t st);
+                          const float* act, int n, hipStream_t st);
 int qfx_launch_round_apply(const long long* buf, int P, float* theta, double lr, double* out, hipStream_t st);
 int qfx_fedavg_norm_scratch(int K, int P);
 int qfx_launch_adam(float* p, const float* g, float* m, float* v, const float* t_in, float* t_out,
@@ -210,14 +210,14 @@ void readout_sum(torch::Tensor part, int64_t tps, int64_t C, int64_t n_samples, 
 int64_t grad_split(int64_t tps, int64_t spc) { return qfx_grad_split((int)tps, (int)spc); }
 
 void round_pack(torch::Tensor buf, int64_t P, torch::Tensor loss, torch::Tensor correct, torch::Tensor nvalid,
-                torch::Tensor act, double samples, double steps) {
+                torch::Tensor act) {
   need(buf, torch::kInt64, "buf");
   for (auto* x : {&loss, &correct, &nvalid, &act}) need(*x, torch::kFloat32, "round_pack metric");
   const int64_t n = loss.numel();
   if (buf.numel() < P + 5 || correct.numel() < n || nvalid.numel() < n || act.numel() < n)
     throw std::invalid_argument("round_pack: sizes");
   check(qfx_launch_round_pack(ptr<long long>(buf), (int)P, ptr<float>(loss), ptr<float>(correct), ptr<float>(nvalid),
-                              ptr<float>(act), (int)n, samples, steps, cur_stream()),
+                              ptr<float>(act), (int)n, cur_stream()),
         "qfx_round_pack");
 }
 

@@ -368,21 +368,35 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
 }
 
 // round epilogue 1: metrics -> exact fixed point in the all-reduce buffer tail, fixed summation order
-//   buf[P+1..P+4] = round(2^32 * [sum loss*nvalid, sum correct*act, samples, steps])
-__global__ void qfx_round_pack_kernel(long long* __restrict__ buf, int P, const float* __restrict__ loss,
-                                      const float* __restrict__ correct, const float* __restrict__ nvalid,
-                                      const float* __restrict__ act, int n, double samples, double steps) {
-  if (threadIdx.x != 0) return;
-  double ls = 0.0, cs = 0.0;
-  for (int i = 0; i < n; ++i) {
-    ls += (double)loss[i] * (double)nvalid[i];
-    cs += (double)correct[i] * (double)act[i];
+//   buf[P+1..P+4] = round(2^32 * [sum loss*nvalid, sum correct*act, sum nvalid (samples), sum act (steps)])
+// Everything comes from device tables (nothing round-dependent is a kernel argument), so the launch can sit
+// inside a captured round graph.  One 256-thread block: strided float64 partials, then a fixed-shape tree.
+__global__ void __launch_bounds__(256) qfx_round_pack_kernel(long long* __restrict__ buf, int P,
+                                                             const float* __restrict__ loss,
+                                                             const float* __restrict__ correct,
+                                                             const float* __restrict__ nvalid,
+                                                             const float* __restrict__ act, int n) {
+  __shared__ double red[4][256];
+  const int t = threadIdx.x;
+  double ls = 0.0, cs = 0.0, ns = 0.0, as = 0.0;
+  for (int i = t; i < n; i += 256) {
+    const double nv = (double)nvalid[i], ac = (double)act[i];
+    ls += (double)loss[i] * nv;
+    cs += (double)correct[i] * ac;
+    ns += nv;
+    as += ac;
   }
-  const double SC = 4294967296.0;
-  buf[P + 1] = llrint(ls * SC);
-  buf[P + 2] = llrint(cs * SC);
-  buf[P + 3] = llrint(samples * SC);
-  buf[P + 4] = llrint(steps * SC);
+  red[0][t] = ls;
+  red[1][t] = cs;
+  red[2][t] = ns;
+  red[3][t] = as;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (t < h)
+      for (int j = 0; j < 4; ++j) red[j][t] += red[j][t + h];
+    __syncthreads();
+  }
+  if (t < 4) buf[P + 1 + t] = llrint(red[t][0] * 4294967296.0);
 }
 
 // round epilogue 2 (after the all-reduce): theta += lr * (sum w Delta) / (sum w) in float64, rounded to
@@ -410,10 +424,8 @@ using namespace qfx;
 extern "C" int qfx_fedavg_norm_scratch(int K, int P) { return K * (1 + (P + NORM_CHUNK - 1) / NORM_CHUNK); }
 
 extern "C" int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct,
-                                     const float* nvalid, const float* act, int n, double samples, double steps,
-                                     hipStream_t st) {
-  hipLaunchKernelGGL(qfx_round_pack_kernel, dim3(1), dim3(64), 0, st, buf, P, loss, correct, nvalid, act, n, samples,
-                     steps);
+                                     const float* nvalid, const float* act, int n, hipStream_t st) {
+  hipLaunchKernelGGL(qfx_round_pack_kernel, dim3(1), dim3(256), 0, st, buf, P, loss, correct, nvalid, act, n);
   return (int)hipGetLastError();
 }
 

@@ -71,7 +71,8 @@ class Aggregator:
 
     def local_reduce(self, theta_k: torch.Tensor, theta_g: torch.Tensor, weights: torch.Tensor,
                      round_num: int, client_ids: list, participants: Optional[list] = None,
-                     dropped: Optional[list] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     dropped: Optional[list] = None, out: Optional[torch.Tensor] = None,
+                     keys: Optional[torch.Tensor] = None) -> torch.Tensor:
         """This rank's contribution [P+1] = [sum_k w_k priv(Delta_k) | sum_k w_k].
 
         float64 normally; int64 ring elements (mod 2^bits, masked) under secure aggregation.
@@ -85,7 +86,7 @@ class Aggregator:
             out, norms = fedavg_hip.fused_local_reduce(
                 theta_k, theta_g, weights, self._mask_u8, client_ids, round_num, self.seed,
                 wrap=self.wrap, dp=self.dp, clip_norm=self.clip_norm,
-                noise_multiplier=self.noise_multiplier, out=out)
+                noise_multiplier=self.noise_multiplier, out=out, keys=keys)
             self.last_norms = norms
             return out
         delta = theta_k.double() - theta_g.double()[None, :]

@@ -40,8 +40,10 @@ class CNNClientTrainer:
         correct = ((logits.argmax(-1) == yb) & (wts > 0)).sum(-1).float()
         return {"loss": loss.detach(), "grad": p.grad, "correct": correct}
 
-    def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int) -> dict:
-        """Same contract as ``VQCClientTrainer.run_round`` (per-step [S,K] loss/correct round buffers)."""
+    def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int,
+                  epilogue=None, extra=None) -> dict:
+        """Same contract as ``VQCClientTrainer.run_round`` (per-step [S,K] loss/correct round buffers, optional
+        ``extra`` per-client tables and device ``epilogue``, here run eagerly)."""
         cfg = self.cfg
         K = len(local_idx)
         P = theta_g.numel()
@@ -57,8 +59,13 @@ class CNNClientTrainer:
         nvalid = (plan.wts > 0).sum(-1).float() * plan.active
         if plan.idx.numel() and int(plan.idx.max()) >= max(1, store.nmax):
             raise RuntimeError("minibatch plan indexes past the client store")
-        dv = PackedUpload({"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active,
-                           "nvalid": nvalid, "w": store.counts[li].to(torch.float64)}).to_device(self.device)
+        tabs = {"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid,
+                "w": store.counts[li].to(torch.float64)}
+        for name, t in (extra or {}).items():
+            if name in tabs or t.shape[0] != K:
+                raise ValueError(f"extra table {name!r} must be a new per-client [K, ...] table")
+            tabs[name] = t
+        dv = PackedUpload(tabs).to_device(self.device)
         params = torch.empty(K, P, dtype=torch.float32, device=self.device)
         opt = BatchedOptimizer(cfg.optimizer if cfg.optimizer != "spsa" else "sgd", (K, P), self.device,
                                cfg.learning_rate, cfg.momentum, backend=self.backend, zero_init=False)
@@ -88,6 +95,8 @@ class CNNClientTrainer:
             opt.step(params, res["grad"], dv["act"][s])
             loss_all[s].copy_(res["loss"])
             correct_all[s].copy_(res["correct"])
+        if epilogue is not None:
+            epilogue(params, dict(dv, loss=loss_all, correct=correct_all), theta_g.to(self.device).float())
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
                 "lid": dv["lid"], "weights": dv["w"], "samples": float(nvalid.sum()), "steps": int(sum(plan.steps_per_client)),
                 "client_ids": cids, "n_samples": store.counts[li].to(torch.float64)}

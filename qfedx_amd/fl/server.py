@@ -205,35 +205,48 @@ class FederatedRunner:
         t0 = time.perf_counter()
         dev = self.device
         P = self.P
-        with self.timer.phase("local_train"):
-            res = self.adapter.trainer.run_round(self.store, local_alive, self.params, r)
         ids = [self.local_ids[i] for i in local_alive]
         fast = self.backend == "hip" and not p.secure_agg and self.server_opt is None
-        with self.timer.phase("aggregate"):
+        trainer = self.adapter.trainer
+        if fast:
+            # round epilogue on the device, run by the trainer right after the local steps (captured into the
+            # round's hipGraph): the fused local reduce writes the head of the all-reduce buffer and a pack
+            # kernel appends the fixed-point metrics.  Round-dependent inputs (DP noise keys, uniform FedAvg
+            # weights) travel as per-client tables with the round's upload, never as kernel arguments.
+            if getattr(self, "_round_buf", None) is None:
+                self._round_buf = torch.zeros(P + 5, dtype=torch.int64, device=dev)
+            buf = self._round_buf
+            extra = {}
+            if p.dp and ids:
+                from ..ops.fedavg_hip import dp_noise_keys
+                extra["dpkeys"] = dp_noise_keys(ids, r, self.noise_seed)
             if t.weighting == "uniform":
-                w = torch.ones(len(local_alive), dtype=torch.float64, device=dev)
-            elif "weights" in res:            # uploaded with the round's tables (no gather launch)
-                w = res["weights"]
-            else:
-                if getattr(self, "_counts_dev", None) is None:
-                    self._counts_dev = self.store.counts.to(torch.float64).to(dev)
-                w = self._counts_dev[res["lid"]]
-            if fast:
-                # round epilogue on the device: fused local reduce writes the head of the all-reduce
-                # buffer, one kernel appends the fixed-point metrics (no host values, no extra copies)
-                if getattr(self, "_round_buf", None) is None:
-                    self._round_buf = torch.zeros(P + 5, dtype=torch.int64, device=dev)
-                buf = self._round_buf
-                if local_alive:
-                    self.aggregator.local_reduce(res["params"], self.params, w, r, ids, participants=participants,
-                                                 dropped=dropped, out=buf[: P + 1])
-                    from ..ops._ext import ext
-                    ext().round_pack(buf, P, res["loss"].reshape(-1), res["correct"].reshape(-1),
-                                     res["nvalid"].reshape(-1), res["act"].reshape(-1), float(res["samples"]),
-                                     float(res["steps"]))
+                extra["fw"] = torch.ones(len(ids), dtype=torch.float64)
+            agg = self.aggregator
+
+            def epilogue(params_k, tabs, theta):
+                agg.local_reduce(params_k, theta, tabs.get("fw", tabs["w"]), r, ids, out=buf[: P + 1],
+                                 keys=tabs.get("dpkeys"))
+                from ..ops._ext import ext
+                ext().round_pack(buf, P, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
+                                 tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1))
+            with self.timer.phase("local_train"):
+                res = trainer.run_round(self.store, local_alive, self.params, r, epilogue=epilogue,
+                                        extra=extra or None)
+            if not local_alive:
+                buf.zero_()
+        else:
+            with self.timer.phase("local_train"):
+                res = trainer.run_round(self.store, local_alive, self.params, r)
+            with self.timer.phase("aggregate"):
+                if t.weighting == "uniform":
+                    w = torch.ones(len(local_alive), dtype=torch.float64, device=dev)
+                elif "weights" in res:            # uploaded with the round's tables (no gather launch)
+                    w = res["weights"]
                 else:
-                    buf.zero_()
-            else:
+                    if getattr(self, "_counts_dev", None) is None:
+                        self._counts_dev = self.store.counts.to(torch.float64).to(dev)
+                    w = self._counts_dev[res["lid"]]
                 if local_alive:
                     contrib = self.aggregator.local_reduce(res["params"], self.params, w, r, ids,
                                                            participants=participants, dropped=dropped)

@@ -149,18 +149,19 @@ def graph_bucket(k: int, k_max: int) -> int:
 def _pad_clients(tabs: dict, kp: int) -> dict:
     """Extend a round's client tables to ``kp`` clients with inactive rows: store slot of client 0, minibatch
     index 0, loss weight 0, step mask 0, FedAvg weight 0 (the optimizer leaves them untouched, the readout
-    writes zero loss / hits for them)."""
+    writes zero loss / hits for them); any other per-client table (first dim K) is zero-padded."""
     K = tabs["lid"].shape[0]
     if kp <= K:
         return tabs
     n = kp - K
-    out = dict(tabs)
-    out["lid"] = torch.cat([tabs["lid"], tabs["lid"][:1].expand(n)])
-    out["idx"] = torch.cat([tabs["idx"], torch.zeros_like(tabs["idx"][:, :1]).expand(-1, n, -1)], 1)
-    out["wts"] = torch.cat([tabs["wts"], torch.zeros_like(tabs["wts"][:, :1]).expand(-1, n, -1)], 1)
-    out["act"] = torch.cat([tabs["act"], torch.zeros_like(tabs["act"][:, :1]).expand(-1, n)], 1)
-    out["nvalid"] = torch.cat([tabs["nvalid"], torch.zeros_like(tabs["nvalid"][:, :1]).expand(-1, n)], 1)
-    out["w"] = torch.cat([tabs["w"], torch.zeros(n, dtype=tabs["w"].dtype)])
+    out = {}
+    for name, t in tabs.items():
+        if name == "lid":
+            out[name] = torch.cat([t, t[:1].expand(n)])
+        elif name in ("idx", "wts", "act", "nvalid"):              # [S, K, ...] step tables
+            out[name] = torch.cat([t, torch.zeros_like(t[:, :1]).expand(-1, n, *t.shape[2:])], 1)
+        else:                                                      # [K, ...] per-client tables (FedAvg weights, keys)
+            out[name] = torch.cat([t, torch.zeros((n,) + tuple(t.shape[1:]), dtype=t.dtype)])
     return out
 
 
@@ -249,12 +250,19 @@ class VQCClientTrainer:
             opt.step(params, res["grad"], act_d[s])
         return params, loss_all, correct_all
 
-    def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int) -> dict:
+    def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int,
+                  epilogue=None, extra: Optional[dict] = None) -> dict:
         """Train clients ``store[local_idx]`` from the global params.
 
         Returns device tensors: ``params`` [K,P], ``loss`` / ``correct`` [S,K] per step, ``nvalid`` /
         ``act`` [S,K] (valid samples / active flag per client and step), ``lid`` [K] (store slots), plus
-        host scalars ``samples`` / ``steps`` and ``n_samples`` (cpu, for weighting)."""
+        host scalars ``samples`` / ``steps`` and ``n_samples`` (cpu, for weighting).
+
+        ``extra``: more per-client host tables [K, ...] uploaded with the round's tables (e.g. DP noise keys).
+        ``epilogue(params, tables, theta)``: device work run right after the local steps, on the trained
+        params (possibly padded with inactive weight-0 rows), the round's device tables and the global params;
+        on the hipGraph path it is captured into the round graph, so it may only launch device work on static
+        buffers (no host values that change per round)."""
         cfg = self.cfg
         K = len(local_idx)
         P = theta_g.numel()
@@ -277,6 +285,10 @@ class VQCClientTrainer:
         graphed = self.use_graph and method == "adjoint" and noise is None
         tabs = {"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid,
                 "w": store.counts[li].to(torch.float64)}   # FedAvg sample-count weights
+        for name, t in (extra or {}).items():
+            if name in tabs or t.shape[0] != K:
+                raise ValueError(f"extra table {name!r} must be a new per-client [K, ...] table")
+            tabs[name] = t
         if graphed:
             tabs = _pad_clients(tabs, graph_bucket(K, len(store)))
         up = PackedUpload(tabs)
@@ -285,16 +297,19 @@ class VQCClientTrainer:
             traj_keys = noise.client_keys("noise_traj", round_num, cids, self.device)
             ro_keys = noise.client_keys("shots", round_num, cids, self.device)
         if graphed:
-            params, loss_all, correct_all, dv = self._graphed(store, up, theta_g, plan, round_num)
+            params, loss_all, correct_all, dv = self._graphed(store, up, theta_g, plan, round_num, epilogue)
             # padding clients (inactive, weight 0) only fill the captured shape: the FedAvg reduce sees the
             # K real rows; their [S, Kpad] metric columns are all zero
             params = params[:K]
             dv = dict(dv, w=dv["w"][:K], lid=dv["lid"][:K])
         else:
             dv = up.to_device(self.device)
-            params, loss_all, correct_all = self._body(store.X, store.y, dv["lid"], theta_g.to(self.device), dv["idx"],
+            theta = theta_g.to(self.device)
+            params, loss_all, correct_all = self._body(store.X, store.y, dv["lid"], theta, dv["idx"],
                                                        dv["wts"], dv["act"], plan.max_steps, round_num, method,
                                                        traj_keys, ro_keys)
+            if epilogue is not None:
+                epilogue(params, dict(dv, loss=loss_all, correct=correct_all), theta)
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
                 "lid": dv["lid"], "weights": dv["w"], **common}
 
@@ -303,42 +318,55 @@ class VQCClientTrainer:
     def use_graph(self) -> bool:
         return self.backend == "hip" and self.device.type == "cuda" and getattr(self, "graphs", True)
 
-    def _graphed(self, store, up, theta_g, plan, round_num):
+    def _graphed(self, store, up, theta_g, plan, round_num, epilogue=None):
         """Replay the whole round as ONE hipGraph (static shapes: #clients, steps, batch).
 
         Captured once per SHAPE, not per client set: each round ONE async copy refreshes the packed
-        static input buffer (client slots, minibatch indices, loss weights, step masks), the global params
-        are copied in, and the captured launches gather every step's minibatches from the (static) client
-        store by slot, so client sampling reuses the graph.  A small LRU bounds the number of live graphs.
+        static input buffer (client slots, minibatch indices, loss weights, step masks), and the captured
+        launches gather every step's minibatches from the (static) client store by slot, so client sampling
+        reuses the graph.  The global params are read in place when they are a float32 device tensor (the
+        runner updates them in place after the collective; a new tensor means a new graph), otherwise copied
+        into a static buffer.  ``epilogue`` (the round's fused FedAvg reduce + metrics pack) is captured after
+        the local steps, so the whole pre-collective round is one graph launch.  A small LRU bounds the live
+        graphs.
         """
         K = up.layout[0][4][0]
-        key = (K, plan.max_steps, plan.B, store.nmax, store.X.data_ptr())
-        cache = self.__dict__.setdefault("_graph_cache", {})
         dev = self.device
+        direct = theta_g.is_cuda and theta_g.dtype == torch.float32 and theta_g.is_contiguous()
+        key = (K, plan.max_steps, plan.B, store.nmax, store.X.data_ptr(), tuple(l[0] for l in up.layout),
+               theta_g.data_ptr() if direct else None, epilogue is not None)
+        cache = self.__dict__.setdefault("_graph_cache", {})
         ent = cache.pop(key, None)
         if ent is None:
             pack = torch.empty(up.nbytes, dtype=torch.uint8, device=dev)
             dv = up.to_device(dev, pack)
-            ent = {"pack": pack, "dv": dv, "theta": theta_g.to(dev).float().clone()}
+            ent = {"pack": pack, "dv": dv, "theta": theta_g if direct else theta_g.to(dev).float().clone()}
             args = (store.X, store.y, dv["lid"], ent["theta"], dv["idx"], dv["wts"], dv["act"], plan.max_steps,
                     round_num, "adjoint")
+
+            def body():
+                out = self._body(*args)
+                if epilogue is not None:
+                    epilogue(out[0], dict(dv, loss=out[1], correct=out[2]), ent["theta"])
+                return out
             # the graph owns its workspaces: eager calls (evaluation) can never regrow/free them
             ent["ws"] = {}
             with self.engine.hip.private_workspace(ent["ws"]):
                 side = torch.cuda.Stream(device=dev)
                 side.wait_stream(torch.cuda.current_stream(dev))
                 with torch.cuda.stream(side):       # warm-up: JIT modules loaded, workspaces sized
-                    self._body(*args)
+                    body()
                 torch.cuda.current_stream(dev).wait_stream(side)
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g):
-                    ent["out"] = self._body(*args)
+                    ent["out"] = body()
             ent["graph"] = g
             while len(cache) >= 4:                  # LRU: drop the oldest shape
                 cache.pop(next(iter(cache)))
         else:
             dv = up.to_device(dev, ent["pack"])     # one H2D copy for all the round's tables
         cache[key] = ent                            # most recently used last
-        ent["theta"].copy_(theta_g.float())
+        if not direct:
+            ent["theta"].copy_(theta_g.float())
         ent["graph"].replay()
         return (*ent["out"], ent["dv"])

@@ -20,18 +20,28 @@ def sgdm_step(params, grads, buf, t_in, t_out, active, lr, mu) -> None:
 _NO_KEYS = {}
 
 
+def dp_noise_keys(client_ids, round_num, seed) -> torch.Tensor:
+    """Host int32 [K, 2] Philox keys of the clients' DP noise in round ``round_num``."""
+    return torch.tensor([philox_key(seed, "dp_noise", round_num, int(c)) for c in client_ids],
+                        dtype=torch.int64).reshape(-1, 2).to(torch.int32)
+
+
 def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp, clip_norm,
-                       noise_multiplier, out=None):
+                       noise_multiplier, out=None, keys=None):
     """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as exact int64 fixed point (scale 2^32)
     [P+1] (per-client terms rounded before the sum -> rank-count invariant), plus norms [K].
     ``angle_mask`` uint8 [P] on the device; ``out`` an optional int64 [P+1] destination (e.g. the head
-    of the round's all-reduce buffer).  DP noise keys are only built / uploaded when DP is on."""
+    of the round's all-reduce buffer).  DP noise keys are only built / uploaded when DP is on; ``keys``
+    (device int32 [K, 2], ``dp_noise_keys``) passes them in already on the device, which keeps the launch
+    free of host values that change per round (capturable into a round graph)."""
     K, P = theta_k.shape
     dev = theta_k.device
-    if dp:
-        keys = torch.tensor([w for c in client_ids for w in philox_key(seed, "dp_noise", round_num, int(c))],
-                            dtype=torch.int64).to(torch.int32)
-        keys = h2d(keys, dev)
+    if dp and keys is not None:
+        if keys.numel() < 2 * K or keys.dtype != torch.int32 or keys.device != dev:
+            raise ValueError("DP keys must be a device int32 [K, 2] tensor")
+        keys = keys.reshape(-1).contiguous()
+    elif dp:
+        keys = h2d(dp_noise_keys(client_ids, round_num, seed).reshape(-1), dev)
     else:
         keys = _NO_KEYS.setdefault(dev, torch.zeros(0, dtype=torch.int32, device=dev))
     norms = torch.empty(ext().fedavg_norm_scratch(K, P), dtype=torch.float64, device=dev)   # [K] + scratch

@@ -256,3 +256,29 @@ def test_graph_bucket_and_client_padding():
         assert torch.equal(out[key][:, :K], tabs[key]) and not out[key][:, K:].any()
     assert out["w"].tolist() == [3.0, 4.0, 5.0, 0, 0, 0, 0, 0] and out["w"].dtype == torch.float64
     assert _pad_clients(tabs, 3) is tabs
+
+
+def test_trainer_epilogue_and_extra_tables():
+    """The trainer runs a device epilogue right after the local steps on the trained params, with the round's
+    tables (plus caller-provided per-client ``extra`` tables); the server's fused FedAvg uses this hook."""
+    from qfedx_amd.api import setup
+    from qfedx_amd.data.datasets import build_federated_data
+    from qfedx_amd.fl.adapters import make_adapter
+    from qfedx_amd.fl.trainer import ShardStore
+    cfg = small_cfg(num_clients=3)
+    device, backend, world = setup(cfg)
+    data = build_federated_data(cfg)
+    adapter = make_adapter(cfg, device, backend)
+    store = ShardStore(data.clients, data.client_ids, device)
+    theta = adapter.init_params(0)
+    seen = {}
+
+    def epi(params, tabs, th):
+        seen.update(params=params.clone(), keys=tabs["dpkeys"].clone(), loss=tabs["loss"].clone(), theta=th)
+
+    keys = torch.arange(4, dtype=torch.int32).reshape(2, 2)
+    res = adapter.trainer.run_round(store, [0, 2], theta, 0, epilogue=epi, extra={"dpkeys": keys})
+    assert torch.equal(seen["params"], res["params"]) and torch.equal(seen["keys"], keys)
+    assert torch.equal(seen["loss"], res["loss"]) and torch.equal(seen["theta"], theta)
+    with pytest.raises(ValueError):
+        adapter.trainer.run_round(store, [0, 2], theta, 0, extra={"w": torch.ones(2)})
