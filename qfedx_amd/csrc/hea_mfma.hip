@@ -121,10 +121,10 @@ __device__ __forceinline__ uint4 quad_perm(uint4 v, uint32_t r) {
 // Global [mem order] <-> LDS [swizzled] tile copies: quad q = 4 (tid + NT i) of the tile sits at LDS dword
 // (q ^ h) & ~3 with its dwords permuted by h & 3, h = h(q >> 5) = h(tid >> 3) ^ h(4 NT / 32 * i).  All of a
 // thread's global loads are issued before its LDS writes.
-template <int NT>
+template <int NT, int TB = TMAX>
 __device__ __forceinline__ void load_tile(const PassArgs& a, const uint32_t* src, uint32_t* dst, int tid, int T,
                                           uint32_t h_q, uint32_t fixed) {
-  constexpr int MQ = (1 << TMAX) / (4 * NT);
+  constexpr int MQ = (1 << TB) / (4 * NT);
   uint4 v[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -141,10 +141,10 @@ __device__ __forceinline__ void load_tile(const PassArgs& a, const uint32_t* src
   }
 }
 
-template <int NT>
+template <int NT, int TB = TMAX>
 __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, const uint32_t* src, int tid, int T,
                                            uint32_t h_q, uint32_t fixed) {
-  constexpr int MQ = (1 << TMAX) / (4 * NT);
+  constexpr int MQ = (1 << TB) / (4 * NT);
   uint4 v[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -164,10 +164,10 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
 // Interleaved adjoint image (word 2w = psi, 2w + 1 = lambda of swizzled amplitude w): a quad's psi and
 // lambda dwords go to LDS as two 16-byte pair runs.  Without a lambda input the lambda words are zeroed (the
 // observable op writes them).
-template <int NT>
+template <int NT, int TB = TMAX>
 __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* psrc, const uint32_t* lsrc,
                                              uint32_t* tile, int tid, int T, uint32_t h_q, uint32_t fixed) {
-  constexpr int MQ = (1 << TMAX) / (4 * NT);
+  constexpr int MQ = (1 << TB) / (4 * NT);
   uint4 v[MQ], l[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -190,10 +190,10 @@ __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* 
   }
 }
 
-template <int NT>
+template <int NT, int TB = TMAX>
 __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, const uint32_t* tile, int tid, int T,
                                              uint32_t h_q, uint32_t fixed) {
-  constexpr int MQ = (1 << TMAX) / (4 * NT);
+  constexpr int MQ = (1 << TB) / (4 * NT);
   uint4 v[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -269,10 +269,10 @@ __device__ __forceinline__ void lds_st(uint32_t* tile, uint32_t byte, uint32_t v
 //   IL = false: forward psi image, NX = 1.
 //   IL = true : interleaved adjoint image; NX = 2 applies U to psi and lambda (one b64 read / write per
 //               amplitude pair), NX = 1 to component SEL only (pairs read, single dwords written).
-template <int NX, int NW, bool IL, int SEL>
+template <int NX, int NW, bool IL, int SEL, int TB = TMAX>
 __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, const int* opw, uint32_t fo, int lane,
                                             int wave, int nbw) {
-  constexpr int MAXB = (1 << (TMAX - 8)) / NW;   // column blocks per wave per op (t = 14: 64 blocks)
+  constexpr int MAXB = (1 << (TB - 8)) / NW;   // column blocks per wave per op (t = 14: 64 blocks)
   constexpr int SH = IL ? 3 : 2;
   static_assert(IL || NX == 1, "the forward image holds psi only");
   const int g4 = lane >> 4, cl = lane & 15;
@@ -358,10 +358,10 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
 // Gradient cross matrix N[b][a] += sum_col psi[b][col] conj(lam[a][col]) over the op's column blocks:
 // K = 16 columns x (re, im), lane (g4, cl) reads amplitude m = cl of columns 4 g4 .. 4 g4 + 3; accR / accI
 // end up holding N[4 g4 + i][cl] (real / imaginary).
-template <int NW>
+template <int NW, int TB = TMAX>
 __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw, uint32_t fo, int lane, int wave,
                                             int nbw, f4& accR, f4& accI) {
-  constexpr int MAXB = (1 << (TMAX - 8)) / NW;
+  constexpr int MAXB = (1 << (TB - 8)) / NW;
   const int g4 = lane >> 4, cl = lane & 15;
   const uint32_t om = (uint32_t)opw[W_OFF + cl] ^ fo;
   uint32_t gb[4];
@@ -434,9 +434,9 @@ struct ClassSigns {
   }
 };
 
-template <int NC, int NT, int CH>
+template <int NC, int NT, int CH, int TB = TMAX>
 __device__ __forceinline__ ClassSigns<NC, CH> class_signs(const int* opw, int tid, uint32_t fixed, int iters) {
-  constexpr int QI = (1 << TMAX) / NT;
+  constexpr int QI = (1 << TB) / NT;
   static_assert((QI / CH) * NC <= 32 && CH * NC <= 64, "class sign masks must fit one / two dwords");
   ClassSigns<NC, CH> cs;
   cs.sgn0 = 0;
@@ -507,13 +507,13 @@ __device__ __forceinline__ void readout_op(const uint32_t* psi_t, const PassArgs
 }
 
 // Adjoint seed lambda = sum_c r_c Z_c psi on the interleaved image (word 2w = psi, 2w + 1 = lambda).
-template <int NC, int NT>
+template <int NC, int NT, int TB = TMAX>
 __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, int T, uint32_t fixed,
                                        const float* rsc_s) {
-  constexpr int QI = (1 << TMAX) / NT;
+  constexpr int QI = (1 << TB) / NT;
   constexpr int CH = QI < RCH ? QI : RCH;
   const int iters = T >= NT ? T / NT : 1;
-  const ClassSigns<NC, CH> cs = class_signs<NC, NT, CH>(opw, tid, fixed, iters);
+  const ClassSigns<NC, CH> cs = class_signs<NC, NT, CH, TB>(opw, tid, fixed, iters);
   float r[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) r[c] = rsc_s[c];
@@ -544,30 +544,48 @@ __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, 
 // push this kernel, which runs at the SGPR limit, into spilling scalars inside the group-op loops.
 __host__ __device__ constexpr int class_kernel(int C) { return C <= 4 ? C : 8; }
 
+// This wave's own LDS operations complete (no workgroup barrier).
+__device__ __forceinline__ void lds_barrier_wave() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ void lds_barrier_dma() {
   __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// minimum waves per SIMD: forward 2 workgroups x 8 waves, adjoint 1 x 16 -> 4 (<= 128 VGPRs)
-template <bool ADJ, int NCK>
-__global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD, 4) hea_pass_kernel(PassArgs a) {
-  constexpr int NT = ADJ ? NT_ADJ : NT_FWD, NW = NT / 64;
-  // psi, or (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
-  __shared__ __attribute__((aligned(16))) uint32_t tile[(ADJ ? 2 : 1) << TMAX];
+// Phase timestamps of workgroups < 8 (scripts/hea_ablate.py): one per phase, read back as cycle deltas.
+#define HEA_MARK()                                                                                   \
+  do {                                                                                               \
+    if (dbg && tid == 0 && ndbg < 64) dbg[ndbg] = (long long)__builtin_readcyclecounter();           \
+    ++ndbg;                                                                                          \
+  } while (0)
+
+// Memory bits of tile tile_id outside the tile.
+__device__ __forceinline__ uint32_t tile_fixed(const PassArgs& a, int tile_id) {
+  const int w1 = a.lo - a.c;
+  return ((uint32_t)(tile_id & ((1 << w1) - 1)) << a.c) | ((uint32_t)(tile_id >> w1) << a.hi);
+}
+
+// The op's OFF base for the tile's fixed bits (their parities with the op's frame row masks).
+__device__ __forceinline__ uint32_t op_fo(const int* opw, uint32_t fixed) {
+  const int nreal = opw[W_NREAL];
+  int fpb = 0;
+  for (int j = 0; j < nreal; ++j) fpb |= par(fixed & (uint32_t)opw[W_RFULL + j]) << j;
+  return (uint32_t)opw[W_OFF + fpb];
+}
+
+// ------------------------------------------------------------------------------------------- forward pass
+// One workgroup per tile of 2^t <= 2^14 amplitudes: 8 waves and 64 KB of LDS, so two workgroups share a CU and
+// one's tile load overlaps the other's group ops (minimum waves per SIMD 4: <= 128 VGPRs).
+template <int NCK>
+__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
+  constexpr int NT = NT_FWD, NW = NT / 64;
+  __shared__ __attribute__((aligned(16))) uint32_t psi_t[1 << TMAX];   // fp16 (re, im), swizzled
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
   __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
   __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];   // op unitary fragments, double buffered
   __shared__ float red[NW * CMAX];
-  // per gradient op of the pass: the 80 cross-matrix entries a partial trace can use (b = a, and b = a ^ e_j),
-  // x (re, im), in 2^-32 fixed point; turned into partial traces once, at the end of the pass
-  __shared__ unsigned long long red64[ADJ ? MAXGRAD * RSTR : 1];
-  __shared__ int gops[ADJ ? MAXGRAD * 2 : 1];            // (slab index, nreal) of the pass' gradient ops
-  int ngrad = 0;
   __shared__ float2 wv[32][2];
   __shared__ float2 tabA[128];
   __shared__ float2 tabB[128];
-  __shared__ float rsc[CMAX + 2];
-  uint32_t* psi_t = tile;                                // forward image
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -575,23 +593,15 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD, 4) hea_pass_kernel(Pass
   const int k = s / a.spc;
   const int T = 1 << a.t;
   const size_t N = (size_t)1 << a.n;
-  const int w1 = a.lo - a.c;
-  const uint32_t fixed = ((uint32_t)(tile_id & ((1 << w1) - 1)) << a.c) | ((uint32_t)(tile_id >> w1) << a.hi);
+  const uint32_t fixed = tile_fixed(a, tile_id);
   const float* prm = a.params + (size_t)k * a.p_stride;
-  // swizzle / parity decomposition: word w = tid + NT i  ->  f(w >> 5) = f(tid >> 5) ^ f(16 i)  (h linear)
-  const uint32_t h_w = swz(a, (uint32_t)tid >> 5);        // for words tid + NT i
   long long* dbg = (a.dbg && blockIdx.x < 8) ? a.dbg + blockIdx.x * 64 : nullptr;
   int ndbg = 0;
-#define HEA_MARK()                                              \
-  do {                                                          \
-    if (dbg && tid == 0 && ndbg < 64) dbg[ndbg] = (long long)__builtin_readcyclecounter(); \
-    ++ndbg;                                                     \
-  } while (0)
   HEA_MARK();
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
 
   // ---------------------------------------------------------------- initial psi tile
-  if (!ADJ && a.gen) {              // adjoint passes always start from stored outputs
+  if (a.gen) {
     if (tid < a.n) {
       float2 w[2];
       l1_factor(a.xang[(size_t)s * a.x_stride + tid], prm[2 * tid], prm[2 * tid + 1], a.feature, w);
@@ -645,25 +655,11 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD, 4) hea_pass_kernel(Pass
         *(uint4*)&psi_t[4 * q] = out;
       }
     }
-  } else if (ADJ) {
-    load_tile_il<NT>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
-                     h_q, fixed);
   } else {
     load_tile<NT>(a, a.psi_in + (size_t)s * N, psi_t, tid, T, h_q, fixed);
   }
-  if (ADJ) {
-    if (tid == 0) {
-      float rho = 0.f;
-      for (int c = 0; c < a.C; ++c) rho = fmaxf(rho, fabsf(a.wread[(size_t)s * a.C + c]));
-      if (rho == 0.f) rho = 1.f;
-      for (int c = 0; c < NCK; ++c) rsc[c] = c < a.C ? a.wread[(size_t)s * a.C + c] / rho : 0.f;
-      rsc[CMAX] = rho / (a.scale * a.scale);
-    }
-  }
 
   // ---------------------------------------------------------------- op list
-  if (ADJ)
-    for (int e = tid; e < MAXGRAD * RSTR; e += NT) red64[e] = 0ull;
   const int ncol = T >> 4, nblk = ncol >> 4;
   const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
   // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op)
@@ -690,96 +686,203 @@ __global__ void __launch_bounds__(ADJ ? NT_ADJ : NT_FWD, 4) hea_pass_kernel(Pass
       dma_frags(a, k, fidx_s[o + 1], tid, wave, frag_s[(o + 1) & 1]);
     }
     const int code = opw[W_CODE];
-    const int nreal = opw[W_NREAL];
 #if QFX_CHECKS_ON
-    QFX_DCHECK(code >= OP_APPLY && code <= OP_BACK);
-    if (code != OP_OBS && code != OP_READOUT) {
-      QFX_DCHECK(nreal >= 0 && nreal <= 4);
+    QFX_DCHECK(code == OP_APPLY || code == OP_READOUT);
+    if (code == OP_APPLY) {
+      QFX_DCHECK(opw[W_NREAL] >= 0 && opw[W_NREAL] <= 4);
       QFX_DCHECK((uint32_t)opw[W_OFF + (lane & 15)] < (uint32_t)T);
       QFX_DCHECK((uint32_t)opw[W_BL + (lane & 31)] < (uint32_t)T);
       QFX_DCHECK((uint32_t)opw[W_BH + (lane & 31)] < (uint32_t)T);
-      // -1 = no unitary (cross-matrix-only gradient ops); every op that applies one names a fragment
-      QFX_DCHECK(fidx_s[o] >= -1 && fidx_s[o] < 4 * a.n_slots);
-      QFX_DCHECK(fidx_s[o] >= 0 || code == OP_GRAD || code == OP_GRAD_L1);
-      if (ADJ && code != OP_APPLY && code != OP_UNAPPLY_PSI && code != OP_UNAPPLY_LAM) {
-        QFX_DCHECK(opw[W_GIDX] >= 0 && opw[W_GIDX] < a.n_gradops);
-        QFX_DCHECK(ngrad < MAXGRAD);
-      }
+      QFX_DCHECK(fidx_s[o] >= 0 && fidx_s[o] < 4 * a.n_slots);
     } else {
-      QFX_DCHECK(nreal >= 1 && nreal <= a.C);
+      QFX_DCHECK(opw[W_NREAL] >= 1 && opw[W_NREAL] <= a.C);
     }
 #endif
-    if (code == OP_APPLY || code == OP_UNAPPLY_PSI || code == OP_UNAPPLY_LAM || code == OP_BACK ||
-        code == OP_GRAD || code == OP_GRAD_L1) {
-      int fpb = 0;
-      for (int j = 0; j < nreal; ++j) fpb |= par(fixed & (uint32_t)opw[W_RFULL + j]) << j;
-      const uint32_t fo = (uint32_t)opw[W_OFF + fpb];
-      if (code == OP_APPLY || code == OP_UNAPPLY_PSI) {
-        group_apply<1, NW, ADJ, 0>(tile, F, opw, fo, lane, wave, nbw);
-      } else if (ADJ && code == OP_UNAPPLY_LAM) {
-        group_apply<1, NW, true, 1>(tile, F, opw, fo, lane, wave, nbw);
-      } else if (ADJ) {   // OP_BACK / OP_GRAD / OP_GRAD_L1
-        f4 accR = {0.f, 0.f, 0.f, 0.f}, accI = {0.f, 0.f, 0.f, 0.f};
-        group_cross<NW>(tile, opw, fo, lane, wave, nbw, accR, accI);
-        if (code == OP_BACK) {
-          if (opw[W_FLAGS] & F_BACK_PSI)
-            group_apply<2, NW, true, 0>(tile, F, opw, fo, lane, wave, nbw);
-          else
-            group_apply<1, NW, true, 1>(tile, F, opw, fo, lane, wave, nbw);
-        }
-        // Cross-wave sum of the partial-trace entries of N, pre-scaled by the sample's rho / scale^2, in 2^-32
-        // fixed point with 64-bit LDS atomics into this op's own region (no barrier, no tail: the regions are
-        // reduced to partial traces once at the end of the pass).  Integer addition is associative, so the sums
-        // are bitwise independent of the order the waves (and, in hea_grad_reduce, samples and tiles) arrive.
-        // Lane (g4, cl) holds N[4 g4 + i][cl]; entry slot: b == a -> b, b ^ a == e_j -> 16 + 16 j + b.
-        const float sc = (float)((double)rsc[CMAX] * FIX);
-        unsigned long long* rg = red64 + ngrad * RSTR;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15, d = bb ^ aa;
-          if (__builtin_popcount(d) <= 1) {
-            const int e = d == 0 ? (int)bb : 16 + 16 * (__builtin_ctz(d)) + (int)bb;
-            atomicAdd(&rg[red_slot(e)], (unsigned long long)fix64(accR[i] * sc));
-            atomicAdd(&rg[RIM + red_slot(e)], (unsigned long long)fix64(accI[i] * sc));
-          }
-        }
-        if (tid == 0) {
-          gops[2 * ngrad] = opw[W_GIDX];
-          gops[2 * ngrad + 1] = nreal;
-        }
-        ++ngrad;
-      }
-    } else if (ADJ && code == OP_OBS) {
-      obs_op<NCK, NT>(tile, opw, tid, T, fixed, rsc);
-    } else if (!ADJ && code == OP_READOUT) {
+    if (code == OP_APPLY) {
+      group_apply<1, NW, false, 0>(psi_t, F, opw, op_fo(opw, fixed), lane, wave, nbw);
+    } else if (code == OP_READOUT) {
       const size_t pidx = ((size_t)s * a.n_tiles + tile_id) * a.C;
       readout_op<NCK, NT>(psi_t, a, opw, tid, lane, wave, T, fixed, red, pidx);
     }
   }
   lds_barrier();
   HEA_MARK();
-  QFX_DCHECK(!ADJ || tile_id < a.slab_tiles);
-  if (ADJ) {   // partial traces: thread (op, j, y, x, comp) sums the 8 entries with b_j = y, a_j = x
-    for (int e = tid; e < ngrad * 32; e += NT) {
-      const int g = e >> 5, r = e & 31, j = r >> 3, y = (r >> 2) & 1, x = (r >> 1) & 1, comp = r & 1;
-      const unsigned long long* rg = red64 + g * RSTR + comp * RIM;
-      unsigned long long v = 0ull;
-      if (j < gops[2 * g + 1]) {
-        const int lowm = (1 << j) - 1;
-        for (int o8 = 0; o8 < 8; ++o8) {    // the other three bits of b
-          const int bb = ((o8 & ~lowm) << 1) | (o8 & lowm) | (y << j);
-          v += rg[red_slot(x == y ? bb : 16 + 16 * j + bb)];
+  if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
+  HEA_MARK();
+}
+
+// ------------------------------------------------------------------------------------------- adjoint pass
+// One workgroup per tile of 2^t <= 2^TB amplitudes holding psi and lambda interleaved (2^(TB+3) bytes of LDS),
+// 2^(TB-4) threads: TB = 14 is a 16-wave workgroup on 128 KB (one per CU); TB = 13 an 8-wave workgroup on
+// 64 KB, two per CU, so one workgroup's tile load (the HBM latency of a fresh 64 KB tile) overlaps the other's
+// group ops and the two workgroups' per-op barriers are independent.  Both have 4 column blocks per wave per
+// op.  Gradient ops accumulate their cross-matrix entries into per-op LDS regions.  TB = 14 has room for one
+// region per gradient op of the pass, reduced to partial traces once at the end.  TB = 13 alternates two
+// regions: at the start of the op after a gradient op, ONE wave reduces that op's region to partial traces and
+// zeroes it, while the other waves go on with the op (its region is next used two gradient ops later, after
+// at least one more barrier).  Measured: spreading that flush over all waves delays every wave by its LDS
+// round trip and was slower (16q adjoint 0.67 -> 0.72 ms).
+template <int NCK, int TB>
+__global__ void __launch_bounds__(1 << (TB - 4), 4) hea_adj_kernel(PassArgs a) {
+  constexpr int NT = 1 << (TB - 4), NW = NT / 64;
+  // (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
+  __shared__ __attribute__((aligned(16))) uint32_t tile[2 << TB];
+  __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
+  __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
+  __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];   // op unitary fragments, double buffered
+  // the 80 cross-matrix entries a partial trace can use (b = a, and b = a ^ e_j) x (re, im), 2^-32 fixed point
+  constexpr bool RING = TB < 14;
+  constexpr int NREG = RING ? 2 : MAXGRAD;
+  __shared__ unsigned long long red64[NREG * RSTR];
+  __shared__ int gmeta_s[NREG][2];                      // (slab index, nreal) of the region's gradient op
+  __shared__ float rsc[CMAX + 2];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s = blockIdx.x / a.n_tiles, tile_id = blockIdx.x % a.n_tiles;
+  const int k = s / a.spc;
+  const int T = 1 << a.t;
+  const size_t N = (size_t)1 << a.n;
+  const uint32_t fixed = tile_fixed(a, tile_id);
+  long long* dbg = (a.dbg && blockIdx.x < 8) ? a.dbg + blockIdx.x * 64 : nullptr;
+  int ndbg = 0;
+  HEA_MARK();
+  const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
+  long long* slab = a.gslab + ((size_t)s * a.slab_tiles + tile_id) * a.n_gradops * 32;
+  QFX_DCHECK(tile_id < a.slab_tiles);
+
+  load_tile_il<NT, TB>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
+                       h_q, fixed);
+  if (tid == 0) {
+    float rho = 0.f;
+    for (int c = 0; c < a.C; ++c) rho = fmaxf(rho, fabsf(a.wread[(size_t)s * a.C + c]));
+    if (rho == 0.f) rho = 1.f;
+    for (int c = 0; c < NCK; ++c) rsc[c] = c < a.C ? a.wread[(size_t)s * a.C + c] / rho : 0.f;
+    rsc[CMAX] = rho / (a.scale * a.scale);
+  }
+  for (int e = tid; e < NREG * RSTR; e += NT) red64[e] = 0ull;
+
+  // Partial traces of a finished gradient op's region (read after a barrier): output r = (j, y, x, comp) sums the
+  // 8 entries with b_j = y, a_j = x (the whole workgroup at the end of the pass, or lanes 0..31 of the flushing
+  // wave).
+  auto reduce_region = [&](int reg, int r) {
+    const int j = r >> 3, y = (r >> 2) & 1, x = (r >> 1) & 1, comp = r & 1;
+    const unsigned long long* rg = red64 + reg * RSTR + comp * RIM;
+    unsigned long long v = 0ull;
+    if (j < gmeta_s[reg][1]) {
+      const int lowm = (1 << j) - 1;
+      for (int o8 = 0; o8 < 8; ++o8) {    // the other three bits of b
+        const int bb = ((o8 & ~lowm) << 1) | (o8 & lowm) | (y << j);
+        v += rg[red_slot(x == y ? bb : 16 + 16 * j + bb)];
+      }
+    }
+    slab[(size_t)gmeta_s[reg][0] * 32 + r] = (long long)v;
+  };
+  auto flush = [&](int reg) {                           // one wave: reduce, then zero the region
+    if (lane < 32) reduce_region(reg, lane);
+    lds_barrier_wave();
+    for (int e = lane; e < RSTR; e += 64) red64[reg * RSTR + e] = 0ull;
+  };
+
+  // ---------------------------------------------------------------- op list
+  const int ncol = T >> 4, nblk = ncol >> 4;
+  const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
+  if (tid < a.nops) fidx_s[tid] = a.fidx[tid];
+  if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
+  int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
+  if (a.nops > 0) dma_frags(a, k, a.fidx[0], tid, wave, frag_s[0]);
+  lds_barrier_dma();
+  HEA_MARK();
+  int ngrad = 0;
+  int pending = -1;                                    // ring: region of the previous op, if a gradient op
+  for (int o = 0; o < a.nops; ++o) {
+    // op o's record and fragments were written during op o - 1; the other buffers were last read at the
+    // start of op o - 1, which every wave has finished at this barrier, so op o + 1's go there right away
+    lds_barrier_dma();
+    HEA_MARK();
+    if (RING && pending >= 0) {
+      if (wave == NW - 1) flush(pending);
+      pending = -1;
+    }
+    const int* opw = opw2[o & 1];
+    uint4 F[4];
+    if (fidx_s[o] >= 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) F[i] = frag_s[o & 1][64 * i + lane];
+    }
+    if (o + 1 < a.nops) {
+      if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
+      if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
+      dma_frags(a, k, fidx_s[o + 1], tid, wave, frag_s[(o + 1) & 1]);
+    }
+    const int code = opw[W_CODE];
+#if QFX_CHECKS_ON
+    QFX_DCHECK(code >= OP_UNAPPLY_PSI && code <= OP_BACK && code != OP_READOUT);
+    if (code != OP_OBS) {
+      QFX_DCHECK(opw[W_NREAL] >= 0 && opw[W_NREAL] <= 4);
+      QFX_DCHECK((uint32_t)opw[W_OFF + (lane & 15)] < (uint32_t)T);
+      QFX_DCHECK((uint32_t)opw[W_BL + (lane & 31)] < (uint32_t)T);
+      QFX_DCHECK((uint32_t)opw[W_BH + (lane & 31)] < (uint32_t)T);
+      // -1 = no unitary (cross-matrix-only gradient ops); every op that applies one names a fragment
+      QFX_DCHECK(fidx_s[o] >= -1 && fidx_s[o] < 4 * a.n_slots);
+      QFX_DCHECK(fidx_s[o] >= 0 || code == OP_GRAD || code == OP_GRAD_L1);
+      if (code != OP_UNAPPLY_PSI && code != OP_UNAPPLY_LAM)
+        QFX_DCHECK(opw[W_GIDX] >= 0 && opw[W_GIDX] < a.n_gradops);
+    } else {
+      QFX_DCHECK(opw[W_NREAL] >= 1 && opw[W_NREAL] <= a.C);
+    }
+#endif
+    if (code == OP_OBS) {
+      obs_op<NCK, NT, TB>(tile, opw, tid, T, fixed, rsc);
+    } else if (code == OP_UNAPPLY_PSI) {
+      group_apply<1, NW, true, 0, TB>(tile, F, opw, op_fo(opw, fixed), lane, wave, nbw);
+    } else if (code == OP_UNAPPLY_LAM) {
+      group_apply<1, NW, true, 1, TB>(tile, F, opw, op_fo(opw, fixed), lane, wave, nbw);
+    } else if (code == OP_BACK || code == OP_GRAD || code == OP_GRAD_L1) {
+      const uint32_t fo = op_fo(opw, fixed);
+      f4 accR = {0.f, 0.f, 0.f, 0.f}, accI = {0.f, 0.f, 0.f, 0.f};
+      group_cross<NW, TB>(tile, opw, fo, lane, wave, nbw, accR, accI);
+      if (code == OP_BACK) {
+        if (opw[W_FLAGS] & F_BACK_PSI)
+          group_apply<2, NW, true, 0, TB>(tile, F, opw, fo, lane, wave, nbw);
+        else
+          group_apply<1, NW, true, 1, TB>(tile, F, opw, fo, lane, wave, nbw);
+      }
+      // Cross-wave sum of the partial-trace entries of N, pre-scaled by the sample's rho / scale^2, in 2^-32
+      // fixed point with 64-bit LDS atomics into the op's region.  Integer addition is associative, so the sums
+      // are bitwise independent of the order the waves (and, in hea_grad_reduce, samples and tiles) arrive.
+      // Lane (g4, cl) holds N[4 g4 + i][cl]; entry slot: b == a -> b, b ^ a == e_j -> 16 + 16 j + b.
+      const int reg = RING ? ngrad & 1 : ngrad;
+      const float sc = (float)((double)rsc[CMAX] * FIX);
+      unsigned long long* rg = red64 + reg * RSTR;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15, d = bb ^ aa;
+        if (__builtin_popcount(d) <= 1) {
+          const int e = d == 0 ? (int)bb : 16 + 16 * (__builtin_ctz(d)) + (int)bb;
+          atomicAdd(&rg[red_slot(e)], (unsigned long long)fix64(accR[i] * sc));
+          atomicAdd(&rg[RIM + red_slot(e)], (unsigned long long)fix64(accI[i] * sc));
         }
       }
-      a.gslab[(((size_t)s * a.slab_tiles + tile_id) * a.n_gradops + gops[2 * g]) * 32 + r] = (long long)v;
+      if (tid == 0) {
+        gmeta_s[reg][0] = opw[W_GIDX];
+        gmeta_s[reg][1] = opw[W_NREAL];
+      }
+      pending = reg;
+      ++ngrad;
     }
   }
-  if (!ADJ && a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
-  if (ADJ && a.store_lam) store_lam_il<NT>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
   lds_barrier();
   HEA_MARK();
-#undef HEA_MARK
+  if (RING) {
+    if (pending >= 0 && wave == NW - 1 && lane < 32) reduce_region(pending, lane);
+  } else {
+    for (int e = tid; e < ngrad * 32; e += NT) reduce_region(e >> 5, e & 31);
+  }
+  if (a.store_lam) store_lam_il<NT, TB>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
+  HEA_MARK();
 }
+#undef HEA_MARK
 
 // Unitary fragments: per (client, slot) U and U^H in the real 32 x 32 embedding, laid out as the MFMA
 // A operand of v_mfma_f32_16x16x32_f16 (lane l: row 16h + (l & 15), k = 8 (l >> 4) .. +7), hi and lo fp16.
@@ -891,10 +994,12 @@ extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_sample
   if (grid == 0) return 0;
 #define HEA_LAUNCH(NCK)                                                                                     \
   do {                                                                                                     \
-    if (adjoint)                                                                                           \
-      hipLaunchKernelGGL((hea::hea_pass_kernel<true, NCK>), dim3(grid), dim3(hea::NT_ADJ), 0, st, a);      \
+    if (!adjoint)                                                                                          \
+      hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);             \
+    else if (a.t <= 13)                                                                                    \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13>), dim3(grid), dim3(1 << 9), 0, st, a);              \
     else                                                                                                   \
-      hipLaunchKernelGGL((hea::hea_pass_kernel<false, NCK>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);     \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14>), dim3(grid), dim3(1 << 10), 0, st, a);             \
   } while (0)
   switch (hea::class_kernel(a.C)) {
     case 1: HEA_LAUNCH(1); break;

@@ -18,12 +18,24 @@ split, so the only rounding is the fp16 state between ops (~2^-12 relative per o
 from __future__ import annotations
 
 import contextlib
+import os
 
 import numpy as np
 import torch
 
 from ._ext import ext
 from .hea_plan import TILE_BITS, build_plan, eligible, pass_programs
+
+ADJ_TILE_BITS = 13   # adjoint tiles: 2^13 amplitudes x (psi, lambda) = 64 KB of LDS -> two workgroups per CU
+
+
+def _same_passes(a, b) -> bool:
+    """Two plans run the same rotation groups (and unitary slots) in the same passes - only their tile geometry
+    differs.  The layer-1 gradient groups may sit in other passes: they exist only in the adjoint programs
+    (the forward generates the whole layer-1 product state in its first pass)."""
+    def sig(plan):
+        return [sorted((g.slot, g.layer, tuple(g.qubits), g.frame) for g in p.groups) for p in plan.passes]
+    return a.n_slots == b.n_slots and sig(a) == sig(b)
 
 _FEATURE = {"ry": 0, "rx": 1, "rz": 2}
 
@@ -44,7 +56,7 @@ _NODBG = torch.zeros(0, dtype=torch.int64)     # no phase timestamps
 
 
 class HeaMfmaProgram:
-    def __init__(self, spec, device, tile_bits: int = TILE_BITS):
+    def __init__(self, spec, device, tile_bits: int | None = None, adj_tile_bits: int | None = None):
         if not eligible(spec):
             raise ValueError("the MFMA engine covers angle-encoded RX/RZ + CNOT-chain VQCs with 8..30 qubits, "
                              "no gate noise and <= 8 classes")
@@ -53,21 +65,40 @@ class HeaMfmaProgram:
         self.C = spec.n_classes
         self.n_theta = spec.n_theta
         self.device = torch.device(device)
+        if tile_bits is None:
+            tile_bits = int(os.environ.get("QFEDX_HEA_TILE", TILE_BITS))
+        if adj_tile_bits is None:
+            adj_tile_bits = int(os.environ.get("QFEDX_HEA_ADJ_TILE", min(tile_bits, ADJ_TILE_BITS)))
+        self.tile_bits = tile_bits
         self.plan = build_plan(self.n, spec.n_layers, spec.readout, spec.entangler == "chain", spec.feature_map,
                                tile_bits)
+        # The adjoint may run on smaller tiles than the forward (2^13 amplitudes: two adjoint workgroups per
+        # CU, one's tile load hidden behind the other's group ops) when that plan has the same passes, rotation
+        # groups and unitary slots: pass outputs are stored in memory order, so the tiling of a pass is free to
+        # differ.
+        plan_a = self.plan
+        if adj_tile_bits != tile_bits:
+            cand = build_plan(self.n, spec.n_layers, spec.readout, spec.entangler == "chain", spec.feature_map,
+                              adj_tile_bits)
+            if _same_passes(self.plan, cand):
+                plan_a = cand
+        self.adj_plan = plan_a
+        self.adj_tile_bits = plan_a.passes[0].t if plan_a.passes else tile_bits
         C = ext()
         self.n_slots = self.plan.n_slots
         self.passes = []
         gmeta = []
-        progs = pass_programs(self.plan, gmeta)
+        progs_f = pass_programs(self.plan, [])
+        progs_a = pass_programs(plan_a, gmeta)
         self.n_gradops = len(gmeta)
-        for p, fwd, adj in progs:
+        for (p, fwd, _), (pa, _, adj) in zip(progs_f, progs_a):
             f = torch.from_numpy(fwd.astype(np.int32)).contiguous()
             a = torch.from_numpy(adj.astype(np.int32)).contiguous()
             ff, fa = _frag_index(fwd), _frag_index(adj)
             C.hea_check_ops(f, ff, self.n_slots, self.n_theta, False, p.t, self.n_gradops)
-            C.hea_check_ops(a, fa, self.n_slots, self.n_theta, True, p.t, self.n_gradops)
-            self.passes.append((p, (f.to(self.device), ff.to(self.device)), (a.to(self.device), fa.to(self.device))))
+            C.hea_check_ops(a, fa, self.n_slots, self.n_theta, True, pa.t, self.n_gradops)
+            self.passes.append((p, (f.to(self.device), ff.to(self.device)), (a.to(self.device), fa.to(self.device)),
+                                pa))
         slot_tab = np.zeros((max(self.n_slots, 1), 9), dtype=np.int32)
         owner = np.zeros(self.n_theta, dtype=np.int32)
         for p in self.plan.passes:
@@ -85,7 +116,7 @@ class HeaMfmaProgram:
             raise RuntimeError("a parameter has no owning pass")
         self.slot_tab = torch.from_numpy(slot_tab).to(self.device)
         self.gmeta = torch.tensor(gmeta, dtype=torch.int32).reshape(-1).to(self.device)
-        self.slab_tiles = max(1 << (self.n - p.t) for p in self.plan.passes)
+        self.slab_tiles = max(1 << (self.n - p.t) for p in plan_a.passes)
         self.scale = float(1 << (self.n // 2))
         self.feature = _FEATURE[spec.feature_map.lower()]
         self._ws = {}
@@ -137,7 +168,7 @@ class HeaMfmaProgram:
         empty = torch.empty(0, dtype=torch.int32, device=self.device)
         fempty = torch.empty(0, dtype=torch.float32, device=self.device)
         J = self.n_passes
-        for j, (p, fwd, _) in enumerate(self.passes):
+        for j, (p, fwd, _, _) in enumerate(self.passes):
             keep = j < J - 1 or store_last
             out = self._buf(f"psi{j}", N, torch.int32) if keep else empty
             psi_in = stored[-1] if j > 0 else empty
@@ -157,7 +188,7 @@ class HeaMfmaProgram:
         J = self.n_passes
         lam_in = empty
         for j in range(J - 1, -1, -1):
-            p, _, adj = self.passes[j]
+            _, _, adj, p = self.passes[j]
             lam_out = self._buf(f"lam{j % 2}", N, torch.int32) if j > 0 else empty
             geom = self._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, x.shape[1], K)
             C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,

@@ -57,8 +57,8 @@ def main():
         torch.cuda.synchronize()
         res[name] = round(a.elapsed_time(b) / 10, 4)
 
-    p0, (f0, fi0), (a0, ai0) = prog.passes[0]
-    p1, (f1, fi1), (a1, ai1) = prog.passes[1]
+    p0, (f0, fi0), (a0, ai0), pa0 = prog.passes[0]
+    p1, (f1, fi1), (a1, ai1), pa1 = prog.passes[1]
     run("gen_only", False, p0, f0[:0], fi0[:0], True, False, False, False)
     run("gen_store", False, p0, f0[:0], fi0[:0], True, False, True, False)
     for k in (1, 3, 7):
@@ -72,12 +72,12 @@ def main():
     run("gen_store_64nop", False, p0, nop, nopf, True, False, True, False)
     nopf2 = fi0[:1].repeat(64).contiguous()
     run("gen_store_64nop_frag", False, p0, nop, nopf2, True, False, True, False)
-    run("adj1_full", True, p1, a1, ai1, False, False, False, True)
-    run("adj0_full", True, p0, a0, ai0, False, True, False, False)
-    run("adj0_load_only", True, p0, a0[:0].contiguous(), ai0[:0].contiguous(), False, True, False, False)
-    run("adj0_load_store", True, p0, a0[:0].contiguous(), ai0[:0].contiguous(), False, True, False, True)
-    run("adj0_1back", True, p0, a0[:1].contiguous(), ai0[:1].contiguous(), False, True, False, False)
-    run("adj0_4back", True, p0, a0[:4].contiguous(), ai0[:4].contiguous(), False, True, False, False)
+    run("adj1_full", True, pa1, a1, ai1, False, False, False, True)
+    run("adj0_full", True, pa0, a0, ai0, False, True, False, False)
+    run("adj0_load_only", True, pa0, a0[:0].contiguous(), ai0[:0].contiguous(), False, True, False, False)
+    run("adj0_load_store", True, pa0, a0[:0].contiguous(), ai0[:0].contiguous(), False, True, False, True)
+    run("adj0_1back", True, pa0, a0[:1].contiguous(), ai0[:1].contiguous(), False, True, False, False)
+    run("adj0_4back", True, pa0, a0[:4].contiguous(), ai0[:4].contiguous(), False, True, False, False)
     print(json.dumps(res), flush=True)
     for k, v in phases.items():
         print("phases", k, v, flush=True)

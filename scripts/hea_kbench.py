@@ -74,7 +74,8 @@ def main():
         res[name] = {"ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1)}
 
     timeit(lambda: prog._frags(params, K), "frags", 0)
-    for j, (p, fwd, adj) in enumerate(prog.passes):
+    for j, ent in enumerate(prog.passes):
+        p, fwd = ent[0], ent[1]
         out = prog._buf(f"psi{j}", N, torch.int32)
         psi_in = stored[j - 1] if j > 0 else empty
         geom = prog._geom(p, j == 0, False, True, False, B, params.shape[1], S, xx.shape[1], K)
@@ -83,7 +84,8 @@ def main():
                                   part if j == J - 1 else fempty, fempty, _NODBG), f"fwd{j}", nb)
     lam = [prog._buf("lam0", N, torch.int32), prog._buf("lam1", N, torch.int32)]
     for j in range(J - 1, -1, -1):
-        p, _, adj = prog.passes[j]
+        ent = prog.passes[j]                          # (fwd pass, fwd prog, adj prog[, adj pass]) (older trees: 3)
+        adj, p = ent[2], ent[-1] if len(ent) > 3 else ent[0]
         geom = prog._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, xx.shape[1], K)
         lin = lam[(j + 1) % 2] if j < J - 1 else empty
         lout = lam[j % 2] if j > 0 else empty
