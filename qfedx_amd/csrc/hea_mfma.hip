@@ -586,6 +586,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   __shared__ float2 wv[32][2];
   __shared__ float2 tabA[128];
   __shared__ float2 tabB[128];
+  __shared__ float2 outer_s;                            // scale x product of the out-of-tile layer-1 factors
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -602,58 +603,72 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
 
   // ---------------------------------------------------------------- initial psi tile
   if (a.gen) {
-    if (tid < a.n) {
-      float2 w[2];
-      l1_factor(a.xang[(size_t)s * a.x_stride + tid], prm[2 * tid], prm[2 * tid + 1], a.feature, w);
-      wv[tid][0] = w[0];
-      wv[tid][1] = w[1];
+    // Product state of layer 1: wave 0 computes every qubit's 2-vector (lane q) and, by a complex product over
+    // the wave, the factor of the qubits outside the tile (their bits are fixed over the tile).  Then the two
+    // half-index tables: each entry is a product of <= 7 factors, all read from LDS before the first multiply
+    // (one LDS round trip instead of one per factor).
+    if (wave == 0) {
+      float2 w[2] = {make_float2(1.f, 0.f), make_float2(1.f, 0.f)};
+      if (tid < a.n) {
+        l1_factor(a.xang[(size_t)s * a.x_stride + tid], prm[2 * tid], prm[2 * tid + 1], a.feature, w);
+        wv[tid][0] = w[0];
+        wv[tid][1] = w[1];
+      }
+      const bool outq = tid < a.n && !(tid < a.c || (tid >= a.lo && tid < a.hi));
+      float2 f = outq ? w[(fixed >> (tid & 31)) & 1] : make_float2(1.f, 0.f);
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) f = cmul(f, make_float2(__shfl_xor(f.x, off, 64), __shfl_xor(f.y, off, 64)));
+      if (tid == 0) outer_s = make_float2(a.scale * f.x, a.scale * f.y);
     }
     lds_barrier();
     HEA_MARK();
     const int ta = a.t >> 1, tb = a.t - ta;
-    if (tid < (1 << ta)) {                          // threads [0, 2^ta): low-half products
-      const int i = tid;
-      float2 v = make_float2(1.f, 0.f);
-      for (int j = 0; j < ta; ++j) {
-        const int mb = j < a.c ? j : a.lo + j - a.c;
-        v = cmul(v, wv[mb][(i >> j) & 1]);
+    constexpr int JMAX = TMAX - (TMAX >> 1);
+    const bool lowt = tid < (1 << ta), hight = tid >= 256 && tid < 256 + (1 << tb);
+    if (lowt || hight) {                            // [0, 2^ta): low-half products; [256, ..): high half
+      const int i = lowt ? tid : tid - 256, j0 = lowt ? 0 : ta, nj = lowt ? ta : tb;
+      float2 fac[JMAX];
+#pragma unroll
+      for (int j = 0; j < JMAX; ++j) {
+        const int tj = j0 + j, mb = tj < a.c ? tj : a.lo + tj - a.c;
+        fac[j] = wv[j < nj ? mb : 0][(i >> j) & 1];
       }
-      tabA[i] = v;
-    } else if (tid >= 256 && tid < 256 + (1 << tb)) {   // threads [256, 256 + 2^tb): high half x fixed bits
-      const int i = tid - 256;
-      float2 v = make_float2(a.scale, 0.f);
-      for (int q = 0; q < a.n; ++q) {
-        const bool in_tile = q < a.c || (q >= a.lo && q < a.hi);
-        if (!in_tile) v = cmul(v, wv[q][(fixed >> q) & 1]);
-      }
-      for (int j = 0; j < tb; ++j) {
-        const int tj = ta + j;
-        const int mb = tj < a.c ? tj : a.lo + tj - a.c;
-        v = cmul(v, wv[mb][(i >> j) & 1]);
-      }
-      tabB[i] = v;
+      float2 v = lowt ? make_float2(1.f, 0.f) : outer_s;
+#pragma unroll
+      for (int j = 0; j < JMAX; ++j)
+        if (j < nj) v = cmul(v, fac[j]);
+      if (lowt)
+        tabA[i] = v;
+      else
+        tabB[i] = v;
     }
     lds_barrier();
     HEA_MARK();
     const uint32_t am = (1u << ta) - 1u;
     // quad q = tid + NT i holds LDS words 4q .. 4q+3 = amplitudes tau_e = (4q + e) ^ h, h = h(q >> 3);
-    // the swizzle only flips bits < 5 and ta >= 4, so the four words share one high-half factor
+    // the swizzle only flips bits < 5 and ta >= 4, so the four words share one high-half factor.  Table reads
+    // are never predicated (quads past a small tile read quad 0); only the stores are.
+    // All quads are computed before the first store: a store to the tile between them kept the compiler from
+    // issuing the next quad's table reads early (one LDS round trip per quad).
     constexpr int QI = (1 << TMAX) / (4 * NT);
+    uint4 out[QI];
 #pragma unroll
     for (int i = 0; i < QI; ++i) {
       const uint32_t q = (uint32_t)(tid + NT * i);
-      if (4 * q < (uint32_t)T) {
-        const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
-        const float2 vb = tabB[((4 * q) ^ h) >> ta];          // same high half for the whole quad
-        uint4 out;
-        uint32_t* ow = (uint32_t*)&out;
+      const uint32_t qq = 4 * q < (uint32_t)T ? q : 0u;
+      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+      const float2 vb = tabB[((4 * qq) ^ h) >> ta];          // same high half for the whole quad
+      uint32_t* ow = (uint32_t*)&out[i];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float2 v = cmul(tabA[((4 * q + e) ^ h) & am], vb);
-          ow[e] = pack_h2(v.x, v.y);
-        }
-        *(uint4*)&psi_t[4 * q] = out;
+      for (int e = 0; e < 4; ++e) {
+        const float2 v = cmul(tabA[((4 * qq + e) ^ h) & am], vb);
+        ow[e] = pack_h2(v.x, v.y);
       }
+    }
+#pragma unroll
+    for (int i = 0; i < QI; ++i) {
+      const uint32_t q = (uint32_t)(tid + NT * i);
+      if (4 * q < (uint32_t)T) *(uint4*)&psi_t[4 * q] = out[i];
     }
   } else {
     load_tile<NT>(a, a.psi_in + (size_t)s * N, psi_t, tid, T, h_q, fixed);
