@@ -22,9 +22,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
-def timed_rounds(cfg, device, backend, world, warmup: int, steps: int):
+def timed_rounds(cfg, device, backend, world, warmup: int, steps: int, counts: list | None = None):
     """Build this rank's runner, run ``warmup`` untimed rounds, then time exactly ``steps`` rounds
-    bracketed by barrier + device sync on both sides; returns (runner, max-over-ranks seconds)."""
+    bracketed by barrier + device sync on both sides; returns (runner, max-over-ranks seconds).  ``counts``
+    (optional list) receives each timed round's number of training clients (participants - dropouts, over all
+    ranks: the sampling is keyed, identical on every rank)."""
     import torch
     from qfedx_amd.data.datasets import build_federated_data
     from qfedx_amd.fl.adapters import make_adapter
@@ -46,7 +48,9 @@ def timed_rounds(cfg, device, backend, world, warmup: int, steps: int):
     sync()
     t0 = time.perf_counter()
     for r in range(warmup, warmup + steps):
-        runner.run_round(r, sync=False)
+        rec = runner.run_round(r, sync=False)
+        if counts is not None:
+            counts.append(rec["participants"] - rec["dropped"])
     sync()
     dt = time.perf_counter() - t0
     return runner, max_over_ranks(dt, world)

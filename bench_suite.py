@@ -65,17 +65,19 @@ def main():
     path, ov, metric, ref = SUITE[args.config]
     cfg = load_config(os.path.join(ROOT, path), ov + list(args.overrides))
     device, backend, world = setup(cfg)
-    runner, dt = timed_rounds(cfg, device, backend, world, args.warmup, args.steps)
+    counts = []
+    runner, dt = timed_rounds(cfg, device, backend, world, args.warmup, args.steps, counts)
     t = cfg.train
-    hist_steps = None
-    # local steps actually run per round (all clients): epochs x ceil(n/B), or the fixed step count
+    # local steps actually run in the timed rounds (all clients): the fixed step count per training client
+    # (participants of each round: Poisson sampling under DP varies them), or epochs x ceil(n/B) at full
+    # participation
     if t.local_steps > 0:
-        per_round = int(round(cfg.data.num_clients * t.client_fraction)) * t.local_steps
+        total = sum(counts) * t.local_steps
     else:
         import math
         per_round = sum(t.local_epochs * math.ceil(int(n) / t.batch_size) for n in runner.store.counts)
-        per_round = int(per_round * world.world_size)   # store holds this rank's clients
-    value = per_round * args.steps / dt
+        total = int(per_round * world.world_size) * args.steps   # store holds this rank's clients
+    value = total / dt
     ev = runner.evaluate()
     if world.is_main:
         kind = cfg.model.kind

@@ -361,7 +361,7 @@ class VQCClientTrainer:
                 with torch.cuda.graph(g):
                     ent["out"] = body()
             ent["graph"] = g
-            while len(cache) >= 4:                  # LRU: drop the oldest shape
+            while len(cache) >= 6:                  # LRU: drop the oldest shape
                 cache.pop(next(iter(cache)))
         else:
             dv = up.to_device(dev, ent["pack"])     # one H2D copy for all the round's tables
