@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from ._ext import ext
-from .hea_plan import TILE_BITS, build_plan, eligible, pass_programs
+from .hea_plan import OP_APPLY, OP_READOUT, TILE_BITS, W_CODE, build_plan, eligible, obs_table, pass_programs
 
 ADJ_TILE_BITS = 13   # adjoint tiles: 2^13 amplitudes x (psi, lambda) = 64 KB of LDS -> two workgroups per CU
 
@@ -91,6 +91,17 @@ class HeaMfmaProgram:
         progs_f = pass_programs(self.plan, [])
         progs_a = pass_programs(plan_a, gmeta)
         self.n_gradops = len(gmeta)
+        # Forward passes after the last one that applies a unitary are identities on the state (they exist for
+        # the adjoint's layer-1 gradient tiles, e.g. every pass of an L = 1 circuit): the forward stops at that
+        # pass, reads out there, and later passes' stored outputs alias its output.
+        applies = [j for j, (_, fwd, _) in enumerate(progs_f) if any(int(w[W_CODE]) == OP_APPLY for w in fwd)]
+        self.fwd_last = applies[-1] if applies else 0
+        J = len(progs_f)
+        if self.fwd_last < J - 1:
+            pr, fr_ops, ar = progs_f[self.fwd_last]
+            fr_ops = np.concatenate([fr_ops, obs_table(self.plan, pr, OP_READOUT)[None]], 0)
+            progs_f = [(p, f if j < self.fwd_last else (fr_ops if j == self.fwd_last else f[:0]), a)
+                       for j, (p, f, a) in enumerate(progs_f)]
         for (p, fwd, _), (pa, _, adj) in zip(progs_f, progs_a):
             f = torch.from_numpy(fwd.astype(np.int32)).contiguous()
             a = torch.from_numpy(adj.astype(np.int32)).contiguous()
@@ -145,7 +156,8 @@ class HeaMfmaProgram:
 
     @property
     def tiles_last(self) -> int:
-        return 1 << (self.n - self.passes[-1][0].t)
+        """Tiles per sample of the pass that reads out <Z> (the last forward pass that runs)."""
+        return 1 << (self.n - self.passes[self.fwd_last][0].t)
 
     def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K):
         return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
@@ -159,24 +171,28 @@ class HeaMfmaProgram:
         return fr
 
     def _forward(self, x, params, fr, K, B, part, store_last: bool = False):
-        """Forward passes; returns the stored pass outputs (all of them with ``store_last``: the adjoint
-        starts each pass from its output)."""
+        """Forward passes up to the readout pass ``fwd_last``; returns the stored pass outputs (all of them with
+        ``store_last``: the adjoint starts each pass from its output; identity passes after ``fwd_last`` alias
+        its output)."""
         C = ext()
         S = K * B
         N = S << self.n
         stored = []
         empty = torch.empty(0, dtype=torch.int32, device=self.device)
         fempty = torch.empty(0, dtype=torch.float32, device=self.device)
-        J = self.n_passes
-        for j, (p, fwd, _, _) in enumerate(self.passes):
-            keep = j < J - 1 or store_last
+        J, R = self.n_passes, self.fwd_last
+        for j in range(R + 1):
+            p, fwd = self.passes[j][0], self.passes[j][1]
+            keep = j < R or store_last
             out = self._buf(f"psi{j}", N, torch.int32) if keep else empty
             psi_in = stored[-1] if j > 0 else empty
             geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K)
             C.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
-                       part if j == J - 1 else fempty, fempty, _NODBG)
+                       part if j == R else fempty, fempty, _NODBG)
             if keep:
                 stored.append(out)
+        if store_last:
+            stored += [stored[R]] * (J - 1 - R)
         return stored
 
     def _adjoint(self, x, params, fr, K, B, stored, wread, gslab):

@@ -74,14 +74,17 @@ def main():
         res[name] = {"ms": round(ms, 4), "GBps": round(nbytes / ms / 1e6, 1)}
 
     timeit(lambda: prog._frags(params, K), "frags", 0)
+    R = getattr(prog, "fwd_last", J - 1)                # forward passes after R are identities (older trees: none)
     for j, ent in enumerate(prog.passes):
+        if j > R:
+            break
         p, fwd = ent[0], ent[1]
         out = prog._buf(f"psi{j}", N, torch.int32)
         psi_in = stored[j - 1] if j > 0 else empty
         geom = prog._geom(p, j == 0, False, True, False, B, params.shape[1], S, xx.shape[1], K)
         nb = 4 * N * ((j > 0) + 1)
         timeit(lambda: C.hea_pass(False, fwd[0], fwd[1], geom, prog.scale, psi_in, out, empty, empty, xx, params, fr, fempty,
-                                  part if j == J - 1 else fempty, fempty, _NODBG), f"fwd{j}", nb)
+                                  part if j == R else fempty, fempty, _NODBG), f"fwd{j}", nb)
     lam = [prog._buf("lam0", N, torch.int32), prog._buf("lam1", N, torch.int32)]
     for j in range(J - 1, -1, -1):
         ent = prog.passes[j]                          # (fwd pass, fwd prog, adj prog[, adj pass]) (older trees: 3)

@@ -40,8 +40,11 @@ def _inputs(spec, K, B, seed=0):
 @pytest.mark.parametrize("n,L,tile,chain,feat", [(8, 2, 14, True, "ry"), (10, 3, 14, True, "ry"),
                                                  (10, 3, 8, True, "ry"), (11, 2, 8, False, "rx"),
                                                  (12, 4, 9, True, "ry"), (9, 1, 8, True, "rz"),
-                                                 (13, 3, 10, True, "ry"), (16, 3, 14, True, "ry")])
+                                                 (13, 3, 10, True, "ry"), (16, 3, 14, True, "ry"),
+                                                 (12, 1, 9, True, "ry"), (20, 1, 14, True, "rx")])
 def test_hea_vjp_matches_dense(cuda, n, L, tile, chain, feat):
+    """L = 1 plans have identity forward passes (they only place layer-1 gradient tiles for the adjoint): the
+    forward reads out at its last applying pass and the later pass outputs alias it."""
     spec = VQCSpec(n, L, 3, feature_map=feat, entangler="chain" if chain else "none")
     prog = HeaMfmaProgram(spec, cuda, tile_bits=tile)
     K, B = 2, 3
