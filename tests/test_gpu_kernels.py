@@ -111,8 +111,9 @@ def test_fused_fedavg_reduce_matches_torch(cuda, dp):
     assert torch.allclose(a, b, atol=1e-6, rtol=1e-6), (a - b).abs().max()
 
 
-@pytest.mark.parametrize("fraction,sampling", [(1.0, "fixed"), (0.5, "fixed"), (0.5, "poisson")])
-def test_graph_round_matches_eager(cuda, fraction, sampling):
+@pytest.mark.parametrize("fraction,sampling,dp", [(1.0, "fixed", False), (0.5, "fixed", False),
+                                                  (0.5, "poisson", False), (0.5, "poisson", True)])
+def test_graph_round_matches_eager(cuda, fraction, sampling, dp):
     """hipGraph-replayed local rounds produce the same global model as eager launches (with client
     sampling the set changes every round while the captured shape is reused; under Poisson sampling the
     client count changes too and the graph runs padded to its bucket, trainer.graph_bucket)."""
@@ -122,7 +123,7 @@ def test_graph_round_matches_eager(cuda, fraction, sampling):
     outs = []
     for graphs in (True, False):
         cfg = small_cfg(num_rounds=6, n_qubits=6, device="cuda", backend="hip", client_fraction=fraction,
-                        sampling=sampling, num_clients=7)
+                        sampling=sampling, num_clients=7, dp=dp, deterministic_noise=dp, noise_multiplier=0.3)
         dev = torch.device("cuda", 0)
         world = init_distributed(dev)
         import qfedx_amd.fl.trainer as tr
