@@ -165,10 +165,192 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
 // --------------------------------------------------------------------------------------------
 // backward of the conv stack for BS samples of one client -> per-workgroup gradient partials
 //   part[(k*G + g)][ dW2 (12800) | db2 (32) | dW1 (400) | db1 (16) ]
+//
+// Per sample the three GEMMs are laid out so that no operand needs an index table and every
+// MFMA operand is one unpredicated ds_read_b32 from a per-lane base:
+//   conv2 wgrad  D[o][(tap, ci)] = sum_p dC2[o][p] P1pad[ci][q(p) + off(tap)]    M=32  N=26x16 K=196
+//                n-tile = one tap (lane = ci), plus a 26th "ones" n-tile that yields db2
+//   conv2 dgrad  D[p][ci] = sum_{tap,o} dC2pad[o][rb(p) - off(tap)] W2[o][ci][tap] M=196 N=16    K=25x32
+//                K ordered (tap, o): the tap offset is wave-uniform, o runs over immediate offsets
+//   conv1 wgrad  D[o][tap] = sum_p dC1[o][p] img[p + off1(tap)]                    M=16  N=32    K=784
+//                tap 25 is a ones column (db1); taps 26..31 are discarded
+// Work split (MFMA count per SIMD balanced; waves w and w+4 share a SIMD): wave w<4 owns dgrad
+// m-tiles 2w, 2w+1 and 7 wgrad n-tiles; wave w>=4 owns dgrad m-tile 4+w, a quarter of the
+// reduction of m-tile 12 (rows 192..195, the only partial tile) and 6 wgrad n-tiles.
 // --------------------------------------------------------------------------------------------
 constexpr int BS = 4;              // samples per backward workgroup
-constexpr int W2T = 801;           // LDS stride of the transposed W2 [16 ci][800 (o,dy,dx)]
+constexpr int CS = 338;            // LDS stride of one zero-padded 18x18 map (== 18 mod 32: channel-strided
+                                   // ds_read_b32 lanes land on distinct banks)
+constexpr int W2R = 802;           // LDS stride of W2 reordered as w2r[ci][tap*32 + o]
+constexpr int DPS = 198;           // LDS stride of the dP1 / argmax1 rows
+constexpr int IMS = 37;            // LDS row stride of the padded image
+constexpr int NT2 = 26;            // conv2 wgrad n-tiles (25 taps + ones)
 constexpr int PART = C2 * K2 + C2 + C1 * K1 + C1;
+
+__device__ __forceinline__ int q14(int p) { return p + 4 * (p / H2); }   // (y, x) of a 14x14 map -> 18*y + x
+__device__ __forceinline__ int tap_off(int r) { return (r / 5) * P1P + r % 5; }
+
+// conv2 wgrad over the 49 k-steps of one sample: acc[j] += A(o rows) x B(n-tile j).  Two register sets
+// alternate: the operands of step ks+1 are read before the MFMAs of step ks issue, so LDS latency
+// overlaps MFMA work (no register copies between the sets, which would wait on the reads).
+template <int NJ>
+__device__ __forceinline__ void wgrad_load(const float* sm, int aoff, const int (&boff)[7], int ks, int kq, float& a,
+                                           float (&b)[NJ]) {
+  const int q = q14(ks * 4 + kq);
+  a = sm[aoff + q];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) b[j] = sm[boff[j] + q];
+}
+
+template <int NJ>
+__device__ __forceinline__ void bwd_wgrad2(const float* sm, int aoff, const int (&boff)[7], f4 (&acc)[7], int kq) {
+  constexpr int NKS = H2 * H2 / 4;
+  static_assert(NKS % 2 == 1, "loop below pairs the steps and peels the last one");
+  float a0, b0[NJ], a1, b1[NJ];
+  wgrad_load<NJ>(sm, aoff, boff, 0, kq, a0, b0);
+#pragma unroll 1
+  for (int ks = 0; ks < NKS - 1; ks += 2) {
+    wgrad_load<NJ>(sm, aoff, boff, ks + 1, kq, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMAs
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma(a0, b0[j], acc[j]);
+    __builtin_amdgcn_sched_barrier(0);
+    wgrad_load<NJ>(sm, aoff, boff, ks + 2, kq, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[j] = mfma(a1, b1[j], acc[j]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = mfma(a0, b0[j], acc[j]);
+}
+
+// conv2 dgrad of NM m-tiles over taps [r0, r1): two accumulator chains per m-tile (even / odd o-quads);
+// the 8 (NM+1) operands of tap r+1 are read while tap r's MFMAs run (alternating register sets)
+template <int NM>
+__device__ __forceinline__ void dgrad_load(const float* sm, const int (&aoff)[NM], int boff, int r, float (&a)[NM][8],
+                                           float (&b)[8]) {
+  const int ro = tap_off(r);
+  const float* bp = sm + boff + r * 32;
+#pragma unroll
+  for (int oc = 0; oc < 8; ++oc) b[oc] = bp[4 * oc];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const float* ap = sm + (aoff[m] - ro);
+#pragma unroll
+    for (int oc = 0; oc < 8; ++oc) a[m][oc] = ap[4 * oc * CS];
+  }
+}
+
+template <int NM>
+__device__ __forceinline__ void dgrad_mma(const float (&a)[NM][8], const float (&b)[8], f4 (&acc)[NM][2]) {
+#pragma unroll
+  for (int oc = 0; oc < 8; ++oc)
+#pragma unroll
+    for (int m = 0; m < NM; ++m) acc[m][oc & 1] = mfma(a[m][oc], b[oc], acc[m][oc & 1]);
+}
+
+template <int NM>
+__device__ __forceinline__ void bwd_dgrad2(const float* sm, const int (&aoff)[NM], int boff, int r0, int r1,
+                                           f4 (&acc)[NM][2]) {
+  float a0[NM][8], b0[8], a1[NM][8], b1[8];
+  dgrad_load<NM>(sm, aoff, boff, r0, a0, b0);
+  int r = r0;
+#pragma unroll 1
+  for (; r + 2 < r1; r += 2) {
+    dgrad_load<NM>(sm, aoff, boff, r + 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMAs
+    dgrad_mma<NM>(a0, b0, acc);
+    __builtin_amdgcn_sched_barrier(0);
+    dgrad_load<NM>(sm, aoff, boff, r + 2, a0, b0);
+    __builtin_amdgcn_sched_barrier(0);
+    dgrad_mma<NM>(a1, b1, acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (r + 1 < r1) {   // two taps left
+    dgrad_load<NM>(sm, aoff, boff, r + 1, a1, b1);
+    __builtin_amdgcn_sched_barrier(0);
+    dgrad_mma<NM>(a0, b0, acc);
+    dgrad_mma<NM>(a1, b1, acc);
+  } else {
+    dgrad_mma<NM>(a0, b0, acc);
+  }
+}
+
+// dP1 rows of a finished dgrad m-tile, ReLU-masked by pool1 > 0 (the conv1 ReLU derivative)
+__device__ __forceinline__ void bwd_dp1_store(float* dp1, const float* p1s, int mt, f4 acc, int i, int kq) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int p = mt * 16 + 4 * kq + r;
+    if (p < H2 * H2) dp1[i * DPS + p] = p1s[i * CS + q14(p) + 2 * P1P + 2] > 0.f ? acc[r] : 0.f;
+  }
+}
+
+// one sample's conv-stack inputs in registers (fixed per-thread element lists, all loads in flight at once)
+struct BwdStage {
+  static constexpr int ND = (C2 * Q2 * Q2 + NT - 1) / NT, NP = (C1 * Q1 * Q1 + NT - 1) / NT,
+                       NI = (IMG * IMG + NT - 1) / NT;
+  uint8_t am2[ND], a1[NP];
+  float pl2[ND], dp2[ND], p1[NP], im[NI];
+
+  __device__ __forceinline__ void load(size_t sidx, const float* __restrict__ X, const float* __restrict__ pool1,
+                                       const uint8_t* __restrict__ am1, const float* __restrict__ pool2,
+                                       const uint8_t* __restrict__ am2g, const float* __restrict__ dP2, int tid) {
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {   // pooled conv2 gradients: one 2x2 window each
+      const int e = tid + j * NT;
+      if (e < C2 * Q2 * Q2) {
+        const size_t q = sidx * C2 * Q2 * Q2 + e;
+        am2[j] = am2g[q];
+        pl2[j] = pool2[q];
+        dp2[j] = dP2[q];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int e = tid + j * NT;
+      if (e < C1 * Q1 * Q1) {
+        p1[j] = pool1[sidx * C1 * Q1 * Q1 + e];
+        a1[j] = am1[sidx * C1 * Q1 * Q1 + e];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int e = tid + j * NT;
+      if (e < IMG * IMG) im[j] = X[sidx * IMG * IMG + e];
+    }
+  }
+  // unpool2 (+ReLU mask) into padded dc2, pool1 -> padded p1s, argmax1, image
+  __device__ __forceinline__ void store(float* dc2, float* p1s, uint8_t* a1s, float* img, int tid) const {
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int e = tid + j * NT;
+      if (e < C2 * Q2 * Q2) {
+        const int o = e / (Q2 * Q2), w = e - o * Q2 * Q2, wy = w / Q2, wx = w - wy * Q2;
+        const float v = pl2[j] > 0.f ? dp2[j] : 0.f;
+        float* d = dc2 + o * CS + (2 * wy + 2) * P1P + 2 * wx + 2;
+        d[0] = am2[j] == 0 ? v : 0.f;
+        d[1] = am2[j] == 1 ? v : 0.f;
+        d[P1P] = am2[j] == 2 ? v : 0.f;
+        d[P1P + 1] = am2[j] == 3 ? v : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int e = tid + j * NT;
+      if (e < C1 * Q1 * Q1) {
+        const int ci = e / (Q1 * Q1), r = e - ci * Q1 * Q1;
+        p1s[ci * CS + (r / Q1 + 2) * P1P + (r % Q1) + 2] = p1[j];
+        a1s[ci * DPS + r] = a1[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int e = tid + j * NT;
+      if (e < IMG * IMG) img[(e / IMG + 2) * IMS + (e % IMG) + 2] = im[j];
+    }
+  }
+};
 
 __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const float* __restrict__ params,
                                               int P, int B, int G, CnnOff off, const float* __restrict__ pool1,
@@ -176,131 +358,108 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
                                               const uint8_t* __restrict__ am2, const float* __restrict__ dP2,
                                               float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* w2t = sm;                          // [16][801]: w2t[ci][o*25+r] = W2[o][ci][r]
-  float* dc2 = w2t + C1 * W2T;              // [32][18*18] padded dL/d conv2-output (post-unpool, ReLU-masked)
-  float* p1s = dc2 + C2 * P1P * P1P;        // [16][18*18] padded pool1 (conv2 input)
-  float* dp1 = p1s + C1 * P1P * P1P;        // [16][196]   dL/d pool1
-  float* img = dp1 + C1 * Q1 * Q1;          // [32*32] padded image
-  float* red = img + IMGP * IMGP;           // [8 waves][2 tiles][256]: conv1-wgrad wave partials
-  float* bsum = red + NW * 2 * 256;         // [48]: db2 | db1 accumulators
-  int* kofT = reinterpret_cast<int*>(bsum + 48);   // [800] (o,dy,dx) -> offset in padded dc2 (dgrad)
-  int* kof2 = kofT + 2 * K2;                // [400] (ci,dy,dx) -> offset in padded pool1 (wgrad)
-  uint8_t* a1s = reinterpret_cast<uint8_t*>(kof2 + K2);   // [16][196] argmax of pool1
+  float* w2r = sm;                          // [16][802]: w2r[ci][tap*32 + o] = W2[o][ci][tap]
+  float* dc2 = w2r + C1 * W2R;              // [32][338] padded dL/d conv2-output (post-unpool, ReLU-masked)
+  float* p1s = dc2 + C2 * CS;               // [16][338] padded pool1 (conv2 input)
+  float* dp1 = p1s + C1 * CS;               // [16][198] dL/d pool1, ReLU-masked
+  float* img = dp1 + C1 * DPS;              // [32][37]  padded image
+  float* ones = img + IMGP * IMS;           // [256]     1.0 (bias columns)
+  float* red12 = ones + 256;                // [4][64]   m-tile 12 partials of waves 4..7
+  uint8_t* a1s = reinterpret_cast<uint8_t*>(red12 + 256);   // [16][198] argmax of pool1
+  float* red = dc2;                         // [8 waves][2][256] conv1 wgrad partials (after the sample loop)
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): per-wave branches are scalar
   const int k = blockIdx.x / G, g = blockIdx.x - k * G;
   const int s0 = g * BS;
   const int ns = min(BS, B - s0);
   const float* prow = params + (size_t)k * P;
   const int i = lane & 15, kq = lane >> 4;
 
-  for (int e = tid; e < C2 * K2; e += NT) {   // W2 [o][ci][r] -> w2t[ci][o*25 + r]
+  for (int e = tid; e < C2 * K2; e += NT) {   // W2 [o][ci][tap] -> w2r[ci][tap*32 + o]
     const int o = e / K2, rem = e - o * K2, ci = rem / 25, r = rem - ci * 25;
-    w2t[ci * W2T + o * 25 + r] = prow[off.w2 + e];
+    w2r[ci * W2R + r * 32 + o] = prow[off.w2 + e];
   }
-  for (int kk = tid; kk < 2 * K2; kk += NT) {  // dgrad: kk = (o,dy,dx): -o*324 ... taps flipped
-    const int o = kk / 25, r = kk - o * 25;
-    kofT[kk] = o * P1P * P1P - (r / 5) * P1P - (r % 5);
-  }
-  for (int kk = tid; kk < K2; kk += NT) {
-    const int ci = kk / 25, r = kk - ci * 25;
-    kof2[kk] = ci * P1P * P1P + (r / 5) * P1P + (r % 5);
-  }
-  for (int e = tid; e < C2 * P1P * P1P; e += NT) dc2[e] = 0.f;
-  for (int e = tid; e < C1 * P1P * P1P; e += NT) p1s[e] = 0.f;
-  for (int e = tid; e < IMGP * IMGP; e += NT) img[e] = 0.f;
-  if (tid < 48) bsum[tid] = 0.f;
+  for (int e = tid; e < (C2 + C1) * CS; e += NT) dc2[e] = 0.f;   // dc2 and p1s are contiguous
+  for (int e = tid; e < IMGP * IMS; e += NT) img[e] = 0.f;
+  if (tid < 256) ones[tid] = 1.f;
 
-  // conv2 wgrad accumulators: wave owns m-tile (wave & 1) and n-tiles nt = (wave >> 1) + 4j
-  constexpr int NJ = 7;
-  f4 wacc[NJ];
+  // conv2 wgrad tiles: m-tile (o rows) and 7 / 6 n-tiles (taps; n-tile 25 = ones -> db2)
+  const int wmt = (wave >> 1) & 1;
+  const int nt0 = wave < 4 ? (wave & 1) * 7 : 14 + (wave & 1) * 6;
+  const int waoff = (int)(dc2 - sm) + (wmt * 16 + i) * CS + 2 * P1P + 2;
+  int wboff[7];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) wacc[j] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 7; ++j) {
+    const int nt = min(nt0 + j, NT2 - 1);
+    wboff[j] = nt < 25 ? (int)(p1s - sm) + i * CS + tap_off(nt) : (int)(ones - sm);
+  }
+  f4 wacc[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) wacc[j] = f4{0.f, 0.f, 0.f, 0.f};
   f4 c1acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  const int dboff = (int)(w2r - sm) + i * W2R + kq;   // dgrad B: w2r[i][tap*32 + 4*oc + kq]
   __syncthreads();
 
+  BwdStage st;
+  st.load((size_t)k * B + s0, X, pool1, am1, pool2, am2, dP2, tid);
   for (int s = 0; s < ns; ++s) {
-    const size_t sidx = (size_t)k * B + s0 + s;
-    // ---- stage: unpool2 (+ReLU mask) into padded dc2, pool1 -> padded p1s, image, argmax1
-    for (int e = tid; e < C2 * H2 * H2; e += NT) {
-      const int o = e / (H2 * H2), r = e - o * H2 * H2, y = r / H2, x = r % H2;
-      const int w = (y >> 1) * Q2 + (x >> 1), pos = ((y & 1) << 1) | (x & 1);
-      const size_t q = sidx * C2 * Q2 * Q2 + o * Q2 * Q2 + w;
-      dc2[o * P1P * P1P + (y + 2) * P1P + x + 2] = (am2[q] == pos && pool2[q] > 0.f) ? dP2[q] : 0.f;
-    }
-    for (int e = tid; e < C1 * Q1 * Q1; e += NT) {
-      const int ci = e / (Q1 * Q1), r = e - ci * Q1 * Q1;
-      p1s[ci * P1P * P1P + (r / Q1 + 2) * P1P + (r % Q1) + 2] = pool1[sidx * C1 * Q1 * Q1 + e];
-      a1s[e] = am1[sidx * C1 * Q1 * Q1 + e];
-    }
-    for (int e = tid; e < IMG * IMG; e += NT) img[(e / IMG + 2) * IMGP + (e % IMG) + 2] = X[sidx * IMG * IMG + e];
+    // ---- stage the sample loaded during the previous one; then issue the next sample's loads, which
+    //      complete behind this sample's MFMA work (one workgroup per CU: nothing else hides them)
+    st.store(dc2, p1s, a1s, img, tid);
+    if (s + 1 < ns) st.load((size_t)k * B + s0 + s + 1, X, pool1, am1, pool2, am2, dP2, tid);
     __syncthreads();
-    // db2 += sum over the 14x14 map
-    if (tid < C2) {
-      float sacc = 0.f;
-      for (int y = 0; y < H2; ++y)
-        for (int x = 0; x < H2; ++x) sacc += dc2[tid * P1P * P1P + (y + 2) * P1P + x + 2];
-      bsum[tid] += sacc;
-    }
 
-    // ---- conv2 wgrad: dW2[o][kk] += sum_p dc2[o][p] * pool1pad[p + kof2[kk]]   (M=32, N=400, K=196)
+    // ---- conv2 wgrad (accumulates over the workgroup's samples)
+    if (wave < 4) bwd_wgrad2<7>(sm, waoff, wboff, wacc, kq);
+    else bwd_wgrad2<6>(sm, waoff, wboff, wacc, kq);
+
+    // ---- conv2 dgrad -> dp1
+    if (wave < 4) {
+      const int mt0 = 2 * wave;
+      const int aoff[2] = {(int)(dc2 - sm) + kq * CS + q14(mt0 * 16 + i) + 4 * P1P + 4,
+                           (int)(dc2 - sm) + kq * CS + q14(mt0 * 16 + 16 + i) + 4 * P1P + 4};
+      f4 acc[2][2] = {};
+      bwd_dgrad2<2>(sm, aoff, dboff, 0, 25, acc);
+      bwd_dp1_store(dp1, p1s, mt0, acc[0][0] + acc[0][1], i, kq);
+      bwd_dp1_store(dp1, p1s, mt0 + 1, acc[1][0] + acc[1][1], i, kq);
+    } else {
+      const int mt = 4 + wave;
+      const int aoff[1] = {(int)(dc2 - sm) + kq * CS + q14(mt * 16 + i) + 4 * P1P + 4};
+      f4 acc[1][2] = {};
+      bwd_dgrad2<1>(sm, aoff, dboff, 0, 25, acc);
+      bwd_dp1_store(dp1, p1s, mt, acc[0][0] + acc[0][1], i, kq);
+      // m-tile 12: rows 192..195 valid (rows past 195 read a clamped in-range row and are dropped)
+      const int w4 = wave - 4;
+      const int aoff12[1] = {(int)(dc2 - sm) + kq * CS + q14(min(192 + i, H2 * H2 - 1)) + 4 * P1P + 4};
+      f4 acc12[1][2] = {};
+      bwd_dgrad2<1>(sm, aoff12, dboff, w4 == 0 ? 0 : 1 + 6 * w4, 7 + 6 * w4, acc12);
+      if (kq == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red12[w4 * 64 + r * 16 + i] = acc12[0][0][r] + acc12[0][1][r];
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {   // m-tile 12 partials in fixed wave order
+      const int r = tid >> 4, ci = tid & 15, p = 192 + r;
+      const float v = ((red12[tid] + red12[64 + tid]) + red12[128 + tid]) + red12[192 + tid];
+      dp1[ci * DPS + p] = p1s[ci * CS + q14(p) + 2 * P1P + 2] > 0.f ? v : 0.f;
+    }
+    __syncthreads();
+
+    // ---- conv1 wgrad: dC1 = unpool1(dp1) on the fly; K = 784 split across the 8 waves
     {
-      const int mt = wave & 1;
-      const int o = mt * 16 + i;
-      for (int ks = 0; ks < 49; ++ks) {
-        const int p = ks * 4 + kq, y = p / H2, x = p % H2;
-        const float a = dc2[o * P1P * P1P + (y + 2) * P1P + x + 2];
-        const float* base = p1s + y * P1P + x;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          const int nt = (wave >> 1) + 4 * j;
-          if (nt < K2 / 16) wacc[j] = mfma(a, base[kof2[nt * 16 + i]], wacc[j]);
-        }
-      }
-    }
-
-    // ---- conv2 dgrad: dP1[ci][p] = sum_{o,dy,dx} dc2pad[o][p + 4*19 - tap] W2[o][ci][tap]  (M=196, N=16, K=800)
-    for (int mt = wave; mt < 13; mt += NW) {
-      const int p = mt * 16 + i;
-      const bool valid = p < H2 * H2;
-      const int pc = valid ? p : 0;
-      const float* base = dc2 + (pc / H2 + 4) * P1P + (pc % H2) + 4;
-      f4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-      for (int ks = 0; ks < 2 * K2 / 4; ++ks) {
-        const int kk = ks * 4 + kq;
-        acc = mfma(valid ? base[kofT[kk]] : 0.f, w2t[i * W2T + kk], acc);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int pr = mt * 16 + 4 * kq + r;
-        if (pr < H2 * H2) dp1[i * Q1 * Q1 + pr] = acc[r];
-      }
-    }
-    __syncthreads();
-    // db1 += sum of the unpooled (ReLU-masked) dP1
-    if (tid < C1) {
-      float sacc = 0.f;
-      for (int w = 0; w < Q1 * Q1; ++w) {
-        const float pv = p1s[tid * P1P * P1P + (w / Q1 + 2) * P1P + (w % Q1) + 2];
-        sacc += pv > 0.f ? dp1[tid * Q1 * Q1 + w] : 0.f;
-      }
-      bsum[C2 + tid] += sacc;
-    }
-
-    // ---- conv1 wgrad: dW1[o][kk] += sum_{p in 28x28} dC1[o][p] img[p + tap(kk)]  (M=16, N=25->32, K=784)
-    //      dC1 = unpool1(dP1) on the fly; K split across the 8 waves (partials reduced at the end)
-    for (int ks = wave; ks < H1 * H1 / 4; ks += NW) {
-      const int p = ks * 4 + kq, y = p / H1, x = p % H1;
-      const int w = (y >> 1) * Q1 + (x >> 1), pos = ((y & 1) << 1) | (x & 1);
-      const int o = i;
-      const float pv = p1s[o * P1P * P1P + (w / Q1 + 2) * P1P + (w % Q1) + 2];
-      const float a = (a1s[o * Q1 * Q1 + w] == pos && pv > 0.f) ? dp1[o * Q1 * Q1 + w] : 0.f;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int tap = h * 16 + i;      // B[kk = p][j = tap]
-        const float b = tap < K1 ? img[(y + tap / 5) * IMGP + x + tap % 5] : 0.f;
-        c1acc[h] = mfma(a, b, c1acc[h]);
+      const int toff0 = (i / 5) * IMS + i % 5;
+      const int t1 = min(16 + i, 24);
+      const int toff1 = (t1 / 5) * IMS + t1 % 5;
+      const bool one1 = 16 + i >= K1;
+      for (int ks = wave; ks < H1 * H1 / 4; ks += NW) {
+        const int p = ks * 4 + kq, y = p / H1, x = p - y * H1;
+        const int w = (y >> 1) * Q1 + (x >> 1), pos = ((y & 1) << 1) | (x & 1);
+        const float a = a1s[i * DPS + w] == pos ? dp1[i * DPS + w] : 0.f;
+        const float* im = img + y * IMS + x;
+        c1acc[0] = mfma(a, im[toff0], c1acc[0]);
+        const float b1 = im[toff1];
+        c1acc[1] = mfma(a, one1 ? 1.f : b1, c1acc[1]);
       }
     }
     __syncthreads();   // LDS is restaged for the next sample
@@ -308,17 +467,16 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
 
   // ---- write partials (fixed order: deterministic)
   float* out = part + (size_t)blockIdx.x * PART;
-  {
-    const int mt = wave & 1;
+  const int nj = wave < 4 ? 7 : 6;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int nt = (wave >> 1) + 4 * j;
-      if (nt < K2 / 16) {
+  for (int j = 0; j < 7; ++j) {
+    const int nt = nt0 + j;
+    if (j < nj) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int o = mt * 16 + 4 * kq + r, kk = nt * 16 + i;
-          out[o * K2 + kk] = wacc[j][r];
-        }
+      for (int r = 0; r < 4; ++r) {
+        const int o = wmt * 16 + 4 * kq + r;
+        if (nt < 25) out[o * K2 + i * 25 + nt] = wacc[j][r];
+        else if (i == 0) out[C2 * K2 + o] = wacc[j][r];
       }
     }
   }
@@ -327,14 +485,13 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
 #pragma unroll
     for (int r = 0; r < 4; ++r) red[(wave * 2 + h) * 256 + (4 * kq + r) * 16 + i] = c1acc[h][r];
   __syncthreads();
-  for (int e = tid; e < C1 * K1; e += NT) {
-    const int o = e / K1, tap = e - o * K1, h = tap >> 4, j = tap & 15;
+  for (int e = tid; e < C1 * (K1 + 1); e += NT) {   // taps 0..24 -> dW1, tap 25 (ones) -> db1
+    const int o = e / (K1 + 1), tap = e - o * (K1 + 1), h = tap >> 4, j = tap & 15;
     float sacc = 0.f;
     for (int w = 0; w < NW; ++w) sacc += red[(w * 2 + h) * 256 + o * 16 + j];
-    out[C2 * K2 + C2 + e] = sacc;
+    if (tap < K1) out[C2 * K2 + C2 + o * K1 + tap] = sacc;
+    else out[C2 * K2 + C2 + C1 * K1 + o] = sacc;
   }
-  if (tid < C2) out[C2 * K2 + tid] = bsum[tid];
-  if (tid < C1) out[C2 * K2 + C2 + C1 * K1 + tid] = bsum[C2 + tid];
 }
 
 // grad[k][dst(e)] = sum_g part[k*G + g][e]   (fixed order over groups)
@@ -432,8 +589,7 @@ size_t fwd_lds() {
   return (size_t)(C2 * W2S + C1 * K1P + C1 + C2) * 4 + (K2 + K1P) * 4 + (size_t)(FSG * IMGP * IMGP + FSG * C1 * P1P * P1P) * 4;
 }
 size_t bwd_lds() {
-  return (size_t)(C1 * W2T + C2 * P1P * P1P + C1 * P1P * P1P + C1 * Q1 * Q1 + IMGP * IMGP + NW * 2 * 256 + 48) * 4 +
-         (size_t)(2 * K2 + K2) * 4 + C1 * Q1 * Q1;
+  return (size_t)(C1 * W2R + (C2 + C1) * CS + C1 * DPS + IMGP * IMS + 256 + 256) * 4 + C1 * DPS;
 }
 
 }  // namespace cnn
