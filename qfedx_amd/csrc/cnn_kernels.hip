@@ -34,8 +34,6 @@ constexpr int C2 = 32, H2 = 14, Q2 = 7;    // conv2 channels, output size, poole
 constexpr int P1P = 18;            // pooled1 zero-padded by 2 (conv2 input)
 constexpr int K1 = 25, K1P = 28;   // conv1 reduction (dy,dx), padded to the MFMA k-step
 constexpr int K2 = 400;            // conv2 reduction (ci,dy,dx)
-constexpr int W2S = 401;           // LDS row stride of W2 [32][400] (odd: conflict-free B fetches)
-constexpr int FSG = 2;             // samples per forward workgroup
 
 struct CnnOff {                    // float offsets of the tensors inside one client's parameter row
   int w1, b1, w2, b2;
@@ -52,113 +50,246 @@ __global__ void mfma_probe(const float* A, const float* B, float* D, int K) {
 }
 
 // --------------------------------------------------------------------------------------------
+// shared helpers
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ int q14(int p) { return p + 4 * (p / H2); }   // (y, x) of a 14x14 map -> 18*y + x
+__device__ __forceinline__ int tap_off(int r) { return (r / 5) * P1P + r % 5; }   // 5x5 tap -> padded 18-wide map
+
+// Software-pipelined loop over k-chunks [c0, c1): chunk c+1's operands are read into the other register
+// set before chunk c's MFMAs issue (the sched barriers keep the compiler from sinking the reads below
+// the MFMAs), so LDS latency overlaps matrix work even with two waves per SIMD.
+template <class Set, class Load, class Mma>
+__device__ __forceinline__ void pipelined(int c0, int c1, Load&& load, Mma&& mma) {
+  Set s0, s1;
+  load(c0, s0);
+  int c = c0;
+#pragma unroll 1
+  for (; c + 2 < c1; c += 2) {
+    load(c + 1, s1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(s0);
+    __builtin_amdgcn_sched_barrier(0);
+    load(c + 2, s0);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(s1);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (c + 1 < c1) {
+    load(c + 1, s1);
+    __builtin_amdgcn_sched_barrier(0);
+    mma(s0);
+    mma(s1);
+  } else {
+    mma(s0);
+  }
+}
+
+// bias + ReLU + 2x2 max-pool (+ argmax 0..3, first maximum wins) of one window held in 4 registers
+__device__ __forceinline__ float relu_pool(f4 acc, float bias, int& arg) {
+  float best = fmaxf(acc[0] + bias, 0.f);
+  arg = 0;
+#pragma unroll
+  for (int r = 1; r < 4; ++r) {
+    const float v = fmaxf(acc[r] + bias, 0.f);
+    if (v > best) { best = v; arg = r; }
+  }
+  return best;
+}
+
+// --------------------------------------------------------------------------------------------
 // forward: conv1 -> ReLU -> pool -> conv2 -> ReLU -> pool for FSG samples of one client
 //   outputs per sample: pool1 [16][196], am1 [16][196] (argmax 0..3), pool2 [32][49], am2 [32][49]
+//
+//   conv1  M = 196 windows x 4 (49 m-tiles), N = 16, K = 28: B (W1) stays in 7 registers for the whole
+//          phase, each lane's 7 tap offsets are registers; two m-tiles per step (two MFMA chains)
+//   conv2  M = 48 windows x 4 (12 full m-tiles) + window 48, N = 32, K ordered (tap, ci) = 25 x 16:
+//          A[row][(r, ci)] = p1pad[ci][q(row) + off(r)], B = w2f[o][r*16 + ci]; the tap offset is
+//          wave-uniform and ci runs over immediate offsets.  Wave w owns 6 full (sample, m-tile)
+//          units as two groups of 3 m-tiles (6 accumulator chains) and half the taps of sample
+//          w/2's last m-tile (window 48); the two halves are summed in fixed order afterwards.
 // --------------------------------------------------------------------------------------------
+constexpr int FSG = 4;             // samples per forward workgroup
+constexpr int CSF = 328;           // LDS stride of one padded 18x18 pool1 map (== 8 mod 32)
+constexpr int W2F = 402;           // LDS stride of W2 reordered as w2f[o][tap*16 + ci] (== 18 mod 32)
+static_assert(FSG * 2 == NW, "conv2 partial m-tile: one (sample, half) per wave");
+
+// conv2 (forward) GEMM row -> offset of its 5x5 window origin in the padded 18-wide map
+__device__ __forceinline__ int fwd_q2(int row) {
+  const int w = min(row >> 2, Q2 * Q2 - 1), pos = row & 3;   // rows past window 48 clamp (dropped later)
+  return (2 * (w / Q2) + (pos >> 1)) * P1P + 2 * (w % Q2) + (pos & 1);
+}
+
+template <int NM>
+struct Fwd2Set {
+  float a[NM][4], b[2][4];
+};
+
+template <int NM>
+__device__ __forceinline__ void fwd_conv2(const float* sm, const int (&aoff)[NM], int boff, int r0, int r1,
+                                          f4 (&acc)[NM][2]) {
+  pipelined<Fwd2Set<NM>>(
+      r0, r1,
+      [&](int r, Fwd2Set<NM>& st) {
+        const float* bp = sm + boff + r * 16;
+#pragma unroll
+        for (int cq = 0; cq < 4; ++cq) {
+          st.b[0][cq] = bp[4 * cq];
+          st.b[1][cq] = bp[16 * W2F + 4 * cq];
+        }
+        const int ro = tap_off(r);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          const float* ap = sm + (aoff[m] + ro);
+#pragma unroll
+          for (int cq = 0; cq < 4; ++cq) st.a[m][cq] = ap[4 * cq * CSF];
+        }
+      },
+      [&](const Fwd2Set<NM>& st) {
+#pragma unroll
+        for (int cq = 0; cq < 4; ++cq)
+#pragma unroll
+          for (int m = 0; m < NM; ++m)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) acc[m][h] = mfma(st.a[m][cq], st.b[h][cq], acc[m][h]);
+      });
+}
+
 __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const float* __restrict__ params,
                                               int P, int B, int G, CnnOff off, float* __restrict__ pool1,
                                               uint8_t* __restrict__ am1, float* __restrict__ pool2,
                                               uint8_t* __restrict__ am2) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* w2s = sm;                          // [32][401]
-  float* w1s = w2s + C2 * W2S;              // [16][28]  (k >= 25 zero)
+  float* w2f = sm;                          // [32][402]: w2f[o][tap*16 + ci] = W2[o][ci][tap]
+  float* w1s = w2f + C2 * W2F;              // [16][28]  (tap >= 25 zero)
   float* b1s = w1s + C1 * K1P;              // [16]
   float* b2s = b1s + C1;                    // [32]
-  int* koff2 = reinterpret_cast<int*>(b2s + C2);   // [400] (ci,dy,dx) -> offset in padded pool1
-  int* koff1 = koff2 + K2;                  // [28]  (dy,dx) -> offset in padded image
-  float* img = reinterpret_cast<float*>(koff1 + K1P);   // [FSG][32*32]
-  float* p1s = img + FSG * IMGP * IMGP;     // [FSG][16][18*18]
+  float* img = b2s + C2;                    // [FSG][32*32] zero-padded images
+  float* p1s = img + FSG * IMGP * IMGP;     // [FSG][16][328] zero-padded pool1
+  float* red = img;                         // [FSG][2 halves][32 o][4]: window-48 partials (images dead)
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int k = blockIdx.x / G, g = blockIdx.x - k * G;
   const int s0 = g * FSG;
   const int ns = min(FSG, B - s0);
   const float* prow = params + (size_t)k * P;
+  const int i = lane & 15, kq = lane >> 4;
 
-  for (int e = tid; e < C2 * K2; e += NT) { const int o = e / K2, kk = e - o * K2; w2s[o * W2S + kk] = prow[off.w2 + e]; }
+  for (int e = tid; e < C2 * K2; e += NT) {   // W2 [o][ci][tap] -> w2f[o][tap*16 + ci]
+    const int o = e / K2, rem = e - o * K2, ci = rem / 25, r = rem - ci * 25;
+    w2f[o * W2F + r * 16 + ci] = prow[off.w2 + e];
+  }
   for (int e = tid; e < C1 * K1P; e += NT) {
     const int o = e / K1P, kk = e - o * K1P;
     w1s[e] = kk < K1 ? prow[off.w1 + o * K1 + kk] : 0.f;
   }
   if (tid < C1) b1s[tid] = prow[off.b1 + tid];
   if (tid < C2) b2s[tid] = prow[off.b2 + tid];
-  for (int kk = tid; kk < K2; kk += NT) {
-    const int ci = kk / 25, r = kk - ci * 25;
-    koff2[kk] = ci * P1P * P1P + (r / 5) * P1P + (r % 5);
-  }
-  if (tid < K1P) koff1[tid] = tid < K1 ? (tid / 5) * IMGP + (tid % 5) : 0;
   for (int e = tid; e < FSG * IMGP * IMGP; e += NT) {
     const int s = e / (IMGP * IMGP), r = e - s * IMGP * IMGP, y = r / IMGP - 2, x = r % IMGP - 2;
     img[e] = (s < ns && y >= 0 && y < IMG && x >= 0 && x < IMG) ? X[((size_t)k * B + s0 + s) * IMG * IMG + y * IMG + x] : 0.f;
   }
-  for (int e = tid; e < FSG * C1 * P1P * P1P; e += NT) p1s[e] = 0.f;
+  for (int e = tid; e < FSG * C1 * CSF; e += NT) p1s[e] = 0.f;
   __syncthreads();
 
-  // ---- conv1: 49 m-tiles (196 pool windows x 4) per sample, N = 16, K = 28
-  const int i = lane & 15, kq = lane >> 4;
-  for (int t = wave; t < ns * 49; t += NW) {
-    const int s = t / 49, mt = t - s * 49;
-    const int w = mt * 4 + (i >> 2), pos = i & 3;
-    const int py = 2 * (w / Q1) + (pos >> 1), px = 2 * (w % Q1) + (pos & 1);
-    const float* im = img + s * IMGP * IMGP + py * IMGP + px;
-    f4 acc = {0.f, 0.f, 0.f, 0.f};
+  // ---- conv1
+  {
+    float bw[K1P / 4];
+    int toff[K1P / 4];
 #pragma unroll
     for (int ks = 0; ks < K1P / 4; ++ks) {
       const int kk = ks * 4 + kq;
-      acc = mfma(im[koff1[kk]], w1s[i * K1P + kk], acc);
+      bw[ks] = w1s[i * K1P + kk];
+      toff[ks] = kk < K1 ? (kk / 5) * IMGP + kk % 5 : 0;   // w1s is zero there
     }
-    // lane holds window wo = mt*4 + kq, its 4 positions, channel o = i
-    const int wo = mt * 4 + kq, o = i;
-    const float bo = b1s[o];
-    float best = fmaxf(acc[0] + bo, 0.f);
-    int arg = 0;
+    const int nu = ns * 49;
+    for (int u = wave; u < nu; u += 2 * NW) {
+      const int u1 = u + NW < nu ? u + NW : u;
+      int ub[2];
 #pragma unroll
-    for (int r = 1; r < 4; ++r) {
-      const float v = fmaxf(acc[r] + bo, 0.f);
-      if (v > best) { best = v; arg = r; }
+      for (int h = 0; h < 2; ++h) {
+        const int uu = h ? u1 : u, s = uu / 49, mt = uu - s * 49;
+        const int w = mt * 4 + (i >> 2), pos = i & 3;
+        ub[h] = s * IMGP * IMGP + (2 * (w / Q1) + (pos >> 1)) * IMGP + 2 * (w % Q1) + (pos & 1);
+      }
+      float av[2][K1P / 4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int ks = 0; ks < K1P / 4; ++ks) av[h][ks] = img[ub[h] + toff[ks]];
+      f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int ks = 0; ks < K1P / 4; ++ks)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) acc[h] = mfma(av[h][ks], bw[ks], acc[h]);
+      // lane holds window wo = mt*4 + kq, its 4 positions, channel o = i
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && u1 == u) break;
+        const int uu = h ? u1 : u, s = uu / 49, mt = uu - s * 49;
+        const int wo = mt * 4 + kq, o = i;
+        int arg;
+        const float best = relu_pool(acc[h], b1s[o], arg);
+        const size_t so = ((size_t)k * B + s0 + s) * C1 * Q1 * Q1 + o * Q1 * Q1 + wo;
+        pool1[so] = best;
+        am1[so] = (uint8_t)arg;
+        p1s[s * C1 * CSF + o * CSF + (wo / Q1 + 2) * P1P + (wo % Q1) + 2] = best;
+      }
     }
-    const size_t so = ((size_t)k * B + s0 + s) * C1 * Q1 * Q1 + o * Q1 * Q1 + wo;
-    pool1[so] = best;
-    am1[so] = (uint8_t)arg;
-    p1s[s * C1 * P1P * P1P + o * P1P * P1P + (wo / Q1 + 2) * P1P + (wo % Q1) + 2] = best;
   }
   __syncthreads();
 
-  // ---- conv2: 13 m-tiles (49 windows x 4, padded to 52) per sample, N = 32 (two n-tiles), K = 400
-  for (int t = wave; t < ns * 13; t += NW) {
-    const int s = t / 13, mt = t - s * 13;
-    const int w = mt * 4 + (i >> 2), pos = i & 3;
-    const bool valid = w < Q2 * Q2;
-    const int wc = valid ? w : 0;
-    const int py = 2 * (wc / Q2) + (pos >> 1), px = 2 * (wc % Q2) + (pos & 1);
-    const float* in = p1s + s * C1 * P1P * P1P + py * P1P + px;
-    f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int ks = 0; ks < K2 / 4; ++ks) {
-      const int kk = ks * 4 + kq;
-      const float a = valid ? in[koff2[kk]] : 0.f;
-      acc0 = mfma(a, w2s[i * W2S + kk], acc0);
-      acc1 = mfma(a, w2s[(16 + i) * W2S + kk], acc1);
-    }
-    const int wo = mt * 4 + kq;
-    if (wo < Q2 * Q2) {
+  // ---- conv2: full m-tiles
+  const int boff = (int)(w2f - sm) + i * W2F + kq;
+#pragma unroll 1
+  for (int gq = 0; gq < 2; ++gq) {
+    const int u = 6 * wave + 3 * gq, s = u / 12, mt0 = u - s * 12;
+    if (s >= ns) break;
+    int aoff[3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) aoff[m] = (int)(p1s - sm) + (s * C1 + kq) * CSF + fwd_q2((mt0 + m) * 16 + i);
+    f4 acc[3][2] = {};
+    fwd_conv2<3>(sm, aoff, boff, 0, 25, acc);
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int wo = (mt0 + m) * 4 + kq;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const f4 acc = h ? acc1 : acc0;
         const int o = h * 16 + i;
-        const float bo = b2s[o];
-        float best = fmaxf(acc[0] + bo, 0.f);
-        int arg = 0;
-#pragma unroll
-        for (int r = 1; r < 4; ++r) {
-          const float v = fmaxf(acc[r] + bo, 0.f);
-          if (v > best) { best = v; arg = r; }
-        }
+        int arg;
+        const float best = relu_pool(acc[m][h], b2s[o], arg);
         const size_t so = ((size_t)k * B + s0 + s) * C2 * Q2 * Q2 + o * Q2 * Q2 + wo;
         pool2[so] = best;
         am2[so] = (uint8_t)arg;
       }
     }
+  }
+  // ---- conv2: window 48 (m-tile 12), half of the taps per wave
+  {
+    const int s = wave >> 1, half = wave & 1;
+    f4 acc[1][2] = {};
+    if (s < ns) {
+      const int aoff[1] = {(int)(p1s - sm) + (s * C1 + kq) * CSF + fwd_q2(12 * 16 + i)};
+      fwd_conv2<1>(sm, aoff, boff, half ? 13 : 0, half ? 25 : 13, acc);
+    }
+    if (s < ns && kq == 0) {   // red aliases the images, dead since conv1
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[((s * 2 + half) * C2 + h * 16 + i) * 4 + r] = acc[0][h][r];
+    }
+  }
+  __syncthreads();
+  if (tid < ns * C2) {
+    const int s = tid / C2, o = tid - s * C2;
+    f4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = red[((s * 2) * C2 + o) * 4 + r] + red[((s * 2 + 1) * C2 + o) * 4 + r];
+    int arg;
+    const float best = relu_pool(v, b2s[o], arg);
+    const size_t so = ((size_t)k * B + s0 + s) * C2 * Q2 * Q2 + o * Q2 * Q2 + Q2 * Q2 - 1;
+    pool2[so] = best;
+    am2[so] = (uint8_t)arg;
   }
 }
 
@@ -187,94 +318,57 @@ constexpr int IMS = 37;            // LDS row stride of the padded image
 constexpr int NT2 = 26;            // conv2 wgrad n-tiles (25 taps + ones)
 constexpr int PART = C2 * K2 + C2 + C1 * K1 + C1;
 
-__device__ __forceinline__ int q14(int p) { return p + 4 * (p / H2); }   // (y, x) of a 14x14 map -> 18*y + x
-__device__ __forceinline__ int tap_off(int r) { return (r / 5) * P1P + r % 5; }
-
-// conv2 wgrad over the 49 k-steps of one sample: acc[j] += A(o rows) x B(n-tile j).  Two register sets
-// alternate: the operands of step ks+1 are read before the MFMAs of step ks issue, so LDS latency
-// overlaps MFMA work (no register copies between the sets, which would wait on the reads).
+// conv2 wgrad over the 49 k-steps of one sample: acc[j] += A(o rows) x B(n-tile j)
 template <int NJ>
-__device__ __forceinline__ void wgrad_load(const float* sm, int aoff, const int (&boff)[7], int ks, int kq, float& a,
-                                           float (&b)[NJ]) {
-  const int q = q14(ks * 4 + kq);
-  a = sm[aoff + q];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) b[j] = sm[boff[j] + q];
-}
+struct WgradSet {
+  float a, b[NJ];
+};
 
 template <int NJ>
 __device__ __forceinline__ void bwd_wgrad2(const float* sm, int aoff, const int (&boff)[7], f4 (&acc)[7], int kq) {
-  constexpr int NKS = H2 * H2 / 4;
-  static_assert(NKS % 2 == 1, "loop below pairs the steps and peels the last one");
-  float a0, b0[NJ], a1, b1[NJ];
-  wgrad_load<NJ>(sm, aoff, boff, 0, kq, a0, b0);
-#pragma unroll 1
-  for (int ks = 0; ks < NKS - 1; ks += 2) {
-    wgrad_load<NJ>(sm, aoff, boff, ks + 1, kq, a1, b1);
-    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMAs
+  pipelined<WgradSet<NJ>>(
+      0, H2 * H2 / 4,
+      [&](int ks, WgradSet<NJ>& st) {
+        const int q = q14(ks * 4 + kq);
+        st.a = sm[aoff + q];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = mfma(a0, b0[j], acc[j]);
-    __builtin_amdgcn_sched_barrier(0);
-    wgrad_load<NJ>(sm, aoff, boff, ks + 2, kq, a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
+        for (int j = 0; j < NJ; ++j) st.b[j] = sm[boff[j] + q];
+      },
+      [&](const WgradSet<NJ>& st) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[j] = mfma(a1, b1[j], acc[j]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) acc[j] = mfma(a0, b0[j], acc[j]);
+        for (int j = 0; j < NJ; ++j) acc[j] = mfma(st.a, st.b[j], acc[j]);
+      });
 }
 
-// conv2 dgrad of NM m-tiles over taps [r0, r1): two accumulator chains per m-tile (even / odd o-quads);
-// the 8 (NM+1) operands of tap r+1 are read while tap r's MFMAs run (alternating register sets)
+// conv2 dgrad of NM m-tiles over taps [r0, r1): two accumulator chains per m-tile (even / odd o-quads)
 template <int NM>
-__device__ __forceinline__ void dgrad_load(const float* sm, const int (&aoff)[NM], int boff, int r, float (&a)[NM][8],
-                                           float (&b)[8]) {
-  const int ro = tap_off(r);
-  const float* bp = sm + boff + r * 32;
-#pragma unroll
-  for (int oc = 0; oc < 8; ++oc) b[oc] = bp[4 * oc];
-#pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    const float* ap = sm + (aoff[m] - ro);
-#pragma unroll
-    for (int oc = 0; oc < 8; ++oc) a[m][oc] = ap[4 * oc * CS];
-  }
-}
-
-template <int NM>
-__device__ __forceinline__ void dgrad_mma(const float (&a)[NM][8], const float (&b)[8], f4 (&acc)[NM][2]) {
-#pragma unroll
-  for (int oc = 0; oc < 8; ++oc)
-#pragma unroll
-    for (int m = 0; m < NM; ++m) acc[m][oc & 1] = mfma(a[m][oc], b[oc], acc[m][oc & 1]);
-}
+struct DgradSet {
+  float a[NM][8], b[8];
+};
 
 template <int NM>
 __device__ __forceinline__ void bwd_dgrad2(const float* sm, const int (&aoff)[NM], int boff, int r0, int r1,
                                            f4 (&acc)[NM][2]) {
-  float a0[NM][8], b0[8], a1[NM][8], b1[8];
-  dgrad_load<NM>(sm, aoff, boff, r0, a0, b0);
-  int r = r0;
-#pragma unroll 1
-  for (; r + 2 < r1; r += 2) {
-    dgrad_load<NM>(sm, aoff, boff, r + 1, a1, b1);
-    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMAs
-    dgrad_mma<NM>(a0, b0, acc);
-    __builtin_amdgcn_sched_barrier(0);
-    dgrad_load<NM>(sm, aoff, boff, r + 2, a0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    dgrad_mma<NM>(a1, b1, acc);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  if (r + 1 < r1) {   // two taps left
-    dgrad_load<NM>(sm, aoff, boff, r + 1, a1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    dgrad_mma<NM>(a0, b0, acc);
-    dgrad_mma<NM>(a1, b1, acc);
-  } else {
-    dgrad_mma<NM>(a0, b0, acc);
-  }
+  pipelined<DgradSet<NM>>(
+      r0, r1,
+      [&](int r, DgradSet<NM>& st) {
+        const int ro = tap_off(r);
+        const float* bp = sm + boff + r * 32;
+#pragma unroll
+        for (int oc = 0; oc < 8; ++oc) st.b[oc] = bp[4 * oc];
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+          const float* ap = sm + (aoff[m] - ro);
+#pragma unroll
+          for (int oc = 0; oc < 8; ++oc) st.a[m][oc] = ap[4 * oc * CS];
+        }
+      },
+      [&](const DgradSet<NM>& st) {
+#pragma unroll
+        for (int oc = 0; oc < 8; ++oc)
+#pragma unroll
+          for (int m = 0; m < NM; ++m) acc[m][oc & 1] = mfma(st.a[m][oc], st.b[oc], acc[m][oc & 1]);
+      });
 }
 
 // dP1 rows of a finished dgrad m-tile, ReLU-masked by pool1 > 0 (the conv1 ReLU derivative)
@@ -586,7 +680,7 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, co
 }
 
 size_t fwd_lds() {
-  return (size_t)(C2 * W2S + C1 * K1P + C1 + C2) * 4 + (K2 + K1P) * 4 + (size_t)(FSG * IMGP * IMGP + FSG * C1 * P1P * P1P) * 4;
+  return (size_t)(C2 * W2F + C1 * K1P + C1 + C2 + FSG * IMGP * IMGP + FSG * C1 * CSF) * 4;
 }
 size_t bwd_lds() {
   return (size_t)(C1 * W2R + (C2 + C1) * CS + C1 * DPS + IMGP * IMS + 256 + 256) * 4 + C1 * DPS;
