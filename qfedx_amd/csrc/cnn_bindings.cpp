@@ -18,7 +18,7 @@ int qfx_cnn_head(const float* h1, const float* mask, const float* params, int P,
                  int B, const long long* y, const float* wts, float* dh1, float* dlog, float* loss, float* correct,
                  float* grad, hipStream_t st);
 int qfx_cnn_partial_size();
-int qfx_cnn_bwd_groups(int B);
+int qfx_cnn_bwd_groups(int K, int B);
 }
 
 namespace {
@@ -64,7 +64,7 @@ void backward(torch::Tensor X, torch::Tensor params, int64_t K, int64_t B, std::
   const int64_t S = K * B;
   const int P = (int)params.size(1);
   std::vector<int> o(off.begin(), off.end());
-  const int64_t G = qfx_cnn_bwd_groups((int)B);
+  const int64_t G = qfx_cnn_bwd_groups((int)K, (int)B);
   check(qfx_cnn_backward(dptr<float>(X, torch::kFloat32, "X", S * IMG), dptr<float>(params, torch::kFloat32, "params", K * P),
                          P, (int)K, (int)B, o.data(), dptr<float>(pool1, torch::kFloat32, "pool1", S * POOL1),
                          dptr<uint8_t>(am1, torch::kUInt8, "am1", S * POOL1), dptr<float>(pool2, torch::kFloat32, "pool2", S * POOL2),
@@ -96,5 +96,5 @@ void register_cnn(pybind11::module& m) {
   m.def("cnn_backward", &backward, "conv stack backward -> deterministic per-client weight/bias grads");
   m.def("cnn_head", &head, "ReLU + dropout + fc2 + weighted CE fwd/bwd per client");
   m.def("cnn_partial_size", []() { return qfx_cnn_partial_size(); });
-  m.def("cnn_bwd_groups", [](int64_t B) { return qfx_cnn_bwd_groups((int)B); });
+  m.def("cnn_bwd_groups", [](int64_t K, int64_t B) { return qfx_cnn_bwd_groups((int)K, (int)B); });
 }

@@ -294,7 +294,7 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
 }
 
 // --------------------------------------------------------------------------------------------
-// backward of the conv stack for BS samples of one client -> per-workgroup gradient partials
+// backward of the conv stack for bs samples of one client -> per-workgroup gradient partials
 //   part[(k*G + g)][ dW2 (12800) | db2 (32) | dW1 (400) | db1 (16) ]
 //
 // Per sample the three GEMMs are laid out so that no operand needs an index table and every
@@ -309,7 +309,7 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
 // m-tiles 2w, 2w+1 and 7 wgrad n-tiles; wave w>=4 owns dgrad m-tile 4+w, a quarter of the
 // reduction of m-tile 12 (rows 192..195, the only partial tile) and 6 wgrad n-tiles.
 // --------------------------------------------------------------------------------------------
-constexpr int BS = 4;              // samples per backward workgroup
+constexpr int BS_MAX = 16;         // samples per backward workgroup, at most (bwd_bs)
 constexpr int CS = 338;            // LDS stride of one zero-padded 18x18 map (== 18 mod 32: channel-strided
                                    // ds_read_b32 lanes land on distinct banks)
 constexpr int W2R = 802;           // LDS stride of W2 reordered as w2r[ci][tap*32 + o]
@@ -450,7 +450,7 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
                                               int P, int B, int G, CnnOff off, const float* __restrict__ pool1,
                                               const uint8_t* __restrict__ am1, const float* __restrict__ pool2,
                                               const uint8_t* __restrict__ am2, const float* __restrict__ dP2,
-                                              float* __restrict__ part) {
+                                              int bs, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* w2r = sm;                          // [16][802]: w2r[ci][tap*32 + o] = W2[o][ci][tap]
   float* dc2 = w2r + C1 * W2R;              // [32][338] padded dL/d conv2-output (post-unpool, ReLU-masked)
@@ -464,8 +464,8 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): per-wave branches are scalar
   const int k = blockIdx.x / G, g = blockIdx.x - k * G;
-  const int s0 = g * BS;
-  const int ns = min(BS, B - s0);
+  const int s0 = g * bs;
+  const int ns = min(bs, B - s0);
   const float* prow = params + (size_t)k * P;
   const int i = lane & 15, kq = lane >> 4;
 
@@ -605,9 +605,12 @@ __global__ void cnn_reduce(const float* __restrict__ part, int G, float* __restr
 
 // --------------------------------------------------------------------------------------------
 // fc head, one block per client: a = ReLU(h1) * dropout; logits = W a + b; weighted CE; backward:
-// dh1 = (W^T dlogits) * dropout * [h1 > 0]; fc2 grads (fixed-order sums over samples)
+// dh1 = (W^T dlogits) * dropout * [h1 > 0]; fc2 grads.  Samples go through LDS in chunks of HB; every
+// stage spreads (sample, class) or (sample, unit) pairs over the block, and all sums over samples run in
+// a fixed order (deterministic).
 // --------------------------------------------------------------------------------------------
-constexpr int HID = 64, CMAXC = 16;
+constexpr int HID = 64, CMAXC = 16, HB = 64;
+constexpr int HG = (CMAXC * HID + CMAXC + 255) / 256;   // fc2 gradient entries per thread
 
 __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, const float* __restrict__ mask,
                                                 const float* __restrict__ params, int P, int off_w, int off_b,
@@ -617,65 +620,85 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, co
                                                 float* __restrict__ correct, float* __restrict__ grad) {
   __shared__ float Ws[CMAXC * HID];
   __shared__ float bs[CMAXC];
-  __shared__ float red[2 * 256];
+  __shared__ float act[HB][HID + 1];       // ReLU(h1) * dropout of the chunk
+  __shared__ float dl[HB][CMAXC + 1];      // logits, then weighted dlogits
+  __shared__ float lsb[HB], csb[HB];       // per-sample weighted loss / correct flag
   const int k = blockIdx.x, tid = threadIdx.x;
   const float* prow = params + (size_t)k * P;
   for (int e = tid; e < C * HID; e += 256) Ws[e] = prow[off_w + e];
   if (tid < C) bs[tid] = prow[off_b + tid];
-  __syncthreads();
+  float gacc[HG];
+#pragma unroll
+  for (int m = 0; m < HG; ++m) gacc[m] = 0.f;
   float lsum = 0.f, csum = 0.f;
-  for (int b = tid; b < B; b += 256) {      // one thread per sample
-    const size_t s = (size_t)k * B + b;
-    float lg[CMAXC];
-    float m = -INFINITY;
-    for (int c = 0; c < C; ++c) {
+  for (int b0 = 0; b0 < B; b0 += HB) {
+    const int nb = min(HB, B - b0);
+    const size_t sb = (size_t)k * B + b0;
+    __syncthreads();   // previous chunk fully consumed (and Ws / bs staged)
+    for (int e = tid; e < nb * HID; e += 256) {
+      const int b = e / HID, j = e - b * HID;
+      act[b][j] = fmaxf(h1[sb * HID + e], 0.f) * mask[sb * HID + e];
+    }
+    __syncthreads();
+    for (int e = tid; e < nb * C; e += 256) {
+      const int b = e / C, c = e - b * C;
       float t = bs[c];
-      for (int j = 0; j < HID; ++j) t = fmaf(Ws[c * HID + j], fmaxf(h1[s * HID + j], 0.f) * mask[s * HID + j], t);
-      lg[c] = t;
-      m = fmaxf(m, t);
+#pragma unroll 16
+      for (int j = 0; j < HID; ++j) t = fmaf(Ws[c * HID + j], act[b][j], t);
+      dl[b][c] = t;
     }
-    float se = 0.f;
-    int am = 0;
-    for (int c = 0; c < C; ++c) {
-      se += expf(lg[c] - m);
-      if (lg[c] > lg[am]) am = c;
-    }
-    const float lse = m + logf(se);
-    const int yy = (int)y[s];
-    const float ws = wts[s];
-    lsum += ws * (lse - lg[yy]);
-    csum += (am == yy && ws > 0.f) ? 1.f : 0.f;
-    for (int c = 0; c < C; ++c) dlog[s * CMAXC + c] = (expf(lg[c] - lse) - (c == yy ? 1.f : 0.f)) * ws;
-    for (int j = 0; j < HID; ++j) {
-      float d = 0.f;
-      for (int c = 0; c < C; ++c) d = fmaf(Ws[c * HID + j], dlog[s * CMAXC + c], d);
-      dh1[s * HID + j] = h1[s * HID + j] > 0.f ? d * mask[s * HID + j] : 0.f;
-    }
-  }
-  red[tid] = lsum;
-  red[256 + tid] = csum;
-  __syncthreads();
-  if (tid == 0) {
-    float a = 0.f, c2 = 0.f;
-    for (int t = 0; t < 256; ++t) { a += red[t]; c2 += red[256 + t]; }
-    loss[k] = a;
-    correct[k] = c2;
-  }
-  // fc2 grads: dW[c][j] = sum_b dlog[b][c] * a[b][j], db[c] = sum_b dlog[b][c]   (sequential over b)
-  for (int e = tid; e < C * HID + C; e += 256) {
-    float sacc = 0.f;
-    if (e < C * HID) {
-      const int c = e / HID, j = e - c * HID;
-      for (int b = 0; b < B; ++b) {
-        const size_t s = (size_t)k * B + b;
-        sacc = fmaf(dlog[s * CMAXC + c], fmaxf(h1[s * HID + j], 0.f) * mask[s * HID + j], sacc);
+    __syncthreads();
+    if (tid < nb) {   // one thread per sample: log-softmax, CE, argmax, dlogits
+      const int b = tid;
+      float m = -INFINITY;
+      int am = 0;
+      for (int c = 0; c < C; ++c) {
+        m = fmaxf(m, dl[b][c]);
+        if (dl[b][c] > dl[b][am]) am = c;
       }
-      grad[(size_t)k * P + off_w + e] = sacc;
-    } else {
-      const int c = e - C * HID;
-      for (int b = 0; b < B; ++b) sacc += dlog[((size_t)k * B + b) * CMAXC + c];
-      grad[(size_t)k * P + off_b + c] = sacc;
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += expf(dl[b][c] - m);
+      const float lse = m + logf(se);
+      const int yy = (int)y[sb + b];
+      const float ws = wts[sb + b];
+      lsb[b] = ws * (lse - dl[b][yy]);
+      csb[b] = (am == yy && ws > 0.f) ? 1.f : 0.f;
+      for (int c = 0; c < C; ++c) {
+        const float d = (expf(dl[b][c] - lse) - (c == yy ? 1.f : 0.f)) * ws;
+        dl[b][c] = d;
+        dlog[(sb + b) * CMAXC + c] = d;
+      }
     }
+    __syncthreads();
+    for (int e = tid; e < nb * HID; e += 256) {   // dh1
+      const int b = e / HID, j = e - b * HID;
+      float d = 0.f;
+      for (int c = 0; c < C; ++c) d = fmaf(Ws[c * HID + j], dl[b][c], d);
+      dh1[sb * HID + e] = h1[sb * HID + e] > 0.f ? d * mask[sb * HID + e] : 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < HG; ++m) {   // fc2 grads: dW[c][j] += sum_b dl[b][c] a[b][j], db[c] += sum_b dl[b][c]
+      const int e = tid + m * 256;
+      if (e < C * HID) {
+        const int c = e / HID, j = e - c * HID;
+        for (int b = 0; b < nb; ++b) gacc[m] = fmaf(dl[b][c], act[b][j], gacc[m]);
+      } else if (e < C * HID + C) {
+        const int c = e - C * HID;
+        for (int b = 0; b < nb; ++b) gacc[m] += dl[b][c];
+      }
+    }
+    if (tid == 0)
+      for (int b = 0; b < nb; ++b) { lsum += lsb[b]; csum += csb[b]; }
+  }
+#pragma unroll
+  for (int m = 0; m < HG; ++m) {
+    const int e = tid + m * 256;
+    if (e < C * HID) grad[(size_t)k * P + off_w + e] = gacc[m];
+    else if (e < C * HID + C) grad[(size_t)k * P + off_b + (e - C * HID)] = gacc[m];
+  }
+  if (tid == 0) {
+    loss[k] = lsum;
+    correct[k] = csum;
   }
 }
 
@@ -709,10 +732,26 @@ extern "C" int qfx_cnn_forward(const float* X, const float* params, int P, int K
   return (int)hipGetLastError();
 }
 
+// Samples per backward workgroup: the most (up to BS_MAX, powers of two) that still give every CU a
+// workgroup.  One workgroup runs per CU (LDS), so fewer, longer workgroups amortise the per-workgroup W2
+// staging and shrink the gradient partials; small client batches fall back to fewer samples each.
+// (The partial grouping fixes the summation order: results are reproducible per device model.)
+static int bwd_bs(int K, int B) {
+  static int ncu = 0;
+  if (ncu <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  int bs = BS_MAX;
+  while (bs > 1 && (long long)K * ((B + bs - 1) / bs) < ncu) bs >>= 1;
+  return bs;
+}
+
 extern "C" int qfx_cnn_backward(const float* X, const float* params, int P, int K, int B, const int* off4,
                                 const float* pool1, const uint8_t* am1, const float* pool2, const uint8_t* am2,
                                 const float* dP2, float* part, float* grad, hipStream_t st) {
-  const int G = (B + BS - 1) / BS;
+  const int bs = bwd_bs(K, B), G = (B + bs - 1) / bs;
   const CnnOff off{off4[0], off4[1], off4[2], off4[3]};
   static bool attr = false;
   if (!attr) {
@@ -720,7 +759,7 @@ extern "C" int qfx_cnn_backward(const float* X, const float* params, int P, int 
     attr = true;
   }
   hipLaunchKernelGGL(cnn_bwd, dim3(K * G), dim3(NT), bwd_lds(), st, X, params, P, B, G, off, pool1, am1, pool2, am2,
-                     dP2, part);
+                     dP2, bs, part);
   hipLaunchKernelGGL(cnn_reduce, dim3((PART + 255) / 256, K), dim3(256), 0, st, part, G, grad, P, off);
   return (int)hipGetLastError();
 }
@@ -735,4 +774,7 @@ extern "C" int qfx_cnn_head(const float* h1, const float* mask, const float* par
 }
 
 extern "C" int qfx_cnn_partial_size() { return PART; }
-extern "C" int qfx_cnn_bwd_groups(int B) { return (B + BS - 1) / BS; }
+extern "C" int qfx_cnn_bwd_groups(int K, int B) {
+  const int bs = bwd_bs(K, B);
+  return (B + bs - 1) / bs;
+}

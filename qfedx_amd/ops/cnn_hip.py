@@ -76,7 +76,7 @@ class HipTinyCNN:
         Xf, pool1, am1, pool2, am2 = self.conv_forward(params, xb)
         h1, w1 = self._fc1(params, pool2, K, B)
         h1 = h1.contiguous()
-        grad = torch.zeros(K, self.P, dtype=torch.float32, device=self.device)
+        grad = torch.empty(K, self.P, dtype=torch.float32, device=self.device)   # every entry is written below
         dh1 = self._buf("dh1", (K, B, 64))
         dlog = self._buf("dlog", (S, 16))
         loss = torch.empty(K, dtype=torch.float32, device=self.device)
@@ -85,10 +85,10 @@ class HipTinyCNN:
         C.cnn_head(h1, m, params, self.fc2w, self.fc2b, self.C, K, B, yb.reshape(S).long().contiguous(),
                    wts.reshape(S).float().contiguous(), dh1, dlog, loss, correct, grad)
         p2 = pool2.view(K, B, 1568)
-        grad[:, self.fc1w: self.fc1b].view(K, 64, 1568).copy_(torch.bmm(dh1.transpose(1, 2), p2))
+        torch.bmm(dh1.transpose(1, 2), p2, out=grad[:, self.fc1w: self.fc1b].view(K, 64, 1568))   # strided C: no copy
         grad[:, self.fc1b: self.fc2w].copy_(dh1.sum(1))
         dP2 = torch.bmm(dh1, w1).reshape(S, 1568).contiguous()
-        G = C.cnn_bwd_groups(B)
+        G = C.cnn_bwd_groups(K, B)
         part = self._buf("part", (K * G, C.cnn_partial_size()))
         C.cnn_backward(Xf, params, K, B, self.off_conv, pool1, am1, pool2, am2, dP2, part, grad)
         return {"loss": loss, "grad": grad, "correct": correct}
