@@ -70,7 +70,7 @@ int qfx_fedavg_norm_scratch(int K, int P);
 int qfx_launch_adam(float* p, const float* g, float* m, float* v, const float* t_in, float* t_out,
                     const float* active, int K, int P, float lr, float b1, float b2, float eps, hipStream_t st);
 int qfx_launch_sgdm(float* p, const float* g, float* buf, const float* t_in, float* t_out, const float* active,
-                    int K, int P, float lr, float mu, hipStream_t st);
+                    int K, int P, float lr, float mu, int keep, hipStream_t st);
 int qfx_launch_round_init(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
                           hipStream_t st);
 int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx, int K,
@@ -263,11 +263,12 @@ void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, to
 }
 
 void sgdm(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor t_in, torch::Tensor t_out,
-          torch::Tensor active, double lr, double mu) {
+          torch::Tensor active, double lr, double mu, bool keep_state) {
   for (auto* x : {&p, &g, &buf}) need(*x, torch::kFloat32, "sgd tensor");
   check_counters(p, t_in, t_out, active);
   check(qfx_launch_sgdm(ptr<float>(p), ptr<float>(g), ptr<float>(buf), ptr<float>(t_in), ptr<float>(t_out),
-                        ptr<float>(active), (int)p.size(0), (int)p.size(1), (float)lr, (float)mu, cur_stream()),
+                        ptr<float>(active), (int)p.size(0), (int)p.size(1), (float)lr, (float)mu, keep_state ? 1 : 0,
+                        cur_stream()),
         "qfx_sgdm");
 }
 

@@ -270,18 +270,37 @@ __global__ void qfx_adam_kernel(float* __restrict__ p, const float* __restrict__
 }
 
 // torch.optim.SGD(momentum) semantics: buf = g on the first step, else mu*buf + g; p -= lr*buf
-__global__ void qfx_sgdm_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ buf,
-                                const float* __restrict__ t_in, float* __restrict__ t_out,
-                                const float* __restrict__ active, int K, int P, float lr, float mu) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)K * P) return;
-  const int k = (int)(i / P);
+// grid (chunks of SG_E parameters, clients): no per-element client division; SG_U elements per thread in flight
+constexpr int SG_U = 4, SG_E = 256 * SG_U;
+__global__ void __launch_bounds__(256) qfx_sgdm_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ buf, const float* __restrict__ t_in,
+                                                       float* __restrict__ t_out, const float* __restrict__ active,
+                                                       int K, int P, float lr, float mu, int keep) {
+  const int k = blockIdx.y;
   const float act = active[k];
-  if (i == (long)k * P) t_out[k] = t_in[k] + act;
+  if (blockIdx.x == 0 && threadIdx.x == 0) t_out[k] = t_in[k] + act;
   if (act == 0.f) return;
-  const float b = (t_in[k] == 0.f) ? g[i] : fmaf(mu, buf[i], g[i]);
-  buf[i] = b;
-  p[i] -= lr * b;
+  const bool first = t_in[k] == 0.f;   // torch SGD: the buffer is the gradient on the first step (never read)
+  const size_t row = (size_t)k * P;
+  const int e0 = blockIdx.x * SG_E + threadIdx.x;
+  float gv[SG_U], bv[SG_U];
+#pragma unroll
+  for (int u = 0; u < SG_U; ++u) {
+    const int e = e0 + u * 256;
+    if (e < P) {
+      gv[u] = g[row + e];
+      bv[u] = first ? 0.f : buf[row + e];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < SG_U; ++u) {
+    const int e = e0 + u * 256;
+    if (e < P) {
+      const float b = first ? gv[u] : fmaf(mu, bv[u], gv[u]);
+      if (keep) buf[row + e] = b;
+      p[row + e] -= lr * b;
+    }
+  }
 }
 
 __device__ __forceinline__ double wrap_pi(double d) {
@@ -324,14 +343,34 @@ __global__ void qfx_delta_norm_final_kernel(const double* __restrict__ partial, 
 // out[e] = sum_k round(2^32 * w_k * priv(wrap(theta_k[e] - theta_g[e]))), out[P] = sum_k round(2^32 w_k)
 // Each client's term is rounded to fixed point BEFORE the sum: integer addition is associative, so the
 // aggregate is bitwise identical for any sharding of clients over GPUs (and equal to the CPU path).
-constexpr int FA_E = 32, FA_G = 8;   // fedavg reduce: parameters per block x client groups per block
+constexpr int FA_E = 64, FA_G = 4;   // fedavg reduce: parameters per block (one wave row) x client groups per block
+constexpr int FA_U = 4;              // client rows in flight per thread
+
+// one client's fixed-point FedAvg term of parameter e
+__device__ __forceinline__ long long fedavg_term(float x, double tg, bool wr, int k, long e, const double* weights,
+                                                 const double* norms, const uint32_t* keys, int dp, float clip,
+                                                 float sigma) {
+  const double SC = 4294967296.0;
+  double d = (double)x - tg;
+  if (wr) d = wrap_pi(d);
+  if (dp) {
+    const double n = norms[k];
+    const double sc = fmin(1.0, (double)clip / fmax(n, 1e-12));
+    d = d * sc;
+    if (sigma > 0.f)
+      d += (double)sigma * (double)clip * (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
+  }
+  return llrint(weights[k] * d * SC);
+}
+
 __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
     const float* __restrict__ theta_k, const float* __restrict__ theta_g,
     const unsigned char* __restrict__ angle_mask, const double* __restrict__ weights,
     const double* __restrict__ norms, const uint32_t* __restrict__ keys, int K, int P, int wrap,
     int dp, float clip, float sigma, long long* __restrict__ out) {
-  // thread (group g, lane el): parameter e = block * FA_E + el, clients k = g, g + FA_G, ...; the FA_G integer
-  // partials are combined in LDS (exact, so the split changes no bit of the result)
+  // thread (group g, lane el): parameter e = block * FA_E + el (a wave reads 256 contiguous bytes of a client
+  // row), clients k = g, g + FA_G, ... with FA_U rows loaded before their terms are formed; the FA_G integer
+  // partials are combined in LDS (exact, so neither split changes a bit of the result)
   __shared__ long long part[FA_G][FA_E];
   const double SC = 4294967296.0;
   const int el = threadIdx.x % FA_E, grp = threadIdx.x / FA_E;
@@ -345,18 +384,15 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
   if (e < P) {
     const double tg = (double)theta_g[e];
     const bool wr = wrap && angle_mask[e];
-    for (int k = grp; k < K; k += FA_G) {
-      double d = (double)theta_k[(size_t)k * P + e] - tg;
-      if (wr) d = wrap_pi(d);
-      if (dp) {
-        const double n = norms[k];
-        const double sc = fmin(1.0, (double)clip / fmax(n, 1e-12));
-        d = d * sc;
-        if (sigma > 0.f)
-          d += (double)sigma * (double)clip * (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
-      }
-      acc += llrint(weights[k] * d * SC);
+    int k = grp;
+    for (; k + (FA_U - 1) * FA_G < K; k += FA_U * FA_G) {
+      float x[FA_U];
+#pragma unroll
+      for (int u = 0; u < FA_U; ++u) x[u] = theta_k[(size_t)(k + u * FA_G) * P + e];
+#pragma unroll
+      for (int u = 0; u < FA_U; ++u) acc += fedavg_term(x[u], tg, wr, k + u * FA_G, e, weights, norms, keys, dp, clip, sigma);
     }
+    for (; k < K; k += FA_G) acc += fedavg_term(theta_k[(size_t)k * P + e], tg, wr, k, e, weights, norms, keys, dp, clip, sigma);
   }
   part[grp][el] = acc;
   __syncthreads();
@@ -501,31 +537,40 @@ extern "C" int qfx_launch_adam(float* p, const float* g, float* m, float* v, con
 }
 
 extern "C" int qfx_launch_sgdm(float* p, const float* g, float* buf, const float* t_in, float* t_out,
-                               const float* active, int K, int P, float lr, float mu, hipStream_t st) {
-  const long tot = (long)K * P;
-  hipLaunchKernelGGL(qfx_sgdm_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, p, g, buf, t_in,
-                     t_out, active, K, P, lr, mu);
+                               const float* active, int K, int P, float lr, float mu, int keep, hipStream_t st) {
+  if (K <= 0 || P <= 0) return 0;
+  hipLaunchKernelGGL(qfx_sgdm_kernel, dim3((unsigned)((P + SG_E - 1) / SG_E), (unsigned)K), dim3(256), 0, st, p, g, buf, t_in,
+                     t_out, active, K, P, lr, mu, keep);
   return (int)hipGetLastError();
 }
 
 // ----------------------------------------------------------------------------------- round prologue
 // local round start: every client row starts from the global params; optimizer moments / counters zeroed
-__global__ void qfx_round_init_kernel(const float* __restrict__ theta, int K, int P, float* __restrict__ params,
-                                      float* __restrict__ m, float* __restrict__ v, float* __restrict__ t, int nt) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < (long)K * P) {
-    params[i] = theta[i % P];
-    if (m) m[i] = 0.f;
-    if (v) v[i] = 0.f;
+// grid (chunks of SG_E parameters, clients): no per-element client modulo
+__global__ void __launch_bounds__(256) qfx_round_init_kernel(const float* __restrict__ theta, int K, int P,
+                                                             float* __restrict__ params, float* __restrict__ m,
+                                                             float* __restrict__ v, float* __restrict__ t, int nt) {
+  const int k = blockIdx.y;
+  const size_t row = (size_t)k * P;
+  const int e0 = blockIdx.x * SG_E + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < SG_U; ++u) {
+    const int e = e0 + u * 256;
+    if (e < P) {
+      params[row + e] = theta[e];
+      if (m) m[row + e] = 0.f;
+      if (v) v[row + e] = 0.f;
+    }
   }
-  if (t && i < nt) t[i] = 0.f;
+  if (t && blockIdx.x == 0 && k == 0)
+    for (int i = threadIdx.x; i < nt; i += 256) t[i] = 0.f;
 }
 
 extern "C" int qfx_launch_round_init(const float* theta, int K, int P, float* params, float* m, float* v, float* t,
                                      int nt, hipStream_t st) {
-  const long tot = (long)K * P > nt ? (long)K * P : nt;
-  hipLaunchKernelGGL(qfx_round_init_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, theta, K, P,
-                     params, m, v, t, nt);
+  if (K <= 0 || P <= 0) return 0;
+  hipLaunchKernelGGL(qfx_round_init_kernel, dim3((unsigned)((P + SG_E - 1) / SG_E), (unsigned)K),
+                     dim3(256), 0, st, theta, K, P, params, m, v, t, nt);
   return (int)hipGetLastError();
 }
 

@@ -92,7 +92,7 @@ class CNNClientTrainer:
                 yb = store.y[rows, dv["idx"][s]]
             mask = tc.dropout_masks(cids, cfg.batch_size, cfg.seed, round_num, s, self.device)
             res = self.loss_and_grads(params, xb, yb, dv["wts"][s], mask)
-            opt.step(params, res["grad"], dv["act"][s])
+            opt.step(params, res["grad"], dv["act"][s], last=s == S - 1)
             loss_all[s].copy_(res["loss"])
             correct_all[s].copy_(res["correct"])
         if epilogue is not None:

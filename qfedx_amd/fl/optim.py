@@ -49,7 +49,9 @@ class BatchedOptimizer:
         """params[k] = theta for every client row and the optimizer state reset (HIP: one kernel)."""
         if self.backend == "hip":
             from ..ops._ext import ext
-            ext().round_init(theta.float().contiguous(), params, self.m, self.v, self._t)
+            # SGD-momentum never reads its buffer on a client's first active step: only Adam's moments are zeroed
+            m = self.m if self.kind == "adam" else None
+            ext().round_init(theta.float().contiguous(), params, m, self.v, self._t)
             self._phase = 0
             self._fresh = True
             return
@@ -57,7 +59,10 @@ class BatchedOptimizer:
         self.reset()
 
     @torch.no_grad()
-    def step(self, params: torch.Tensor, grads: torch.Tensor, active: Optional[torch.Tensor] = None) -> None:
+    def step(self, params: torch.Tensor, grads: torch.Tensor, active: Optional[torch.Tensor] = None,
+             last: bool = False) -> None:
+        """One update of every active client row.  ``last``: no later step of this round reads the optimizer
+        state (it is reset by the next ``init_round``), so the HIP SGD-momentum path skips storing its buffer."""
         if active is None:
             active = torch.ones(params.shape[0], device=params.device)
         active = active.to(params.dtype)
@@ -70,7 +75,8 @@ class BatchedOptimizer:
                 fedavg_hip.adam_step(params, grads, self.m, self.v, t_in, t_out, active, self.lr, self.b1,
                                      self.b2, self.eps)
             else:
-                fedavg_hip.sgdm_step(params, grads, self.m, t_in, t_out, active, self.lr, self.momentum)
+                fedavg_hip.sgdm_step(params, grads, self.m, t_in, t_out, active, self.lr, self.momentum,
+                                     keep_state=not last)
             self._phase ^= 1
             return
         a = active[:, None]

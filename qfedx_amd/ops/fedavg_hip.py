@@ -13,8 +13,9 @@ def adam_step(params, grads, m, v, t_in, t_out, active, lr, b1, b2, eps) -> None
     ext().adam(params, grads.float().contiguous(), m, v, t_in, t_out, active.float().contiguous(), lr, b1, b2, eps)
 
 
-def sgdm_step(params, grads, buf, t_in, t_out, active, lr, mu) -> None:
-    ext().sgdm(params, grads.float().contiguous(), buf, t_in, t_out, active.float().contiguous(), lr, mu)
+def sgdm_step(params, grads, buf, t_in, t_out, active, lr, mu, keep_state: bool = True) -> None:
+    """Fused client-batched SGD-momentum; ``keep_state=False`` (a round's last local step) skips the buffer store."""
+    ext().sgdm(params, grads.float().contiguous(), buf, t_in, t_out, active.float().contiguous(), lr, mu, keep_state)
 
 
 _NO_KEYS = {}
