@@ -71,6 +71,7 @@ int qfx_launch_adam(float* p, const float* g, float* m, float* v, const float* t
                     const float* active, int K, int P, float lr, float b1, float b2, float eps, hipStream_t st);
 int qfx_launch_sgdm(float* p, const float* g, float* buf, const float* t_in, float* t_out, const float* active,
                     int K, int P, float lr, float mu, int keep, hipStream_t st);
+int qfx_launch_host_upload(const void* host_src, void* dst, long nbytes, hipStream_t st);
 int qfx_launch_round_init(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
                           hipStream_t st);
 int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx, int K,
@@ -273,6 +274,18 @@ void sgdm(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor t_i
 }
 
 // params[k, :] = theta; optional m, v (same shape) and t (any length) zeroed
+// dst (device, uint8) <- src (pinned host, uint8) by a copy kernel that reads the host memory directly
+void host_upload(torch::Tensor src, torch::Tensor dst) {
+  if (src.device().is_cuda() || !src.is_pinned()) throw std::invalid_argument("host_upload: src must be pinned host memory");
+  if (!dst.device().is_cuda()) throw std::invalid_argument("host_upload: dst must be a device tensor");
+  if (src.scalar_type() != torch::kUInt8 || dst.scalar_type() != torch::kUInt8 || !src.is_contiguous() ||
+      !dst.is_contiguous())
+    throw std::invalid_argument("host_upload: contiguous uint8 tensors expected");
+  const int64_t n = src.numel();
+  if (dst.numel() < n || n % 16) throw std::invalid_argument("host_upload: size (16-byte multiple, dst >= src)");
+  check(qfx_launch_host_upload(src.data_ptr(), dst.data_ptr(), (long)n, cur_stream()), "qfx_host_upload");
+}
+
 void round_init(torch::Tensor theta, torch::Tensor params, c10::optional<torch::Tensor> m,
                 c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> t) {
   need(theta, torch::kFloat32, "theta");
@@ -387,6 +400,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("readout_sum", &readout_sum);
   m.def("amp_init", &amp_init);
   m.def("round_init", &round_init);
+  m.def("host_upload", &host_upload);
   m.def("batch_plan", &qfx_runtime::batch_plan);
   m.def("batch_gather", &batch_gather);
   m.def("amp_scratch", &amp_scratch);

@@ -574,6 +574,28 @@ extern "C" int qfx_launch_round_init(const float* theta, int K, int P, float* pa
   return (int)hipGetLastError();
 }
 
+// ----------------------------------------------------------------------------------- host upload
+// dst[0:n16) = src[0:n16) (16-byte words) where src is pinned host memory read by the kernel itself.  A kernel
+// launch never waits on the stream, unlike a small hipMemcpyAsync issued behind a graph launch, which was seen
+// to block the host until the queue drained (the GPU then idles while the host builds the next round).
+__global__ void __launch_bounds__(256) qfx_host_upload_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                              long n16) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) dst[i] = src[i];
+}
+
+extern "C" int qfx_launch_host_upload(const void* host_src, void* dst, long nbytes, hipStream_t st) {
+  if (nbytes <= 0) return 0;
+  if (nbytes % 16) return (int)hipErrorInvalidValue;
+  void* dsrc = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&dsrc, const_cast<void*>(host_src), 0);
+  if (e != hipSuccess) return (int)e;
+  const long n16 = nbytes / 16;
+  const long blocks = (n16 + 255) / 256;
+  hipLaunchKernelGGL(qfx_host_upload_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, st,
+                     (const uint4*)dsrc, (uint4*)dst, n16);
+  return (int)hipGetLastError();
+}
+
 // per-step minibatch gather + feature encoding, one block per sample s = k*B + b:
 //   x_out[s, 0:F] = enc(X[lid[k], idx[s], 0:F]),  y_out[s] = Y[lid[k], idx[s]]
 // enc: 0 = alpha * x (ROADMAP RY(alpha x)), 1 = per-sample min-max -> pi * x^ (qAngle.py:36-41; constant

@@ -34,17 +34,89 @@ def resolve_backend(spec: str, device: torch.device) -> str:
     return spec
 
 
-def h2d(t: torch.Tensor, device) -> torch.Tensor:
-    """Host -> device copy that never stalls the host on the GPU queue.
+class _PinnedRing:
+    """Reusable pinned staging slots for host -> device uploads.
 
-    A pageable-memory copy blocks until the stream reaches it (i.e. a hidden device sync).  Staging
-    through pinned memory makes it a true async DMA; torch's caching host allocator keeps the pinned
-    block alive until the copy has completed, so the staging buffer is never overwritten early.
+    Slot i is handed out again only after the event recorded behind its upload has completed, which
+    blocks the host only when the GPU is ``SLOTS`` uploads behind.  The upload itself is a copy KERNEL
+    that reads the pinned slot (``host_upload``): a small ``hipMemcpyAsync`` queued behind a hipGraph
+    launch was measured to block the host until the stream drained every few rounds, which left the GPU
+    idle while the host built the next round.
     """
+
+    SLOTS = 16
+
+    def __init__(self):
+        self.bufs = [None] * self.SLOTS
+        self.events = [None] * self.SLOTS
+        self.i = 0
+
+    def acquire(self, nbytes: int):
+        i = self.i
+        self.i = (i + 1) % self.SLOTS
+        if self.events[i] is not None:
+            self.events[i].synchronize()
+        buf = self.bufs[i]
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(4096, 1 << (nbytes - 1).bit_length()), dtype=torch.uint8, pin_memory=True)
+            self.bufs[i] = buf
+        return i, buf[:nbytes]
+
+    def release(self, i: int, device) -> None:
+        ev = self.events[i]
+        if ev is None:
+            ev = self.events[i] = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+
+
+_RING = None
+
+
+def _upload_ext():
+    try:
+        from ..ops._ext import ext
+        return ext()
+    except Exception:   # no extension (portable torch backend): plain pinned async copies
+        return None
+
+
+def _upload(fill, nbytes: int, device, dst: torch.Tensor | None = None) -> torch.Tensor:
+    """``fill(pinned_uint8_view)`` writes ``nbytes`` (a multiple of 16); returns the device uint8 buffer."""
+    global _RING
+    E = _upload_ext()
+    if E is None:
+        src = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        fill(src)
+        if dst is None:
+            return src.to(device, non_blocking=True)
+        return dst.copy_(src, non_blocking=True)
+    if _RING is None:
+        _RING = _PinnedRing()
+    i, src = _RING.acquire(nbytes)
+    fill(src)
+    if dst is None:
+        dst = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    E.host_upload(src, dst[:nbytes])
+    _RING.release(i, device)
+    return dst
+
+
+def h2d(t: torch.Tensor, device) -> torch.Tensor:
+    """Host -> device copy that never stalls the host on the GPU queue (see ``_PinnedRing``)."""
     device = torch.device(device)
     if device.type != "cuda" or t.device.type == "cuda":
         return t.to(device)
-    return t.pin_memory().to(device, non_blocking=True)
+    t = t.contiguous()
+    nb = t.numel() * t.element_size()
+    if nb == 0:
+        return torch.empty(t.shape, dtype=t.dtype, device=device)
+    padded = (nb + 15) // 16 * 16
+
+    def fill(buf):
+        buf[:nb].copy_(t.reshape(-1).view(torch.uint8))
+
+    out = _upload(fill, padded, device)
+    return out[:nb].view(t.dtype).view(t.shape)
 
 
 class PackedUpload:
@@ -68,8 +140,7 @@ class PackedUpload:
             off += (nbytes + self.ALIGN - 1) // self.ALIGN * self.ALIGN
         self.nbytes = max(off, self.ALIGN)
 
-    def _staging(self, pin: bool) -> torch.Tensor:
-        buf = torch.empty(self.nbytes, dtype=torch.uint8, pin_memory=pin)
+    def _fill(self, buf: torch.Tensor) -> torch.Tensor:
         for _, off, nb, _, _, t in self.layout:
             if nb:
                 buf[off: off + nb].copy_(t.reshape(-1).view(torch.uint8))
@@ -78,13 +149,10 @@ class PackedUpload:
     def to_device(self, device, dst: torch.Tensor | None = None) -> dict:
         device = torch.device(device)
         if device.type == "cuda":
-            src = self._staging(True)
-            if dst is None:
-                dst = src.to(device, non_blocking=True)
-            else:
-                dst.copy_(src, non_blocking=True)
+            dst = _upload(self._fill, self.nbytes, device, dst)
         else:
-            dst = self._staging(False) if dst is None else dst.copy_(self._staging(False))
+            staged = self._fill(torch.empty(self.nbytes, dtype=torch.uint8))
+            dst = staged if dst is None else dst.copy_(staged)
         return self.views(dst)
 
     def views(self, buf: torch.Tensor) -> dict:

@@ -1,7 +1,10 @@
-"""Host-side cost of enqueueing one federated round (no device sync) vs the device time per round: tells
-whether small per-rank shares are host-bound.  python scripts/host_round_time.py [--clients 8]"""
+"""Host-side cost of the headline round: per-call time of ``run_round(sync=False)`` (the host's own work,
+the GPU runs behind it) vs the wall period of the same rounds.  If the host cost approaches the period,
+the GPU idles between rounds waiting for launches.
+
+    python scripts/host_round_time.py [--rounds 30] [--profile]   (--profile: cProfile top functions)
+"""
 import argparse
-import json
 import os
 import sys
 import time
@@ -11,37 +14,51 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--clients", type=int, default=8)
-    ap.add_argument("--rounds", type=int, default=40)
-    args = ap.parse_args()
+    ap.add_argument("--rounds", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--profile", action="store_true")
+    a = ap.parse_args()
     import torch
     import bench
     from qfedx_amd.api import setup
-    from qfedx_amd.parallel.dist import World
-    ns = argparse.Namespace(gpus=1, steps=args.rounds, warmup=3, qubits=16, layers=3, clients=args.clients, batch=32,
-                            local_steps=1, classes=3, dp=False, backend="auto", device="auto", engine="mfma")
-    cfg = bench.make_config(ns)
-    device, backend, world = setup(cfg)
     from qfedx_amd.data.datasets import build_federated_data
     from qfedx_amd.fl.adapters import make_adapter
     from qfedx_amd.fl.server import FederatedRunner
-    data = build_federated_data(cfg)
+    from qfedx_amd.parallel.dist import shard_clients
+
+    args = bench.argparse.Namespace(gpus=1, clients=64, batch=32, qubits=16, layers=3, classes=3, local_steps=1,
+                                    dp=False, backend="auto", device="auto", dist_backend="auto", engine="mfma")
+    cfg = bench.make_config(args)
+    device, backend, world = setup(cfg)
+    data = build_federated_data(cfg, clients=shard_clients(cfg.data.num_clients, 1, 0))
     runner = FederatedRunner(cfg, make_adapter(cfg, device, backend), data, world, device, backend)
-    for r in range(5):
+    for r in range(a.warmup):
         runner.run_round(r, sync=False)
     torch.cuda.synchronize()
     host = []
+    prof = None
+    if a.profile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
-    for r in range(5, 5 + args.rounds):
+    for r in range(a.warmup, a.warmup + a.rounds):
         h0 = time.perf_counter()
         runner.run_round(r, sync=False)
         host.append(time.perf_counter() - h0)
+    t_host = time.perf_counter() - t0
     torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / args.rounds
+    wall = time.perf_counter() - t0
+    if prof is not None:
+        prof.disable()
     host.sort()
-    print(json.dumps({"clients": args.clients, "wall_ms_per_round": round(wall * 1e3, 3),
-                      "host_ms_median": round(host[len(host) // 2] * 1e3, 3),
-                      "host_ms_p90": round(host[int(0.9 * len(host))] * 1e3, 3)}), flush=True)
+    print(f"rounds {a.rounds}: wall {1e3 * wall / a.rounds:.3f} ms/round, host loop {1e3 * t_host / a.rounds:.3f} "
+          f"ms/round, run_round host p50 {1e3 * host[len(host) // 2]:.3f} ms, p90 {1e3 * host[int(0.9 * len(host))]:.3f} ms")
+    if prof is not None:
+        import pstats
+        st = pstats.Stats(prof)
+        st.sort_stats("cumulative").print_stats(25)
+        st.print_callers("copy_")
 
 
 if __name__ == "__main__":

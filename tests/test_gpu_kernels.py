@@ -208,3 +208,23 @@ def test_round_init_and_counter_pingpong(cuda):
         outs.append((p.cpu(), opt.t.cpu()))
     assert torch.allclose(outs[0][0], outs[1][0], atol=1e-6)
     assert torch.equal(outs[0][1], outs[1][1]) and outs[1][1].tolist() == [3, 1, 0, 2, 3]
+
+
+def test_host_upload_ring_roundtrip(cuda):
+    """h2d / PackedUpload go through the pinned ring + copy kernel: exact bytes, also across slot reuse while
+    earlier uploads may still be queued behind device work."""
+    from qfedx_amd.utils.device import PackedUpload, h2d
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(512, 512, device=cuda)
+    outs = []
+    for it in range(40):                       # > ring slots: every slot is reused at least twice
+        a = a @ a * 1e-3                       # keep the stream busy so uploads queue behind work
+        t = torch.randint(-2 ** 40, 2 ** 40, (it + 3,), generator=g)
+        w = torch.rand(it % 5 + 1, 3, generator=g)
+        up = PackedUpload({"t": t, "w": w, "b": torch.tensor([it], dtype=torch.int32)})
+        dv = up.to_device(cuda)
+        outs.append((t, w, it, h2d(w * 2, cuda), dv))
+    torch.cuda.synchronize()
+    for t, w, it, w2, dv in outs:
+        assert torch.equal(dv["t"].cpu(), t) and torch.equal(dv["w"].cpu(), w) and int(dv["b"].item()) == it
+        assert torch.equal(w2.cpu(), w * 2)
