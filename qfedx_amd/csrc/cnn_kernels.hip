@@ -604,15 +604,101 @@ __global__ void cnn_reduce(const float* __restrict__ part, int G, float* __restr
 }
 
 // --------------------------------------------------------------------------------------------
+// fc1 forward, split over the 1568-long reduction: h1p[ks][s][j] = sum_{c in chunk ks} pool2[s][c] W1[j][c]
+//   grid (client x 32-sample tile, F1KS chunks): 1024 workgroups at 128 clients x 32 samples instead of a
+//   128-tile batched GEMM; the chunk sums (+ bias) are added in fixed order by cnn_head, which reads h1 anyway.
+// --------------------------------------------------------------------------------------------
+constexpr int HID = 64;
+constexpr int F1IN = C2 * Q2 * Q2;             // 1568
+constexpr int F1KS = 8, F1KC = F1IN / F1KS;    // 8 chunks of 196
+constexpr int F1S = 198;                       // LDS row stride (== 6 mod 32: row-strided lanes on distinct banks)
+static_assert(F1KC % 4 == 0, "chunks are whole float4 runs and whole MFMA k-steps");
+
+struct Fc1Set {
+  float a, b[2];
+};
+
+__global__ void __launch_bounds__(256) cnn_fc1(const float* __restrict__ pool2, const float* __restrict__ params,
+                                               int P, int off_w1, int B, int MT, long S, float* __restrict__ h1p) {
+  __shared__ float As[32 * F1S];
+  __shared__ float Bs[HID * F1S];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k = blockIdx.x / MT, mt = blockIdx.x - k * MT, ks = blockIdx.y;
+  const int s0 = mt * 32, ns = min(32, B - s0);
+  const int c0 = ks * F1KC;
+  const float4* A = reinterpret_cast<const float4*>(pool2 + ((size_t)k * B + s0) * F1IN + c0);
+  // parameter rows are only 8-byte aligned (P is even, not a multiple of 4): W goes as float2
+  const float2* W = reinterpret_cast<const float2*>(params + (size_t)k * P + off_w1 + c0);
+  constexpr int Q4 = F1KC / 4, Q2W = F1KC / 2;   // float4 / float2 per row chunk
+  constexpr int NA = (32 * Q4 + 255) / 256, NB = (HID * Q2W + 255) / 256;
+  float4 va[NA];
+  float2 vb[NB];
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int e = tid + u * 256, r = e / Q4, c = e - r * Q4;
+    va[u] = (e < 32 * Q4 && r < ns) ? A[(size_t)r * (F1IN / 4) + c] : float4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int e = tid + u * 256, r = e / Q2W, c = e - r * Q2W;
+    if (e < HID * Q2W) vb[u] = W[(size_t)r * (F1IN / 2) + c];
+  }
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int e = tid + u * 256, r = e / Q4, c = e - r * Q4;
+    if (e < 32 * Q4) {
+      float* d = As + r * F1S + 4 * c;
+      d[0] = va[u].x; d[1] = va[u].y; d[2] = va[u].z; d[3] = va[u].w;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NB; ++u) {
+    const int e = tid + u * 256, r = e / Q2W, c = e - r * Q2W;
+    if (e < HID * Q2W) {
+      float* d = Bs + r * F1S + 2 * c;
+      d[0] = vb[u].x;
+      d[1] = vb[u].y;
+    }
+  }
+  __syncthreads();
+  // wave w: m-tile (w & 1) x n-tiles 2(w >> 1), 2(w >> 1) + 1
+  const int i = lane & 15, kq = lane >> 4;
+  const int mtl = wave & 1, nt0 = (wave >> 1) * 2;
+  const float* ap = As + (mtl * 16 + i) * F1S + kq;
+  const float* bp = Bs + (nt0 * 16 + i) * F1S + kq;
+  f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  pipelined<Fc1Set>(
+      0, F1KC / 4,
+      [&](int st, Fc1Set& o) {
+        o.a = ap[4 * st];
+        o.b[0] = bp[4 * st];
+        o.b[1] = bp[16 * F1S + 4 * st];
+      },
+      [&](const Fc1Set& o) {
+        acc[0] = mfma(o.a, o.b[0], acc[0]);
+        acc[1] = mfma(o.a, o.b[1], acc[1]);
+      });
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sr = mtl * 16 + 4 * kq + r;
+      if (sr < ns) h1p[((size_t)ks * S + (size_t)k * B + s0 + sr) * HID + (nt0 + h) * 16 + i] = acc[h][r];
+    }
+}
+
+// --------------------------------------------------------------------------------------------
 // fc head, one block per client: a = ReLU(h1) * dropout; logits = W a + b; weighted CE; backward:
 // dh1 = (W^T dlogits) * dropout * [h1 > 0]; fc2 grads.  Samples go through LDS in chunks of HB; every
 // stage spreads (sample, class) or (sample, unit) pairs over the block, and all sums over samples run in
 // a fixed order (deterministic).
 // --------------------------------------------------------------------------------------------
-constexpr int HID = 64, CMAXC = 16, HB = 64;
+constexpr int CMAXC = 16, HB = 64;
 constexpr int HG = (CMAXC * HID + CMAXC + 255) / 256;   // fc2 gradient entries per thread
 
-__global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, const float* __restrict__ mask,
+__global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1p, int nsplit, long S, int off_b1,
+                                                const float* __restrict__ mask,
                                                 const float* __restrict__ params, int P, int off_w, int off_b,
                                                 int C, int B, const long long* __restrict__ y,
                                                 const float* __restrict__ wts, float* __restrict__ dh1,
@@ -620,6 +706,7 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, co
                                                 float* __restrict__ correct, float* __restrict__ grad) {
   __shared__ float Ws[CMAXC * HID];
   __shared__ float bs[CMAXC];
+  __shared__ float hv[HB][HID + 1];        // h1 = b1 + fc1 chunk sums (fixed order)
   __shared__ float act[HB][HID + 1];       // ReLU(h1) * dropout of the chunk
   __shared__ float dl[HB][CMAXC + 1];      // logits, then weighted dlogits
   __shared__ float lsb[HB], csb[HB];       // per-sample weighted loss / correct flag
@@ -630,14 +717,17 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, co
   float gacc[HG];
 #pragma unroll
   for (int m = 0; m < HG; ++m) gacc[m] = 0.f;
-  float lsum = 0.f, csum = 0.f;
+  float lsum = 0.f, csum = 0.f, db1 = 0.f;
   for (int b0 = 0; b0 < B; b0 += HB) {
     const int nb = min(HB, B - b0);
     const size_t sb = (size_t)k * B + b0;
     __syncthreads();   // previous chunk fully consumed (and Ws / bs staged)
     for (int e = tid; e < nb * HID; e += 256) {
       const int b = e / HID, j = e - b * HID;
-      act[b][j] = fmaxf(h1[sb * HID + e], 0.f) * mask[sb * HID + e];
+      float h = prow[off_b1 + j];
+      for (int q = 0; q < nsplit; ++q) h += h1p[((size_t)q * S + sb) * HID + e];
+      hv[b][j] = h;
+      act[b][j] = fmaxf(h, 0.f) * mask[sb * HID + e];
     }
     __syncthreads();
     for (int e = tid; e < nb * C; e += 256) {
@@ -670,11 +760,13 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, co
       }
     }
     __syncthreads();
-    for (int e = tid; e < nb * HID; e += 256) {   // dh1
+    for (int e = tid; e < nb * HID; e += 256) {   // dh1 (kept in hv for the fc1 bias gradient)
       const int b = e / HID, j = e - b * HID;
       float d = 0.f;
       for (int c = 0; c < C; ++c) d = fmaf(Ws[c * HID + j], dl[b][c], d);
-      dh1[sb * HID + e] = h1[sb * HID + e] > 0.f ? d * mask[sb * HID + e] : 0.f;
+      d = hv[b][j] > 0.f ? d * mask[sb * HID + e] : 0.f;
+      dh1[sb * HID + e] = d;
+      hv[b][j] = d;
     }
 #pragma unroll
     for (int m = 0; m < HG; ++m) {   // fc2 grads: dW[c][j] += sum_b dl[b][c] a[b][j], db[c] += sum_b dl[b][c]
@@ -689,7 +781,11 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, co
     }
     if (tid == 0)
       for (int b = 0; b < nb; ++b) { lsum += lsb[b]; csum += csb[b]; }
+    __syncthreads();
+    if (tid < HID)   // fc1 bias gradient: sum over samples of dh1 (fixed order)
+      for (int b = 0; b < nb; ++b) db1 += hv[b][tid];
   }
+  if (tid < HID) grad[(size_t)k * P + off_b1 + tid] = db1;
 #pragma unroll
   for (int m = 0; m < HG; ++m) {
     const int e = tid + m * 256;
@@ -764,14 +860,24 @@ extern "C" int qfx_cnn_backward(const float* X, const float* params, int P, int 
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_cnn_head(const float* h1, const float* mask, const float* params, int P, int off_w, int off_b,
-                            int C, int K, int B, const long long* y, const float* wts, float* dh1, float* dlog,
-                            float* loss, float* correct, float* grad, hipStream_t st) {
-  if (C > CMAXC) return -2;
-  hipLaunchKernelGGL(cnn_head, dim3(K), dim3(256), 0, st, h1, mask, params, P, off_w, off_b, C, B, y, wts, dh1, dlog,
-                     loss, correct, grad);
+extern "C" int qfx_cnn_fc1(const float* pool2, const float* params, int P, int off_w1, int K, int B, float* h1p,
+                           hipStream_t st) {
+  const int MT = (B + 31) / 32;
+  if (K <= 0 || B <= 0) return 0;
+  hipLaunchKernelGGL(cnn_fc1, dim3(K * MT, F1KS), dim3(256), 0, st, pool2, params, P, off_w1, B, MT, (long)K * B, h1p);
   return (int)hipGetLastError();
 }
+
+extern "C" int qfx_cnn_head(const float* h1p, int off_b1, const float* mask, const float* params, int P, int off_w,
+                            int off_b, int C, int K, int B, const long long* y, const float* wts, float* dh1,
+                            float* dlog, float* loss, float* correct, float* grad, hipStream_t st) {
+  if (C > CMAXC) return -2;
+  hipLaunchKernelGGL(cnn_head, dim3(K), dim3(256), 0, st, h1p, F1KS, (long)K * B, off_b1, mask, params, P, off_w,
+                     off_b, C, B, y, wts, dh1, dlog, loss, correct, grad);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_cnn_fc1_splits() { return F1KS; }
 
 extern "C" int qfx_cnn_partial_size() { return PART; }
 extern "C" int qfx_cnn_bwd_groups(int K, int B) {
