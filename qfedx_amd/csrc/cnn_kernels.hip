@@ -119,6 +119,26 @@ __device__ __forceinline__ int fwd_q2(int row) {
   return (2 * (w / Q2) + (pos >> 1)) * P1P + 2 * (w % Q2) + (pos & 1);
 }
 
+// W2 [o][ci][tap] of one client row -> LDS at dst[o*so + ci*sc + tap*st]: all 25 loads of a thread are issued
+// before any store (a plain strided loop waits on each load in turn: one workgroup per CU hides nothing)
+__device__ __forceinline__ void stage_w2(const float* __restrict__ w2g, float* dst, int so, int sc, int st, int tid) {
+  constexpr int NU = (C2 * K2 + NT - 1) / NT;
+  float v[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int e = tid + u * NT;
+    if (e < C2 * K2) v[u] = w2g[e];
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int e = tid + u * NT;
+    if (e < C2 * K2) {
+      const int o = e / K2, rem = e - o * K2, ci = rem / 25, r = rem - ci * 25;
+      dst[o * so + ci * sc + r * st] = v[u];
+    }
+  }
+}
+
 template <int NM>
 struct Fwd2Set {
   float a[NM][4], b[2][4];
@@ -175,19 +195,25 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
   const float* prow = params + (size_t)k * P;
   const int i = lane & 15, kq = lane >> 4;
 
-  for (int e = tid; e < C2 * K2; e += NT) {   // W2 [o][ci][tap] -> w2f[o][tap*16 + ci]
-    const int o = e / K2, rem = e - o * K2, ci = rem / 25, r = rem - ci * 25;
-    w2f[o * W2F + r * 16 + ci] = prow[off.w2 + e];
-  }
+  stage_w2(prow + off.w2, w2f, W2F, 1, 16, tid);   // w2f[o][tap*16 + ci]
   for (int e = tid; e < C1 * K1P; e += NT) {
     const int o = e / K1P, kk = e - o * K1P;
     w1s[e] = kk < K1 ? prow[off.w1 + o * K1 + kk] : 0.f;
   }
   if (tid < C1) b1s[tid] = prow[off.b1 + tid];
   if (tid < C2) b2s[tid] = prow[off.b2 + tid];
-  for (int e = tid; e < FSG * IMGP * IMGP; e += NT) {
-    const int s = e / (IMGP * IMGP), r = e - s * IMGP * IMGP, y = r / IMGP - 2, x = r % IMGP - 2;
-    img[e] = (s < ns && y >= 0 && y < IMG && x >= 0 && x < IMG) ? X[((size_t)k * B + s0 + s) * IMG * IMG + y * IMG + x] : 0.f;
+  {
+    constexpr int NU = FSG * IMGP * IMGP / NT;
+    static_assert(NU * NT == FSG * IMGP * IMGP, "whole image rows per thread");
+    float v[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int e = tid + u * NT;
+      const int s = e / (IMGP * IMGP), r = e - s * IMGP * IMGP, y = r / IMGP - 2, x = r % IMGP - 2;
+      v[u] = (s < ns && y >= 0 && y < IMG && x >= 0 && x < IMG) ? X[((size_t)k * B + s0 + s) * IMG * IMG + y * IMG + x] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) img[tid + u * NT] = v[u];
   }
   for (int e = tid; e < FSG * C1 * CSF; e += NT) p1s[e] = 0.f;
   __syncthreads();
@@ -469,10 +495,7 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
   const float* prow = params + (size_t)k * P;
   const int i = lane & 15, kq = lane >> 4;
 
-  for (int e = tid; e < C2 * K2; e += NT) {   // W2 [o][ci][tap] -> w2r[ci][tap*32 + o]
-    const int o = e / K2, rem = e - o * K2, ci = rem / 25, r = rem - ci * 25;
-    w2r[ci * W2R + r * 32 + o] = prow[off.w2 + e];
-  }
+  stage_w2(prow + off.w2, w2r, 1, W2R, 32, tid);   // w2r[ci][tap*32 + o]
   for (int e = tid; e < (C2 + C1) * CS; e += NT) dc2[e] = 0.f;   // dc2 and p1s are contiguous
   for (int e = tid; e < IMGP * IMS; e += NT) img[e] = 0.f;
   if (tid < 256) ones[tid] = 1.f;

@@ -29,9 +29,9 @@ class CNNClientTrainer:
             from ..ops.cnn_hip import HipTinyCNN
             self._hip = HipTinyCNN(num_classes, self.device)
 
-    def loss_and_grads(self, params, xb, yb, wts, mask):
+    def loss_and_grads(self, params, xb, yb, wts, mask, loss_out=None, correct_out=None):
         if self._hip is not None:
-            return self._hip.loss_and_grads(params, xb, yb, wts, mask)
+            return self._hip.loss_and_grads(params, xb, yb, wts, mask, loss_out, correct_out)
         p = params.detach().requires_grad_(True)
         logits = tc.batched_forward(p, xb, self.C, mask)
         nll = F.cross_entropy(logits.reshape(-1, self.C), yb.reshape(-1), reduction="none").reshape(yb.shape)
@@ -91,10 +91,11 @@ class CNNClientTrainer:
                 xb = store.X[rows, dv["idx"][s]]
                 yb = store.y[rows, dv["idx"][s]]
             mask = tc.dropout_masks(cids, cfg.batch_size, cfg.seed, round_num, s, self.device)
-            res = self.loss_and_grads(params, xb, yb, dv["wts"][s], mask)
+            res = self.loss_and_grads(params, xb, yb, dv["wts"][s], mask, loss_all[s], correct_all[s])
             opt.step(params, res["grad"], dv["act"][s], last=s == S - 1)
-            loss_all[s].copy_(res["loss"])
-            correct_all[s].copy_(res["correct"])
+            if res["loss"].data_ptr() != loss_all[s].data_ptr():    # portable path: separate outputs
+                loss_all[s].copy_(res["loss"])
+                correct_all[s].copy_(res["correct"])
         if epilogue is not None:
             epilogue(params, dict(dv, loss=loss_all, correct=correct_all), theta_g.to(self.device).float())
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],

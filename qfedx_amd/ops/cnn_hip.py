@@ -68,7 +68,9 @@ class HipTinyCNN:
 
     @torch.no_grad()
     def loss_and_grads(self, params: torch.Tensor, xb: torch.Tensor, yb: torch.Tensor, wts: torch.Tensor,
-                       mask: torch.Tensor) -> dict:
+                       mask: torch.Tensor, loss_out: torch.Tensor | None = None,
+                       correct_out: torch.Tensor | None = None) -> dict:
+        """``loss_out`` / ``correct_out``: optional contiguous fp32 [K] rows the head writes into directly."""
         C = ext()
         params = params.float().contiguous()
         K, B = xb.shape[:2]
@@ -80,8 +82,8 @@ class HipTinyCNN:
         grad = torch.empty(K, self.P, dtype=torch.float32, device=self.device)   # every entry is written below
         dh1 = self._buf("dh1", (K, B, 64))
         dlog = self._buf("dlog", (S, 16))
-        loss = torch.empty(K, dtype=torch.float32, device=self.device)
-        correct = torch.empty(K, dtype=torch.float32, device=self.device)
+        loss = loss_out if loss_out is not None else torch.empty(K, dtype=torch.float32, device=self.device)
+        correct = correct_out if correct_out is not None else torch.empty(K, dtype=torch.float32, device=self.device)
         m = mask.float().contiguous() if mask is not None else torch.ones(K, B, 64, device=self.device)
         C.cnn_head(h1p, self.fc1b, m, params, self.fc2w, self.fc2b, self.C, K, B, yb.reshape(S).long().contiguous(),
                    wts.reshape(S).float().contiguous(), dh1, dlog, loss, correct, grad)
