@@ -14,12 +14,11 @@ int qfx_cnn_forward(const float* X, const float* params, int P, int K, int B, co
 int qfx_cnn_backward(const float* X, const float* params, int P, int K, int B, const int* off4, const float* pool1,
                      const uint8_t* am1, const float* pool2, const uint8_t* am2, const float* dP2, float* part,
                      float* grad, hipStream_t st);
-int qfx_cnn_fc1(const float* pool2, const float* params, int P, int off_w1, int K, int B, float* h1p, hipStream_t st);
-int qfx_cnn_fc1_splits();
-int qfx_cnn_head(const float* h1p, int off_b1, const float* mask, const float* params, int P, int off_w, int off_b,
+int qfx_cnn_head(const float* h1, int off_b1, const float* mask, const float* params, int P, int off_w, int off_b,
                  int C, int K, int B, const long long* y, const float* wts, float* dh1, float* dlog, float* loss,
                  float* correct, float* grad, hipStream_t st);
 int qfx_cnn_partial_size();
+int qfx_cnn_fc1_wgrad(const float* dh1, const float* pool2, int K, int B, float* grad, int P, int off_w1, hipStream_t st);
 int qfx_cnn_bwd_groups(int K, int B);
 }
 
@@ -76,23 +75,13 @@ void backward(torch::Tensor X, torch::Tensor params, int64_t K, int64_t B, std::
         "cnn_backward");
 }
 
-void fc1(torch::Tensor pool2, torch::Tensor params, int64_t off_w1, int64_t K, int64_t B, torch::Tensor h1p) {
-  const int64_t S = K * B;
-  const int P = (int)params.size(1);
-  if (params.size(0) < K || off_w1 < 0 || off_w1 + 64 * POOL2 > P) throw std::invalid_argument("cnn_fc1: params/offset");
-  check(qfx_cnn_fc1(dptr<float>(pool2, torch::kFloat32, "pool2", S * POOL2),
-                    dptr<float>(params, torch::kFloat32, "params", K * P), P, (int)off_w1, (int)K, (int)B,
-                    dptr<float>(h1p, torch::kFloat32, "h1p", qfx_cnn_fc1_splits() * S * 64), stream()),
-        "cnn_fc1");
-}
-
-// h1p: [fc1 splits, K*B, 64] partial sums from cnn_fc1; off_b1: fc1 bias offset in the parameter row
-void head(torch::Tensor h1p, int64_t off_b1, torch::Tensor mask, torch::Tensor params, int64_t off_w, int64_t off_b,
+// h1: fc1 pre-activations [K*B, 64]; off_b1: fc1 bias offset in the parameter row (its gradient is written here)
+void head(torch::Tensor h1, int64_t off_b1, torch::Tensor mask, torch::Tensor params, int64_t off_w, int64_t off_b,
           int64_t C, int64_t K, int64_t B, torch::Tensor y, torch::Tensor wts, torch::Tensor dh1, torch::Tensor dlog,
           torch::Tensor loss, torch::Tensor correct, torch::Tensor grad) {
   const int64_t S = K * B;
   const int P = (int)params.size(1);
-  check(qfx_cnn_head(dptr<float>(h1p, torch::kFloat32, "h1p", qfx_cnn_fc1_splits() * S * 64), (int)off_b1,
+  check(qfx_cnn_head(dptr<float>(h1, torch::kFloat32, "h1", S * 64), (int)off_b1,
                      dptr<float>(mask, torch::kFloat32, "mask", S * 64),
                      dptr<float>(params, torch::kFloat32, "params", K * P), P, (int)off_w, (int)off_b, (int)C, (int)K,
                      (int)B, dptr<long long>(y, torch::kInt64, "y", S), dptr<float>(wts, torch::kFloat32, "wts", S),
@@ -102,15 +91,23 @@ void head(torch::Tensor h1p, int64_t off_b1, torch::Tensor mask, torch::Tensor p
         "cnn_head");
 }
 
+void fc1_wgrad(torch::Tensor dh1, torch::Tensor pool2, int64_t K, int64_t B, torch::Tensor grad, int64_t off_w1) {
+  const int64_t S = K * B;
+  const int P = (int)grad.size(1);
+  if (grad.size(0) < K || off_w1 < 0 || off_w1 + 64 * POOL2 > P) throw std::invalid_argument("cnn_fc1_wgrad: grad/offset");
+  check(qfx_cnn_fc1_wgrad(dptr<float>(dh1, torch::kFloat32, "dh1", S * 64), dptr<float>(pool2, torch::kFloat32, "pool2", S * POOL2),
+                          (int)K, (int)B, dptr<float>(grad, torch::kFloat32, "grad", K * P), P, (int)off_w1, stream()),
+        "cnn_fc1_wgrad");
+}
+
 }  // namespace
 
 void register_cnn(pybind11::module& m) {
   m.def("cnn_mfma_probe", &mfma_probe);
   m.def("cnn_forward", &forward, "fused conv1/conv2 + bias + ReLU + maxpool (MFMA implicit GEMM)");
   m.def("cnn_backward", &backward, "conv stack backward -> deterministic per-client weight/bias grads");
-  m.def("cnn_fc1", &fc1, "fc1 forward as split-reduction partial sums [splits, K*B, 64]");
-  m.def("cnn_fc1_splits", []() { return qfx_cnn_fc1_splits(); });
-  m.def("cnn_head", &head, "fc1 partial sums + bias, ReLU + dropout + fc2 + weighted CE fwd/bwd per client");
+  m.def("cnn_head", &head, "ReLU + dropout + fc2 + weighted CE fwd/bwd per client (+ fc1 bias gradient)");
   m.def("cnn_partial_size", []() { return qfx_cnn_partial_size(); });
+  m.def("cnn_fc1_wgrad", &fc1_wgrad, "fc1 weight gradient into the flat [K, P] gradient rows (MFMA)");
   m.def("cnn_bwd_groups", [](int64_t K, int64_t B) { return qfx_cnn_bwd_groups((int)K, (int)B); });
 }

@@ -627,100 +627,15 @@ __global__ void cnn_reduce(const float* __restrict__ part, int G, float* __restr
 }
 
 // --------------------------------------------------------------------------------------------
-// fc1 forward, split over the 1568-long reduction: h1p[ks][s][j] = sum_{c in chunk ks} pool2[s][c] W1[j][c]
-//   grid (client x 32-sample tile, F1KS chunks): 1024 workgroups at 128 clients x 32 samples instead of a
-//   128-tile batched GEMM; the chunk sums (+ bias) are added in fixed order by cnn_head, which reads h1 anyway.
-// --------------------------------------------------------------------------------------------
-constexpr int HID = 64;
-constexpr int F1IN = C2 * Q2 * Q2;             // 1568
-constexpr int F1KS = 8, F1KC = F1IN / F1KS;    // 8 chunks of 196
-constexpr int F1S = 198;                       // LDS row stride (== 6 mod 32: row-strided lanes on distinct banks)
-static_assert(F1KC % 4 == 0, "chunks are whole float4 runs and whole MFMA k-steps");
-
-struct Fc1Set {
-  float a, b[2];
-};
-
-__global__ void __launch_bounds__(256) cnn_fc1(const float* __restrict__ pool2, const float* __restrict__ params,
-                                               int P, int off_w1, int B, int MT, long S, float* __restrict__ h1p) {
-  __shared__ float As[32 * F1S];
-  __shared__ float Bs[HID * F1S];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int k = blockIdx.x / MT, mt = blockIdx.x - k * MT, ks = blockIdx.y;
-  const int s0 = mt * 32, ns = min(32, B - s0);
-  const int c0 = ks * F1KC;
-  const float4* A = reinterpret_cast<const float4*>(pool2 + ((size_t)k * B + s0) * F1IN + c0);
-  // parameter rows are only 8-byte aligned (P is even, not a multiple of 4): W goes as float2
-  const float2* W = reinterpret_cast<const float2*>(params + (size_t)k * P + off_w1 + c0);
-  constexpr int Q4 = F1KC / 4, Q2W = F1KC / 2;   // float4 / float2 per row chunk
-  constexpr int NA = (32 * Q4 + 255) / 256, NB = (HID * Q2W + 255) / 256;
-  float4 va[NA];
-  float2 vb[NB];
-#pragma unroll
-  for (int u = 0; u < NA; ++u) {
-    const int e = tid + u * 256, r = e / Q4, c = e - r * Q4;
-    va[u] = (e < 32 * Q4 && r < ns) ? A[(size_t)r * (F1IN / 4) + c] : float4{0.f, 0.f, 0.f, 0.f};
-  }
-#pragma unroll
-  for (int u = 0; u < NB; ++u) {
-    const int e = tid + u * 256, r = e / Q2W, c = e - r * Q2W;
-    if (e < HID * Q2W) vb[u] = W[(size_t)r * (F1IN / 2) + c];
-  }
-#pragma unroll
-  for (int u = 0; u < NA; ++u) {
-    const int e = tid + u * 256, r = e / Q4, c = e - r * Q4;
-    if (e < 32 * Q4) {
-      float* d = As + r * F1S + 4 * c;
-      d[0] = va[u].x; d[1] = va[u].y; d[2] = va[u].z; d[3] = va[u].w;
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < NB; ++u) {
-    const int e = tid + u * 256, r = e / Q2W, c = e - r * Q2W;
-    if (e < HID * Q2W) {
-      float* d = Bs + r * F1S + 2 * c;
-      d[0] = vb[u].x;
-      d[1] = vb[u].y;
-    }
-  }
-  __syncthreads();
-  // wave w: m-tile (w & 1) x n-tiles 2(w >> 1), 2(w >> 1) + 1
-  const int i = lane & 15, kq = lane >> 4;
-  const int mtl = wave & 1, nt0 = (wave >> 1) * 2;
-  const float* ap = As + (mtl * 16 + i) * F1S + kq;
-  const float* bp = Bs + (nt0 * 16 + i) * F1S + kq;
-  f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-  pipelined<Fc1Set>(
-      0, F1KC / 4,
-      [&](int st, Fc1Set& o) {
-        o.a = ap[4 * st];
-        o.b[0] = bp[4 * st];
-        o.b[1] = bp[16 * F1S + 4 * st];
-      },
-      [&](const Fc1Set& o) {
-        acc[0] = mfma(o.a, o.b[0], acc[0]);
-        acc[1] = mfma(o.a, o.b[1], acc[1]);
-      });
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int sr = mtl * 16 + 4 * kq + r;
-      if (sr < ns) h1p[((size_t)ks * S + (size_t)k * B + s0 + sr) * HID + (nt0 + h) * 16 + i] = acc[h][r];
-    }
-}
-
-// --------------------------------------------------------------------------------------------
 // fc head, one block per client: a = ReLU(h1) * dropout; logits = W a + b; weighted CE; backward:
 // dh1 = (W^T dlogits) * dropout * [h1 > 0]; fc2 grads.  Samples go through LDS in chunks of HB; every
 // stage spreads (sample, class) or (sample, unit) pairs over the block, and all sums over samples run in
 // a fixed order (deterministic).
 // --------------------------------------------------------------------------------------------
-constexpr int CMAXC = 16, HB = 64;
+constexpr int HID = 64, CMAXC = 16, HB = 64;
 constexpr int HG = (CMAXC * HID + CMAXC + 255) / 256;   // fc2 gradient entries per thread
 
-__global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1p, int nsplit, long S, int off_b1,
+__global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, int off_b1,
                                                 const float* __restrict__ mask,
                                                 const float* __restrict__ params, int P, int off_w, int off_b,
                                                 int C, int B, const long long* __restrict__ y,
@@ -729,7 +644,7 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1p, i
                                                 float* __restrict__ correct, float* __restrict__ grad) {
   __shared__ float Ws[CMAXC * HID];
   __shared__ float bs[CMAXC];
-  __shared__ float hv[HB][HID + 1];        // h1 = b1 + fc1 chunk sums (fixed order)
+  __shared__ float hv[HB][HID + 1];        // h1, then dh1 (fc1 bias gradient)
   __shared__ float act[HB][HID + 1];       // ReLU(h1) * dropout of the chunk
   __shared__ float dl[HB][CMAXC + 1];      // logits, then weighted dlogits
   __shared__ float lsb[HB], csb[HB];       // per-sample weighted loss / correct flag
@@ -747,8 +662,7 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1p, i
     __syncthreads();   // previous chunk fully consumed (and Ws / bs staged)
     for (int e = tid; e < nb * HID; e += 256) {
       const int b = e / HID, j = e - b * HID;
-      float h = prow[off_b1 + j];
-      for (int q = 0; q < nsplit; ++q) h += h1p[((size_t)q * S + sb) * HID + e];
+      const float h = h1[sb * HID + e];
       hv[b][j] = h;
       act[b][j] = fmaxf(h, 0.f) * mask[sb * HID + e];
     }
@@ -821,6 +735,48 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1p, i
   }
 }
 
+// --------------------------------------------------------------------------------------------
+// fc1 weight gradient written straight into the parameter-gradient rows:
+//   grad[k][off_w1 + j*1568 + c] = sum_s dh1[k,s][j] pool2[k,s][c]
+// grid (64-column tile, client): M = 64 units (one m-tile per wave), N = 64 columns (4 n-tiles), K = the client's
+// samples in chunks of 32; operands come straight from global (dh1 rows stay in L2, each pool2 tile is read once),
+// all 40 loads of a chunk in flight before its MFMAs.  Bandwidth-bound: pool2 read + gradient write once.
+// --------------------------------------------------------------------------------------------
+constexpr int F1IN = C2 * Q2 * Q2;   // 1568 fc1 inputs
+
+__global__ void __launch_bounds__(256) cnn_fc1_wgrad(const float* __restrict__ dh1, const float* __restrict__ pool2,
+                                                     int B, float* __restrict__ grad, int P, int off_w1) {
+  const int k = blockIdx.y, c0 = blockIdx.x * 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, kq = lane >> 4;
+  const float* dh = dh1 + (size_t)k * B * HID + wave * 16 + i;
+  const float* p2 = pool2 + (size_t)k * B * F1IN + c0 + i;
+  f4 acc[4] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  for (int s0 = 0; s0 < B; s0 += 32) {
+    float a[8], b[8][4];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int s = s0 + ks * 4 + kq;
+      const bool ok = s < B;
+      a[ks] = ok ? dh[(size_t)s * HID] : 0.f;
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt)
+        b[ks][nt] = (ok && c0 + nt * 16 + i < F1IN) ? p2[(size_t)s * F1IN + nt * 16] : 0.f;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma(a[ks], b[ks][nt], acc[nt]);
+  }
+  float* g = grad + (size_t)k * P + off_w1 + (size_t)(wave * 16 + 4 * kq) * F1IN + c0 + i;
+#pragma unroll
+  for (int nt = 0; nt < 4; ++nt)
+    if (c0 + nt * 16 + i < F1IN)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) g[(size_t)r * F1IN + nt * 16] = acc[nt][r];
+}
+
 size_t fwd_lds() {
   return (size_t)(C2 * W2F + C1 * K1P + C1 + C2 + FSG * IMGP * IMGP + FSG * C1 * CSF) * 4;
 }
@@ -883,24 +839,21 @@ extern "C" int qfx_cnn_backward(const float* X, const float* params, int P, int 
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_cnn_fc1(const float* pool2, const float* params, int P, int off_w1, int K, int B, float* h1p,
-                           hipStream_t st) {
-  const int MT = (B + 31) / 32;
-  if (K <= 0 || B <= 0) return 0;
-  hipLaunchKernelGGL(cnn_fc1, dim3(K * MT, F1KS), dim3(256), 0, st, pool2, params, P, off_w1, B, MT, (long)K * B, h1p);
-  return (int)hipGetLastError();
-}
-
-extern "C" int qfx_cnn_head(const float* h1p, int off_b1, const float* mask, const float* params, int P, int off_w,
+extern "C" int qfx_cnn_head(const float* h1, int off_b1, const float* mask, const float* params, int P, int off_w,
                             int off_b, int C, int K, int B, const long long* y, const float* wts, float* dh1,
                             float* dlog, float* loss, float* correct, float* grad, hipStream_t st) {
   if (C > CMAXC) return -2;
-  hipLaunchKernelGGL(cnn_head, dim3(K), dim3(256), 0, st, h1p, F1KS, (long)K * B, off_b1, mask, params, P, off_w,
-                     off_b, C, B, y, wts, dh1, dlog, loss, correct, grad);
+  hipLaunchKernelGGL(cnn_head, dim3(K), dim3(256), 0, st, h1, off_b1, mask, params, P, off_w, off_b, C, B, y, wts, dh1,
+                     dlog, loss, correct, grad);
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_cnn_fc1_splits() { return F1KS; }
+extern "C" int qfx_cnn_fc1_wgrad(const float* dh1, const float* pool2, int K, int B, float* grad, int P, int off_w1,
+                                 hipStream_t st) {
+  if (K <= 0 || B <= 0) return 0;
+  hipLaunchKernelGGL(cnn_fc1_wgrad, dim3((F1IN + 63) / 64, K), dim3(256), 0, st, dh1, pool2, B, grad, P, off_w1);
+  return (int)hipGetLastError();
+}
 
 extern "C" int qfx_cnn_partial_size() { return PART; }
 extern "C" int qfx_cnn_bwd_groups(int K, int B) {

@@ -3,8 +3,8 @@
 One local step of K clients x B samples:
   1. ``cnn_forward``  - fused conv1/conv2 + bias + ReLU + 2x2 max-pool (fp32 MFMA implicit GEMM, per
                         client weights), writes pooled maps + argmax codes
-  2. ``cnn_fc1``      - fc1 as split-reduction MFMA partial sums (8 chunks of the 1568 inputs per client tile)
-  3. ``cnn_head``     - chunk sums + bias, ReLU + keyed dropout + fc2 + weighted CE, dlogits, fc2 grads, dL/dh1
+  2. fc1              - ``baddbmm`` over the client batch (plain batched GEMM -> hipBLASLt/rocBLAS)
+  3. ``cnn_head``     - ReLU + keyed dropout + fc2 + weighted CE, dlogits, fc2 grads, dL/dh1, fc1 bias grad
   4. fc1 backward     - two batched GEMMs (weight grad, dL/dpool2)
   5. ``cnn_backward`` - unpool + ReLU masks, conv2 weight/input grads, conv1 weight grads (MFMA),
                         deterministic fixed-order reduction into the flat [K, P] gradient
@@ -76,19 +76,17 @@ class HipTinyCNN:
         K, B = xb.shape[:2]
         S = K * B
         Xf, pool1, am1, pool2, am2 = self.conv_forward(params, xb)
-        h1p = self._buf("h1p", (C.cnn_fc1_splits(), S, 64))
-        C.cnn_fc1(pool2, params, self.fc1w, K, B, h1p)        # split-reduction partials; cnn_head adds them
-        w1 = params[:, self.fc1w: self.fc1b].view(K, 64, 1568)
+        h1, w1 = self._fc1(params, pool2, K, B)
+        h1 = h1.contiguous()
         grad = torch.empty(K, self.P, dtype=torch.float32, device=self.device)   # every entry is written below
         dh1 = self._buf("dh1", (K, B, 64))
         dlog = self._buf("dlog", (S, 16))
         loss = loss_out if loss_out is not None else torch.empty(K, dtype=torch.float32, device=self.device)
         correct = correct_out if correct_out is not None else torch.empty(K, dtype=torch.float32, device=self.device)
         m = mask.float().contiguous() if mask is not None else torch.ones(K, B, 64, device=self.device)
-        C.cnn_head(h1p, self.fc1b, m, params, self.fc2w, self.fc2b, self.C, K, B, yb.reshape(S).long().contiguous(),
+        C.cnn_head(h1, self.fc1b, m, params, self.fc2w, self.fc2b, self.C, K, B, yb.reshape(S).long().contiguous(),
                    wts.reshape(S).float().contiguous(), dh1, dlog, loss, correct, grad)
-        p2 = pool2.view(K, B, 1568)
-        torch.bmm(dh1.transpose(1, 2), p2, out=grad[:, self.fc1w: self.fc1b].view(K, 64, 1568))   # strided C: no copy
+        C.cnn_fc1_wgrad(dh1, pool2, K, B, grad, self.fc1w)      # written straight into the gradient rows
         dP2 = torch.bmm(dh1, w1).reshape(S, 1568).contiguous()
         G = C.cnn_bwd_groups(K, B)
         part = self._buf("part", (K * G, C.cnn_partial_size()))
