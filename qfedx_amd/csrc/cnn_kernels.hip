@@ -397,6 +397,12 @@ __device__ __forceinline__ void bwd_dgrad2(const float* sm, const int (&aoff)[NM
       });
 }
 
+// conv1 wgrad operands of one k-step: unpool1 (argmax code vs position) is resolved at MFMA time
+struct C1Set {
+  float d, b0, b1;
+  int a1, pos;
+};
+
 // dP1 rows of a finished dgrad m-tile, ReLU-masked by pool1 > 0 (the conv1 ReLU derivative)
 __device__ __forceinline__ void bwd_dp1_store(float* dp1, const float* p1s, int mt, f4 acc, int i, int kq) {
 #pragma unroll
@@ -481,11 +487,12 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
   float* w2r = sm;                          // [16][802]: w2r[ci][tap*32 + o] = W2[o][ci][tap]
   float* dc2 = w2r + C1 * W2R;              // [32][338] padded dL/d conv2-output (post-unpool, ReLU-masked)
   float* p1s = dc2 + C2 * CS;               // [16][338] padded pool1 (conv2 input)
-  float* dp1 = p1s + C1 * CS;               // [16][198] dL/d pool1, ReLU-masked
-  float* img = dp1 + C1 * DPS;              // [32][37]  padded image
-  float* ones = img + IMGP * IMS;           // [256]     1.0 (bias columns)
+  // conv1 wgrad of sample s runs during sample s+1's conv2 work: its inputs are double buffered (index s & 1)
+  float* dp1b = p1s + C1 * CS;              // [2][16][198] dL/d pool1, ReLU-masked
+  float* imgb = dp1b + 2 * C1 * DPS;        // [2][32][37]  padded images
+  float* ones = imgb + 2 * IMGP * IMS;      // [256]     1.0 (bias columns)
   float* red12 = ones + 256;                // [4][64]   m-tile 12 partials of waves 4..7
-  uint8_t* a1s = reinterpret_cast<uint8_t*>(red12 + 256);   // [16][198] argmax of pool1
+  uint8_t* a1sb = reinterpret_cast<uint8_t*>(red12 + 256);   // [2][16][198] argmax of pool1
   float* red = dc2;                         // [8 waves][2][256] conv1 wgrad partials (after the sample loop)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): per-wave branches are scalar
@@ -497,7 +504,7 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
 
   stage_w2(prow + off.w2, w2r, 1, W2R, 32, tid);   // w2r[ci][tap*32 + o]
   for (int e = tid; e < (C2 + C1) * CS; e += NT) dc2[e] = 0.f;   // dc2 and p1s are contiguous
-  for (int e = tid; e < IMGP * IMS; e += NT) img[e] = 0.f;
+  for (int e = tid; e < 2 * IMGP * IMS; e += NT) imgb[e] = 0.f;
   if (tid < 256) ones[tid] = 1.f;
 
   // conv2 wgrad tiles: m-tile (o rows) and 7 / 6 n-tiles (taps; n-tile 25 = ones -> db2)
@@ -517,14 +524,40 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
   const int dboff = (int)(w2r - sm) + i * W2R + kq;   // dgrad B: w2r[i][tap*32 + 4*oc + kq]
   __syncthreads();
 
+  // conv1 wgrad (dC1 = unpool1(dp1) on the fly; K = 784 split across the 8 waves) of one finished sample
+  const int toff0 = (i / 5) * IMS + i % 5;
+  const int t1 = min(16 + i, 24);
+  const int toff1 = (t1 / 5) * IMS + t1 % 5;
+  const bool one1 = 16 + i >= K1;
+  auto conv1_wgrad = [&](const float* dp1, const uint8_t* a1s, const float* img) {
+    pipelined<C1Set>(
+        0, (H1 * H1 / 4 - wave + NW - 1) / NW,
+        [&](int m, C1Set& c) {
+          const int p = (wave + NW * m) * 4 + kq, y = p / H1, x = p - y * H1;
+          const int w = (y >> 1) * Q1 + (x >> 1);
+          c.pos = ((y & 1) << 1) | (x & 1);
+          c.a1 = a1s[i * DPS + w];
+          c.d = dp1[i * DPS + w];
+          const float* im = img + y * IMS + x;
+          c.b0 = im[toff0];
+          c.b1 = im[toff1];
+        },
+        [&](const C1Set& c) {
+          const float a = c.a1 == c.pos ? c.d : 0.f;
+          c1acc[0] = mfma(a, c.b0, c1acc[0]);
+          c1acc[1] = mfma(a, one1 ? 1.f : c.b1, c1acc[1]);
+        });
+  };
+
   BwdStage st;
   st.load((size_t)k * B + s0, X, pool1, am1, pool2, am2, dP2, tid);
   for (int s = 0; s < ns; ++s) {
+    float* dp1 = dp1b + (s & 1) * C1 * DPS;
     // ---- stage the sample loaded during the previous one; then issue the next sample's loads, which
     //      complete behind this sample's MFMA work (one workgroup per CU: nothing else hides them)
-    st.store(dc2, p1s, a1s, img, tid);
+    st.store(dc2, p1s, a1sb + (s & 1) * C1 * DPS, imgb + (s & 1) * IMGP * IMS, tid);
     if (s + 1 < ns) st.load((size_t)k * B + s0 + s + 1, X, pool1, am1, pool2, am2, dP2, tid);
-    __syncthreads();
+    __syncthreads();   // staged sample visible; the previous sample's dp1 complete
 
     // ---- conv2 wgrad (accumulates over the workgroup's samples)
     if (wave < 4) bwd_wgrad2<7>(sm, waoff, wboff, wacc, kq);
@@ -555,32 +588,25 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
         for (int r = 0; r < 4; ++r) red12[w4 * 64 + r * 16 + i] = acc12[0][0][r] + acc12[0][1][r];
       }
     }
-    __syncthreads();
-    if (tid < 64) {   // m-tile 12 partials in fixed wave order
-      const int r = tid >> 4, ci = tid & 15, p = 192 + r;
-      const float v = ((red12[tid] + red12[64 + tid]) + red12[128 + tid]) + red12[192 + tid];
-      dp1[ci * DPS + p] = p1s[ci * CS + q14(p) + 2 * P1P + 2] > 0.f ? v : 0.f;
-    }
-    __syncthreads();
 
-    // ---- conv1 wgrad: dC1 = unpool1(dp1) on the fly; K = 784 split across the 8 waves
-    {
-      const int toff0 = (i / 5) * IMS + i % 5;
-      const int t1 = min(16 + i, 24);
-      const int toff1 = (t1 / 5) * IMS + t1 % 5;
-      const bool one1 = 16 + i >= K1;
-      for (int ks = wave; ks < H1 * H1 / 4; ks += NW) {
-        const int p = ks * 4 + kq, y = p / H1, x = p - y * H1;
-        const int w = (y >> 1) * Q1 + (x >> 1), pos = ((y & 1) << 1) | (x & 1);
-        const float a = a1s[i * DPS + w] == pos ? dp1[i * DPS + w] : 0.f;
-        const float* im = img + y * IMS + x;
-        c1acc[0] = mfma(a, im[toff0], c1acc[0]);
-        const float b1 = im[toff1];
-        c1acc[1] = mfma(a, one1 ? 1.f : b1, c1acc[1]);
-      }
+    // ---- conv1 wgrad of the previous sample (its buffers are not touched by this sample)
+    if (s > 0) conv1_wgrad(dp1b + ((s - 1) & 1) * C1 * DPS, a1sb + ((s - 1) & 1) * C1 * DPS,
+                           imgb + ((s - 1) & 1) * IMGP * IMS);
+
+    // m-tile 12 partials in fixed wave order -> dp1 rows 192..195.  The ReLU mask is read before the barrier:
+    // after it the other waves may already restage p1s for the next sample.
+    const int r12 = tid >> 4, ci12 = tid & 15;
+    const bool m12 = tid < 64 && p1s[ci12 * CS + q14(192 + r12) + 2 * P1P + 2] > 0.f;
+    __syncthreads();
+    if (tid < 64) {
+      const float v = ((red12[tid] + red12[64 + tid]) + red12[128 + tid]) + red12[192 + tid];
+      dp1[ci12 * DPS + 192 + r12] = m12 ? v : 0.f;
     }
-    __syncthreads();   // LDS is restaged for the next sample
   }
+  __syncthreads();   // the last sample's dp1 rows 192..195
+  if (ns > 0) conv1_wgrad(dp1b + ((ns - 1) & 1) * C1 * DPS, a1sb + ((ns - 1) & 1) * C1 * DPS,
+                          imgb + ((ns - 1) & 1) * IMGP * IMS);
+  __syncthreads();   // red aliases dc2
 
   // ---- write partials (fixed order: deterministic)
   float* out = part + (size_t)blockIdx.x * PART;
@@ -781,7 +807,7 @@ size_t fwd_lds() {
   return (size_t)(C2 * W2F + C1 * K1P + C1 + C2 + FSG * IMGP * IMGP + FSG * C1 * CSF) * 4;
 }
 size_t bwd_lds() {
-  return (size_t)(C1 * W2R + (C2 + C1) * CS + C1 * DPS + IMGP * IMS + 256 + 256) * 4 + C1 * DPS;
+  return (size_t)(C1 * W2R + (C2 + C1) * CS + 2 * C1 * DPS + 2 * IMGP * IMS + 256 + 256) * 4 + 2 * C1 * DPS;
 }
 
 }  // namespace cnn

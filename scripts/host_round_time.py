@@ -57,8 +57,7 @@ def main():
     if prof is not None:
         import pstats
         st = pstats.Stats(prof)
-        st.sort_stats("cumulative").print_stats(25)
-        st.print_callers("copy_")
+        st.sort_stats("tottime").print_stats(12)
 
 
 if __name__ == "__main__":
