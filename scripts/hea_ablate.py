@@ -78,6 +78,9 @@ def main():
     run("adj0_load_store", True, pa0, a0[:0].contiguous(), ai0[:0].contiguous(), False, True, False, True)
     run("adj0_1back", True, pa0, a0[:1].contiguous(), ai0[:1].contiguous(), False, True, False, False)
     run("adj0_4back", True, pa0, a0[:4].contiguous(), ai0[:4].contiguous(), False, True, False, False)
+    run("adj0_5back", True, pa0, a0[:5].contiguous(), ai0[:5].contiguous(), False, True, False, False)
+    run("adj0_5back_1grad", True, pa0, a0[:6].contiguous(), ai0[:6].contiguous(), False, True, False, False)
+    run("adj0_load_64nop", True, pa0, nop, nopf, False, True, False, False)
     print(json.dumps(res), flush=True)
     for k, v in phases.items():
         print("phases", k, v, flush=True)
