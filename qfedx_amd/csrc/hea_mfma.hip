@@ -601,6 +601,13 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   HEA_MARK();
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
 
+  // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op); op 0's
+  // are requested before the initial tile, so their latency hides behind the tile load / layer-1 generation
+  if (tid < a.nops) fidx_s[tid] = a.fidx[tid];   // LDS copy: the prefetch below never waits on a global load
+  if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
+  int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
+  if (a.nops > 0) dma_frags(a, k, a.fidx[0], tid, wave, frag_s[0]);
+
   // ---------------------------------------------------------------- initial psi tile
   if (a.gen) {
     // Product state of layer 1: wave 0 computes every qubit's 2-vector (lane q) and, by a complex product over
@@ -677,11 +684,6 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   // ---------------------------------------------------------------- op list
   const int ncol = T >> 4, nblk = ncol >> 4;
   const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
-  // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op)
-  if (tid < a.nops) fidx_s[tid] = a.fidx[tid];   // LDS copy: the prefetch below never waits on a global load
-  if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
-  int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
-  if (a.nops > 0) dma_frags(a, k, a.fidx[0], tid, wave, frag_s[0]);
   lds_barrier_dma();
   HEA_MARK();
   for (int o = 0; o < a.nops; ++o) {
@@ -766,6 +768,11 @@ __global__ void __launch_bounds__(1 << (TB - 4), 4) hea_adj_kernel(PassArgs a) {
   long long* slab = a.gslab + ((size_t)s * a.slab_tiles + tile_id) * a.n_gradops * 32;
   QFX_DCHECK(tile_id < a.slab_tiles);
 
+  // op 0's record and fragments are requested before the tile load (their latency hides behind it)
+  if (tid < a.nops) fidx_s[tid] = a.fidx[tid];
+  if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
+  int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
+  if (a.nops > 0) dma_frags(a, k, a.fidx[0], tid, wave, frag_s[0]);
   load_tile_il<NT, TB>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
                        h_q, fixed);
   if (tid == 0) {
@@ -802,10 +809,6 @@ __global__ void __launch_bounds__(1 << (TB - 4), 4) hea_adj_kernel(PassArgs a) {
   // ---------------------------------------------------------------- op list
   const int ncol = T >> 4, nblk = ncol >> 4;
   const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
-  if (tid < a.nops) fidx_s[tid] = a.fidx[tid];
-  if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
-  int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
-  if (a.nops > 0) dma_frags(a, k, a.fidx[0], tid, wave, frag_s[0]);
   lds_barrier_dma();
   HEA_MARK();
   int ngrad = 0;
