@@ -50,8 +50,9 @@ def test_conv_forward_matches_torch(cuda, K, B):
     assert torch.allclose(lg, tc.batched_forward(params, X, 3), atol=1e-4, rtol=1e-4)
 
 
-@pytest.mark.parametrize("K,B,C", [(2, 3, 3), (3, 32, 3), (2, 7, 10), (2, 70, 10)])
+@pytest.mark.parametrize("K,B,C", [(2, 3, 3), (3, 32, 3), (2, 7, 10), (2, 70, 10), (128, 40, 10)])
 def test_loss_and_grads_match_autograd(cuda, K, B, C):
+    # (128, 40): the backward takes 16 samples per workgroup (one per CU) and the last group holds 8
     from qfedx_amd.ops.cnn_hip import HipTinyCNN
     params, X, y, w, mask = _batch(K, B, C, seed=K + B)
     hip = HipTinyCNN(C, cuda)
