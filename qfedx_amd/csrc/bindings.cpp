@@ -274,9 +274,20 @@ void sgdm(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor t_i
 }
 
 // params[k, :] = theta; optional m, v (same shape) and t (any length) zeroed
-// dst (device, uint8) <- src (pinned host, uint8) by a copy kernel that reads the host memory directly
+// Pinned host staging memory allocated mapped + portable (device-readable from every GPU of the process, whatever
+// the current device was at allocation), as a CPU uint8 tensor that frees itself with hipHostFree.
+torch::Tensor host_alloc(int64_t nbytes) {
+  if (nbytes <= 0) throw std::invalid_argument("host_alloc: size");
+  void* p = nullptr;
+  if (hipHostMalloc(&p, (size_t)nbytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess || !p)
+    throw std::runtime_error("host_alloc: hipHostMalloc failed");
+  return torch::from_blob(p, {nbytes}, [](void* q) { (void)hipHostFree(q); },
+                          torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCPU));
+}
+
+// dst (device, uint8) <- src (host_alloc memory, uint8) by a copy kernel that reads the host memory directly
 void host_upload(torch::Tensor src, torch::Tensor dst) {
-  if (src.device().is_cuda() || !src.is_pinned()) throw std::invalid_argument("host_upload: src must be pinned host memory");
+  if (src.device().is_cuda()) throw std::invalid_argument("host_upload: src must be host memory from host_alloc");
   if (!dst.device().is_cuda()) throw std::invalid_argument("host_upload: dst must be a device tensor");
   if (src.scalar_type() != torch::kUInt8 || dst.scalar_type() != torch::kUInt8 || !src.is_contiguous() ||
       !dst.is_contiguous())
@@ -400,6 +411,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("readout_sum", &readout_sum);
   m.def("amp_init", &amp_init);
   m.def("round_init", &round_init);
+  m.def("host_alloc", &host_alloc);
   m.def("host_upload", &host_upload);
   m.def("batch_plan", &qfx_runtime::batch_plan);
   m.def("batch_gather", &batch_gather);

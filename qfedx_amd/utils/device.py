@@ -51,14 +51,14 @@ class _PinnedRing:
         self.events = [None] * self.SLOTS
         self.i = 0
 
-    def acquire(self, nbytes: int):
+    def acquire(self, nbytes: int, alloc):
         i = self.i
         self.i = (i + 1) % self.SLOTS
         if self.events[i] is not None:
             self.events[i].synchronize()
         buf = self.bufs[i]
         if buf is None or buf.numel() < nbytes:
-            buf = torch.empty(max(4096, 1 << (nbytes - 1).bit_length()), dtype=torch.uint8, pin_memory=True)
+            buf = alloc(max(4096, 1 << (nbytes - 1).bit_length()))   # mapped + portable pinned memory
             self.bufs[i] = buf
         return i, buf[:nbytes]
 
@@ -92,7 +92,7 @@ def _upload(fill, nbytes: int, device, dst: torch.Tensor | None = None) -> torch
         return dst.copy_(src, non_blocking=True)
     if _RING is None:
         _RING = _PinnedRing()
-    i, src = _RING.acquire(nbytes)
+    i, src = _RING.acquire(nbytes, E.host_alloc)
     fill(src)
     if dst is None:
         dst = torch.empty(nbytes, dtype=torch.uint8, device=device)
