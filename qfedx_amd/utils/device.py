@@ -58,8 +58,15 @@ class _PinnedRing:
             self.events[i].synchronize()
         buf = self.bufs[i]
         if buf is None or buf.numel() < nbytes:
-            buf = alloc(max(4096, 1 << (nbytes - 1).bit_length()))   # mapped + portable pinned memory
-            self.bufs[i] = buf
+            # mapped + portable pinned memory.  hipHostMalloc is slow (~0.2 ms): the first use sizes EVERY slot,
+            # so the allocations land in a run's first round instead of one per round for the next 15
+            size = max(65536, 1 << (nbytes - 1).bit_length())
+            for j in range(self.SLOTS):
+                if self.bufs[j] is None or self.bufs[j].numel() < nbytes:
+                    if self.events[j] is not None:
+                        self.events[j].synchronize()
+                    self.bufs[j] = alloc(size)
+            buf = self.bufs[i]
         return i, buf[:nbytes]
 
     def release(self, i: int, device) -> None:

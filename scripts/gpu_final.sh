@@ -6,4 +6,4 @@ export TMPDIR=/tmp
 bash scripts/gpu_round.sh || exit $?
 timeout -k 10 300 python bench.py --steps 30 --warmup 5 --clients 8 > gpurun_out/share8.log 2>&1
 rc=$?; echo "share8 rc=$rc"; grep '"metric"' gpurun_out/share8.log; [ $rc -eq 0 ] || exit $rc
-bash scripts/gpu_suite.sh vqc16q_64_mfma vqc20q_dp64_mfma vqc24q_ps256_mfma
+STEPS=10 WARMUP=8 bash scripts/gpu_suite.sh vqc16q_64_mfma vqc20q_dp64_mfma vqc24q_ps256_mfma cfed128 cfed128_epoch
