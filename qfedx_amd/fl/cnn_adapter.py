@@ -90,7 +90,10 @@ class CNNClientTrainer:
             else:
                 xb = store.X[rows, dv["idx"][s]]
                 yb = store.y[rows, dv["idx"][s]]
-            mask = tc.dropout_masks(cids, cfg.batch_size, cfg.seed, round_num, s, self.device)
+            if self._hip is not None:   # the head forms the mask from the keyed uniforms (no extra launches)
+                mask = ("uniforms", tc.dropout_uniforms(cids, cfg.batch_size, cfg.seed, round_num, s, self.device), 0.5)
+            else:
+                mask = tc.dropout_masks(cids, cfg.batch_size, cfg.seed, round_num, s, self.device)
             res = self.loss_and_grads(params, xb, yb, dv["wts"][s], mask, loss_all[s], correct_all[s])
             opt.step(params, res["grad"], dv["act"][s], last=s == S - 1)
             if res["loss"].data_ptr() != loss_all[s].data_ptr():    # portable path: separate outputs
