@@ -14,9 +14,10 @@ int qfx_cnn_forward(const float* X, const float* params, int P, int K, int B, co
 int qfx_cnn_backward(const float* X, const float* params, int P, int K, int B, const int* off4, const float* pool1,
                      const uint8_t* am1, const float* pool2, const uint8_t* am2, const float* dP2, float* part,
                      float* grad, hipStream_t st);
-int qfx_cnn_head(const float* h1, int off_b1, const float* mask, const float* drop_u, float drop_p, float drop_scale,
-                 const float* params, int P, int off_w, int off_b, int C, int K, int B, const long long* y,
-                 const float* wts, float* dh1, float* dlog, float* loss, float* correct, float* grad, hipStream_t st);
+int qfx_cnn_head(const float* h1, int off_b1, const float* mask, const long long* dkeys, unsigned drop_stream,
+                 float drop_p, float drop_scale, const float* params, int P, int off_w, int off_b, int C, int K, int B,
+                 const long long* y, const float* wts, float* dh1, float* dlog, float* loss, float* correct,
+                 float* grad, hipStream_t st);
 int qfx_cnn_partial_size();
 int qfx_cnn_fc1_wgrad(const float* dh1, const float* pool2, int K, int B, float* grad, int P, int off_w1, hipStream_t st);
 int qfx_cnn_bwd_groups(int K, int B);
@@ -76,20 +77,20 @@ void backward(torch::Tensor X, torch::Tensor params, int64_t K, int64_t B, std::
 }
 
 // h1: fc1 pre-activations [K*B, 64]; off_b1: fc1 bias offset in the parameter row (its gradient is written here).
-// Dropout: ``mask`` [K*B, 64], or (mask undefined) keyed uniforms ``drop_u`` [K*B, 64] kept (x drop_scale) where
-// u >= drop_p.
-void head(torch::Tensor h1, int64_t off_b1, c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> drop_u,
-          double drop_p, double drop_scale, torch::Tensor params, int64_t off_w, int64_t off_b, int64_t C, int64_t K,
+// Dropout: ``mask`` [K*B, 64], or (mask undefined) per-client Philox keys ``dkeys`` [K, 2] (int64 words) whose
+// uniforms of stream ``drop_stream`` are kept (x drop_scale) where u >= drop_p.
+void head(torch::Tensor h1, int64_t off_b1, c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> dkeys,
+          int64_t drop_stream, double drop_p, double drop_scale, torch::Tensor params, int64_t off_w, int64_t off_b, int64_t C, int64_t K,
           int64_t B, torch::Tensor y, torch::Tensor wts, torch::Tensor dh1, torch::Tensor dlog, torch::Tensor loss,
           torch::Tensor correct, torch::Tensor grad) {
   const int64_t S = K * B;
   const int P = (int)params.size(1);
-  const bool hm = mask.has_value() && mask->defined(), hu = drop_u.has_value() && drop_u->defined();
-  if (hm == hu) throw std::invalid_argument("cnn_head: pass exactly one of mask / drop_u");
+  const bool hm = mask.has_value() && mask->defined(), hu = dkeys.has_value() && dkeys->defined();
+  if (hm == hu) throw std::invalid_argument("cnn_head: pass exactly one of mask / dkeys");
   check(qfx_cnn_head(dptr<float>(h1, torch::kFloat32, "h1", S * 64), (int)off_b1,
                      hm ? dptr<float>(*mask, torch::kFloat32, "mask", S * 64) : nullptr,
-                     hu ? dptr<float>(*drop_u, torch::kFloat32, "drop_u", S * 64) : nullptr, (float)drop_p,
-                     (float)drop_scale,
+                     hu ? dptr<long long>(*dkeys, torch::kInt64, "dkeys", 2 * K) : nullptr, (unsigned)drop_stream,
+                     (float)drop_p, (float)drop_scale,
                      dptr<float>(params, torch::kFloat32, "params", K * P), P, (int)off_w, (int)off_b, (int)C, (int)K,
                      (int)B, dptr<long long>(y, torch::kInt64, "y", S), dptr<float>(wts, torch::kFloat32, "wts", S),
                      dptr<float>(dh1, torch::kFloat32, "dh1", S * 64), dptr<float>(dlog, torch::kFloat32, "dlog", S * 16),

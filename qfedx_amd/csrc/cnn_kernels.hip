@@ -17,6 +17,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "philox.h"
+
 namespace qfx {
 namespace cnn {
 
@@ -661,11 +663,12 @@ __global__ void cnn_reduce(const float* __restrict__ part, int G, float* __restr
 constexpr int HID = 64, CMAXC = 16, HB = 64;
 constexpr int HG = (CMAXC * HID + CMAXC + 255) / 256;   // fc2 gradient entries per thread
 
-// Dropout: either a [K*B, 64] mask, or (mask == nullptr) the keyed uniforms u with keep value drop_scale where
-// u >= drop_p (the mask is formed here instead of by separate elementwise launches; same fp32 values).
+// Dropout: either a [K*B, 64] mask, or (mask == nullptr) the client's keyed Philox uniforms u (element b*64 + j of
+// stream drop_stream, tinycnn.dropout_masks' exact values) kept x drop_scale where u >= drop_p - generated here
+// instead of by a uniforms kernel and elementwise launches.
 __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, int off_b1,
-                                                const float* __restrict__ mask, const float* __restrict__ drop_u,
-                                                float drop_p, float drop_scale,
+                                                const float* __restrict__ mask, const long long* __restrict__ dkeys,
+                                                unsigned drop_stream, float drop_p, float drop_scale,
                                                 const float* __restrict__ params, int P, int off_w, int off_b,
                                                 int C, int B, const long long* __restrict__ y,
                                                 const float* __restrict__ wts, float* __restrict__ dh1,
@@ -693,7 +696,9 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
       const int b = e / HID, j = e - b * HID;
       const float h = h1[sb * HID + e];
       hv[b][j] = h;
-      const float mk = mask ? mask[sb * HID + e] : (drop_u[sb * HID + e] >= drop_p ? drop_scale : 0.f);
+      const float mk = mask ? mask[sb * HID + e]
+                            : (philox_uniform_at((uint64_t)(b0 * HID + e), (uint32_t)dkeys[2 * k],
+                                                 (uint32_t)dkeys[2 * k + 1], drop_stream) >= drop_p ? drop_scale : 0.f);
       act[b][j] = fmaxf(h, 0.f) * mk;
     }
     __syncthreads();
@@ -731,8 +736,10 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
       const int b = e / HID, j = e - b * HID;
       float d = 0.f;
       for (int c = 0; c < C; ++c) d = fmaf(Ws[c * HID + j], dl[b][c], d);
-      const float mk = mask ? mask[sb * HID + e] : (drop_u[sb * HID + e] >= drop_p ? drop_scale : 0.f);
-      d = hv[b][j] > 0.f ? d * mk : 0.f;
+      if (mask)
+        d = hv[b][j] > 0.f ? d * mask[sb * HID + e] : 0.f;
+      else   // keyed mask values are 0 or drop_scale: kept with h1 > 0 exactly where act > 0
+        d = act[b][j] > 0.f ? d * drop_scale : 0.f;
       dh1[sb * HID + e] = d;
       hv[b][j] = d;
     }
@@ -870,14 +877,14 @@ extern "C" int qfx_cnn_backward(const float* X, const float* params, int P, int 
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_cnn_head(const float* h1, int off_b1, const float* mask, const float* drop_u, float drop_p,
-                            float drop_scale, const float* params, int P, int off_w, int off_b, int C, int K, int B,
-                            const long long* y, const float* wts, float* dh1, float* dlog, float* loss, float* correct,
-                            float* grad, hipStream_t st) {
+extern "C" int qfx_cnn_head(const float* h1, int off_b1, const float* mask, const long long* dkeys,
+                            unsigned drop_stream, float drop_p, float drop_scale, const float* params, int P, int off_w,
+                            int off_b, int C, int K, int B, const long long* y, const float* wts, float* dh1,
+                            float* dlog, float* loss, float* correct, float* grad, hipStream_t st) {
   if (C > CMAXC) return -2;
-  if (!mask && !drop_u) return -3;
-  hipLaunchKernelGGL(cnn_head, dim3(K), dim3(256), 0, st, h1, off_b1, mask, drop_u, drop_p, drop_scale, params, P,
-                     off_w, off_b, C, B, y, wts, dh1, dlog, loss, correct, grad);
+  if (!mask && !dkeys) return -3;
+  hipLaunchKernelGGL(cnn_head, dim3(K), dim3(256), 0, st, h1, off_b1, mask, dkeys, drop_stream, drop_p, drop_scale,
+                     params, P, off_w, off_b, C, B, y, wts, dh1, dlog, loss, correct, grad);
   return (int)hipGetLastError();
 }
 

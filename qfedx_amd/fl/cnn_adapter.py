@@ -61,6 +61,8 @@ class CNNClientTrainer:
             raise RuntimeError("minibatch plan indexes past the client store")
         tabs = {"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid,
                 "w": store.counts[li].to(torch.float64)}
+        if self._hip is not None:   # dropout Philox keys ride with the round's tables; the head draws the masks
+            tabs["dkeys"] = tc.dropout_keys(cids, cfg.seed, round_num)
         for name, t in (extra or {}).items():
             if name in tabs or t.shape[0] != K:
                 raise ValueError(f"extra table {name!r} must be a new per-client [K, ...] table")
@@ -90,8 +92,8 @@ class CNNClientTrainer:
             else:
                 xb = store.X[rows, dv["idx"][s]]
                 yb = store.y[rows, dv["idx"][s]]
-            if self._hip is not None:   # the head forms the mask from the keyed uniforms (no extra launches)
-                mask = ("uniforms", tc.dropout_uniforms(cids, cfg.batch_size, cfg.seed, round_num, s, self.device), 0.5)
+            if self._hip is not None:   # the head draws the keyed mask itself (no upload or launches per step)
+                mask = ("philox", dv["dkeys"], s, 0.5)
             else:
                 mask = tc.dropout_masks(cids, cfg.batch_size, cfg.seed, round_num, s, self.device)
             res = self.loss_and_grads(params, xb, yb, dv["wts"][s], mask, loss_all[s], correct_all[s])

@@ -117,17 +117,16 @@ def batched_forward(params: torch.Tensor, x: torch.Tensor, num_classes: int = 3,
     return torch.baddbmm(v["fc2.bias"][:, None, :], h, v["fc2.weight"].transpose(1, 2))
 
 
-def dropout_uniforms(K_ids, B: int, seed: int, round_num: int, step: int, device) -> torch.Tensor:
-    """The keyed uniforms [K, B * 64] behind ``dropout_masks`` (keyed by (seed, round, client, step))."""
-    from ..quantum.noise import uniforms
-    from ..utils.device import h2d
+def dropout_keys(K_ids, seed: int, round_num: int) -> torch.Tensor:
+    """Host int64 [K, 2] Philox keys of the clients' dropout streams in round ``round_num`` (step = stream)."""
     from ..utils.seeding import philox_key
-    keys = h2d(torch.tensor([philox_key(seed, "dropout", round_num, int(c)) for c in K_ids], dtype=torch.int64),
-               device)
-    return uniforms(keys, B * 64, stream=step)      # HIP Philox kernel on GPU, bit-identical torch oracle on CPU
+    return torch.tensor([philox_key(seed, "dropout", round_num, int(c)) for c in K_ids], dtype=torch.int64)
 
 
 def dropout_masks(K_ids, B: int, seed: int, round_num: int, step: int, device, p: float = 0.5) -> torch.Tensor:
     """Inverted-dropout masks [K, B, 64] keyed by (seed, round, client, step) - rank-count invariant."""
-    u = dropout_uniforms(K_ids, B, seed, round_num, step, device)
+    from ..quantum.noise import uniforms
+    from ..utils.device import h2d
+    keys = h2d(dropout_keys(K_ids, seed, round_num), device)
+    u = uniforms(keys, B * 64, stream=step)      # HIP Philox kernel on GPU, bit-identical torch oracle on CPU
     return ((u >= p).float() / (1 - p)).reshape(len(K_ids), B, 64)

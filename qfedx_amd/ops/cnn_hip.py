@@ -70,9 +70,9 @@ class HipTinyCNN:
     def loss_and_grads(self, params: torch.Tensor, xb: torch.Tensor, yb: torch.Tensor, wts: torch.Tensor,
                        mask, loss_out: torch.Tensor | None = None,
                        correct_out: torch.Tensor | None = None) -> dict:
-        """``mask``: [K, B, 64] dropout mask, ``None`` (no dropout) or ``("uniforms", u, p)`` - keyed uniforms the
-        head turns into the inverted-dropout mask itself (u >= p kept x 1/(1-p), the same fp32 values as
-        ``tinycnn.dropout_masks``).  ``loss_out`` / ``correct_out``: optional contiguous fp32 [K] rows the head
+        """``mask``: [K, B, 64] dropout mask, ``None`` (no dropout) or ``("philox", keys, stream, p)`` - per-client
+        device Philox keys [K, 2] from which the head draws the inverted-dropout mask itself (u >= p kept x
+        1/(1-p): ``tinycnn.dropout_masks``' exact values).  ``loss_out`` / ``correct_out``: optional contiguous fp32 [K] rows the head
         writes into directly."""
         C = ext()
         params = params.float().contiguous()
@@ -87,12 +87,13 @@ class HipTinyCNN:
         loss = loss_out if loss_out is not None else torch.empty(K, dtype=torch.float32, device=self.device)
         correct = correct_out if correct_out is not None else torch.empty(K, dtype=torch.float32, device=self.device)
         if isinstance(mask, tuple):
-            _, u, p = mask
-            m, du, dp, ds = None, u.float().contiguous(), float(p), float(torch.tensor(1.0) / (1 - p))
+            _, dkeys, stream, p = mask
+            m, dk, dst, dp, ds = None, dkeys.reshape(K, 2).long().contiguous(), int(stream), float(p), \
+                float(torch.tensor(1.0) / (1 - p))
         else:
             m = mask.float().contiguous() if mask is not None else torch.ones(K, B, 64, device=self.device)
-            du, dp, ds = None, 0.0, 1.0
-        C.cnn_head(h1, self.fc1b, m, du, dp, ds, params, self.fc2w, self.fc2b, self.C, K, B, yb.reshape(S).long().contiguous(),
+            dk, dst, dp, ds = None, 0, 0.0, 1.0
+        C.cnn_head(h1, self.fc1b, m, dk, dst, dp, ds, params, self.fc2w, self.fc2b, self.C, K, B, yb.reshape(S).long().contiguous(),
                    wts.reshape(S).float().contiguous(), dh1, dlog, loss, correct, grad)
         C.cnn_fc1_wgrad(dh1, pool2, K, B, grad, self.fc1w)      # written straight into the gradient rows
         dP2 = torch.bmm(dh1, w1).reshape(S, 1568).contiguous()

@@ -104,18 +104,18 @@ def test_cfed_federated_run_hip_matches_cpu(cuda):
 
 
 def test_head_dropout_from_uniforms_matches_mask(cuda):
-    """The head forming the inverted-dropout mask from the keyed uniforms gives bit-identical results to the
+    """The head drawing the inverted-dropout mask from the clients' Philox keys gives bit-identical results to the
     materialised ``dropout_masks`` tensor."""
     from qfedx_amd.ops.cnn_hip import HipTinyCNN
     K, B, C = 3, 20, 10
     params, X, y, w, _ = _batch(K, B, C, seed=5)
     hip = HipTinyCNN(C, cuda)
     ids = [7, 11, 19]
-    u = tc.dropout_uniforms(ids, B, 42, 3, 1, cuda)
+    keys = tc.dropout_keys(ids, 42, 3).to(cuda)
     m = tc.dropout_masks(ids, B, 42, 3, 1, cuda)
     args = (params.to(cuda), X.to(cuda), y.to(cuda), w.to(cuda))
     r1 = hip.loss_and_grads(*args, m)
     r1 = {k: v.clone() for k, v in r1.items()}
-    r2 = hip.loss_and_grads(*args, ("uniforms", u, 0.5))
+    r2 = hip.loss_and_grads(*args, ("philox", keys, 1, 0.5))
     for k in ("loss", "grad", "correct"):
         assert torch.equal(r1[k], r2[k]), k
