@@ -335,7 +335,9 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
 //                tap 25 is a ones column (db1); taps 26..31 are discarded
 // Work split (MFMA count per SIMD balanced; waves w and w+4 share a SIMD): wave w<4 owns dgrad
 // m-tiles 2w, 2w+1 and 7 wgrad n-tiles; wave w>=4 owns dgrad m-tile 4+w, a quarter of the
-// reduction of m-tile 12 (rows 192..195, the only partial tile) and 6 wgrad n-tiles.
+// reduction of m-tile 12 (rows 192..195, the only partial tile) and 6 wgrad n-tiles.  Every wave
+// also takes an eighth of the previous sample's conv1 wgrad (its inputs are double buffered), so
+// a sample costs two barriers; the next sample's global inputs load into registers meanwhile.
 // --------------------------------------------------------------------------------------------
 constexpr int BS_MAX = 16;         // samples per backward workgroup, at most (bwd_bs)
 constexpr int CS = 338;            // LDS stride of one zero-padded 18x18 map (== 18 mod 32: channel-strided
