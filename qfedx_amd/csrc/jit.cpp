@@ -23,6 +23,7 @@
 #include <stdexcept>
 #include <string>
 #include <sys/stat.h>
+#include <unistd.h>
 #include <unordered_map>
 #include <vector>
 
@@ -535,14 +536,24 @@ int jit_prepare(const std::vector<int>& blob, int p, bool adjoint, const std::st
     e->code = hiprtc_compile(spec.source, include_dir, arch);
     if (!cache_dir.empty()) {
       mkdir(cache_dir.c_str(), 0755);
-      std::string tmp = path + ".tmp";
+      // one temp file per process: the ranks of a node share the cache and may compile the same key at once;
+      // each renames a complete file of its own over the entry, so a reader never sees a partial code object
+      const std::string tag = "." + std::to_string((long)getpid()) + ".tmp";
+      std::string tmp = path + tag;
+      bool ok;
       {
         std::ofstream f(tmp, std::ios::binary);
         f.write(e->code.data(), (std::streamsize)e->code.size());
+        ok = (bool)f;
       }
-      std::rename(tmp.c_str(), path.c_str());
-      std::ofstream fs(cache_dir + "/" + key + ".hip");
-      fs << spec.source;
+      if (ok) std::rename(tmp.c_str(), path.c_str());
+      else std::remove(tmp.c_str());
+      const std::string src = cache_dir + "/" + key + ".hip";
+      {
+        std::ofstream fs(src + tag);
+        fs << spec.source;
+      }
+      std::rename((src + tag).c_str(), src.c_str());
     }
   }
   g_entries.push_back(std::move(e));
