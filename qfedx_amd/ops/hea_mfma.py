@@ -26,6 +26,7 @@ import torch
 from ._ext import ext
 from .hea_plan import OP_APPLY, OP_READOUT, TILE_BITS, W_CODE, build_plan, eligible, obs_table, pass_programs
 
+HEA_CHUNKS = 1       # client chunks per training step on staggered streams (A/B: scripts/hea_kbench.py)
 ADJ_TILE_BITS = 13   # adjoint tiles: 2^13 amplitudes x (psi, lambda) = 64 KB of LDS -> two workgroups per CU
 
 
@@ -164,16 +165,17 @@ class HeaMfmaProgram:
                 int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
                 self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops]
 
-    def _frags(self, params: torch.Tensor, K: int) -> torch.Tensor:
-        fr = self._buf("frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
+    def _frags(self, params: torch.Tensor, K: int, tag: str = "") -> torch.Tensor:
+        fr = self._buf(f"{tag}frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
         if self.n_slots:
             ext().hea_frags(params, params.shape[1], self.slot_tab, self.n_slots, K, fr)
         return fr
 
-    def _forward(self, x, params, fr, K, B, part, store_last: bool = False):
+    def _forward(self, x, params, fr, K, B, part, store_last: bool = False, tag: str = "", after_first=None):
         """Forward passes up to the readout pass ``fwd_last``; returns the stored pass outputs (all of them with
         ``store_last``: the adjoint starts each pass from its output; identity passes after ``fwd_last`` alias
-        its output)."""
+        its output).  ``tag`` names this client chunk's workspaces; ``after_first()`` runs right after the
+        first pass is queued."""
         C = ext()
         S = K * B
         N = S << self.n
@@ -184,18 +186,20 @@ class HeaMfmaProgram:
         for j in range(R + 1):
             p, fwd = self.passes[j][0], self.passes[j][1]
             keep = j < R or store_last
-            out = self._buf(f"psi{j}", N, torch.int32) if keep else empty
+            out = self._buf(f"{tag}psi{j}", N, torch.int32) if keep else empty
             psi_in = stored[-1] if j > 0 else empty
             geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K)
             C.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
                        part if j == R else fempty, fempty, _NODBG)
+            if j == 0 and after_first is not None:
+                after_first()
             if keep:
                 stored.append(out)
         if store_last:
             stored += [stored[R]] * (J - 1 - R)
         return stored
 
-    def _adjoint(self, x, params, fr, K, B, stored, wread, gslab):
+    def _adjoint(self, x, params, fr, K, B, stored, wread, gslab, tag: str = ""):
         C = ext()
         S = K * B
         N = S << self.n
@@ -205,7 +209,7 @@ class HeaMfmaProgram:
         lam_in = empty
         for j in range(J - 1, -1, -1):
             _, _, adj, p = self.passes[j]
-            lam_out = self._buf(f"lam{j % 2}", N, torch.int32) if j > 0 else empty
+            lam_out = self._buf(f"{tag}lam{j % 2}", N, torch.int32) if j > 0 else empty
             geom = self._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, x.shape[1], K)
             C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
                        params, fr, wread, fempty, gslab, _NODBG)
@@ -263,25 +267,29 @@ class HeaMfmaProgram:
         return z.view(S, self.C).clone(), grad[:, : self.n_theta]
 
     # ------------------------------------------------------------------ train step
-    def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
-                       out_correct=None, init: torch.Tensor | None = None) -> dict:
-        """One adjoint training step (same contract as ``HipProgram.loss_and_grads``)."""
-        if init is not None:
-            raise ValueError("the MFMA engine starts from the angle feature map (no initial states)")
-        x, p, K, B = self._prep(xang, params)
-        S = K * B
+    def _chunks(self, K: int, B: int) -> int:
+        """Client chunks of a training step (``QFEDX_HEA_CHUNKS`` overrides).  Chunk i runs on its own stream
+        and starts once chunk i-1's first forward pass is queued, so HBM-bound forward passes of one chunk
+        overlap the LDS/MFMA-bound adjoint passes of another and no pass drains the GPU by itself."""
+        env = os.environ.get("QFEDX_HEA_CHUNKS")
+        n = int(env) if env else HEA_CHUNKS
+        return max(1, min(n, K))
+
+    def _stream(self, i: int) -> torch.cuda.Stream:
+        streams = self.__dict__.setdefault("_streams", [])
+        while len(streams) <= i:
+            streams.append(torch.cuda.Stream(device=self.device))
+        return streams[i]
+
+    def _step(self, x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, tag="", after_first=None):
+        """Forward, readout + CE, adjoint and gradient reduction of clients [0, K) of the given row slices."""
         C = ext()
-        yy = y.reshape(S).long().contiguous()
-        ww = wmask.reshape(S).float().contiguous()
-        fr = self._frags(p, K)
-        part = self._buf("part", S * self.tiles_last * self.C, torch.float32)
-        expz = self._buf("expz", S * self.C, torch.float32)
-        wread = self._buf("wread", S * self.C, torch.float32)
-        gslab = self._buf("gslab", S * self.slab_tiles * self.n_gradops * 32, torch.int64)
-        loss = torch.empty(K, dtype=torch.float32, device=self.device) if out_loss is None else out_loss
-        correct = torch.empty(K, dtype=torch.float32, device=self.device) if out_correct is None else out_correct
-        grad = torch.empty_like(p)
-        stored = self._forward(x, p, fr, K, B, part, store_last=True)
+        S = K * B
+        fr = self._frags(p, K, tag)
+        part = self._buf(f"{tag}part", S * self.tiles_last * self.C, torch.float32)
+        wread = self._buf(f"{tag}wread", S * self.C, torch.float32)
+        gslab = self._buf(f"{tag}gslab", S * self.slab_tiles * self.n_gradops * 32, torch.int64)
+        stored = self._forward(x, p, fr, K, B, part, store_last=True, tag=tag, after_first=after_first)
         if noise is None:
             C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss, correct,
                          grad, True, 0.0, 0.0, 0, _NO_KEYS, 0)
@@ -289,6 +297,57 @@ class HeaMfmaProgram:
             from .statevec_hip import _keys
             C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss, correct,
                          grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
-        self._adjoint(x, p, fr, K, B, stored, wread, gslab)
+        self._adjoint(x, p, fr, K, B, stored, wread, gslab, tag)
         C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1])
+
+    def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
+                       out_correct=None, init: torch.Tensor | None = None) -> dict:
+        """One adjoint training step (same contract as ``HipProgram.loss_and_grads``).
+
+        Clients are independent within a step, so the step runs as ``_chunks`` client chunks on staggered
+        streams (fork/join events; captured into the round's hipGraph as parallel branches).  Every chunk
+        writes only its own client rows, so results are bitwise those of one chunk."""
+        if init is not None:
+            raise ValueError("the MFMA engine starts from the angle feature map (no initial states)")
+        x, p, K, B = self._prep(xang, params)
+        S = K * B
+        yy = y.reshape(S).long().contiguous()
+        ww = wmask.reshape(S).float().contiguous()
+        expz = self._buf("expz", S * self.C, torch.float32)
+        loss = torch.empty(K, dtype=torch.float32, device=self.device) if out_loss is None else out_loss
+        correct = torch.empty(K, dtype=torch.float32, device=self.device) if out_correct is None else out_correct
+        grad = torch.empty_like(p)
+        n = self._chunks(K, B) if noise is None else 1
+        if n == 1:
+            self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step)
+        else:
+            bounds = [(i * K) // n for i in range(n + 1)]
+            cur = torch.cuda.current_stream(self.device)
+            C = self.C
+            # size every chunk's workspaces on the launching stream before forking (nothing allocates on a branch)
+            for i in range(n):
+                k0, k1 = bounds[i], bounds[i + 1]
+                Si = (k1 - k0) * B
+                self._buf(f"c{i}frags", max((k1 - k0) * self.n_slots * 4 * 128 * 4, 1), torch.int32)
+                for name, numel, dt in ((f"c{i}part", Si * self.tiles_last * C, torch.float32),
+                                        (f"c{i}wread", Si * C, torch.float32),
+                                        (f"c{i}gslab", Si * self.slab_tiles * self.n_gradops * 32, torch.int64)):
+                    self._buf(name, numel, dt)
+                for j in range(self.fwd_last + 1):
+                    self._buf(f"c{i}psi{j}", Si << self.n, torch.int32)
+                for j in range(min(2, self.n_passes - 1)):
+                    self._buf(f"c{i}lam{j}", Si << self.n, torch.int32)
+            gates = [torch.cuda.Event() for _ in range(n - 1)]
+            for i in range(n):
+                k0, k1 = bounds[i], bounds[i + 1]
+                st = cur if i == 0 else self._stream(i - 1)
+                if i > 0:
+                    st.wait_event(gates[i - 1])         # after chunk i-1's first pass (and all prior work)
+                rec = (lambda e=gates[i]: e.record()) if i < n - 1 else None
+                r0, r1 = k0 * B, k1 * B
+                with torch.cuda.stream(st):
+                    self._step(x[r0:r1], p[k0:k1], yy[r0:r1], ww[r0:r1], k1 - k0, B, loss[k0:k1],
+                               correct[k0:k1], grad[k0:k1], expz[r0 * C:r1 * C], None, None, step, f"c{i}", rec)
+            for i in range(n - 1):
+                cur.wait_stream(self._stream(i))
         return {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}

@@ -114,6 +114,48 @@ def test_hea_24q_three_passes_match_valu_engine(cuda):
     np.testing.assert_allclose(g.cpu().numpy(), g_ref.cpu().numpy(), atol=3e-3)
 
 
+@pytest.mark.parametrize("chunks", [2, 3])
+def test_hea_chunked_step_is_bitwise_single_chunk(cuda, monkeypatch, chunks):
+    """A step split into client chunks on staggered streams (eager and hipGraph-captured) gives bitwise the
+    loss, hits, <Z> and gradients of one chunk: every chunk writes only its own client rows."""
+    spec = VQCSpec(12, 3, 3, readout_scale=2.0)
+    K, B = 5, 4
+    g = torch.Generator().manual_seed(11)
+    xang = spec.encode_features(torch.rand(K, B, 12, generator=g)).to(cuda)
+    y = torch.randint(0, 3, (K, B), generator=g).to(cuda)
+    w = torch.full((K, B), 1.0 / B, device=cuda)
+    params = torch.stack([spec.init_params(k) for k in range(K)])
+    params = (params + 0.3 * torch.randn(params.shape, generator=g)).to(cuda)
+
+    def run(n, graph=False):
+        monkeypatch.setenv("QFEDX_HEA_CHUNKS", str(n))
+        prog = HeaMfmaProgram(spec, cuda)
+        if not graph:
+            out = prog.loss_and_grads(xang, y, w, params, spec)
+            torch.cuda.synchronize()
+            return {k: v.clone() for k, v in out.items()}
+        ws = {}
+        with prog.private_workspace(ws):
+            side = torch.cuda.Stream(device=cuda)
+            side.wait_stream(torch.cuda.current_stream(cuda))
+            with torch.cuda.stream(side):
+                prog.loss_and_grads(xang, y, w, params, spec)
+            torch.cuda.current_stream(cuda).wait_stream(side)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                out = prog.loss_and_grads(xang, y, w, params, spec)
+        gr.replay()
+        gr.replay()
+        torch.cuda.synchronize()
+        return {k: v.clone() for k, v in out.items()}
+
+    ref = run(1)
+    for graph in (False, True):
+        got = run(chunks, graph)
+        for k in ("loss", "correct", "grad", "expz"):
+            assert torch.equal(got[k], ref[k]), (k, graph)
+
+
 @pytest.mark.parametrize("C,tile", [(2, 14), (4, 8), (5, 14), (8, 9), (8, 14)])
 def test_hea_class_counts_match_dense(cuda, C, tile):
     """Readout / observable ops are specialised per class count (register sign tables up to 4 classes,
