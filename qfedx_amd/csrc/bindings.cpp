@@ -74,12 +74,17 @@ int qfx_launch_sgdm(float* p, const float* g, float* buf, const float* t_in, flo
 int qfx_launch_host_upload(const void* host_src, void* dst, long nbytes, hipStream_t st);
 int qfx_launch_round_init(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
                           hipStream_t st);
+int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
+                              const float* X, const long long* Y, const long long* lid, const long long* idx,
+                              int steps, int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride,
+                              long long* yo, hipStream_t st);
 int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx, int K,
                             int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride, long long* yo,
                             hipStream_t st);
 int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
                       const double* weights, double* norms, const uint32_t* keys, int K, int P, int wrap, int dp,
-                      float clip, float sigma, long long* out, hipStream_t st);
+                      float clip, float sigma, long long* out, long long* pack_buf, const float* loss,
+                      const float* correct, const float* nvalid, const float* act, int n_metrics, hipStream_t st);
 }
 
 namespace qfx_runtime {
@@ -337,9 +342,49 @@ void batch_gather(torch::Tensor X, torch::Tensor Y, torch::Tensor lid, torch::Te
         "qfx_batch_gather");
 }
 
+// round_init + the minibatch gather of every local step in one launch: idx [steps, K, B] int64,
+// x_out [steps, K, B, >= F] fp32, y_out [steps * K * B] int64 (same checks as round_init / batch_gather)
+void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<torch::Tensor> m,
+                    c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> t, torch::Tensor X, torch::Tensor Y,
+                    torch::Tensor lid, torch::Tensor idx, int64_t mode, double alpha, torch::Tensor x_out,
+                    torch::Tensor y_out) {
+  need(theta, torch::kFloat32, "theta");
+  need(params, torch::kFloat32, "params");
+  const int64_t K = params.size(0), P = params.size(1);
+  if (theta.numel() != P) throw std::invalid_argument("round_prologue: theta size != params row");
+  torch::Tensor mt = m ? *m : torch::Tensor(), vt = v ? *v : torch::Tensor(), tt = t ? *t : torch::Tensor();
+  for (auto* x : {&mt, &vt})
+    if (x->defined()) {
+      need(*x, torch::kFloat32, "round_prologue state");
+      if (x->numel() != K * P) throw std::invalid_argument("round_prologue: state shape");
+    }
+  if (tt.defined()) need(tt, torch::kFloat32, "round_prologue t");
+  need(X, torch::kFloat32, "X");
+  need(Y, torch::kInt64, "Y");
+  need(lid, torch::kInt64, "lid");
+  need(idx, torch::kInt64, "idx");
+  need(x_out, torch::kFloat32, "x_out");
+  need(y_out, torch::kInt64, "y_out");
+  if (X.dim() != 3 || Y.dim() != 2 || idx.dim() != 3 || Y.size(1) != X.size(1))
+    throw std::invalid_argument("round_prologue: shapes");
+  const int64_t S = idx.size(0), B = idx.size(2), F = X.size(2);
+  if (idx.size(1) != K || lid.numel() != K || x_out.dim() != 4 || x_out.size(0) != S || x_out.size(1) != K ||
+      x_out.size(2) != B || x_out.size(3) < F || y_out.numel() < S * K * B || mode < 0 || mode > 2)
+    throw std::invalid_argument("round_prologue: output shapes / mode");
+  check(qfx_launch_round_prologue(ptr<float>(theta), (int)K, (int)P, ptr<float>(params), ptr<float>(mt), ptr<float>(vt),
+                                  ptr<float>(tt), tt.defined() ? (int)tt.numel() : 0, ptr<float>(X),
+                                  ptr<long long>(Y), ptr<long long>(lid), ptr<long long>(idx), (int)S, (int)B,
+                                  (long)X.size(1), (int)F, (int)mode, (float)alpha, ptr<float>(x_out),
+                                  (int)x_out.size(3), ptr<long long>(y_out), cur_stream()),
+        "qfx_round_prologue");
+}
+
+// pack_buf (optional, the round's [P + 5] all-reduce buffer): one more block of the same launch packs the round
+// metrics (loss, correct, nvalid, act: float32 [n]) into its tail, as round_pack does
 void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_mask, torch::Tensor weights,
             torch::Tensor norms, torch::Tensor keys, bool wrap, bool dp, double clip, double sigma,
-            torch::Tensor out) {
+            torch::Tensor out, torch::Tensor pack_buf, torch::Tensor loss, torch::Tensor correct,
+            torch::Tensor nvalid, torch::Tensor act) {
   need(theta_k, torch::kFloat32, "theta_k");
   need(theta_g, torch::kFloat32, "theta_g");
   need(weights, torch::kFloat64, "weights");
@@ -349,9 +394,22 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
   if (out.numel() < P + 1) throw std::invalid_argument("fedavg out too small");
   if (norms.numel() < qfx_fedavg_norm_scratch(K, P)) throw std::invalid_argument("fedavg norms scratch too small");
   if (dp && keys.numel() < 2 * K) throw std::invalid_argument("fedavg: DP needs 2 key words per client");
+  const bool pack = pack_buf.defined() && pack_buf.numel() > 0;
+  int64_t n = 0;
+  if (pack) {
+    need(pack_buf, torch::kInt64, "pack_buf");
+    for (auto* x : {&loss, &correct, &nvalid, &act}) need(*x, torch::kFloat32, "fedavg metric");
+    n = loss.numel();
+    if (pack_buf.numel() < P + 5 || correct.numel() < n || nvalid.numel() < n || act.numel() < n)
+      throw std::invalid_argument("fedavg: metric pack sizes");
+    if (out.data_ptr() != pack_buf.data_ptr()) throw std::invalid_argument("fedavg: out must be the head of pack_buf");
+  }
   check(qfx_launch_fedavg(ptr<float>(theta_k), ptr<float>(theta_g), ptr<unsigned char>(angle_mask),
                           ptr<double>(weights), ptr<double>(norms), ptr<uint32_t>(keys), K, P, wrap ? 1 : 0,
-                          dp ? 1 : 0, (float)clip, (float)sigma, ptr<long long>(out), cur_stream()),
+                          dp ? 1 : 0, (float)clip, (float)sigma, ptr<long long>(out),
+                          pack ? ptr<long long>(pack_buf) : nullptr, pack ? ptr<float>(loss) : nullptr,
+                          pack ? ptr<float>(correct) : nullptr, pack ? ptr<float>(nvalid) : nullptr,
+                          pack ? ptr<float>(act) : nullptr, (int)n, cur_stream()),
         "qfx_fedavg");
 }
 
@@ -415,6 +473,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("host_upload", &host_upload);
   m.def("batch_plan", &qfx_runtime::batch_plan);
   m.def("batch_gather", &batch_gather);
+  m.def("round_prologue", &round_prologue);
   m.def("amp_scratch", &amp_scratch);
   m.def("readout_noise", &readout_noise);
   m.def("philox_uniform", &philox_uniform);

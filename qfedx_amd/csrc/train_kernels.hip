@@ -340,6 +340,40 @@ __global__ void qfx_delta_norm_final_kernel(const double* __restrict__ partial, 
   norms[k] = sqrt(s);
 }
 
+// round epilogue 1 body: metrics -> exact fixed point in the all-reduce buffer tail, fixed summation order
+//   buf[P+1..P+4] = round(2^32 * [sum loss*nvalid, sum correct*act, sum nvalid (samples), sum act (steps)])
+// Everything comes from device tables (nothing round-dependent is a kernel argument), so the launch can sit
+// inside a captured round graph.  One 256-thread block: strided float64 partials, then a fixed-shape tree.
+struct RoundPack {          // metrics of the round epilogue (buf == nullptr: not packed by this launch)
+  long long* buf;
+  const float *loss, *correct, *nvalid, *act;
+  int n;
+};
+
+__device__ __forceinline__ void round_pack_block(const RoundPack& rp, int P) {
+  __shared__ double red[4][256];
+  const int t = threadIdx.x;
+  double ls = 0.0, cs = 0.0, ns = 0.0, as = 0.0;
+  for (int i = t; i < rp.n; i += 256) {
+    const double nv = (double)rp.nvalid[i], ac = (double)rp.act[i];
+    ls += (double)rp.loss[i] * nv;
+    cs += (double)rp.correct[i] * ac;
+    ns += nv;
+    as += ac;
+  }
+  red[0][t] = ls;
+  red[1][t] = cs;
+  red[2][t] = ns;
+  red[3][t] = as;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (t < h)
+      for (int j = 0; j < 4; ++j) red[j][t] += red[j][t + h];
+    __syncthreads();
+  }
+  if (t < 4) rp.buf[P + 1 + t] = llrint(red[t][0] * 4294967296.0);
+}
+
 // out[e] = sum_k round(2^32 * w_k * priv(wrap(theta_k[e] - theta_g[e]))), out[P] = sum_k round(2^32 w_k)
 // Each client's term is rounded to fixed point BEFORE the sum: integer addition is associative, so the
 // aggregate is bitwise identical for any sharding of clients over GPUs (and equal to the CPU path).
@@ -367,7 +401,13 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
     const float* __restrict__ theta_k, const float* __restrict__ theta_g,
     const unsigned char* __restrict__ angle_mask, const double* __restrict__ weights,
     const double* __restrict__ norms, const uint32_t* __restrict__ keys, int K, int P, int wrap,
-    int dp, float clip, float sigma, long long* __restrict__ out) {
+    int dp, float clip, float sigma, long long* __restrict__ out, RoundPack rp) {
+  // the block past the parameter blocks (launched only with rp.buf) packs the round metrics into the tail of
+  // the all-reduce buffer: the parameter blocks write out[0..P], the pack block out[P+1..P+4]
+  if (blockIdx.x == gridDim.x - 1 && rp.buf != nullptr) {
+    round_pack_block(rp, P);
+    return;
+  }
   // thread (group g, lane el): parameter e = block * FA_E + el (a wave reads 256 contiguous bytes of a client
   // row), clients k = g, g + FA_G, ... with FA_U rows loaded before their terms are formed; the FA_G integer
   // partials are combined in LDS (exact, so neither split changes a bit of the result)
@@ -403,37 +443,8 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
   }
 }
 
-// round epilogue 1: metrics -> exact fixed point in the all-reduce buffer tail, fixed summation order
-//   buf[P+1..P+4] = round(2^32 * [sum loss*nvalid, sum correct*act, sum nvalid (samples), sum act (steps)])
-// Everything comes from device tables (nothing round-dependent is a kernel argument), so the launch can sit
-// inside a captured round graph.  One 256-thread block: strided float64 partials, then a fixed-shape tree.
-__global__ void __launch_bounds__(256) qfx_round_pack_kernel(long long* __restrict__ buf, int P,
-                                                             const float* __restrict__ loss,
-                                                             const float* __restrict__ correct,
-                                                             const float* __restrict__ nvalid,
-                                                             const float* __restrict__ act, int n) {
-  __shared__ double red[4][256];
-  const int t = threadIdx.x;
-  double ls = 0.0, cs = 0.0, ns = 0.0, as = 0.0;
-  for (int i = t; i < n; i += 256) {
-    const double nv = (double)nvalid[i], ac = (double)act[i];
-    ls += (double)loss[i] * nv;
-    cs += (double)correct[i] * ac;
-    ns += nv;
-    as += ac;
-  }
-  red[0][t] = ls;
-  red[1][t] = cs;
-  red[2][t] = ns;
-  red[3][t] = as;
-  __syncthreads();
-  for (int h = 128; h > 0; h >>= 1) {
-    if (t < h)
-      for (int j = 0; j < 4; ++j) red[j][t] += red[j][t + h];
-    __syncthreads();
-  }
-  if (t < 4) buf[P + 1 + t] = llrint(red[t][0] * 4294967296.0);
-}
+// round epilogue 1 on its own (the HIP round path packs in the FedAvg launch's last block instead)
+__global__ void __launch_bounds__(256) qfx_round_pack_kernel(RoundPack rp, int P) { round_pack_block(rp, P); }
 
 // round epilogue 2 (after the all-reduce): theta += lr * (sum w Delta) / (sum w) in float64, rounded to
 // fp32 - the same operations as Aggregator.finalize + apply; rounds with zero total weight keep theta.
@@ -461,7 +472,7 @@ extern "C" int qfx_fedavg_norm_scratch(int K, int P) { return K * (1 + (P + NORM
 
 extern "C" int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct,
                                      const float* nvalid, const float* act, int n, hipStream_t st) {
-  hipLaunchKernelGGL(qfx_round_pack_kernel, dim3(1), dim3(256), 0, st, buf, P, loss, correct, nvalid, act, n);
+  hipLaunchKernelGGL(qfx_round_pack_kernel, dim3(1), dim3(256), 0, st, RoundPack{buf, loss, correct, nvalid, act, n}, P);
   return (int)hipGetLastError();
 }
 
@@ -547,30 +558,38 @@ extern "C" int qfx_launch_sgdm(float* p, const float* g, float* buf, const float
 // ----------------------------------------------------------------------------------- round prologue
 // local round start: every client row starts from the global params; optimizer moments / counters zeroed
 // grid (chunks of SG_E parameters, clients): no per-element client modulo
-__global__ void __launch_bounds__(256) qfx_round_init_kernel(const float* __restrict__ theta, int K, int P,
-                                                             float* __restrict__ params, float* __restrict__ m,
-                                                             float* __restrict__ v, float* __restrict__ t, int nt) {
-  const int k = blockIdx.y;
-  const size_t row = (size_t)k * P;
-  const int e0 = blockIdx.x * SG_E + threadIdx.x;
+struct RoundInit {
+  const float* theta;
+  int K, P;
+  float *params, *m, *v, *t;   // m / v / t may be null
+  int nt;
+};
+
+__device__ __forceinline__ void round_init_chunk(const RoundInit& ri, int k, int chunk) {
+  const size_t row = (size_t)k * ri.P;
+  const int e0 = chunk * SG_E + threadIdx.x;
 #pragma unroll
   for (int u = 0; u < SG_U; ++u) {
     const int e = e0 + u * 256;
-    if (e < P) {
-      params[row + e] = theta[e];
-      if (m) m[row + e] = 0.f;
-      if (v) v[row + e] = 0.f;
+    if (e < ri.P) {
+      ri.params[row + e] = ri.theta[e];
+      if (ri.m) ri.m[row + e] = 0.f;
+      if (ri.v) ri.v[row + e] = 0.f;
     }
   }
-  if (t && blockIdx.x == 0 && k == 0)
-    for (int i = threadIdx.x; i < nt; i += 256) t[i] = 0.f;
+  if (ri.t && chunk == 0 && k == 0)
+    for (int i = threadIdx.x; i < ri.nt; i += 256) ri.t[i] = 0.f;
+}
+
+__global__ void __launch_bounds__(256) qfx_round_init_kernel(RoundInit ri) {
+  round_init_chunk(ri, blockIdx.y, blockIdx.x);
 }
 
 extern "C" int qfx_launch_round_init(const float* theta, int K, int P, float* params, float* m, float* v, float* t,
                                      int nt, hipStream_t st) {
   if (K <= 0 || P <= 0) return 0;
   hipLaunchKernelGGL(qfx_round_init_kernel, dim3((unsigned)((P + SG_E - 1) / SG_E), (unsigned)K),
-                     dim3(256), 0, st, theta, K, P, params, m, v, t, nt);
+                     dim3(256), 0, st, RoundInit{theta, K, P, params, m, v, t, nt});
   return (int)hipGetLastError();
 }
 
@@ -596,21 +615,30 @@ extern "C" int qfx_launch_host_upload(const void* host_src, void* dst, long nbyt
   return (int)hipGetLastError();
 }
 
-// per-step minibatch gather + feature encoding, one block per sample s = k*B + b:
+// per-step minibatch gather + feature encoding, one block per sample row s = (step * K + k) * B + b:
 //   x_out[s, 0:F] = enc(X[lid[k], idx[s], 0:F]),  y_out[s] = Y[lid[k], idx[s]]
 // enc: 0 = alpha * x (ROADMAP RY(alpha x)), 1 = per-sample min-max -> pi * x^ (qAngle.py:36-41; constant
 // rows -> 0), 2 = raw copy (amplitude encoding: normalised later by the state-load kernel)
-__global__ void __launch_bounds__(256) qfx_batch_gather_kernel(
-    const float* __restrict__ X, const long long* __restrict__ Y, const long long* __restrict__ lid,
-    const long long* __restrict__ idx, int B, long nmax, int F, int mode, float alpha, float* __restrict__ xo,
-    int x_stride, long long* __restrict__ yo) {
+struct BatchGather {
+  const float* X;
+  const long long *Y, *lid, *idx;
+  int K, B;
+  long nmax;
+  int F, mode;
+  float alpha;
+  float* xo;
+  int x_stride;
+  long long* yo;
+};
+
+__device__ __forceinline__ void gather_row(const BatchGather& g, long s) {
   __shared__ float smn[4], smx[4];
-  const long s = blockIdx.x;
-  const long row = lid[s / B] * nmax + idx[s];
-  const float* xr = X + row * F;
-  float* out = xo + s * (long)x_stride;
-  if (threadIdx.x == 0) yo[s] = Y[row];
-  if (mode == 1) {
+  const long row = g.lid[(s / g.B) % g.K] * g.nmax + g.idx[s];
+  const int F = g.F;
+  const float* xr = g.X + row * F;
+  float* out = g.xo + s * (long)g.x_stride;
+  if (threadIdx.x == 0) g.yo[s] = g.Y[row];
+  if (g.mode == 1) {
     float mn = INFINITY, mx = -INFINITY;
     for (int f = threadIdx.x; f < F; f += blockDim.x) {
       const float v = xr[f];
@@ -636,11 +664,39 @@ __global__ void __launch_bounds__(256) qfx_batch_gather_kernel(
     const float rng = mx - mn;
     const float pi_f = 3.14159265358979323846f;
     for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = rng > 0.f ? ((xr[f] - mn) / rng) * pi_f : 0.f;
-  } else if (mode == 0) {
-    for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = alpha * xr[f];
+  } else if (g.mode == 0) {
+    for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = g.alpha * xr[f];
   } else {
     for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = xr[f];
   }
+}
+
+__global__ void __launch_bounds__(256) qfx_batch_gather_kernel(BatchGather g) { gather_row(g, blockIdx.x); }
+
+// Round prologue in ONE launch: blocks [0, K * chunks) initialise the client rows / optimizer state (as
+// qfx_round_init_kernel), the rest gather and encode the minibatches of EVERY local step of the round (as
+// qfx_batch_gather_kernel over steps * K * B rows).  Neither part reads what the other writes.
+__global__ void __launch_bounds__(256) qfx_round_prologue_kernel(RoundInit ri, int chunks, BatchGather g) {
+  const int init_blocks = ri.K * chunks;
+  if ((int)blockIdx.x < init_blocks) {
+    round_init_chunk(ri, blockIdx.x / chunks, blockIdx.x % chunks);
+    return;
+  }
+  gather_row(g, (long)blockIdx.x - init_blocks);
+}
+
+extern "C" int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, float* m, float* v, float* t,
+                                         int nt, const float* X, const long long* Y, const long long* lid,
+                                         const long long* idx, int steps, int B, long nmax, int F, int mode,
+                                         float alpha, float* xo, int x_stride, long long* yo, hipStream_t st) {
+  if (K <= 0 || P <= 0) return 0;
+  const int chunks = (P + SG_E - 1) / SG_E;
+  const long blocks = (long)K * chunks + (long)steps * K * B;
+  if (blocks > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(qfx_round_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                     RoundInit{theta, K, P, params, m, v, t, nt}, chunks,
+                     BatchGather{X, Y, lid, idx, K, B, nmax, F, mode, alpha, xo, x_stride, yo});
+  return (int)hipGetLastError();
 }
 
 extern "C" int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx,
@@ -648,14 +704,16 @@ extern "C" int qfx_launch_batch_gather(const float* X, const long long* Y, const
                                        long long* yo, hipStream_t st) {
   if (K <= 0 || B <= 0) return 0;
   const int threads = F > 64 ? 256 : 64;
-  hipLaunchKernelGGL(qfx_batch_gather_kernel, dim3((unsigned)((long)K * B)), dim3(threads), 0, st, X, Y, lid, idx, B,
-                     nmax, F, mode, alpha, xo, x_stride, yo);
+  hipLaunchKernelGGL(qfx_batch_gather_kernel, dim3((unsigned)((long)K * B)), dim3(threads), 0, st,
+                     BatchGather{X, Y, lid, idx, K, B, nmax, F, mode, alpha, xo, x_stride, yo});
   return (int)hipGetLastError();
 }
 
 extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
                                  const double* weights, double* norms, const uint32_t* keys, int K, int P,
-                                 int wrap, int dp, float clip, float sigma, long long* out, hipStream_t st) {
+                                 int wrap, int dp, float clip, float sigma, long long* out, long long* pack_buf,
+                                 const float* loss, const float* correct, const float* nvalid, const float* act,
+                                 int n_metrics, hipStream_t st) {
   if (dp) {   // clipping needs the per-client norms; without DP they are not computed
     const int nc = (P + NORM_CHUNK - 1) / NORM_CHUNK;
     double* partial = norms + K;   // scratch tail of the norms buffer: K * nc doubles
@@ -663,7 +721,9 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                        wrap, partial);
     hipLaunchKernelGGL(qfx_delta_norm_final_kernel, dim3((K + 63) / 64), dim3(64), 0, st, partial, nc, K, norms);
   }
-  hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3((P + FA_E - 1) / FA_E), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
-                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out);
+  const RoundPack rp{pack_buf, loss, correct, nvalid, act, n_metrics};
+  const unsigned blocks = (unsigned)((P + FA_E - 1) / FA_E) + (pack_buf ? 1u : 0u);
+  hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3(blocks), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
+                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out, rp);
   return (int)hipGetLastError();
 }

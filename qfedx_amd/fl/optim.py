@@ -58,6 +58,15 @@ class BatchedOptimizer:
         params.copy_(theta[None, :].expand_as(params))
         self.reset()
 
+    def init_state(self):
+        """(m, v, t) for a round-prologue kernel that does ``init_round``'s work itself (HIP backend): the
+        optimizer counts as freshly reset once that kernel is queued."""
+        if self.backend != "hip":
+            raise RuntimeError("init_state() is for the fused HIP round prologue")
+        self._phase = 0
+        self._fresh = True
+        return (self.m if self.kind == "adam" else None), self.v, self._t
+
     @torch.no_grad()
     def step(self, params: torch.Tensor, grads: torch.Tensor, active: Optional[torch.Tensor] = None,
              last: bool = False) -> None:

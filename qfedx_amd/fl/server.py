@@ -210,9 +210,10 @@ class FederatedRunner:
         trainer = self.adapter.trainer
         if fast:
             # round epilogue on the device, run by the trainer right after the local steps (captured into the
-            # round's hipGraph): the fused local reduce writes the head of the all-reduce buffer and a pack
-            # kernel appends the fixed-point metrics.  Round-dependent inputs (DP noise keys, uniform FedAvg
-            # weights) travel as per-client tables with the round's upload, never as kernel arguments.
+            # round's hipGraph): the fused local reduce writes the head of the all-reduce buffer and the last
+            # block of the same launch appends the fixed-point metrics.  Round-dependent inputs (DP noise keys,
+            # uniform FedAvg weights) travel as per-client tables with the round's upload, never as kernel
+            # arguments.
             if getattr(self, "_round_buf", None) is None:
                 self._round_buf = torch.zeros(P + 5, dtype=torch.int64, device=dev)
             buf = self._round_buf
@@ -225,11 +226,11 @@ class FederatedRunner:
             agg = self.aggregator
 
             def epilogue(params_k, tabs, theta):
+                # one launch: the fused reduce writes the buffer head, its last block packs the metrics
                 agg.local_reduce(params_k, theta, tabs.get("fw", tabs["w"]), r, ids, out=buf[: P + 1],
-                                 keys=tabs.get("dpkeys"))
-                from ..ops._ext import ext
-                ext().round_pack(buf, P, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
-                                 tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1))
+                                 keys=tabs.get("dpkeys"),
+                                 pack=(buf, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
+                                       tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)))
             with self.timer.phase("local_train"):
                 res = trainer.run_round(self.store, local_alive, self.params, r, epilogue=epilogue,
                                         extra=extra or None)

@@ -214,19 +214,27 @@ class VQCClientTrainer:
         opt_kind = "sgd" if cfg.optimizer == "spsa" else cfg.optimizer
         opt = BatchedOptimizer(opt_kind, (K, P), self.device, cfg.learning_rate, cfg.momentum,
                                backend=self.backend, zero_init=False)
-        opt.init_round(params, theta.float())
         loss_all = torch.empty(steps, K, dtype=torch.float32, device=self.device)
         correct_all = torch.empty(steps, K, dtype=torch.float32, device=self.device)
         BT = idx_d.shape[-1] * T
         fused = self.backend == "hip" and X.is_cuda
+        # one prologue launch: client rows + optimizer state initialised and every step's minibatch gathered
+        # and encoded up front (trajectory replicas, T > 1, gather per step)
+        upfront = fused and T == 1
         if fused:
             from ..ops._ext import ext
             mode = 2 if spec.amplitude else (1 if spec.feature_scale == "minmax" else 0)
-            xbuf = torch.empty(K, BT, X.shape[-1], dtype=torch.float32, device=self.device)
-            ybuf = torch.empty(K * BT, dtype=torch.int64, device=self.device)
+            xbuf = torch.empty(steps if upfront else 1, K, BT, X.shape[-1], dtype=torch.float32, device=self.device)
+            ybuf = torch.empty((steps if upfront else 1) * K * BT, dtype=torch.int64, device=self.device)
             dummy = torch.zeros(K, BT, 0 if spec.noisy else 1, device=self.device) if spec.amplitude else None
         else:
             rows = lid[:, None]
+        if upfront:
+            m, v, t = opt.init_state()
+            ext().round_prologue(theta.float().contiguous(), params, m, v, t, X, Y, lid, idx_d.contiguous(), mode,
+                                 float(spec.alpha), xbuf, ybuf)
+        else:
+            opt.init_round(params, theta.float())
         for s in range(steps):
             bi = idx_d[s]
             ws = wts_d[s]
@@ -234,10 +242,13 @@ class VQCClientTrainer:
                 bi = bi.repeat(1, T)
                 ws = ws.repeat(1, T) / T
             if fused:
-                ext().batch_gather(X, Y, lid, bi.contiguous(), mode, float(spec.alpha), xbuf, ybuf)
-                yb = ybuf.view(K, BT)
-                init = xbuf if spec.amplitude else None
-                xang = dummy if spec.amplitude else xbuf
+                if upfront:
+                    xs, yb = xbuf[s], ybuf.view(steps, K, BT)[s]
+                else:
+                    ext().batch_gather(X, Y, lid, bi.contiguous(), mode, float(spec.alpha), xbuf[0], ybuf)
+                    xs, yb = xbuf[0], ybuf.view(K, BT)
+                init = xs if spec.amplitude else None
+                xang = dummy if spec.amplitude else xs
             else:
                 xb = X[rows, bi]                     # [K, B, F]
                 yb = Y[rows, bi]

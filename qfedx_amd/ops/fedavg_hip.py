@@ -19,6 +19,7 @@ def sgdm_step(params, grads, buf, t_in, t_out, active, lr, mu, keep_state: bool 
 
 
 _NO_KEYS = {}
+_NO_PACK = {}
 
 
 def dp_noise_keys(client_ids, round_num, seed) -> torch.Tensor:
@@ -28,13 +29,15 @@ def dp_noise_keys(client_ids, round_num, seed) -> torch.Tensor:
 
 
 def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp, clip_norm,
-                       noise_multiplier, out=None, keys=None):
+                       noise_multiplier, out=None, keys=None, pack=None):
     """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as exact int64 fixed point (scale 2^32)
     [P+1] (per-client terms rounded before the sum -> rank-count invariant), plus norms [K].
     ``angle_mask`` uint8 [P] on the device; ``out`` an optional int64 [P+1] destination (e.g. the head
     of the round's all-reduce buffer).  DP noise keys are only built / uploaded when DP is on; ``keys``
     (device int32 [K, 2], ``dp_noise_keys``) passes them in already on the device, which keeps the launch
-    free of host values that change per round (capturable into a round graph)."""
+    free of host values that change per round (capturable into a round graph).  ``pack`` = (buf, loss,
+    correct, nvalid, act): ``out`` is the head of the round's [P + 5] all-reduce buffer ``buf`` and one more
+    block of the same launch packs the round metrics into its tail (what ``round_pack`` does on its own)."""
     K, P = theta_k.shape
     dev = theta_k.device
     if dp and keys is not None:
@@ -50,7 +53,11 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
         out = torch.empty(P + 1, dtype=torch.int64, device=dev)
     if angle_mask.dtype != torch.uint8:
         angle_mask = angle_mask.to(torch.uint8)
+    if pack is None:
+        e = _NO_PACK.setdefault(dev, (torch.zeros(0, dtype=torch.int64, device=dev),
+                                      torch.zeros(0, dtype=torch.float32, device=dev)))
+        pack = (e[0], e[1], e[1], e[1], e[1])
     ext().fedavg(theta_k.float().contiguous(), theta_g.float().contiguous(), angle_mask.contiguous(),
                  weights.double().contiguous(), norms, keys, bool(wrap), bool(dp), float(clip_norm),
-                 float(noise_multiplier) if dp else 0.0, out)
+                 float(noise_multiplier) if dp else 0.0, out, *pack)
     return out, (norms[:K] if dp else None)

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Interleaved bench.py A/B of the working tree against a built copy of another tree in ab/old (same box):
+# headline (64 clients) and the 8-client per-rank share, ROUNDS rounds each.
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+root=$PWD
+for r in $(seq ${ROUNDS:-3}); do for v in old new; do for cl in 64 8; do
+  d=$root; [ $v = old ] && d=$root/ab/old
+  (cd $d && timeout -k 10 300 python bench.py --steps 40 --warmup 5 --clients $cl) > gpurun_out/abtree_${v}_${cl}_$r.log 2>&1 || exit 1
+  echo "$v clients=$cl r=$r $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/abtree_${v}_${cl}_$r.log)"
+done; done; done

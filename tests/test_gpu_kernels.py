@@ -192,6 +192,60 @@ def test_batch_gather_matches_torch(cuda, mode, F):
     assert torch.equal(yo.cpu().view(K, B), Y[lid[:, None], idx])
 
 
+@pytest.mark.parametrize("mode,F", [(0, 16), (1, 16), (1, 300), (2, 784)])
+def test_round_prologue_matches_init_and_per_step_gathers(cuda, mode, F):
+    """One prologue launch (client rows + Adam state init, every step's minibatch gathered) == round_init +
+    one batch_gather per step (bitwise)."""
+    from qfedx_amd.ops._ext import ext
+    g = torch.Generator().manual_seed(F + 1)
+    Nc, nmax, K, B, S, P = 7, 40, 4, 9, 3, 3000
+    X = torch.randn(Nc, nmax, F, generator=g).to(cuda)
+    Y = torch.randint(0, 5, (Nc, nmax), generator=g).to(cuda)
+    lid = torch.tensor([5, 2, 0, 6]).to(cuda)
+    idx = torch.randint(0, nmax, (S, K, B), generator=g).to(cuda)
+    theta = torch.randn(P, generator=g).to(cuda)
+    xo = torch.full((S, K, B, F), 7.0, device=cuda)
+    yo = torch.full((S * K * B,), -1, dtype=torch.int64, device=cuda)
+    p, m, v, t = (torch.full((K, P), 9.0, device=cuda), torch.ones(K, P, device=cuda),
+                  torch.ones(K, P, device=cuda), torch.ones(2, K, device=cuda))
+    ext().round_prologue(theta, p, m, v, t, X, Y, lid, idx, mode, 2.5, xo, yo)
+    p2, m2, v2, t2 = (torch.full((K, P), 9.0, device=cuda), torch.ones(K, P, device=cuda),
+                      torch.ones(K, P, device=cuda), torch.ones(2, K, device=cuda))
+    ext().round_init(theta, p2, m2, v2, t2)
+    for s in range(S):
+        xr = torch.empty(K, B, F, device=cuda)
+        yr = torch.empty(K * B, dtype=torch.int64, device=cuda)
+        ext().batch_gather(X, Y, lid, idx[s].contiguous(), mode, 2.5, xr, yr)
+        assert torch.equal(xo[s], xr) and torch.equal(yo.view(S, K * B)[s], yr)
+    for a, b in ((p, p2), (m, m2), (v, v2), (t, t2)):
+        assert torch.equal(a, b)
+    assert torch.equal(p, theta[None].expand(K, P)) and not m.any() and not t.any()
+
+
+@pytest.mark.parametrize("dp", [False, True])
+def test_fedavg_launch_packs_round_metrics(cuda, dp):
+    """The FedAvg reduce with the metric pack fused into its last block == reduce + round_pack (bitwise)."""
+    from qfedx_amd.ops import fedavg_hip
+    from qfedx_amd.ops._ext import ext
+    K, P, n = 5, 300, 24
+    g = torch.Generator().manual_seed(2)
+    tk = (torch.randn(K, P, generator=g) * 2).to(cuda)
+    tg = torch.randn(P, generator=g).to(cuda)
+    w = (torch.rand(K, generator=g).double() + 0.5).to(cuda)
+    mask = (torch.arange(P) < 200).to(torch.uint8).to(cuda)
+    mets = [torch.rand(n, generator=g).to(cuda) for _ in range(4)]
+    keys = torch.randint(0, 2 ** 31 - 1, (K, 2), generator=g, dtype=torch.int64).to(torch.int32).to(cuda)
+    bufs = []
+    for fused in (True, False):
+        buf = torch.full((P + 5,), 123, dtype=torch.int64, device=cuda)
+        fedavg_hip.fused_local_reduce(tk, tg, w, mask, list(range(K)), 3, 9, True, dp, 0.8, 1.1, out=buf[: P + 1],
+                                      keys=keys, pack=(buf, *mets) if fused else None)
+        if not fused:
+            ext().round_pack(buf, P, *mets)
+        bufs.append(buf.cpu())
+    assert torch.equal(bufs[0], bufs[1])
+
+
 def test_round_init_and_counter_pingpong(cuda):
     from qfedx_amd.fl.optim import BatchedOptimizer
     K, P = 5, 37
