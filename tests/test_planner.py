@@ -84,3 +84,41 @@ def test_jit_codegen_emits_straight_line_kernel():
     blob = C.plan(torch.from_numpy(ops), torch.from_numpy(coef), 12, 16, 12, spec.readout, spec.n_theta, 2, 0)
     src = C.jit_source(blob, 0, True)
     assert "qfx_jit_pass" in src and "adj_step<R," in src and "switch" not in src
+
+
+def _jit_worker(cache, n_layers, q):
+    import torch as _t
+    from qfedx_amd.ops._ext import ext as _ext
+    from qfedx_amd.ops.statevec_hip import ARCH, CSRC
+    spec = VQCSpec(n_qubits=8, n_layers=n_layers, n_classes=2)
+    ops, coef = spec.program()
+    Cx = _ext()
+    blob = Cx.plan(_t.from_numpy(ops), _t.from_numpy(coef), 8, 16, 8, spec.readout, spec.n_theta, 2, 0)
+    q.put(Cx.jit_prepare(blob, 0, False, cache, CSRC, ARCH, False)[1])
+
+
+def test_jit_cache_concurrent_writers(tmp_path):
+    """Ranks of a node share the code-object cache: several processes compiling the same pass at once leave one
+    complete entry (per-process temp files renamed into place), byte-identical to a single process's compile."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    shared, alone = str(tmp_path / "shared"), str(tmp_path / "alone")
+    procs = [ctx.Process(target=_jit_worker, args=(shared, 1, q)) for _ in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+        assert p.exitcode == 0
+    keys = {q.get(timeout=10) for _ in procs}
+    p = ctx.Process(target=_jit_worker, args=(alone, 1, q))
+    p.start()
+    p.join(300)
+    assert p.exitcode == 0 and q.get(timeout=10) in keys and len(keys) == 1
+    import os
+    names = sorted(os.listdir(shared))
+    assert not [f for f in names if f.endswith(".tmp")], names
+    key = keys.pop()
+    a = open(os.path.join(shared, key + ".co"), "rb").read()
+    b = open(os.path.join(alone, key + ".co"), "rb").read()
+    assert len(a) > 0 and a == b
