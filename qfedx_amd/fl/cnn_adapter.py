@@ -18,6 +18,9 @@ from ..utils.device import PackedUpload
 from .trainer import BatchPlan, ShardStore
 
 
+UPFRONT_GATHER_BYTES = 1 << 30   # round prologue gathers every step up front below this image-buffer size
+
+
 class CNNClientTrainer:
     def __init__(self, num_classes: int, train_cfg, device, backend: str = "torch"):
         self.C = num_classes
@@ -71,24 +74,35 @@ class CNNClientTrainer:
         params = torch.empty(K, P, dtype=torch.float32, device=self.device)
         opt = BatchedOptimizer(cfg.optimizer if cfg.optimizer != "spsa" else "sgd", (K, P), self.device,
                                cfg.learning_rate, cfg.momentum, backend=self.backend, zero_init=False)
-        opt.init_round(params, theta_g.to(self.device).float())
         S = plan.max_steps
         loss_all = torch.empty(S, K, dtype=torch.float32, device=self.device)
         correct_all = torch.empty(S, K, dtype=torch.float32, device=self.device)
         fused = self.backend == "hip" and store.X.is_cuda
+        upfront = False
         if fused:   # minibatches gathered straight from the device store by slot (no per-round shard copy)
             from ..ops._ext import ext
             img = tuple(store.X.shape[2:])
             Xf = store.X.view(store.X.shape[0], store.X.shape[1], -1)
             B = plan.B
-            xbuf = torch.empty(K, B, Xf.shape[-1], dtype=torch.float32, device=self.device)
-            ybuf = torch.empty(K * B, dtype=torch.int64, device=self.device)
+            # one prologue launch (client rows + optimizer state, every step's minibatch) while the round's
+            # images fit a modest buffer; long rounds gather per step
+            upfront = S * K * B * Xf.shape[-1] * 4 <= UPFRONT_GATHER_BYTES
+            xbuf = torch.empty(S if upfront else 1, K, B, Xf.shape[-1], dtype=torch.float32, device=self.device)
+            ybuf = torch.empty((S if upfront else 1) * K * B, dtype=torch.int64, device=self.device)
         else:
             rows = dv["lid"][:, None]
+        if upfront:
+            m, v, t = opt.init_state()
+            ext().round_prologue(theta_g.to(self.device).float().contiguous(), params, m, v, t, Xf, store.y,
+                                 dv["lid"], dv["idx"].contiguous(), 2, 1.0, xbuf, ybuf)
+        else:
+            opt.init_round(params, theta_g.to(self.device).float())
         for s in range(S):
-            if fused:
-                ext().batch_gather(Xf, store.y, dv["lid"], dv["idx"][s], 2, 1.0, xbuf, ybuf)
-                xb, yb = xbuf.view(K, B, *img), ybuf.view(K, B)
+            if upfront:
+                xb, yb = xbuf[s].view(K, B, *img), ybuf.view(S, K, B)[s]
+            elif fused:
+                ext().batch_gather(Xf, store.y, dv["lid"], dv["idx"][s], 2, 1.0, xbuf[0], ybuf)
+                xb, yb = xbuf[0].view(K, B, *img), ybuf.view(K, B)
             else:
                 xb = store.X[rows, dv["idx"][s]]
                 yb = store.y[rows, dv["idx"][s]]
