@@ -657,7 +657,9 @@ __global__ void cnn_reduce(const float* __restrict__ part, int G, float* __restr
 }
 
 // --------------------------------------------------------------------------------------------
-// fc head, one block per client: a = ReLU(h1) * dropout; logits = W a + b; weighted CE; backward:
+// fc head, one block per client: h1 = pool2 W1^T (the fc1 GEMM, no bias) + b1 (added here: a broadcast bias in
+// the GEMM cost torch a separate expand-copy launch per step); a = ReLU(h1) * dropout; logits = W a + b; weighted
+// CE; backward:
 // dh1 = (W^T dlogits) * dropout * [h1 > 0]; fc2 grads.  Samples go through LDS in chunks of HB; every
 // stage spreads (sample, class) or (sample, unit) pairs over the block, and all sums over samples run in
 // a fixed order (deterministic).
@@ -678,6 +680,7 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
                                                 float* __restrict__ correct, float* __restrict__ grad) {
   __shared__ float Ws[CMAXC * HID];
   __shared__ float bs[CMAXC];
+  __shared__ float b1s[HID];               // fc1 bias
   __shared__ float hv[HB][HID + 1];        // h1, then dh1 (fc1 bias gradient)
   __shared__ float act[HB][HID + 1];       // ReLU(h1) * dropout of the chunk
   __shared__ float dl[HB][CMAXC + 1];      // logits, then weighted dlogits
@@ -686,6 +689,7 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
   const float* prow = params + (size_t)k * P;
   for (int e = tid; e < C * HID; e += 256) Ws[e] = prow[off_w + e];
   if (tid < C) bs[tid] = prow[off_b + tid];
+  if (tid < HID) b1s[tid] = prow[off_b1 + tid];
   float gacc[HG];
 #pragma unroll
   for (int m = 0; m < HG; ++m) gacc[m] = 0.f;
@@ -696,7 +700,7 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
     __syncthreads();   // previous chunk fully consumed (and Ws / bs staged)
     for (int e = tid; e < nb * HID; e += 256) {
       const int b = e / HID, j = e - b * HID;
-      const float h = h1[sb * HID + e];
+      const float h = h1[sb * HID + e] + b1s[j];
       hv[b][j] = h;
       const float mk = mask ? mask[sb * HID + e]
                             : (philox_uniform_at((uint64_t)(b0 * HID + e), (uint32_t)dkeys[2 * k],

@@ -79,8 +79,8 @@ class HipTinyCNN:
         K, B = xb.shape[:2]
         S = K * B
         Xf, pool1, am1, pool2, am2 = self.conv_forward(params, xb)
-        h1, w1 = self._fc1(params, pool2, K, B)
-        h1 = h1.contiguous()
+        w1 = params[:, self.fc1w: self.fc1b].view(K, 64, 1568)
+        h1 = torch.bmm(pool2.view(K, B, 1568), w1.transpose(1, 2))    # the head adds the fc1 bias
         grad = torch.empty(K, self.P, dtype=torch.float32, device=self.device)   # every entry is written below
         dh1 = self._buf("dh1", (K, B, 64))
         dlog = self._buf("dlog", (S, 16))
