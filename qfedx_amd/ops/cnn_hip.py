@@ -3,9 +3,9 @@
 One local step of K clients x B samples:
   1. ``cnn_forward``  - fused conv1/conv2 + bias + ReLU + 2x2 max-pool (fp32 MFMA implicit GEMM, per
                         client weights), writes pooled maps + argmax codes
-  2. fc1              - ``baddbmm`` over the client batch (plain batched GEMM -> hipBLASLt/rocBLAS)
+  2. fc1              - ``bmm`` over the client batch (plain batched GEMM -> hipBLASLt/rocBLAS; bias in the head)
   3. ``cnn_head``     - fc1 bias + ReLU + keyed dropout + fc2 + weighted CE, dlogits, fc2 grads, dL/dh1, fc1 bias grad
-  4. fc1 backward     - two batched GEMMs (weight grad, dL/dpool2)
+  4. fc1 backward     - ``cnn_fc1_wgrad`` (weight grad into the gradient rows) + one batched GEMM (dL/dpool2)
   5. ``cnn_backward`` - unpool + ReLU masks, conv2 weight/input grads, conv1 weight grads (MFMA),
                         deterministic fixed-order reduction into the flat [K, P] gradient
 No autograd graph, no per-client Python loop; every buffer is sized [K, ...] once per shape.
