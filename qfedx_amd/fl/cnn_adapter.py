@@ -15,10 +15,7 @@ import torch.nn.functional as F
 from ..models import tinycnn as tc
 from .optim import BatchedOptimizer
 from ..utils.device import PackedUpload
-from .trainer import BatchPlan, ShardStore
-
-
-UPFRONT_GATHER_BYTES = 1 << 30   # round prologue gathers every step up front below this image-buffer size
+from .trainer import UPFRONT_GATHER_BYTES, BatchPlan, ShardStore
 
 
 class CNNClientTrainer:

@@ -22,6 +22,8 @@ from ..utils.device import PackedUpload, h2d
 from ..utils.seeding import _philox4x32_np, philox4x32, philox_key
 from .optim import BatchedOptimizer
 
+UPFRONT_GATHER_BYTES = 1 << 30   # round prologue gathers every step up front below this input-buffer size
+
 
 class ShardStore:
     """Device-resident padded shards: X [K, Nmax, F], y [K, Nmax], counts [K]."""
@@ -219,8 +221,9 @@ class VQCClientTrainer:
         BT = idx_d.shape[-1] * T
         fused = self.backend == "hip" and X.is_cuda
         # one prologue launch: client rows + optimizer state initialised and every step's minibatch gathered
-        # and encoded up front (trajectory replicas, T > 1, gather per step)
-        upfront = fused and T == 1
+        # and encoded up front (trajectory replicas, T > 1, and rounds whose inputs pass UPFRONT_GATHER_BYTES
+        # gather per step)
+        upfront = fused and T == 1 and steps * K * BT * X.shape[-1] * 4 <= UPFRONT_GATHER_BYTES
         if fused:
             from ..ops._ext import ext
             mode = 2 if spec.amplitude else (1 if spec.feature_scale == "minmax" else 0)

@@ -136,6 +136,22 @@ def test_graph_round_matches_eager(cuda, fraction, sampling, dp):
     assert torch.equal(outs[0]["params"], outs[1]["params"])
 
 
+def test_upfront_and_per_step_gathers_give_the_same_run(cuda, monkeypatch):
+    """Rounds whose minibatches are gathered by the prologue launch == rounds gathering per step (the path taken
+    past UPFRONT_GATHER_BYTES), bitwise, with several local steps per round."""
+    from tests.test_fl import small_cfg
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.parallel.dist import init_distributed
+    import qfedx_amd.fl.trainer as tr
+    outs = []
+    for cap in (tr.UPFRONT_GATHER_BYTES, 0):
+        monkeypatch.setattr(tr, "UPFRONT_GATHER_BYTES", cap)
+        cfg = small_cfg(num_rounds=3, n_qubits=8, device="cuda", backend="hip", num_clients=5, local_epochs=2)
+        dev = torch.device("cuda", 0)
+        outs.append(run_experiment(cfg, world=init_distributed(dev), device=dev, backend="hip"))
+    assert torch.equal(outs[0]["params"], outs[1]["params"])
+
+
 def test_hip_federated_run_matches_cpu(cuda):
     from tests.test_fl import small_cfg
     from qfedx_amd.api import run_experiment
