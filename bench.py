@@ -46,6 +46,7 @@ def timed_rounds(cfg, device, backend, world, warmup: int, steps: int, counts: l
     for r in range(warmup):
         runner.run_round(r, sync=False)
     sync()
+    runner.timer.reset()                    # per-phase HIP-event times of the timed rounds only
     t0 = time.perf_counter()
     for r in range(warmup, warmup + steps):
         rec = runner.run_round(r, sync=False)
@@ -54,6 +55,42 @@ def timed_rounds(cfg, device, backend, world, warmup: int, steps: int, counts: l
     sync()
     dt = time.perf_counter() - t0
     return runner, max_over_ranks(dt, world)
+
+
+def phase_ms(runner, world, steps: int) -> dict:
+    """Per-round milliseconds of the runner's phases over the timed rounds (HIP events; max over ranks):
+    ``local_train_ms`` = the round graph (every local step + the fused FedAvg reduce), ``comm_ms`` = the
+    all-reduce + finalize/apply."""
+    from qfedx_amd.parallel.dist import max_over_ranks
+    tot = runner.timer.resolve()
+    return {f"{k}_ms": round(max_over_ranks(v / max(steps, 1), world), 4) for k, v in sorted(tot.items())}
+
+
+def precision_check(runner, batch: int) -> dict:
+    """Accuracy evidence for the fp16-state MFMA engine at the bench shape: ONE untimed adjoint VJP of this
+    rank's clients (first ``batch`` samples of each shard, the current global params) on the MFMA engine and
+    on the fp32 VALU engine (ahead-of-time interpreter kernels, no JIT), same inputs and readout weights.
+    Returns the max abs differences of <Z> and of the parameter gradient, and the gradient's max magnitude."""
+    import torch
+    from qfedx_amd.ops.statevec_hip import HipProgram
+    eng = runner.adapter.engine
+    spec = runner.adapter.spec
+    if getattr(eng, "hip", None) is None or not hasattr(eng.hip, "vjp") or isinstance(eng.hip, HipProgram):
+        return {}
+    store = runner.store
+    xang = spec.encode_features(store.X[:, :batch].float())
+    K, B = xang.shape[:2]
+    th = runner.params[: spec.n_theta].float()[None].expand(K, -1).contiguous()
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    w = (torch.randn(K * B, spec.n_classes, generator=g) / B).to(xang.device)
+    z_m, g_m = eng.hip.vjp(xang, th, w)
+    ref = HipProgram(eng.ops, eng.coef, spec.n_qubits, spec.readout, xang.device, n_theta=spec.n_theta,
+                     state_dtype="fp32", jit=False, x_width=spec.x_width)
+    z_r, g_r = ref.vjp(xang, th, w)
+    torch.cuda.synchronize()
+    return {"max_abs_err_expz": float((z_m - z_r).abs().max()), "max_abs_err_grad": float((g_m - g_r).abs().max()),
+            "max_abs_grad": float(g_r.abs().max()), "precision_ref": "fp32 VALU engine (interpreter kernels)",
+            "precision_samples": int(K * B)}
 
 
 def make_config(args):
@@ -126,6 +163,9 @@ def main():
                          "several ranks share one GPU in tests")
     ap.add_argument("--engine", default="mfma", choices=["mfma", "valu"],
                     help="mfma: fp16-state MFMA group-unitary engine (ops/hea_mfma.py); valu: fp32 pass engine")
+    ap.add_argument("--precision-check", type=int, default=1,
+                    help="after timing, one untimed VJP on the fp32 VALU engine at the bench shape: report the "
+                         "MFMA engine's max abs <Z> / gradient differences (0 = skip)")
     args = ap.parse_args()
     relaunch_if_needed(args.gpus)
 
@@ -136,7 +176,9 @@ def main():
     cfg = make_config(args)
     device, backend, world = setup(cfg)
     runner, dt = timed_rounds(cfg, device, backend, world, args.warmup, args.steps)
+    phases = phase_ms(runner, world, args.steps)
     ev = runner.evaluate()
+    prec = precision_check(runner, args.batch) if (args.precision_check and device.type == "cuda") else {}
     local_steps_total = args.clients * args.local_steps * args.steps
     value = local_steps_total / dt
     rounds_per_s = args.steps / dt
@@ -162,6 +204,9 @@ def main():
             "samples_per_sec": round(value * args.batch, 1),
             "backend": backend,
             "test_acc_after": round(ev["test_acc"], 4),
+            "dist_backend": world.backend,
+            **phases,
+            **prec,
             "config": {
                 "model": f"vqc-{args.qubits}q-{args.layers}L-hea-cnot-chain",
                 "global_batch": args.clients * args.batch,

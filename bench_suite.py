@@ -37,6 +37,12 @@ SUITE = {
                   "client local-steps/sec (16-qubit VQC x 64 clients federated rounds)", None),
     "vqc16q_64_mfma": ("configs/headline_16q_64clients.yaml", ["model.state_dtype=mfma"],
                        "client local-steps/sec (16-qubit VQC x 64 clients, fp16 MFMA engine)", None),
+    "vqc16q_64_mfma_secagg": ("configs/headline_16q_64clients.yaml",
+                              ["model.state_dtype=mfma", "privacy.secure_agg=true"],
+                              "client local-steps/sec (16-qubit VQC x 64 clients, pairwise-mask SecAgg on the device)",
+                              None),
+    "cfed128_secagg": ("configs/baseline4_cfed_128clients.yaml", ["train.local_steps=1", "privacy.secure_agg=true"],
+                       "client local-steps/sec (CFed TinyCNN x 128 clients, batch 32, SecAgg on the device)", 258.0),
     "vqc20q_dp64_mfma": ("configs/baseline3_20q_dp_64clients.yaml", ["model.state_dtype=mfma"],
                          "client local-steps/sec (20-qubit VQC x 64 non-IID clients, DP, fp16 MFMA engine)", None),
     "vqc48q_mps64": ("configs/mps_48q_64clients.yaml", [],
@@ -99,6 +105,7 @@ def main():
                        "seq_len": cfg.model.n_qubits if kind == "vqc" else 784,
                        "parallelism": f"client-parallel dp{world.world_size}", "n_clients": cfg.data.num_clients,
                        "grad": t.grad_method, "optimizer": t.optimizer, "dp": cfg.privacy.dp,
+                       "secure_agg": cfg.privacy.secure_agg,
                        "shots": cfg.noise.shots},
         }
         print(json.dumps(rec), flush=True)

@@ -68,6 +68,7 @@ def build(verbose: bool = False, force: bool = False, debug=None) -> str:
     BUILD, EXT_NAME, dbg = _mode(debug)
     os.makedirs(BUILD, exist_ok=True)
     checks = ["-DQFX_DEVICE_CHECKS=1"] if dbg else []
+    extra = os.environ.get("QFEDX_EXTRA_HIPFLAGS", "").split()   # e.g. -DQFX_HEA_ABLATE=1 (timing builds)
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     hips = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     cpps = sorted(glob.glob(os.path.join(CSRC, "*.cpp")))
@@ -85,11 +86,11 @@ def build(verbose: bool = False, force: bool = False, debug=None) -> str:
     hh = _hash(headers)
     for src in hips:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-        key = _hash([src]) + hh + ARCH
+        key = _hash([src]) + hh + ARCH + " ".join(extra)
         objs.append(obj)
         if stamps.get(obj) != key or not os.path.exists(obj):
             cmd = ["hipcc", "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fno-gpu-rdc",
-                   "-munsafe-fp-atomics", *checks, "-I", CSRC, src, "-o", obj]
+                   "-munsafe-fp-atomics", *checks, *extra, "-I", CSRC, src, "-o", obj]
             jobs.append((obj, key, cmd))
     for src in cpps:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")

@@ -48,7 +48,8 @@ class ModelConfig:
     init_std: float = 0.1
     state_dtype: str = "auto"           # auto (mfma when eligible on HIP, else fp32) | fp32 | bf16 (VALU pass
                                         # engine storage) | mfma (fp16 MFMA engine, hardware-efficient ansatz)
-    simulator: str = "statevector"      # statevector | mps (tensor network past statevector memory)
+    simulator: str = "statevector"      # statevector | mps (tensor network past statevector memory) | density
+                                        # (exact Kraus channels, <= 10 qubits; auto for noise.kind=amplitude)
     mps_chi: int = 64                   # MPS bond-dimension cap (exact while the circuit's bound fits)
 
 
@@ -92,7 +93,7 @@ class PrivacyConfig:
 @dataclass
 class NoiseConfig:
     """Quantum noise model (ROADMAP.md:64-73)."""
-    kind: str = "none"                  # none | depolarizing | amplitude
+    kind: str = "none"                  # none | depolarizing | amplitude (exact, density simulator) | amplitude_twirl
     p: float = 0.0                      # depolarizing probability per gate
     gamma: float = 0.0                  # amplitude damping per gate
     readout_p01: float = 0.0            # P(read 1 | 0)

@@ -65,7 +65,8 @@ int qfx_launch_grad_reduce(const float* slab, int tps, int spc, int K, int G, co
 int qfx_grad_split(int tps, int spc);
 int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct, const float* nvalid,
                           const float* act, int n, hipStream_t st);
-int qfx_launch_round_apply(const long long* buf, int P, float* theta, double lr, double* out, hipStream_t st);
+int qfx_launch_round_apply(long long* buf, int P, float* theta, double lr, double* out, int bits,
+                           double ring_scale, hipStream_t st);
 int qfx_fedavg_norm_scratch(int K, int P);
 int qfx_launch_adam(float* p, const float* g, float* m, float* v, const float* t_in, float* t_out,
                     const float* active, int K, int P, float lr, float b1, float b2, float eps, hipStream_t st);
@@ -84,7 +85,9 @@ int qfx_launch_batch_gather(const float* X, const long long* Y, const long long*
 int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned char* angle_mask,
                       const double* weights, double* norms, const uint32_t* keys, int K, int P, int wrap, int dp,
                       float clip, float sigma, long long* out, long long* pack_buf, const float* loss,
-                      const float* correct, const float* nvalid, const float* act, int n_metrics, hipStream_t st);
+                      const float* correct, const float* nvalid, const float* act, int n_metrics, long long* sat,
+                      const uint32_t* sa_seeds, const int* sa_sign, const int* sa_round, int sa_n, double sa_scale,
+                      int sa_bits, hipStream_t st);
 }
 
 namespace qfx_runtime {
@@ -227,12 +230,15 @@ void round_pack(torch::Tensor buf, int64_t P, torch::Tensor loss, torch::Tensor 
         "qfx_round_pack");
 }
 
-void round_apply(torch::Tensor buf, int64_t P, torch::Tensor theta, double lr, torch::Tensor out) {
+// bits > 0: the update / weight entries are SecAgg ring elements (Z_2^bits, scale ring_scale)
+void round_apply(torch::Tensor buf, int64_t P, torch::Tensor theta, double lr, torch::Tensor out, int64_t bits,
+                 double ring_scale) {
   need(buf, torch::kInt64, "buf");
   need(theta, torch::kFloat32, "theta");
   need(out, torch::kFloat64, "out");
-  if (buf.numel() < P + 5 || theta.numel() < P || out.numel() < 5) throw std::invalid_argument("round_apply: sizes");
-  check(qfx_launch_round_apply(ptr<long long>(buf), (int)P, ptr<float>(theta), lr, ptr<double>(out), cur_stream()),
+  if (buf.numel() < P + 6 || theta.numel() < P || out.numel() < 6) throw std::invalid_argument("round_apply: sizes");
+  check(qfx_launch_round_apply(ptr<long long>(buf), (int)P, ptr<float>(theta), lr, ptr<double>(out), (int)bits,
+                               ring_scale, cur_stream()),
         "qfx_round_apply");
 }
 
@@ -379,13 +385,18 @@ void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<tor
         "qfx_round_prologue");
 }
 
-// pack_buf (optional, the round's [P + 5] all-reduce buffer): one more block of the same launch packs the round
-// metrics (loss, correct, nvalid, act: float32 [n]) into its tail, as round_pack does
+// pack_buf (optional, the round's [P + 6] all-reduce buffer): one more block of the same launch packs the round
+// metrics (loss, correct, nvalid, act: float32 [n]) into its tail, as round_pack does.  sat: int64 [1] counter
+// of saturated fixed-point terms (with pack_buf, it must be pack_buf[P + 5])
 void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_mask, torch::Tensor weights,
             torch::Tensor norms, torch::Tensor keys, bool wrap, bool dp, double clip, double sigma,
             torch::Tensor out, torch::Tensor pack_buf, torch::Tensor loss, torch::Tensor correct,
-            torch::Tensor nvalid, torch::Tensor act) {
+            torch::Tensor nvalid, torch::Tensor act, torch::Tensor sat, c10::optional<torch::Tensor> sa_seeds,
+            c10::optional<torch::Tensor> sa_sign, c10::optional<torch::Tensor> sa_round, double sa_scale,
+            int64_t sa_bits) {
   need(theta_k, torch::kFloat32, "theta_k");
+  need(sat, torch::kInt64, "sat");
+  if (sat.numel() < 1) throw std::invalid_argument("fedavg: sat counter missing");
   need(theta_g, torch::kFloat32, "theta_g");
   need(weights, torch::kFloat64, "weights");
   need(norms, torch::kFloat64, "norms");
@@ -400,16 +411,34 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
     need(pack_buf, torch::kInt64, "pack_buf");
     for (auto* x : {&loss, &correct, &nvalid, &act}) need(*x, torch::kFloat32, "fedavg metric");
     n = loss.numel();
-    if (pack_buf.numel() < P + 5 || correct.numel() < n || nvalid.numel() < n || act.numel() < n)
+    if (pack_buf.numel() < P + 6 || correct.numel() < n || nvalid.numel() < n || act.numel() < n)
       throw std::invalid_argument("fedavg: metric pack sizes");
     if (out.data_ptr() != pack_buf.data_ptr()) throw std::invalid_argument("fedavg: out must be the head of pack_buf");
+    if (sat.data_ptr() != (void*)(ptr<long long>(pack_buf) + P + 5))
+      throw std::invalid_argument("fedavg: sat must be pack_buf[P + 5]");
+  }
+  // SecAgg: pair-seed key words [K, N, 2] int32, signs [K, N] int32, round [1] int32 (all device tensors)
+  const bool sa = sa_seeds.has_value() && sa_seeds->defined();
+  int sa_n = 0;
+  if (sa) {
+    if (!sa_sign.has_value() || !sa_round.has_value()) throw std::invalid_argument("fedavg: SecAgg needs seeds, signs, round");
+    need(*sa_seeds, torch::kInt32, "sa_seeds");
+    need(*sa_sign, torch::kInt32, "sa_sign");
+    need(*sa_round, torch::kInt32, "sa_round");
+    if (sa_sign->dim() != 2 || sa_sign->size(0) < K) throw std::invalid_argument("fedavg: sa_sign must be [K, N]");
+    sa_n = (int)sa_sign->size(1);
+    if (sa_seeds->numel() < (int64_t)K * sa_n * 2 || sa_round->numel() < 1)
+      throw std::invalid_argument("fedavg: SecAgg table sizes");
+    if (sa_bits < 2 || sa_bits > 62 || !(sa_scale > 0)) throw std::invalid_argument("fedavg: SecAgg bits / scale");
   }
   check(qfx_launch_fedavg(ptr<float>(theta_k), ptr<float>(theta_g), ptr<unsigned char>(angle_mask),
                           ptr<double>(weights), ptr<double>(norms), ptr<uint32_t>(keys), K, P, wrap ? 1 : 0,
                           dp ? 1 : 0, (float)clip, (float)sigma, ptr<long long>(out),
                           pack ? ptr<long long>(pack_buf) : nullptr, pack ? ptr<float>(loss) : nullptr,
                           pack ? ptr<float>(correct) : nullptr, pack ? ptr<float>(nvalid) : nullptr,
-                          pack ? ptr<float>(act) : nullptr, (int)n, cur_stream()),
+                          pack ? ptr<float>(act) : nullptr, (int)n, ptr<long long>(sat),
+                          sa ? ptr<uint32_t>(*sa_seeds) : nullptr, sa ? ptr<int>(*sa_sign) : nullptr,
+                          sa ? ptr<int>(*sa_round) : nullptr, sa_n, sa_scale, (int)sa_bits, cur_stream()),
         "qfx_fedavg");
 }
 
@@ -459,6 +488,41 @@ void jit_launch(int64_t handle, torch::Tensor blob, int64_t pass_off, torch::Ten
 }  // namespace
 
 void register_cnn(pybind11::module& m);
+
+extern "C" {
+int qfx_dm_gate_bytes();
+int qfx_dm_run(const void* gates, int G, int n, const float* rows, int W, long S, const int* readout, int C,
+               const float* superop, void* scratch, float* expz, hipStream_t st);
+int qfx_dm_lds_qubits();
+}
+
+// Exact density-matrix run (density.hip): gates = lowered program bytes (ops/density.py), rows [S, W] slot values,
+// superop [32] float (4 x 4 complex noise channel) or empty, scratch [S, 4^n] complex64 (n > LDS qubits), expz [S, C]
+void dm_run(torch::Tensor gates, int64_t G, int64_t n, torch::Tensor rows, torch::Tensor readout, torch::Tensor superop,
+            torch::Tensor scratch, torch::Tensor expz) {
+  need(gates, torch::kInt32, "gates");
+  need(rows, torch::kFloat32, "rows");
+  need(readout, torch::kInt32, "readout");
+  need(expz, torch::kFloat32, "expz");
+  if (gates.numel() * 4 < G * qfx_dm_gate_bytes()) throw std::invalid_argument("dm_run: gate table too small");
+  if (rows.dim() != 2) throw std::invalid_argument("dm_run: rows must be [S, W]");
+  const int64_t S = rows.size(0), C = readout.numel();
+  if (expz.numel() < S * C) throw std::invalid_argument("dm_run: expz too small");
+  const bool noisy = superop.defined() && superop.numel() > 0;
+  if (noisy) {
+    need(superop, torch::kFloat32, "superop");
+    if (superop.numel() != 32) throw std::invalid_argument("dm_run: superop must be 4 x 4 complex");
+  }
+  const bool global = n > qfx_dm_lds_qubits();
+  if (global) {
+    need(scratch, torch::kComplexFloat, "scratch");
+    if (scratch.numel() < S * (int64_t(1) << (2 * n))) throw std::invalid_argument("dm_run: scratch too small");
+  }
+  check(qfx_dm_run(gates.data_ptr(), (int)G, (int)n, ptr<float>(rows), (int)rows.size(1), (long)S, ptr<int>(readout),
+                   (int)C, noisy ? ptr<float>(superop) : nullptr, global ? scratch.data_ptr() : nullptr,
+                   ptr<float>(expz), cur_stream()),
+        "qfx_dm_run");
+}
 void register_hea(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -491,5 +555,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("jit_source", &jit_source, py::arg("blob"), py::arg("p"), py::arg("adjoint"), py::arg("bf16") = false);
   m.def("jit_launch", &jit_launch);
   register_cnn(m);
+  m.def("dm_run", &dm_run, "exact density-matrix simulation of a lowered noisy program (one workgroup per row)");
+  m.def("dm_gate_bytes", []() { return qfx_dm_gate_bytes(); });
+  m.def("dm_lds_qubits", []() { return qfx_dm_lds_qubits(); });
   register_hea(m);
 }

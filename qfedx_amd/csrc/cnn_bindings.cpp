@@ -21,6 +21,14 @@ int qfx_cnn_head(const float* h1, int off_b1, const float* mask, const long long
 int qfx_cnn_partial_size();
 int qfx_cnn_fc1_wgrad(const float* dh1, const float* pool2, int K, int B, float* grad, int P, int off_w1, hipStream_t st);
 int qfx_cnn_bwd_groups(int K, int B);
+int qfx_cnn_fc1_forward(const float* pool2, const float* params, int P, int off_w1, int K, int B, float* h1p,
+                        hipStream_t st);
+int qfx_cnn_fc1_dgrad(const float* dh1, const float* params, int P, int off_w1, int K, int B, float* dP2,
+                      hipStream_t st);
+int qfx_cnn_eval_head(const float* h1p, const float* params, int P, int off_b1, int off_w, int off_b, int C, int K,
+                      int B, const long long* y, float* logits, double* stats, hipStream_t st);
+int qfx_cnn_fc1_splits();
+int qfx_cnn_eval_blocks(int B);
 }
 
 namespace {
@@ -76,7 +84,7 @@ void backward(torch::Tensor X, torch::Tensor params, int64_t K, int64_t B, std::
         "cnn_backward");
 }
 
-// h1: fc1 pre-activations [K*B, 64]; off_b1: fc1 bias offset in the parameter row (its gradient is written here).
+// h1: the fc1 forward's split partial sums [K, FC_KS, B, 64] (cnn_fc1_forward); off_b1: fc1 bias offset in the parameter row (its gradient is written here).
 // Dropout: ``mask`` [K*B, 64], or (mask undefined) per-client Philox keys ``dkeys`` [K, 2] (int64 words) whose
 // uniforms of stream ``drop_stream`` are kept (x drop_scale) where u >= drop_p.
 void head(torch::Tensor h1, int64_t off_b1, c10::optional<torch::Tensor> mask, c10::optional<torch::Tensor> dkeys,
@@ -87,7 +95,7 @@ void head(torch::Tensor h1, int64_t off_b1, c10::optional<torch::Tensor> mask, c
   const int P = (int)params.size(1);
   const bool hm = mask.has_value() && mask->defined(), hu = dkeys.has_value() && dkeys->defined();
   if (hm == hu) throw std::invalid_argument("cnn_head: pass exactly one of mask / dkeys");
-  check(qfx_cnn_head(dptr<float>(h1, torch::kFloat32, "h1", S * 64), (int)off_b1,
+  check(qfx_cnn_head(dptr<float>(h1, torch::kFloat32, "h1", S * 64 * qfx_cnn_fc1_splits()), (int)off_b1,
                      hm ? dptr<float>(*mask, torch::kFloat32, "mask", S * 64) : nullptr,
                      hu ? dptr<long long>(*dkeys, torch::kInt64, "dkeys", 2 * K) : nullptr, (unsigned)drop_stream,
                      (float)drop_p, (float)drop_scale,
@@ -108,6 +116,45 @@ void fc1_wgrad(torch::Tensor dh1, torch::Tensor pool2, int64_t K, int64_t B, tor
         "cnn_fc1_wgrad");
 }
 
+void check_w1(const torch::Tensor& params, int64_t K, int64_t off_w1) {
+  if (params.dim() != 2 || params.size(0) < K || off_w1 < 0 || off_w1 + 64 * POOL2 > params.size(1))
+    throw std::invalid_argument("cnn fc1: params [K, P] / fc1 weight offset");
+}
+
+// h1p [K, FC_KS, B, 64]: per input-chunk partial sums of pool2 W1^T (no bias), summed in fixed order by the heads
+void fc1_forward(torch::Tensor pool2, torch::Tensor params, int64_t off_w1, int64_t K, int64_t B, torch::Tensor h1p) {
+  check_w1(params, K, off_w1);
+  const int P = (int)params.size(1);
+  check(qfx_cnn_fc1_forward(dptr<float>(pool2, torch::kFloat32, "pool2", K * B * POOL2),
+                            dptr<float>(params, torch::kFloat32, "params", K * P), P, (int)off_w1, (int)K, (int)B,
+                            dptr<float>(h1p, torch::kFloat32, "h1p", K * B * 64 * qfx_cnn_fc1_splits()), stream()),
+        "cnn_fc1_forward");
+}
+
+void fc1_dgrad(torch::Tensor dh1, torch::Tensor params, int64_t off_w1, int64_t K, int64_t B, torch::Tensor dP2) {
+  check_w1(params, K, off_w1);
+  const int P = (int)params.size(1);
+  check(qfx_cnn_fc1_dgrad(dptr<float>(dh1, torch::kFloat32, "dh1", K * B * 64),
+                          dptr<float>(params, torch::kFloat32, "params", K * P), P, (int)off_w1, (int)K, (int)B,
+                          dptr<float>(dP2, torch::kFloat32, "dP2", K * B * POOL2), stream()),
+        "cnn_fc1_dgrad");
+}
+
+// logits [K*B, C]; with labels y [K*B] (int64), stats [K * eval_blocks(B), 2] float64 = per-block (CE sum, hits)
+void eval_head(torch::Tensor h1p, torch::Tensor params, int64_t off_b1, int64_t off_w, int64_t off_b, int64_t C,
+               int64_t K, int64_t B, c10::optional<torch::Tensor> y, torch::Tensor logits, torch::Tensor stats) {
+  const int P = (int)params.size(1);
+  const bool hy = y.has_value() && y->defined();
+  check(qfx_cnn_eval_head(dptr<float>(h1p, torch::kFloat32, "h1p", K * B * 64 * qfx_cnn_fc1_splits()),
+                          dptr<float>(params, torch::kFloat32, "params", K * P), P, (int)off_b1, (int)off_w, (int)off_b,
+                          (int)C, (int)K, (int)B, hy ? dptr<long long>(*y, torch::kInt64, "y", K * B) : nullptr,
+                          dptr<float>(logits, torch::kFloat32, "logits", K * B * C),
+                          hy ? dptr<double>(stats, torch::kFloat64, "stats", 2 * K * qfx_cnn_eval_blocks((int)B))
+                             : nullptr,
+                          stream()),
+        "cnn_eval_head");
+}
+
 }  // namespace
 
 void register_cnn(pybind11::module& m) {
@@ -118,4 +165,9 @@ void register_cnn(pybind11::module& m) {
   m.def("cnn_partial_size", []() { return qfx_cnn_partial_size(); });
   m.def("cnn_fc1_wgrad", &fc1_wgrad, "fc1 weight gradient into the flat [K, P] gradient rows (MFMA)");
   m.def("cnn_bwd_groups", [](int64_t K, int64_t B) { return qfx_cnn_bwd_groups((int)K, (int)B); });
+  m.def("cnn_fc1_forward", &fc1_forward, "fc1 pre-activation partial sums [K, FC_KS, B, 64] (MFMA, split inputs)");
+  m.def("cnn_fc1_dgrad", &fc1_dgrad, "fc1 input gradient dL/dpool2 [K*B, 1568] (MFMA)");
+  m.def("cnn_eval_head", &eval_head, "eval: fc1 partials + bias + ReLU + fc2 -> logits, fused CE / argmax-hit sums");
+  m.def("cnn_fc1_splits", []() { return qfx_cnn_fc1_splits(); });
+  m.def("cnn_eval_blocks", [](int64_t B) { return qfx_cnn_eval_blocks((int)B); });
 }

@@ -657,14 +657,16 @@ __global__ void cnn_reduce(const float* __restrict__ part, int G, float* __restr
 }
 
 // --------------------------------------------------------------------------------------------
-// fc head, one block per client: h1 = pool2 W1^T (the fc1 GEMM, no bias) + b1 (added here: a broadcast bias in
-// the GEMM cost torch a separate expand-copy launch per step); a = ReLU(h1) * dropout; logits = W a + b; weighted
-// CE; backward:
+// fc head, one block per client: h1 = sum of the cnn_fc1_fwd partials (fixed order) + b1; a = ReLU(h1) * dropout;
+// logits = W a + b; weighted CE; backward:
 // dh1 = (W^T dlogits) * dropout * [h1 > 0]; fc2 grads.  Samples go through LDS in chunks of HB; every
 // stage spreads (sample, class) or (sample, unit) pairs over the block, and all sums over samples run in
 // a fixed order (deterministic).
 // --------------------------------------------------------------------------------------------
 constexpr int HID = 64, CMAXC = 16, HB = 64;
+constexpr int F1IN = C2 * Q2 * Q2;   // 1568 fc1 inputs
+constexpr int FC_KS = 4, FC_KC = F1IN / FC_KS, FC_T = FC_KC / 4, FC_U = 7;   // fc1 split: 392 inputs, 98 steps
+static_assert(FC_KC * FC_KS == F1IN && FC_T % FC_U == 0, "fc1 split");
 constexpr int HG = (CMAXC * HID + CMAXC + 255) / 256;   // fc2 gradient entries per thread
 
 // Dropout: either a [K*B, 64] mask, or (mask == nullptr) the client's keyed Philox uniforms u (element b*64 + j of
@@ -700,7 +702,10 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
     __syncthreads();   // previous chunk fully consumed (and Ws / bs staged)
     for (int e = tid; e < nb * HID; e += 256) {
       const int b = e / HID, j = e - b * HID;
-      const float h = h1[sb * HID + e] + b1s[j];
+      float h = 0.f;                           // the FC_KS fc1 partials in fixed order, then the bias
+#pragma unroll
+      for (int g = 0; g < FC_KS; ++g) h += h1[(((size_t)k * FC_KS + g) * B + b0 + b) * HID + j];
+      h += b1s[j];
       hv[b][j] = h;
       const float mk = mask ? mask[sb * HID + e]
                             : (philox_uniform_at((uint64_t)(b0 * HID + e), (uint32_t)dkeys[2 * k],
@@ -786,8 +791,6 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
 // samples in chunks of 32; operands come straight from global (dh1 rows stay in L2, each pool2 tile is read once),
 // all 40 loads of a chunk in flight before its MFMAs.  Bandwidth-bound: pool2 read + gradient write once.
 // --------------------------------------------------------------------------------------------
-constexpr int F1IN = C2 * Q2 * Q2;   // 1568 fc1 inputs
-
 __global__ void __launch_bounds__(256) cnn_fc1_wgrad(const float* __restrict__ dh1, const float* __restrict__ pool2,
                                                      int B, float* __restrict__ grad, int P, int off_w1) {
   const int k = blockIdx.y, c0 = blockIdx.x * 64;
@@ -821,6 +824,174 @@ __global__ void __launch_bounds__(256) cnn_fc1_wgrad(const float* __restrict__ d
       for (int r = 0; r < 4; ++r) g[(size_t)r * F1IN + nt * 16] = acc[nt][r];
 }
 
+// --------------------------------------------------------------------------------------------
+// fc1 forward, split over the inputs:  h1p[k][g][s][j] = sum_{c in chunk g} pool2[k][s][c] W1[k][j][c]
+// grid (sample tile of 32, client, chunk g < FC_KS): 4 waves, wave w owns units 16w .. 16w + 15 (one n-tile) of
+// two m-tiles (32 samples).  MFMA step t, lane group kq <-> input c = g * FC_KC + 4 t + kq: the 64 lanes of a load
+// read 16 rows x 16 contiguous bytes.  The FC_KS partial sums are added in fixed order by the consumer (cnn_head /
+// cnn_eval_head), so a client's h1 never depends on how many clients share the launch (unlike a library batched
+// GEMM, whose algorithm and split-K change with the batch count).
+// --------------------------------------------------------------------------------------------
+
+__global__ void __launch_bounds__(256) cnn_fc1_fwd(const float* __restrict__ pool2, const float* __restrict__ params,
+                                                   int P, int off_w1, int B, float* __restrict__ h1p) {
+  const int s0 = blockIdx.x * 32, k = blockIdx.y, g = blockIdx.z;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, kq = lane >> 4;
+  const int cb = g * FC_KC + kq;
+  const bool ok0 = s0 + i < B, ok1 = s0 + 16 + i < B;
+  const float* a0 = pool2 + ((size_t)k * B + (ok0 ? s0 + i : 0)) * F1IN + cb;
+  const float* a1 = pool2 + ((size_t)k * B + (ok1 ? s0 + 16 + i : 0)) * F1IN + cb;
+  const float* bw = params + (size_t)k * P + off_w1 + (size_t)(wave * 16 + i) * F1IN + cb;
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int t0 = 0; t0 < FC_T; t0 += FC_U) {
+    float x0[FC_U], x1[FC_U], w[FC_U];
+#pragma unroll
+    for (int u = 0; u < FC_U; ++u) {
+      const int c = 4 * (t0 + u);
+      x0[u] = ok0 ? a0[c] : 0.f;
+      x1[u] = ok1 ? a1[c] : 0.f;
+      w[u] = bw[c];
+    }
+#pragma unroll
+    for (int u = 0; u < FC_U; ++u) {
+      acc0 = mfma(x0[u], w[u], acc0);
+      acc1 = mfma(x1[u], w[u], acc1);
+    }
+  }
+  float* out = h1p + (((size_t)k * FC_KS + g) * B) * HID + wave * 16 + i;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int sa = s0 + 4 * kq + r, sb = s0 + 16 + 4 * kq + r;
+    if (sa < B) out[(size_t)sa * HID] = acc0[r];
+    if (sb < B) out[(size_t)sb * HID] = acc1[r];
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// fc1 input gradient:  dP2[k][s][c] = sum_j dh1[k][s][j] W1[k][j][c]
+// grid (128-input chunk, client, sample tile of 32): wave w owns inputs c0 + 32 w + [0, 32) (two n-tiles) of two
+// m-tiles; K = the 64 units, step t, lane group kq <-> unit j = 4 t + kq (16 steps; a W1 load reads 4 rows x 64
+// contiguous bytes).  Every operand of the launch is loaded before the first MFMA.
+// --------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) cnn_fc1_dgrad(const float* __restrict__ dh1, const float* __restrict__ params,
+                                                     int P, int off_w1, int B, float* __restrict__ dP2) {
+  const int c0 = blockIdx.x * 128, k = blockIdx.y, s0 = blockIdx.z * 32;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 15, kq = lane >> 4;
+  const bool ok0 = s0 + i < B, ok1 = s0 + 16 + i < B;
+  const float* d0 = dh1 + ((size_t)k * B + (ok0 ? s0 + i : 0)) * HID + kq;
+  const float* d1 = dh1 + ((size_t)k * B + (ok1 ? s0 + 16 + i : 0)) * HID + kq;
+  const int ca = c0 + 32 * wave + i, cbn = ca + 16;
+  const bool oka = ca < F1IN, okb = cbn < F1IN;
+  const float* w = params + (size_t)k * P + off_w1 + (size_t)kq * F1IN;
+  float x0[16], x1[16], wa[16], wb[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    x0[t] = ok0 ? d0[4 * t] : 0.f;
+    x1[t] = ok1 ? d1[4 * t] : 0.f;
+    wa[t] = oka ? w[(size_t)(4 * t) * F1IN + ca] : 0.f;
+    wb[t] = okb ? w[(size_t)(4 * t) * F1IN + cbn] : 0.f;
+  }
+  f4 a00 = {0.f, 0.f, 0.f, 0.f}, a01 = a00, a10 = a00, a11 = a00;
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    a00 = mfma(x0[t], wa[t], a00);
+    a01 = mfma(x0[t], wb[t], a01);
+    a10 = mfma(x1[t], wa[t], a10);
+    a11 = mfma(x1[t], wb[t], a11);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int sa = s0 + 4 * kq + r, sb = s0 + 16 + 4 * kq + r;
+    float* ra = dP2 + ((size_t)k * B + sa) * F1IN;
+    float* rb = dP2 + ((size_t)k * B + sb) * F1IN;
+    if (sa < B) {
+      if (oka) ra[ca] = a00[r];
+      if (okb) ra[cbn] = a01[r];
+    }
+    if (sb < B) {
+      if (oka) rb[ca] = a10[r];
+      if (okb) rb[cbn] = a11[r];
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Evaluation head (reference evaluate_model, Classical_FL.py:83-102): h1 = sum of the FC_KS fc1 partials (fixed
+// order) + b1, ReLU (no dropout), logits = W2 h1 + b2 -> logits [K * B, C]; with labels, per-block fixed-order
+// sums of the cross-entropy and of the argmax hits -> stats[block] = (loss_sum, correct) in float64.
+// grid (sample tile of 64, client), 256 threads: thread (sample, class) pairs for the logits, one thread per sample
+// for the softmax / argmax (first maximum, as torch.argmax).
+// --------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) cnn_eval_head(const float* __restrict__ h1p, const float* __restrict__ params,
+                                                     int P, int off_b1, int off_w, int off_b, int C, int B,
+                                                     const long long* __restrict__ y, float* __restrict__ logits,
+                                                     double* __restrict__ stats) {
+  __shared__ float Ws[CMAXC * HID];
+  __shared__ float bs[CMAXC], b1s[HID];
+  __shared__ float act[HB][HID + 1];
+  __shared__ float dl[HB][CMAXC + 1];
+  __shared__ double ls[HB], cs[HB];
+  const int s0 = blockIdx.x * HB, k = blockIdx.y, tid = threadIdx.x;
+  const int nb = min(HB, B - s0);
+  const float* prow = params + (size_t)k * P;
+  for (int e = tid; e < C * HID; e += 256) Ws[e] = prow[off_w + e];
+  if (tid < C) bs[tid] = prow[off_b + tid];
+  if (tid < HID) b1s[tid] = prow[off_b1 + tid];
+  __syncthreads();
+  for (int e = tid; e < nb * HID; e += 256) {
+    const int b = e / HID, j = e - b * HID;
+    float h = 0.f;
+#pragma unroll
+    for (int g = 0; g < FC_KS; ++g) h += h1p[(((size_t)k * FC_KS + g) * B + s0 + b) * HID + j];
+    act[b][j] = fmaxf(h + b1s[j], 0.f);
+  }
+  __syncthreads();
+  for (int e = tid; e < nb * C; e += 256) {
+    const int b = e / C, c = e - b * C;
+    float t = bs[c];
+#pragma unroll 16
+    for (int j = 0; j < HID; ++j) t = fmaf(Ws[c * HID + j], act[b][j], t);
+    dl[b][c] = t;
+    logits[((size_t)k * B + s0 + b) * C + c] = t;
+  }
+  __syncthreads();
+  if (!y) return;
+  if (tid < HB) {
+    double l = 0.0, h = 0.0;
+    if (tid < nb) {
+      const int b = tid;
+      float m = -INFINITY;
+      int am = 0;
+      for (int c = 0; c < C; ++c) {
+        m = fmaxf(m, dl[b][c]);
+        if (dl[b][c] > dl[b][am]) am = c;
+      }
+      float se = 0.f;
+      for (int c = 0; c < C; ++c) se += expf(dl[b][c] - m);
+      const int yy = (int)y[(size_t)k * B + s0 + b];
+      l = (double)(m + logf(se) - dl[b][yy]);
+      h = am == yy ? 1.0 : 0.0;
+    }
+    ls[tid] = l;
+    cs[tid] = h;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double l = 0.0, h = 0.0;
+    for (int b = 0; b < nb; ++b) {
+      l += ls[b];
+      h += cs[b];
+    }
+    const size_t blk = (size_t)k * gridDim.x + blockIdx.x;
+    stats[2 * blk] = l;
+    stats[2 * blk + 1] = h;
+  }
+}
+
 size_t fwd_lds() {
   return (size_t)(C2 * W2F + C1 * K1P + C1 + C2 + FSG * IMGP * IMGP + FSG * C1 * CSF) * 4;
 }
@@ -851,19 +1022,14 @@ extern "C" int qfx_cnn_forward(const float* X, const float* params, int P, int K
   return (int)hipGetLastError();
 }
 
-// Samples per backward workgroup: the most (up to BS_MAX, powers of two) that still give every CU a
-// workgroup.  One workgroup runs per CU (LDS), so fewer, longer workgroups amortise the per-workgroup W2
-// staging and shrink the gradient partials; small client batches fall back to fewer samples each.
-// (The partial grouping fixes the summation order: results are reproducible per device model.)
-static int bwd_bs(int K, int B) {
-  static int ncu = 0;
-  if (ncu <= 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-  }
-  int bs = BS_MAX;
-  while (bs > 1 && (long long)K * ((B + bs - 1) / bs) < ncu) bs >>= 1;
+// Samples per backward workgroup: a function of the client batch B ONLY (a quarter of it, a power of two,
+// at most BS_MAX).  The workgroup accumulates its samples' weight gradients in MFMA registers and cnn_reduce
+// sums the per-workgroup partials in fixed order, so the grouping fixes the fp32 summation order: choosing
+// it from the per-rank client count or the CU count (as round 2 did) made a client's gradient depend on how
+// many clients share its rank, breaking the bitwise rank-count invariance of the federated result.
+static int bwd_bs(int /*K*/, int B) {
+  int bs = 1;
+  while (bs * 2 <= BS_MAX && bs * 2 * 4 <= B) bs *= 2;
   return bs;
 }
 
@@ -906,3 +1072,30 @@ extern "C" int qfx_cnn_bwd_groups(int K, int B) {
   const int bs = bwd_bs(K, B);
   return (B + bs - 1) / bs;
 }
+
+extern "C" int qfx_cnn_fc1_forward(const float* pool2, const float* params, int P, int off_w1, int K, int B, float* h1p,
+                                   hipStream_t st) {
+  if (K <= 0 || B <= 0) return 0;
+  hipLaunchKernelGGL(cnn_fc1_fwd, dim3((B + 31) / 32, K, FC_KS), dim3(256), 0, st, pool2, params, P, off_w1, B, h1p);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_cnn_fc1_dgrad(const float* dh1, const float* params, int P, int off_w1, int K, int B, float* dP2,
+                                 hipStream_t st) {
+  if (K <= 0 || B <= 0) return 0;
+  hipLaunchKernelGGL(cnn_fc1_dgrad, dim3((F1IN + 127) / 128, K, (B + 31) / 32), dim3(256), 0, st, dh1, params, P,
+                     off_w1, B, dP2);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_cnn_eval_head(const float* h1p, const float* params, int P, int off_b1, int off_w, int off_b, int C,
+                                 int K, int B, const long long* y, float* logits, double* stats, hipStream_t st) {
+  if (C > CMAXC) return -2;
+  if (K <= 0 || B <= 0) return 0;
+  hipLaunchKernelGGL(cnn_eval_head, dim3((B + HB - 1) / HB, K), dim3(256), 0, st, h1p, params, P, off_b1, off_w, off_b,
+                     C, B, y, logits, stats);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_cnn_fc1_splits() { return FC_KS; }
+extern "C" int qfx_cnn_eval_blocks(int B) { return (B + HB - 1) / HB; }

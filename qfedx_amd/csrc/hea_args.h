@@ -27,4 +27,5 @@ struct HeaPassArgs {
   int n_gradops;
   int hrow[5];               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
   long long* dbg;            // optional phase timestamps (s_memtime) of workgroups < 8, [8][64]
+  int ablate;                // timing ablations (builds with QFX_HEA_ABLATE only; QFEDX_HEA_ABLATE bit mask)
 };

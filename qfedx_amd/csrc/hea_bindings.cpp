@@ -5,6 +5,7 @@
 #include <torch/extension.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -77,6 +78,14 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.n_slots = (int)geom[17];
   a.slab_tiles = (int)geom[18];
   const int64_t K = geom[19];
+  {
+    static int ablate = -1;    // only the QFX_HEA_ABLATE timing builds read it
+    if (ablate < 0) {
+      const char* e = getenv("QFEDX_HEA_ABLATE");
+      ablate = e ? atoi(e) : 0;
+    }
+    a.ablate = ablate;
+  }
   a.n_gradops = (int)geom[25];
   a.scale = (float)scale;
   a.dbg = dbg.defined() && dbg.numel() >= 8 * 64 ? dp<long long>(dbg, torch::kInt64, "dbg", 8 * 64) : nullptr;

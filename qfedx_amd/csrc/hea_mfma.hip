@@ -20,12 +20,20 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "hea_args.h"
 #include "qfx_check.h"
 
 #if QFX_CHECKS_ON
 __device__ unsigned int qfx_check_word = 0;
+#endif
+
+// Timing ablations (scripts/gpu_ab_*.sh): a build with -DQFX_HEA_ABLATE=1 skips parts of every op by the bit mask
+// QFEDX_HEA_ABLATE (1 op barriers, 2 gradient atomics, 4 cross matrices, 8 unitary applications).  Results are
+// wrong in such a build; release builds compile the checks out.
+#ifndef QFX_HEA_ABLATE
+#define QFX_HEA_ABLATE 0
 #endif
 
 namespace hea {
@@ -40,6 +48,7 @@ constexpr int F_BACK_PSI = 1;
 constexpr int TMAX = 14;
 constexpr int NT_FWD = 512;    // forward: 8 waves, 64 KB LDS -> 2 workgroups per CU
 constexpr int NT_ADJ = 1024;   // adjoint: 16 waves, 128 KB LDS (psi + lambda) -> 1 workgroup per CU
+constexpr int ADJ_WAVES_13 = 8;   // default waves of a 2^13 adjoint workgroup (QFEDX_HEA_ADJ_WAVES overrides)
 constexpr int CMAX = 8;
 constexpr int MAXOPS = 128;    // ops per pass program (host-checked)
 constexpr int MAXGRAD = 12;    // gradient ops per pass program (host-checked)
@@ -355,6 +364,13 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
   }
 }
 
+// i * (re, im) = (-im, re) on a packed fp16 pair: dst.lo = src.hi * (-1), dst.hi = src.lo * 1
+__device__ __forceinline__ uint32_t mul_i(uint32_t v) {
+  uint32_t r;
+  __asm__("v_pk_mul_f16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(v), "s"(0x3C00BC00u));
+  return r;
+}
+
 // Gradient cross matrix N[b][a] += sum_col psi[b][col] conj(lam[a][col]) over the op's column blocks:
 // K = 16 columns x (re, im), lane (g4, cl) reads amplitude m = cl of columns 4 g4 .. 4 g4 + 3; accR / accI
 // end up holding N[4 g4 + i][cl] (real / imaginary).
@@ -380,29 +396,33 @@ __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw
     }
     const uint4 A = make_uint4(pv[0], pv[1], pv[2], pv[3]);
     const uint4 Br = make_uint4(lv[0], lv[1], lv[2], lv[3]);
-    // i*lam: (re, im) -> (-im, re)
-    const uint4 Bi = make_uint4((lv[0] >> 16 ^ 0x8000u) | (lv[0] << 16), (lv[1] >> 16 ^ 0x8000u) | (lv[1] << 16),
-                                (lv[2] >> 16 ^ 0x8000u) | (lv[2] << 16), (lv[3] >> 16 ^ 0x8000u) | (lv[3] << 16));
+    // i*lam: (re, im) -> (-im, re), one v_pk_mul_f16 per dword (exact: a product with +-1)
+    const uint4 Bi = make_uint4(mul_i(lv[0]), mul_i(lv[1]), mul_i(lv[2]), mul_i(lv[3]));
     accR = mfma(A, Br, accR);
     accI = mfma(A, Bi, accI);
   }
 }
 
 // An op's unitary fragments (4 x 64 lanes x 16 B = 4 KB, contiguous in global memory) go to an LDS slot by
-// direct global -> LDS DMA (global_load_lds_dwordx4, 1 KB per wave-instruction, waves 0..3), issued one op
-// ahead: no VGPRs are held for the prefetch.  The LDS base of a wave-instruction is wave-uniform (M0); the
-// DMA is complete once the issuing wave has passed s_waitcnt vmcnt(0) (lds_barrier_dma).
-__device__ __forceinline__ void dma_frags(const PassArgs& a, int k, int fi, int tid, int wave, uint4* slot) {
-  if (fi < 0 || wave >= 4) return;
-  const uint4* fr = (const uint4*)a.frags + ((size_t)k * a.n_slots * 4 + fi) * 128 + tid;
+// direct global -> LDS DMA (global_load_lds_dwordx4, 1 KB per wave-instruction), issued one op ahead by wave 0
+// alone (four instructions): no VGPRs are held for the prefetch, and the other waves never wait on vector memory
+// at an op barrier (the wave that flushes gradient partials to the slab must not wait for those stores there).
+// The LDS base of a wave-instruction is wave-uniform (M0); the DMA is complete once wave 0 has passed
+// s_waitcnt vmcnt(0) (op_barrier).
+__device__ __forceinline__ void dma_frags(const PassArgs& a, int k, int fi, int lane, int wave, uint4* slot) {
+  if (fi < 0 || wave != 0) return;
+  const uint4* fr = (const uint4*)a.frags + ((size_t)k * a.n_slots * 4 + fi) * 128 + lane;
   // Issued as inline asm: the compiler's wait-count pass cannot tell which LDS bytes a builtin DMA writes (no
   // alias scopes reach codegen), so it waited for the DMA before the op's first LDS store or atomic and exposed
-  // the fragment latency in every op.  The slot is only read after lds_barrier_dma's vmcnt(0) + barrier, and a
+  // the fragment latency in every op.  The slot is only read after op_barrier's vmcnt(0) + barrier, and a
   // vector-memory op unknown to the pass can only make its other waits longer, never shorter.
-  const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)(slot + 64 * wave);
-  __asm__ volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(fr),
-                   "s"(__builtin_amdgcn_readfirstlane(lds))
-                   : "memory", "m0");
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)(slot + 64 * j);
+    __asm__ volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(fr + 64 * j),
+                     "s"(__builtin_amdgcn_readfirstlane(lds))
+                     : "memory", "m0");
+  }
 }
 
 // Readout / observable ops walk the tile words w = tid + NT i (i < T / NT).  The sign of class c at word w is
@@ -551,6 +571,15 @@ __device__ __forceinline__ void lds_barrier_dma() {
   __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Op barrier: wave 0 (the fragment DMA) and waves 0..1 (the next op record's global load, tid < OPW) wait for their
+// vector memory; every other wave only for its LDS operations.  A wave that stored gradient partials to the slab
+// (or anything else) thus never waits for those stores' completion at a barrier (each store stays counted in
+// vmcnt for ~1-3K cycles under load).
+__device__ __forceinline__ void op_barrier(int wave) {
+  if (wave < 2) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Phase timestamps of workgroups < 8 (scripts/hea_ablate.py): one per phase, read back as cycle deltas.
 #define HEA_MARK()                                                                                   \
   do {                                                                                               \
@@ -606,7 +635,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   if (tid < a.nops) fidx_s[tid] = a.fidx[tid];   // LDS copy: the prefetch below never waits on a global load
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
-  if (a.nops > 0) dma_frags(a, k, a.fidx[0], tid, wave, frag_s[0]);
+  if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
 
   // ---------------------------------------------------------------- initial psi tile
   if (a.gen) {
@@ -689,7 +718,10 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   for (int o = 0; o < a.nops; ++o) {
     // op o's record and fragments were written during op o - 1; the other buffers were last read at the
     // start of op o - 1, which every wave has finished at this barrier, so op o + 1's go there right away
-    lds_barrier_dma();
+    if (QFX_HEA_ABLATE && (a.ablate & 1) && o > 0)
+      lds_barrier_wave();
+    else
+      op_barrier(wave);
     HEA_MARK();
     const int* opw = opw2[o & 1];
     uint4 F[4];
@@ -700,7 +732,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
     if (o + 1 < a.nops) {
       if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
       if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
-      dma_frags(a, k, fidx_s[o + 1], tid, wave, frag_s[(o + 1) & 1]);
+      dma_frags(a, k, fidx_s[o + 1], lane, wave, frag_s[(o + 1) & 1]);
     }
     const int code = opw[W_CODE];
 #if QFX_CHECKS_ON
@@ -739,9 +771,12 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
 // zeroes it, while the other waves go on with the op (its region is next used two gradient ops later, after
 // at least one more barrier).  Measured: spreading that flush over all waves delays every wave by its LDS
 // round trip and was slower (16q adjoint 0.67 -> 0.72 ms).
-template <int NCK, int TB>
-__global__ void __launch_bounds__(1 << (TB - 4), 4) hea_adj_kernel(PassArgs a) {
-  constexpr int NT = 1 << (TB - 4), NW = NT / 64;
+// WV = waves per workgroup: 2^(TB - 10) gives 4 column blocks per wave per op (the round-2 layout); fewer waves
+// give each wave more blocks per op, amortising the per-op setup / epilogue over more MFMAs.
+template <int NCK, int TB, int WV>
+__global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(PassArgs a) {
+  constexpr int NT = 64 * WV, NW = WV;
+  static_assert(NW % 2 == 0 && (1 << (TB - 8)) % NW == 0, "column blocks per wave must be whole, block pairs aligned");
   // (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
   __shared__ __attribute__((aligned(16))) uint32_t tile[2 << TB];
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
@@ -772,7 +807,7 @@ __global__ void __launch_bounds__(1 << (TB - 4), 4) hea_adj_kernel(PassArgs a) {
   if (tid < a.nops) fidx_s[tid] = a.fidx[tid];
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
-  if (a.nops > 0) dma_frags(a, k, a.fidx[0], tid, wave, frag_s[0]);
+  if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
   load_tile_il<NT, TB>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
                        h_q, fixed);
   if (tid == 0) {
@@ -816,7 +851,10 @@ __global__ void __launch_bounds__(1 << (TB - 4), 4) hea_adj_kernel(PassArgs a) {
   for (int o = 0; o < a.nops; ++o) {
     // op o's record and fragments were written during op o - 1; the other buffers were last read at the
     // start of op o - 1, which every wave has finished at this barrier, so op o + 1's go there right away
-    lds_barrier_dma();
+    if (QFX_HEA_ABLATE && (a.ablate & 1) && o > 0)
+      lds_barrier_wave();
+    else
+      op_barrier(wave);
     HEA_MARK();
     if (RING && pending >= 0) {
       if (wave == NW - 1) flush(pending);
@@ -831,7 +869,7 @@ __global__ void __launch_bounds__(1 << (TB - 4), 4) hea_adj_kernel(PassArgs a) {
     if (o + 1 < a.nops) {
       if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
       if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
-      dma_frags(a, k, fidx_s[o + 1], tid, wave, frag_s[(o + 1) & 1]);
+      dma_frags(a, k, fidx_s[o + 1], lane, wave, frag_s[(o + 1) & 1]);
     }
     const int code = opw[W_CODE];
 #if QFX_CHECKS_ON
@@ -859,8 +897,8 @@ __global__ void __launch_bounds__(1 << (TB - 4), 4) hea_adj_kernel(PassArgs a) {
     } else if (code == OP_BACK || code == OP_GRAD || code == OP_GRAD_L1) {
       const uint32_t fo = op_fo(opw, fixed);
       f4 accR = {0.f, 0.f, 0.f, 0.f}, accI = {0.f, 0.f, 0.f, 0.f};
-      group_cross<NW, TB>(tile, opw, fo, lane, wave, nbw, accR, accI);
-      if (code == OP_BACK) {
+      if (!(QFX_HEA_ABLATE && (a.ablate & 4))) group_cross<NW, TB>(tile, opw, fo, lane, wave, nbw, accR, accI);
+      if (code == OP_BACK && !(QFX_HEA_ABLATE && (a.ablate & 8))) {
         if (opw[W_FLAGS] & F_BACK_PSI)
           group_apply<2, NW, true, 0, TB>(tile, F, opw, fo, lane, wave, nbw);
         else
@@ -876,6 +914,7 @@ __global__ void __launch_bounds__(1 << (TB - 4), 4) hea_adj_kernel(PassArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15, d = bb ^ aa;
+        if (QFX_HEA_ABLATE && (a.ablate & 2)) break;
         if (__builtin_popcount(d) <= 1) {
           const int e = d == 0 ? (int)bb : 16 + 16 * (__builtin_ctz(d)) + (int)bb;
           atomicAdd(&rg[red_slot(e)], (unsigned long long)fix64(accR[i] * sc));
@@ -1010,14 +1049,21 @@ extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_sample
   if (a.t > hea::TMAX || a.t < 8 || a.C > hea::CMAX || a.n > 30 || a.c < 2) return -2;
   const unsigned grid = (unsigned)(n_samples * a.n_tiles);
   if (grid == 0) return 0;
+  static int adj_waves = 0;   // waves per 2^13 adjoint workgroup (QFEDX_HEA_ADJ_WAVES = 4 | 8)
+  if (!adj_waves) {
+    const char* e = getenv("QFEDX_HEA_ADJ_WAVES");
+    adj_waves = (e && atoi(e) == 8) ? 8 : (e && atoi(e) == 4 ? 4 : hea::ADJ_WAVES_13);
+  }
 #define HEA_LAUNCH(NCK)                                                                                     \
   do {                                                                                                     \
     if (!adjoint)                                                                                          \
       hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);             \
+    else if (a.t <= 13 && adj_waves == 4)                                                                  \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 4>), dim3(grid), dim3(256), 0, st, a);              \
     else if (a.t <= 13)                                                                                    \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13>), dim3(grid), dim3(1 << 9), 0, st, a);              \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8>), dim3(grid), dim3(512), 0, st, a);              \
     else                                                                                                   \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14>), dim3(grid), dim3(1 << 10), 0, st, a);             \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14, 16>), dim3(grid), dim3(1024), 0, st, a);            \
   } while (0)
   switch (hea::class_kernel(a.C)) {
     case 1: HEA_LAUNCH(1); break;

@@ -380,10 +380,47 @@ __device__ __forceinline__ void round_pack_block(const RoundPack& rp, int P) {
 constexpr int FA_E = 64, FA_G = 4;   // fedavg reduce: parameters per block (one wave row) x client groups per block
 constexpr int FA_U = 4;              // client rows in flight per thread
 
-// one client's fixed-point FedAvg term of parameter e
+// Pairwise-mask secure aggregation inside the reduce (privacy/secure_agg.py is the host protocol and
+// oracle).  Client row k's masked term of element e (e < P: weighted update, e == P: the weight) in Z_2^bits:
+//   encode(x) = round(x * scale) mod 2^bits,  + sum_j sign[k][j] * PRG(seed[k][j], round)[e]  mod 2^bits
+// with PRG = Philox4x32-10 keyed by the 64-bit pair seed, counter (e / 2, 0, round, 0x5EC), element e the 48-bit
+// value of words 2 (e & 1), 2 (e & 1) + 1 (prg_mask's exact layout).  sign is +1 toward peers j > k, -1 toward
+// j < k, 0 for non-participants, the client itself and padding rows; the orphan-mask correction of a dropped peer
+// d (the survivor reveals seed[k][d], the server removes that mask) cancels the survivor's mask toward d exactly
+// mod 2^bits, so the host folds it into sign[k][d] = 0.  Sums run in wrapping int64 (2^bits divides 2^64); the
+// decode (round_apply) reduces mod 2^bits.
+struct SecAgg {
+  const uint32_t* seeds;     // [K][N][2] pair-seed key words (lo, hi); nullptr = plain exact aggregation
+  const int* sign;           // [K][N]
+  const int* round;          // [1] (a device word: the reduce is captured in the round graph)
+  int N;
+  double scale;
+  long long mask;            // 2^bits - 1
+};
+
+__device__ __forceinline__ long long secagg_masks(const SecAgg& sa, int k, long e) {
+  const uint32_t rnd = (uint32_t)sa.round[0];
+  const uint64_t blk = (uint64_t)e >> 1;
+  long long acc = 0;
+  for (int j = 0; j < sa.N; ++j) {
+    const int sg = sa.sign[(size_t)k * sa.N + j];
+    if (sg == 0) continue;
+    const uint32_t* key = sa.seeds + ((size_t)k * sa.N + j) * 2;
+    const u32x4 o = philox4x32_10({(uint32_t)blk, (uint32_t)(blk >> 32), rnd, 0x5ECu}, key[0], key[1]);
+    const uint64_t w = (e & 1) ? ((uint64_t)o.w << 32 | o.z) : ((uint64_t)o.y << 32 | o.x);
+    const long long m = (long long)(w & (uint64_t)sa.mask);
+    acc += sg > 0 ? m : -m;
+  }
+  return acc;
+}
+
+// one client's fixed-point FedAvg term of parameter e.  A term is held to |v| <= FA_SAT = 2^53 (exactly
+// representable, and up to 2^10 such terms still sum inside int64): a larger w_k * Delta (|w Delta| > 2^21, e.g.
+// sample-count weights times a diverged CNN delta) is clamped and counted in *nsat instead of wrapping in llrint.
+constexpr double FA_SAT = 9007199254740992.0;
 __device__ __forceinline__ long long fedavg_term(float x, double tg, bool wr, int k, long e, const double* weights,
                                                  const double* norms, const uint32_t* keys, int dp, float clip,
-                                                 float sigma) {
+                                                 float sigma, int& nsat, const SecAgg& sa) {
   const double SC = 4294967296.0;
   double d = (double)x - tg;
   if (wr) d = wrap_pi(d);
@@ -394,14 +431,29 @@ __device__ __forceinline__ long long fedavg_term(float x, double tg, bool wr, in
     if (sigma > 0.f)
       d += (double)sigma * (double)clip * (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
   }
-  return llrint(weights[k] * d * SC);
+  if (sa.seeds) {                      // SecAgg ring element: held to +-2^(bits - 1) before it wraps
+    double v = weights[k] * d * sa.scale;
+    const double lim = (double)(sa.mask >> 1);
+    if (!(fabs(v) <= lim)) {
+      ++nsat;
+      v = v > 0.0 ? lim : (v < 0.0 ? -lim : 0.0);
+    }
+    return ((long long)llrint(v) & sa.mask) + secagg_masks(sa, k, e);
+  }
+  double v = weights[k] * d * SC;
+  if (!(fabs(v) <= FA_SAT)) {          // also catches NaN (clamped to 0)
+    ++nsat;
+    v = v > 0.0 ? FA_SAT : (v < 0.0 ? -FA_SAT : 0.0);
+  }
+  return llrint(v);
 }
 
 __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
     const float* __restrict__ theta_k, const float* __restrict__ theta_g,
     const unsigned char* __restrict__ angle_mask, const double* __restrict__ weights,
     const double* __restrict__ norms, const uint32_t* __restrict__ keys, int K, int P, int wrap,
-    int dp, float clip, float sigma, long long* __restrict__ out, RoundPack rp) {
+    int dp, float clip, float sigma, long long* __restrict__ out, RoundPack rp, long long* __restrict__ sat,
+    SecAgg sa) {
   // the block past the parameter blocks (launched only with rp.buf) packs the round metrics into the tail of
   // the all-reduce buffer: the parameter blocks write out[0..P], the pack block out[P+1..P+4]
   if (blockIdx.x == gridDim.x - 1 && rp.buf != nullptr) {
@@ -417,10 +469,23 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
   const long e = (long)blockIdx.x * FA_E + el;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     long long ws = 0;
-    for (int k = 0; k < K; ++k) ws += llrint(weights[k] * SC);
+    int wsat = 0;
+    for (int k = 0; k < K; ++k) {
+      if (sa.seeds) {                  // the weight is element P of the client's masked vector
+        const double v = weights[k] * sa.scale, lim = (double)(sa.mask >> 1);
+        if (!(fabs(v) <= lim)) ++wsat;
+        ws += ((long long)llrint(fmin(fmax(v, -lim), lim)) & sa.mask) + secagg_masks(sa, k, P);
+        continue;
+      }
+      const double v = weights[k] * SC;
+      if (!(fabs(v) <= FA_SAT)) ++wsat;
+      ws += llrint(fmin(fmax(v, -FA_SAT), FA_SAT));
+    }
     out[P] = ws;
+    if (wsat && sat) atomicAdd((unsigned long long*)sat, (unsigned long long)wsat);
   }
   long long acc = 0;
+  int nsat = 0;
   if (e < P) {
     const double tg = (double)theta_g[e];
     const bool wr = wrap && angle_mask[e];
@@ -430,10 +495,15 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
 #pragma unroll
       for (int u = 0; u < FA_U; ++u) x[u] = theta_k[(size_t)(k + u * FA_G) * P + e];
 #pragma unroll
-      for (int u = 0; u < FA_U; ++u) acc += fedavg_term(x[u], tg, wr, k + u * FA_G, e, weights, norms, keys, dp, clip, sigma);
+      for (int u = 0; u < FA_U; ++u)
+        acc += fedavg_term(x[u], tg, wr, k + u * FA_G, e, weights, norms, keys, dp, clip, sigma, nsat, sa);
     }
-    for (; k < K; k += FA_G) acc += fedavg_term(theta_k[(size_t)k * P + e], tg, wr, k, e, weights, norms, keys, dp, clip, sigma);
+    for (; k < K; k += FA_G)
+      acc += fedavg_term(theta_k[(size_t)k * P + e], tg, wr, k, e, weights, norms, keys, dp, clip, sigma, nsat, sa);
   }
+  // saturated terms are counted (an integer: the count is exact in any order); the host raises on a nonzero
+  // count when it reads the round's metrics back (self-cleaning: round_apply zeroes it after the all-reduce)
+  if (nsat && sat) atomicAdd((unsigned long long*)sat, (unsigned long long)nsat);
   part[grp][el] = acc;
   __syncthreads();
   if (grp == 0 && e < P) {
@@ -448,19 +518,37 @@ __global__ void __launch_bounds__(256) qfx_round_pack_kernel(RoundPack rp, int P
 
 // round epilogue 2 (after the all-reduce): theta += lr * (sum w Delta) / (sum w) in float64, rounded to
 // fp32 - the same operations as Aggregator.finalize + apply; rounds with zero total weight keep theta.
-//   out[0..3] = metrics, out[4] = weight sum
-__global__ void qfx_round_apply_kernel(const long long* __restrict__ buf, int P, float* __restrict__ theta, double lr,
-                                       double* __restrict__ out) {
+//   out[0..3] = metrics, out[4] = saturated FedAvg terms over all ranks (buf[P + 5], which this launch zeroes for
+//   the next round: nothing else reads it, and the next round's reduce runs after it), out[5] = weight sum
+// With SecAgg (bits > 0) the update and weight entries are ring elements: reduced mod 2^bits, read as signed and
+// divided by the SecAgg scale (decode_fixed); the metric tail stays plain 2^32 fixed point.
+__device__ __forceinline__ double ring_decode(long long v, int bits, double scale) {
+  const long long m = (1LL << bits) - 1;
+  long long u = v & m;
+  if (u >> (bits - 1)) u -= (1LL << bits);
+  return (double)u / scale;
+}
+
+__global__ void qfx_round_apply_kernel(long long* __restrict__ buf, int P, float* __restrict__ theta, double lr,
+                                       double* __restrict__ out, int bits, double ring_scale) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const double SC = 4294967296.0;
-  const double wsum = (double)buf[P] / SC;
+  const double wsum = bits ? ring_decode(buf[P], bits, ring_scale) : (double)buf[P] / SC;
   if (e < P) {
-    const double mean = ((double)buf[e] / SC) / fmax(wsum, 1e-300);
+    const double upd = bits ? ring_decode(buf[e], bits, ring_scale) : (double)buf[e] / SC;
+    const double mean = upd / fmax(wsum, 1e-300);
     const double th = (double)theta[e];
     theta[e] = wsum > 0.0 ? (float)(th + lr * mean) : (float)th;
-  } else if (e < P + 5) {
+  } else if (e < P + 6) {
     const int j = (int)(e - P);
-    out[j] = j < 4 ? (double)buf[P + 1 + j] / SC : wsum;
+    if (j < 4) {
+      out[j] = (double)buf[P + 1 + j] / SC;
+    } else if (j == 4) {
+      out[j] = (double)buf[P + 5];
+      buf[P + 5] = 0;
+    } else {
+      out[j] = wsum;
+    }
   }
 }
 
@@ -476,9 +564,11 @@ extern "C" int qfx_launch_round_pack(long long* buf, int P, const float* loss, c
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_launch_round_apply(const long long* buf, int P, float* theta, double lr, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(qfx_round_apply_kernel, dim3((unsigned)((P + 5 + 255) / 256)), dim3(256), 0, st, buf, P, theta,
-                     lr, out);
+extern "C" int qfx_launch_round_apply(long long* buf, int P, float* theta, double lr, double* out, int bits,
+                                      double ring_scale, hipStream_t st) {
+  if (bits < 0 || bits > 62) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(qfx_round_apply_kernel, dim3((unsigned)((P + 6 + 255) / 256)), dim3(256), 0, st, buf, P, theta,
+                     lr, out, bits, ring_scale);
   return (int)hipGetLastError();
 }
 
@@ -713,7 +803,8 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                                  const double* weights, double* norms, const uint32_t* keys, int K, int P,
                                  int wrap, int dp, float clip, float sigma, long long* out, long long* pack_buf,
                                  const float* loss, const float* correct, const float* nvalid, const float* act,
-                                 int n_metrics, hipStream_t st) {
+                                 int n_metrics, long long* sat, const uint32_t* sa_seeds, const int* sa_sign,
+                                 const int* sa_round, int sa_n, double sa_scale, int sa_bits, hipStream_t st) {
   if (dp) {   // clipping needs the per-client norms; without DP they are not computed
     const int nc = (P + NORM_CHUNK - 1) / NORM_CHUNK;
     double* partial = norms + K;   // scratch tail of the norms buffer: K * nc doubles
@@ -724,6 +815,7 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
   const RoundPack rp{pack_buf, loss, correct, nvalid, act, n_metrics};
   const unsigned blocks = (unsigned)((P + FA_E - 1) / FA_E) + (pack_buf ? 1u : 0u);
   hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3(blocks), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
-                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out, rp);
+                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out, rp, sat,
+                     SecAgg{sa_seeds, sa_sign, sa_round, sa_n, sa_scale, sa_seeds ? (1LL << sa_bits) - 1 : 0});
   return (int)hipGetLastError();
 }

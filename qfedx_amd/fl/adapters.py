@@ -32,20 +32,28 @@ class VQCAdapter:
     def __init__(self, cfg, device, backend: str):
         m = cfg.model
         self.noise = NoiseModel.from_config(getattr(cfg, "noise", None), cfg.train.seed)
+        sim = getattr(m, "simulator", "statevector")
+        if sim not in ("statevector", "mps", "density"):
+            raise ValueError(f"model.simulator must be statevector, mps or density, got '{sim}'")
+        if self.noise is not None and self.noise.exact_only and sim != "density":
+            if sim == "mps" or m.n_qubits > 10:
+                raise ValueError("noise.kind=amplitude (exact amplitude damping) runs on the density-matrix simulator "
+                                 "(<= 10 qubits); use noise.kind=amplitude_twirl (Pauli-twirl trajectories) beyond")
+            sim = "density"                   # exact Kraus channel: the only simulator that realises it
+        self.simulator = sim
+        # statevector / MPS engines realise Pauli channels as trajectories; the density simulator applies the
+        # channel itself (no trajectory ops in the circuit)
         self.spec = VQCSpec(m.n_qubits, m.n_layers, m.n_classes, m.feature_map, m.feature_scale,
                             m.alpha, m.entangler, None, m.readout_scale, m.init_std,
-                            noisy=self.noise is not None and self.noise.gate_noise)
+                            noisy=self.noise is not None and self.noise.pauli_noise and sim != "density")
         self.device = torch.device(device)
-        sim = getattr(m, "simulator", "statevector")
-        if sim not in ("statevector", "mps"):
-            raise ValueError(f"model.simulator must be statevector or mps, got '{sim}'")
         # the circuit engine follows model.simulator; optimizer / aggregation kernels follow the runtime backend
         self.state_dtype = resolve_state_dtype(m.state_dtype, self.spec, backend, self.noise)
-        self.engine = VQCEngine(self.spec, device, "mps" if sim == "mps" else backend, self.state_dtype,
+        self.engine = VQCEngine(self.spec, device, sim if sim in ("mps", "density") else backend, self.state_dtype,
                                 noise=self.noise, mps_chi=int(getattr(m, "mps_chi", 64)))
         self.trainer = VQCClientTrainer(self.spec, self.engine, cfg.train, device, backend)
         # QR/SVD recompression is data dependent: the MPS round runs eagerly, not as a captured graph
-        self.trainer.graphs = bool(getattr(cfg.runtime, "use_graphs", True)) and sim != "mps"
+        self.trainer.graphs = bool(getattr(cfg.runtime, "use_graphs", True)) and sim not in ("mps", "density")
         self.n_params = self.spec.n_params
         self.eval_batch = 4096
 

@@ -22,6 +22,7 @@ from ..privacy.secure_agg import SecureAggregator
 
 
 EXACT_SCALE = float(2 ** 32)   # fixed-point scale of the exact (rank-count invariant) aggregation
+SAT_LIMIT = float(2 ** 53)     # largest fixed-point term (|w * Delta| <= 2^21): exact in float64, 2^10 terms fit int64
 
 
 def wrap_angles(d: torch.Tensor) -> torch.Tensor:
@@ -53,8 +54,9 @@ class Aggregator:
     def __init__(self, n_params: int, angle_mask: Optional[torch.Tensor], device, backend: str = "torch",
                  aggregate: str = "delta", wrap: bool = True, dp: bool = False, clip_norm: float = 1.0,
                  noise_multiplier: float = 1.0, secure_agg: bool = False, secagg: Optional[SecureAggregator] = None,
-                 seed: int = 0):
+                 seed: int = 0, num_clients: int = 0):
         self.P = n_params
+        self.num_clients = num_clients      # all clients of the federation (SecAgg sign / seed tables)
         self.device = torch.device(device)
         self.backend = backend
         self.aggregate = aggregate
@@ -68,11 +70,13 @@ class Aggregator:
         self.secagg = secagg
         self.seed = seed
         self.last_norms: Optional[torch.Tensor] = None
+        self.last_saturation: Optional[torch.Tensor] = None   # [1] count of clamped fixed-point terms
 
     def local_reduce(self, theta_k: torch.Tensor, theta_g: torch.Tensor, weights: torch.Tensor,
                      round_num: int, client_ids: list, participants: Optional[list] = None,
                      dropped: Optional[list] = None, out: Optional[torch.Tensor] = None,
-                     keys: Optional[torch.Tensor] = None, pack: Optional[tuple] = None) -> torch.Tensor:
+                     keys: Optional[torch.Tensor] = None, pack: Optional[tuple] = None,
+                     secagg_tabs: Optional[tuple] = None) -> torch.Tensor:
         """This rank's contribution [P+1] = [sum_k w_k priv(Delta_k) | sum_k w_k].
 
         float64 normally; int64 ring elements (mod 2^bits, masked) under secure aggregation.
@@ -81,15 +85,28 @@ class Aggregator:
         ``pack`` (HIP fast path only): (buf, loss, correct, nvalid, act) - the same launch also packs the round
         metrics into the tail of the all-reduce buffer ``buf`` whose head is ``out``.
         """
-        if self.backend == "hip" and not self.secure_agg:
+        if self.backend == "hip":
             from ..ops import fedavg_hip
             if getattr(self, "_mask_u8", None) is None:
                 self._mask_u8 = self.angle_mask.to(torch.uint8).contiguous()
-            out, norms = fedavg_hip.fused_local_reduce(
+            sa = None
+            if self.secure_agg:
+                # the fused kernel masks every client's ring element itself (K18 on the device); ``secagg_tabs``
+                # = (seeds, sign, round) device tables (uploaded with the round), else built and uploaded here
+                if secagg_tabs is None:
+                    from ..utils.device import h2d
+                    parts = list(participants if participants is not None else client_ids)
+                    n_all = max([self.num_clients] + [int(c) + 1 for c in parts + list(client_ids)])
+                    seeds, sign = self.secagg.round_tables(client_ids, parts, dropped or [], n_all)
+                    secagg_tabs = (h2d(seeds, self.device), h2d(sign, self.device),
+                                   h2d(torch.tensor([round_num], dtype=torch.int32), self.device))
+                sa = (*secagg_tabs, self.secagg.scale, self.secagg.bits)
+            out, norms, sat = fedavg_hip.fused_local_reduce(
                 theta_k, theta_g, weights, self._mask_u8, client_ids, round_num, self.seed,
                 wrap=self.wrap, dp=self.dp, clip_norm=self.clip_norm,
-                noise_multiplier=self.noise_multiplier, out=out, keys=keys, pack=pack)
+                noise_multiplier=self.noise_multiplier, out=out, keys=keys, pack=pack, secagg=sa)
             self.last_norms = norms
+            self.last_saturation = sat
             return out
         if pack is not None:
             raise ValueError("the metric pack is fused into the HIP reduce only")
@@ -106,8 +123,13 @@ class Aggregator:
         weighted = torch.cat([delta * w[:, None], w[:, None]], -1)    # [K, P+1]
         if not self.secure_agg:
             # per-client fixed point BEFORE summation: integer sums are associative, so the aggregate
-            # is bitwise identical however clients are sharded over ranks
-            return torch.round(weighted * EXACT_SCALE).to(torch.int64).sum(0)
+            # is bitwise identical however clients are sharded over ranks.  Terms are
+            # held to 2^53 (as the HIP kernel does) and the clamped ones counted, never wrapped.
+            v = weighted * EXACT_SCALE
+            bad = ~(v.abs() <= SAT_LIMIT)
+            self.last_saturation = bad.sum().reshape(1)
+            v = torch.where(torch.isnan(v), torch.zeros_like(v), v).clamp(-SAT_LIMIT, SAT_LIMIT)
+            return torch.round(v).to(torch.int64).sum(0)
         sa = self.secagg
         parts = list(participants if participants is not None else client_ids)
         total = torch.zeros(self.P + 1, dtype=torch.int64, device=delta.device)

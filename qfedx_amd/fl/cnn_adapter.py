@@ -157,9 +157,15 @@ class TinyCNNAdapter:
             return 0.0, 0.0, 0.0
         loss_sum = torch.zeros((), dtype=torch.float64, device=X.device)
         correct = torch.zeros((), dtype=torch.float64, device=X.device)
+        hip = self.trainer._hip
         for s in range(0, X.shape[0], self.eval_batch):       # no per-batch host sync (reference :100)
-            logits = self._fwd(params, X[s: s + self.eval_batch])
-            yb = y[s: s + self.eval_batch]
+            xb, yb = X[s: s + self.eval_batch], y[s: s + self.eval_batch]
+            if hip is not None:                               # HIP: CE and argmax hits fused into the eval head
+                _, ls, hits = hip.logits(params[None].float(), xb.reshape(1, -1, 1, 28, 28).float(), yb[None])
+                loss_sum += ls
+                correct += hits
+                continue
+            logits = self._fwd(params, xb)
             loss_sum += F.cross_entropy(logits, yb, reduction="sum").double()
             correct += (logits.argmax(-1) == yb).sum().double()
         return float(loss_sum), float(correct), float(X.shape[0])

@@ -96,7 +96,7 @@ class FederatedRunner:
             self.secagg.setup(self.local_ids, world)
         self.aggregator = Aggregator(self.P, adapter.angle_mask(), device, backend, t.aggregate,
                                      t.wrap_angles, p.dp, p.clip_norm, p.noise_multiplier, p.secure_agg,
-                                     self.secagg, self.noise_seed)
+                                     self.secagg, self.noise_seed, num_clients=self.num_clients)
         self.accountant = RDPAccountant()
         # test shard for this rank
         Xt, yt = data.test
@@ -206,7 +206,7 @@ class FederatedRunner:
         dev = self.device
         P = self.P
         ids = [self.local_ids[i] for i in local_alive]
-        fast = self.backend == "hip" and not p.secure_agg and self.server_opt is None
+        fast = self.backend == "hip" and self.server_opt is None
         trainer = self.adapter.trainer
         if fast:
             # round epilogue on the device, run by the trainer right after the local steps (captured into the
@@ -215,7 +215,7 @@ class FederatedRunner:
             # uniform FedAvg weights) travel as per-client tables with the round's upload, never as kernel
             # arguments.
             if getattr(self, "_round_buf", None) is None:
-                self._round_buf = torch.zeros(P + 5, dtype=torch.int64, device=dev)
+                self._round_buf = torch.zeros(P + 6, dtype=torch.int64, device=dev)
             buf = self._round_buf
             extra = {}
             if p.dp and ids:
@@ -223,12 +223,20 @@ class FederatedRunner:
                 extra["dpkeys"] = dp_noise_keys(ids, r, self.noise_seed)
             if t.weighting == "uniform":
                 extra["fw"] = torch.ones(len(ids), dtype=torch.float64)
+            if p.secure_agg and ids:
+                # SecAgg on the device: every local client's pair-seed keys and mask signs for this round ride with
+                # the round's tables; the fused reduce masks each client's ring element (K18), so the round stays
+                # one graph launch
+                extra["sa_seed"], extra["sa_sign"] = self.secagg.round_tables(ids, participants, dropped,
+                                                                              self.num_clients)
+                extra["sa_round"] = torch.full((len(ids),), r, dtype=torch.int32)
             agg = self.aggregator
 
             def epilogue(params_k, tabs, theta):
                 # one launch: the fused reduce writes the buffer head, its last block packs the metrics
+                sa = (tabs["sa_seed"], tabs["sa_sign"], tabs["sa_round"]) if "sa_seed" in tabs else None
                 agg.local_reduce(params_k, theta, tabs.get("fw", tabs["w"]), r, ids, out=buf[: P + 1],
-                                 keys=tabs.get("dpkeys"),
+                                 keys=tabs.get("dpkeys"), secagg_tabs=sa,
                                  pack=(buf, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
                                        tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)))
             with self.timer.phase("local_train"):
@@ -257,14 +265,18 @@ class FederatedRunner:
                 correct = (res["correct"].double() * res["act"].double()).sum()
                 host_m = h2d(torch.tensor([float(res.get("samples", 0.0)), float(res.get("steps", 0))],
                                           dtype=torch.float64), dev)
-                metrics = torch.cat([torch.stack([loss_sum, correct]).to(dev), host_m])
+                sat = self.aggregator.last_saturation if local_alive else None
+                sat = (sat.to(dev).double().reshape(1) if sat is not None
+                       else torch.zeros(1, dtype=torch.float64, device=dev))
+                metrics = torch.cat([torch.stack([loss_sum, correct]).to(dev), host_m, sat])
         with self.timer.phase("comm"):
             if fast:
                 all_reduce_(buf, self.world)              # ONE collective per round (CC2+CC3)
-                out = torch.empty(5, dtype=torch.float64, device=dev)
+                out = torch.empty(6, dtype=torch.float64, device=dev)
                 from ..ops._ext import ext
-                ext().round_apply(buf, P, self.params, 1.0, out)   # finalize + apply, in place
-                metrics = out[:4]
+                ring = (p.secagg_bits, p.secagg_scale) if p.secure_agg else (0, 1.0)
+                ext().round_apply(buf, P, self.params, 1.0, out, *ring)   # finalize + apply, in place
+                metrics = out[:5]                                     # + saturated fixed-point terms
             elif self.server_opt is not None:
                 # server optimizer (CC5): small all-reduce of [weight | metrics]; the update sums are
                 # reduce-scattered inside the sharded step and the new params all-gathered
@@ -273,12 +285,12 @@ class FederatedRunner:
                 all_reduce_(tail, self.world)
                 wsum = tail[0].double() / EXACT_SCALE
                 metrics = tail[1:].double() / EXACT_SCALE
-                self.params = self.server_opt.step(self.params, contrib[:P].to(torch.int64), wsum)
+                self._set_params(self.server_opt.step(self.params, contrib[:P].to(torch.int64), wsum))
             elif p.secure_agg:
                 all_reduce_(contrib, self.world)          # int64 ring elements: exact, mod later
                 all_reduce_(metrics, self.world)
                 mean_upd, wsum = self.aggregator.finalize(contrib)
-                self.params = self.aggregator.apply(self.params, mean_upd, wsum=wsum)
+                self._set_params(self.aggregator.apply(self.params, mean_upd, wsum=wsum))
             else:
                 # ONE collective per round (CC2+CC3): [exact fixed-point update | weight | metrics]
                 buf = torch.cat([contrib.to(torch.int64),
@@ -286,7 +298,7 @@ class FederatedRunner:
                 all_reduce_(buf, self.world)
                 mean_upd, wsum = self.aggregator.finalize(buf[: P + 1])
                 metrics = buf[P + 1:].double() / EXACT_SCALE
-                self.params = self.aggregator.apply(self.params, mean_upd, wsum=wsum)
+                self._set_params(self.aggregator.apply(self.params, mean_upd, wsum=wsum))
         if p.dp:
             # the subsampled-Gaussian RDP bound holds for Poisson sampling at rate q; a fixed-size subset
             # drawn without replacement is accounted conservatively with no amplification (q = 1)
@@ -300,12 +312,21 @@ class FederatedRunner:
             rec["epsilon"] = self.accountant.get_epsilon(p.delta)
         return self.resolve_record(rec) if sync else rec
 
+    def _set_params(self, new: torch.Tensor) -> None:
+        """Update the global params IN PLACE: the trainer's cached round hipGraph reads them at a fixed address,
+        so a fresh tensor per round (SecAgg / server-optimizer paths) would miss the graph cache every round."""
+        self.params.copy_(new.to(self.params.dtype))
+
     def resolve_record(self, rec: dict) -> dict:
         """Read a round's metrics back (syncs with the device) and fill the derived fields."""
         if "_metrics" not in rec:
             return rec
         m = rec.pop("_metrics").double().cpu().tolist()
         dt = time.perf_counter() - rec.pop("_t0")
+        if len(m) > 4 and m[4] > 0:
+            raise RuntimeError(f"round {rec['round']}: {int(m[4])} fixed-point FedAvg terms saturated at 2^53 "
+                               "(|w * Delta| > 2^21): lower the aggregation weights (train.weighting=uniform) or "
+                               "the update magnitude (DP clipping / learning rate)")
         rec.update({"train_loss": m[0] / max(m[2], 1.0) if m[2] else float("nan"),
                     "train_acc": m[1] / max(m[2], 1.0) if m[2] else float("nan"),
                     "local_steps": int(round(m[3])), "round_time_s": dt,

@@ -22,7 +22,10 @@ from ..utils.device import PackedUpload, h2d
 from ..utils.seeding import _philox4x32_np, philox4x32, philox_key
 from .optim import BatchedOptimizer
 
-UPFRONT_GATHER_BYTES = 1 << 30   # round prologue gathers every step up front below this input-buffer size
+# The round prologue gathers every step's inputs up front below this buffer size.  The buffer lives in the round
+# graph's private pool and up to _GRAPH_LRU graphs stay cached, so the cap bounds that reserve too (1.5 GiB).
+UPFRONT_GATHER_BYTES = 1 << 28
+_GRAPH_LRU = 6
 
 
 class ShardStore:
@@ -209,7 +212,7 @@ class VQCClientTrainer:
         shot-sampled, all keyed per client and step."""
         cfg, spec = self.cfg, self.spec
         noise = self.engine.noise
-        T = noise.trajectories if (noise is not None and noise.gate_noise) else 1
+        T = noise.trajectories if (noise is not None and spec.noisy) else 1
         K = lid.shape[0]
         P = theta.numel()
         params = torch.empty(K, P, dtype=torch.float32, device=self.device)
@@ -375,7 +378,7 @@ class VQCClientTrainer:
                 with torch.cuda.graph(g):
                     ent["out"] = body()
             ent["graph"] = g
-            while len(cache) >= 6:                  # LRU: drop the oldest shape
+            while len(cache) >= _GRAPH_LRU:         # LRU: drop the oldest shape
                 cache.pop(next(iter(cache)))
         else:
             dv = up.to_device(dev, ent["pack"])     # one H2D copy for all the round's tables

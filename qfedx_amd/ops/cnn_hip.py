@@ -3,12 +3,17 @@
 One local step of K clients x B samples:
   1. ``cnn_forward``  - fused conv1/conv2 + bias + ReLU + 2x2 max-pool (fp32 MFMA implicit GEMM, per
                         client weights), writes pooled maps + argmax codes
-  2. fc1              - ``bmm`` over the client batch (plain batched GEMM -> hipBLASLt/rocBLAS; bias in the head)
-  3. ``cnn_head``     - fc1 bias + ReLU + keyed dropout + fc2 + weighted CE, dlogits, fc2 grads, dL/dh1, fc1 bias grad
-  4. fc1 backward     - ``cnn_fc1_wgrad`` (weight grad into the gradient rows) + one batched GEMM (dL/dpool2)
+  2. ``cnn_fc1_forward`` - fc1 as per-client MFMA tiles, split over the 1568 inputs into FC_KS partial sums (no
+                        library GEMM: a batched GEMM's algorithm changes with the client count, so a client's result
+                        would depend on how clients are sharded over ranks)
+  3. ``cnn_head``     - fc1 partials (fixed order) + bias + ReLU + keyed dropout + fc2 + weighted CE, dlogits, fc2
+                        grads, dL/dh1, fc1 bias grad
+  4. fc1 backward     - ``cnn_fc1_wgrad`` (weight grad into the gradient rows) + ``cnn_fc1_dgrad`` (dL/dpool2)
   5. ``cnn_backward`` - unpool + ReLU masks, conv2 weight/input grads, conv1 weight grads (MFMA),
                         deterministic fixed-order reduction into the flat [K, P] gradient
-No autograd graph, no per-client Python loop; every buffer is sized [K, ...] once per shape.
+No autograd graph, no per-client Python loop, no library kernels; every buffer is sized [K, ...] once per shape.
+Evaluation (reference ``evaluate_model``, ``Classical_FL.py:83-102``) runs the same conv + fc1 kernels and
+``cnn_eval_head`` (logits, fused CE / argmax-hit sums).
 """
 from __future__ import annotations
 
@@ -51,20 +56,29 @@ class HipTinyCNN:
         return Xf, pool1, am1, pool2, am2
 
     def _fc1(self, params, pool2, K, B):
-        w = params[:, self.fc1w: self.fc1b].view(K, 64, 1568)
-        bias = params[:, self.fc1b: self.fc2w]
-        return torch.baddbmm(bias[:, None, :], pool2.view(K, B, 1568), w.transpose(1, 2)), w
+        """fc1 pre-activation partial sums [K, FC_KS, B, 64] (bias added by the heads)."""
+        C = ext()
+        h1p = self._buf("h1p", (K, C.cnn_fc1_splits(), B, 64))
+        C.cnn_fc1_forward(pool2, params, self.fc1w, K, B, h1p)
+        return h1p
 
     @torch.no_grad()
-    def logits(self, params: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
-        """Eval forward (no dropout): [K, B, C]."""
+    def logits(self, params: torch.Tensor, X: torch.Tensor, y: torch.Tensor | None = None):
+        """Eval forward (no dropout): logits [K, B, C]; with labels ``y`` [K, B] also the (CE sum, hits) float64
+        device scalars, summed per 64-sample block by the head and over the blocks here."""
         params = params.float().contiguous()
         K, B = X.shape[:2]
         _, _, _, pool2, _ = self.conv_forward(params, X)
-        h1, _ = self._fc1(params, pool2, K, B)
-        w2 = params[:, self.fc2w: self.fc2b].view(K, self.C, 64)
-        b2 = params[:, self.fc2b: self.fc2b + self.C]
-        return torch.baddbmm(b2[:, None, :], torch.relu(h1), w2.transpose(1, 2))
+        h1p = self._fc1(params, pool2, K, B)
+        C = ext()
+        out = torch.empty(K * B, self.C, dtype=torch.float32, device=self.device)
+        stats = self._buf("eval_stats", (K * C.cnn_eval_blocks(B), 2), torch.float64)
+        yy = y.reshape(-1).long().contiguous() if y is not None else None
+        C.cnn_eval_head(h1p, params, self.fc1b, self.fc2w, self.fc2b, self.C, K, B, yy, out, stats)
+        if y is None:
+            return out.view(K, B, self.C)
+        s = stats.sum(0)
+        return out.view(K, B, self.C), s[0], s[1]
 
     @torch.no_grad()
     def loss_and_grads(self, params: torch.Tensor, xb: torch.Tensor, yb: torch.Tensor, wts: torch.Tensor,
@@ -79,8 +93,7 @@ class HipTinyCNN:
         K, B = xb.shape[:2]
         S = K * B
         Xf, pool1, am1, pool2, am2 = self.conv_forward(params, xb)
-        w1 = params[:, self.fc1w: self.fc1b].view(K, 64, 1568)
-        h1 = torch.bmm(pool2.view(K, B, 1568), w1.transpose(1, 2))    # the head adds the fc1 bias
+        h1 = self._fc1(params, pool2, K, B)                            # partial sums; the head adds them + bias
         grad = torch.empty(K, self.P, dtype=torch.float32, device=self.device)   # every entry is written below
         dh1 = self._buf("dh1", (K, B, 64))
         dlog = self._buf("dlog", (S, 16))
@@ -96,7 +109,8 @@ class HipTinyCNN:
         C.cnn_head(h1, self.fc1b, m, dk, dst, dp, ds, params, self.fc2w, self.fc2b, self.C, K, B, yb.reshape(S).long().contiguous(),
                    wts.reshape(S).float().contiguous(), dh1, dlog, loss, correct, grad)
         C.cnn_fc1_wgrad(dh1, pool2, K, B, grad, self.fc1w)      # written straight into the gradient rows
-        dP2 = torch.bmm(dh1, w1).reshape(S, 1568).contiguous()
+        dP2 = self._buf("dP2", (S, 1568))
+        C.cnn_fc1_dgrad(dh1, params, self.fc1w, K, B, dP2)
         G = C.cnn_bwd_groups(K, B)
         part = self._buf("part", (K * G, C.cnn_partial_size()))
         C.cnn_backward(Xf, params, K, B, self.off_conv, pool1, am1, pool2, am2, dP2, part, grad)

@@ -68,6 +68,12 @@ class VQCEngine:
                 raise ValueError("amplitude-encoded initial states need a dense 2^n vector (n <= 26 with mps)")
             self.prog = MPSProgram(ops, coef, spec.n_qubits, self.device, chi_max=mps_chi)
             self.hip = None
+        elif backend == "density":
+            # exact density matrices with the Kraus gate channel (HIP kernel on a GPU, torch on CPU)
+            from .density import DensityProgram
+            kraus = noise.kraus() if (noise is not None and noise.gate_noise) else None
+            self.prog = DensityProgram(ops, coef, spec.n_qubits, spec.readout, self.device, kraus=kraus)
+            self.hip = None
         elif backend == "hip" and state_dtype in ("mfma", "fp16"):
             # fp16 states + MFMA group unitaries (ops/hea_mfma.py) for the hardware-efficient ansatz
             from .hea_mfma import HeaMfmaProgram
@@ -140,6 +146,11 @@ class VQCEngine:
         if self.backend == "hip":
             nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
             return self.hip.expz(xang, theta, nz, readout_keys, step, init)
+        if self.backend == "density":
+            if init is not None:
+                raise ValueError("the density-matrix simulator starts from |0><0| (angle feature maps)")
+            z = self.prog.expz(self._rows(xang, theta)).reshape(K, B, -1).float()
+            return self._readout(z, readout_keys, step)
         psi = self.prog.run(self._rows(xang, theta), state=self._init_rows(init))
         z = self.prog.expz(psi, self.spec.readout).reshape(K, B, -1).float()
         return self._readout(z, readout_keys, step)
@@ -180,6 +191,10 @@ class VQCEngine:
         th, a, b = spec.split(params)
         if method == "autograd" and self.backend == "mps":
             method = "adjoint"               # the MPS adjoint IS reverse-mode AD through the network
+        if method in ("adjoint", "autograd") and self.backend == "density":
+            # mixed states: the parameter-shift rule holds for exp(-i theta P / 2) rotations with channels that do
+            # not depend on theta in between; the statevector adjoint does not apply
+            method = "param_shift"
         if method == "autograd":
             return self._autograd(xang, y, wmask, params, init)
         K, B, _ = xang.shape
@@ -297,6 +312,7 @@ class VQCEngine:
         P = self.spec.n_theta
         R = 2 * P
         state_bytes = (self.spec.n_qubits * 2 * 8 * self.prog.chi_max ** 2 if self.backend == "mps"
+                       else self.prog.state_bytes() if self.backend == "density"
                        else (1 << self.spec.n_qubits) * 8)
         rows_per_chunk = max(1, min(K * R, self.state_budget_bytes() // max(1, B * state_bytes)))
         contrib_all = torch.zeros(K * R, dtype=torch.float64, device=params.device)

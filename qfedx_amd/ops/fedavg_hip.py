@@ -29,15 +29,20 @@ def dp_noise_keys(client_ids, round_num, seed) -> torch.Tensor:
 
 
 def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp, clip_norm,
-                       noise_multiplier, out=None, keys=None, pack=None):
+                       noise_multiplier, out=None, keys=None, pack=None, sat=None, secagg=None):
     """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as exact int64 fixed point (scale 2^32)
     [P+1] (per-client terms rounded before the sum -> rank-count invariant), plus norms [K].
     ``angle_mask`` uint8 [P] on the device; ``out`` an optional int64 [P+1] destination (e.g. the head
     of the round's all-reduce buffer).  DP noise keys are only built / uploaded when DP is on; ``keys``
     (device int32 [K, 2], ``dp_noise_keys``) passes them in already on the device, which keeps the launch
     free of host values that change per round (capturable into a round graph).  ``pack`` = (buf, loss,
-    correct, nvalid, act): ``out`` is the head of the round's [P + 5] all-reduce buffer ``buf`` and one more
-    block of the same launch packs the round metrics into its tail (what ``round_pack`` does on its own)."""
+    correct, nvalid, act): ``out`` is the head of the round's [P + 6] all-reduce buffer ``buf`` and one more
+    block of the same launch packs the round metrics into its tail (what ``round_pack`` does on its own).
+    ``sat``: int64 [1] device counter that receives the number of fixed-point terms clamped at 2^53 (with
+    ``pack``: ``buf[P + 5]``, zeroed by ``round_apply``; else a fresh zero counter).
+    ``secagg`` = (seeds int32 [K, N, 2], sign int32 [K, N], round int32 [1] device tensors, scale, bits): the
+    [P + 1] head holds SecAgg ring elements instead, each client's term masked in the kernel
+    (``SecureAggregator.round_tables``).  Returns (out, norms, sat)."""
     K, P = theta_k.shape
     dev = theta_k.device
     if dp and keys is not None:
@@ -53,11 +58,17 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
         out = torch.empty(P + 1, dtype=torch.int64, device=dev)
     if angle_mask.dtype != torch.uint8:
         angle_mask = angle_mask.to(torch.uint8)
+    if pack is not None:
+        sat = pack[0][P + 5: P + 6]
+    elif sat is None:
+        sat = torch.zeros(1, dtype=torch.int64, device=dev)
     if pack is None:
         e = _NO_PACK.setdefault(dev, (torch.zeros(0, dtype=torch.int64, device=dev),
                                       torch.zeros(0, dtype=torch.float32, device=dev)))
         pack = (e[0], e[1], e[1], e[1], e[1])
     ext().fedavg(theta_k.float().contiguous(), theta_g.float().contiguous(), angle_mask.contiguous(),
                  weights.double().contiguous(), norms, keys, bool(wrap), bool(dp), float(clip_norm),
-                 float(noise_multiplier) if dp else 0.0, out, *pack)
-    return out, (norms[:K] if dp else None)
+                 float(noise_multiplier) if dp else 0.0, out, *pack, sat,
+                 *((secagg[0].contiguous(), secagg[1].contiguous(), secagg[2].contiguous(), float(secagg[3]),
+                    int(secagg[4])) if secagg is not None else (None, None, None, 1.0, 48)))
+    return out, (norms[:K] if dp else None), sat

@@ -348,6 +348,14 @@ class HeaMfmaProgram:
                 with torch.cuda.stream(st):
                     self._step(x[r0:r1], p[k0:k1], yy[r0:r1], ww[r0:r1], k1 - k0, B, loss[k0:k1],
                                correct[k0:k1], grad[k0:k1], expz[r0 * C:r1 * C], None, None, step, f"c{i}", rec)
+                if i > 0:
+                    # allocated on the launching stream, used on this side stream: a later regrow of a workspace
+                    # must not hand its memory out while the side stream may still read it
+                    for name, t in self._ws.items():
+                        if name.startswith(f"c{i}"):
+                            t.record_stream(st)
+                    for t in (x, p, yy, ww, loss, correct, grad, expz):
+                        t.record_stream(st)
             for i in range(n - 1):
                 cur.wait_stream(self._stream(i))
         return {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}

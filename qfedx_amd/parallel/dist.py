@@ -27,6 +27,9 @@ import torch
 import torch.distributed as dist
 
 
+_OWN_PORT: list = []     # MASTER_PORT values picked here for single-rank groups
+
+
 @dataclass
 class World:
     rank: int = 0
@@ -41,19 +44,34 @@ class World:
 
     @property
     def distributed(self) -> bool:
-        return self.world_size > 1
+        """A process group exists: collectives run through it (also for ONE rank when a backend was named)."""
+        return self.backend != "none"
 
 
 def init_distributed(device: torch.device, backend: str = "auto", timeout_s: int = 600) -> World:
+    """This process's place in the job.  WORLD_SIZE > 1 (torchrun) always creates the process group; at
+    WORLD_SIZE = 1 a group is created only when ``backend`` is named explicitly ("nccl" / "gloo"): a
+    single-rank RCCL communicator then runs every collective of the round exactly as in an 8-GPU job (the
+    GPU tests use it to exercise the RCCL path on a one-GPU box); "auto" at one rank skips the group."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    if ws <= 1:
+    if ws <= 1 and backend == "auto":
         return World(0, 1, 0, "none", device)
     if backend == "auto":
         backend = "nccl" if device.type == "cuda" else "gloo"
+    if backend == "nccl" and device.type != "cuda":
+        raise ValueError("dist_backend=nccl (RCCL) needs a GPU device")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29500")
+    if "MASTER_PORT" not in os.environ:
+        if ws > 1:
+            os.environ["MASTER_PORT"] = "29500"
+        else:                               # a private single-rank group: any free local port
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            _OWN_PORT.append(os.environ["MASTER_PORT"])
     if not dist.is_initialized():
         kw = {}
         if backend == "nccl" and device.type == "cuda":
@@ -66,6 +84,9 @@ def init_distributed(device: torch.device, backend: str = "auto", timeout_s: int
 def shutdown(world: World) -> None:
     if world.distributed and dist.is_initialized():
         dist.destroy_process_group()
+    while _OWN_PORT:                          # the private single-rank port is not reused by a later group
+        if os.environ.get("MASTER_PORT") == _OWN_PORT.pop():
+            os.environ.pop("MASTER_PORT", None)
 
 
 def shard_clients(num_clients: int, world_size: int, rank: int) -> list[int]:

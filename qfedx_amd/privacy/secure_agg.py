@@ -16,7 +16,9 @@ Protocol (Bonawitz et al. style, single round, honest-but-curious server):
     seeds with the dropped client and the server removes the orphan masks (ROADMAP:91).
 
 PRG = Philox4x32-10 keyed by the pair seed, counter = (element/4, round) - the same generator the
-HIP aggregation kernel uses on device.
+HIP aggregation kernel uses on device: ``round_tables`` gives the fused FedAvg kernel
+(``csrc/train_kernels.hip``, ``secagg_masks``) every local client's pair-seed key words and mask signs for a
+round, and the kernel masks each client's encoded update itself (the round stays on the hipGraph path).
 """
 from __future__ import annotations
 
@@ -24,6 +26,7 @@ import hashlib
 import secrets
 from typing import Iterable, Optional
 
+import numpy as np
 import torch
 
 from ..utils.seeding import MASK32, derive_seed, philox4x32
@@ -147,6 +150,41 @@ class SecureAggregator:
         enc = encode_fixed(update, self.scale, self.bits)
         return torch.remainder(enc + self.client_mask(client, participants, round_num, update.numel(),
                                                       update.device).view_as(enc), self.modulus)
+
+    def seed_matrix(self, rows: Iterable[int], num_clients: int) -> np.ndarray:
+        """uint64 [len(rows), num_clients] pair seeds s_{i,j} of clients ``rows`` (held here) with every client j
+        (diagonal 0).  Pair seeds do not depend on the round, so they are derived once (modular exponentiations)
+        and cached."""
+        cache = self.__dict__.setdefault("_seed_rows", {})
+        out = np.zeros((len(list(rows)), num_clients), dtype=np.uint64)
+        for r, i in enumerate(rows):
+            i = int(i)
+            row = cache.get(i)
+            if row is None or row.shape[0] != num_clients:
+                row = np.array([self.registry.pair_seed(i, j) if j != i else 0 for j in range(num_clients)],
+                               dtype=np.uint64)
+                cache[i] = row
+            out[r] = row
+        return out
+
+    def round_tables(self, clients: list[int], participants: Iterable[int], dropped: Iterable[int],
+                     num_clients: int) -> tuple[torch.Tensor, torch.Tensor]:
+        """Device-kernel tables of one round for the masking clients ``clients`` (rows): pair-seed key words
+        int32 [K, N, 2] (lo, hi 32-bit halves) and mask signs int32 [K, N] over ALL N clients: +1 toward
+        participating peers j > i, -1 toward j < i, 0 for the client itself and non-participants.  A dropped
+        peer d's orphan mask is removed by the correction the survivors enable (``aggregate``); that exactly
+        cancels the survivor's mask toward d mod 2^bits, so its sign is 0 (net)."""
+        K = len(clients)
+        live = np.zeros(num_clients, dtype=bool)
+        live[[int(c) for c in participants]] = True
+        live[[int(d) for d in dropped]] = False
+        cid = np.asarray([int(c) for c in clients], dtype=np.int64)[:, None]
+        j = np.arange(num_clients, dtype=np.int64)[None, :]
+        sign = np.where(live[None, :] & (j != cid), np.where(j > cid, 1, -1), 0).astype(np.int32)
+        seeds = self.seed_matrix(clients, num_clients)
+        words = np.stack([seeds & np.uint64(0xFFFFFFFF), seeds >> np.uint64(32)], -1).astype(np.uint32)
+        return (torch.from_numpy(words.view(np.int32).reshape(K, num_clients, 2).copy()),
+                torch.from_numpy(sign.reshape(K, num_clients)))
 
     def aggregate(self, masked: list[torch.Tensor], survivors: list[int], dropped: Optional[list[int]] = None,
                   round_num: int = 0) -> torch.Tensor:

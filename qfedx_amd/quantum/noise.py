@@ -1,14 +1,16 @@
 """Quantum noise model (ROADMAP.md:64-73): ``NoiseConfig`` -> gate noise as stochastic
 Pauli trajectories, readout confusion and finite-shot sampling of the <Z> readout.
 
-Gate noise.  After every gate, each qubit it acts on passes through a single-qubit Pauli channel
-    rho -> (1 - px - py - pz) rho + px X rho X + py Y rho Y + pz Z rho Z
-    * depolarizing(p):         px = py = pz = p / 3
-    * amplitude damping(gamma): its Pauli twirl, px = py = gamma / 4,
-                                pz = (1 - gamma / 2 - sqrt(1 - gamma)) / 2
-      (exact amplitude-damping jumps are norm-dependent, i.e. need a reduction over the whole state
-      between gates; the twirled channel keeps every trajectory unitary, so the tiled kernels and
-      adjoint gradients apply unchanged - the approximation is documented, not hidden).
+Gate noise.  After every gate, each qubit it acts on passes through a single-qubit channel:
+    * ``depolarizing``(p):         Pauli channel px = py = pz = p / 3
+    * ``amplitude``(gamma):        EXACT amplitude damping, K0 = diag(1, sqrt(1 - gamma)), K1 = sqrt(gamma) |0><1|.
+                                   Its jumps are norm-dependent, so it runs on the density-matrix simulator
+                                   (ops/density.py, csrc/density.hip; <= 10 qubits, auto-selected)
+    * ``amplitude_twirl``(gamma):  the Pauli twirl of amplitude damping, px = py = gamma / 4,
+                                   pz = (1 - gamma / 2 - sqrt(1 - gamma)) / 2 - a unitary-trajectory
+                                   approximation for the statevector engines past density-matrix sizes
+Pauli channels run on the statevector engines as stochastic trajectories (exact in expectation); the density
+simulator applies any of the three as exact Kraus maps.
 A trajectory is realised by ``pauli`` ops (``Circuit.pauli``) whose per-sample selector 0/1/2/3 =
 I/X/Y/Z is an extra x-slot column drawn from Philox keyed by (seed, round, client, local step,
 sample, op): the statevector kernels execute it like any other 1-qubit gate, averaging over samples
@@ -31,16 +33,24 @@ import torch
 from ..utils.seeding import philox_key, philox_uniform_rows
 
 
+EXACT_ONLY = ("amplitude", "amplitude_damping", "amp")     # channels with no Pauli-trajectory realisation
+
+
 def pauli_probs(kind: str, p: float = 0.0, gamma: float = 0.0) -> tuple[float, float, float]:
+    """Pauli-channel probabilities of a noise kind the statevector trajectories realise exactly in expectation."""
     kind = (kind or "none").lower()
     if kind in ("none", "ideal", ""):
         return 0.0, 0.0, 0.0
     if kind in ("depolarizing", "depolarising", "dep"):
         return p / 3.0, p / 3.0, p / 3.0
-    if kind in ("amplitude", "amplitude_damping", "amp"):
+    if kind in ("amplitude_twirl", "amp_twirl"):
         pz = (1.0 - gamma / 2.0 - math.sqrt(max(0.0, 1.0 - gamma))) / 2.0
         return gamma / 4.0, gamma / 4.0, pz
-    raise ValueError(f"unknown noise kind '{kind}' (none | depolarizing | amplitude)")
+    if kind in EXACT_ONLY:
+        raise ValueError("exact amplitude damping is not a Pauli channel: it runs on the density-matrix simulator "
+                         "(model.simulator=density, <= 10 qubits); noise.kind=amplitude_twirl is its Pauli-twirl "
+                         "approximation for statevector trajectories")
+    raise ValueError(f"unknown noise kind '{kind}' (none | depolarizing | amplitude | amplitude_twirl)")
 
 
 @dataclass
@@ -53,19 +63,38 @@ class NoiseModel:
     shots: int = 0
     trajectories: int = 1
     seed: int = 0
+    kind: str = "none"
+    p: float = 0.0
+    gamma: float = 0.0
 
     @classmethod
     def from_config(cls, nc, seed: int = 0) -> Optional["NoiseModel"]:
         if nc is None:
             return None
-        px, py, pz = pauli_probs(nc.kind, nc.p, nc.gamma)
+        kind = (nc.kind or "none").lower()
+        px, py, pz = (0.0, 0.0, 0.0) if kind in EXACT_ONLY else pauli_probs(kind, nc.p, nc.gamma)
         m = cls(px, py, pz, float(nc.readout_p01), float(nc.readout_p10), int(nc.shots),
-                max(1, int(nc.trajectories)), seed)
+                max(1, int(nc.trajectories)), seed, kind, float(nc.p), float(nc.gamma))
         return m if (m.gate_noise or m.readout_noise) else None
 
     @property
+    def exact_only(self) -> bool:
+        """The gate channel has no Pauli-trajectory realisation (exact amplitude damping): density simulator."""
+        return self.kind in EXACT_ONLY and self.gamma > 0
+
+    @property
     def gate_noise(self) -> bool:
+        return self.px + self.py + self.pz > 0 or self.exact_only
+
+    @property
+    def pauli_noise(self) -> bool:
+        """Gate noise realised as Pauli trajectories on the statevector engines."""
         return self.px + self.py + self.pz > 0
+
+    def kraus(self):
+        """Kraus operators of the per-gate channel (ops/density.py)."""
+        from ..ops.density import kraus_ops
+        return kraus_ops(self.kind, self.p, self.gamma)
 
     @property
     def readout_noise(self) -> bool:
@@ -124,8 +153,10 @@ def _op_on(n: int, q: int, m: np.ndarray) -> np.ndarray:
     return out
 
 
-def density_expz(ops: np.ndarray, coef: np.ndarray, n: int, slots: np.ndarray, readout, probs) -> np.ndarray:
-    """Exact <Z_c> of the lowered program under the Pauli channel ``probs`` after every gate.
+def density_expz(ops: np.ndarray, coef: np.ndarray, n: int, slots: np.ndarray, readout, probs,
+                 kraus=None) -> np.ndarray:
+    """Exact <Z_c> of the lowered program with a channel after every gate on each qubit it touches: the Pauli
+    channel ``probs`` = (px, py, pz), or the Kraus operators ``kraus`` (list of 2 x 2) when given.
 
     ``ops``/``coef`` = the NOISELESS program (no ``pauli`` ops); ``slots`` = parameter row.
     """
@@ -135,6 +166,9 @@ def density_expz(ops: np.ndarray, coef: np.ndarray, n: int, slots: np.ndarray, r
     rho = np.zeros((dim, dim), complex)
     rho[0, 0] = 1.0
     px, py, pz = probs
+    if kraus is None:
+        kraus = [math.sqrt(max(0.0, 1 - px - py - pz)) * _PAULI[0], math.sqrt(px) * _PAULI[1],
+                 math.sqrt(py) * _PAULI[2], math.sqrt(pz) * _PAULI[3]]
     for (kind, q0, q1, slot), (sc, off) in zip(ops, coef):
         name = inv[int(kind)]
         ang = sc * (slots[slot] if slot >= 0 else 0.0) + off
@@ -152,11 +186,10 @@ def density_expz(ops: np.ndarray, coef: np.ndarray, n: int, slots: np.ndarray, r
             qs = (q0,)
         rho = U @ rho @ U.conj().T
         for q in qs:
-            acc = (1 - px - py - pz) * rho
-            for pr, P in ((px, _PAULI[1]), (py, _PAULI[2]), (pz, _PAULI[3])):
-                if pr:
-                    Pq = _op_on(n, q, P)
-                    acc = acc + pr * Pq @ rho @ Pq
+            acc = np.zeros_like(rho)
+            for K in kraus:
+                Kq = _op_on(n, q, K)
+                acc = acc + Kq @ rho @ Kq.conj().T
             rho = acc
     diag = np.real(np.diag(rho))
     idx = np.arange(dim)

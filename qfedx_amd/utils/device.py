@@ -77,14 +77,21 @@ class _PinnedRing:
 
 
 _RING = None
+_UPLOAD_BACKEND: list = []   # resolved once: [extension with host_alloc/host_upload] or [None]
 
 
 def _upload_ext():
-    try:
-        from ..ops._ext import ext
-        return ext()
-    except Exception:   # no extension (portable torch backend): plain pinned async copies
-        return None
+    """The extension's pinned-ring upload entry points, resolved ONCE per process (a failed import is not
+    retried per upload, and a stale build without ``host_alloc``/``host_upload`` takes the plain-copy path)."""
+    if not _UPLOAD_BACKEND:
+        try:
+            from ..ops._ext import ext
+            E = ext()
+            ok = hasattr(E, "host_alloc") and hasattr(E, "host_upload")
+        except Exception:   # no extension (portable torch backend): plain pinned async copies
+            E, ok = None, False
+        _UPLOAD_BACKEND.append(E if ok else None)
+    return _UPLOAD_BACKEND[0]
 
 
 def _upload(fill, nbytes: int, device, dst: torch.Tensor | None = None) -> torch.Tensor:

@@ -16,6 +16,10 @@ import torch
 
 
 class PhaseTimer:
+    # pending event pairs are folded into the totals once this many accumulate (bounded memory on long runs;
+    # a blocking drain only if the GPU is a further MAX_PENDING phases behind)
+    MAX_PENDING = 256
+
     def __init__(self, device: torch.device | str = "cpu", enabled: bool = True):
         self.device = torch.device(device)
         self.enabled = enabled
@@ -37,20 +41,31 @@ class PhaseTimer:
                 yield
                 e.record()
                 self._pending.append((name, s, e))
+                if len(self._pending) >= self.MAX_PENDING:
+                    self._drain(block=len(self._pending) >= 2 * self.MAX_PENDING)
             else:
                 t0 = time.perf_counter()
                 yield
                 self.totals[name] += (time.perf_counter() - t0) * 1e3
                 self.counts[name] += 1
 
+    def _drain(self, block: bool) -> None:
+        """Fold finished phases into the totals, oldest first.  Non-blocking: stops at the first phase whose
+        end event the GPU has not reached (``block``: waits for every pending phase)."""
+        if block and self._pending:
+            self._pending[-1][2].synchronize()
+        done = 0
+        for name, s, e in self._pending:
+            if not block and not e.query():
+                break
+            self.totals[name] += s.elapsed_time(e)
+            self.counts[name] += 1
+            done += 1
+        del self._pending[:done]
+
     def resolve(self) -> dict[str, float]:
         """Return accumulated milliseconds per phase (syncs once on GPU)."""
-        if self._pending:
-            self._pending[-1][2].synchronize()
-            for name, s, e in self._pending:
-                self.totals[name] += s.elapsed_time(e)
-                self.counts[name] += 1
-            self._pending.clear()
+        self._drain(block=True)
         return dict(self.totals)
 
     def reset(self) -> None:

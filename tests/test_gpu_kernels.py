@@ -253,13 +253,39 @@ def test_fedavg_launch_packs_round_metrics(cuda, dp):
     keys = torch.randint(0, 2 ** 31 - 1, (K, 2), generator=g, dtype=torch.int64).to(torch.int32).to(cuda)
     bufs = []
     for fused in (True, False):
-        buf = torch.full((P + 5,), 123, dtype=torch.int64, device=cuda)
+        buf = torch.full((P + 6,), 123, dtype=torch.int64, device=cuda)
+        buf[P + 5] = 0
         fedavg_hip.fused_local_reduce(tk, tg, w, mask, list(range(K)), 3, 9, True, dp, 0.8, 1.1, out=buf[: P + 1],
                                       keys=keys, pack=(buf, *mets) if fused else None)
         if not fused:
             ext().round_pack(buf, P, *mets)
         bufs.append(buf.cpu())
-    assert torch.equal(bufs[0], bufs[1])
+    assert torch.equal(bufs[0][: P + 5], bufs[1][: P + 5])
+    assert bufs[0][P + 5] == 0
+
+
+def test_fedavg_saturation_is_counted_not_wrapped(cuda):
+    """A fixed-point term past 2^53 (w * Delta > 2^21) is clamped and counted; round_apply reports the count
+    and zeroes the counter for the next round."""
+    from qfedx_amd.ops import fedavg_hip
+    from qfedx_amd.ops._ext import ext
+    K, P = 3, 70
+    tg = torch.zeros(P, device=cuda)
+    tk = torch.zeros(K, P, device=cuda)
+    tk[1, 5] = 1.0e4
+    tk[2, 6] = float("nan")
+    w = torch.tensor([1.0, 1.0e3, 1.0], dtype=torch.float64, device=cuda)   # 1e3 * 1e4 = 1e7 > 2^21
+    mask = torch.zeros(P, dtype=torch.uint8, device=cuda)
+    buf = torch.zeros(P + 6, dtype=torch.int64, device=cuda)
+    mets = [torch.zeros(4, device=cuda) for _ in range(4)]
+    fedavg_hip.fused_local_reduce(tk, tg, w, mask, [0, 1, 2], 0, 0, False, False, 1.0, 0.0, out=buf[: P + 1],
+                                  pack=(buf, *mets))
+    assert int(buf[P + 5]) == 2 and int(buf[5]) == 2 ** 53 and int(buf[6]) == 0
+    out = torch.zeros(6, dtype=torch.float64, device=cuda)
+    theta = torch.zeros(P, device=cuda)
+    ext().round_apply(buf, P, theta, 1.0, out, 0, 1.0)
+    torch.cuda.synchronize()
+    assert out[4].item() == 2.0 and int(buf[P + 5]) == 0
 
 
 def test_round_init_and_counter_pingpong(cuda):
@@ -298,3 +324,86 @@ def test_host_upload_ring_roundtrip(cuda):
     for t, w, it, w2, dv in outs:
         assert torch.equal(dv["t"].cpu(), t) and torch.equal(dv["w"].cpu(), w) and int(dv["b"].item()) == it
         assert torch.equal(w2.cpu(), w * 2)
+
+
+def test_padded_inactive_client_rows_mfma(cuda):
+    """MFMA engine, several local steps with clients that stop early (non-IID shard sizes) and a graph padded from
+    3 to 4 client rows (trainer.graph_bucket): the active rows are bitwise the eager, unpadded run's, and the
+    padding row is never touched (its params stay theta, its loss / hit columns stay zero)."""
+    from tests.test_fl import small_cfg
+    from qfedx_amd.data.datasets import build_federated_data
+    from qfedx_amd.fl.adapters import make_adapter
+    from qfedx_amd.fl.trainer import ShardStore, graph_bucket
+    dev = torch.device("cuda", 0)
+    cfg = small_cfg(n_qubits=10, n_layers=2, num_clients=7, samples_per_client=40, batch_size=8, local_epochs=2,
+                    device="cuda", backend="hip", partition_type="non_iid", alpha=0.3)
+    data = build_federated_data(cfg, clients=list(range(7)))
+    ad = make_adapter(cfg, dev, "hip")
+    assert ad.state_dtype == "mfma"
+    sizes = [40, 23, 9, 40, 17, 30, 40]               # unequal shards: clients run 10, 6 and 8 steps
+    store = ShardStore([(X[:n], y[:n]) for (X, y), n in zip(data.clients, sizes)], data.client_ids, dev)
+    theta = ad.init_params(cfg.train.seed).to(dev)
+    tr = ad.trainer
+    local = [0, 1, 5]
+    assert graph_bucket(len(local), len(store)) == 4
+    steps = sorted({int(store.counts[i]) for i in local})
+    assert len(steps) > 1                           # clients finish at different steps
+    outs = {}
+    for graphs in (True, False):
+        tr.graphs = graphs
+        outs[graphs] = []
+        for r in range(3):                            # the graph is replayed twice; its outputs are static buffers
+            rec = tr.run_round(store, local, theta, r)
+            outs[graphs].append((rec["params"][: len(local)].clone(), rec["loss"][:, : len(local)].clone(),
+                                 rec["correct"][:, : len(local)].clone()))
+    for (pg, lg, cg), (pe, le, ce) in zip(outs[True], outs[False]):
+        assert lg.shape[0] >= 3                       # several local steps
+        assert torch.equal(pg, pe) and torch.equal(lg, le) and torch.equal(cg, ce)
+    ent = next(reversed(tr._graph_cache.values()))
+    p_pad, loss_pad, corr_pad = ent["out"][0], ent["out"][1], ent["out"][2]
+    assert p_pad.shape[0] == 4
+    assert torch.equal(p_pad[3], theta.float())
+    assert not loss_pad[:, 3].any() and not corr_pad[:, 3].any()
+
+
+@pytest.mark.parametrize("dp", [False, True])
+def test_secagg_masks_in_fused_reduce_match_host_protocol(cuda, dp):
+    """SecAgg on the device (K18): the fused FedAvg kernel masks every local client's ring element with the pairwise
+    Philox masks itself.  Without DP the masked local sum is bitwise the host SecureAggregator's (mod 2^48),
+    including the orphan-mask correction of dropped peers on and off this rank; with DP (and angle wrap) the decoded
+    update matches to fixed-point resolution.  The round-apply kernel decodes the ring sum like finalize + apply."""
+    from qfedx_amd.fl.aggregator import Aggregator
+    from qfedx_amd.ops._ext import ext
+    from qfedx_amd.privacy.secure_agg import SecureAggregator
+    K, P, N = 5, 301, 30
+    g = torch.Generator().manual_seed(7)
+    tk = torch.randn(K, P, generator=g) * 0.3
+    tg = torch.randn(P, generator=g)
+    w = torch.rand(K, generator=g).double() * 40 + 1
+    mask = torch.zeros(P)
+    if dp:
+        mask[:100] = 1
+    ids = [3, 8, 11, 20, 29]                      # this rank's surviving clients
+    participants = [1, 2, 3, 7, 8, 11, 20, 25, 29]
+    dropped = [7, 25]                             # 7 was local, 25 on another rank
+    sa = SecureAggregator(123)
+    kw = dict(dp=dp, clip_norm=0.9, noise_multiplier=0.7, seed=5, secure_agg=True, secagg=sa, num_clients=N)
+    cpu = Aggregator(P, mask, "cpu", "torch", wrap=dp, **kw)
+    gpu = Aggregator(P, mask, cuda, "hip", wrap=dp, **kw)
+    a = cpu.local_reduce(tk, tg, w, 4, ids, participants=participants, dropped=dropped)
+    b = gpu.local_reduce(tk.to(cuda), tg.to(cuda), w.to(cuda), 4, ids, participants=participants, dropped=dropped)
+    m = (1 << sa.bits) - 1
+    if not dp:
+        assert torch.equal(b.cpu() & m, a & m)
+    ma, wa = cpu.finalize(a)
+    mb, wb = gpu.finalize(b.cpu())
+    assert abs(float(wa) - float(wb)) < 1e-6
+    assert torch.allclose(ma, mb, atol=4 / sa.scale)
+    # the round-apply decode (SecAgg ring) == finalize + apply
+    buf = torch.zeros(P + 6, dtype=torch.int64, device=cuda)
+    buf[: P + 1] = b
+    theta = tg.to(cuda).clone()
+    out = torch.zeros(6, dtype=torch.float64, device=cuda)
+    ext().round_apply(buf, P, theta, 1.0, out, sa.bits, sa.scale)
+    ref = gpu.apply(tg.to(cuda), mb.to(cuda), wsum=wb)
+    assert torch.equal(theta, ref) and abs(out[5].item() - float(wb)) < 1e-12

@@ -27,8 +27,9 @@ def _free_port() -> int:
 
 
 def _cfg(**kw):
-    return small_cfg(num_rounds=3, n_qubits=10, n_layers=2, num_clients=6, samples_per_client=32, batch_size=8,
-                     device="cuda", backend="hip", dist_backend="gloo", **kw)
+    base = dict(num_rounds=3, n_qubits=10, n_layers=2, num_clients=6, samples_per_client=32, batch_size=8,
+                device="cuda", backend="hip", dist_backend="gloo")
+    return small_cfg(**{**base, **kw})
 
 
 def _worker(rank, world, port, kw, out_path):
@@ -43,7 +44,10 @@ def _worker(rank, world, port, kw, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kw", [{}, dict(dp=True, client_fraction=0.5, deterministic_noise=True)])
+@pytest.mark.parametrize("kw", [{}, dict(dp=True, client_fraction=0.5, deterministic_noise=True),
+                                # CFed: the CNN backward's per-workgroup sample grouping depends on the batch only,
+                                # so 6 clients on one rank and 3 + 3 on two ranks sum gradients in the same order
+                                dict(kind="tinycnn", batch_size=32, samples_per_client=64, learning_rate=0.01)])
 def test_two_ranks_on_gpu_match_single_process(tmp_path, kw):
     """Clients sharded over 2 GPU ranks give the bitwise-same global model as one rank (exact fixed-point
     FedAvg; RNG keyed by client, never by rank)."""

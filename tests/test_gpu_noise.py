@@ -24,6 +24,7 @@ def test_philox_uniform_kernel_bitwise(cuda):
 
 
 def _noisy_setup(n, L, K, B, kind="depolarizing", p=0.2, gamma=0.2, readout=(0.0, 0.0), shots=0, seed=0):
+    kind = "amplitude_twirl" if kind == "amplitude" else kind
     px, py, pz = pauli_probs(kind, p, gamma)
     nm = NoiseModel(px, py, pz, readout[0], readout[1], shots)
     spec = VQCSpec(n, L, 3, readout_scale=2.0, init_std=1.0, noisy=nm.gate_noise)
@@ -83,3 +84,40 @@ def test_batched_param_shift_hip_matches_adjoint(cuda, n):
     eng._budget = (1 << n) * 8 * B * 5       # several chunks
     ps = eng.loss_and_grads(x, y, w, params, "param_shift")["grad"]
     assert torch.allclose(adj, ps, atol=3e-5)
+
+
+@pytest.mark.parametrize("n,kind,p,gamma", [(4, "amplitude", 0.0, 0.2), (6, "amplitude", 0.0, 0.1),
+                                            (7, "depolarizing", 0.05, 0.0), (8, "amplitude", 0.0, 0.05)])
+def test_density_kernel_matches_float64_kraus_oracle(cuda, n, kind, p, gamma):
+    """csrc/density.hip (rho in LDS up to 6 qubits, in a global slab beyond) == the float64 density-matrix oracle
+    with the exact Kraus channel after every gate (ROADMAP.md:66-73 amplitude damping)."""
+    import numpy as np
+    from qfedx_amd.ops.density import DensityProgram, kraus_ops
+    from qfedx_amd.quantum.noise import density_expz
+    spec = VQCSpec(n, 2, 3, init_std=1.0)
+    ops, coef = spec.program()
+    kr = kraus_ops(kind, p, gamma)
+    g = torch.Generator().manual_seed(n)
+    S = 3
+    rows = torch.cat([torch.randn(S, spec.n_theta, generator=g), torch.rand(S, n, generator=g) * 3], -1)
+    z = DensityProgram(ops, coef, n, spec.readout, cuda, kraus=kr).expz(rows.to(cuda)).cpu()
+    for s in range(S):
+        ref = density_expz(ops, coef, n, rows[s].double().numpy(), spec.readout, (0, 0, 0), kraus=kr)
+        assert np.allclose(z[s].numpy(), ref, atol=3e-5), (n, z[s], ref)
+
+
+def test_density_engine_param_shift_on_gpu_matches_cpu(cuda):
+    """Exact amplitude-damping VQC step on the HIP density kernel == the torch density path (parameter shift)."""
+    from qfedx_amd.quantum.noise import NoiseModel
+    nm = NoiseModel(kind="amplitude", gamma=0.1)
+    spec = VQCSpec(4, 2, 3, readout_scale=2.0, init_std=1.0)
+    g = torch.Generator().manual_seed(1)
+    x = spec.encode_features(torch.rand(2, 5, 4, generator=g))
+    y = torch.randint(0, 3, (2, 5), generator=g)
+    w = torch.full((2, 5), 0.2)
+    params = torch.stack([spec.init_params(k) for k in range(2)])
+    rg = VQCEngine(spec, cuda, "density", noise=nm).loss_and_grads(x.to(cuda), y.to(cuda), w.to(cuda),
+                                                                     params.to(cuda), "param_shift")
+    rc = VQCEngine(spec, "cpu", "density", noise=nm).loss_and_grads(x, y, w, params, "param_shift")
+    assert torch.allclose(rg["loss"].cpu(), rc["loss"], atol=2e-5)
+    assert torch.allclose(rg["grad"].cpu(), rc["grad"], atol=5e-5)

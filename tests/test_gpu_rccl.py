@@ -1,0 +1,67 @@
+"""The RCCL ("nccl") path on the one GPU of a test box: a single-rank RCCL communicator runs every collective of
+a federated round exactly as in an 8-GPU job (the broadcast of theta, the int64 fixed-point all-reduce of the
+round buffer, the metric all-reduces of the evaluation, barrier(device_ids) and max_over_ranks on a device
+tensor).  Each case runs in a child process so the process group never leaks into other tests."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from tests.test_fl import small_cfg
+from qfedx_amd.api import run_experiment
+from qfedx_amd.parallel.dist import init_distributed, shutdown, max_over_ranks, barrier
+import torch.distributed as dist
+
+def cfg(backend, **kw):
+    return small_cfg(num_rounds=3, n_qubits=10, n_layers=2, num_clients=6, samples_per_client=32, batch_size=8,
+                     device="cuda", backend="hip", dist_backend=backend, **kw)
+
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+kw = {kw}
+plain = run_experiment(cfg("auto", **kw), world=init_distributed(dev, "auto"), device=dev, backend="hip")
+world = init_distributed(dev, "nccl")
+assert world.distributed and world.backend == "nccl" and dist.get_backend() == "nccl", world
+rccl = run_experiment(cfg("nccl", **kw), world=world, device=dev, backend="hip")
+barrier(world)
+m = max_over_ranks(1.5, world)
+assert m == 1.5, m
+same = torch.equal(plain["params"].cpu(), rccl["params"].cpu()) and plain["accuracies"] == rccl["accuracies"]
+shutdown(world)
+print("RESULT", int(same))
+"""
+
+
+@pytest.mark.parametrize("kw", [{}, dict(dp=True, client_fraction=0.5, deterministic_noise=True),
+                                dict(kind="tinycnn", batch_size=32, samples_per_client=64, learning_rate=0.01)])
+def test_single_rank_rccl_round_matches_no_group(kw):
+    """The HIP round with a one-rank RCCL communicator is bitwise the run without a process group."""
+    code = _SCRIPT.format(root=ROOT, kw=repr(kw))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "RESULT 1" in r.stdout, r.stdout[-2000:]
+
+
+def test_bench_rccl_single_rank():
+    """bench.py with --dist-backend nccl at one GPU: the round's all-reduce, barrier and max-over-ranks go
+    through RCCL; the JSON line reports it, with the per-phase times and the precision fields."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist-backend", "nccl", "--qubits", "12",
+           "--clients", "8", "--batch", "8", "--steps", "3", "--warmup", "2"]
+    r = subprocess.run(cmd, cwd="/tmp", capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{") and '"metric"' in l]
+    assert len(recs) == 1
+    rec = recs[0]
+    assert rec["dist_backend"] == "nccl" and rec["engine"] == "mfma" and rec["value"] > 0
+    assert rec["comm_ms"] >= 0 and rec["local_train_ms"] > 0
+    assert rec["max_abs_err_expz"] < 5e-3 and rec["max_abs_err_grad"] < 5e-3 * max(1.0, rec["max_abs_grad"])

@@ -18,7 +18,7 @@ def _keys(n, purpose="noise_traj"):
     return torch.tensor([philox_key(7, purpose, 0, c) for c in range(n)], dtype=torch.int64)
 
 
-@pytest.mark.parametrize("kind,p,gamma", [("depolarizing", 0.15, 0.0), ("amplitude", 0.0, 0.3)])
+@pytest.mark.parametrize("kind,p,gamma", [("depolarizing", 0.15, 0.0), ("amplitude_twirl", 0.0, 0.3)])
 def test_trajectory_average_matches_density_matrix(kind, p, gamma):
     px, py, pz = pauli_probs(kind, p, gamma)
     nm = NoiseModel(px, py, pz)
@@ -119,3 +119,55 @@ def test_param_shift_with_shots_is_unbiased():
     # 400 samples x 64 shots per shifted circuit: the shot estimator is within a few sigma of exact
     assert torch.allclose(est, ref, atol=0.08), (est, ref)
     assert not torch.allclose(est, ref, atol=1e-6)
+
+
+@pytest.mark.parametrize("kind,p,gamma", [("amplitude", 0.0, 0.25), ("depolarizing", 0.1, 0.0),
+                                          ("amplitude_twirl", 0.0, 0.3)])
+def test_density_simulator_matches_float64_kraus_oracle(kind, p, gamma):
+    """ops/density.py (torch path, the CPU side of csrc/density.hip) == the float64 density-matrix oracle with the
+    channel's exact Kraus operators after every gate (ROADMAP.md:66-69)."""
+    from qfedx_amd.ops.density import DensityProgram, kraus_ops
+    spec = VQCSpec(4, 2, 3, init_std=1.0, entangler="ring")
+    ops, coef = spec.program()
+    kr = kraus_ops(kind, p, gamma)
+    prog = DensityProgram(ops, coef, 4, spec.readout, "cpu", kraus=kr)
+    g = torch.Generator().manual_seed(3)
+    rows = torch.cat([torch.randn(5, spec.n_theta, generator=g), torch.rand(5, 4, generator=g) * 3], -1).double()
+    z = prog.expz(rows)
+    for s in range(5):
+        ref = density_expz(ops, coef, 4, rows[s].numpy(), spec.readout, (0, 0, 0), kraus=kr)
+        assert np.allclose(z[s].numpy(), ref, atol=2e-6), (z[s], ref)
+
+
+def test_exact_amplitude_damping_differs_from_twirl_and_decays():
+    """Exact amplitude damping is not its Pauli twirl: |1> relaxes toward |0> (<Z> -> +1), which the twirl cannot
+    do (its fixed point is the maximally mixed state)."""
+    from qfedx_amd.ops.density import DensityProgram, kraus_ops
+    from qfedx_amd.quantum.circuit import Circuit
+    qc = Circuit(1)
+    qc.x(0)                                      # |1>, then 12 gates that leave populations alone
+    for _ in range(12):
+        qc.z(0)
+    ops, coef = qc.to_program({})
+    rows = torch.zeros(1, 1, dtype=torch.float64)
+    ex = DensityProgram(ops, coef, 1, [0], "cpu", kraus=kraus_ops("amplitude", gamma=0.3)).expz(rows)[0, 0]
+    tw = DensityProgram(ops, coef, 1, [0], "cpu", kraus=kraus_ops("amplitude_twirl", gamma=0.3)).expz(rows)[0, 0]
+    assert abs(float(ex) - (1 - 2 * 0.7 ** 13)) < 1e-6 and abs(float(tw) + 0.7 ** 13) < 1e-6
+
+
+def test_amplitude_noise_config_uses_density_simulator_and_trains():
+    """noise.kind=amplitude selects the exact density-matrix simulator (parameter-shift gradients) and a short
+    federated run trains; the twirl keeps the statevector trajectories."""
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.fl.adapters import make_adapter
+    from tests.test_fl import small_cfg
+    cfg = small_cfg(num_rounds=2, kind="vqc", n_qubits=3, n_layers=1, num_clients=2, samples_per_client=24,
+                    batch_size=12, grad_method="param_shift", optimizer="sgd")
+    cfg.noise.kind, cfg.noise.gamma = "amplitude", 0.05
+    ad = make_adapter(cfg, torch.device("cpu"), "torch")
+    assert ad.simulator == "density" and ad.engine.backend == "density" and not ad.spec.noisy
+    out = run_experiment(cfg)
+    assert len(out["accuracies"]) == 3 and all(np.isfinite(out["accuracies"]))
+    cfg.noise.kind = "amplitude_twirl"
+    ad2 = make_adapter(cfg, torch.device("cpu"), "torch")
+    assert ad2.simulator == "statevector" and ad2.spec.noisy

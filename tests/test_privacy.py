@@ -149,3 +149,35 @@ def test_noise_seed_secret_vs_deterministic():
     from qfedx_amd.privacy.dp import draw_noise_seed
     assert draw_noise_seed(World(), True, 42) == 42
     assert draw_noise_seed(World()) != draw_noise_seed(World())
+
+
+def test_secagg_round_tables_reproduce_host_masks():
+    """The device kernel's SecAgg tables (pair-seed key words + net mask signs): summing sign * PRG(seed) over them
+    equals the host protocol's total mask of the surviving local clients plus the orphan-mask corrections of the
+    dropped peers (mod 2^48) - the kernel side of K18, checked on the CPU."""
+    import numpy as np
+    from qfedx_amd.privacy.secure_agg import SecureAggregator, prg_mask
+    sa = SecureAggregator(77)
+    N, P, r = 12, 37, 5
+    parts = [0, 2, 3, 5, 6, 9, 11]
+    dropped = [5, 11]
+    ids = [2, 3, 6]                                   # surviving clients of this rank
+    seeds, sign = sa.round_tables(ids, parts, dropped, N)
+    assert seeds.shape == (3, N, 2) and sign.shape == (3, N) and seeds.dtype == torch.int32
+    mod = sa.modulus
+    dev = torch.zeros(P, dtype=torch.int64)
+    for k in range(len(ids)):
+        for j in range(N):
+            if int(sign[k, j]):
+                lo, hi = (int(x) & 0xFFFFFFFF for x in seeds[k, j])
+                dev = dev + int(sign[k, j]) * prg_mask(lo | (hi << 32), r, P, sa.bits)
+    host = torch.zeros(P, dtype=torch.int64)
+    for c in ids:
+        host = host + sa.client_mask(c, parts, r, P)
+    for d in dropped:
+        for c in ids:
+            m = prg_mask(sa.registry.pair_seed(c, d), r, P, sa.bits)
+            host = host - m if c < d else host + m
+    assert torch.equal(torch.remainder(dev, mod), torch.remainder(host, mod))
+    assert int(sign[0, 2]) == 0 and int(sign[0, 5]) == 0 and int(sign[0, 1]) == 0   # self, dropped, absent
+    assert int(sign[0, 3]) == 1 and int(sign[1, 2]) == -1
