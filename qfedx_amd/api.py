@@ -26,7 +26,8 @@ def run_experiment(cfg: ExperimentConfig, world=None, device=None, backend=None)
     set_seeds(cfg.train.seed)
     if world is None:
         device, backend, world = setup(cfg)
-    my_clients = shard_clients(cfg.data.num_clients, world.world_size, world.rank)
+    n_clients = 1 if getattr(cfg.train, "mode", "federated") == "centralized" else cfg.data.num_clients
+    my_clients = shard_clients(n_clients, world.world_size, world.rank)
     data = build_federated_data(cfg, clients=my_clients)
     adapter = make_adapter(cfg, device, backend)
     runner = FederatedRunner(cfg, adapter, data, world, device, backend)

@@ -20,7 +20,7 @@ import yaml
 
 @dataclass
 class DataConfig:
-    dataset: str = "synthetic"          # mnist | synthetic | iris
+    dataset: str = "synthetic"          # mnist | synthetic | synthetic_digits (MNIST-like images) | iris
     raw_folder: str = "./dataset/raw"
     processed_folder: str = "./dataset/processed"
     digits: tuple = (0, 1, 2)
@@ -56,6 +56,8 @@ class ModelConfig:
 @dataclass
 class TrainConfig:
     num_rounds: int = 30
+    mode: str = "federated"             # federated | centralized (all shards pooled into one client: the
+                                        # ROADMAP.md:109 centralized-VQC baseline)
     local_epochs: int = 1
     local_steps: int = 0                # if >0, overrides local_epochs with a fixed step count
     learning_rate: float = 0.05
@@ -116,6 +118,9 @@ class RuntimeConfig:
     log_every: int = 5
     overlap_comm: bool = True
     use_graphs: bool = True            # hipGraph capture of the local round (HIP backend)
+    log_client_norms: bool = True      # DP rounds: every client's pre-clip update norm reaches every rank in the
+                                       # round all-reduce (CC6); clip fraction + norm quantiles per round (not
+                                       # under SecAgg, where per-client statistics would leak)
 
 
 @dataclass

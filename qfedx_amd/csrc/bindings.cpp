@@ -66,7 +66,7 @@ int qfx_grad_split(int tps, int spc);
 int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct, const float* nvalid,
                           const float* act, int n, hipStream_t st);
 int qfx_launch_round_apply(long long* buf, int P, float* theta, double lr, double* out, int bits,
-                           double ring_scale, hipStream_t st);
+                           double ring_scale, int n_norms, hipStream_t st);
 int qfx_fedavg_norm_scratch(int K, int P);
 int qfx_launch_adam(float* p, const float* g, float* m, float* v, const float* t_in, float* t_out,
                     const float* active, int K, int P, float lr, float b1, float b2, float eps, hipStream_t st);
@@ -87,7 +87,7 @@ int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned
                       float clip, float sigma, long long* out, long long* pack_buf, const float* loss,
                       const float* correct, const float* nvalid, const float* act, int n_metrics, long long* sat,
                       const uint32_t* sa_seeds, const int* sa_sign, const int* sa_round, int sa_n, double sa_scale,
-                      int sa_bits, hipStream_t st);
+                      int sa_bits, long long* sa_masks, const int* norm_cid, hipStream_t st);
 }
 
 namespace qfx_runtime {
@@ -231,14 +231,16 @@ void round_pack(torch::Tensor buf, int64_t P, torch::Tensor loss, torch::Tensor 
 }
 
 // bits > 0: the update / weight entries are SecAgg ring elements (Z_2^bits, scale ring_scale)
+// n_norms: per-client norm slots buf[P + 6 ..] (CC6) copied to out[6 ..] and zeroed
 void round_apply(torch::Tensor buf, int64_t P, torch::Tensor theta, double lr, torch::Tensor out, int64_t bits,
-                 double ring_scale) {
+                 double ring_scale, int64_t n_norms) {
   need(buf, torch::kInt64, "buf");
   need(theta, torch::kFloat32, "theta");
   need(out, torch::kFloat64, "out");
-  if (buf.numel() < P + 6 || theta.numel() < P || out.numel() < 6) throw std::invalid_argument("round_apply: sizes");
+  if (buf.numel() < P + 6 + n_norms || theta.numel() < P || out.numel() < 6 + n_norms)
+    throw std::invalid_argument("round_apply: sizes");
   check(qfx_launch_round_apply(ptr<long long>(buf), (int)P, ptr<float>(theta), lr, ptr<double>(out), (int)bits,
-                               ring_scale, cur_stream()),
+                               ring_scale, (int)n_norms, cur_stream()),
         "qfx_round_apply");
 }
 
@@ -393,7 +395,7 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
             torch::Tensor out, torch::Tensor pack_buf, torch::Tensor loss, torch::Tensor correct,
             torch::Tensor nvalid, torch::Tensor act, torch::Tensor sat, c10::optional<torch::Tensor> sa_seeds,
             c10::optional<torch::Tensor> sa_sign, c10::optional<torch::Tensor> sa_round, double sa_scale,
-            int64_t sa_bits) {
+            int64_t sa_bits, c10::optional<torch::Tensor> sa_masks, c10::optional<torch::Tensor> norm_cid) {
   need(theta_k, torch::kFloat32, "theta_k");
   need(sat, torch::kInt64, "sat");
   if (sat.numel() < 1) throw std::invalid_argument("fedavg: sat counter missing");
@@ -430,6 +432,15 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
     if (sa_seeds->numel() < (int64_t)K * sa_n * 2 || sa_round->numel() < 1)
       throw std::invalid_argument("fedavg: SecAgg table sizes");
     if (sa_bits < 2 || sa_bits > 62 || !(sa_scale > 0)) throw std::invalid_argument("fedavg: SecAgg bits / scale");
+    if (!sa_masks.has_value()) throw std::invalid_argument("fedavg: SecAgg needs a [K, P + 1] mask workspace");
+    need(*sa_masks, torch::kInt64, "sa_masks");
+    if (sa_masks->numel() < (int64_t)K * (P + 1)) throw std::invalid_argument("fedavg: SecAgg mask workspace size");
+  }
+  // CC6: global client ids [K] int32 of the rows; the pack block scatters the DP norms into buf[P + 6 + cid]
+  const bool nc = norm_cid.has_value() && norm_cid->defined() && norm_cid->numel() > 0;
+  if (nc) {
+    need(*norm_cid, torch::kInt32, "norm_cid");
+    if (!pack || !dp || norm_cid->numel() < K) throw std::invalid_argument("fedavg: norm slots need pack + DP + [K] ids");
   }
   check(qfx_launch_fedavg(ptr<float>(theta_k), ptr<float>(theta_g), ptr<unsigned char>(angle_mask),
                           ptr<double>(weights), ptr<double>(norms), ptr<uint32_t>(keys), K, P, wrap ? 1 : 0,
@@ -438,7 +449,8 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
                           pack ? ptr<float>(correct) : nullptr, pack ? ptr<float>(nvalid) : nullptr,
                           pack ? ptr<float>(act) : nullptr, (int)n, ptr<long long>(sat),
                           sa ? ptr<uint32_t>(*sa_seeds) : nullptr, sa ? ptr<int>(*sa_sign) : nullptr,
-                          sa ? ptr<int>(*sa_round) : nullptr, sa_n, sa_scale, (int)sa_bits, cur_stream()),
+                          sa ? ptr<int>(*sa_round) : nullptr, sa_n, sa_scale, (int)sa_bits,
+                          sa ? ptr<long long>(*sa_masks) : nullptr, nc ? ptr<int>(*norm_cid) : nullptr, cur_stream()),
         "qfx_fedavg");
 }
 

@@ -1022,14 +1022,14 @@ extern "C" int qfx_cnn_forward(const float* X, const float* params, int P, int K
   return (int)hipGetLastError();
 }
 
-// Samples per backward workgroup: a function of the client batch B ONLY (a quarter of it, a power of two,
-// at most BS_MAX).  The workgroup accumulates its samples' weight gradients in MFMA registers and cnn_reduce
+// Samples per backward workgroup: a function of the client batch B ONLY (half of it, a power of two, at most
+// BS_MAX: B = 32 -> 16, two workgroups per client).  The workgroup accumulates its samples' weight gradients in MFMA registers and cnn_reduce
 // sums the per-workgroup partials in fixed order, so the grouping fixes the fp32 summation order: choosing
 // it from the per-rank client count or the CU count (as round 2 did) made a client's gradient depend on how
 // many clients share its rank, breaking the bitwise rank-count invariance of the federated result.
 static int bwd_bs(int /*K*/, int B) {
   int bs = 1;
-  while (bs * 2 <= BS_MAX && bs * 2 * 4 <= B) bs *= 2;
+  while (bs * 2 <= BS_MAX && bs * 2 * 2 <= B) bs *= 2;
   return bs;
 }
 

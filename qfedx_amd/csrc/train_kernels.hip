@@ -348,6 +348,12 @@ struct RoundPack {          // metrics of the round epilogue (buf == nullptr: no
   long long* buf;
   const float *loss, *correct, *nvalid, *act;
   int n;
+  // CC6: the K local clients' update norms (DP: pre-clip l2 norms) scattered as 2^32 fixed point into the
+  // buffer's per-client slots buf[P + 6 + cid[k]] (zero elsewhere on this rank): the round's SUM all-reduce then
+  // delivers every client's norm to every rank with no extra collective.  norms == nullptr: not logged.
+  const double* norms;
+  const int* cid;
+  int K;
 };
 
 __device__ __forceinline__ void round_pack_block(const RoundPack& rp, int P) {
@@ -372,6 +378,8 @@ __device__ __forceinline__ void round_pack_block(const RoundPack& rp, int P) {
     __syncthreads();
   }
   if (t < 4) rp.buf[P + 1 + t] = llrint(red[t][0] * 4294967296.0);
+  if (rp.norms)
+    for (int k = t; k < rp.K; k += 256) rp.buf[P + 6 + rp.cid[k]] = llrint(rp.norms[k] * 4294967296.0);
 }
 
 // out[e] = sum_k round(2^32 * w_k * priv(wrap(theta_k[e] - theta_g[e]))), out[P] = sum_k round(2^32 w_k)
@@ -396,22 +404,36 @@ struct SecAgg {
   int N;
   double scale;
   long long mask;            // 2^bits - 1
+  long long* masks;          // [K][P + 1] each client's total pair mask per element (qfx_secagg_mask_kernel)
 };
 
-__device__ __forceinline__ long long secagg_masks(const SecAgg& sa, int k, long e) {
+// Every client's total pair mask, one thread per (client, element pair): one Philox block per peer yields the 48-bit
+// values of elements 2 b and 2 b + 1 (prg_mask's layout), so the K x N x (P + 1) / 2 generator calls - the work
+// each client would do on its own device - spread over the whole GPU.
+__global__ void __launch_bounds__(256) qfx_secagg_mask_kernel(SecAgg sa, int P) {
+  const int k = blockIdx.y;
+  const long b = (long)blockIdx.x * 256 + threadIdx.x;      // element pair
+  const long e0 = 2 * b;
+  if (e0 > P) return;
   const uint32_t rnd = (uint32_t)sa.round[0];
-  const uint64_t blk = (uint64_t)e >> 1;
-  long long acc = 0;
+  long long a0 = 0, a1 = 0;
   for (int j = 0; j < sa.N; ++j) {
     const int sg = sa.sign[(size_t)k * sa.N + j];
     if (sg == 0) continue;
     const uint32_t* key = sa.seeds + ((size_t)k * sa.N + j) * 2;
-    const u32x4 o = philox4x32_10({(uint32_t)blk, (uint32_t)(blk >> 32), rnd, 0x5ECu}, key[0], key[1]);
-    const uint64_t w = (e & 1) ? ((uint64_t)o.w << 32 | o.z) : ((uint64_t)o.y << 32 | o.x);
-    const long long m = (long long)(w & (uint64_t)sa.mask);
-    acc += sg > 0 ? m : -m;
+    const u32x4 o = philox4x32_10({(uint32_t)b, (uint32_t)((uint64_t)b >> 32), rnd, 0x5ECu}, key[0], key[1]);
+    const long long m0 = (long long)(((uint64_t)o.y << 32 | o.x) & (uint64_t)sa.mask);
+    const long long m1 = (long long)(((uint64_t)o.w << 32 | o.z) & (uint64_t)sa.mask);
+    a0 += sg > 0 ? m0 : -m0;
+    a1 += sg > 0 ? m1 : -m1;
   }
-  return acc;
+  long long* row = sa.masks + (size_t)k * (P + 1);
+  row[e0] = a0;
+  if (e0 + 1 <= P) row[e0 + 1] = a1;
+}
+
+__device__ __forceinline__ long long secagg_masks(const SecAgg& sa, int k, long e, int P) {
+  return sa.masks[(size_t)k * (P + 1) + e];
 }
 
 // one client's fixed-point FedAvg term of parameter e.  A term is held to |v| <= FA_SAT = 2^53 (exactly
@@ -420,7 +442,7 @@ __device__ __forceinline__ long long secagg_masks(const SecAgg& sa, int k, long 
 constexpr double FA_SAT = 9007199254740992.0;
 __device__ __forceinline__ long long fedavg_term(float x, double tg, bool wr, int k, long e, const double* weights,
                                                  const double* norms, const uint32_t* keys, int dp, float clip,
-                                                 float sigma, int& nsat, const SecAgg& sa) {
+                                                 float sigma, int& nsat, const SecAgg& sa, int sa_P) {
   const double SC = 4294967296.0;
   double d = (double)x - tg;
   if (wr) d = wrap_pi(d);
@@ -438,7 +460,7 @@ __device__ __forceinline__ long long fedavg_term(float x, double tg, bool wr, in
       ++nsat;
       v = v > 0.0 ? lim : (v < 0.0 ? -lim : 0.0);
     }
-    return ((long long)llrint(v) & sa.mask) + secagg_masks(sa, k, e);
+    return ((long long)llrint(v) & sa.mask) + secagg_masks(sa, k, e, sa_P);
   }
   double v = weights[k] * d * SC;
   if (!(fabs(v) <= FA_SAT)) {          // also catches NaN (clamped to 0)
@@ -474,7 +496,7 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
       if (sa.seeds) {                  // the weight is element P of the client's masked vector
         const double v = weights[k] * sa.scale, lim = (double)(sa.mask >> 1);
         if (!(fabs(v) <= lim)) ++wsat;
-        ws += ((long long)llrint(fmin(fmax(v, -lim), lim)) & sa.mask) + secagg_masks(sa, k, P);
+        ws += ((long long)llrint(fmin(fmax(v, -lim), lim)) & sa.mask) + secagg_masks(sa, k, P, P);
         continue;
       }
       const double v = weights[k] * SC;
@@ -496,10 +518,10 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
       for (int u = 0; u < FA_U; ++u) x[u] = theta_k[(size_t)(k + u * FA_G) * P + e];
 #pragma unroll
       for (int u = 0; u < FA_U; ++u)
-        acc += fedavg_term(x[u], tg, wr, k + u * FA_G, e, weights, norms, keys, dp, clip, sigma, nsat, sa);
+        acc += fedavg_term(x[u], tg, wr, k + u * FA_G, e, weights, norms, keys, dp, clip, sigma, nsat, sa, P);
     }
     for (; k < K; k += FA_G)
-      acc += fedavg_term(theta_k[(size_t)k * P + e], tg, wr, k, e, weights, norms, keys, dp, clip, sigma, nsat, sa);
+      acc += fedavg_term(theta_k[(size_t)k * P + e], tg, wr, k, e, weights, norms, keys, dp, clip, sigma, nsat, sa, P);
   }
   // saturated terms are counted (an integer: the count is exact in any order); the host raises on a nonzero
   // count when it reads the round's metrics back (self-cleaning: round_apply zeroes it after the all-reduce)
@@ -530,7 +552,7 @@ __device__ __forceinline__ double ring_decode(long long v, int bits, double scal
 }
 
 __global__ void qfx_round_apply_kernel(long long* __restrict__ buf, int P, float* __restrict__ theta, double lr,
-                                       double* __restrict__ out, int bits, double ring_scale) {
+                                       double* __restrict__ out, int bits, double ring_scale, int n_norms) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const double SC = 4294967296.0;
   const double wsum = bits ? ring_decode(buf[P], bits, ring_scale) : (double)buf[P] / SC;
@@ -549,6 +571,10 @@ __global__ void qfx_round_apply_kernel(long long* __restrict__ buf, int P, float
     } else {
       out[j] = wsum;
     }
+  } else if (e < P + 6 + n_norms) {    // CC6 per-client norm slots: read out, zeroed for the next round
+    const int j = (int)(e - P);
+    out[j] = (double)buf[P + j] / SC;
+    buf[P + j] = 0;
   }
 }
 
@@ -560,15 +586,16 @@ extern "C" int qfx_fedavg_norm_scratch(int K, int P) { return K * (1 + (P + NORM
 
 extern "C" int qfx_launch_round_pack(long long* buf, int P, const float* loss, const float* correct,
                                      const float* nvalid, const float* act, int n, hipStream_t st) {
-  hipLaunchKernelGGL(qfx_round_pack_kernel, dim3(1), dim3(256), 0, st, RoundPack{buf, loss, correct, nvalid, act, n}, P);
+  hipLaunchKernelGGL(qfx_round_pack_kernel, dim3(1), dim3(256), 0, st,
+                     RoundPack{buf, loss, correct, nvalid, act, n, nullptr, nullptr, 0}, P);
   return (int)hipGetLastError();
 }
 
 extern "C" int qfx_launch_round_apply(long long* buf, int P, float* theta, double lr, double* out, int bits,
-                                      double ring_scale, hipStream_t st) {
-  if (bits < 0 || bits > 62) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(qfx_round_apply_kernel, dim3((unsigned)((P + 6 + 255) / 256)), dim3(256), 0, st, buf, P, theta,
-                     lr, out, bits, ring_scale);
+                                      double ring_scale, int n_norms, hipStream_t st) {
+  if (bits < 0 || bits > 62 || n_norms < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(qfx_round_apply_kernel, dim3((unsigned)((P + 6 + n_norms + 255) / 256)), dim3(256), 0, st, buf,
+                     P, theta, lr, out, bits, ring_scale, n_norms);
   return (int)hipGetLastError();
 }
 
@@ -804,7 +831,8 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                                  int wrap, int dp, float clip, float sigma, long long* out, long long* pack_buf,
                                  const float* loss, const float* correct, const float* nvalid, const float* act,
                                  int n_metrics, long long* sat, const uint32_t* sa_seeds, const int* sa_sign,
-                                 const int* sa_round, int sa_n, double sa_scale, int sa_bits, hipStream_t st) {
+                                 const int* sa_round, int sa_n, double sa_scale, int sa_bits, long long* sa_masks,
+                                 const int* norm_cid, hipStream_t st) {
   if (dp) {   // clipping needs the per-client norms; without DP they are not computed
     const int nc = (P + NORM_CHUNK - 1) / NORM_CHUNK;
     double* partial = norms + K;   // scratch tail of the norms buffer: K * nc doubles
@@ -812,10 +840,15 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                        wrap, partial);
     hipLaunchKernelGGL(qfx_delta_norm_final_kernel, dim3((K + 63) / 64), dim3(64), 0, st, partial, nc, K, norms);
   }
-  const RoundPack rp{pack_buf, loss, correct, nvalid, act, n_metrics};
+  const RoundPack rp{pack_buf, loss, correct, nvalid, act, n_metrics, (dp && norm_cid) ? norms : nullptr, norm_cid, K};
+  const SecAgg sa{sa_seeds, sa_sign, sa_round, sa_n, sa_scale, sa_seeds ? (1LL << sa_bits) - 1 : 0, sa_masks};
+  if (sa_seeds) {
+    if (!sa_masks) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(qfx_secagg_mask_kernel, dim3((unsigned)(((P + 2) / 2 + 255) / 256), (unsigned)K), dim3(256), 0,
+                       st, sa, P);
+  }
   const unsigned blocks = (unsigned)((P + FA_E - 1) / FA_E) + (pack_buf ? 1u : 0u);
   hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3(blocks), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
-                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out, rp, sat,
-                     SecAgg{sa_seeds, sa_sign, sa_round, sa_n, sa_scale, sa_seeds ? (1LL << sa_bits) - 1 : 0});
+                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out, rp, sat, sa);
   return (int)hipGetLastError();
 }

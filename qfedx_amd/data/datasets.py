@@ -108,12 +108,51 @@ def load_synthetic_images_federated(num_clients: int, n_classes: int, samples_pe
     return FederatedData(shards, ids, (Xt, torch.from_numpy(yt)), n_classes, 28 * 28, num_clients)
 
 
+def load_synthetic_digits_federated(num_clients: int, n_classes: int, samples_per_client: int, test_samples: int,
+                                    alpha: float, seed: int, features: str, n_features: int, images: bool,
+                                    clients: Optional[list[int]] = None) -> FederatedData:
+    """Synthetic MNIST-like digit images (the images of MNIST are absent offline), the SAME shards for the TinyCNN
+    (images) and the VQC (``features``, e.g. PCA to n_qubits, fitted on the full training set) - the data of the
+    ROADMAP.md:104-109 VQC vs classical-FL comparison."""
+    base = load_synthetic_images_federated(num_clients, n_classes, samples_per_client, test_samples, alpha, seed,
+                                           clients)
+    if images:
+        return base
+    every = synthetic_images_shards(num_clients, n_classes, samples_per_client, alpha, seed)
+    _, tf = make_features(torch.cat([x for x, _ in every]), features, n_features)
+    shards = [(make_features(x, features, n_features, tf)[0], y) for x, y in base.clients]
+    Xt, yt = base.test
+    return FederatedData(shards, base.client_ids, (make_features(Xt, features, n_features, tf)[0], yt), n_classes,
+                         n_features, num_clients, tf)
+
+
+def pool_clients(data: FederatedData, keep: bool) -> FederatedData:
+    """Centralized baseline (ROADMAP.md:109): every client's shard pooled into ONE client (id 0), held by the
+    rank with ``keep``; FedAvg over one client trained on all the data is centralized training, and the round
+    loop, optimizer, DP and evaluation stay exactly those of the federated runs it is compared with."""
+    X = torch.cat([x for x, _ in data.clients]) if data.clients else None
+    y = torch.cat([t for _, t in data.clients]) if data.clients else None
+    clients = [(X, y)] if keep else []
+    return FederatedData(clients, [0] if keep else [], data.test, data.n_classes, data.n_features, 1,
+                         data.transformer)
+
+
 def build_federated_data(cfg, clients: Optional[list[int]] = None, images: bool = False) -> FederatedData:
-    """Dispatch on ``cfg.data.dataset`` (ExperimentConfig)."""
+    """Dispatch on ``cfg.data.dataset`` (ExperimentConfig).  ``train.mode=centralized`` pools every client's
+    shard into one client (``pool_clients``); ``clients`` then only says whether this rank holds it (rank 0)."""
+    if getattr(cfg.train, "mode", "federated") == "centralized":
+        import copy
+        c2 = copy.deepcopy(cfg)
+        c2.train.mode = "federated"
+        return pool_clients(build_federated_data(c2, None, images), clients is None or 0 in clients)
     d, m, t = cfg.data, cfg.model, cfg.train
     non_iid = d.partition_type.lower() != "iid"
     amp = getattr(m, "kind", "vqc") == "vqc" and str(getattr(m, "feature_map", "")).lower() == "amplitude"
     nf = d.n_features if d.n_features > 0 else ((1 << m.n_qubits) if amp else m.n_qubits)
+    if d.dataset == "synthetic_digits":
+        return load_synthetic_digits_federated(d.num_clients, m.n_classes, d.samples_per_client, d.test_samples,
+                                               d.alpha, t.seed, d.features, nf, images or m.kind == "tinycnn",
+                                               clients)
     if d.dataset == "synthetic":
         if images or m.kind == "tinycnn":
             return load_synthetic_images_federated(d.num_clients, m.n_classes, d.samples_per_client,

@@ -8,6 +8,8 @@ A grid spec (YAML)::
       model.n_qubits: [2, 4, 8]
       privacy.noise_multiplier: [0.5, 1.0, 2.0]
     fixed: {privacy.dp: true}         # overrides applied to every run
+    extra:                            # single runs beside the product (baselines), with ``fixed`` and seeds
+      - {train.mode: centralized}
 
 Every run is one ``run_experiment`` in this process (or under ``torchrun`` - all ranks execute the
 grid in lockstep); rank 0 appends one summary line per run to ``<out>/results.jsonl`` and the
@@ -37,6 +39,11 @@ def expand_grid(spec: dict) -> list[dict]:
     for combo in combos:
         ov = dict(fixed)
         ov.update(dict(zip(keys, combo)))
+        for s in seeds:
+            runs.append({"overrides": ov, "seed": int(s)})
+    for extra in spec.get("extra", []) or []:
+        ov = dict(fixed)
+        ov.update(extra)
         for s in seeds:
             runs.append({"overrides": ov, "seed": int(s)})
     return runs

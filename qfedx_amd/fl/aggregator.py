@@ -76,7 +76,7 @@ class Aggregator:
                      round_num: int, client_ids: list, participants: Optional[list] = None,
                      dropped: Optional[list] = None, out: Optional[torch.Tensor] = None,
                      keys: Optional[torch.Tensor] = None, pack: Optional[tuple] = None,
-                     secagg_tabs: Optional[tuple] = None) -> torch.Tensor:
+                     secagg_tabs: Optional[tuple] = None, norm_cid: Optional[torch.Tensor] = None) -> torch.Tensor:
         """This rank's contribution [P+1] = [sum_k w_k priv(Delta_k) | sum_k w_k].
 
         float64 normally; int64 ring elements (mod 2^bits, masked) under secure aggregation.
@@ -104,7 +104,8 @@ class Aggregator:
             out, norms, sat = fedavg_hip.fused_local_reduce(
                 theta_k, theta_g, weights, self._mask_u8, client_ids, round_num, self.seed,
                 wrap=self.wrap, dp=self.dp, clip_norm=self.clip_norm,
-                noise_multiplier=self.noise_multiplier, out=out, keys=keys, pack=pack, secagg=sa)
+                noise_multiplier=self.noise_multiplier, out=out, keys=keys, pack=pack, secagg=sa,
+                norm_cid=norm_cid)
             self.last_norms = norms
             self.last_saturation = sat
             return out

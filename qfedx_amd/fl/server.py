@@ -116,6 +116,9 @@ class FederatedRunner:
                                                  t.server_momentum)
         self.params = adapter.init_params(t.seed).to(device)
         broadcast_(self.params, world)                      # CC1: identical theta on all ranks
+        # CC6: per-client update norms in the round all-reduce (DP only: they drive the clipping)
+        self.n_norm_slots = (self.num_clients if (p.dp and not p.secure_agg and
+                                                  getattr(cfg.runtime, "log_client_norms", True)) else 0)
 
     # ------------------------------------------------------------------ eval
     @torch.no_grad()
@@ -215,7 +218,7 @@ class FederatedRunner:
             # uniform FedAvg weights) travel as per-client tables with the round's upload, never as kernel
             # arguments.
             if getattr(self, "_round_buf", None) is None:
-                self._round_buf = torch.zeros(P + 6, dtype=torch.int64, device=dev)
+                self._round_buf = torch.zeros(P + 6 + self.n_norm_slots, dtype=torch.int64, device=dev)
             buf = self._round_buf
             extra = {}
             if p.dp and ids:
@@ -230,13 +233,15 @@ class FederatedRunner:
                 extra["sa_seed"], extra["sa_sign"] = self.secagg.round_tables(ids, participants, dropped,
                                                                               self.num_clients)
                 extra["sa_round"] = torch.full((len(ids),), r, dtype=torch.int32)
+            if self.n_norm_slots and ids:
+                extra["cid"] = torch.tensor(ids, dtype=torch.int32)
             agg = self.aggregator
 
             def epilogue(params_k, tabs, theta):
                 # one launch: the fused reduce writes the buffer head, its last block packs the metrics
                 sa = (tabs["sa_seed"], tabs["sa_sign"], tabs["sa_round"]) if "sa_seed" in tabs else None
                 agg.local_reduce(params_k, theta, tabs.get("fw", tabs["w"]), r, ids, out=buf[: P + 1],
-                                 keys=tabs.get("dpkeys"), secagg_tabs=sa,
+                                 keys=tabs.get("dpkeys"), secagg_tabs=sa, norm_cid=tabs.get("cid"),
                                  pack=(buf, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
                                        tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)))
             with self.timer.phase("local_train"):
@@ -268,15 +273,23 @@ class FederatedRunner:
                 sat = self.aggregator.last_saturation if local_alive else None
                 sat = (sat.to(dev).double().reshape(1) if sat is not None
                        else torch.zeros(1, dtype=torch.float64, device=dev))
-                metrics = torch.cat([torch.stack([loss_sum, correct]).to(dev), host_m, sat])
+                # CC6: this rank's clients' norms in their global slots (zero elsewhere): the metric SUM all-reduce
+                # gathers them
+                nslots = torch.zeros(self.n_norm_slots, dtype=torch.float64, device=dev)
+                if self.n_norm_slots and local_alive and self.aggregator.last_norms is not None:
+                    nslots[torch.tensor(ids, device=dev)] = self.aggregator.last_norms.double().to(dev)
+                metrics = torch.cat([torch.stack([loss_sum, correct]).to(dev), host_m, sat, nslots])
+        norms = None
         with self.timer.phase("comm"):
             if fast:
                 all_reduce_(buf, self.world)              # ONE collective per round (CC2+CC3)
-                out = torch.empty(6, dtype=torch.float64, device=dev)
+                NN = self.n_norm_slots
+                out = torch.empty(6 + NN, dtype=torch.float64, device=dev)
                 from ..ops._ext import ext
                 ring = (p.secagg_bits, p.secagg_scale) if p.secure_agg else (0, 1.0)
-                ext().round_apply(buf, P, self.params, 1.0, out, *ring)   # finalize + apply, in place
+                ext().round_apply(buf, P, self.params, 1.0, out, *ring, NN)   # finalize + apply, in place
                 metrics = out[:5]                                     # + saturated fixed-point terms
+                norms = out[6:6 + NN] if NN else None
             elif self.server_opt is not None:
                 # server optimizer (CC5): small all-reduce of [weight | metrics]; the update sums are
                 # reduce-scattered inside the sharded step and the new params all-gathered
@@ -299,6 +312,8 @@ class FederatedRunner:
                 mean_upd, wsum = self.aggregator.finalize(buf[: P + 1])
                 metrics = buf[P + 1:].double() / EXACT_SCALE
                 self._set_params(self.aggregator.apply(self.params, mean_upd, wsum=wsum))
+        if not fast and self.n_norm_slots:
+            norms, metrics = metrics[5:], metrics[:5]
         if p.dp:
             # the subsampled-Gaussian RDP bound holds for Poisson sampling at rate q; a fixed-size subset
             # drawn without replacement is accounted conservatively with no amplification (q = 1)
@@ -306,6 +321,7 @@ class FederatedRunner:
             self.accountant.step(q, p.noise_multiplier, 1)
         rec = {"round": r + 1, "participants": len(participants), "dropped": len(dropped),
                "_metrics": metrics, "_t0": t0,
+               "_norms": (norms, [c for c in participants if c not in dropped_set]) if norms is not None else None,
                "comm_bytes_per_rank": int((self.P + 1 + 4) * 8),
                "upload_bytes": int(len(participants) - len(dropped)) * (self.P + 1) * 4}
         if p.dp:
@@ -323,6 +339,14 @@ class FederatedRunner:
             return rec
         m = rec.pop("_metrics").double().cpu().tolist()
         dt = time.perf_counter() - rec.pop("_t0")
+        nrm = rec.pop("_norms", None)
+        if nrm is not None:                      # CC6: every client's pre-clip update norm, clip fraction
+            vals = nrm[0].double().cpu().numpy()[nrm[1]] if nrm[1] else np.zeros(0)
+            if vals.size:
+                C = self.cfg.privacy.clip_norm
+                q = np.quantile(vals, [0.1, 0.5, 0.9])
+                rec.update({"clip_frac": float((vals > C).mean()), "norm_p10": float(q[0]), "norm_p50": float(q[1]),
+                            "norm_p90": float(q[2])})
         if len(m) > 4 and m[4] > 0:
             raise RuntimeError(f"round {rec['round']}: {int(m[4])} fixed-point FedAvg terms saturated at 2^53 "
                                "(|w * Delta| > 2^21): lower the aggregation weights (train.weighting=uniform) or "

@@ -29,7 +29,7 @@ def dp_noise_keys(client_ids, round_num, seed) -> torch.Tensor:
 
 
 def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp, clip_norm,
-                       noise_multiplier, out=None, keys=None, pack=None, sat=None, secagg=None):
+                       noise_multiplier, out=None, keys=None, pack=None, sat=None, secagg=None, norm_cid=None):
     """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as exact int64 fixed point (scale 2^32)
     [P+1] (per-client terms rounded before the sum -> rank-count invariant), plus norms [K].
     ``angle_mask`` uint8 [P] on the device; ``out`` an optional int64 [P+1] destination (e.g. the head
@@ -42,7 +42,9 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
     ``pack``: ``buf[P + 5]``, zeroed by ``round_apply``; else a fresh zero counter).
     ``secagg`` = (seeds int32 [K, N, 2], sign int32 [K, N], round int32 [1] device tensors, scale, bits): the
     [P + 1] head holds SecAgg ring elements instead, each client's term masked in the kernel
-    (``SecureAggregator.round_tables``).  Returns (out, norms, sat)."""
+    (``SecureAggregator.round_tables``).  ``norm_cid`` (device int32 [K] global client ids; needs ``pack`` and
+    DP): the pack block scatters the clients' pre-clip norms into ``buf[P + 6 + id]`` (CC6).
+    Returns (out, norms, sat)."""
     K, P = theta_k.shape
     dev = theta_k.device
     if dp and keys is not None:
@@ -70,5 +72,7 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
                  weights.double().contiguous(), norms, keys, bool(wrap), bool(dp), float(clip_norm),
                  float(noise_multiplier) if dp else 0.0, out, *pack, sat,
                  *((secagg[0].contiguous(), secagg[1].contiguous(), secagg[2].contiguous(), float(secagg[3]),
-                    int(secagg[4])) if secagg is not None else (None, None, None, 1.0, 48)))
+                    int(secagg[4]), torch.empty(K * (P + 1), dtype=torch.int64, device=dev))
+                   if secagg is not None else (None, None, None, 1.0, 48, None)),
+                 norm_cid)
     return out, (norms[:K] if dp else None), sat

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_rccl.py tests/test_gpu_simulator.py tests/test_gpu_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "rccl or simulator or norms_ride" > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "gpu_tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
 for r in 1 2; do
   for m in 0 1 2 4 8 3 12; do

@@ -78,3 +78,35 @@ def test_mlflow_file_store_tracking(tmp_path):
     assert [s for _, _, s in acc] == [0, 1, 2, 3] and all(0.0 <= v <= 1.0 for _, v, _ in acc)
     assert len(glob.glob(os.path.join(run, "artifacts", "checkpoints", "round_*.pt"))) == 3
     assert yaml.safe_load(open(os.path.join(run, "artifacts", "config.yaml")))["train"]["num_rounds"] == 3
+
+
+def test_roadmap_digits_grid_has_baselines_and_alpha_axis(tmp_path):
+    """Reduced ROADMAP.md:102-116 model-comparison grid: VQC on PCA features across the Dirichlet alpha axis, the
+    classical FL TinyCNN under the same DP, and the centralized-VQC baseline, all in one report table."""
+    import yaml
+    spec = yaml.safe_load(open(os.path.join(ROOT, "configs", "grid_roadmap_digits.yaml")))
+    spec["seeds"] = [0]
+    spec["fixed"] = {"train.num_rounds": 1, "runtime.device": "cpu", "runtime.log_every": 100}
+    spec["grid"] = {"model.n_qubits": [4], "privacy.dp": [True], "data.alpha": [0.1, 1.0]}
+    spec["extra"] = [e for e in spec["extra"] if e.get("privacy.dp")]
+    out = str(tmp_path / "g")
+    res = run_grid(spec, out)
+    kinds = {(r["config"]["model"]["kind"], r["config"]["train"]["mode"]) for r in res}
+    assert kinds == {("vqc", "federated"), ("tinycnn", "federated"), ("vqc", "centralized")}
+    assert {r["config"]["data"]["alpha"] for r in res if r["config"]["model"]["kind"] == "vqc"} >= {0.1, 1.0}
+    assert all(r["epsilon"] and r["epsilon"] > 0 for r in res)
+    rep = write_report(os.path.join(out, "results.jsonl"))
+    assert "tinycnn" in rep["markdown"] and "centralized" in rep["markdown"] and "alpha" in rep["markdown"]
+
+
+def test_centralized_mode_pools_every_shard_into_one_client():
+    from qfedx_amd.config import ExperimentConfig, apply_overrides
+    from qfedx_amd.data.datasets import build_federated_data
+    cfg = ExperimentConfig()
+    apply_overrides(cfg, ["data.dataset=iris", "data.num_clients=3", "model.n_qubits=4"])
+    fed = build_federated_data(cfg)
+    cfg.train.mode = "centralized"
+    cen = build_federated_data(cfg, clients=[0])
+    assert cen.num_clients == 1 and cen.client_ids == [0] and len(cen.clients) == 1
+    assert cen.clients[0][1].shape[0] == sum(fed.sizes())
+    assert build_federated_data(cfg, clients=[]).clients == []

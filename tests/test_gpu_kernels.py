@@ -407,3 +407,21 @@ def test_secagg_masks_in_fused_reduce_match_host_protocol(cuda, dp):
     ext().round_apply(buf, P, theta, 1.0, out, sa.bits, sa.scale)
     ref = gpu.apply(tg.to(cuda), mb.to(cuda), wsum=wb)
     assert torch.equal(theta, ref) and abs(out[5].item() - float(wb)) < 1e-12
+
+
+def test_dp_client_norms_ride_in_round_buffer(cuda):
+    """CC6 on the HIP fast path: the fused reduce's pack block scatters each client's pre-clip norm into the round
+    all-reduce buffer and round_apply reads them back; round 1's norm quantiles match the CPU path's."""
+    from tests.test_fl import small_cfg
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.parallel.dist import init_distributed
+    kw = dict(num_rounds=2, dp=True, clip_norm=0.05, noise_multiplier=0.5, num_clients=5, deterministic_noise=True,
+              optimizer="sgd")
+    cpu = run_experiment(small_cfg(**kw))
+    dev = torch.device("cuda", 0)
+    gpu = run_experiment(small_cfg(device="cuda", backend="hip", **kw), world=init_distributed(dev), device=dev,
+                         backend="hip")
+    hc, hg = cpu["history"][0], gpu["history"][0]
+    for key in ("norm_p10", "norm_p50", "norm_p90"):
+        assert abs(hc[key] - hg[key]) < 1e-3 * max(1.0, hc[key]), (key, hc[key], hg[key])
+    assert all(0.0 <= h["clip_frac"] <= 1.0 for h in gpu["history"])

@@ -21,8 +21,9 @@ from qfedx_amd.parallel.dist import init_distributed, shutdown, max_over_ranks, 
 import torch.distributed as dist
 
 def cfg(backend, **kw):
-    return small_cfg(num_rounds=3, n_qubits=10, n_layers=2, num_clients=6, samples_per_client=32, batch_size=8,
-                     device="cuda", backend="hip", dist_backend=backend, **kw)
+    base = dict(num_rounds=3, n_qubits=10, n_layers=2, num_clients=6, samples_per_client=32, batch_size=8,
+                device="cuda", backend="hip", dist_backend=backend)
+    return small_cfg(**{{**base, **kw}})
 
 dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
