@@ -108,6 +108,10 @@ def main():
                        "secure_agg": cfg.privacy.secure_agg,
                        "shots": cfg.noise.shots},
         }
+        eng = getattr(runner.adapter, "engine", None)
+        if t.grad_method == "param_shift" and eng is not None and hasattr(eng.hip, "shift_pass_counts"):
+            # pass launches per sample of one gradient: naive shifted circuits vs prefix reuse + pi identity
+            rec["param_shift"] = dict(eng.hip.shift_pass_counts(), reuse=bool(eng.ps_reuse))
         print(json.dumps(rec), flush=True)
     shutdown(world)
 

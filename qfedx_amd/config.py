@@ -118,6 +118,7 @@ class RuntimeConfig:
     log_every: int = 5
     overlap_comm: bool = True
     use_graphs: bool = True            # hipGraph capture of the local round (HIP backend)
+    graph_comm: bool = True            # capture the round's all-reduce + apply into that graph (RCCL / no group)
     log_client_norms: bool = True      # DP rounds: every client's pre-clip update norm reaches every rank in the
                                        # round all-reduce (CC6); clip fraction + norm quantiles per round (not
                                        # under SecAgg, where per-client statistics would leak)

@@ -27,5 +27,6 @@ struct HeaPassArgs {
   int n_gradops;
   int hrow[5];               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
   long long* dbg;            // optional phase timestamps (s_memtime) of workgroups < 8, [8][64]
+  int in_rep;                // forward: shifted parameter rows per stored input sample (param-shift prefix reuse)
   int ablate;                // timing ablations (builds with QFX_HEA_ABLATE only; QFEDX_HEA_ABLATE bit mask)
 };

@@ -51,12 +51,12 @@ void check(int rc, const char* what) {
 }
 
 // geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
-//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops]
+//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep]
 void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<int64_t> geom, double scale, torch::Tensor psi_in,
               torch::Tensor psi_out, torch::Tensor lam_in, torch::Tensor lam_out, torch::Tensor xang,
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
               torch::Tensor gslab, torch::Tensor dbg) {
-  need(geom.size() == 26, "geometry vector must have 26 entries");
+  need(geom.size() == 27, "geometry vector must have 27 entries");
   HeaPassArgs a{};
   a.n = (int)geom[0];
   a.t = (int)geom[1];
@@ -87,6 +87,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
     a.ablate = ablate;
   }
   a.n_gradops = (int)geom[25];
+  a.in_rep = (int)geom[26];
   a.scale = (float)scale;
   a.dbg = dbg.defined() && dbg.numel() >= 8 * 64 ? dp<long long>(dbg, torch::kInt64, "dbg", 8 * 64) : nullptr;
   for (int b = 0; b < 5; ++b) {
@@ -106,14 +107,16 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   need(a.nops <= 128, "at most 128 ops per pass program");
   a.ops = dp<int>(ops, torch::kInt32, "ops", 0);
   a.fidx = a.nops ? dp<int>(fidx, torch::kInt32, "fidx", a.nops) : nullptr;
+  need(a.in_rep >= 1 && (!adjoint || a.in_rep == 1) && K % a.in_rep == 0,
+       "in_rep: forward only, parameter rows a multiple of it");
   const int64_t states = S << a.n;
-  a.psi_in = a.gen ? nullptr : dp<uint32_t>(psi_in, torch::kInt32, "psi_in", states);
+  a.psi_in = a.gen ? nullptr : dp<uint32_t>(psi_in, torch::kInt32, "psi_in", states / a.in_rep);
   need(!(adjoint && a.store_psi), "adjoint passes store lambda only");
   a.psi_out = a.store_psi ? dp<uint32_t>(psi_out, torch::kInt32, "psi_out", states) : nullptr;
   a.lam_in = (adjoint && a.load_lam) ? dp<uint32_t>(lam_in, torch::kInt32, "lam_in", states) : nullptr;
   a.lam_out = (adjoint && a.store_lam) ? dp<uint32_t>(lam_out, torch::kInt32, "lam_out", states) : nullptr;
   need(a.x_stride >= a.n, "x stride must cover n feature angles");
-  a.xang = dp<float>(xang, torch::kFloat32, "xang", S * a.x_stride);
+  a.xang = a.gen ? dp<float>(xang, torch::kFloat32, "xang", S / a.in_rep * a.x_stride) : nullptr;   // layer-1 only
   a.params = dp<float>(params, torch::kFloat32, "params", K * a.p_stride);
   a.frags = a.n_slots ? (const void*)dp<int32_t>(frags, torch::kInt32, "frags", K * a.n_slots * 4 * 128 * 4) : nullptr;
   a.wread = adjoint ? dp<float>(wread, torch::kFloat32, "wread", S * a.C) : nullptr;

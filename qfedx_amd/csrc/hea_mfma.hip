@@ -30,8 +30,9 @@ __device__ unsigned int qfx_check_word = 0;
 #endif
 
 // Timing ablations (scripts/gpu_ab_*.sh): a build with -DQFX_HEA_ABLATE=1 skips parts of every op by the bit mask
-// QFEDX_HEA_ABLATE (1 op barriers, 2 gradient atomics, 4 cross matrices, 8 unitary applications).  Results are
-// wrong in such a build; release builds compile the checks out.
+// QFEDX_HEA_ABLATE (1 op barriers, 2 gradient atomics, 4 cross matrices, 8 unitary applications, 16 gradient-region
+// flushes, 32 the adjoint tile load, 64 next-op record / fragment staging).  Results are wrong in such a build;
+// release builds compile the checks out.
 #ifndef QFX_HEA_ABLATE
 #define QFX_HEA_ABLATE 0
 #endif
@@ -621,6 +622,9 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s = blockIdx.x / a.n_tiles, tile_id = blockIdx.x % a.n_tiles;
   const int k = s / a.spc;
+  // in_rep > 1: in_rep consecutive parameter rows (clients) share each input sample - a parameter-shift branch
+  // starts from the stored unshifted state of its client's sample (sample s reads input row s_in)
+  const int s_in = a.in_rep > 1 ? (s / (a.in_rep * a.spc)) * a.spc + s % a.spc : s;
   const int T = 1 << a.t;
   const size_t N = (size_t)1 << a.n;
   const uint32_t fixed = tile_fixed(a, tile_id);
@@ -646,7 +650,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
     if (wave == 0) {
       float2 w[2] = {make_float2(1.f, 0.f), make_float2(1.f, 0.f)};
       if (tid < a.n) {
-        l1_factor(a.xang[(size_t)s * a.x_stride + tid], prm[2 * tid], prm[2 * tid + 1], a.feature, w);
+        l1_factor(a.xang[(size_t)s_in * a.x_stride + tid], prm[2 * tid], prm[2 * tid + 1], a.feature, w);
         wv[tid][0] = w[0];
         wv[tid][1] = w[1];
       }
@@ -707,7 +711,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
       if (4 * q < (uint32_t)T) *(uint4*)&psi_t[4 * q] = out[i];
     }
   } else {
-    load_tile<NT>(a, a.psi_in + (size_t)s * N, psi_t, tid, T, h_q, fixed);
+    load_tile<NT>(a, a.psi_in + (size_t)s_in * N, psi_t, tid, T, h_q, fixed);
   }
 
   // ---------------------------------------------------------------- op list
@@ -808,8 +812,9 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
   if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
-  load_tile_il<NT, TB>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
-                       h_q, fixed);
+  if (!(QFX_HEA_ABLATE && (a.ablate & 32)))
+    load_tile_il<NT, TB>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
+                         h_q, fixed);
   if (tid == 0) {
     float rho = 0.f;
     for (int c = 0; c < a.C; ++c) rho = fmaxf(rho, fabsf(a.wread[(size_t)s * a.C + c]));
@@ -857,16 +862,16 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
       op_barrier(wave);
     HEA_MARK();
     if (RING && pending >= 0) {
-      if (wave == NW - 1) flush(pending);
+      if (wave == NW - 1 && !(QFX_HEA_ABLATE && (a.ablate & 16))) flush(pending);
       pending = -1;
     }
-    const int* opw = opw2[o & 1];
+    const int* opw = opw2[(QFX_HEA_ABLATE && (a.ablate & 64)) ? 0 : (o & 1)];   // ablation: op 0's record
     uint4 F[4];
     if (fidx_s[o] >= 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) F[i] = frag_s[o & 1][64 * i + lane];
     }
-    if (o + 1 < a.nops) {
+    if (o + 1 < a.nops && !(QFX_HEA_ABLATE && (a.ablate & 64))) {
       if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
       if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
       dma_frags(a, k, fidx_s[o + 1], lane, wave, frag_s[(o + 1) & 1]);

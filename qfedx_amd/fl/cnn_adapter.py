@@ -41,9 +41,9 @@ class CNNClientTrainer:
         return {"loss": loss.detach(), "grad": p.grad, "correct": correct}
 
     def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int,
-                  epilogue=None, extra=None) -> dict:
+                  epilogue=None, extra=None, post=None) -> dict:
         """Same contract as ``VQCClientTrainer.run_round`` (per-step [S,K] loss/correct round buffers, optional
-        ``extra`` per-client tables and device ``epilogue``, here run eagerly)."""
+        ``extra`` per-client tables and device ``epilogue``, here run eagerly; ``post`` is left to the caller)."""
         cfg = self.cfg
         K = len(local_idx)
         P = theta_g.numel()

@@ -236,6 +236,20 @@ class FederatedRunner:
             if self.n_norm_slots and ids:
                 extra["cid"] = torch.tensor(ids, dtype=torch.int32)
             agg = self.aggregator
+            NN = self.n_norm_slots
+            if getattr(self, "_round_outs", None) is None:     # [metrics | sat | wsum | norms], one per graph variant
+                self._round_outs = [torch.zeros(6 + NN, dtype=torch.float64, device=dev) for _ in range(2)]
+                self._out_writes = [0, 0]
+                self._flip = 0
+            ring = (p.secagg_bits, p.secagg_scale) if p.secure_agg else (0, 1.0)
+            world, params_g, outs = self.world, self.params, self._round_outs
+
+            def post(v):
+                # ONE collective per round (CC2+CC3), then finalize + apply in place; captured into the round
+                # graph (variant v writes metrics buffer v) when the collective allows it
+                all_reduce_(buf, world)
+                from ..ops._ext import ext
+                ext().round_apply(buf, P, params_g, 1.0, outs[v], *ring, NN)
 
             def epilogue(params_k, tabs, theta):
                 # one launch: the fused reduce writes the buffer head, its last block packs the metrics
@@ -244,9 +258,11 @@ class FederatedRunner:
                                  keys=tabs.get("dpkeys"), secagg_tabs=sa, norm_cid=tabs.get("cid"),
                                  pack=(buf, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
                                        tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)))
+            graph_comm = (getattr(self.cfg.runtime, "graph_comm", True)
+                          and (not self.world.distributed or self.world.backend == "nccl"))
             with self.timer.phase("local_train"):
                 res = trainer.run_round(self.store, local_alive, self.params, r, epilogue=epilogue,
-                                        extra=extra or None)
+                                        extra=extra or None, post=post if graph_comm else None)
             if not local_alive:
                 buf.zero_()
         else:
@@ -282,12 +298,14 @@ class FederatedRunner:
         norms = None
         with self.timer.phase("comm"):
             if fast:
-                all_reduce_(buf, self.world)              # ONE collective per round (CC2+CC3)
-                NN = self.n_norm_slots
-                out = torch.empty(6 + NN, dtype=torch.float64, device=dev)
-                from ..ops._ext import ext
-                ring = (p.secagg_bits, p.secagg_scale) if p.secure_agg else (0, 1.0)
-                ext().round_apply(buf, P, self.params, 1.0, out, *ring, NN)   # finalize + apply, in place
+                if res.get("post_done"):
+                    v = res["post_variant"]
+                else:
+                    v = self._flip
+                    self._flip ^= 1
+                    post(v)
+                self._out_writes[v] += 1
+                out = self._round_outs[v]
                 metrics = out[:5]                                     # + saturated fixed-point terms
                 norms = out[6:6 + NN] if NN else None
             elif self.server_opt is not None:
@@ -321,6 +339,7 @@ class FederatedRunner:
             self.accountant.step(q, p.noise_multiplier, 1)
         rec = {"round": r + 1, "participants": len(participants), "dropped": len(dropped),
                "_metrics": metrics, "_t0": t0,
+               "_out_stamp": (v, self._out_writes[v]) if fast else None,
                "_norms": (norms, [c for c in participants if c not in dropped_set]) if norms is not None else None,
                "comm_bytes_per_rank": int((self.P + 1 + 4) * 8),
                "upload_bytes": int(len(participants) - len(dropped)) * (self.P + 1) * 4}
@@ -337,6 +356,10 @@ class FederatedRunner:
         """Read a round's metrics back (syncs with the device) and fill the derived fields."""
         if "_metrics" not in rec:
             return rec
+        stamp = rec.pop("_out_stamp", None)
+        if stamp is not None and self._out_writes[stamp[0]] != stamp[1]:
+            raise RuntimeError(f"round {rec['round']}: its metrics buffer was reused by a later round; resolve "
+                               "records (resolve_record) within two rounds")
         m = rec.pop("_metrics").double().cpu().tolist()
         dt = time.perf_counter() - rec.pop("_t0")
         nrm = rec.pop("_norms", None)

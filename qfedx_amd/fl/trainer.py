@@ -268,7 +268,7 @@ class VQCClientTrainer:
         return params, loss_all, correct_all
 
     def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int,
-                  epilogue=None, extra: Optional[dict] = None) -> dict:
+                  epilogue=None, extra: Optional[dict] = None, post=None) -> dict:
         """Train clients ``store[local_idx]`` from the global params.
 
         Returns device tensors: ``params`` [K,P], ``loss`` / ``correct`` [S,K] per step, ``nvalid`` /
@@ -279,7 +279,11 @@ class VQCClientTrainer:
         ``epilogue(params, tables, theta)``: device work run right after the local steps, on the trained
         params (possibly padded with inactive weight-0 rows), the round's device tables and the global params;
         on the hipGraph path it is captured into the round graph, so it may only launch device work on static
-        buffers (no host values that change per round)."""
+        buffers (no host values that change per round).
+        ``post()``: the round's collective + global update (all-reduce of the epilogue's buffer, apply to
+        ``theta_g`` in place), run after the epilogue: captured into the round graph too when possible (then the
+        whole round - host upload, local steps, reduce, all-reduce, apply - is ONE graph launch), else run
+        eagerly.  The returned ``post_done`` says it ran (the caller must not run it again)."""
         cfg = self.cfg
         K = len(local_idx)
         P = theta_g.numel()
@@ -313,8 +317,10 @@ class VQCClientTrainer:
         if noise is not None:
             traj_keys = noise.client_keys("noise_traj", round_num, cids, self.device)
             ro_keys = noise.client_keys("shots", round_num, cids, self.device)
+        post_v = None
         if graphed:
-            params, loss_all, correct_all, dv = self._graphed(store, up, theta_g, plan, round_num, epilogue)
+            params, loss_all, correct_all, dv, post_v = self._graphed(store, up, theta_g, plan, round_num,
+                                                                      epilogue, post)
             # padding clients (inactive, weight 0) only fill the captured shape: the FedAvg reduce sees the
             # K real rows; their [S, Kpad] metric columns are all zero
             params = params[:K]
@@ -328,36 +334,42 @@ class VQCClientTrainer:
             if epilogue is not None:
                 epilogue(params, dict(dv, loss=loss_all, correct=correct_all), theta)
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
-                "lid": dv["lid"], "weights": dv["w"], **common}
+                "lid": dv["lid"], "weights": dv["w"], "post_done": post_v is not None, "post_variant": post_v,
+                **common}
 
     # ------------------------------------------------------------------ hipGraph capture
     @property
     def use_graph(self) -> bool:
         return self.backend == "hip" and self.device.type == "cuda" and getattr(self, "graphs", True)
 
-    def _graphed(self, store, up, theta_g, plan, round_num, epilogue=None):
+    def _graphed(self, store, up, theta_g, plan, round_num, epilogue=None, post=None):
         """Replay the whole round as ONE hipGraph (static shapes: #clients, steps, batch).
 
-        Captured once per SHAPE, not per client set: each round ONE async copy refreshes the packed
-        static input buffer (client slots, minibatch indices, loss weights, step masks), and the captured
-        launches gather every step's minibatches from the (static) client store by slot, so client sampling
-        reuses the graph.  The global params are read in place when they are a float32 device tensor (the
-        runner updates them in place after the collective; a new tensor means a new graph), otherwise copied
-        into a static buffer.  ``epilogue`` (the round's fused FedAvg reduce + metrics pack) is captured after
-        the local steps, so the whole pre-collective round is one graph launch.  A small LRU bounds the live
-        graphs.
+        Captured once per SHAPE, not per client set, in two variants that differ only in the pinned host buffer
+        their first node (a copy kernel) reads the round's packed tables from (client slots, minibatch indices,
+        loss weights, step masks, per-client keys): round r fills pinned buffer r % 2 - free once round r - 2's
+        replay has finished - and replays variant r % 2, so the host stays a round ahead with no upload launch
+        of its own.  The captured launches gather every step's minibatches from the (static) client store by
+        slot, so client sampling reuses the graph.  The global params are read in place when they are a float32
+        device tensor (the runner updates them in place), otherwise copied into a static buffer.  ``epilogue``
+        (the fused FedAvg reduce + metrics pack) and ``post`` (the collective + in-place apply) are captured
+        after the local steps, so a round is one graph launch; if the collective cannot be captured, ``post``
+        runs eagerly after the replay.  A small LRU bounds the live graphs.
         """
         K = up.layout[0][4][0]
         dev = self.device
         direct = theta_g.is_cuda and theta_g.dtype == torch.float32 and theta_g.is_contiguous()
         key = (K, plan.max_steps, plan.B, store.nmax, store.X.data_ptr(), tuple(l[0] for l in up.layout),
-               theta_g.data_ptr() if direct else None, epilogue is not None)
+               theta_g.data_ptr() if direct else None, epilogue is not None, post is not None)
         cache = self.__dict__.setdefault("_graph_cache", {})
         ent = cache.pop(key, None)
         if ent is None:
+            from ..ops._ext import ext
+            E = ext()
             pack = torch.empty(up.nbytes, dtype=torch.uint8, device=dev)
             dv = up.to_device(dev, pack)
-            ent = {"pack": pack, "dv": dv, "theta": theta_g if direct else theta_g.to(dev).float().clone()}
+            ent = {"pack": pack, "dv": dv, "theta": theta_g if direct else theta_g.to(dev).float().clone(),
+                   "pin": [E.host_alloc(up.nbytes), E.host_alloc(up.nbytes)], "events": [None, None], "flip": 0}
             args = (store.X, store.y, dv["lid"], ent["theta"], dv["idx"], dv["wts"], dv["act"], plan.max_steps,
                     round_num, "adjoint")
 
@@ -368,22 +380,59 @@ class VQCClientTrainer:
                 return out
             # the graph owns its workspaces: eager calls (evaluation) can never regrow/free them
             ent["ws"] = {}
+            cur = torch.cuda.current_stream(dev)
             with self.engine.hip.private_workspace(ent["ws"]):
                 side = torch.cuda.Stream(device=dev)
-                side.wait_stream(torch.cuda.current_stream(dev))
-                with torch.cuda.stream(side):       # warm-up: JIT modules loaded, workspaces sized
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):       # warm-up (no collective / apply): modules loaded, sizes fixed
                     body()
-                torch.cuda.current_stream(dev).wait_stream(side)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    ent["out"] = body()
-            ent["graph"] = g
+                cur.wait_stream(side)
+                ent["graphs"], ent["out"] = [], []
+                ent["post_in_graph"] = post is not None and getattr(self, "graph_comm", True)
+                for v in range(2):
+                    up._fill(ent["pin"][v][: up.nbytes])
+                    g = torch.cuda.CUDAGraph()
+                    try:
+                        with torch.cuda.graph(g):
+                            E.host_upload(ent["pin"][v][: up.nbytes], pack)
+                            out = body()
+                            if ent["post_in_graph"]:
+                                post(v)
+                    except Exception:
+                        if not ent["post_in_graph"]:
+                            raise
+                        # the collective refused capture: graphs without it, post() runs eagerly
+                        self.graph_comm = False
+                        ent["post_in_graph"] = False
+                        torch.cuda.synchronize(dev)
+                        ent["graphs"], ent["out"] = [], []
+                        for v2 in range(2):
+                            g = torch.cuda.CUDAGraph()
+                            with torch.cuda.graph(g):
+                                E.host_upload(ent["pin"][v2][: up.nbytes], pack)
+                                out = body()
+                            ent["graphs"].append(g)
+                            ent["out"].append(out)
+                        break
+                    ent["graphs"].append(g)
+                    ent["out"].append(out)
             while len(cache) >= _GRAPH_LRU:         # LRU: drop the oldest shape
-                cache.pop(next(iter(cache)))
-        else:
-            dv = up.to_device(dev, ent["pack"])     # one H2D copy for all the round's tables
+                old = cache.pop(next(iter(cache)))
+                for ev in old["events"]:
+                    if ev is not None:
+                        ev.synchronize()
         cache[key] = ent                            # most recently used last
         if not direct:
             ent["theta"].copy_(theta_g.float())
-        ent["graph"].replay()
-        return (*ent["out"], ent["dv"])
+        v = ent["flip"]
+        ent["flip"] ^= 1
+        if ent["events"][v] is not None:
+            ent["events"][v].synchronize()          # pinned buffer v: its last reader (round r - 2) is done
+        up._fill(ent["pin"][v][: up.nbytes])
+        ent["graphs"][v].replay()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        ent["events"][v] = ev
+        if post is not None and not ent["post_in_graph"]:
+            post(v)
+        return (*ent["out"][v], ent["dv"], v if post is not None else None)

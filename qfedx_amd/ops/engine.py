@@ -12,12 +12,14 @@ Backends:
                 network, or parameter shift when the bond bound exceeds ``mps_chi``
 
 Gradient methods (ROADMAP.md:23,38,130-135): ``adjoint`` (default; 1 forward + 1 reverse sweep),
-``param_shift`` (2 shifted circuits per rotation gate, batched), ``spsa`` (2 perturbed losses),
+``param_shift`` (2 shifted circuits per rotation gate, batched; on the MFMA engine the same shot-sampled
+estimator from stored pass prefixes + the pi identity, ``HeaMfmaProgram.param_shift``), ``spsa`` (2 perturbed losses),
 ``autograd`` (torch complex autograd; CPU cross-check only).
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -59,6 +61,7 @@ class VQCEngine:
         self.coef = torch.from_numpy(coef)
         self.n_slots = spec.n_theta + spec.x_width
         self.state_dtype = state_dtype
+        self.ps_reuse = os.environ.get("QFEDX_PS_REUSE", "1") != "0"   # 0: naive shifted rows (A/B, tests)
         if backend == "torch":
             self.prog = TorchProgram(ops, coef, spec.n_qubits, self.device)
             self.hip = None
@@ -232,7 +235,12 @@ class VQCEngine:
                 gth = gs.reshape(K, B, P).sum(1).float()
             elif method == "param_shift":
                 # shifted expectations carry the readout channel themselves: w = dL/d<Z>_noisy unscaled
-                if self._simple_shift_slots():
+                if (self.backend == "hip" and hasattr(self.hip, "param_shift") and init is None
+                        and self.ps_reuse):
+                    # MFMA engine: prefix reuse + the pi identity (same estimator, ~2.5x fewer pass launches)
+                    nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
+                    gth = self.hip.param_shift(xang, params, w, nz, readout_keys, step)
+                elif self._simple_shift_slots():
                     gth = self.param_shift_batched(xang, params, w, readout_keys, step, init)
                 else:
                     gth = self._param_shift(self._rows(xang, th), w, K, B, init=init)

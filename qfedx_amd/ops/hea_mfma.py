@@ -132,6 +132,9 @@ class HeaMfmaProgram:
         self.scale = float(1 << (self.n // 2))
         self.feature = _FEATURE[spec.feature_map.lower()]
         self._ws = {}
+        self._ps_budget = None
+        if self.device.type == "cuda":
+            self._shift_budget()      # query free HBM now, never inside a graph capture
 
     # ------------------------------------------------------------------ workspaces
     @contextlib.contextmanager
@@ -160,10 +163,10 @@ class HeaMfmaProgram:
         """Tiles per sample of the pass that reads out <Z> (the last forward pass that runs)."""
         return 1 << (self.n - self.passes[self.fwd_last][0].t)
 
-    def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K):
+    def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K, in_rep: int = 1):
         return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
                 int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
-                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops]
+                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep)]
 
     def _frags(self, params: torch.Tensor, K: int, tag: str = "") -> torch.Tensor:
         fr = self._buf(f"{tag}frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
@@ -186,7 +189,9 @@ class HeaMfmaProgram:
         for j in range(R + 1):
             p, fwd = self.passes[j][0], self.passes[j][1]
             keep = j < R or store_last
-            out = self._buf(f"{tag}psi{j}", N, torch.int32) if keep else empty
+            # evaluation only needs the previous pass output: two ping-pong buffers instead of one per pass
+            name = f"{tag}psi{j}" if store_last else f"{tag}pe{j % 2}"
+            out = self._buf(name, N, torch.int32) if keep else empty
             psi_in = stored[-1] if j > 0 else empty
             geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K)
             C.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
@@ -235,11 +240,17 @@ class HeaMfmaProgram:
         if th.shape[1] < self.n_theta + 2 * self.C:    # pad theta-only rows to the kernel's param stride
             th = torch.cat([th, th.new_zeros(K, self.n_theta + 2 * self.C - th.shape[1])], 1)
         S = K * B
-        fr = self._frags(th, K)
-        part = self._buf("part", S * self.tiles_last * self.C, torch.float32)
-        self._forward(x, th, fr, K, B, part)
         out = self._buf("expz", S * self.C, torch.float32)
-        ext().readout_sum(part, self.tiles_last, self.C, S, out)
+        # clients per launch: two live states per sample fit the HBM budget (24q: 128 MiB per sample)
+        Kc = max(1, min(K, self._shift_budget() // max(1, 2 * B * ((1 << self.n) * 4))))
+        for k0 in range(0, K, Kc):
+            k1 = min(K, k0 + Kc)
+            Sc = (k1 - k0) * B
+            thc = th[k0:k1] if Kc < K else th
+            fr = self._frags(thc, k1 - k0)
+            part = self._buf("part", Sc * self.tiles_last * self.C, torch.float32)
+            self._forward(x[k0 * B:k1 * B], thc, fr, k1 - k0, B, part)
+            ext().readout_sum(part, self.tiles_last, self.C, Sc, out[k0 * B * self.C:k1 * B * self.C])
         if noise is not None:
             from .statevec_hip import _keys
             ext().readout_noise(out, self.C, B, S, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
@@ -265,6 +276,177 @@ class HeaMfmaProgram:
         grad = torch.zeros(K, th.shape[1], dtype=torch.float32, device=self.device)
         ext().hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, th, grad, th.shape[1])
         return z.view(S, self.C).clone(), grad[:, : self.n_theta]
+
+    # ------------------------------------------------------------------ parameter shift (prefix reuse)
+    def shift_owners(self) -> list:
+        """Per forward pass j <= fwd_last: the theta indices whose rotation it applies (layer 1 is generated in
+        pass 0; rotation group g of pass j carries theta_slot(layer, q) and its phase partner)."""
+        own = [[] for _ in range(self.fwd_last + 1)]
+        for q in range(self.n):
+            own[0] += [self.plan.theta_slot(1, q), self.plan.theta_slot(1, q) + 1]
+        for j in range(self.fwd_last + 1):
+            for g in self.plan.passes[j].groups:
+                for q in g.qubits:
+                    own[j] += [self.plan.theta_slot(g.layer, q), self.plan.theta_slot(g.layer, q) + 1]
+        flat = sorted(i for o in own for i in o)
+        if flat != list(range(self.n_theta)):
+            raise RuntimeError("forward passes do not own every parameter exactly once")
+        return own
+
+    def shift_pass_counts(self) -> dict:
+        """Pass launches per sample of one parameter-shift gradient: naive (2 n_theta shifted circuits, every
+        forward pass each) vs prefix reuse + the pi identity (one +pi branch per parameter from its pass on, the
+        unshifted forward, C adjoint sweeps)."""
+        F = self.fwd_last + 1
+        own = self.shift_owners()
+        branch = sum(len(o) * (F - j) for j, o in enumerate(own))
+        return {"naive_fwd_passes": 2 * self.n_theta * F, "reuse_fwd_passes": branch + F,
+                "reuse_adj_passes": self.C * self.n_passes, "branch_fwd_passes": branch}
+
+    def _shift_budget(self) -> int:
+        """Bytes of HBM the chunked evaluation / parameter-shift paths may hold in live states."""
+        if self._ps_budget is None:
+            env = os.environ.get("QFEDX_PS_BUDGET_MB")
+            if env:
+                self._ps_budget = int(env) << 20
+            else:
+                free, _ = torch.cuda.mem_get_info(self.device)
+                self._ps_budget = int(0.4 * free)
+        return self._ps_budget
+
+    @torch.no_grad()
+    def shifted_expz(self, xang: torch.Tensor, params: torch.Tensor, with_mean: bool = True) -> torch.Tensor:
+        """Exact <Z> at theta +- pi/2 e_j for every client, parameter j, sign and sample -> [K, n_theta, 2, B, C]
+        (sign 0: +pi/2), from the prefix-reuse identities of ``param_shift``.  ``with_mean=False`` drops the
+        common term m (only the +- difference is wanted) and skips the +pi branches."""
+        E = ext()
+        x, th, K, B = self._prep(xang, params)
+        P, C, n = self.n_theta, self.C, self.n
+        if th.shape[1] < P + 2 * C:
+            th = torch.cat([th, th.new_zeros(K, P + 2 * C - th.shape[1])], 1)
+        ps = th.shape[1]
+        F = self.fwd_last + 1
+        own = self.shift_owners()
+        sb = (1 << n) * 4                                   # fp16 (re, im) per amplitude
+        budget = self._shift_budget()
+        Kc = max(1, min(K, (budget // 2) // max(1, (F + 3) * B * sb)))
+        rows_max = max(B, (budget // 2) // (2 * sb))        # samples per +pi chunk (two ping-pong states)
+        f0 = torch.empty(K, B, C, dtype=torch.float32, device=self.device)
+        jac = torch.empty(K, B, C, P, dtype=torch.float32, device=self.device)
+        fpi = torch.empty(K, P, B, C, dtype=torch.float32, device=self.device) if with_mean else None
+        empty = torch.empty(0, dtype=torch.int32, device=self.device)
+        eye = torch.eye(C, dtype=torch.float32, device=self.device)
+        for k0 in range(0, K, Kc):
+            k1 = min(K, k0 + Kc)
+            nk, S = k1 - k0, (k1 - k0) * B
+            xs, ths = x[k0 * B:k1 * B], th[k0:k1].contiguous()
+            fr = self._frags(ths, nk, "ps")
+            part = self._buf("pspart", S * self.tiles_last * C, torch.float32)
+            stored = self._forward(xs, ths, fr, nk, B, part, store_last=True, tag="ps")
+            z = self._buf("psz", S * C, torch.float32)
+            E.readout_sum(part, self.tiles_last, C, S, z)
+            f0[k0:k1] = z.view(nk, B, C)
+            # per-sample Jacobian rows: one adjoint sweep per class over the stored forward, reduced with spc = 1
+            gslab = self._buf("psgslab", S * self.slab_tiles * self.n_gradops * 32, torch.int64)
+            th_rep = ths.repeat_interleave(B, 0).contiguous()
+            g = torch.zeros(S, ps, dtype=torch.float32, device=self.device)
+            for c in range(C):
+                wr = eye[c].expand(S, C).contiguous()
+                self._adjoint(xs, ths, fr, nk, B, stored, wr, gslab, "ps")
+                E.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, 1, S, th_rep, g, ps)
+                jac[k0:k1, :, c] = g[:, :P].view(nk, B, P)
+            if not with_mean:
+                continue
+            # +pi branches: parameter rows (client, owned parameter) from their pass on
+            per = max(1, rows_max // B)                     # parameter rows per chunk
+            for j, sl in enumerate(own):
+                if not sl:
+                    continue
+                Pj = len(sl)
+                slots = torch.tensor(sl, dtype=torch.long, device=self.device)
+                nr = min(Pj, per)
+                nkc = max(1, per // Pj) if nr == Pj else 1
+                for a0 in range(0, nk, nkc):
+                    a1 = min(nk, a0 + nkc)
+                    for r0 in range(0, Pj, nr):
+                        r1 = min(Pj, r0 + nr)
+                        src = stored[j - 1][(a0 * B) << n:(a1 * B) << n] if j > 0 else empty
+                        zb = self._pi_branch(j, xs[a0 * B:a1 * B], ths[a0:a1], slots[r0:r1], B, src)
+                        fpi[k0 + a0:k0 + a1].index_copy_(1, slots[r0:r1], zb)
+        jt = jac.permute(0, 3, 1, 2)                        # [K, P, B, C]
+        m = 0.5 * (f0.unsqueeze(1) + fpi) if with_mean else torch.zeros_like(jt)
+        return torch.stack([m + jt, m - jt], 2).contiguous()
+
+    @torch.no_grad()
+    def param_shift(self, xang: torch.Tensor, params: torch.Tensor, w: torch.Tensor, noise=None, keys=None,
+                    step: int = 0, exact_only: bool = False) -> torch.Tensor:
+        """dL/dtheta by the parameter-shift rule with prefix reuse (ROADMAP.md:23,130-135).
+
+        The naive estimator runs 2 n_theta shifted circuits per sample from |0>, each shot-sampled.  Two exact
+        identities for a rotation exp(-i theta P / 2) (P^2 = 1) give the SAME shifted expectations with far
+        fewer pass launches (``shift_pass_counts``):
+
+          * f(theta +- pi/2) = m +- f'(theta),  m = (f(theta) + f(theta + pi)) / 2   (f = a + b cos + c sin)
+          * f'(theta) for every parameter, sample and class = C adjoint sweeps (one per class, w = e_c) over the
+            stored unshifted forward, reduced per sample (spc = 1)
+          * f(theta + pi) for a parameter applied in forward pass j starts from the stored unshifted OUTPUT of
+            pass j - 1 (the kernel's ``in_rep`` maps each shifted row to its client's stored sample) and runs
+            only passes j..fwd_last; layer-1 parameters regenerate the product state in pass 0
+
+        The exact shifted expectations are then readout-confused / shot-sampled exactly as the naive estimator
+        samples them (same Philox key per (client, slot, sign) row: ``VQCEngine.param_shift_batched``), so the
+        estimator's distribution is the hardware one.  With ``shots == 0`` the sampled difference is affine in
+        f', so m is not needed (no +pi branches).  Work is chunked over clients and over shifted rows to fit
+        ``_shift_budget`` (0.4 of free HBM).  ``exact_only``: skip the readout model (tests).
+        w = dL/d<Z>_noisy [K, B, C] -> [K, n_theta]."""
+        K, B, C = w.shape
+        P = self.n_theta
+        need_m = not exact_only and noise is not None and noise.shots > 0
+        zz = self.shifted_expz(xang, params, with_mean=need_m)
+        if noise is not None and not exact_only:
+            from .statevec_hip import _keys
+            kk = None
+            if noise.shots > 0:
+                j = torch.arange(2 * P, device=self.device, dtype=torch.int64)
+                kk = keys.to(self.device).long()[:, None, :].repeat(1, 2 * P, 1)
+                kk[..., 0] = (kk[..., 0] ^ ((j + 1) * 0x9E3779B9)) & 0xFFFFFFFF
+                kk[..., 1] = (kk[..., 1] + (j + 1) * 0x85EBCA6B) & 0xFFFFFFFF
+                kk = kk.reshape(K * 2 * P, 2).contiguous()
+            ext().readout_noise(zz, C, B, K * 2 * P * B, noise.p01, noise.p10, noise.shots, _keys(kk, noise),
+                                int(step))
+        d = (zz[:, :, 0] - zz[:, :, 1]).double() * w.reshape(K, 1, B, C).double()
+        return (0.5 * d.sum((2, 3))).float()
+
+    def _pi_branch(self, j, xs, ths, slots, B, src) -> torch.Tensor:
+        """<Z> of theta + pi e_slot for clients ths [na, ps] x slots [nr] owned by forward pass j: passes
+        j..fwd_last, the first reading the clients' stored pass j - 1 outputs ``src`` [na B 2^n] (each row
+        shared by nr parameter rows: in_rep) or, for j = 0, regenerating the product state.  -> [na, nr, B, C]"""
+        E = ext()
+        na, nr = ths.shape[0], slots.numel()
+        Kr, S = na * nr, na * nr * B
+        ps = ths.shape[1]
+        thr = ths.repeat_interleave(nr, 0).view(na, nr, ps).clone()
+        thr[:, torch.arange(nr, device=self.device), slots] += float(np.pi)
+        thr = thr.view(Kr, ps).contiguous()
+        fr = self._frags(thr, Kr, "pb")
+        R = self.fwd_last
+        part = self._buf("pbpart", S * self.tiles_last * self.C, torch.float32)
+        N = S << self.n
+        empty = torch.empty(0, dtype=torch.int32, device=self.device)
+        fempty = torch.empty(0, dtype=torch.float32, device=self.device)
+        psi_in = src
+        for jj in range(j, R + 1):
+            p, fwd = self.passes[jj][0], self.passes[jj][1]
+            keep = jj < R
+            out = self._buf(f"pbpsi{(jj - j) % 2}", N, torch.int32) if keep else empty
+            first = jj == j
+            geom = self._geom(p, jj == 0, False, keep, False, B, ps, S, xs.shape[1], Kr, nr if first else 1)
+            E.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, xs, thr, fr, fempty,
+                       part if jj == R else fempty, fempty, _NODBG)
+            psi_in = out
+        z = self._buf("pbz", S * self.C, torch.float32)
+        E.readout_sum(part, self.tiles_last, self.C, S, z)
+        return z.view(na, nr, B, self.C)
 
     # ------------------------------------------------------------------ train step
     def _chunks(self, K: int, B: int) -> int:

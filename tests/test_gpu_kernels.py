@@ -283,7 +283,7 @@ def test_fedavg_saturation_is_counted_not_wrapped(cuda):
     assert int(buf[P + 5]) == 2 and int(buf[5]) == 2 ** 53 and int(buf[6]) == 0
     out = torch.zeros(6, dtype=torch.float64, device=cuda)
     theta = torch.zeros(P, device=cuda)
-    ext().round_apply(buf, P, theta, 1.0, out, 0, 1.0)
+    ext().round_apply(buf, P, theta, 1.0, out, 0, 1.0, 0)
     torch.cuda.synchronize()
     assert out[4].item() == 2.0 and int(buf[P + 5]) == 0
 
@@ -404,7 +404,7 @@ def test_secagg_masks_in_fused_reduce_match_host_protocol(cuda, dp):
     buf[: P + 1] = b
     theta = tg.to(cuda).clone()
     out = torch.zeros(6, dtype=torch.float64, device=cuda)
-    ext().round_apply(buf, P, theta, 1.0, out, sa.bits, sa.scale)
+    ext().round_apply(buf, P, theta, 1.0, out, sa.bits, sa.scale, 0)
     ref = gpu.apply(tg.to(cuda), mb.to(cuda), wsum=wb)
     assert torch.equal(theta, ref) and abs(out[5].item() - float(wb)) < 1e-12
 

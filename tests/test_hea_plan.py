@@ -107,3 +107,50 @@ def test_trimmed_plan_full_groups():
             allv, dirs = hp._group_geom(plan, p, g)[0], hp._group_geom(plan, p, g)[6]
             total += hp._best_cols(p.H, allv, dirs)[0]
         assert total == hp.FULL_SCORE * len(groups)
+
+
+@pytest.mark.parametrize("n,L,tile,min_ratio", [(24, 3, 14, 2.0), (16, 3, 14, 2.0), (14, 3, 10, 2.0),
+                                                (12, 3, 14, 1.5)])
+def test_param_shift_owners_and_pass_savings(n, L, tile, min_ratio):
+    """Every parameter is applied by exactly one forward pass (layer 1 in the generating pass 0), and the
+    prefix-reuse + pi-identity estimator launches >= 2x fewer passes than 2 n_theta naive shifted circuits
+    (adjoint passes weighted 2x)."""
+    from qfedx_amd.models.vqc import VQCSpec
+    from qfedx_amd.ops.hea_mfma import HeaMfmaProgram
+    prog = HeaMfmaProgram(VQCSpec(n, L, 2), "cpu", tile_bits=tile)
+    own = prog.shift_owners()
+    assert sorted(i for o in own for i in o) == list(range(prog.n_theta))
+    assert all(prog.plan.theta_slot(1, q) in own[0] for q in range(n))
+    c = prog.shift_pass_counts()
+    assert c["naive_fwd_passes"] / (c["reuse_fwd_passes"] + 2 * c["reuse_adj_passes"]) >= min_ratio
+
+
+def test_pi_identity_of_shifted_expectations():
+    """f(theta +- pi/2) = (f(theta) + f(theta + pi)) / 2 +- f'(theta) for every rotation parameter of the HEA
+    (float64 dense oracle; the identity HeaMfmaProgram.shifted_expz builds on)."""
+    import torch
+    from qfedx_amd.models.vqc import VQCSpec
+    from qfedx_amd.ops.statevec_torch import TorchProgram, slot_grads
+    spec = VQCSpec(5, 3, 2)
+    ops, coef = spec.program()
+    prog = TorchProgram(ops, coef, 5, dtype=torch.complex128)
+    g = torch.Generator().manual_seed(0)
+    P = spec.n_theta
+    th = torch.randn(P, generator=g, dtype=torch.float64)
+    x = torch.rand(5, generator=g, dtype=torch.float64) * 3
+    rows = []
+    for d in (0.0, np.pi, np.pi / 2, -np.pi / 2):
+        for j in range(P):
+            t = th.clone()
+            t[j] += d
+            rows.append(torch.cat([t, x]))
+    z = prog.expz(prog.run(torch.stack(rows)), spec.readout).reshape(4, P, -1)
+    base = torch.cat([th, x])[None]
+    psi = prog.run(base)
+    for c in range(2):
+        w = torch.zeros(1, 2, dtype=torch.float64)
+        w[0, c] = 1
+        gg = slot_grads(prog.adjoint_grads(base, psi, w, spec.readout), prog.ops, prog.coef, base.shape[1])[0, :P]
+        m = 0.5 * (z[0, :, c] + z[1, :, c])
+        np.testing.assert_allclose(z[2, :, c].numpy(), (m + gg).numpy(), atol=1e-10)
+        np.testing.assert_allclose(z[3, :, c].numpy(), (m - gg).numpy(), atol=1e-10)
