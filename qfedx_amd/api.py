@@ -35,4 +35,5 @@ def run_experiment(cfg: ExperimentConfig, world=None, device=None, backend=None)
     out["world_size"] = world.world_size
     out["backend"] = backend
     out["device"] = str(device)
+    out["simulator"] = getattr(adapter, "simulator", None)     # statevector | mps | density (VQC adapters)
     return out

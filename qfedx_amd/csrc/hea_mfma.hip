@@ -53,11 +53,18 @@ constexpr int ADJ_WAVES_13 = 8;   // default waves of a 2^13 adjoint workgroup (
 constexpr int CMAX = 8;
 constexpr int MAXOPS = 128;    // ops per pass program (host-checked)
 constexpr int MAXGRAD = 12;    // gradient ops per pass program (host-checked)
-// Per gradient op, 80 cross-matrix entries e = 16 k + b (k = 0: b == a, k = 1 + j: b ^ a = e_j) x (re, im) as
-// u64 LDS atomics.  A half-wave's active lanes add entries {b + 16 k} with b in {i, i + 4}: unskewed they all
-// sit on one bank pair (5-way conflicts); slot(e) = e + s(k), s = 0, 1, 2, 3, 8, spreads them over distinct
-// 8-byte bank pairs (b + s(k) distinct mod 16).
-constexpr int RIM = 88, RSTR = 2 * RIM;
+// Per gradient op, 80 cross-matrix entries e = 16 k + b (k = 0: b == a, k = 1 + j: b ^ a = e_j), each one u64
+// LDS atomic holding (re, im) as two biased 32-bit fixed-point halves (PK_*).  A half-wave's active lanes add
+// entries {b + 16 k} with b in {i, i + 4}: unskewed they all sit on one bank pair (5-way conflicts);
+// slot(e) = e + s(k), s = 0, 1, 2, 3, 8, spreads them over distinct 8-byte bank pairs (b + s(k) distinct mod 16).
+constexpr int RIM = 88, RSTR = RIM;
+// Packed entry halves: N / rho in 2^-22 units plus a bias of 2^26 per add.  |N / rho| <= C <= 8 (Cauchy-Schwarz
+// on the tile's psi and lambda / rho, rho = max |w_c|), so each add lies in [2^25, 2^27) and the sum of <= 16
+// waves' adds stays below 2^31: no carry ever crosses into the other half, and integer addition keeps the
+// cross-wave sums independent of arrival order.  One atomic and ~4 VALU per entry and component instead of
+// two int64 atomics with a 7-op fp32 -> int64 split each.
+constexpr float PK_SCALE = 0x1p22f;
+constexpr uint32_t PK_BIAS = 1u << 26;
 __device__ __forceinline__ int red_slot(int e) {
   const int k = e >> 4;
   return e + (k < 4 ? k : 8);
@@ -81,16 +88,6 @@ __device__ __forceinline__ float2 unpack_h2(uint32_t u) {
 }
 
 __device__ __forceinline__ int par(uint32_t x) { return __builtin_popcount(x) & 1; }
-
-// round(y) as int64 in single precision (|y| < 2^62): the rounded value splits exactly into 2^32 hi + lo with
-// lo in [0, 2^32).  Seven fp32 VALU ops instead of the fp64 multiply / round / split chain (the gradient
-// partials are fixed point at 2^-32 of their scale; fp32 keeps 24 of their bits, the fp16 state ~11).
-__device__ __forceinline__ long long fix64(float y) {
-  const float r = __builtin_rintf(y);
-  const float hf = __builtin_floorf(r * 0x1p-32f);
-  const float lf = __builtin_fmaf(hf, -0x1p32f, r);
-  return (long long)(((unsigned long long)(unsigned int)(int)hf << 32) | (unsigned long long)(unsigned int)lf);
-}
 
 // Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup fence and so also drains every
 // outstanding GLOBAL load (vmcnt(0)) - including the next op's prefetched record and unitary fragments.
@@ -171,9 +168,15 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
   }
 }
 
-// Interleaved adjoint image (word 2w = psi, 2w + 1 = lambda of swizzled amplitude w): a quad's psi and
-// lambda dwords go to LDS as two 16-byte pair runs.  Without a lambda input the lambda words are zeroed (the
-// observable op writes them).
+// Adjoint image: two planes, psi at word w (swizzled amplitude w, as in the forward image) and lambda at word
+// lam_word<TB>() + w = 2^TB + 4 + w.  An amplitude's psi and lambda differ by a constant byte offset, which every
+// LDS access carries as its instruction offset, so psi and lambda of one amplitude share one address VGPR and land
+// in registers exactly where the MFMA operands want them (an interleaved image read them as b64 pairs and spent a
+// v_mov per dword splitting the pairs).  The 4-word skew keeps the compiler from fusing the two reads into one
+// ds_read2st64_b32 (a register pair, split again by v_movs); a uniform shift leaves every read conflict free.
+// Without a lambda input the lambda plane is zeroed (the observable op writes it).
+template <int TB>
+__host__ __device__ constexpr uint32_t lam_word() { return (1u << TB) + 4u; }
 template <int NT, int TB = TMAX>
 __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* psrc, const uint32_t* lsrc,
                                              uint32_t* tile, int tid, int T, uint32_t h_q, uint32_t fixed) {
@@ -192,10 +195,9 @@ __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* 
     const uint32_t q = 4u * (tid + NT * i);
     if (q < (uint32_t)T) {
       const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
-      const uint4 pv = quad_perm(v[i], h & 3u), lv = quad_perm(l[i], h & 3u);
-      const uint32_t w0 = 2u * ((q ^ h) & ~3u);
-      *(uint4*)&tile[w0] = make_uint4(pv.x, lv.x, pv.y, lv.y);
-      *(uint4*)&tile[w0 + 4] = make_uint4(pv.z, lv.z, pv.w, lv.w);
+      const uint32_t w0 = (q ^ h) & ~3u;
+      *(uint4*)&tile[w0] = quad_perm(v[i], h & 3u);
+      *(uint4*)&tile[lam_word<TB>() + w0] = quad_perm(l[i], h & 3u);
     }
   }
 }
@@ -203,23 +205,7 @@ __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* 
 template <int NT, int TB = TMAX>
 __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, const uint32_t* tile, int tid, int T,
                                              uint32_t h_q, uint32_t fixed) {
-  constexpr int MQ = (1 << TB) / (4 * NT);
-  uint4 v[MQ];
-#pragma unroll
-  for (int i = 0; i < MQ; ++i) {
-    const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) {
-      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
-      const uint32_t w0 = 2u * ((q ^ h) & ~3u);
-      const uint4 a0 = *(const uint4*)&tile[w0], a1 = *(const uint4*)&tile[w0 + 4];
-      v[i] = quad_perm(make_uint4(a0.y, a0.w, a1.y, a1.w), h & 3u);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < MQ; ++i) {
-    const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
-  }
+  store_tile<NT, TB>(a, dst, tile + lam_word<TB>(), tid, T, h_q, fixed);
 }
 
 // RZ(ph) RX(th) F(x)|0> for a layer-1 qubit
@@ -283,7 +269,8 @@ template <int NX, int NW, bool IL, int SEL, int TB = TMAX>
 __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, const int* opw, uint32_t fo, int lane,
                                             int wave, int nbw) {
   constexpr int MAXB = (1 << (TB - 8)) / NW;   // column blocks per wave per op (t = 14: 64 blocks)
-  constexpr int SH = IL ? 3 : 2;
+  constexpr int SH = 2;
+  constexpr uint32_t LP = 4u * lam_word<TB>();  // lambda plane (adjoint image), bytes
   static_assert(IL || NX == 1, "the forward image holds psi only");
   const int g4 = lane >> 4, cl = lane & 15;
   uint32_t oin[4], oout[4];
@@ -297,21 +284,13 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
   uint32_t base[MAXB];
 #pragma unroll
   for (int i = 0; i < MAXB; ++i) base[i] = (bl ^ (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)]) << SH;
+  // plane x of the image: psi (0) or lambda (1); a forward image has psi only
   auto load = [&](uint32_t b, uint4* X) {
-    if constexpr (!IL) {
-      X[0] = make_uint4(lds_ld(tile, b ^ oin[0]), lds_ld(tile, b ^ oin[1]), lds_ld(tile, b ^ oin[2]),
-                        lds_ld(tile, b ^ oin[3]));
-    } else {
-      const uint2 p0 = lds_ld2(tile, b ^ oin[0]), p1 = lds_ld2(tile, b ^ oin[1]), p2 = lds_ld2(tile, b ^ oin[2]),
-                  p3 = lds_ld2(tile, b ^ oin[3]);
-      if constexpr (NX == 2) {
-        X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
-        X[1] = make_uint4(p0.y, p1.y, p2.y, p3.y);
-      } else if constexpr (SEL == 0) {
-        X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
-      } else {
-        X[0] = make_uint4(p0.y, p1.y, p2.y, p3.y);
-      }
+    const uint32_t a0 = b ^ oin[0], a1 = b ^ oin[1], a2 = b ^ oin[2], a3 = b ^ oin[3];
+#pragma unroll
+    for (int x = 0; x < NX; ++x) {
+      const uint32_t pl = (NX == 2 ? x : (IL ? SEL : 0)) ? LP : 0u;
+      X[x] = make_uint4(lds_ld(tile, a0 + pl), lds_ld(tile, a1 + pl), lds_ld(tile, a2 + pl), lds_ld(tile, a3 + pl));
     }
   };
   auto compute_store = [&](uint32_t b, const uint4* X) {
@@ -324,17 +303,14 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
       d0[x] = mfma(F[2], X[x], d0[x]);
       d1[x] = mfma(F[3], X[x], d1[x]);
     }
-    if constexpr (IL && NX == 2) {
-      lds_st2(tile, b ^ oout[0], make_uint2(pack_h2(d0[0][0], d0[0][1]), pack_h2(d0[1][0], d0[1][1])));
-      lds_st2(tile, b ^ oout[1], make_uint2(pack_h2(d0[0][2], d0[0][3]), pack_h2(d0[1][2], d0[1][3])));
-      lds_st2(tile, b ^ oout[2], make_uint2(pack_h2(d1[0][0], d1[0][1]), pack_h2(d1[1][0], d1[1][1])));
-      lds_st2(tile, b ^ oout[3], make_uint2(pack_h2(d1[0][2], d1[0][3]), pack_h2(d1[1][2], d1[1][3])));
-    } else {
-      constexpr uint32_t tb = IL ? 4u * SEL : 0u;
-      lds_st(tile, b ^ oout[0] ^ tb, pack_h2(d0[0][0], d0[0][1]));
-      lds_st(tile, b ^ oout[1] ^ tb, pack_h2(d0[0][2], d0[0][3]));
-      lds_st(tile, b ^ oout[2] ^ tb, pack_h2(d1[0][0], d1[0][1]));
-      lds_st(tile, b ^ oout[3] ^ tb, pack_h2(d1[0][2], d1[0][3]));
+    const uint32_t s0 = b ^ oout[0], s1 = b ^ oout[1], s2 = b ^ oout[2], s3 = b ^ oout[3];
+#pragma unroll
+    for (int x = 0; x < NX; ++x) {
+      const uint32_t pl = (NX == 2 ? x : (IL ? SEL : 0)) ? LP : 0u;
+      lds_st(tile, s0 + pl, pack_h2(d0[x][0], d0[x][1]));
+      lds_st(tile, s1 + pl, pack_h2(d0[x][2], d0[x][3]));
+      lds_st(tile, s2 + pl, pack_h2(d1[x][0], d1[x][1]));
+      lds_st(tile, s3 + pl, pack_h2(d1[x][2], d1[x][3]));
     }
   };
   if (nbw <= 0) return;
@@ -380,20 +356,21 @@ __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw
                                             int nbw, f4& accR, f4& accI) {
   constexpr int MAXB = (1 << (TB - 8)) / NW;
   const int g4 = lane >> 4, cl = lane & 15;
+  constexpr uint32_t LP = 4u * lam_word<TB>();
   const uint32_t om = (uint32_t)opw[W_OFF + cl] ^ fo;
   uint32_t gb[4];
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) gb[jj] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + jj] ^ om) << 3;
+  for (int jj = 0; jj < 4; ++jj) gb[jj] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + jj] ^ om) << 2;
 #pragma unroll
   for (int i = 0; i < MAXB; ++i) {
     if (i >= nbw) break;
-    const uint32_t bh = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << 3;
+    const uint32_t bh = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << 2;
     uint32_t pv[4], lv[4];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {            // (psi, lambda) of one amplitude: one b64 read
-      const uint2 v = lds_ld2(tile, gb[jj] ^ bh);
-      pv[jj] = v.x;
-      lv[jj] = v.y;
+    for (int jj = 0; jj < 4; ++jj) {            // psi and lambda of one amplitude: one address, two planes
+      const uint32_t ad = gb[jj] ^ bh;
+      pv[jj] = lds_ld(tile, ad);
+      lv[jj] = lds_ld(tile, ad + LP);
     }
     const uint4 A = make_uint4(pv[0], pv[1], pv[2], pv[3]);
     const uint4 Br = make_uint4(lv[0], lv[1], lv[2], lv[3]);
@@ -527,7 +504,7 @@ __device__ __forceinline__ void readout_op(const uint32_t* psi_t, const PassArgs
   }
 }
 
-// Adjoint seed lambda = sum_c r_c Z_c psi on the interleaved image (word 2w = psi, 2w + 1 = lambda).
+// Adjoint seed lambda = sum_c r_c Z_c psi on the adjoint image (psi plane word w, lambda plane word 2^TB + w).
 template <int NC, int NT, int TB = TMAX>
 __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, int T, uint32_t fixed,
                                        const float* rsc_s) {
@@ -543,7 +520,7 @@ __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, 
     if (i0 >= iters) break;
     uint32_t v[CH];
 #pragma unroll
-    for (int j = 0; j < CH; ++j) v[j] = tile[2 * ((tid + NT * (i0 + j)) & (T - 1))];   // in bounds; writes masked
+    for (int j = 0; j < CH; ++j) v[j] = tile[(tid + NT * (i0 + j)) & (T - 1)];   // in bounds; writes masked
     float rr[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) rr[c] = cs.flip(c, i0 / CH) ? -r[c] : r[c];
@@ -554,7 +531,7 @@ __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, 
       for (int c = 0; c < NC; ++c) fsum += cs.mul(rr[c], j, c);
       const float2 f = unpack_h2(v[j]);
       const int w = tid + NT * (i0 + j);
-      if (i0 + j < iters && w < T) tile[2 * w + 1] = pack_h2(fsum * f.x, fsum * f.y);
+      if (i0 + j < iters && w < T) tile[lam_word<TB>() + w] = pack_h2(fsum * f.x, fsum * f.y);
     }
   }
 }
@@ -594,23 +571,28 @@ __device__ __forceinline__ uint32_t tile_fixed(const PassArgs& a, int tile_id) {
   return ((uint32_t)(tile_id & ((1 << w1) - 1)) << a.c) | ((uint32_t)(tile_id >> w1) << a.hi);
 }
 
-// The op's OFF base for the tile's fixed bits (their parities with the op's frame row masks).
-__device__ __forceinline__ uint32_t op_fo(const int* opw, uint32_t fixed) {
-  const int nreal = opw[W_NREAL];
+// The op's OFF base for the tile's fixed bits (their parities with the op's frame row masks), computed for every
+// op of the pass once per workgroup (lane o, straight from the global records, behind the tile load): inside the
+// op loop it was a dependent chain of nreal LDS reads per op and wave.
+__device__ __forceinline__ uint32_t op_fo_global(const int* ow, uint32_t fixed) {
+  const int nreal = ow[W_NREAL];
   int fpb = 0;
-  for (int j = 0; j < nreal; ++j) fpb |= par(fixed & (uint32_t)opw[W_RFULL + j]) << j;
-  return (uint32_t)opw[W_OFF + fpb];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j < nreal) fpb |= par(fixed & (uint32_t)ow[W_RFULL + j]) << j;
+  return (uint32_t)ow[W_OFF + fpb];
 }
 
 // ------------------------------------------------------------------------------------------- forward pass
 // One workgroup per tile of 2^t <= 2^14 amplitudes: 8 waves and 64 KB of LDS, so two workgroups share a CU and
 // one's tile load overlaps the other's group ops (minimum waves per SIMD 4: <= 128 VGPRs).
-template <int NCK>
+template <int NCK, bool FULL>
 __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   constexpr int NT = NT_FWD, NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint32_t psi_t[1 << TMAX];   // fp16 (re, im), swizzled
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
   __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
+  __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (op_fo_global)
   __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];   // op unitary fragments, double buffered
   __shared__ float red[NW * CMAX];
   __shared__ float2 wv[32][2];
@@ -636,7 +618,10 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
 
   // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op); op 0's
   // are requested before the initial tile, so their latency hides behind the tile load / layer-1 generation
-  if (tid < a.nops) fidx_s[tid] = a.fidx[tid];   // LDS copy: the prefetch below never waits on a global load
+  if (tid < a.nops) {                            // LDS copies: the prefetch below never waits on a global load
+    fidx_s[tid] = a.fidx[tid];
+    fo_s[tid] = op_fo_global(a.ops + (size_t)tid * OPW, fixed);
+  }
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
   if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
@@ -716,7 +701,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
 
   // ---------------------------------------------------------------- op list
   const int ncol = T >> 4, nblk = ncol >> 4;
-  const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
+  const int nbw = FULL ? (1 << (TMAX - 8)) / NW : (wave < nblk ? (nblk - wave + NW - 1) / NW : 0);   // (uniform)
   lds_barrier_dma();
   HEA_MARK();
   for (int o = 0; o < a.nops; ++o) {
@@ -752,7 +737,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
     }
 #endif
     if (code == OP_APPLY) {
-      group_apply<1, NW, false, 0>(psi_t, F, opw, op_fo(opw, fixed), lane, wave, nbw);
+      group_apply<1, NW, false, 0>(psi_t, F, opw, fo_s[o], lane, wave, nbw);
     } else if (code == OP_READOUT) {
       const size_t pidx = ((size_t)s * a.n_tiles + tile_id) * a.C;
       readout_op<NCK, NT>(psi_t, a, opw, tid, lane, wave, T, fixed, red, pidx);
@@ -777,14 +762,15 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
 // round trip and was slower (16q adjoint 0.67 -> 0.72 ms).
 // WV = waves per workgroup: 2^(TB - 10) gives 4 column blocks per wave per op (the round-2 layout); fewer waves
 // give each wave more blocks per op, amortising the per-op setup / epilogue over more MFMAs.
-template <int NCK, int TB, int WV>
+template <int NCK, int TB, int WV, bool FULL>
 __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(PassArgs a) {
   constexpr int NT = 64 * WV, NW = WV;
   static_assert(NW % 2 == 0 && (1 << (TB - 8)) % NW == 0, "column blocks per wave must be whole, block pairs aligned");
   // (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
-  __shared__ __attribute__((aligned(16))) uint32_t tile[2 << TB];
+  __shared__ __attribute__((aligned(16))) uint32_t tile[lam_word<TB>() + (1 << TB)];
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
   __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
+  __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (op_fo_global)
   __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];   // op unitary fragments, double buffered
   // the 80 cross-matrix entries a partial trace can use (b = a, and b = a ^ e_j) x (re, im), 2^-32 fixed point
   constexpr bool RING = TB < 14;
@@ -808,7 +794,10 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   QFX_DCHECK(tile_id < a.slab_tiles);
 
   // op 0's record and fragments are requested before the tile load (their latency hides behind it)
-  if (tid < a.nops) fidx_s[tid] = a.fidx[tid];
+  if (tid < a.nops) {
+    fidx_s[tid] = a.fidx[tid];
+    fo_s[tid] = op_fo_global(a.ops + (size_t)tid * OPW, fixed);
+  }
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
   if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
@@ -820,7 +809,8 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
     for (int c = 0; c < a.C; ++c) rho = fmaxf(rho, fabsf(a.wread[(size_t)s * a.C + c]));
     if (rho == 0.f) rho = 1.f;
     for (int c = 0; c < NCK; ++c) rsc[c] = c < a.C ? a.wread[(size_t)s * a.C + c] / rho : 0.f;
-    rsc[CMAX] = rho / (a.scale * a.scale);
+    rsc[CMAX] = rho;
+    rsc[CMAX + 1] = PK_SCALE / (a.scale * a.scale);
   }
   for (int e = tid; e < NREG * RSTR; e += NT) red64[e] = 0ull;
 
@@ -829,16 +819,18 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   // wave).
   auto reduce_region = [&](int reg, int r) {
     const int j = r >> 3, y = (r >> 2) & 1, x = (r >> 1) & 1, comp = r & 1;
-    const unsigned long long* rg = red64 + reg * RSTR + comp * RIM;
-    unsigned long long v = 0ull;
+    const unsigned long long* rg = red64 + reg * RSTR;
+    long long v = 0;
     if (j < gmeta_s[reg][1]) {
       const int lowm = (1 << j) - 1;
       for (int o8 = 0; o8 < 8; ++o8) {    // the other three bits of b
         const int bb = ((o8 & ~lowm) << 1) | (o8 & lowm) | (y << j);
-        v += rg[red_slot(x == y ? bb : 16 + 16 * j + bb)];
+        const unsigned long long u = rg[red_slot(x == y ? bb : 16 + 16 * j + bb)];
+        v += (long long)(uint32_t)(comp ? (u >> 32) : u) - (long long)NW * PK_BIAS;
       }
     }
-    slab[(size_t)gmeta_s[reg][0] * 32 + r] = (long long)v;
+    // 2^-22 units of N / rho -> the slab's 2^-32 units of N (one exact integer sum per tile: deterministic)
+    slab[(size_t)gmeta_s[reg][0] * 32 + r] = __double2ll_rn((double)v * (double)rsc[CMAX] * (FIX / (double)PK_SCALE));
   };
   auto flush = [&](int reg) {                           // one wave: reduce, then zero the region
     if (lane < 32) reduce_region(reg, lane);
@@ -848,7 +840,9 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
 
   // ---------------------------------------------------------------- op list
   const int ncol = T >> 4, nblk = ncol >> 4;
-  const int nbw = wave < nblk ? (nblk - wave + NW - 1) / NW : 0;   // this wave's column blocks (uniform)
+  // FULL (t == TB): every wave owns exactly (2^(TB - 8)) / NW column blocks - a compile-time count, so the block
+  // loops of the group ops carry no bounds checks or branches
+  const int nbw = FULL ? (1 << (TB - 8)) / NW : (wave < nblk ? (nblk - wave + NW - 1) / NW : 0);
   lds_barrier_dma();
   HEA_MARK();
   int ngrad = 0;
@@ -878,7 +872,7 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
     }
     const int code = opw[W_CODE];
 #if QFX_CHECKS_ON
-    QFX_DCHECK(code >= OP_UNAPPLY_PSI && code <= OP_BACK && code != OP_READOUT);
+    QFX_DCHECK(code >= OP_APPLY && code <= OP_BACK && code != OP_READOUT);
     if (code != OP_OBS) {
       QFX_DCHECK(opw[W_NREAL] >= 0 && opw[W_NREAL] <= 4);
       QFX_DCHECK((uint32_t)opw[W_OFF + (lane & 15)] < (uint32_t)T);
@@ -887,7 +881,7 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
       // -1 = no unitary (cross-matrix-only gradient ops); every op that applies one names a fragment
       QFX_DCHECK(fidx_s[o] >= -1 && fidx_s[o] < 4 * a.n_slots);
       QFX_DCHECK(fidx_s[o] >= 0 || code == OP_GRAD || code == OP_GRAD_L1);
-      if (code != OP_UNAPPLY_PSI && code != OP_UNAPPLY_LAM)
+      if (code != OP_UNAPPLY_PSI && code != OP_UNAPPLY_LAM && code != OP_APPLY)
         QFX_DCHECK(opw[W_GIDX] >= 0 && opw[W_GIDX] < a.n_gradops);
     } else {
       QFX_DCHECK(opw[W_NREAL] >= 1 && opw[W_NREAL] <= a.C);
@@ -895,12 +889,13 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
 #endif
     if (code == OP_OBS) {
       obs_op<NCK, NT, TB>(tile, opw, tid, T, fixed, rsc);
-    } else if (code == OP_UNAPPLY_PSI) {
-      group_apply<1, NW, true, 0, TB>(tile, F, opw, op_fo(opw, fixed), lane, wave, nbw);
+    } else if (code == OP_UNAPPLY_PSI || code == OP_APPLY) {
+      // U^H (or, re-applying a recomputed last pass, U) on the psi plane
+      group_apply<1, NW, true, 0, TB>(tile, F, opw, fo_s[o], lane, wave, nbw);
     } else if (code == OP_UNAPPLY_LAM) {
-      group_apply<1, NW, true, 1, TB>(tile, F, opw, op_fo(opw, fixed), lane, wave, nbw);
+      group_apply<1, NW, true, 1, TB>(tile, F, opw, fo_s[o], lane, wave, nbw);
     } else if (code == OP_BACK || code == OP_GRAD || code == OP_GRAD_L1) {
-      const uint32_t fo = op_fo(opw, fixed);
+      const uint32_t fo = fo_s[o];
       f4 accR = {0.f, 0.f, 0.f, 0.f}, accI = {0.f, 0.f, 0.f, 0.f};
       if (!(QFX_HEA_ABLATE && (a.ablate & 4))) group_cross<NW, TB>(tile, opw, fo, lane, wave, nbw, accR, accI);
       if (code == OP_BACK && !(QFX_HEA_ABLATE && (a.ablate & 8))) {
@@ -909,12 +904,12 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
         else
           group_apply<1, NW, true, 1, TB>(tile, F, opw, fo, lane, wave, nbw);
       }
-      // Cross-wave sum of the partial-trace entries of N, pre-scaled by the sample's rho / scale^2, in 2^-32
-      // fixed point with 64-bit LDS atomics into the op's region.  Integer addition is associative, so the sums
-      // are bitwise independent of the order the waves (and, in hea_grad_reduce, samples and tiles) arrive.
+      // Cross-wave sum of the partial-trace entries of N / rho into the op's region: packed biased fixed point
+      // (PK_*), one u64 LDS atomic per entry.  Integer addition is associative, so the sums are bitwise
+      // independent of the order the waves (and, in hea_grad_reduce, samples and tiles) arrive.
       // Lane (g4, cl) holds N[4 g4 + i][cl]; entry slot: b == a -> b, b ^ a == e_j -> 16 + 16 j + b.
       const int reg = RING ? ngrad & 1 : ngrad;
-      const float sc = (float)((double)rsc[CMAX] * FIX);
+      const float sc = rsc[CMAX + 1];
       unsigned long long* rg = red64 + reg * RSTR;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -922,8 +917,8 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
         if (QFX_HEA_ABLATE && (a.ablate & 2)) break;
         if (__builtin_popcount(d) <= 1) {
           const int e = d == 0 ? (int)bb : 16 + 16 * (__builtin_ctz(d)) + (int)bb;
-          atomicAdd(&rg[red_slot(e)], (unsigned long long)fix64(accR[i] * sc));
-          atomicAdd(&rg[RIM + red_slot(e)], (unsigned long long)fix64(accI[i] * sc));
+          const uint32_t lo = (uint32_t)(int)(accR[i] * sc) + PK_BIAS, hi = (uint32_t)(int)(accI[i] * sc) + PK_BIAS;
+          atomicAdd(&rg[red_slot(e)], ((unsigned long long)hi << 32) | lo);
         }
       }
       if (tid == 0) {
@@ -1059,16 +1054,25 @@ extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_sample
     const char* e = getenv("QFEDX_HEA_ADJ_WAVES");
     adj_waves = (e && atoi(e) == 8) ? 8 : (e && atoi(e) == 4 ? 4 : hea::ADJ_WAVES_13);
   }
+  static int adj_full = -1;   // compile-time block count for full 2^13 adjoint tiles (QFEDX_HEA_ADJ_FULL = 0 | 1)
+  if (adj_full < 0) {
+    const char* e = getenv("QFEDX_HEA_ADJ_FULL");
+    adj_full = e ? (atoi(e) != 0) : 0;
+  }
 #define HEA_LAUNCH(NCK)                                                                                     \
   do {                                                                                                     \
-    if (!adjoint)                                                                                          \
-      hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);             \
+    if (!adjoint && a.t == hea::TMAX)                                                                      \
+      hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK, true>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);       \
+    else if (!adjoint)                                                                                     \
+      hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK, false>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);      \
     else if (a.t <= 13 && adj_waves == 4)                                                                  \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 4>), dim3(grid), dim3(256), 0, st, a);              \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 4, false>), dim3(grid), dim3(256), 0, st, a);       \
+    else if (a.t == 13 && adj_full)                                                                        \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, true>), dim3(grid), dim3(512), 0, st, a);        \
     else if (a.t <= 13)                                                                                    \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8>), dim3(grid), dim3(512), 0, st, a);              \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, false>), dim3(grid), dim3(512), 0, st, a);       \
     else                                                                                                   \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14, 16>), dim3(grid), dim3(1024), 0, st, a);            \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14, 16, true>), dim3(grid), dim3(1024), 0, st, a);      \
   } while (0)
   switch (hea::class_kernel(a.C)) {
     case 1: HEA_LAUNCH(1); break;

@@ -90,14 +90,18 @@ class HeaMfmaProgram:
         self.passes = []
         gmeta = []
         progs_f = pass_programs(self.plan, [])
-        progs_a = pass_programs(plan_a, gmeta)
-        self.n_gradops = len(gmeta)
         # Forward passes after the last one that applies a unitary are identities on the state (they exist for
         # the adjoint's layer-1 gradient tiles, e.g. every pass of an L = 1 circuit): the forward stops at that
         # pass, reads out there, and later passes' stored outputs alias its output.
         applies = [j for j, (_, fwd, _) in enumerate(progs_f) if any(int(w[W_CODE]) == OP_APPLY for w in fwd)]
         self.fwd_last = applies[-1] if applies else 0
         J = len(progs_f)
+        # The adjoint of the last pass re-applies that pass's groups in-tile from its stored INPUT, so the
+        # forward's last pass only reads out (QFEDX_HEA_RECOMPUTE=0: store its output instead).  Needs a stored
+        # input (J >= 2) and a last pass that applies groups.
+        self.recompute = (J >= 2 and self.fwd_last == J - 1 and os.environ.get("QFEDX_HEA_RECOMPUTE", "1") != "0")
+        progs_a = pass_programs(plan_a, gmeta, recompute_last=self.recompute)
+        self.n_gradops = len(gmeta)
         if self.fwd_last < J - 1:
             pr, fr_ops, ar = progs_f[self.fwd_last]
             fr_ops = np.concatenate([fr_ops, obs_table(self.plan, pr, OP_READOUT)[None]], 0)
@@ -188,7 +192,7 @@ class HeaMfmaProgram:
         J, R = self.n_passes, self.fwd_last
         for j in range(R + 1):
             p, fwd = self.passes[j][0], self.passes[j][1]
-            keep = j < R or store_last
+            keep = j < R or (store_last and not self.recompute)
             # evaluation only needs the previous pass output: two ping-pong buffers instead of one per pass
             name = f"{tag}psi{j}" if store_last else f"{tag}pe{j % 2}"
             out = self._buf(name, N, torch.int32) if keep else empty
@@ -200,7 +204,9 @@ class HeaMfmaProgram:
                 after_first()
             if keep:
                 stored.append(out)
-        if store_last:
+        if store_last and self.recompute:
+            stored.append(stored[R - 1])             # the last adjoint pass starts from its pass's input
+        elif store_last:
             stored += [stored[R]] * (J - 1 - R)
         return stored
 
@@ -515,7 +521,7 @@ class HeaMfmaProgram:
                                         (f"c{i}wread", Si * C, torch.float32),
                                         (f"c{i}gslab", Si * self.slab_tiles * self.n_gradops * 32, torch.int64)):
                     self._buf(name, numel, dt)
-                for j in range(self.fwd_last + 1):
+                for j in range(self.fwd_last + (0 if self.recompute else 1)):
                     self._buf(f"c{i}psi{j}", Si << self.n, torch.int32)
                 for j in range(min(2, self.n_passes - 1)):
                     self._buf(f"c{i}lam{j}", Si << self.n, torch.int32)

@@ -557,9 +557,12 @@ def obs_table(plan: HEAPlan, p: Pass, code: int) -> np.ndarray:
     return w
 
 
-def pass_programs(plan: HEAPlan, meta: list | None = None):
+def pass_programs(plan: HEAPlan, meta: list | None = None, recompute_last: bool = False):
     """Forward and adjoint op lists per pass: list of (Pass, fwd_ops [k, OP_WORDS], adj_ops).  ``meta``
-    (optional list) receives one row per gradient op: [tiles of its pass, nreal, theta slots x4, phi slots x4]."""
+    (optional list) receives one row per gradient op: [tiles of its pass, nreal, theta slots x4, phi slots x4].
+    ``recompute_last``: the last pass's adjoint starts from that pass's INPUT and re-applies its groups in-tile
+    before the observable op, so the forward's last pass never stores its output (one state write and read of
+    HBM per sample saved for a few in-tile group ops)."""
     out = []
     gidx = [0]
     gmeta = meta if meta is not None else []
@@ -568,8 +571,13 @@ def pass_programs(plan: HEAPlan, meta: list | None = None):
         fwd = [group_table(plan, p, g, OP_APPLY) for g in p.groups]
         if j == J - 1:
             fwd.append(obs_table(plan, p, OP_READOUT))
-        # the adjoint of pass j starts from pass j's stored OUTPUT (no recompute) and walks back
-        adj = [obs_table(plan, p, OP_OBS)] if j == J - 1 else []
+        # the adjoint of pass j starts from pass j's stored OUTPUT (or, recomputing the last pass, its input) and
+        # walks back
+        adj = []
+        if j == J - 1 and recompute_last:
+            adj = [group_table(plan, p, g, OP_APPLY) for g in p.groups]
+        if j == J - 1:
+            adj.append(obs_table(plan, p, OP_OBS))
         rev = list(reversed(p.groups))
         for i, g in enumerate(rev):
             # gradient cross matrix + U^H on lambda (and on psi while it is still needed further back)
@@ -670,7 +678,8 @@ def _round16(z):
     return (z.real.astype(np.float16).astype(np.float64) + 1j * z.imag.astype(np.float16).astype(np.float64))
 
 
-def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp16: bool = False):
+def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp16: bool = False,
+            recompute_last: bool = False):
     """Tile-exact execution of ``plan`` with the kernel's tables.
 
     xang [K, B, n] encoded feature angles, params [K, P] (theta first), wread [K, B, C] = dL/d<Z_c>.
@@ -679,7 +688,7 @@ def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp1
     """
     n, t = plan.n, plan.t
     K, B, _ = xang.shape
-    progs = pass_programs(plan)
+    progs = pass_programs(plan, recompute_last=recompute_last)
     rnd = _round16 if fp16 else (lambda z: z)
     scale = float(1 << (n // 2))
     expz = np.zeros((K, B, plan.C))
@@ -730,7 +739,8 @@ def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp1
             lam = None
             for j in range(len(progs) - 1, -1, -1):
                 p, _, adj = progs[j]
-                psi_in = stored[j + 1]                    # output of forward pass j
+                # output of forward pass j (its input when the last pass is recomputed in-tile)
+                psi_in = stored[j] if (recompute_last and j == len(progs) - 1) else stored[j + 1]
                 lam_out = np.zeros(1 << n, dtype=np.complex128)
                 sg_w = np.array([sigma(p.H, int(x)) for x in range(1 << p.t)])
                 for tid in range(1 << (n - p.t)):

@@ -110,3 +110,18 @@ def test_centralized_mode_pools_every_shard_into_one_client():
     assert cen.num_clients == 1 and cen.client_ids == [0] and len(cen.clients) == 1
     assert cen.clients[0][1].shape[0] == sum(fed.sizes())
     assert build_federated_data(cfg, clients=[]).clients == []
+
+
+def test_noise_grid_runs_exact_amplitude_damping(tmp_path):
+    """configs/grid_noise.yaml: noise.kind=amplitude runs EXACT amplitude damping on the density-matrix simulator,
+    amplitude_twirl its Pauli twirl on statevector trajectories (ROADMAP.md:66-73)."""
+    import yaml
+    spec = yaml.safe_load(open(os.path.join(ROOT, "configs", "grid_noise.yaml")))
+    spec["base"] = os.path.join(ROOT, "configs", spec["base"])
+    spec["seeds"] = [0]
+    spec["fixed"] = {"train.num_rounds": 1, "runtime.device": "cpu", "runtime.log_every": 100}
+    res = run_grid(spec, str(tmp_path / "g"))
+    sim = {r["config"]["noise"]["kind"]: r["simulator"] for r in res}
+    assert sim["amplitude"] == "density" and sim["amplitude_twirl"] == "statevector"
+    assert sim["none"] == "statevector" and sim["depolarizing"] == "statevector"
+    assert all(r["final_loss"] == r["final_loss"] for r in res)       # finite

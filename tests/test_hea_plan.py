@@ -41,6 +41,12 @@ def test_emulated_plan_matches_dense(n, L, t, chain, feat):
     ez3, gr3 = hp.emulate(plan, x.numpy(), params.numpy(), wr.numpy(), fp16=True)   # kernel storage format
     np.testing.assert_allclose(ez3, ez, atol=2e-3)
     np.testing.assert_allclose(gr3, gr, atol=3e-3 * max(1.0, np.abs(gr).max()))
+    if len(plan.passes) >= 2:
+        # last adjoint pass re-applies its groups from the pass input: the same fp16 values (same ops, same
+        # rounding), so the gradients are bitwise those of the stored-output program
+        ez4, gr4 = hp.emulate(plan, x.numpy(), params.numpy(), wr.numpy(), fp16=True, recompute_last=True)
+        np.testing.assert_array_equal(ez4, ez3)
+        np.testing.assert_array_equal(gr4, gr3)
 
 
 @pytest.mark.parametrize("n,L,passes", [(16, 3, 2), (16, 2, 2), (20, 2, 2), (20, 3, 2), (24, 2, 3), (12, 3, 1)])
