@@ -78,7 +78,9 @@ def precision_check(runner, batch: int) -> dict:
     if getattr(eng, "hip", None) is None or not hasattr(eng.hip, "vjp") or isinstance(eng.hip, HipProgram):
         return {}
     store = runner.store
-    xang = spec.encode_features(store.X[:, :batch].float())
+    # at most ~4 GiB of fp32 reference states (all clients at the 16q headline; a few at 24q)
+    kmax = max(1, (4 << 30) // (batch * (8 << spec.n_qubits)))
+    xang = spec.encode_features(store.X[:kmax, :batch].float())
     K, B = xang.shape[:2]
     th = runner.params[: spec.n_theta].float()[None].expand(K, -1).contiguous()
     g = torch.Generator(device="cpu").manual_seed(1234)

@@ -33,6 +33,9 @@ SUITE = {
                           None),
     "vqc16q_bf16_8": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1"],
                       "client local-steps/sec (16-qubit VQC bf16 state x 8 clients)", None),
+    "vqc16q_bf16_8_mfma": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1", "model.state_dtype=mfma"],
+                           "client local-steps/sec (16-qubit VQC x 8 clients, fp16 MFMA engine in place of bf16 "
+                           "storage)", None),
     "vqc16q_64": ("configs/headline_16q_64clients.yaml", ["model.state_dtype=fp32"],
                   "client local-steps/sec (16-qubit VQC x 64 clients federated rounds)", None),
     "vqc16q_64_mfma": ("configs/headline_16q_64clients.yaml", ["model.state_dtype=mfma"],
@@ -109,6 +112,13 @@ def main():
                        "shots": cfg.noise.shots},
         }
         eng = getattr(runner.adapter, "engine", None)
+        if kind == "vqc" and backend == "hip":
+            from bench import precision_check
+            rec.update(precision_check(runner, t.batch_size))     # untimed: MFMA vs fp32 VALU engine
+            if cfg.model.state_dtype == "mfma" and "bf16" in path:
+                rec["dtype_note"] = ("BASELINE config 2 names bf16 state storage; the fp16 MFMA engine stores "
+                                     "fp16 amplitudes (11-bit significand vs bf16's 8), so the substitution is more "
+                                     "precise, not less: see max_abs_err_* against the fp32 engine")
         if t.grad_method == "param_shift" and eng is not None and hasattr(eng.hip, "shift_pass_counts"):
             # pass launches per sample of one gradient: naive shifted circuits vs prefix reuse + pi identity
             rec["param_shift"] = dict(eng.hip.shift_pass_counts(), reuse=bool(eng.ps_reuse))

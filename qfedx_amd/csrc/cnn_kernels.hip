@@ -665,8 +665,9 @@ __global__ void cnn_reduce(const float* __restrict__ part, int G, float* __restr
 // --------------------------------------------------------------------------------------------
 constexpr int HID = 64, CMAXC = 16, HB = 64;
 constexpr int F1IN = C2 * Q2 * Q2;   // 1568 fc1 inputs
-constexpr int FC_KS = 4, FC_KC = F1IN / FC_KS, FC_T = FC_KC / 4, FC_U = 7;   // fc1 split: 392 inputs, 98 steps
-static_assert(FC_KC * FC_KS == F1IN && FC_T % FC_U == 0, "fc1 split");
+constexpr int FC_KS = 7, FC_KC = F1IN / FC_KS, FC_T16 = FC_KC / 16;   // fc1 split: 224 inputs, 14 x 16 per chunk
+static_assert(FC_KC * FC_KS == F1IN && FC_T16 * 16 == FC_KC, "fc1 split");
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));   // client parameter rows are only 4-B aligned
 constexpr int HG = (CMAXC * HID + CMAXC + 255) / 256;   // fc2 gradient entries per thread
 
 // Dropout: either a [K*B, 64] mask, or (mask == nullptr) the client's keyed Philox uniforms u (element b*64 + j of
@@ -827,38 +828,43 @@ __global__ void __launch_bounds__(256) cnn_fc1_wgrad(const float* __restrict__ d
 // --------------------------------------------------------------------------------------------
 // fc1 forward, split over the inputs:  h1p[k][g][s][j] = sum_{c in chunk g} pool2[k][s][c] W1[k][j][c]
 // grid (sample tile of 32, client, chunk g < FC_KS): 4 waves, wave w owns units 16w .. 16w + 15 (one n-tile) of
-// two m-tiles (32 samples).  MFMA step t, lane group kq <-> input c = g * FC_KC + 4 t + kq: the 64 lanes of a load
-// read 16 rows x 16 contiguous bytes.  The FC_KS partial sums are added in fixed order by the consumer (cnn_head /
-// cnn_eval_head), so a client's h1 never depends on how many clients share the launch (unlike a library batched
-// GEMM, whose algorithm and split-K change with the batch count).
+// two m-tiles (32 samples).  K order: MFMA step 4T + u, lane group kq <-> input c = g FC_KC + 16 T + 4 kq + u, so
+// one 16-byte load per lane feeds four steps (A: a pool2 row, B: a W1 row, both contiguous in c) and the 64 lanes
+// of a load read 16 rows x 64 contiguous bytes.  The next T's loads are in flight during this T's MFMAs.  The
+// FC_KS partial sums are added in fixed order by the consumer (cnn_head / cnn_eval_head), so a client's h1 never
+// depends on how many clients share the launch (unlike a library batched GEMM, whose algorithm and split-K change
+// with the batch count).
 // --------------------------------------------------------------------------------------------
-
 __global__ void __launch_bounds__(256) cnn_fc1_fwd(const float* __restrict__ pool2, const float* __restrict__ params,
                                                    int P, int off_w1, int B, float* __restrict__ h1p) {
   const int s0 = blockIdx.x * 32, k = blockIdx.y, g = blockIdx.z;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, kq = lane >> 4;
-  const int cb = g * FC_KC + kq;
+  const int cb = g * FC_KC + 4 * kq;
   const bool ok0 = s0 + i < B, ok1 = s0 + 16 + i < B;
-  const float* a0 = pool2 + ((size_t)k * B + (ok0 ? s0 + i : 0)) * F1IN + cb;
-  const float* a1 = pool2 + ((size_t)k * B + (ok1 ? s0 + 16 + i : 0)) * F1IN + cb;
-  const float* bw = params + (size_t)k * P + off_w1 + (size_t)(wave * 16 + i) * F1IN + cb;
+  const f4u* a0 = (const f4u*)(pool2 + ((size_t)k * B + (ok0 ? s0 + i : 0)) * F1IN + cb);
+  const f4u* a1 = (const f4u*)(pool2 + ((size_t)k * B + (ok1 ? s0 + 16 + i : 0)) * F1IN + cb);
+  const f4u* bw = (const f4u*)(params + (size_t)k * P + off_w1 + (size_t)(wave * 16 + i) * F1IN + cb);
+  const f4u zero = {0.f, 0.f, 0.f, 0.f};
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  for (int t0 = 0; t0 < FC_T; t0 += FC_U) {
-    float x0[FC_U], x1[FC_U], w[FC_U];
+  f4u x0 = ok0 ? a0[0] : zero, x1 = ok1 ? a1[0] : zero, w = bw[0];
 #pragma unroll
-    for (int u = 0; u < FC_U; ++u) {
-      const int c = 4 * (t0 + u);
-      x0[u] = ok0 ? a0[c] : 0.f;
-      x1[u] = ok1 ? a1[c] : 0.f;
-      w[u] = bw[c];
+  for (int T = 0; T < FC_T16; ++T) {
+    f4u nx0 = zero, nx1 = zero, nw = zero;
+    if (T + 1 < FC_T16) {                         // 16 inputs ahead = 4 float4
+      nx0 = ok0 ? a0[4 * (T + 1)] : zero;
+      nx1 = ok1 ? a1[4 * (T + 1)] : zero;
+      nw = bw[4 * (T + 1)];
     }
 #pragma unroll
-    for (int u = 0; u < FC_U; ++u) {
+    for (int u = 0; u < 4; ++u) {
       acc0 = mfma(x0[u], w[u], acc0);
       acc1 = mfma(x1[u], w[u], acc1);
     }
+    x0 = nx0;
+    x1 = nx1;
+    w = nw;
   }
   float* out = h1p + (((size_t)k * FC_KS + g) * B) * HID + wave * 16 + i;
 #pragma unroll
@@ -871,52 +877,68 @@ __global__ void __launch_bounds__(256) cnn_fc1_fwd(const float* __restrict__ poo
 
 // --------------------------------------------------------------------------------------------
 // fc1 input gradient:  dP2[k][s][c] = sum_j dh1[k][s][j] W1[k][j][c]
-// grid (128-input chunk, client, sample tile of 32): wave w owns inputs c0 + 32 w + [0, 32) (two n-tiles) of two
-// m-tiles; K = the 64 units, step t, lane group kq <-> unit j = 4 t + kq (16 steps; a W1 load reads 4 rows x 64
-// contiguous bytes).  Every operand of the launch is loaded before the first MFMA.
+// grid (256-input chunk, client, sample tile of 32): wave w owns inputs cw = c0 + 64 w + [0, 64) as four n-tiles
+// whose columns interleave (n-tile q, lane i <-> input cw + 4 i + q), so ONE 16-byte W1 load per lane holds the B
+// operand of all four n-tiles at one unit j, and a load's 64 lanes read 4 rows x 256 contiguous bytes.  K order:
+// step 4T + u, lane group kq <-> unit j = 16 T + 4 kq + u (dh1 rows: one 16-byte load per lane feeds four steps).
+// The four n-tiles of an accumulator row are four consecutive inputs: one 16-byte store.
 // --------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) cnn_fc1_dgrad(const float* __restrict__ dh1, const float* __restrict__ params,
                                                      int P, int off_w1, int B, float* __restrict__ dP2) {
-  const int c0 = blockIdx.x * 128, k = blockIdx.y, s0 = blockIdx.z * 32;
+  const int c0 = blockIdx.x * 256, k = blockIdx.y, s0 = blockIdx.z * 32;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 15, kq = lane >> 4;
+  const int cc = c0 + 64 * wave + 4 * i;                 // this lane's 4 consecutive inputs
+  const bool okc = cc < F1IN;                            // F1IN % 4 == 0: all four or none
   const bool ok0 = s0 + i < B, ok1 = s0 + 16 + i < B;
-  const float* d0 = dh1 + ((size_t)k * B + (ok0 ? s0 + i : 0)) * HID + kq;
-  const float* d1 = dh1 + ((size_t)k * B + (ok1 ? s0 + 16 + i : 0)) * HID + kq;
-  const int ca = c0 + 32 * wave + i, cbn = ca + 16;
-  const bool oka = ca < F1IN, okb = cbn < F1IN;
-  const float* w = params + (size_t)k * P + off_w1 + (size_t)kq * F1IN;
-  float x0[16], x1[16], wa[16], wb[16];
+  const f4u* d0 = (const f4u*)(dh1 + ((size_t)k * B + (ok0 ? s0 + i : 0)) * HID + 4 * kq);
+  const f4u* d1 = (const f4u*)(dh1 + ((size_t)k * B + (ok1 ? s0 + 16 + i : 0)) * HID + 4 * kq);
+  const float* w = params + (size_t)k * P + off_w1 + (okc ? cc : 0);
+  const f4u zero = {0.f, 0.f, 0.f, 0.f};
+  f4u x0[4], x1[4];
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    x0[t] = ok0 ? d0[4 * t] : 0.f;
-    x1[t] = ok1 ? d1[4 * t] : 0.f;
-    wa[t] = oka ? w[(size_t)(4 * t) * F1IN + ca] : 0.f;
-    wb[t] = okb ? w[(size_t)(4 * t) * F1IN + cbn] : 0.f;
+  for (int T = 0; T < 4; ++T) {
+    x0[T] = ok0 ? d0[4 * T] : zero;
+    x1[T] = ok1 ? d1[4 * T] : zero;
   }
-  f4 a00 = {0.f, 0.f, 0.f, 0.f}, a01 = a00, a10 = a00, a11 = a00;
+  f4 acc[2][4];
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
-    a00 = mfma(x0[t], wa[t], a00);
-    a01 = mfma(x0[t], wb[t], a01);
-    a10 = mfma(x1[t], wa[t], a10);
-    a11 = mfma(x1[t], wb[t], a11);
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[m][q] = f4{0.f, 0.f, 0.f, 0.f};
+  auto wrow = [&](int T, int u) -> f4u {
+    return okc ? *(const f4u*)(w + (size_t)(16 * T + 4 * kq + u) * F1IN) : zero;
+  };
+  f4u wv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) wv[u] = wrow(0, u);
+#pragma unroll
+  for (int T = 0; T < 4; ++T) {
+    f4u nw[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) nw[u] = T + 1 < 4 ? wrow(T + 1, u) : zero;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc[0][q] = mfma(x0[T][u], wv[u][q], acc[0][q]);
+        acc[1][q] = mfma(x1[T][u], wv[u][q], acc[1][q]);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) wv[u] = nw[u];
   }
+  if (!okc) return;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int sa = s0 + 4 * kq + r, sb = s0 + 16 + 4 * kq + r;
-    float* ra = dP2 + ((size_t)k * B + sa) * F1IN;
-    float* rb = dP2 + ((size_t)k * B + sb) * F1IN;
-    if (sa < B) {
-      if (oka) ra[ca] = a00[r];
-      if (okb) ra[cbn] = a01[r];
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sm = s0 + 16 * m + 4 * kq + r;
+      if (sm < B) {
+        const f4 v = {acc[m][0][r], acc[m][1][r], acc[m][2][r], acc[m][3][r]};
+        *(f4*)(dP2 + ((size_t)k * B + sm) * F1IN + cc) = v;
+      }
     }
-    if (sb < B) {
-      if (oka) rb[ca] = a10[r];
-      if (okb) rb[cbn] = a11[r];
-    }
-  }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1083,7 +1105,7 @@ extern "C" int qfx_cnn_fc1_forward(const float* pool2, const float* params, int 
 extern "C" int qfx_cnn_fc1_dgrad(const float* dh1, const float* params, int P, int off_w1, int K, int B, float* dP2,
                                  hipStream_t st) {
   if (K <= 0 || B <= 0) return 0;
-  hipLaunchKernelGGL(cnn_fc1_dgrad, dim3((F1IN + 127) / 128, K, (B + 31) / 32), dim3(256), 0, st, dh1, params, P,
+  hipLaunchKernelGGL(cnn_fc1_dgrad, dim3((F1IN + 255) / 256, K, (B + 31) / 32), dim3(256), 0, st, dh1, params, P,
                      off_w1, B, dP2);
   return (int)hipGetLastError();
 }

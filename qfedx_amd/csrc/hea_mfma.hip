@@ -49,7 +49,6 @@ constexpr int F_BACK_PSI = 1;
 constexpr int TMAX = 14;
 constexpr int NT_FWD = 512;    // forward: 8 waves, 64 KB LDS -> 2 workgroups per CU
 constexpr int NT_ADJ = 1024;   // adjoint: 16 waves, 128 KB LDS (psi + lambda) -> 1 workgroup per CU
-constexpr int ADJ_WAVES_13 = 8;   // default waves of a 2^13 adjoint workgroup (QFEDX_HEA_ADJ_WAVES overrides)
 constexpr int CMAX = 8;
 constexpr int MAXOPS = 128;    // ops per pass program (host-checked)
 constexpr int MAXGRAD = 12;    // gradient ops per pass program (host-checked)
@@ -168,16 +167,18 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
   }
 }
 
-// Adjoint image: two planes, psi at word w (swizzled amplitude w, as in the forward image) and lambda at word
-// lam_word<TB>() + w = 2^TB + 4 + w.  An amplitude's psi and lambda differ by a constant byte offset, which every
-// LDS access carries as its instruction offset, so psi and lambda of one amplitude share one address VGPR and land
-// in registers exactly where the MFMA operands want them (an interleaved image read them as b64 pairs and spent a
-// v_mov per dword splitting the pairs).  The 4-word skew keeps the compiler from fusing the two reads into one
-// ds_read2st64_b32 (a register pair, split again by v_movs); a uniform shift leaves every read conflict free.
-// Without a lambda input the lambda plane is zeroed (the observable op writes it).
+// Adjoint LDS image, two layouts (template PL; QFEDX_HEA_PLANES selects):
+//   PL = false, interleaved: word 2w = psi, 2w + 1 = lambda of swizzled amplitude w.  One ds_read_b64 /
+//     ds_write_b64 moves an amplitude's (psi, lambda) pair: half the LDS instructions of two b32 accesses (the
+//     LDS issue rate, not bandwidth, bounds this kernel: PMC WAIT_INST_LDS), at a v_mov per dword splitting the
+//     pairs into MFMA operands.
+//   PL = true, planes: psi at word w, lambda at word lam_word<TB>() + w = 2^TB + 4 + w.  psi and lambda of one
+//     amplitude share one address VGPR (constant instruction offset) and land where the MFMA operands want them;
+//     the 4-word skew keeps the compiler from fusing the pair into a ds_read2st64_b32 (split again by v_movs).
+// Without a lambda input the lambda words are zeroed (the observable op writes them).
 template <int TB>
 __host__ __device__ constexpr uint32_t lam_word() { return (1u << TB) + 4u; }
-template <int NT, int TB = TMAX>
+template <int NT, int TB, bool PL>
 __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* psrc, const uint32_t* lsrc,
                                              uint32_t* tile, int tid, int T, uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
@@ -196,16 +197,42 @@ __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* 
     if (q < (uint32_t)T) {
       const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
       const uint32_t w0 = (q ^ h) & ~3u;
-      *(uint4*)&tile[w0] = quad_perm(v[i], h & 3u);
-      *(uint4*)&tile[lam_word<TB>() + w0] = quad_perm(l[i], h & 3u);
+      const uint4 pv = quad_perm(v[i], h & 3u), lv = quad_perm(l[i], h & 3u);
+      if constexpr (PL) {
+        *(uint4*)&tile[w0] = pv;
+        *(uint4*)&tile[lam_word<TB>() + w0] = lv;
+      } else {
+        *(uint4*)&tile[2 * w0] = make_uint4(pv.x, lv.x, pv.y, lv.y);
+        *(uint4*)&tile[2 * w0 + 4] = make_uint4(pv.z, lv.z, pv.w, lv.w);
+      }
     }
   }
 }
 
-template <int NT, int TB = TMAX>
+template <int NT, int TB, bool PL>
 __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, const uint32_t* tile, int tid, int T,
                                              uint32_t h_q, uint32_t fixed) {
-  store_tile<NT, TB>(a, dst, tile + lam_word<TB>(), tid, T, h_q, fixed);
+  if constexpr (PL) {
+    store_tile<NT, TB>(a, dst, tile + lam_word<TB>(), tid, T, h_q, fixed);
+  } else {
+    constexpr int MQ = (1 << TB) / (4 * NT);
+    uint4 v[MQ];
+#pragma unroll
+    for (int i = 0; i < MQ; ++i) {
+      const uint32_t q = 4u * (tid + NT * i);
+      if (q < (uint32_t)T) {
+        const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+        const uint32_t w0 = 2u * ((q ^ h) & ~3u);
+        const uint4 a0 = *(const uint4*)&tile[w0], a1 = *(const uint4*)&tile[w0 + 4];
+        v[i] = quad_perm(make_uint4(a0.y, a0.w, a1.y, a1.w), h & 3u);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < MQ; ++i) {
+      const uint32_t q = 4u * (tid + NT * i);
+      if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
+    }
+  }
 }
 
 // RZ(ph) RX(th) F(x)|0> for a layer-1 qubit
@@ -256,6 +283,13 @@ __device__ __forceinline__ void lds_st(uint32_t* tile, uint32_t byte, uint32_t v
 }
 
 
+// i * (re, im) = (-im, re) on a packed fp16 pair: dst.lo = src.hi * (-1), dst.hi = src.lo * 1
+__device__ __forceinline__ uint32_t mul_i(uint32_t v) {
+  uint32_t r;
+  __asm__("v_pk_mul_f16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(v), "s"(0x3C00BC00u));
+  return r;
+}
+
 // Y = U X on the op's column blocks for NX targets (tile byte bases tb[x]) sharing the addressing.  Lane
 // (g4, cl) owns column cl of a 16-column block: it reads amplitudes m = 4 g4 .. 4 g4 + 3 (B operand,
 // k = 2m + re/im) and writes rows m' = 2 g4, 2 g4 + 1, 8 + 2 g4, 9 + 2 g4 of the two 16-row output blocks.
@@ -265,12 +299,21 @@ __device__ __forceinline__ void lds_st(uint32_t* tile, uint32_t byte, uint32_t v
 //   IL = false: forward psi image, NX = 1.
 //   IL = true : interleaved adjoint image; NX = 2 applies U to psi and lambda (one b64 read / write per
 //               amplitude pair), NX = 1 to component SEL only (pairs read, single dwords written).
-template <int NX, int NW, bool IL, int SEL, int TB = TMAX>
+//   CROSS (interleaved adjoint image only): also accumulate the op's gradient cross matrix N = sum psi lambda^H
+//               from the SAME registers (the group_cross reads saved): an MFMA against the constant identity
+//               fragments IRE / IIM (exact in fp16) transposes each block's psi and lambda so the column index
+//               lands in registers - lane cl then holds (re, im) of amplitude cl for columns 4 g4 .. 4 g4 + 3, packed
+//               as the K = 32 operand of one MFMA that sums over columns (accR: B = lambda, accI: B = i lambda).
+//               Accumulator layout as group_cross: lane (g4, cl) holds N[4 g4 + i][cl].
+template <int NX, int NW, bool IL, int SEL, int TB = TMAX, bool PL = false, bool CROSS = false>
 __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, const int* opw, uint32_t fo, int lane,
-                                            int wave, int nbw) {
+                                            int wave, int nbw, f4* acc = nullptr, uint4 IRE = {}, uint4 IIM = {}) {
   constexpr int MAXB = (1 << (TB - 8)) / NW;   // column blocks per wave per op (t = 14: 64 blocks)
-  constexpr int SH = 2;
-  constexpr uint32_t LP = 4u * lam_word<TB>();  // lambda plane (adjoint image), bytes
+  constexpr bool PAIR = IL && !PL;             // interleaved adjoint image: (psi, lambda) word pairs
+  static_assert(!CROSS || PAIR, "the fused cross matrix reads the interleaved image");
+  constexpr int NL = CROSS ? 2 : NX;           // registers loaded per block: psi and lambda for the cross
+  constexpr int SH = PAIR ? 3 : 2;
+  constexpr uint32_t LP = 4u * lam_word<TB>();  // lambda plane (planes image), bytes
   static_assert(IL || NX == 1, "the forward image holds psi only");
   const int g4 = lane >> 4, cl = lane & 15;
   uint32_t oin[4], oout[4];
@@ -287,14 +330,36 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
   // plane x of the image: psi (0) or lambda (1); a forward image has psi only
   auto load = [&](uint32_t b, uint4* X) {
     const uint32_t a0 = b ^ oin[0], a1 = b ^ oin[1], a2 = b ^ oin[2], a3 = b ^ oin[3];
+    if constexpr (PAIR) {
+      const uint2 p0 = lds_ld2(tile, a0), p1 = lds_ld2(tile, a1), p2 = lds_ld2(tile, a2), p3 = lds_ld2(tile, a3);
+      if constexpr (NL == 2) {
+        X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
+        X[1] = make_uint4(p0.y, p1.y, p2.y, p3.y);
+      } else if constexpr (SEL == 0) {
+        X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
+      } else {
+        X[0] = make_uint4(p0.y, p1.y, p2.y, p3.y);
+      }
+    } else {
 #pragma unroll
-    for (int x = 0; x < NX; ++x) {
-      const uint32_t pl = (NX == 2 ? x : (IL ? SEL : 0)) ? LP : 0u;
-      X[x] = make_uint4(lds_ld(tile, a0 + pl), lds_ld(tile, a1 + pl), lds_ld(tile, a2 + pl), lds_ld(tile, a3 + pl));
+      for (int x = 0; x < NX; ++x) {
+        const uint32_t pl = (NX == 2 ? x : (IL ? SEL : 0)) ? LP : 0u;
+        X[x] = make_uint4(lds_ld(tile, a0 + pl), lds_ld(tile, a1 + pl), lds_ld(tile, a2 + pl), lds_ld(tile, a3 + pl));
+      }
     }
   };
-  auto compute_store = [&](uint32_t b, const uint4* X) {
+  auto compute_store = [&](uint32_t b, const uint4* XL) {
     const f4 z = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (CROSS) {
+      const f4 pr = mfma(XL[0], IRE, z), pi = mfma(XL[0], IIM, z), lr = mfma(XL[1], IRE, z), li = mfma(XL[1], IIM, z);
+      const uint4 A = make_uint4(pack_h2(pr[0], pi[0]), pack_h2(pr[1], pi[1]), pack_h2(pr[2], pi[2]), pack_h2(pr[3], pi[3]));
+      const uint4 Br = make_uint4(pack_h2(lr[0], li[0]), pack_h2(lr[1], li[1]), pack_h2(lr[2], li[2]), pack_h2(lr[3], li[3]));
+      const uint4 Bi = make_uint4(mul_i(Br.x), mul_i(Br.y), mul_i(Br.z), mul_i(Br.w));
+      acc[0] = mfma(A, Br, acc[0]);
+      acc[1] = mfma(A, Bi, acc[1]);
+    }
+    // the apply targets among the loaded registers: both, or component SEL (psi 0 / lambda 1)
+    const uint4* X = (CROSS && NX == 1) ? XL + SEL : XL;
     f4 d0[NX], d1[NX];
 #pragma unroll
     for (int x = 0; x < NX; ++x) {
@@ -304,24 +369,31 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
       d1[x] = mfma(F[3], X[x], d1[x]);
     }
     const uint32_t s0 = b ^ oout[0], s1 = b ^ oout[1], s2 = b ^ oout[2], s3 = b ^ oout[3];
+    if constexpr (PAIR && NX == 2) {
+      lds_st2(tile, s0, make_uint2(pack_h2(d0[0][0], d0[0][1]), pack_h2(d0[1][0], d0[1][1])));
+      lds_st2(tile, s1, make_uint2(pack_h2(d0[0][2], d0[0][3]), pack_h2(d0[1][2], d0[1][3])));
+      lds_st2(tile, s2, make_uint2(pack_h2(d1[0][0], d1[0][1]), pack_h2(d1[1][0], d1[1][1])));
+      lds_st2(tile, s3, make_uint2(pack_h2(d1[0][2], d1[0][3]), pack_h2(d1[1][2], d1[1][3])));
+    } else {
 #pragma unroll
-    for (int x = 0; x < NX; ++x) {
-      const uint32_t pl = (NX == 2 ? x : (IL ? SEL : 0)) ? LP : 0u;
-      lds_st(tile, s0 + pl, pack_h2(d0[x][0], d0[x][1]));
-      lds_st(tile, s1 + pl, pack_h2(d0[x][2], d0[x][3]));
-      lds_st(tile, s2 + pl, pack_h2(d1[x][0], d1[x][1]));
-      lds_st(tile, s3 + pl, pack_h2(d1[x][2], d1[x][3]));
+      for (int x = 0; x < NX; ++x) {
+        const uint32_t pl = PAIR ? 4u * SEL : ((NX == 2 ? x : (IL ? SEL : 0)) ? LP : 0u);
+        lds_st(tile, (s0 ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d0[x][0], d0[x][1]));
+        lds_st(tile, (s1 ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d0[x][2], d0[x][3]));
+        lds_st(tile, (s2 ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d1[x][0], d1[x][1]));
+        lds_st(tile, (s3 ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d1[x][2], d1[x][3]));
+      }
     }
   };
   if (nbw <= 0) return;
-  uint4 B0[NX], B1[NX];
+  uint4 B0[NL], B1[NL];
   load(base[0], B0);
   if (nbw > 1) load(base[1], B1);
-  constexpr bool PREFETCH = true;
+  constexpr bool PREFETCH = !CROSS;             // the fused cross needs the registers of the prefetched pair
 #pragma unroll
   for (int p = 0; p < MAXB; p += 2) {
     if (p >= nbw) break;
-    uint4 C0[NX], C1[NX];
+    uint4 C0[NL], C1[NL];
     if (PREFETCH && p + 2 < MAXB && p + 2 < nbw) {
       load(base[p + 2 < MAXB ? p + 2 : 0], C0);
       if (p + 3 < nbw) load(base[p + 3 < MAXB ? p + 3 : 0], C1);
@@ -330,7 +402,7 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
     if (p + 1 < nbw) compute_store(base[p + 1 < MAXB ? p + 1 : 0], B1);
     if (PREFETCH) {
 #pragma unroll
-      for (int x = 0; x < NX; ++x) {
+      for (int x = 0; x < NL; ++x) {
         B0[x] = C0[x];
         B1[x] = C1[x];
       }
@@ -341,36 +413,36 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
   }
 }
 
-// i * (re, im) = (-im, re) on a packed fp16 pair: dst.lo = src.hi * (-1), dst.hi = src.lo * 1
-__device__ __forceinline__ uint32_t mul_i(uint32_t v) {
-  uint32_t r;
-  __asm__("v_pk_mul_f16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(v), "s"(0x3C00BC00u));
-  return r;
-}
-
 // Gradient cross matrix N[b][a] += sum_col psi[b][col] conj(lam[a][col]) over the op's column blocks:
 // K = 16 columns x (re, im), lane (g4, cl) reads amplitude m = cl of columns 4 g4 .. 4 g4 + 3; accR / accI
 // end up holding N[4 g4 + i][cl] (real / imaginary).
-template <int NW, int TB = TMAX>
+template <int NW, int TB = TMAX, bool PL = false>
 __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw, uint32_t fo, int lane, int wave,
                                             int nbw, f4& accR, f4& accI) {
   constexpr int MAXB = (1 << (TB - 8)) / NW;
   const int g4 = lane >> 4, cl = lane & 15;
   constexpr uint32_t LP = 4u * lam_word<TB>();
+  constexpr int SH = PL ? 2 : 3;
   const uint32_t om = (uint32_t)opw[W_OFF + cl] ^ fo;
   uint32_t gb[4];
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) gb[jj] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + jj] ^ om) << 2;
+  for (int jj = 0; jj < 4; ++jj) gb[jj] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + jj] ^ om) << SH;
 #pragma unroll
   for (int i = 0; i < MAXB; ++i) {
     if (i >= nbw) break;
-    const uint32_t bh = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << 2;
+    const uint32_t bh = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << SH;
     uint32_t pv[4], lv[4];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {            // psi and lambda of one amplitude: one address, two planes
+    for (int jj = 0; jj < 4; ++jj) {            // psi and lambda of one amplitude: one b64 pair or two planes
       const uint32_t ad = gb[jj] ^ bh;
-      pv[jj] = lds_ld(tile, ad);
-      lv[jj] = lds_ld(tile, ad + LP);
+      if constexpr (PL) {
+        pv[jj] = lds_ld(tile, ad);
+        lv[jj] = lds_ld(tile, ad + LP);
+      } else {
+        const uint2 v = lds_ld2(tile, ad);
+        pv[jj] = v.x;
+        lv[jj] = v.y;
+      }
     }
     const uint4 A = make_uint4(pv[0], pv[1], pv[2], pv[3]);
     const uint4 Br = make_uint4(lv[0], lv[1], lv[2], lv[3]);
@@ -505,7 +577,7 @@ __device__ __forceinline__ void readout_op(const uint32_t* psi_t, const PassArgs
 }
 
 // Adjoint seed lambda = sum_c r_c Z_c psi on the adjoint image (psi plane word w, lambda plane word 2^TB + w).
-template <int NC, int NT, int TB = TMAX>
+template <int NC, int NT, int TB = TMAX, bool PL = false>
 __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, int T, uint32_t fixed,
                                        const float* rsc_s) {
   constexpr int QI = (1 << TB) / NT;
@@ -520,7 +592,7 @@ __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, 
     if (i0 >= iters) break;
     uint32_t v[CH];
 #pragma unroll
-    for (int j = 0; j < CH; ++j) v[j] = tile[(tid + NT * (i0 + j)) & (T - 1)];   // in bounds; writes masked
+    for (int j = 0; j < CH; ++j) v[j] = tile[(PL ? 1 : 2) * ((tid + NT * (i0 + j)) & (T - 1))];   // in bounds
     float rr[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) rr[c] = cs.flip(c, i0 / CH) ? -r[c] : r[c];
@@ -531,7 +603,7 @@ __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, 
       for (int c = 0; c < NC; ++c) fsum += cs.mul(rr[c], j, c);
       const float2 f = unpack_h2(v[j]);
       const int w = tid + NT * (i0 + j);
-      if (i0 + j < iters && w < T) tile[lam_word<TB>() + w] = pack_h2(fsum * f.x, fsum * f.y);
+      if (i0 + j < iters && w < T) tile[PL ? lam_word<TB>() + w : 2 * w + 1] = pack_h2(fsum * f.x, fsum * f.y);
     }
   }
 }
@@ -762,12 +834,12 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
 // round trip and was slower (16q adjoint 0.67 -> 0.72 ms).
 // WV = waves per workgroup: 2^(TB - 10) gives 4 column blocks per wave per op (the round-2 layout); fewer waves
 // give each wave more blocks per op, amortising the per-op setup / epilogue over more MFMAs.
-template <int NCK, int TB, int WV, bool FULL>
+template <int NCK, int TB, int WV, bool FULL, bool PL, bool FUSE>
 __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(PassArgs a) {
   constexpr int NT = 64 * WV, NW = WV;
   static_assert(NW % 2 == 0 && (1 << (TB - 8)) % NW == 0, "column blocks per wave must be whole, block pairs aligned");
   // (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
-  __shared__ __attribute__((aligned(16))) uint32_t tile[lam_word<TB>() + (1 << TB)];
+  __shared__ __attribute__((aligned(16))) uint32_t tile[PL ? lam_word<TB>() + (1 << TB) : (2 << TB)];
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
   __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
   __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (op_fo_global)
@@ -802,7 +874,7 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
   if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
   if (!(QFX_HEA_ABLATE && (a.ablate & 32)))
-    load_tile_il<NT, TB>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
+    load_tile_il<NT, TB, PL>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
                          h_q, fixed);
   if (tid == 0) {
     float rho = 0.f;
@@ -839,6 +911,18 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   };
 
   // ---------------------------------------------------------------- op list
+  // identity fragments (rows: re of amplitude n, then im) for the fused cross-matrix transposes (FUSE)
+  uint4 IRE = {}, IIM = {};
+  if constexpr (FUSE) {
+    const int n = lane & 15, g4 = lane >> 4;
+    uint32_t* re = (uint32_t*)&IRE;
+    uint32_t* im = (uint32_t*)&IIM;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      re[j] = n == 4 * g4 + j ? 0x00003C00u : 0u;
+      im[j] = n == 4 * g4 + j ? 0x3C000000u : 0u;
+    }
+  }
   const int ncol = T >> 4, nblk = ncol >> 4;
   // FULL (t == TB): every wave owns exactly (2^(TB - 8)) / NW column blocks - a compile-time count, so the block
   // loops of the group ops carry no bounds checks or branches
@@ -888,22 +972,31 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
     }
 #endif
     if (code == OP_OBS) {
-      obs_op<NCK, NT, TB>(tile, opw, tid, T, fixed, rsc);
+      obs_op<NCK, NT, TB, PL>(tile, opw, tid, T, fixed, rsc);
     } else if (code == OP_UNAPPLY_PSI || code == OP_APPLY) {
       // U^H (or, re-applying a recomputed last pass, U) on the psi plane
-      group_apply<1, NW, true, 0, TB>(tile, F, opw, fo_s[o], lane, wave, nbw);
+      group_apply<1, NW, true, 0, TB, PL>(tile, F, opw, fo_s[o], lane, wave, nbw);
     } else if (code == OP_UNAPPLY_LAM) {
-      group_apply<1, NW, true, 1, TB>(tile, F, opw, fo_s[o], lane, wave, nbw);
+      group_apply<1, NW, true, 1, TB, PL>(tile, F, opw, fo_s[o], lane, wave, nbw);
     } else if (code == OP_BACK || code == OP_GRAD || code == OP_GRAD_L1) {
       const uint32_t fo = fo_s[o];
-      f4 accR = {0.f, 0.f, 0.f, 0.f}, accI = {0.f, 0.f, 0.f, 0.f};
-      if (!(QFX_HEA_ABLATE && (a.ablate & 4))) group_cross<NW, TB>(tile, opw, fo, lane, wave, nbw, accR, accI);
-      if (code == OP_BACK && !(QFX_HEA_ABLATE && (a.ablate & 8))) {
+      f4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      if (FUSE && code == OP_BACK) {
+        // cross matrix from the apply's own registers (one pass over the blocks, no group_cross reads)
         if (opw[W_FLAGS] & F_BACK_PSI)
-          group_apply<2, NW, true, 0, TB>(tile, F, opw, fo, lane, wave, nbw);
+          group_apply<2, NW, true, 0, TB, PL, FUSE>(tile, F, opw, fo, lane, wave, nbw, acc2, IRE, IIM);
         else
-          group_apply<1, NW, true, 1, TB>(tile, F, opw, fo, lane, wave, nbw);
+          group_apply<1, NW, true, 1, TB, PL, FUSE>(tile, F, opw, fo, lane, wave, nbw, acc2, IRE, IIM);
+      } else {
+        if (!(QFX_HEA_ABLATE && (a.ablate & 4))) group_cross<NW, TB, PL>(tile, opw, fo, lane, wave, nbw, acc2[0], acc2[1]);
+        if (code == OP_BACK && !(QFX_HEA_ABLATE && (a.ablate & 8))) {
+          if (opw[W_FLAGS] & F_BACK_PSI)
+            group_apply<2, NW, true, 0, TB, PL>(tile, F, opw, fo, lane, wave, nbw);
+          else
+            group_apply<1, NW, true, 1, TB, PL>(tile, F, opw, fo, lane, wave, nbw);
+        }
       }
+      const f4 accR = acc2[0], accI = acc2[1];
       // Cross-wave sum of the partial-trace entries of N / rho into the op's region: packed biased fixed point
       // (PK_*), one u64 LDS atomic per entry.  Integer addition is associative, so the sums are bitwise
       // independent of the order the waves (and, in hea_grad_reduce, samples and tiles) arrive.
@@ -917,7 +1010,9 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
         if (QFX_HEA_ABLATE && (a.ablate & 2)) break;
         if (__builtin_popcount(d) <= 1) {
           const int e = d == 0 ? (int)bb : 16 + 16 * (__builtin_ctz(d)) + (int)bb;
-          const uint32_t lo = (uint32_t)(int)(accR[i] * sc) + PK_BIAS, hi = (uint32_t)(int)(accI[i] * sc) + PK_BIAS;
+          // round to nearest: truncation would bias every add toward zero, and a tile's sum has thousands
+          const uint32_t lo = (uint32_t)(int)__builtin_rintf(accR[i] * sc) + PK_BIAS,
+                         hi = (uint32_t)(int)__builtin_rintf(accI[i] * sc) + PK_BIAS;
           atomicAdd(&rg[red_slot(e)], ((unsigned long long)hi << 32) | lo);
         }
       }
@@ -936,7 +1031,7 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   } else {
     for (int e = tid; e < ngrad * 32; e += NT) reduce_region(e >> 5, e & 31);
   }
-  if (a.store_lam) store_lam_il<NT, TB>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
+  if (a.store_lam) store_lam_il<NT, TB, PL>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
   HEA_MARK();
 }
 #undef HEA_MARK
@@ -1049,15 +1144,15 @@ extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_sample
   if (a.t > hea::TMAX || a.t < 8 || a.C > hea::CMAX || a.n > 30 || a.c < 2) return -2;
   const unsigned grid = (unsigned)(n_samples * a.n_tiles);
   if (grid == 0) return 0;
-  static int adj_waves = 0;   // waves per 2^13 adjoint workgroup (QFEDX_HEA_ADJ_WAVES = 4 | 8)
-  if (!adj_waves) {
-    const char* e = getenv("QFEDX_HEA_ADJ_WAVES");
-    adj_waves = (e && atoi(e) == 8) ? 8 : (e && atoi(e) == 4 ? 4 : hea::ADJ_WAVES_13);
+  static int planes = -1;   // adjoint LDS image: 0 interleaved (psi, lambda) pairs, 1 planes (QFEDX_HEA_PLANES)
+  if (planes < 0) {
+    const char* e = getenv("QFEDX_HEA_PLANES");
+    planes = e ? (atoi(e) != 0) : 0;
   }
-  static int adj_full = -1;   // compile-time block count for full 2^13 adjoint tiles (QFEDX_HEA_ADJ_FULL = 0 | 1)
-  if (adj_full < 0) {
-    const char* e = getenv("QFEDX_HEA_ADJ_FULL");
-    adj_full = e ? (atoi(e) != 0) : 0;
+  static int fuse = -1;     // BACK ops: cross matrix from the apply's registers (QFEDX_HEA_FUSE, default on)
+  if (fuse < 0) {
+    const char* e = getenv("QFEDX_HEA_FUSE");
+    fuse = e ? (atoi(e) != 0) : 1;
   }
 #define HEA_LAUNCH(NCK)                                                                                     \
   do {                                                                                                     \
@@ -1065,14 +1160,16 @@ extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_sample
       hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK, true>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);       \
     else if (!adjoint)                                                                                     \
       hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK, false>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);      \
-    else if (a.t <= 13 && adj_waves == 4)                                                                  \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 4, false>), dim3(grid), dim3(256), 0, st, a);       \
-    else if (a.t == 13 && adj_full)                                                                        \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, true>), dim3(grid), dim3(512), 0, st, a);        \
+    else if (a.t <= 13 && planes)                                                                          \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, false, true, false>), dim3(grid), dim3(512), 0, st, a); \
+    else if (a.t <= 13 && fuse)                                                                            \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, false, false, true>), dim3(grid), dim3(512), 0, st, a); \
     else if (a.t <= 13)                                                                                    \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, false>), dim3(grid), dim3(512), 0, st, a);       \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, false, false, false>), dim3(grid), dim3(512), 0, st, a); \
+    else if (fuse)                                                                                         \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14, 16, true, false, true>), dim3(grid), dim3(1024), 0, st, a); \
     else                                                                                                   \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14, 16, true>), dim3(grid), dim3(1024), 0, st, a);      \
+      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14, 16, true, false, false>), dim3(grid), dim3(1024), 0, st, a); \
   } while (0)
   switch (hea::class_kernel(a.C)) {
     case 1: HEA_LAUNCH(1); break;

@@ -96,10 +96,11 @@ class HeaMfmaProgram:
         applies = [j for j, (_, fwd, _) in enumerate(progs_f) if any(int(w[W_CODE]) == OP_APPLY for w in fwd)]
         self.fwd_last = applies[-1] if applies else 0
         J = len(progs_f)
-        # The adjoint of the last pass re-applies that pass's groups in-tile from its stored INPUT, so the
-        # forward's last pass only reads out (QFEDX_HEA_RECOMPUTE=0: store its output instead).  Needs a stored
-        # input (J >= 2) and a last pass that applies groups.
-        self.recompute = (J >= 2 and self.fwd_last == J - 1 and os.environ.get("QFEDX_HEA_RECOMPUTE", "1") != "0")
+        # QFEDX_HEA_RECOMPUTE=1: the adjoint of the last pass re-applies that pass's groups in-tile from its stored
+        # INPUT, so the forward's last pass only reads out.  Needs a stored input (J >= 2) and a last pass that
+        # applies groups.  Opt-in: at 16q the saved state write did not shorten the forward pass, and the
+        # re-applied groups lengthened the adjoint one.
+        self.recompute = (J >= 2 and self.fwd_last == J - 1 and os.environ.get("QFEDX_HEA_RECOMPUTE", "0") == "1")
         progs_a = pass_programs(plan_a, gmeta, recompute_last=self.recompute)
         self.n_gradops = len(gmeta)
         if self.fwd_last < J - 1:
