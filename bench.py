@@ -46,7 +46,7 @@ def timed_rounds(cfg, device, backend, world, warmup: int, steps: int, counts: l
     for r in range(warmup):
         runner.run_round(r, sync=False)
     sync()
-    runner.timer.reset()                    # per-phase HIP-event times of the timed rounds only
+    runner.timer.enabled = False            # no phase events inside the timed rounds (phase_ms calibrates after)
     t0 = time.perf_counter()
     for r in range(warmup, warmup + steps):
         rec = runner.run_round(r, sync=False)
@@ -57,13 +57,22 @@ def timed_rounds(cfg, device, backend, world, warmup: int, steps: int, counts: l
     return runner, max_over_ranks(dt, world)
 
 
-def phase_ms(runner, world, steps: int) -> dict:
-    """Per-round milliseconds of the runner's phases over the timed rounds (HIP events; max over ranks):
-    ``local_train_ms`` = the round graph (every local step + the fused FedAvg reduce), ``comm_ms`` = the
-    all-reduce + finalize/apply."""
-    from qfedx_amd.parallel.dist import max_over_ranks
-    tot = runner.timer.resolve()
-    return {f"{k}_ms": round(max_over_ranks(v / max(steps, 1), world), 4) for k, v in sorted(tot.items())}
+def phase_ms(runner, world, steps: int, calib: int = 5) -> dict:
+    """Per-round milliseconds of the runner's phases (HIP events; max over ranks), from ``calib`` untimed rounds run
+    after the timed ones (the timed rounds record no events: each one idles the GPU between graph launches):
+    ``local_train_ms`` = the round graph (every local step + the fused FedAvg reduce, and the collective + apply when
+    they are captured with it), ``comm_ms`` = whatever of the all-reduce + finalize/apply runs outside the graph."""
+    import torch
+    from qfedx_amd.parallel.dist import barrier, max_over_ranks
+    tm = runner.timer
+    tm.reset()
+    tm.enabled, tm.every = True, 1
+    for r in range(10_000, 10_000 + calib):
+        runner.run_round(r, sync=False)
+    barrier(world)
+    if runner.device.type == "cuda":
+        torch.cuda.synchronize()
+    return {f"{k}_ms": round(max_over_ranks(v, world), 4) for k, v in sorted(tm.per_phase().items())}
 
 
 def precision_check(runner, batch: int) -> dict:

@@ -119,6 +119,7 @@ class RuntimeConfig:
     overlap_comm: bool = True
     use_graphs: bool = True            # hipGraph capture of the local round (HIP backend)
     graph_comm: bool = True            # capture the round's all-reduce + apply into that graph (RCCL / no group)
+    timer_every: int = 0               # time the GPU phases every N-th round (0: 16 on GPU, every round on CPU)
     log_client_norms: bool = True      # DP rounds: every client's pre-clip update norm reaches every rank in the
                                        # round all-reduce (CC6); clip fraction + norm quantiles per round (not
                                        # under SecAgg, where per-client statistics would leak)

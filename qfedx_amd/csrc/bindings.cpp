@@ -73,6 +73,7 @@ int qfx_launch_adam(float* p, const float* g, float* m, float* v, const float* t
 int qfx_launch_sgdm(float* p, const float* g, float* buf, const float* t_in, float* t_out, const float* active,
                     int K, int P, float lr, float mu, int keep, hipStream_t st);
 int qfx_launch_host_upload(const void* host_src, void* dst, long nbytes, hipStream_t st);
+int qfx_launch_round_signal(long long* ctr, long long* host_flag, hipStream_t st);
 int qfx_launch_round_init(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
                           hipStream_t st);
 int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
@@ -289,10 +290,13 @@ void sgdm(torch::Tensor p, torch::Tensor g, torch::Tensor buf, torch::Tensor t_i
 // params[k, :] = theta; optional m, v (same shape) and t (any length) zeroed
 // Pinned host staging memory allocated mapped + portable (device-readable from every GPU of the process, whatever
 // the current device was at allocation), as a CPU uint8 tensor that frees itself with hipHostFree.
-torch::Tensor host_alloc(int64_t nbytes) {
+// ``coherent``: fine-grained (device writes are visible to the host without a kernel-boundary flush; the round
+// signal word).
+torch::Tensor host_alloc(int64_t nbytes, bool coherent) {
   if (nbytes <= 0) throw std::invalid_argument("host_alloc: size");
   void* p = nullptr;
-  if (hipHostMalloc(&p, (size_t)nbytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess || !p)
+  const unsigned flags = hipHostMallocMapped | hipHostMallocPortable | (coherent ? hipHostMallocCoherent : 0u);
+  if (hipHostMalloc(&p, (size_t)nbytes, flags) != hipSuccess || !p)
     throw std::runtime_error("host_alloc: hipHostMalloc failed");
   return torch::from_blob(p, {nbytes}, [](void* q) { (void)hipHostFree(q); },
                           torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCPU));
@@ -308,6 +312,14 @@ void host_upload(torch::Tensor src, torch::Tensor dst) {
   const int64_t n = src.numel();
   if (dst.numel() < n || n % 16) throw std::invalid_argument("host_upload: size (16-byte multiple, dst >= src)");
   check(qfx_launch_host_upload(src.data_ptr(), dst.data_ptr(), (long)n, cur_stream()), "qfx_host_upload");
+}
+
+// ctr: device int64 [1] (the graph entry's round counter); flag: coherent host_alloc memory holding one int64
+void round_signal(torch::Tensor ctr, torch::Tensor flag) {
+  need(ctr, torch::kInt64, "ctr");
+  if (flag.device().is_cuda() || flag.numel() < 8 || flag.scalar_type() != torch::kUInt8)
+    throw std::invalid_argument("round_signal: flag must be >= 8 bytes of host_alloc memory");
+  check(qfx_launch_round_signal(ptr<long long>(ctr), (long long*)flag.data_ptr(), cur_stream()), "qfx_round_signal");
 }
 
 void round_init(torch::Tensor theta, torch::Tensor params, c10::optional<torch::Tensor> m,
@@ -545,7 +557,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("readout_sum", &readout_sum);
   m.def("amp_init", &amp_init);
   m.def("round_init", &round_init);
-  m.def("host_alloc", &host_alloc);
+  m.def("host_alloc", &host_alloc, py::arg("nbytes"), py::arg("coherent") = false);
+  m.def("round_signal", &round_signal);
   m.def("host_upload", &host_upload);
   m.def("batch_plan", &qfx_runtime::batch_plan);
   m.def("batch_gather", &batch_gather);

@@ -578,9 +578,26 @@ __global__ void qfx_round_apply_kernel(long long* __restrict__ buf, int P, float
   }
 }
 
+// Round-completion signal, the last node of a captured round: bumps the graph entry's device counter and
+// publishes it to a coherent pinned host word (system-scope release store).  The host reuses a pinned upload
+// buffer once the counter shows the round that read it has finished - no HIP event per round (an event record
+// between two graph launches cost ~5 us of GPU idle each on this stack; scripts/graph_gap.py).
+__global__ void qfx_round_signal_kernel(long long* __restrict__ ctr, long long* host_flag) {
+  if (threadIdx.x == 0) {
+    const long long c = ctr[0] + 1;
+    ctr[0] = c;
+    __hip_atomic_store(host_flag, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace qfx
 
 using namespace qfx;
+
+extern "C" int qfx_launch_round_signal(long long* ctr, long long* host_flag, hipStream_t st) {
+  hipLaunchKernelGGL(qfx_round_signal_kernel, dim3(1), dim3(64), 0, st, ctr, host_flag);
+  return (int)hipGetLastError();
+}
 
 extern "C" int qfx_fedavg_norm_scratch(int K, int P) { return K * (1 + (P + NORM_CHUNK - 1) / NORM_CHUNK); }
 

@@ -105,7 +105,8 @@ class FederatedRunner:
         self.y_test = yt[sl[0]: sl[-1] + 1].to(device) if sl else yt[:0].to(device)
         self.metrics = MetricsWriter(cfg.runtime.metrics_path, world.rank, cfg.to_dict(), cfg.runtime.tracking_dir,
                                      cfg.runtime.experiment or cfg.name)
-        self.timer = PhaseTimer(device)
+        self.timer = PhaseTimer(device, every=int(getattr(cfg.runtime, "timer_every", 0) or
+                                                  (16 if torch.device(device).type == "cuda" else 1)))
         self.start_round = 0
         self.history: list[dict] = []
         self.server_opt = None
@@ -197,6 +198,7 @@ class FederatedRunner:
         record holds device tensors until :meth:`resolve_record`."""
         t = self.cfg.train
         p = self.cfg.privacy
+        self.timer.step(r)
         # under DP the participant set is part of the mechanism: keyed by the secret like the noise
         participants = sample_participants(self.num_clients, t.client_fraction,
                                            self.noise_seed if p.dp else t.seed, r, self.poisson)

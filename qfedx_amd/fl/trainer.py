@@ -11,6 +11,8 @@ fixes the step count for every client (benchmarks).
 """
 from __future__ import annotations
 
+import time
+
 import math
 
 import numpy as np
@@ -27,6 +29,26 @@ from .optim import BatchedOptimizer
 UPFRONT_GATHER_BYTES = 1 << 28
 _GRAPH_LRU = 6
 
+
+
+def _wait_rounds(ent: dict, n: int) -> None:
+    """Block until graph entry ``ent`` has completed ``n`` replays (its last node publishes the count to a coherent
+    pinned word): spins briefly, then yields; the GPU is normally far ahead of this."""
+    if n <= 0:
+        return
+    flag = ent["flag"].view(torch.int64)
+    spins, t0 = 0, None
+    while int(flag[0]) < n:
+        spins += 1
+        if spins > 64:
+            time.sleep(20e-6)
+            if t0 is None:
+                t0 = time.perf_counter()
+            elif time.perf_counter() - t0 > 5.0:     # never expected: drain the GPU, then the word must be there
+                torch.cuda.synchronize()
+                if int(flag[0]) < n:
+                    raise RuntimeError(f"round signal stuck at {int(flag[0])} < {n}: device writes to the coherent "
+                                       "pinned word are not visible to the host")
 
 class ShardStore:
     """Device-resident padded shards: X [K, Nmax, F], y [K, Nmax], counts [K]."""
@@ -369,7 +391,11 @@ class VQCClientTrainer:
             pack = torch.empty(up.nbytes, dtype=torch.uint8, device=dev)
             dv = up.to_device(dev, pack)
             ent = {"pack": pack, "dv": dv, "theta": theta_g if direct else theta_g.to(dev).float().clone(),
-                   "pin": [E.host_alloc(up.nbytes), E.host_alloc(up.nbytes)], "events": [None, None], "flip": 0}
+                   "pin": [E.host_alloc(up.nbytes), E.host_alloc(up.nbytes)], "flip": 0,
+                   # round-completion counter: device word + coherent host mirror written by the graph's last node
+                   "ctr": torch.zeros(1, dtype=torch.int64, device=dev), "flag": E.host_alloc(8, True),
+                   "launched": 0}
+            ent["flag"].zero_()
             args = (store.X, store.y, dv["lid"], ent["theta"], dv["idx"], dv["wts"], dv["act"], plan.max_steps,
                     round_num, "adjoint")
 
@@ -398,6 +424,7 @@ class VQCClientTrainer:
                             out = body()
                             if ent["post_in_graph"]:
                                 post(v)
+                            E.round_signal(ent["ctr"], ent["flag"])
                     except Exception:
                         if not ent["post_in_graph"]:
                             raise
@@ -411,6 +438,7 @@ class VQCClientTrainer:
                             with torch.cuda.graph(g):
                                 E.host_upload(ent["pin"][v2][: up.nbytes], pack)
                                 out = body()
+                                E.round_signal(ent["ctr"], ent["flag"])
                             ent["graphs"].append(g)
                             ent["out"].append(out)
                         break
@@ -418,21 +446,17 @@ class VQCClientTrainer:
                     ent["out"].append(out)
             while len(cache) >= _GRAPH_LRU:         # LRU: drop the oldest shape
                 old = cache.pop(next(iter(cache)))
-                for ev in old["events"]:
-                    if ev is not None:
-                        ev.synchronize()
+                _wait_rounds(old, old["launched"])   # its replays are done with their pinned buffers
         cache[key] = ent                            # most recently used last
         if not direct:
             ent["theta"].copy_(theta_g.float())
         v = ent["flip"]
         ent["flip"] ^= 1
-        if ent["events"][v] is not None:
-            ent["events"][v].synchronize()          # pinned buffer v: its last reader (round r - 2) is done
+        n = ent["launched"]
+        _wait_rounds(ent, n - 1)                    # pinned buffer v: its last reader (replay n - 2) is done
         up._fill(ent["pin"][v][: up.nbytes])
         ent["graphs"][v].replay()
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        ent["events"][v] = ev
+        ent["launched"] = n + 1
         if post is not None and not ent["post_in_graph"]:
             post(v)
         return (*ent["out"][v], ent["dv"], v if post is not None else None)

@@ -20,17 +20,29 @@ class PhaseTimer:
     # a blocking drain only if the GPU is a further MAX_PENDING phases behind)
     MAX_PENDING = 256
 
-    def __init__(self, device: torch.device | str = "cpu", enabled: bool = True):
+    def __init__(self, device: torch.device | str = "cpu", enabled: bool = True, every: int = 1):
         self.device = torch.device(device)
         self.enabled = enabled
+        # GPU phases are timed on every ``every``-th round only (``step``): each HIP event recorded between two
+        # round-graph launches idles the GPU for ~5 us on this stack (scripts/graph_gap.py)
+        self.every = max(1, int(every))
+        self.active = True
         self.gpu = self.device.type == "cuda"
         self._pending: list[tuple[str, object, object]] = []
         self.totals: dict[str, float] = defaultdict(float)
         self.counts: dict[str, int] = defaultdict(int)
 
+    def step(self, round_num: int) -> None:
+        self.active = round_num % self.every == 0
+
+    def per_phase(self) -> dict[str, float]:
+        """Mean milliseconds per timed occurrence of each phase (syncs once on GPU)."""
+        tot = self.resolve()
+        return {k: v / max(self.counts[k], 1) for k, v in tot.items()}
+
     @contextlib.contextmanager
     def phase(self, name: str):
-        if not self.enabled:
+        if not (self.enabled and self.active):
             yield
             return
         with torch.profiler.record_function(f"qfedx::{name}"):
