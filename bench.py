@@ -52,6 +52,7 @@ def timed_rounds(cfg, device, backend, world, warmup: int, steps: int, counts: l
         rec = runner.run_round(r, sync=False)
         if counts is not None:
             counts.append(rec["participants"] - rec["dropped"])
+    runner.host_ms = 1e3 * (time.perf_counter() - t0) / max(steps, 1)   # host time to enqueue a round
     sync()
     dt = time.perf_counter() - t0
     return runner, max_over_ranks(dt, world)
@@ -216,6 +217,7 @@ def main():
             "backend": backend,
             "test_acc_after": round(ev["test_acc"], 4),
             "dist_backend": world.backend,
+            "host_ms_per_round": round(getattr(runner, "host_ms", 0.0), 4),   # enqueue time (GPU runs behind)
             **phases,
             **prec,
             "config": {
