@@ -28,5 +28,6 @@ struct HeaPassArgs {
   int hrow[5];               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
   long long* dbg;            // optional phase timestamps (s_memtime) of workgroups < 8, [8][64]
   int in_rep;                // forward: shifted parameter rows per stored input sample (param-shift prefix reuse)
+  int pair;                  // forward: two samples per workgroup on 2^13 tiles (hea_fwd2_kernel)
   int ablate;                // timing ablations (builds with QFX_HEA_ABLATE only; QFEDX_HEA_ABLATE bit mask)
 };

@@ -51,12 +51,12 @@ void check(int rc, const char* what) {
 }
 
 // geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
-//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep]
+//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, pair]
 void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<int64_t> geom, double scale, torch::Tensor psi_in,
               torch::Tensor psi_out, torch::Tensor lam_in, torch::Tensor lam_out, torch::Tensor xang,
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
               torch::Tensor gslab, torch::Tensor dbg) {
-  need(geom.size() == 27, "geometry vector must have 27 entries");
+  need(geom.size() == 28, "geometry vector must have 28 entries");
   HeaPassArgs a{};
   a.n = (int)geom[0];
   a.t = (int)geom[1];
@@ -88,6 +88,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   }
   a.n_gradops = (int)geom[25];
   a.in_rep = (int)geom[26];
+  a.pair = (int)geom[27];
   a.scale = (float)scale;
   a.dbg = dbg.defined() && dbg.numel() >= 8 * 64 ? dp<long long>(dbg, torch::kInt64, "dbg", 8 * 64) : nullptr;
   for (int b = 0; b < 5; ++b) {
@@ -109,6 +110,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.fidx = a.nops ? dp<int>(fidx, torch::kInt32, "fidx", a.nops) : nullptr;
   need(a.in_rep >= 1 && (!adjoint || a.in_rep == 1) && K % a.in_rep == 0,
        "in_rep: forward only, parameter rows a multiple of it");
+  need(!a.pair || (!adjoint && a.t == 13 && a.spc % 2 == 0), "paired forward: forward passes on 2^13 tiles, even spc");
   const int64_t states = S << a.n;
   a.psi_in = a.gen ? nullptr : dp<uint32_t>(psi_in, torch::kInt32, "psi_in", states / a.in_rep);
   need(!(adjoint && a.store_psi), "adjoint passes store lambda only");

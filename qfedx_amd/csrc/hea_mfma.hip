@@ -576,6 +576,89 @@ __device__ __forceinline__ void readout_op(const uint32_t* psi_t, const PassArgs
   }
 }
 
+// <Z_c> partial sums of a PAIRED forward tile (two samples of one client interleaved: word 2w = sample A,
+// 2w + 1 = sample B of swizzled amplitude w; one b64 read per amplitude pair), written for both samples.
+template <int NC, int NT, int TB>
+__device__ __forceinline__ void readout_pair_op(const uint32_t* tile, const PassArgs& a, const int* opw, int tid,
+                                                int lane, int wave, int T, uint32_t fixed, float* red, size_t pidxA,
+                                                size_t pidxB) {
+  constexpr int QI = (1 << TB) / NT, NW = NT / 64;
+  constexpr int CH = QI < RCH ? QI : RCH;
+  const int iters = T >= NT ? T / NT : 1;
+  const ClassSigns<NC, CH> cs = class_signs<NC, NT, CH, TB>(opw, tid, fixed, iters);
+  float acc[2][NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[0][c] = acc[1][c] = 0.f;
+#pragma unroll 1
+  for (int i0 = 0; i0 < QI; i0 += CH) {
+    if (i0 >= iters) break;
+    uint2 v[CH];
+#pragma unroll
+    for (int j = 0; j < CH; ++j) v[j] = *(const uint2*)&tile[2 * ((tid + NT * (i0 + j)) & (T - 1))];
+    float sum[2][NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) sum[0][c] = sum[1][c] = 0.f;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const float2 fa = unpack_h2(v[j].x), fb = unpack_h2(v[j].y);
+      const float pa = fa.x * fa.x + fa.y * fa.y, pb = fb.x * fb.x + fb.y * fb.y;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        sum[0][c] += cs.mul(pa, j, c);
+        sum[1][c] += cs.mul(pb, j, c);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const bool f = cs.flip(c, i0 / CH);
+      acc[0][c] += f ? -sum[0][c] : sum[0][c];
+      acc[1][c] += f ? -sum[1][c] : sum[1][c];
+    }
+  }
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      float v = tid < T ? acc[x][c] : 0.f;
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0) red[(x * NW + wave) * CMAX + c] = v;
+    }
+  lds_barrier();
+  if (tid < 2 * a.C) {
+    const int x = tid / a.C, c = tid - x * a.C;
+    float v = 0.f;
+    for (int w = 0; w < NW; ++w) v += red[(x * NW + w) * CMAX + c];
+    a.part[(x ? pidxB : pidxA) + c] = v / (a.scale * a.scale);
+  }
+}
+
+// Paired image store: sample A (even words) and sample B (odd words) of every amplitude to their states.
+template <int NT, int TB>
+__device__ __forceinline__ void store_pair_il(const PassArgs& a, uint32_t* dstA, uint32_t* dstB, const uint32_t* tile,
+                                              int tid, int T, uint32_t h_q, uint32_t fixed) {
+  constexpr int MQ = (1 << TB) / (4 * NT);
+  uint4 va[MQ], vb[MQ];
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) {
+      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+      const uint32_t w0 = 2u * ((q ^ h) & ~3u);
+      const uint4 a0 = *(const uint4*)&tile[w0], a1 = *(const uint4*)&tile[w0 + 4];
+      va[i] = quad_perm(make_uint4(a0.x, a0.z, a1.x, a1.z), h & 3u);
+      vb[i] = quad_perm(make_uint4(a0.y, a0.w, a1.y, a1.w), h & 3u);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) {
+      *(uint4*)&dstA[mem_of(q, a, fixed)] = va[i];
+      *(uint4*)&dstB[mem_of(q, a, fixed)] = vb[i];
+    }
+  }
+}
+
 // Adjoint seed lambda = sum_c r_c Z_c psi on the adjoint image (psi plane word w, lambda plane word 2^TB + w).
 template <int NC, int NT, int TB = TMAX, bool PL = false>
 __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, int T, uint32_t fixed,
@@ -819,6 +902,148 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   HEA_MARK();
   if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
   HEA_MARK();
+}
+
+// ------------------------------------------------------------------------------------------- paired forward
+// Two samples of one client per workgroup on 2^13-amplitude tiles of the adjoint's plan (same passes, groups and
+// slots), interleaved like the adjoint image: every group op moves (sample A, sample B) amplitude pairs with one
+// ds_read_b64 / ds_write_b64 and applies U to both (the same client unitary), so a tile costs half the LDS
+// instructions per amplitude of the single-sample 2^14 forward at the same 64 KB of LDS and amplitudes per
+// workgroup.  Samples s = 2 * pair and s + 1 (spc even: a pair never straddles two clients).
+template <int NCK>
+__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd2_kernel(PassArgs a) {
+  constexpr int NT = NT_FWD, NW = NT / 64, TB = 13;
+  __shared__ __attribute__((aligned(16))) uint32_t tile[2 << TB];   // (A, B) fp16 (re, im) pairs, swizzled
+  __shared__ int opw2[2][OPW];
+  __shared__ int fidx_s[MAXOPS];
+  __shared__ uint32_t fo_s[MAXOPS];
+  __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];
+  __shared__ float red[2 * NW * CMAX];
+  __shared__ float2 wv[2][32][2];
+  __shared__ float2 tabA[2][128];
+  __shared__ float2 tabB[2][128];
+  __shared__ float2 outer_s[2];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int sp = blockIdx.x / a.n_tiles, tile_id = blockIdx.x % a.n_tiles;
+  const int s = 2 * sp;                                 // sample A; sample B = s + 1 (same client)
+  const int k = s / a.spc;
+  const int s_in = a.in_rep > 1 ? (s / (a.in_rep * a.spc)) * a.spc + s % a.spc : s;
+  const int T = 1 << a.t;
+  const size_t N = (size_t)1 << a.n;
+  const uint32_t fixed = tile_fixed(a, tile_id);
+  const float* prm = a.params + (size_t)k * a.p_stride;
+  const uint32_t h_q = swz(a, (uint32_t)tid >> 3);
+
+  if (tid < a.nops) {
+    fidx_s[tid] = a.fidx[tid];
+    fo_s[tid] = op_fo_global(a.ops + (size_t)tid * OPW, fixed);
+  }
+  if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
+  int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
+  if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
+
+  if (a.gen) {
+    // layer-1 product states of both samples: wave x computes sample x's qubit factors and outer factor
+    if (wave < 2) {
+      const int x = wave;
+      float2 w[2] = {make_float2(1.f, 0.f), make_float2(1.f, 0.f)};
+      if (lane < a.n) {
+        l1_factor(a.xang[(size_t)(s_in + x) * a.x_stride + lane], prm[2 * lane], prm[2 * lane + 1], a.feature, w);
+        wv[x][lane][0] = w[0];
+        wv[x][lane][1] = w[1];
+      }
+      const bool outq = lane < a.n && !(lane < a.c || (lane >= a.lo && lane < a.hi));
+      float2 f = outq ? w[(fixed >> (lane & 31)) & 1] : make_float2(1.f, 0.f);
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) f = cmul(f, make_float2(__shfl_xor(f.x, off, 64), __shfl_xor(f.y, off, 64)));
+      if (lane == 0) outer_s[x] = make_float2(a.scale * f.x, a.scale * f.y);
+    }
+    lds_barrier();
+    const int ta = a.t >> 1, tb = a.t - ta;
+    constexpr int JMAX = TB - (TB >> 1);
+    {
+      // threads [0, 256) build sample A's half tables, [256, 512) sample B's
+      const int x = tid >> 8, u = tid & 255;
+      const bool lowt = u < (1 << ta), hight = u >= 128 && u < 128 + (1 << tb);
+      if (lowt || hight) {
+        const int i = lowt ? u : u - 128, j0 = lowt ? 0 : ta, nj = lowt ? ta : tb;
+        float2 fac[JMAX];
+#pragma unroll
+        for (int j = 0; j < JMAX; ++j) {
+          const int tj = j0 + j, mb = tj < a.c ? tj : a.lo + tj - a.c;
+          fac[j] = wv[x][j < nj ? mb : 0][(i >> j) & 1];
+        }
+        float2 v = lowt ? make_float2(1.f, 0.f) : outer_s[x];
+#pragma unroll
+        for (int j = 0; j < JMAX; ++j)
+          if (j < nj) v = cmul(v, fac[j]);
+        if (lowt)
+          tabA[x][i] = v;
+        else
+          tabB[x][i] = v;
+      }
+    }
+    lds_barrier();
+    const uint32_t am = (1u << ta) - 1u;
+    constexpr int QI = (1 << TB) / (4 * NT);
+    uint4 oa[QI], ob[QI];
+#pragma unroll
+    for (int i = 0; i < QI; ++i) {
+      const uint32_t q = (uint32_t)(tid + NT * i);
+      const uint32_t qq = 4 * q < (uint32_t)T ? q : 0u;
+      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+      const float2 va = tabB[0][((4 * qq) ^ h) >> ta], vbb = tabB[1][((4 * qq) ^ h) >> ta];
+      uint32_t* wa = (uint32_t*)&oa[i];
+      uint32_t* wb = (uint32_t*)&ob[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t ix = ((4 * qq + e) ^ h) & am;
+        const float2 v0 = cmul(tabA[0][ix], va), v1 = cmul(tabA[1][ix], vbb);
+        wa[e] = pack_h2(v0.x, v0.y);
+        wb[e] = pack_h2(v1.x, v1.y);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < QI; ++i) {
+      const uint32_t q = (uint32_t)(tid + NT * i);
+      if (4 * q < (uint32_t)T) {
+        *(uint4*)&tile[8 * q] = make_uint4(oa[i].x, ob[i].x, oa[i].y, ob[i].y);
+        *(uint4*)&tile[8 * q + 4] = make_uint4(oa[i].z, ob[i].z, oa[i].w, ob[i].w);
+      }
+    }
+  } else {
+    load_tile_il<NT, TB, false>(a, a.psi_in + (size_t)s_in * N, a.psi_in + (size_t)(s_in + 1) * N, tile, tid, T,
+                                h_q, fixed);
+  }
+
+  constexpr int NBW = (1 << (TB - 8)) / NW;            // t == 13 (host-checked): 4 column blocks per wave
+  lds_barrier_dma();
+  for (int o = 0; o < a.nops; ++o) {
+    op_barrier(wave);
+    const int* opw = opw2[o & 1];
+    uint4 F[4];
+    if (fidx_s[o] >= 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) F[i] = frag_s[o & 1][64 * i + lane];
+    }
+    if (o + 1 < a.nops) {
+      if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
+      if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
+      dma_frags(a, k, fidx_s[o + 1], lane, wave, frag_s[(o + 1) & 1]);
+    }
+    const int code = opw[W_CODE];
+    QFX_DCHECK(code == OP_APPLY || code == OP_READOUT);
+    if (code == OP_APPLY) {
+      group_apply<2, NW, true, 0, TB, false>(tile, F, opw, fo_s[o], lane, wave, NBW);   // U on both samples
+    } else if (code == OP_READOUT) {
+      readout_pair_op<NCK, NT, TB>(tile, a, opw, tid, lane, wave, T, fixed, red,
+                                   ((size_t)s * a.n_tiles + tile_id) * a.C, ((size_t)(s + 1) * a.n_tiles + tile_id) * a.C);
+    }
+  }
+  lds_barrier();
+  if (a.store_psi) store_pair_il<NT, TB>(a, a.psi_out + (size_t)s * N, a.psi_out + (size_t)(s + 1) * N, tile, tid, T, h_q, fixed);
 }
 
 // ------------------------------------------------------------------------------------------- adjoint pass
@@ -1142,7 +1367,7 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
 extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_samples, hipStream_t st) {
   const hea::PassArgs& a = *args;
   if (a.t > hea::TMAX || a.t < 8 || a.C > hea::CMAX || a.n > 30 || a.c < 2) return -2;
-  const unsigned grid = (unsigned)(n_samples * a.n_tiles);
+  const unsigned grid = (unsigned)((a.pair && !adjoint ? n_samples / 2 : n_samples) * a.n_tiles);
   if (grid == 0) return 0;
   static int planes = -1;   // adjoint LDS image: 0 interleaved (psi, lambda) pairs, 1 planes (QFEDX_HEA_PLANES)
   if (planes < 0) {
@@ -1156,7 +1381,9 @@ extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_sample
   }
 #define HEA_LAUNCH(NCK)                                                                                     \
   do {                                                                                                     \
-    if (!adjoint && a.t == hea::TMAX)                                                                      \
+    if (!adjoint && a.pair)                                                                                \
+      hipLaunchKernelGGL((hea::hea_fwd2_kernel<NCK>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);            \
+    else if (!adjoint && a.t == hea::TMAX)                                                                 \
       hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK, true>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);       \
     else if (!adjoint)                                                                                     \
       hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK, false>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);      \

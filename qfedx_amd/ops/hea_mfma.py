@@ -89,7 +89,13 @@ class HeaMfmaProgram:
         self.n_slots = self.plan.n_slots
         self.passes = []
         gmeta = []
-        progs_f = pass_programs(self.plan, [])
+        # Paired forward (QFEDX_HEA_FWD_PAIR, default on): when the adjoint runs its own 2^13 plan, the forward runs
+        # that plan too, two samples of a client per workgroup (hea_fwd2_kernel; an odd sample count falls back to
+        # one sample per 2^13 tile)
+        self.fwd_pair = (plan_a is not self.plan and self.adj_tile_bits == 13
+                         and os.environ.get("QFEDX_HEA_FWD_PAIR", "1") != "0")
+        fplan = plan_a if self.fwd_pair else self.plan
+        progs_f = pass_programs(fplan, [])
         # Forward passes after the last one that applies a unitary are identities on the state (they exist for
         # the adjoint's layer-1 gradient tiles, e.g. every pass of an L = 1 circuit): the forward stops at that
         # pass, reads out there, and later passes' stored outputs alias its output.
@@ -105,7 +111,7 @@ class HeaMfmaProgram:
         self.n_gradops = len(gmeta)
         if self.fwd_last < J - 1:
             pr, fr_ops, ar = progs_f[self.fwd_last]
-            fr_ops = np.concatenate([fr_ops, obs_table(self.plan, pr, OP_READOUT)[None]], 0)
+            fr_ops = np.concatenate([fr_ops, obs_table(fplan, pr, OP_READOUT)[None]], 0)
             progs_f = [(p, f if j < self.fwd_last else (fr_ops if j == self.fwd_last else f[:0]), a)
                        for j, (p, f, a) in enumerate(progs_f)]
         for (p, fwd, _), (pa, _, adj) in zip(progs_f, progs_a):
@@ -137,9 +143,15 @@ class HeaMfmaProgram:
         self.scale = float(1 << (self.n // 2))
         self.feature = _FEATURE[spec.feature_map.lower()]
         self._ws = {}
+        self.pair_kernel = True
         self._ps_budget = None
         if self.device.type == "cuda":
             self._shift_budget()      # query free HBM now, never inside a graph capture
+
+    def _paired(self, B: int) -> bool:
+        """Forward passes on the two-sample kernel (``pair_kernel = False`` keeps the one-sample 2^13 kernel on the
+        same plan: bitwise the same results, used by the tests)."""
+        return self.fwd_pair and self.pair_kernel and B % 2 == 0
 
     # ------------------------------------------------------------------ workspaces
     @contextlib.contextmanager
@@ -168,10 +180,11 @@ class HeaMfmaProgram:
         """Tiles per sample of the pass that reads out <Z> (the last forward pass that runs)."""
         return 1 << (self.n - self.passes[self.fwd_last][0].t)
 
-    def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K, in_rep: int = 1):
+    def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K, in_rep: int = 1,
+              pair: bool = False):
         return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
                 int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
-                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep)]
+                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep), int(pair)]
 
     def _frags(self, params: torch.Tensor, K: int, tag: str = "") -> torch.Tensor:
         fr = self._buf(f"{tag}frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
@@ -198,7 +211,8 @@ class HeaMfmaProgram:
             name = f"{tag}psi{j}" if store_last else f"{tag}pe{j % 2}"
             out = self._buf(name, N, torch.int32) if keep else empty
             psi_in = stored[-1] if j > 0 else empty
-            geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K)
+            geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K,
+                              pair=self._paired(B))
             C.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
                        part if j == R else fempty, fempty, _NODBG)
             if j == 0 and after_first is not None:
@@ -447,7 +461,8 @@ class HeaMfmaProgram:
             keep = jj < R
             out = self._buf(f"pbpsi{(jj - j) % 2}", N, torch.int32) if keep else empty
             first = jj == j
-            geom = self._geom(p, jj == 0, False, keep, False, B, ps, S, xs.shape[1], Kr, nr if first else 1)
+            geom = self._geom(p, jj == 0, False, keep, False, B, ps, S, xs.shape[1], Kr, nr if first else 1,
+                              pair=self._paired(B))
             E.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, xs, thr, fr, fempty,
                        part if jj == R else fempty, fempty, _NODBG)
             psi_in = out

@@ -10,9 +10,13 @@ MPI / Slurm (``ROADMAP.md:39,77-89``).  Design here:
   all-reduce per round (CC2+CC3), latency-bound on xGMI (<= 0.5 MB), so fewer/larger messages;
 * ``exact`` mode all-reduces a fixed-point int64 encoding: integer sums are associative, so the
   aggregate is bitwise identical for 1/2/4/8 ranks (SURVEY §7.3 item 10);
-* a dedicated comm stream + events lets the collective overlap compute (``CommStream``), and
-  ``BucketedAllReduce`` splits large models (TinyCNN, 455 KB) into layer buckets whose consumers wait
-  only on their own bucket's event (CC4);
+* the round's collective and the in-place apply are captured into the round's hipGraph with the local steps
+  (``fl/trainer.py`` ``_graphed``; RCCL accepts capture), so a round is one graph launch with no host
+  round trip between training and aggregation.  Nothing of round r + 1 can overlap the collective: its local
+  steps start from the theta the collective produces, and the theta-independent part (the minibatch gather of the
+  round prologue) is a few microseconds.  A comm-stream / layer-bucket overlap design was removed in round 3 as
+  dead code for that reason: the one message per round is <= 1 MB (TinyCNN, 911 KB as int64), latency-bound on
+  xGMI, so bucketing would only add launches (CC4);
 * ``ShardedServerState``: reduce-scatter + all-gather for a server optimizer whose state is
   sharded P/world per rank (CC5).
 """
@@ -137,121 +141,6 @@ def max_over_ranks(x: float, world: World, device=None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device or world.device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
-
-
-class CommStream:
-    """Dedicated HIP stream for collectives; ``wait`` makes the compute stream consume the result."""
-
-    def __init__(self, world: World):
-        self.world = world
-        self.cuda = world.device.type == "cuda"
-        self.stream = torch.cuda.Stream(device=world.device) if self.cuda else None
-        self._event = None
-        self._work = None
-
-    def all_reduce_async(self, buf: torch.Tensor) -> None:
-        if not self.world.distributed:
-            return
-        if self.cuda:
-            ready = torch.cuda.Event()
-            ready.record()                       # buffer produced on the compute stream
-            with torch.cuda.stream(self.stream):
-                self.stream.wait_event(ready)
-                dist.all_reduce(buf)
-                self._event = torch.cuda.Event()
-                self._event.record(self.stream)
-            buf.record_stream(self.stream)
-        else:
-            self._work = dist.all_reduce(buf, async_op=True)
-
-    def wait(self) -> None:
-        if self._event is not None:
-            torch.cuda.current_stream().wait_event(self._event)
-            self._event = None
-        if self._work is not None:
-            self._work.wait()
-            self._work = None
-
-
-class FusedRoundBuffer:
-    """One flat buffer per round: [update sum (P) | sum of weights | metric scalars...].
-
-    ``exact=True`` packs everything as fixed-point int64 (scale 2^-frac_bits) so the all-reduce is
-    associative -> bitwise rank-count invariance.  Metrics must then be integers or fixed-point.
-    """
-
-    def __init__(self, P: int, n_metrics: int, device, exact: bool = False, frac_bits: int = 32):
-        self.P = P
-        self.n_metrics = n_metrics
-        self.exact = exact
-        self.scale = float(2 ** frac_bits)
-        dtype = torch.int64 if exact else torch.float64
-        self.buf = torch.zeros(P + 1 + n_metrics, dtype=dtype, device=device)
-
-    def pack(self, update_sum: torch.Tensor, weight_sum: torch.Tensor, metrics: torch.Tensor) -> torch.Tensor:
-        vals = torch.cat([update_sum.reshape(-1).double(), weight_sum.reshape(1).double(),
-                          metrics.reshape(-1).double()])
-        if self.exact:
-            self.buf.copy_(torch.round(vals * self.scale).to(torch.int64))
-        else:
-            self.buf.copy_(vals)
-        return self.buf
-
-    def unpack(self):
-        vals = self.buf.double() / self.scale if self.exact else self.buf
-        return vals[: self.P], vals[self.P], vals[self.P + 1:]
-
-
-class BucketedAllReduce:
-    """Layer-bucketed all-reduce of a flat parameter vector on the comm stream (CC4).
-
-    Buckets are contiguous [start, end) slices (e.g. TinyCNN layer boundaries, merged up to
-    ``bucket_bytes``); ``wait_bucket(i)`` blocks the compute stream only on bucket i.
-    """
-
-    def __init__(self, world: World, boundaries: list[int], bucket_bytes: int = 1 << 20, elem_bytes: int = 8):
-        self.world = world
-        self.buckets: list[tuple[int, int]] = []
-        acc_start = 0
-        for end in boundaries[1:]:
-            if (end - acc_start) * elem_bytes >= bucket_bytes:
-                self.buckets.append((acc_start, end))
-                acc_start = end
-        if acc_start < boundaries[-1]:
-            self.buckets.append((acc_start, boundaries[-1]))
-        self.cuda = world.device.type == "cuda"
-        self.stream = torch.cuda.Stream(device=world.device) if self.cuda else None
-        self.events: list = []
-        self.works: list = []
-
-    def launch(self, flat: torch.Tensor) -> None:
-        self.events, self.works = [], []
-        if not self.world.distributed:
-            return
-        if self.cuda:
-            ready = torch.cuda.Event()
-            ready.record()
-            with torch.cuda.stream(self.stream):
-                self.stream.wait_event(ready)
-                for s, e in self.buckets:
-                    dist.all_reduce(flat[s:e])
-                    ev = torch.cuda.Event()
-                    ev.record(self.stream)
-                    self.events.append(ev)
-            flat.record_stream(self.stream)
-        else:
-            for s, e in self.buckets:
-                self.works.append(dist.all_reduce(flat[s:e], async_op=True))
-
-    def wait_bucket(self, i: int) -> None:
-        if self.events:
-            torch.cuda.current_stream().wait_event(self.events[i])
-        elif self.works:
-            self.works[i].wait()
-
-    def wait_all(self) -> None:
-        for i in range(len(self.buckets)):
-            self.wait_bucket(i)
 
 
 def reduce_scatter_(full: torch.Tensor, world: World) -> torch.Tensor:

@@ -169,3 +169,25 @@ def test_hea_class_counts_match_dense(cuda, C, tile):
     torch.cuda.synchronize()
     np.testing.assert_allclose(z.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
     np.testing.assert_allclose(g.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
+
+
+@pytest.mark.parametrize("n,L", [(16, 3), (14, 2)])
+def test_paired_forward_is_bitwise_single_sample_kernel(cuda, n, L):
+    """The two-sample forward kernel (hea_fwd2_kernel) on the adjoint's 2^13 plan gives bitwise the <Z>, stored pass
+    outputs (through the adjoint) and gradients of the one-sample kernel on the same plan, and matches the dense
+    float64 oracle."""
+    spec = VQCSpec(n, L, 3)
+    prog = HeaMfmaProgram(spec, cuda)
+    if not prog.fwd_pair:
+        pytest.skip("no separate 2^13 plan at this size")
+    K, B = 3, 4
+    x, params, wr = _inputs(spec, K, B, seed=11)
+    xx, th, ww = x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda)
+    z2, g2 = prog.vjp(xx, th, ww)
+    prog.pair_kernel = False
+    z1, g1 = prog.vjp(xx, th, ww)
+    torch.cuda.synchronize()
+    assert torch.equal(z1, z2) and torch.equal(g1, g2)
+    ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
+    np.testing.assert_allclose(z2.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
+    np.testing.assert_allclose(g2.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
