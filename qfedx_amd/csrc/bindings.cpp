@@ -74,6 +74,9 @@ int qfx_launch_sgdm(float* p, const float* g, float* buf, const float* t_in, flo
                     int K, int P, float lr, float mu, int keep, hipStream_t st);
 int qfx_launch_host_upload(const void* host_src, void* dst, long nbytes, hipStream_t st);
 int qfx_launch_round_signal(long long* ctr, long long* host_flag, hipStream_t st);
+int qfx_launch_ps_combine(const float* f0, const float* fpi, const float* jac, const float* w, const long long* keys,
+                          float p01, float p10, int shots, unsigned stream, int K, int P, int B, int C, int noisy,
+                          float* out, hipStream_t st);
 int qfx_launch_round_init(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
                           hipStream_t st);
 int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
@@ -312,6 +315,32 @@ void host_upload(torch::Tensor src, torch::Tensor dst) {
   const int64_t n = src.numel();
   if (dst.numel() < n || n % 16) throw std::invalid_argument("host_upload: size (16-byte multiple, dst >= src)");
   check(qfx_launch_host_upload(src.data_ptr(), dst.data_ptr(), (long)n, cur_stream()), "qfx_host_upload");
+}
+
+// f0 [K,B,C], fpi [K,P,B,C] (empty: no mean term), jac [K,B,C,P], w [K,B,C], keys [K,2] int64 (shots > 0) -> out [K,P]
+void ps_combine(torch::Tensor f0, torch::Tensor fpi, torch::Tensor jac, torch::Tensor w, torch::Tensor keys,
+                double p01, double p10, int64_t shots, int64_t stream, int64_t noisy, torch::Tensor out) {
+  need(jac, torch::kFloat32, "jac");
+  need(w, torch::kFloat32, "w");
+  need(out, torch::kFloat32, "out");
+  const int64_t K = out.size(0), P = out.size(1);
+  const int64_t B = w.size(1), C = w.size(2);
+  if (w.dim() != 3 || w.size(0) != K || jac.numel() != K * B * C * P)
+    throw std::invalid_argument("ps_combine: w [K,B,C] / jac [K,B,C,P] shapes");
+  if (fpi.numel()) {
+    need(f0, torch::kFloat32, "f0");
+    need(fpi, torch::kFloat32, "fpi");
+    if (f0.numel() != K * B * C || fpi.numel() != K * P * B * C) throw std::invalid_argument("ps_combine: f0 / fpi");
+  }
+  if (noisy && shots > 0) {
+    need(keys, torch::kInt64, "keys");
+    if (keys.numel() < 2 * K) throw std::invalid_argument("ps_combine: keys [K, 2]");
+  }
+  check(qfx_launch_ps_combine(fpi.numel() ? ptr<float>(f0) : nullptr, ptr<float>(fpi), ptr<float>(jac), ptr<float>(w),
+                              (noisy && shots > 0) ? ptr<long long>(keys) : nullptr, (float)p01, (float)p10,
+                              (int)shots, (unsigned)stream, (int)K, (int)P, (int)B, (int)C, (int)noisy,
+                              ptr<float>(out), cur_stream()),
+        "qfx_ps_combine");
 }
 
 // ctr: device int64 [1] (the graph entry's round counter); flag: coherent host_alloc memory holding one int64
@@ -559,6 +588,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("round_init", &round_init);
   m.def("host_alloc", &host_alloc, py::arg("nbytes"), py::arg("coherent") = false);
   m.def("round_signal", &round_signal);
+  m.def("ps_combine", &ps_combine);
   m.def("host_upload", &host_upload);
   m.def("batch_plan", &qfx_runtime::batch_plan);
   m.def("batch_gather", &batch_gather);

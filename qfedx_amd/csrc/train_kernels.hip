@@ -578,6 +578,41 @@ __global__ void qfx_round_apply_kernel(long long* __restrict__ buf, int P, float
   }
 }
 
+// Parameter-shift combine (ops/hea_mfma.py HeaMfmaProgram.param_shift): for client k and parameter j, the exact
+// shifted expectations z+- = m +- f' (m = (f(theta) + f(theta + pi)) / 2, or 0 when only their difference counts),
+// each confused / shot-sampled on the Philox stream of its (client, slot, sign) row exactly as the naive
+// shifted-row path samples it (row key = client key mixed with row + 1), then dL/dtheta_j = 1/2 sum_(b, c)
+// (z+ - z-) w[b][c].  One block per (j, k); per-thread partials and the block sum in fixed order (deterministic).
+__global__ void __launch_bounds__(64) qfx_ps_combine_kernel(const float* __restrict__ f0, const float* __restrict__ fpi,
+                                                            const float* __restrict__ jac, const float* __restrict__ w,
+                                                            const long long* __restrict__ keys, float p01, float p10,
+                                                            int shots, unsigned stream, int P, int B, int C,
+                                                            int noisy, float* __restrict__ out) {
+  const int j = blockIdx.x, k = blockIdx.y, tid = threadIdx.x;
+  __shared__ double red[64];
+  double acc = 0.0;
+  for (int e = tid; e < 2 * B * C; e += 64) {
+    const int sg = e / (B * C), bc = e - sg * B * C, b = bc / C, c = bc - b * C;
+    const float jv = jac[(((size_t)k * B + b) * C + c) * P + j];
+    const float m = fpi ? 0.5f * (f0[((size_t)k * B + b) * C + c] + fpi[(((size_t)k * P + j) * B + b) * C + c]) : 0.f;
+    float z = sg ? m - jv : m + jv;
+    if (noisy) {
+      const uint32_t row = (uint32_t)(2 * j + sg) + 1u;
+      const uint32_t k0 = keys ? ((uint32_t)keys[2 * k] ^ (row * 0x9E3779B9u)) : 0u;
+      const uint32_t k1 = keys ? ((uint32_t)keys[2 * k + 1] + row * 0x85EBCA6Bu) : 0u;
+      z = noisy_z(z, p01, p10, shots, k0, k1, stream, ((uint64_t)b * C + c) * (uint64_t)shots);
+    }
+    acc += (sg ? -0.5 : 0.5) * (double)z * (double)w[((size_t)k * B + b) * C + c];
+  }
+  red[tid] = acc;
+  __syncthreads();
+  for (int off = 32; off > 0; off >>= 1) {
+    if (tid < off) red[tid] += red[tid + off];
+    __syncthreads();
+  }
+  if (tid == 0) out[(size_t)k * P + j] = (float)red[0];
+}
+
 // Round-completion signal, the last node of a captured round: bumps the graph entry's device counter and
 // publishes it to a coherent pinned host word (system-scope release store).  The host reuses a pinned upload
 // buffer once the counter shows the round that read it has finished - no HIP event per round (an event record
@@ -593,6 +628,15 @@ __global__ void qfx_round_signal_kernel(long long* __restrict__ ctr, long long* 
 }  // namespace qfx
 
 using namespace qfx;
+
+extern "C" int qfx_launch_ps_combine(const float* f0, const float* fpi, const float* jac, const float* w,
+                                     const long long* keys, float p01, float p10, int shots, unsigned stream, int K,
+                                     int P, int B, int C, int noisy, float* out, hipStream_t st) {
+  if (K <= 0 || P <= 0) return 0;
+  hipLaunchKernelGGL(qfx_ps_combine_kernel, dim3((unsigned)P, (unsigned)K), dim3(64), 0, st, f0, fpi, jac, w, keys,
+                     p01, p10, shots, stream, P, B, C, noisy, out);
+  return (int)hipGetLastError();
+}
 
 extern "C" int qfx_launch_round_signal(long long* ctr, long long* host_flag, hipStream_t st) {
   hipLaunchKernelGGL(qfx_round_signal_kernel, dim3(1), dim3(64), 0, st, ctr, host_flag);

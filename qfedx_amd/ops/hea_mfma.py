@@ -340,6 +340,15 @@ class HeaMfmaProgram:
         """Exact <Z> at theta +- pi/2 e_j for every client, parameter j, sign and sample -> [K, n_theta, 2, B, C]
         (sign 0: +pi/2), from the prefix-reuse identities of ``param_shift``.  ``with_mean=False`` drops the
         common term m (only the +- difference is wanted) and skips the +pi branches."""
+        f0, fpi, jac = self._shift_parts(xang, params, with_mean)
+        jt = jac.permute(0, 3, 1, 2)                        # [K, P, B, C]
+        m = 0.5 * (f0.unsqueeze(1) + fpi) if with_mean else torch.zeros_like(jt)
+        return torch.stack([m + jt, m - jt], 2).contiguous()
+
+    @torch.no_grad()
+    def _shift_parts(self, xang: torch.Tensor, params: torch.Tensor, with_mean: bool):
+        """f(theta) [K, B, C], f(theta + pi e_j) [K, P, B, C] (None without the mean term) and the per-sample
+        Jacobian d<Z_c>/dtheta_j [K, B, C, P]."""
         E = ext()
         x, th, K, B = self._prep(xang, params)
         P, C, n = self.n_theta, self.C, self.n
@@ -394,9 +403,7 @@ class HeaMfmaProgram:
                         src = stored[j - 1][(a0 * B) << n:(a1 * B) << n] if j > 0 else empty
                         zb = self._pi_branch(j, xs[a0 * B:a1 * B], ths[a0:a1], slots[r0:r1], B, src)
                         fpi[k0 + a0:k0 + a1].index_copy_(1, slots[r0:r1], zb)
-        jt = jac.permute(0, 3, 1, 2)                        # [K, P, B, C]
-        m = 0.5 * (f0.unsqueeze(1) + fpi) if with_mean else torch.zeros_like(jt)
-        return torch.stack([m + jt, m - jt], 2).contiguous()
+        return f0, fpi, jac
 
     @torch.no_grad()
     def param_shift(self, xang: torch.Tensor, params: torch.Tensor, w: torch.Tensor, noise=None, keys=None,
@@ -422,21 +429,19 @@ class HeaMfmaProgram:
         w = dL/d<Z>_noisy [K, B, C] -> [K, n_theta]."""
         K, B, C = w.shape
         P = self.n_theta
-        need_m = not exact_only and noise is not None and noise.shots > 0
-        zz = self.shifted_expz(xang, params, with_mean=need_m)
-        if noise is not None and not exact_only:
-            from .statevec_hip import _keys
-            kk = None
-            if noise.shots > 0:
-                j = torch.arange(2 * P, device=self.device, dtype=torch.int64)
-                kk = keys.to(self.device).long()[:, None, :].repeat(1, 2 * P, 1)
-                kk[..., 0] = (kk[..., 0] ^ ((j + 1) * 0x9E3779B9)) & 0xFFFFFFFF
-                kk[..., 1] = (kk[..., 1] + (j + 1) * 0x85EBCA6B) & 0xFFFFFFFF
-                kk = kk.reshape(K * 2 * P, 2).contiguous()
-            ext().readout_noise(zz, C, B, K * 2 * P * B, noise.p01, noise.p10, noise.shots, _keys(kk, noise),
-                                int(step))
-        d = (zz[:, :, 0] - zz[:, :, 1]).double() * w.reshape(K, 1, B, C).double()
-        return (0.5 * d.sum((2, 3))).float()
+        noisy = noise is not None and not exact_only
+        need_m = noisy and noise.shots > 0
+        f0, fpi, jac = self._shift_parts(xang, params, with_mean=need_m)
+        # shifted expectations, their readout model and the shift rule in one device launch (HIP, qfx_ps_combine)
+        out = torch.empty(K, P, dtype=torch.float32, device=self.device)
+        kk = keys.to(self.device).long().contiguous() if (need_m and keys is not None) else _NO_KEYS.to(self.device)
+        if need_m and keys is None:
+            raise ValueError("shot sampling needs per-client Philox keys")
+        fe = torch.empty(0, device=self.device)
+        ext().ps_combine(f0 if need_m else fe, fpi if need_m else fe, jac.contiguous(), w.float().contiguous(), kk,
+                         noise.p01 if noisy else 0.0, noise.p10 if noisy else 0.0, noise.shots if noisy else 0,
+                         int(step), int(noisy), out)
+        return out
 
     def _pi_branch(self, j, xs, ths, slots, B, src) -> torch.Tensor:
         """<Z> of theta + pi e_slot for clients ths [na, ps] x slots [nr] owned by forward pass j: passes
