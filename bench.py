@@ -47,12 +47,15 @@ def timed_rounds(cfg, device, backend, world, warmup: int, steps: int, counts: l
         runner.run_round(r, sync=False)
     sync()
     runner.timer.enabled = False            # no phase events inside the timed rounds (phase_ms calibrates after)
+    from qfedx_amd.fl import trainer as _tr
+    w0 = _tr.WAIT_S[0]
     t0 = time.perf_counter()
     for r in range(warmup, warmup + steps):
         rec = runner.run_round(r, sync=False)
         if counts is not None:
             counts.append(rec["participants"] - rec["dropped"])
-    runner.host_ms = 1e3 * (time.perf_counter() - t0) / max(steps, 1)   # host time to enqueue a round
+    # host time to build and enqueue a round, without the time it waited for the GPU to free a pinned buffer
+    runner.host_ms = 1e3 * (time.perf_counter() - t0 - (_tr.WAIT_S[0] - w0)) / max(steps, 1)
     sync()
     dt = time.perf_counter() - t0
     return runner, max_over_ranks(dt, world)

@@ -37,7 +37,9 @@ def _wait_rounds(ent: dict, n: int) -> None:
     if n <= 0:
         return
     flag = ent["flag"].view(torch.int64)
-    spins, t0 = 0, None
+    if int(flag[0]) >= n:
+        return
+    spins, t0, tw = 0, None, time.perf_counter()
     while int(flag[0]) < n:
         spins += 1
         if spins > 64:
@@ -49,6 +51,10 @@ def _wait_rounds(ent: dict, n: int) -> None:
                 if int(flag[0]) < n:
                     raise RuntimeError(f"round signal stuck at {int(flag[0])} < {n}: device writes to the coherent "
                                        "pinned word are not visible to the host")
+    WAIT_S[0] += time.perf_counter() - tw
+
+
+WAIT_S = [0.0]     # host seconds spent waiting for the GPU in _wait_rounds (bench: host enqueue cost = loop - wait)
 
 class ShardStore:
     """Device-resident padded shards: X [K, Nmax, F], y [K, Nmax], counts [K]."""

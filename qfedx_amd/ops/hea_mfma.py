@@ -89,11 +89,12 @@ class HeaMfmaProgram:
         self.n_slots = self.plan.n_slots
         self.passes = []
         gmeta = []
-        # Paired forward (QFEDX_HEA_FWD_PAIR, default on): when the adjoint runs its own 2^13 plan, the forward runs
+        # Paired forward (QFEDX_HEA_FWD_PAIR=1, opt-in): when the adjoint runs its own 2^13 plan, the forward runs
         # that plan too, two samples of a client per workgroup (hea_fwd2_kernel; an odd sample count falls back to
-        # one sample per 2^13 tile)
+        # one sample per 2^13 tile).  Measured even with the 2^14 one-sample forward at 16q (fwd0 +1%, fwd1 -2%):
+        # the forward is not LDS-issue bound, so the long-tested 2^14 path stays the default.
         self.fwd_pair = (plan_a is not self.plan and self.adj_tile_bits == 13
-                         and os.environ.get("QFEDX_HEA_FWD_PAIR", "1") != "0")
+                         and os.environ.get("QFEDX_HEA_FWD_PAIR", "0") == "1")
         fplan = plan_a if self.fwd_pair else self.plan
         progs_f = pass_programs(fplan, [])
         # Forward passes after the last one that applies a unitary are identities on the state (they exist for
