@@ -614,14 +614,16 @@ __global__ void __launch_bounds__(64) qfx_ps_combine_kernel(const float* __restr
 }
 
 // Round-completion signal, the last node of a captured round: bumps the graph entry's device counter and
-// publishes it to a coherent pinned host word (system-scope release store).  The host reuses a pinned upload
-// buffer once the counter shows the round that read it has finished - no HIP event per round (an event record
-// between two graph launches cost ~5 us of GPU idle each on this stack; scripts/graph_gap.py).
+// publishes it to a coherent pinned host word.  The host reuses a pinned upload buffer once the counter shows the
+// round that read it has finished - no HIP event per round (an event record between two graph launches cost ~5 us
+// of GPU idle each on this stack; scripts/graph_gap.py).  The store is RELAXED at system scope: the host needs the
+// count only (the upload kernel that read the buffer finished before this node in stream order), and a release
+// would write back the whole L2 - dirty with the round's states - before the store.
 __global__ void qfx_round_signal_kernel(long long* __restrict__ ctr, long long* host_flag) {
   if (threadIdx.x == 0) {
     const long long c = ctr[0] + 1;
     ctr[0] = c;
-    __hip_atomic_store(host_flag, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(host_flag, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
