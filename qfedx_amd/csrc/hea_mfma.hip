@@ -46,6 +46,7 @@ enum { W_CODE = 0, W_SLOT = 1, W_NREAL = 2, W_FLAGS = 3, W_RFULL = 4, W_RT = 8, 
        W_BL = 36, W_BH = 68, W_GIDX = 100 };
 constexpr double FIX = 4294967296.0;   // 2^32: fixed point of the scaled gradient partial traces
 constexpr int F_BACK_PSI = 1;
+constexpr int F_BACK_TRANS = 2;   // OP_BACK (with F_BACK_PSI) in the transposed form: cross matrix at the op input
 constexpr int TMAX = 14;
 constexpr int NT_FWD = 512;    // forward: 8 waves, 64 KB LDS -> 2 workgroups per CU
 constexpr int NT_ADJ = 1024;   // adjoint: 16 waves, 128 KB LDS (psi + lambda) -> 1 workgroup per CU
@@ -292,7 +293,7 @@ __device__ __forceinline__ uint32_t mul_i(uint32_t v) {
 
 // Y = U X on the op's column blocks for NX targets (tile byte bases tb[x]) sharing the addressing.  Lane
 // (g4, cl) owns column cl of a 16-column block: it reads amplitudes m = 4 g4 .. 4 g4 + 3 (B operand,
-// k = 2m + re/im) and writes rows m' = 2 g4, 2 g4 + 1, 8 + 2 g4, 9 + 2 g4 of the two 16-row output blocks.
+// k = 2m + re/im) and writes the same amplitudes back (row 4 g4 + i of output tile 0 / 1 = re / im of m' = 4 g4 + i).
 // A wave's blocks are blk = wave + NW i (i < nbw <= MAXB, fully unrolled): (blk & 1) = (wave & 1), so the
 // block bases are BL[lane] ^ BH[blk >> 1] precomputed in registers.  Blocks go in pairs (independent MFMA
 // chains) and the next pair's operands are read before the current pair is written (disjoint blocks).
@@ -307,7 +308,7 @@ __device__ __forceinline__ uint32_t mul_i(uint32_t v) {
 //               Accumulator layout as group_cross: lane (g4, cl) holds N[4 g4 + i][cl].
 template <int NX, int NW, bool IL, int SEL, int TB = TMAX, bool PL = false, bool CROSS = false>
 __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, const int* opw, uint32_t fo, int lane,
-                                            int wave, int nbw, f4* acc = nullptr, uint4 IRE = {}, uint4 IIM = {}) {
+                                            int wave, int nbw, f4* acc = nullptr) {
   constexpr int MAXB = (1 << (TB - 8)) / NW;   // column blocks per wave per op (t = 14: 64 blocks)
   constexpr bool PAIR = IL && !PL;             // interleaved adjoint image: (psi, lambda) word pairs
   static_assert(!CROSS || PAIR, "the fused cross matrix reads the interleaved image");
@@ -316,13 +317,21 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
   constexpr uint32_t LP = 4u * lam_word<TB>();  // lambda plane (planes image), bytes
   static_assert(IL || NX == 1, "the forward image holds psi only");
   const int g4 = lane >> 4, cl = lane & 15;
-  uint32_t oin[4], oout[4];
+  uint32_t oin[4];
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) oin[jj] = ((uint32_t)opw[W_OFF + 4 * g4 + jj] ^ fo) << SH;
-  oout[0] = ((uint32_t)opw[W_OFF + 2 * g4] ^ fo) << SH;
-  oout[1] = ((uint32_t)opw[W_OFF + 2 * g4 + 1] ^ fo) << SH;
-  oout[2] = ((uint32_t)opw[W_OFF + 8 + 2 * g4] ^ fo) << SH;
-  oout[3] = ((uint32_t)opw[W_OFF + 9 + 2 * g4] ^ fo) << SH;
+  // CROSS: identity fragments (rows: re of amplitude n, then im), built here so they are not live across the
+  // kernel's op loop
+  uint4 IRE = {}, IIM = {};
+  if constexpr (CROSS) {
+    uint32_t* re = (uint32_t*)&IRE;
+    uint32_t* im = (uint32_t*)&IIM;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      re[j] = cl == 4 * g4 + j ? 0x00003C00u : 0u;
+      im[j] = cl == 4 * g4 + j ? 0x3C000000u : 0u;
+    }
+  }
   const uint32_t bl = (uint32_t)opw[W_BL + (wave & 1) * 16 + cl];
   uint32_t base[MAXB];
 #pragma unroll
@@ -368,20 +377,18 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
       d0[x] = mfma(F[2], X[x], d0[x]);
       d1[x] = mfma(F[3], X[x], d1[x]);
     }
-    const uint32_t s0 = b ^ oout[0], s1 = b ^ oout[1], s2 = b ^ oout[2], s3 = b ^ oout[3];
+    // output amplitude 4 g4 + i = (tile 0, tile 1) register i, written where it was read
     if constexpr (PAIR && NX == 2) {
-      lds_st2(tile, s0, make_uint2(pack_h2(d0[0][0], d0[0][1]), pack_h2(d0[1][0], d0[1][1])));
-      lds_st2(tile, s1, make_uint2(pack_h2(d0[0][2], d0[0][3]), pack_h2(d0[1][2], d0[1][3])));
-      lds_st2(tile, s2, make_uint2(pack_h2(d1[0][0], d1[0][1]), pack_h2(d1[1][0], d1[1][1])));
-      lds_st2(tile, s3, make_uint2(pack_h2(d1[0][2], d1[0][3]), pack_h2(d1[1][2], d1[1][3])));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        lds_st2(tile, b ^ oin[i], make_uint2(pack_h2(d0[0][i], d1[0][i]), pack_h2(d0[1][i], d1[1][i])));
     } else {
 #pragma unroll
       for (int x = 0; x < NX; ++x) {
         const uint32_t pl = PAIR ? 4u * SEL : ((NX == 2 ? x : (IL ? SEL : 0)) ? LP : 0u);
-        lds_st(tile, (s0 ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d0[x][0], d0[x][1]));
-        lds_st(tile, (s1 ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d0[x][2], d0[x][3]));
-        lds_st(tile, (s2 ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d1[x][0], d1[x][1]));
-        lds_st(tile, (s3 ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d1[x][2], d1[x][3]));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          lds_st(tile, ((b ^ oin[i]) ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d0[x][i], d1[x][i]));
       }
     }
   };
@@ -450,6 +457,99 @@ __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw
     const uint4 Bi = make_uint4(mul_i(lv[0]), mul_i(lv[1]), mul_i(lv[2]), mul_i(lv[3]));
     accR = mfma(A, Br, accR);
     accI = mfma(A, Bi, accI);
+  }
+}
+
+// Transposed BACK op (F_BACK_TRANS): psi_in = U^H psi_out and lambda_in = U^H lambda_out as Y^T = X^T M^T, the
+// state block as the A operand and the U^H fragments as the B operand (the fragment registers of M are the B
+// layout of M^T).  The A registers are the ones the U-as-A form reads (lane (g4, cl): column cl, amplitudes
+// 4 g4 .. 4 g4 + 3), and the result lands transposed: lane (g4, cl) holds amplitude m' = cl of columns 4 g4 + i
+// in register i, re in tile 0 and im in tile 1 (fragment rows (component, m')).  That is the operand layout of the
+// cross-matrix MFMA (K = columns), so the op's gradient cross matrix is taken at its INPUT,
+// N = sum_col psi_in lambda_in^H, from the rounded results themselves: per block 8 apply + 2 cross MFMAs and no
+// transposes (the output-side fused form needs 4 identity-MFMA transposes and their packs), and
+// hea_grad_reduce applies the input-side generators (X, and RX^H Z RX = cos(theta) Z + sin(theta) Y).  The
+// results go back amplitude-major: lane (g4, cl) writes amplitude cl of columns 4 g4 .. 4 g4 + 3, one 16-lane
+// b64 store group = 16 amplitudes of one column (the planner keeps their pair banks distinct).
+template <int NW, int TB, bool PL>
+__device__ __forceinline__ void group_back_t(uint32_t* tile, const uint4* F, const int* opw, uint32_t fo, int lane,
+                                             int wave, int nbw, f4* acc) {
+  constexpr int MAXB = (1 << (TB - 8)) / NW;
+  constexpr int SH = PL ? 2 : 3;
+  constexpr uint32_t LP = 4u * lam_word<TB>();
+  const int g4 = lane >> 4, cl = lane & 15;
+  // load address of block i, amplitude 4 g4 + j: lo[j] ^ bh[i]; store address of column 4 g4 + r: ost[r] ^ bh[i]
+  uint32_t lo[4], ost[4], bh[MAXB];
+  const uint32_t om = (uint32_t)opw[W_OFF + cl] ^ fo, bl = (uint32_t)opw[W_BL + (wave & 1) * 16 + cl] ^ fo;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    lo[j] = ((uint32_t)opw[W_OFF + 4 * g4 + j] ^ bl) << SH;
+    ost[j] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + j] ^ om) << SH;
+  }
+#pragma unroll
+  for (int i = 0; i < MAXB; ++i) bh[i] = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << SH;
+  auto load = [&](int i, uint4* X) {
+    const uint32_t b = bh[i];
+    if constexpr (PL) {
+      X[0] = make_uint4(lds_ld(tile, b ^ lo[0]), lds_ld(tile, b ^ lo[1]), lds_ld(tile, b ^ lo[2]), lds_ld(tile, b ^ lo[3]));
+      X[1] = make_uint4(lds_ld(tile, (b ^ lo[0]) + LP), lds_ld(tile, (b ^ lo[1]) + LP), lds_ld(tile, (b ^ lo[2]) + LP),
+                        lds_ld(tile, (b ^ lo[3]) + LP));
+    } else {
+      const uint2 p0 = lds_ld2(tile, b ^ lo[0]), p1 = lds_ld2(tile, b ^ lo[1]), p2 = lds_ld2(tile, b ^ lo[2]),
+                  p3 = lds_ld2(tile, b ^ lo[3]);
+      X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
+      X[1] = make_uint4(p0.y, p1.y, p2.y, p3.y);
+    }
+  };
+  auto compute_store = [&](int i, const uint4* X) {
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    f4 pr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[0]), z, 0, 0, 0);
+    f4 pi = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[1]), z, 0, 0, 0);
+    f4 lr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[0]), z, 0, 0, 0);
+    f4 li = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[1]), z, 0, 0, 0);
+    pr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[2]), pr, 0, 0, 0);
+    pi = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[3]), pi, 0, 0, 0);
+    lr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[2]), lr, 0, 0, 0);
+    li = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[3]), li, 0, 0, 0);
+    // (re, im) of amplitude cl, columns 4 g4 + r: the stored values, the cross matrix's A (psi) and B (lambda,
+    // i lambda = (-im, re): exactly i times the rounded lambda, rounding is sign symmetric)
+    const uint4 P = make_uint4(pack_h2(pr[0], pi[0]), pack_h2(pr[1], pi[1]), pack_h2(pr[2], pi[2]), pack_h2(pr[3], pi[3]));
+    const uint4 Lr = make_uint4(pack_h2(lr[0], li[0]), pack_h2(lr[1], li[1]), pack_h2(lr[2], li[2]), pack_h2(lr[3], li[3]));
+    const uint4 Li = make_uint4(mul_i(Lr.x), mul_i(Lr.y), mul_i(Lr.z), mul_i(Lr.w));
+    acc[0] = mfma(P, Lr, acc[0]);
+    acc[1] = mfma(P, Li, acc[1]);
+    const uint32_t bb = bh[i];
+    const uint32_t* Pw = (const uint32_t*)&P;
+    const uint32_t* Lw = (const uint32_t*)&Lr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t ad = ost[r] ^ bb;
+      if constexpr (PL) {
+        lds_st(tile, ad, Pw[r]);
+        lds_st(tile, ad + LP, Lw[r]);
+      } else {
+        // psi and lambda words from two unpaired registers in one ds_write2_b32 (a b64 store needs them
+        // adjacent, and the cross-matrix operands need each of psi and lambda in four adjacent registers: the
+        // compiler merges two dword stores into a b64 with two v_movs).  Issued as asm, the store is unknown
+        // to the wait-count pass; LDS operations complete in order, so its waits only become conservative.
+        const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)((char*)tile + ad);
+        __asm__ volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(Pw[r]), "v"(Lw[r]) : "memory");
+      }
+    }
+  };
+  // one block at a time with the next block's reads in flight (four independent MFMA chains per block; a pair of
+  // blocks plus the next pair's operands pushed the kernel past 128 VGPRs into spills)
+  if (nbw <= 0) return;
+  uint4 Bc[2];
+  load(0, Bc);
+#pragma unroll
+  for (int i = 0; i < MAXB; ++i) {
+    if (i >= nbw) break;
+    uint4 Bn[2];
+    if (i + 1 < MAXB && i + 1 < nbw) load(i + 1 < MAXB ? i + 1 : 0, Bn);
+    compute_store(i, Bc);
+    Bc[0] = Bn[0];
+    Bc[1] = Bn[1];
   }
 }
 
@@ -1136,18 +1236,6 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   };
 
   // ---------------------------------------------------------------- op list
-  // identity fragments (rows: re of amplitude n, then im) for the fused cross-matrix transposes (FUSE)
-  uint4 IRE = {}, IIM = {};
-  if constexpr (FUSE) {
-    const int n = lane & 15, g4 = lane >> 4;
-    uint32_t* re = (uint32_t*)&IRE;
-    uint32_t* im = (uint32_t*)&IIM;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      re[j] = n == 4 * g4 + j ? 0x00003C00u : 0u;
-      im[j] = n == 4 * g4 + j ? 0x3C000000u : 0u;
-    }
-  }
   const int ncol = T >> 4, nblk = ncol >> 4;
   // FULL (t == TB): every wave owns exactly (2^(TB - 8)) / NW column blocks - a compile-time count, so the block
   // loops of the group ops carry no bounds checks or branches
@@ -1206,12 +1294,15 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
     } else if (code == OP_BACK || code == OP_GRAD || code == OP_GRAD_L1) {
       const uint32_t fo = fo_s[o];
       f4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      if (FUSE && code == OP_BACK) {
+      if (code == OP_BACK && (opw[W_FLAGS] & F_BACK_TRANS)) {
+        // U^H on psi and lambda, cross matrix at the op input from the results (hea_grad_reduce: input side)
+        group_back_t<NW, TB, PL>(tile, F, opw, fo, lane, wave, nbw, acc2);
+      } else if (FUSE && code == OP_BACK) {
         // cross matrix from the apply's own registers (one pass over the blocks, no group_cross reads)
         if (opw[W_FLAGS] & F_BACK_PSI)
-          group_apply<2, NW, true, 0, TB, PL, FUSE>(tile, F, opw, fo, lane, wave, nbw, acc2, IRE, IIM);
+          group_apply<2, NW, true, 0, TB, PL, FUSE>(tile, F, opw, fo, lane, wave, nbw, acc2);
         else
-          group_apply<1, NW, true, 1, TB, PL, FUSE>(tile, F, opw, fo, lane, wave, nbw, acc2, IRE, IIM);
+          group_apply<1, NW, true, 1, TB, PL, FUSE>(tile, F, opw, fo, lane, wave, nbw, acc2);
       } else {
         if (!(QFX_HEA_ABLATE && (a.ablate & 4))) group_cross<NW, TB, PL>(tile, opw, fo, lane, wave, nbw, acc2[0], acc2[1]);
         if (code == OP_BACK && !(QFX_HEA_ABLATE && (a.ablate & 8))) {
@@ -1263,6 +1354,8 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
 
 // Unitary fragments: per (client, slot) U and U^H in the real 32 x 32 embedding, laid out as the MFMA
 // A operand of v_mfma_f32_16x16x32_f16 (lane l: row 16h + (l & 15), k = 8 (l >> 4) .. +7), hi and lo fp16.
+// Rows are ordered (component, amplitude): row 16 h + m' is the re (h = 0) or im (h = 1) part of output m'.
+// The same registers are the B operand of the transposed product X^T M^T (group_back_t).
 // frags[((k * n_slots + slot) * 4 + f) * 128 + h * 64 + lane], f = 0 U hi, 1 U lo, 2 U^H hi, 3 U^H lo.
 __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__ params, int p_stride,
                                                        const int* __restrict__ slot_tab, int n_slots,
@@ -1290,11 +1383,12 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
       u[j][1][1] = make_float2(1.f, 0.f);
     }
   }
-  const int r = 16 * h + (lane & 15);
+  // real output row r = 16 h + (lane & 15) is component cr = h (0 re, 1 im) of amplitude m' = lane & 15: a block's
+  // result then holds the re and im of one amplitude in the same register of its two 16-row tiles
   _Float16 hi[8], lo[8];
   for (int jj = 0; jj < 8; ++jj) {
     const int kk = 8 * (lane >> 4) + jj;
-    const int mp = r >> 1, cr = r & 1, m = kk >> 1, ck = kk & 1;
+    const int mp = lane & 15, cr = h, m = kk >> 1, ck = kk & 1;
     const int row = dag ? m : mp, colm = dag ? mp : m;   // U^H[mp][m] = conj(U[m][mp])
     float2 v = make_float2(1.f, 0.f);
     for (int j = 0; j < 4; ++j) v = cmul(v, u[j][(row >> j) & 1][(colm >> j) & 1]);
@@ -1327,7 +1421,8 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
   const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
   const int* m = gmeta + g * 10;
-  const int nt = m[0], nreal = m[1];
+  // m[1]: nreal in bits 0..3; bit 4 = cross matrix taken at the op INPUT (transposed BACK ops)
+  const int nt = m[0], nreal = m[1] & 15, inside = (m[1] >> 4) & 1;
   const int R = spc * nt;
   __shared__ long long part[8][32];
   __shared__ double pt[32];
@@ -1355,10 +1450,19 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   if (tid < nreal) {
     const double* p = pt + 8 * tid;
     const float* prm = params + (size_t)k * p_stride;
-    const double ph = prm[m[6 + tid]];
-    const double cp = cos(ph), sp = sin(ph);
-    grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
-    grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
+    if (inside) {
+      // at the op input: d/dtheta = Im<lam|X|psi> = Im(n01 + n10);
+      // d/dphi = Im<lam|RX^H Z RX|psi> = cos(theta) Im(n00 - n11) + sin(theta) Re(n01 - n10)
+      const double th = prm[m[2 + tid]];
+      const double ct = cos(th), st = sin(th);
+      grad[(size_t)k * p_stride + m[2 + tid]] = (float)(p[3] + p[5]);
+      grad[(size_t)k * p_stride + m[6 + tid]] = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
+    } else {
+      const double ph = prm[m[6 + tid]];
+      const double cp = cos(ph), sp = sin(ph);
+      grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
+      grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
+    }
   }
 }
 

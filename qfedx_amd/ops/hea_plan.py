@@ -49,6 +49,7 @@ OP_APPLY, OP_UNAPPLY_PSI, OP_UNAPPLY_LAM, OP_GRAD, OP_GRAD_L1, OP_OBS, OP_READOU
 OP_WORDS = 128
 W_CODE, W_SLOT, W_NREAL, W_FLAGS, W_RFULL, W_RT, W_TH, W_PH, W_OFF, W_BL, W_BH = 0, 1, 2, 3, 4, 8, 12, 16, 20, 36, 68
 F_BACK_PSI = 1             # OP_BACK also un-applies the group on psi (still needed further back)
+F_BACK_TRANS = 2           # OP_BACK (with F_BACK_PSI) in the transposed form: cross matrix at the op input
 W_GIDX = 100               # gradient ops: global index of the op's partial-trace record in the slab
 MAX_CLASSES = 8
 BANK_BITS = 5              # ds_read_b32 / ds_write_b32: bank = dword address % 32 per 32-lane half
@@ -455,19 +456,23 @@ def _group_geom(plan: HEAPlan, p: Pass, g: Group):
 FULL_SCORE = 4
 
 
-def _best_cols(H, allv, dirs):
+def _best_cols(H, allv, dirs, stores: bool = True):
     """(score, (c0, c1, c2, c3)): column bits maximising conflict-free access patterns (FULL_SCORE = all):
-    apply reads, forward b32 apply writes, cross-matrix reads, and the adjoint's ds_write_b64 pair stores,
-    whose lane groups are 16 contiguous lanes (one row, 16 columns) with bank (byte / 4) mod 32, i.e. the
-    16 columns need distinct swizzled pair indices mod 16."""
+    apply reads and writes (a lane writes the amplitudes it read: columns x m-bit 2 per 32-lane half),
+    cross-matrix reads, the ds_write_b64 pair stores of the U-as-A form, whose lane groups are 16 contiguous
+    lanes (one amplitude, 16 columns) with bank (byte / 4) mod 32, i.e. the 16 columns need distinct swizzled
+    pair indices mod 16, and the transposed BACK's pair stores (16 amplitudes of one column: the group vectors'
+    pair indices mod 16 independent; a property of H alone; ``stores=False`` for the layer-1 gradient groups, whose
+    ops only read)."""
     bv = [_bank(H, v) for v in allv]
     bd = {b: _bank(H, d) for b, d in dirs.items()}
     best = (-1, None)
     import itertools
+    st = int(_rank([x & 15 for x in bv]) == 4) if stores else 1
     for combo in itertools.combinations(sorted(dirs), 4):
         cb = [bd[b] for b in combo]
         sa = int(_rank(cb + [bv[2]]) == 5)
-        sw = int(_rank(cb + [bv[1]]) == 5)
+        sw = st
         s16 = int(_rank([x & 15 for x in cb]) == 4)
         for c2 in combo:
             sg = int(_rank(bv + [bd[c2]]) == 5)
@@ -490,8 +495,8 @@ def layout_pass(plan: HEAPlan, p: Pass, seed: int = 0, tries: int = 48) -> None:
     for i in range(tries):
         H = [0] * BANK_BITS if i == 0 else [int(x) for x in rng.integers(0, 1 << hb, BANK_BITS)] if hb else [0] * 5
         cols, score = [], 0
-        for allv, _, _, _, _, _, dirs in geoms:
-            sc, c = _best_cols(H, allv, dirs)
+        for gi, (allv, _, _, _, _, _, dirs) in enumerate(geoms):
+            sc, c = _best_cols(H, allv, dirs, gi < len(p.groups))
             cols.append(c)
             score += sc
         if best is None or score > best[0]:
@@ -557,12 +562,21 @@ def obs_table(plan: HEAPlan, p: Pass, code: int) -> np.ndarray:
     return w
 
 
-def pass_programs(plan: HEAPlan, meta: list | None = None, recompute_last: bool = False):
+def _trans_default() -> bool:
+    """Transposed BACK ops (``F_BACK_TRANS``, kernel ``group_back_t``): on unless QFEDX_HEA_TRANS=0 (A/B)."""
+    return os.environ.get("QFEDX_HEA_TRANS", "1") != "0"
+
+
+def pass_programs(plan: HEAPlan, meta: list | None = None, recompute_last: bool = False, trans: bool | None = None):
     """Forward and adjoint op lists per pass: list of (Pass, fwd_ops [k, OP_WORDS], adj_ops).  ``meta``
     (optional list) receives one row per gradient op: [tiles of its pass, nreal, theta slots x4, phi slots x4].
     ``recompute_last``: the last pass's adjoint starts from that pass's INPUT and re-applies its groups in-tile
     before the observable op, so the forward's last pass never stores its output (one state write and read of
-    HBM per sample saved for a few in-tile group ops)."""
+    HBM per sample saved for a few in-tile group ops).  ``trans``: BACK ops that un-apply psi too run transposed
+    (``F_BACK_TRANS``): their cross matrix is taken at the op input, flagged for hea_grad_reduce by bit 4 of the
+    meta row's nreal word."""
+    if trans is None:
+        trans = _trans_default()
     out = []
     gidx = [0]
     gmeta = meta if meta is not None else []
@@ -582,13 +596,15 @@ def pass_programs(plan: HEAPlan, meta: list | None = None, recompute_last: bool 
         for i, g in enumerate(rev):
             # gradient cross matrix + U^H on lambda (and on psi while it is still needed further back)
             psi_needed = i < len(rev) - 1 or bool(p.l1)
-            adj.append(group_table(plan, p, g, OP_BACK, F_BACK_PSI if psi_needed else 0))
+            flags = (F_BACK_PSI | (F_BACK_TRANS if trans else 0)) if psi_needed else 0
+            adj.append(group_table(plan, p, g, OP_BACK, flags))
         for g in p.l1:
             adj.append(group_table(plan, p, g, OP_GRAD_L1))
         for w in adj:
             if w[W_CODE] in (OP_BACK, OP_GRAD, OP_GRAD_L1):
                 w[W_GIDX] = gidx[0]
-                gmeta.append([1 << (plan.n - p.t), int(w[W_NREAL])] + [int(v) for v in w[W_TH:W_TH + 4]] +
+                inside = 16 if (int(w[W_CODE]) == OP_BACK and int(w[W_FLAGS]) & F_BACK_TRANS) else 0
+                gmeta.append([1 << (plan.n - p.t), int(w[W_NREAL]) | inside] + [int(v) for v in w[W_TH:W_TH + 4]] +
                              [int(v) for v in w[W_PH:W_PH + 4]])
                 gidx[0] += 1
         out.append((p, np.stack(fwd) if fwd else np.zeros((0, OP_WORDS), np.int64),
@@ -649,8 +665,10 @@ def _addr(w, t, fixed):
     return base[:, None] ^ off[None, :]
 
 
-def _grad(w, ps, lm, th, gk, gfac):
-    """Cross matrix N[b][a] = sum_col psi[b] conj(lam[a]); per qubit 2 x 2 partial trace -> d/dtheta, d/dphi."""
+def _grad(w, ps, lm, th, gk, gfac, inside: bool = False):
+    """Cross matrix N[b][a] = sum_col psi[b] conj(lam[a]); per qubit 2 x 2 partial trace -> d/dtheta, d/dphi.
+    ``inside``: psi and lambda are the op's INPUT states (transposed BACK ops): the generators are X for theta and
+    RX^H Z RX = cos(theta) Z + sin(theta) Y for phi (hea_grad_reduce_kernel)."""
     N = ps.T @ lm.conj()
     for jq in range(int(w[W_NREAL])):
         nn = np.zeros((2, 2), dtype=np.complex128)
@@ -659,6 +677,11 @@ def _grad(w, ps, lm, th, gk, gfac):
                 if ((bb ^ aa) & ~(1 << jq)) == 0:
                     nn[(bb >> jq) & 1, (aa >> jq) & 1] += N[bb, aa]
         sth, sph = int(w[W_TH + jq]), int(w[W_PH + jq])
+        if inside:
+            t = th[sth]
+            gk[sth] += (nn[0, 1] + nn[1, 0]).imag * gfac
+            gk[sph] += (np.cos(t) * (nn[0, 0] - nn[1, 1]).imag + np.sin(t) * (nn[0, 1] - nn[1, 0]).real) * gfac
+            continue
         ph = th[sph]
         gk[sth] += (np.exp(-1j * ph) * nn[1, 0] + np.exp(1j * ph) * nn[0, 1]).imag * gfac
         gk[sph] += (nn[0, 0] - nn[1, 1]).imag * gfac
@@ -759,7 +782,13 @@ def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp1
                             lm = rnd((rr @ sg) * ps)
                             continue
                         a = _addr(w, p.t, fixed)
-                        if code == OP_BACK:
+                        if code == OP_BACK and int(w[W_FLAGS]) & F_BACK_TRANS:
+                            # transposed BACK: U^H on both, cross matrix of the rounded input states
+                            Uh = Us[int(w[W_SLOT])].conj().T
+                            lm[a] = rnd((Uh @ lm[a].T).T)
+                            ps[a] = rnd((Uh @ ps[a].T).T)
+                            _grad(w, ps[a], lm[a], th, grads[k], gfac, inside=True)
+                        elif code == OP_BACK:
                             _grad(w, ps[a], lm[a], th, grads[k], gfac)
                             Uh = Us[int(w[W_SLOT])].conj().T
                             lm[a] = rnd((Uh @ lm[a].T).T)

@@ -109,9 +109,9 @@ def test_trimmed_plan_full_groups():
     for p in plan.passes:
         groups = p.groups + p.l1
         total = 0
-        for g in groups:
+        for gi, g in enumerate(groups):
             allv, dirs = hp._group_geom(plan, p, g)[0], hp._group_geom(plan, p, g)[6]
-            total += hp._best_cols(p.H, allv, dirs)[0]
+            total += hp._best_cols(p.H, allv, dirs, gi < len(p.groups))[0]
         assert total == hp.FULL_SCORE * len(groups)
 
 
