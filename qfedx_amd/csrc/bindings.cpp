@@ -72,8 +72,8 @@ int qfx_launch_adam(float* p, const float* g, float* m, float* v, const float* t
                     const float* active, int K, int P, float lr, float b1, float b2, float eps, hipStream_t st);
 int qfx_launch_sgdm(float* p, const float* g, float* buf, const float* t_in, float* t_out, const float* active,
                     int K, int P, float lr, float mu, int keep, hipStream_t st);
-int qfx_launch_host_upload(const void* host_src, void* dst, long nbytes, hipStream_t st);
-int qfx_launch_round_signal(long long* ctr, long long* host_flag, hipStream_t st);
+int qfx_launch_host_upload(const void* host_src, void* dst, long nbytes, long long* ctr, long long* host_flag,
+                           hipStream_t st);
 int qfx_launch_ps_combine(const float* f0, const float* fpi, const float* jac, const float* w, const long long* keys,
                           float p01, float p10, int shots, unsigned stream, int K, int P, int B, int C, int noisy,
                           float* out, hipStream_t st);
@@ -305,8 +305,11 @@ torch::Tensor host_alloc(int64_t nbytes, bool coherent) {
                           torch::TensorOptions().dtype(torch::kUInt8).device(torch::kCPU));
 }
 
-// dst (device, uint8) <- src (host_alloc memory, uint8) by a copy kernel that reads the host memory directly
-void host_upload(torch::Tensor src, torch::Tensor dst) {
+// dst (device, uint8) <- src (host_alloc memory, uint8) by a copy kernel that reads the host memory directly.
+// Optional round signal (ctr: device int64 [2] = round counter + block arrival count, zero-initialised; flag: coherent
+// host_alloc memory holding one int64): the kernel's last block bumps ctr[0] and publishes it to flag.
+void host_upload(torch::Tensor src, torch::Tensor dst, c10::optional<torch::Tensor> ctr,
+                 c10::optional<torch::Tensor> flag) {
   if (src.device().is_cuda()) throw std::invalid_argument("host_upload: src must be host memory from host_alloc");
   if (!dst.device().is_cuda()) throw std::invalid_argument("host_upload: dst must be a device tensor");
   if (src.scalar_type() != torch::kUInt8 || dst.scalar_type() != torch::kUInt8 || !src.is_contiguous() ||
@@ -314,7 +317,17 @@ void host_upload(torch::Tensor src, torch::Tensor dst) {
     throw std::invalid_argument("host_upload: contiguous uint8 tensors expected");
   const int64_t n = src.numel();
   if (dst.numel() < n || n % 16) throw std::invalid_argument("host_upload: size (16-byte multiple, dst >= src)");
-  check(qfx_launch_host_upload(src.data_ptr(), dst.data_ptr(), (long)n, cur_stream()), "qfx_host_upload");
+  long long* cp = nullptr;
+  long long* fp = nullptr;
+  if (ctr && ctr->defined()) {
+    need(*ctr, torch::kInt64, "ctr");
+    if (ctr->numel() < 2) throw std::invalid_argument("host_upload: ctr needs 2 int64 words (count, arrivals)");
+    if (!flag || flag->device().is_cuda() || flag->numel() < 8 || flag->scalar_type() != torch::kUInt8)
+      throw std::invalid_argument("host_upload: flag must be >= 8 bytes of host_alloc memory");
+    cp = ptr<long long>(*ctr);
+    fp = (long long*)flag->data_ptr();
+  }
+  check(qfx_launch_host_upload(src.data_ptr(), dst.data_ptr(), (long)n, cp, fp, cur_stream()), "qfx_host_upload");
 }
 
 // f0 [K,B,C], fpi [K,P,B,C] (empty: no mean term), jac [K,B,C,P], w [K,B,C], keys [K,2] int64 (shots > 0) -> out [K,P]
@@ -341,14 +354,6 @@ void ps_combine(torch::Tensor f0, torch::Tensor fpi, torch::Tensor jac, torch::T
                               (int)shots, (unsigned)stream, (int)K, (int)P, (int)B, (int)C, (int)noisy,
                               ptr<float>(out), cur_stream()),
         "qfx_ps_combine");
-}
-
-// ctr: device int64 [1] (the graph entry's round counter); flag: coherent host_alloc memory holding one int64
-void round_signal(torch::Tensor ctr, torch::Tensor flag) {
-  need(ctr, torch::kInt64, "ctr");
-  if (flag.device().is_cuda() || flag.numel() < 8 || flag.scalar_type() != torch::kUInt8)
-    throw std::invalid_argument("round_signal: flag must be >= 8 bytes of host_alloc memory");
-  check(qfx_launch_round_signal(ptr<long long>(ctr), (long long*)flag.data_ptr(), cur_stream()), "qfx_round_signal");
 }
 
 void round_init(torch::Tensor theta, torch::Tensor params, c10::optional<torch::Tensor> m,
@@ -587,9 +592,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("amp_init", &amp_init);
   m.def("round_init", &round_init);
   m.def("host_alloc", &host_alloc, py::arg("nbytes"), py::arg("coherent") = false);
-  m.def("round_signal", &round_signal);
   m.def("ps_combine", &ps_combine);
-  m.def("host_upload", &host_upload);
+  m.def("host_upload", &host_upload, py::arg("src"), py::arg("dst"), py::arg("ctr") = py::none(),
+        py::arg("flag") = py::none());
   m.def("batch_plan", &qfx_runtime::batch_plan);
   m.def("batch_gather", &batch_gather);
   m.def("round_prologue", &round_prologue);

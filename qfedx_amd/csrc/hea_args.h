@@ -31,3 +31,15 @@ struct HeaPassArgs {
   int pair;                  // forward: two samples per workgroup on 2^13 tiles (hea_fwd2_kernel)
   int ablate;                // timing ablations (builds with QFX_HEA_ABLATE only; QFEDX_HEA_ABLATE bit mask)
 };
+
+// Launch arguments of a fused Adam epilogue (m == nullptr: none).  cnt: one zero-initialised arrival counter per
+// client (the client's last block resets it).
+struct QfxAdamArgs {
+  float* m;
+  float* v;
+  const float* t_in;
+  float* t_out;
+  const float* active;
+  unsigned* cnt;
+  float lr, b1, b2, eps;
+};

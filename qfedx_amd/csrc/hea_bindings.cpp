@@ -17,7 +17,7 @@ int qfx_hea_pass(int adjoint, const HeaPassArgs* args, int n_samples, hipStream_
 int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                   hipStream_t st);
 int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc, int K,
-                        const float* params, float* grad, int p_stride, hipStream_t st);
+                        float* params, float* grad, int p_stride, const QfxAdamArgs* adam, hipStream_t st);
 int qfx_hea_args_size();
 int qfx_hea_check_status(hipStream_t st);
 }
@@ -171,12 +171,29 @@ void hea_frags(torch::Tensor params, int64_t p_stride, torch::Tensor slot_tab, i
         "qfx_hea_frags");
 }
 
+// adam: optional (m, v, t_in, t_out, active, cnt) device tensors [K, P] / [K] (cnt int32, zero-initialised) and
+// lr, b1, b2, eps: the clients' Adam step fused into the reduction (the last block of each client updates its row)
 void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops, torch::Tensor gmeta, int64_t spc,
-                     int64_t K, torch::Tensor params, torch::Tensor grad, int64_t p_stride) {
+                     int64_t K, torch::Tensor params, torch::Tensor grad, int64_t p_stride,
+                     c10::optional<std::vector<torch::Tensor>> adam, c10::optional<std::vector<double>> hyper) {
+  QfxAdamArgs ad{};
+  if (adam && !adam->empty()) {
+    const auto& a = *adam;
+    need(a.size() == 6 && hyper && hyper->size() == 4, "grad_reduce: adam = (m, v, t_in, t_out, active, cnt), hyper = (lr, b1, b2, eps)");
+    need(params.size(1) == p_stride && params.is_contiguous(), "grad_reduce: fused Adam needs contiguous [K, P] params");
+    ad.m = dp<float>(a[0], torch::kFloat32, "m", K * p_stride);
+    ad.v = dp<float>(a[1], torch::kFloat32, "v", K * p_stride);
+    ad.t_in = dp<float>(a[2], torch::kFloat32, "t_in", K);
+    ad.t_out = dp<float>(a[3], torch::kFloat32, "t_out", K);
+    ad.active = dp<float>(a[4], torch::kFloat32, "active", K);
+    ad.cnt = dp<unsigned>(a[5], torch::kInt32, "cnt", K);
+    ad.lr = (float)(*hyper)[0], ad.b1 = (float)(*hyper)[1], ad.b2 = (float)(*hyper)[2], ad.eps = (float)(*hyper)[3];
+    need(n_gradops > 0, "grad_reduce: fused Adam needs at least one gradient op");
+  }
   check(qfx_hea_grad_reduce(dp<long long>(gslab, torch::kInt64, "gslab", K * spc * slab_tiles * n_gradops * 32),
                             (int)slab_tiles, (int)n_gradops, dp<int>(gmeta, torch::kInt32, "gmeta", n_gradops * 10),
                             (int)spc, (int)K, dp<float>(params, torch::kFloat32, "params", K * p_stride),
-                            dp<float>(grad, torch::kFloat32, "grad", K * p_stride), (int)p_stride, cur()),
+                            dp<float>(grad, torch::kFloat32, "grad", K * p_stride), (int)p_stride, &ad, cur()),
         "qfx_hea_grad_reduce");
 }
 
@@ -186,7 +203,10 @@ void register_hea(pybind11::module& m) {
   m.def("hea_pass", &hea_pass);
   m.def("hea_frags", &hea_frags);
   m.def("hea_check_ops", &hea_check_ops);
-  m.def("hea_grad_reduce", &hea_grad_reduce);
+  m.def("hea_grad_reduce", &hea_grad_reduce, pybind11::arg("gslab"), pybind11::arg("slab_tiles"),
+        pybind11::arg("n_gradops"), pybind11::arg("gmeta"), pybind11::arg("spc"), pybind11::arg("K"),
+        pybind11::arg("params"), pybind11::arg("grad"), pybind11::arg("p_stride"),
+        pybind11::arg("adam") = pybind11::none(), pybind11::arg("hyper") = pybind11::none());
   m.def("hea_args_size", []() { return qfx_hea_args_size(); });
   // -1: release build (no device checks); 0: no failure since the last read; else the failing source line
   m.def("hea_check_status", []() { return qfx_hea_check_status(cur()); });

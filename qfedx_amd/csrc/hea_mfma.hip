@@ -23,6 +23,7 @@
 #include <cstdlib>
 
 #include "hea_args.h"
+#include "qfx_adam.h"
 #include "qfx_check.h"
 
 #if QFX_CHECKS_ON
@@ -35,6 +36,11 @@ __device__ unsigned int qfx_check_word = 0;
 // release builds compile the checks out.
 #ifndef QFX_HEA_ABLATE
 #define QFX_HEA_ABLATE 0
+#endif
+// Gate precision: 1 (default) applies every unitary as its fp16 hi + lo halves (exact to ~2^-22), 0 as the hi half
+// only (fp16-rounded gate: half the apply MFMAs).
+#ifndef QFX_HEA_GATE_LO
+#define QFX_HEA_GATE_LO 1
 #endif
 
 namespace hea {
@@ -237,7 +243,7 @@ __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, c
 }
 
 // RZ(ph) RX(th) F(x)|0> for a layer-1 qubit
-__device__ void l1_factor(float x, float th, float ph, int feature, float2* w) {
+__device__ __forceinline__ void l1_factor(float x, float th, float ph, int feature, float2* w) {
   float sa, ca;
   __sincosf(0.5f * x, &sa, &ca);
   float2 v0, v1;
@@ -374,8 +380,10 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
     for (int x = 0; x < NX; ++x) {
       d0[x] = mfma(F[0], X[x], z);
       d1[x] = mfma(F[1], X[x], z);
-      d0[x] = mfma(F[2], X[x], d0[x]);
-      d1[x] = mfma(F[3], X[x], d1[x]);
+      if (QFX_HEA_GATE_LO) {
+        d0[x] = mfma(F[2], X[x], d0[x]);
+        d1[x] = mfma(F[3], X[x], d1[x]);
+      }
     }
     // output amplitude 4 g4 + i = (tile 0, tile 1) register i, written where it was read
     if constexpr (PAIR && NX == 2) {
@@ -507,10 +515,12 @@ __device__ __forceinline__ void group_back_t(uint32_t* tile, const uint4* F, con
     f4 pi = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[1]), z, 0, 0, 0);
     f4 lr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[0]), z, 0, 0, 0);
     f4 li = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[1]), z, 0, 0, 0);
-    pr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[2]), pr, 0, 0, 0);
-    pi = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[3]), pi, 0, 0, 0);
-    lr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[2]), lr, 0, 0, 0);
-    li = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[3]), li, 0, 0, 0);
+    if (QFX_HEA_GATE_LO) {
+      pr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[2]), pr, 0, 0, 0);
+      pi = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[3]), pi, 0, 0, 0);
+      lr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[2]), lr, 0, 0, 0);
+      li = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[3]), li, 0, 0, 0);
+    }
     // (re, im) of amplitude cl, columns 4 g4 + r: the stored values, the cross matrix's A (psi) and B (lambda,
     // i lambda = (-im, re): exactly i times the rounded lambda, rounding is sign symmetric)
     const uint4 P = make_uint4(pack_h2(pr[0], pi[0]), pack_h2(pr[1], pi[1]), pack_h2(pr[2], pi[2]), pack_h2(pr[3], pi[3]));
@@ -895,7 +905,9 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
         wv[tid][1] = w[1];
       }
       const bool outq = tid < a.n && !(tid < a.c || (tid >= a.lo && tid < a.hi));
-      float2 f = outq ? w[(fixed >> (tid & 31)) & 1] : make_float2(1.f, 0.f);
+      // value select, not w[bit]: a run-time index put w in scratch (a global round trip per workgroup)
+      const float2 w0 = w[0], w1 = w[1];
+      float2 f = outq ? (((fixed >> (tid & 31)) & 1) ? w1 : w0) : make_float2(1.f, 0.f);
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) f = cmul(f, make_float2(__shfl_xor(f.x, off, 64), __shfl_xor(f.y, off, 64)));
       if (tid == 0) outer_s = make_float2(a.scale * f.x, a.scale * f.y);
@@ -1055,7 +1067,8 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd2_kernel(PassArgs a) {
         wv[x][lane][1] = w[1];
       }
       const bool outq = lane < a.n && !(lane < a.c || (lane >= a.lo && lane < a.hi));
-      float2 f = outq ? w[(fixed >> (lane & 31)) & 1] : make_float2(1.f, 0.f);
+      const float2 w0 = w[0], w1 = w[1];
+      float2 f = outq ? (((fixed >> (lane & 31)) & 1) ? w1 : w0) : make_float2(1.f, 0.f);
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) f = cmul(f, make_float2(__shfl_xor(f.x, off, 64), __shfl_xor(f.y, off, 64)));
       if (lane == 0) outer_s[x] = make_float2(a.scale * f.x, a.scale * f.y);
@@ -1365,33 +1378,34 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
   const int* st = slot_tab + slot * 9;
   const int nreal = st[0];
   const float* prm = params + (size_t)k * p_stride;
-  float2 u[4][2][2];
+  // per qubit j: RZ(ph) RX(th) = [[e- c, -i e- s], [-i e+ s, e+ c]], e-+ = cp -+ i sp (identity past nreal)
+  float cj[4], sj[4], cpj[4], spj[4];
+#pragma unroll
   for (int j = 0; j < 4; ++j) {
+    cj[j] = 1.f, sj[j] = 0.f, cpj[j] = 1.f, spj[j] = 0.f;
     if (j < nreal) {
-      float s, c, sp, cp;
-      __sincosf(0.5f * prm[st[1 + j]], &s, &c);
-      __sincosf(0.5f * prm[st[5 + j]], &sp, &cp);
-      // RZ(ph) RX(th) = [[e- c, -i e- s], [-i e+ s, e+ c]],  e-+ = cp -+ i sp
-      u[j][0][0] = make_float2(cp * c, -sp * c);
-      u[j][0][1] = make_float2(-sp * s, -cp * s);
-      u[j][1][0] = make_float2(sp * s, -cp * s);
-      u[j][1][1] = make_float2(cp * c, sp * c);
-    } else {
-      u[j][0][0] = make_float2(1.f, 0.f);
-      u[j][0][1] = make_float2(0.f, 0.f);
-      u[j][1][0] = make_float2(0.f, 0.f);
-      u[j][1][1] = make_float2(1.f, 0.f);
+      __sincosf(0.5f * prm[st[1 + j]], &sj[j], &cj[j]);
+      __sincosf(0.5f * prm[st[5 + j]], &spj[j], &cpj[j]);
     }
   }
   // real output row r = 16 h + (lane & 15) is component cr = h (0 re, 1 im) of amplitude m' = lane & 15: a block's
   // result then holds the re and im of one amplitude in the same register of its two 16-row tiles
   _Float16 hi[8], lo[8];
+#pragma unroll
   for (int jj = 0; jj < 8; ++jj) {
     const int kk = 8 * (lane >> 4) + jj;
     const int mp = lane & 15, cr = h, m = kk >> 1, ck = kk & 1;
     const int row = dag ? m : mp, colm = dag ? mp : m;   // U^H[mp][m] = conj(U[m][mp])
     float2 v = make_float2(1.f, 0.f);
-    for (int j = 0; j < 4; ++j) v = cmul(v, u[j][(row >> j) & 1][(colm >> j) & 1]);
+    // entry (row_j, col_j) of qubit j's 2 x 2 factor, formed arithmetically (a run-time index into a table of
+    // the four entries put it in scratch): diagonal (cp c, +-sp c), off-diagonal (+-sp s, -cp s), sign + for row 1
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool rb = (row >> j) & 1, cb = (colm >> j) & 1;
+      const float e = rb ? spj[j] : -spj[j];
+      const float2 f = rb == cb ? make_float2(cpj[j] * cj[j], e * cj[j]) : make_float2(e * sj[j], -cpj[j] * sj[j]);
+      v = cmul(v, f);
+    }
     if (dag) v.y = -v.y;
     const float val = cr == 0 ? (ck == 0 ? v.x : -v.y) : (ck == 0 ? v.y : v.x);
     hi[jj] = (_Float16)val;
@@ -1400,6 +1414,7 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
   uint4 H, Lw;
   uint32_t* hp = (uint32_t*)&H;
   uint32_t* lp = (uint32_t*)&Lw;
+#pragma unroll
   for (int i = 0; i < 4; ++i) {
     half2v a2 = {hi[2 * i], hi[2 * i + 1]}, b2 = {lo[2 * i], lo[2 * i + 1]};
     hp[i] = __builtin_bit_cast(uint32_t, a2);
@@ -1413,10 +1428,16 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
 // Per client and gradient op: exact int64 sums of the 32 partial-trace slots over the client's samples and
 // the op's tiles, then per real qubit j (slots 8j + 4y + 2x + comp = n_j[y][x].(re, im))
 //   d/dtheta = Im(e^{-i phi} n10 + e^{i phi} n01),   d/dphi = Im(n00 - n11).
+//
+// Optional Adam epilogue (ad.m != nullptr; the local optimizer step fused into this launch): the last of a client's
+// n_gradops blocks to finish - arrival counter ad.cnt[k], reset by that block - updates the client's parameter row
+// from the complete gradient row (the readout-parameter entries were written by the readout launch before), with
+// the element update of qfx_adam_kernel (qfx_adam.h): bitwise the separate launch.  Every block has read its
+// parameters before it arrives.
 __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* __restrict__ gslab, int slab_tiles,
                                                               int n_gradops, const int* __restrict__ gmeta, int spc,
-                                                              const float* __restrict__ params,
-                                                              float* __restrict__ grad, int p_stride) {
+                                                              float* __restrict__ params,
+                                                              float* __restrict__ grad, int p_stride, QfxAdamArgs ad) {
   // 8 groups of 32 lanes split the client's (sample, tile) rows; 4 independent loads in flight per lane; the
   // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
   const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
@@ -1463,6 +1484,26 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
       grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
       grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
     }
+  }
+  if (!ad.m) return;
+  __shared__ int last_s;
+  // The block's gradient stores are complete in L2 after the barrier; ONE agent-scope release (thread 0) makes
+  // them visible across XCDs before the arrival.  A release is an L2 writeback on this chip: issued by every
+  // thread it made the launch 7x slower (16q x 64 clients: 13 -> 98 us).
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(&ad.cnt[k], 1u);
+    last_s = prev == (unsigned)(n_gradops - 1);
+    if (last_s) ad.cnt[k] = 0u;                       // ready for the next launch
+  }
+  __syncthreads();
+  if (!last_s) return;
+  for (int i = tid; i < p_stride; i += 256) {
+    const long e = (long)k * p_stride + i;
+    // device-coherent load: other blocks (other CUs) wrote these entries
+    const float gi = __hip_atomic_load(&grad[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    qfx_adam_elem(params, gi, ad.m, ad.v, ad.t_in, ad.t_out, ad.active, k, e, i == 0, ad.lr, ad.b1, ad.b2, ad.eps);
   }
 }
 
@@ -1522,10 +1563,14 @@ extern "C" int qfx_hea_frags(const float* params, int p_stride, const int* slot_
 }
 
 extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc,
-                                   int K, const float* params, float* grad, int p_stride, hipStream_t st) {
-  if (K == 0 || n_gradops == 0) return 0;
+                                   int K, float* params, float* grad, int p_stride, const QfxAdamArgs* adam,
+                                   hipStream_t st) {
+  if (K == 0) return 0;
+  if (n_gradops == 0) return adam && adam->m ? (int)hipErrorInvalidValue : 0;   // no block would run the epilogue
+  QfxAdamArgs ad{};
+  if (adam) ad = *adam;
   hipLaunchKernelGGL(hea::hea_grad_reduce_kernel, dim3(K, n_gradops), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
-                     gmeta, spc, params, grad, p_stride);
+                     gmeta, spc, params, grad, p_stride, ad);
   return (int)hipGetLastError();
 }
 

@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include "philox.h"
+#include "qfx_adam.h"
 #include "qfx_plan.h"
 
 namespace qfx {
@@ -255,18 +256,7 @@ __global__ void qfx_adam_kernel(float* __restrict__ p, const float* __restrict__
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)K * P) return;
   const int k = (int)(i / P);
-  const float act = active[k];
-  const float tk = t_in[k] + act;
-  if (i == (long)k * P) t_out[k] = tk;
-  if (act == 0.f) return;
-  const float gi = g[i];
-  const float mi = b1 * m[i] + (1.f - b1) * gi;
-  const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
-  m[i] = mi;
-  v[i] = vi;
-  const float mh = mi / (1.f - powf(b1, tk));
-  const float vh = vi / (1.f - powf(b2, tk));
-  p[i] -= lr * mh / (sqrtf(vh) + eps);
+  qfx_adam_elem(p, g[i], m, v, t_in, t_out, active, k, i, i == (long)k * P, lr, b1, b2, eps);
 }
 
 // torch.optim.SGD(momentum) semantics: buf = g on the first step, else mu*buf + g; p -= lr*buf
@@ -613,20 +603,6 @@ __global__ void __launch_bounds__(64) qfx_ps_combine_kernel(const float* __restr
   if (tid == 0) out[(size_t)k * P + j] = (float)red[0];
 }
 
-// Round-completion signal, the last node of a captured round: bumps the graph entry's device counter and
-// publishes it to a coherent pinned host word.  The host reuses a pinned upload buffer once the counter shows the
-// round that read it has finished - no HIP event per round (an event record between two graph launches cost ~5 us
-// of GPU idle each on this stack; scripts/graph_gap.py).  The store is RELAXED at system scope: the host needs the
-// count only (the upload kernel that read the buffer finished before this node in stream order), and a release
-// would write back the whole L2 - dirty with the round's states - before the store.
-__global__ void qfx_round_signal_kernel(long long* __restrict__ ctr, long long* host_flag) {
-  if (threadIdx.x == 0) {
-    const long long c = ctr[0] + 1;
-    ctr[0] = c;
-    __hip_atomic_store(host_flag, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
 }  // namespace qfx
 
 using namespace qfx;
@@ -640,10 +616,6 @@ extern "C" int qfx_launch_ps_combine(const float* f0, const float* fpi, const fl
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_launch_round_signal(long long* ctr, long long* host_flag, hipStream_t st) {
-  hipLaunchKernelGGL(qfx_round_signal_kernel, dim3(1), dim3(64), 0, st, ctr, host_flag);
-  return (int)hipGetLastError();
-}
 
 extern "C" int qfx_fedavg_norm_scratch(int K, int P) { return K * (1 + (P + NORM_CHUNK - 1) / NORM_CHUNK); }
 
@@ -777,12 +749,34 @@ extern "C" int qfx_launch_round_init(const float* theta, int K, int P, float* pa
 // dst[0:n16) = src[0:n16) (16-byte words) where src is pinned host memory read by the kernel itself.  A kernel
 // launch never waits on the stream, unlike a small hipMemcpyAsync issued behind a graph launch, which was seen
 // to block the host until the queue drained (the GPU then idles while the host builds the next round).
+//
+// With a signal (ctr != nullptr) the kernel is also the captured round's completion signal for the pinned buffer
+// it read: the last block to finish (arrival count in ctr[1], reset by that block for the next replay) bumps the
+// round counter ctr[0] and publishes it to the coherent pinned word host_flag.  A block's loads from src have
+// returned once its stores are issued, so the host may refill the buffer from then on; this replaces a separate
+// one-thread signal node at the end of the round (one launch fewer per round).  The store is RELAXED at system
+// scope: the host needs the count only, and a release would first write back the whole L2, dirty with the round's
+// states.  (An event record between graph launches, the alternative, cost ~5 us of GPU idle each on this stack:
+// scripts/graph_gap.py.)
 __global__ void __launch_bounds__(256) qfx_host_upload_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
-                                                              long n16) {
+                                                              long n16, long long* __restrict__ ctr,
+                                                              long long* host_flag) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) dst[i] = src[i];
+  if (!ctr) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long prev = atomicAdd((unsigned long long*)&ctr[1], 1ull);
+    if (prev == (unsigned long long)gridDim.x - 1) {
+      ctr[1] = 0;
+      const long long c = ctr[0] + 1;
+      ctr[0] = c;
+      __hip_atomic_store(host_flag, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
-extern "C" int qfx_launch_host_upload(const void* host_src, void* dst, long nbytes, hipStream_t st) {
+extern "C" int qfx_launch_host_upload(const void* host_src, void* dst, long nbytes, long long* ctr, long long* host_flag,
+                                      hipStream_t st) {
   if (nbytes <= 0) return 0;
   if (nbytes % 16) return (int)hipErrorInvalidValue;
   void* dsrc = nullptr;
@@ -791,7 +785,7 @@ extern "C" int qfx_launch_host_upload(const void* host_src, void* dst, long nbyt
   const long n16 = nbytes / 16;
   const long blocks = (n16 + 255) / 256;
   hipLaunchKernelGGL(qfx_host_upload_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, st,
-                     (const uint4*)dsrc, (uint4*)dst, n16);
+                     (const uint4*)dsrc, (uint4*)dst, n16, ctr, host_flag);
   return (int)hipGetLastError();
 }
 

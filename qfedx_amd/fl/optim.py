@@ -67,6 +67,19 @@ class BatchedOptimizer:
         self._fresh = True
         return (self.m if self.kind == "adam" else None), self.v, self._t
 
+    def fused_adam(self, params: torch.Tensor, active: torch.Tensor):
+        """Hand this step's Adam update to a kernel that fuses it (the MFMA engine's gradient reduction,
+        ``hea_grad_reduce``): returns ([m, v, t_in, t_out, active], [lr, b1, b2, eps]) and does ``step``'s
+        bookkeeping (counter ping-pong), or None when that path does not apply (not HIP Adam)."""
+        if self.kind != "adam" or self.backend != "hip" or not params.is_cuda:
+            return None
+        if not self._fresh:
+            raise RuntimeError("BatchedOptimizer(zero_init=False): call init_round() or reset() first")
+        t_in, t_out = self._t[self._phase], self._t[1 - self._phase]
+        self._phase ^= 1
+        return ([self.m, self.v, t_in, t_out, active.float().contiguous()],
+                [float(self.lr), float(self.b1), float(self.b2), float(self.eps)])
+
     @torch.no_grad()
     def step(self, params: torch.Tensor, grads: torch.Tensor, active: Optional[torch.Tensor] = None,
              last: bool = False) -> None:

@@ -32,8 +32,9 @@ _GRAPH_LRU = 6
 
 
 def _wait_rounds(ent: dict, n: int) -> None:
-    """Block until graph entry ``ent`` has completed ``n`` replays (its last node publishes the count to a coherent
-    pinned word): spins briefly, then yields; the GPU is normally far ahead of this."""
+    """Block until graph entry ``ent`` has finished the uploads of ``n`` replays (the round's first node, the upload
+    kernel, publishes the count to a coherent pinned word once every block has read its pinned buffer): spins
+    briefly, then yields; the GPU is normally far ahead of this."""
     if n <= 0:
         return
     flag = ent["flag"].view(torch.int64)
@@ -291,8 +292,9 @@ class VQCClientTrainer:
             xang = self.engine.augment(xang, traj_keys, s)
             res = self.engine.loss_and_grads(xang, yb, ws, params, method, rng_keys=(cfg.seed, round_num, s),
                                              readout_keys=ro_keys, step=s, out_loss=loss_all[s],
-                                             out_correct=correct_all[s], init=init)
-            opt.step(params, res["grad"], act_d[s])
+                                             out_correct=correct_all[s], init=init, fused_opt=(opt, act_d[s]))
+            if not res.get("opt_done", False):      # the MFMA engine runs HIP Adam inside its gradient reduction
+                opt.step(params, res["grad"], act_d[s])
         return params, loss_all, correct_all
 
     def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int,
@@ -398,8 +400,9 @@ class VQCClientTrainer:
             dv = up.to_device(dev, pack)
             ent = {"pack": pack, "dv": dv, "theta": theta_g if direct else theta_g.to(dev).float().clone(),
                    "pin": [E.host_alloc(up.nbytes), E.host_alloc(up.nbytes)], "flip": 0,
-                   # round-completion counter: device word + coherent host mirror written by the graph's last node
-                   "ctr": torch.zeros(1, dtype=torch.int64, device=dev), "flag": E.host_alloc(8, True),
+                   # upload-completion counter (round count + block arrivals) and its coherent host mirror, both
+                   # written by the graph's first node (the upload kernel's last block)
+                   "ctr": torch.zeros(2, dtype=torch.int64, device=dev), "flag": E.host_alloc(8, True),
                    "launched": 0}
             ent["flag"].zero_()
             args = (store.X, store.y, dv["lid"], ent["theta"], dv["idx"], dv["wts"], dv["act"], plan.max_steps,
@@ -426,11 +429,10 @@ class VQCClientTrainer:
                     g = torch.cuda.CUDAGraph()
                     try:
                         with torch.cuda.graph(g):
-                            E.host_upload(ent["pin"][v][: up.nbytes], pack)
+                            E.host_upload(ent["pin"][v][: up.nbytes], pack, ent["ctr"], ent["flag"])
                             out = body()
                             if ent["post_in_graph"]:
                                 post(v)
-                            E.round_signal(ent["ctr"], ent["flag"])
                     except Exception:
                         if not ent["post_in_graph"]:
                             raise
@@ -442,9 +444,8 @@ class VQCClientTrainer:
                         for v2 in range(2):
                             g = torch.cuda.CUDAGraph()
                             with torch.cuda.graph(g):
-                                E.host_upload(ent["pin"][v2][: up.nbytes], pack)
+                                E.host_upload(ent["pin"][v2][: up.nbytes], pack, ent["ctr"], ent["flag"])
                                 out = body()
-                                E.round_signal(ent["ctr"], ent["flag"])
                             ent["graphs"].append(g)
                             ent["out"].append(out)
                         break
@@ -452,7 +453,10 @@ class VQCClientTrainer:
                     ent["out"].append(out)
             while len(cache) >= _GRAPH_LRU:         # LRU: drop the oldest shape
                 old = cache.pop(next(iter(cache)))
-                _wait_rounds(old, old["launched"])   # its replays are done with their pinned buffers
+                # the counter only says its uploads are done: drain the device before the graph and its
+                # workspaces are released (rare: more live shapes than the LRU holds)
+                _wait_rounds(old, old["launched"])
+                torch.cuda.current_stream(dev).synchronize()
         cache[key] = ent                            # most recently used last
         if not direct:
             ent["theta"].copy_(theta_g.float())

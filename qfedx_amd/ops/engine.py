@@ -169,14 +169,20 @@ class VQCEngine:
                        params: torch.Tensor, method: str = "adjoint", spsa_c: float = 0.1,
                        rng_keys: tuple = (0,), readout_keys: Optional[torch.Tensor] = None,
                        step: int = 0, out_loss: Optional[torch.Tensor] = None,
-                       out_correct: Optional[torch.Tensor] = None, init: Optional[torch.Tensor] = None) -> dict:
+                       out_correct: Optional[torch.Tensor] = None, init: Optional[torch.Tensor] = None,
+                       fused_opt=None) -> dict:
         """Loss [K], gradient [K,P], correct [K] for [K,B] minibatches.  ``out_loss`` / ``out_correct``
         (optional [K] views, e.g. rows of a round buffer) receive the loss / hit counts in place.
-        ``init`` = raw amplitudes [K,B,F<=2^n] or complex states (amplitude encoding; None otherwise)."""
+        ``init`` = raw amplitudes [K,B,F<=2^n] or complex states (amplitude encoding; None otherwise).
+        ``fused_opt`` = (BatchedOptimizer, active [K]): an engine that can fuse the local optimizer step into its
+        own launches (the MFMA engine: HIP Adam in the gradient reduction) does so and returns ``opt_done``."""
         spec = self.spec
         self._check(xang, init)
         if self.backend == "hip" and method == "adjoint":
             nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
+            if fused_opt is not None and getattr(self.hip, "fuses_optimizer", False):
+                return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step, out_loss,
+                                               out_correct, init, fused_opt=fused_opt)
             return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step, out_loss,
                                            out_correct, init)
         res = self._loss_and_grads(xang, y, wmask, params, method, spsa_c, rng_keys, readout_keys, step, init)

@@ -165,6 +165,15 @@ class HeaMfmaProgram:
         finally:
             self._ws = saved
 
+    def _zbuf(self, name: str, numel: int, dtype) -> torch.Tensor:
+        """Workspace that is zero when created (e.g. arrival counters that their kernel resets after use): created
+        outside graph capture (the capture's warm-up run), so no fill is ever captured."""
+        t = self._ws.get(name)
+        if t is None or t.numel() < numel or t.dtype != dtype:
+            t = torch.zeros(numel, dtype=dtype, device=self.device)
+            self._ws[name] = t
+        return t[:numel]
+
     def _buf(self, name: str, numel: int, dtype) -> torch.Tensor:
         t = self._ws.get(name)
         if t is None or t.numel() < numel or t.dtype != dtype:
@@ -491,8 +500,13 @@ class HeaMfmaProgram:
             streams.append(torch.cuda.Stream(device=self.device))
         return streams[i]
 
-    def _step(self, x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, tag="", after_first=None):
-        """Forward, readout + CE, adjoint and gradient reduction of clients [0, K) of the given row slices."""
+    fuses_optimizer = True    # VQCEngine: loss_and_grads(fused_opt=...) may run the Adam step in the reduction
+
+    def _step(self, x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, tag="", after_first=None,
+              adam=None):
+        """Forward, readout + CE, adjoint and gradient reduction of clients [0, K) of the given row slices.
+        ``adam`` = (tensors, hyper) from ``BatchedOptimizer.fused_adam``: the clients' Adam step runs in the
+        gradient reduction's epilogue (one launch fewer per local step)."""
         C = ext()
         S = K * B
         fr = self._frags(p, K, tag)
@@ -508,15 +522,23 @@ class HeaMfmaProgram:
             C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss, correct,
                          grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
         self._adjoint(x, p, fr, K, B, stored, wread, gslab, tag)
-        C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1])
+        if adam is None:
+            C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1])
+        else:
+            cnt = self._zbuf(f"{tag}adamcnt", K, torch.int32)
+            C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1],
+                              adam[0] + [cnt], adam[1])
 
     def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
-                       out_correct=None, init: torch.Tensor | None = None) -> dict:
+                       out_correct=None, init: torch.Tensor | None = None, fused_opt=None) -> dict:
         """One adjoint training step (same contract as ``HipProgram.loss_and_grads``).
 
         Clients are independent within a step, so the step runs as ``_chunks`` client chunks on staggered
         streams (fork/join events; captured into the round's hipGraph as parallel branches).  Every chunk
-        writes only its own client rows, so results are bitwise those of one chunk."""
+        writes only its own client rows, so results are bitwise those of one chunk.
+        ``fused_opt`` = (BatchedOptimizer, active): on one chunk, with params updated in place (a contiguous fp32
+        tensor) and HIP Adam, the optimizer step runs in the gradient reduction's epilogue and the result says
+        ``opt_done``; otherwise the caller steps the optimizer itself."""
         if init is not None:
             raise ValueError("the MFMA engine starts from the angle feature map (no initial states)")
         x, p, K, B = self._prep(xang, params)
@@ -528,8 +550,12 @@ class HeaMfmaProgram:
         correct = torch.empty(K, dtype=torch.float32, device=self.device) if out_correct is None else out_correct
         grad = torch.empty_like(p)
         n = self._chunks(K, B) if noise is None else 1
+        adam = None
+        if (fused_opt is not None and n == 1 and self.n_gradops > 0 and p.data_ptr() == params.data_ptr()
+                and os.environ.get("QFEDX_FUSED_ADAM", "1") != "0"):
+            adam = fused_opt[0].fused_adam(p, fused_opt[1])
         if n == 1:
-            self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step)
+            self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=adam)
         else:
             bounds = [(i * K) // n for i in range(n + 1)]
             cur = torch.cuda.current_stream(self.device)
@@ -568,4 +594,7 @@ class HeaMfmaProgram:
                         t.record_stream(st)
             for i in range(n - 1):
                 cur.wait_stream(self._stream(i))
-        return {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}
+        res = {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}
+        if adam is not None:
+            res["opt_done"] = True
+        return res

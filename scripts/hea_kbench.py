@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--clients", type=int, default=64)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--precision", action="store_true", help="also report errors against the fp32 VALU engine")
     args = ap.parse_args()
     import torch
     from qfedx_amd.models.vqc import VQCSpec
@@ -99,6 +100,23 @@ def main():
     grad = torch.zeros(K, params.shape[1], device=dev)
     timeit(lambda: C.hea_grad_reduce(gslab, prog.slab_tiles, prog.n_gradops, prog.gmeta, B, K, params, grad,
                                      params.shape[1]), "grad_reduce", 0)
+    if args.precision:
+        # max |error| of <Z> and of the gradient against the fp32 VALU engine (as bench.py's precision fields)
+        from qfedx_amd.ops.engine import VQCEngine
+        from qfedx_amd.ops.statevec_hip import HipProgram
+        eng = VQCEngine(spec, dev, "hip", "mfma")
+        kp = min(K, 16)
+        xang = spec.encode_features(x[:kp].float())
+        th = params[:kp, : spec.n_theta].float().contiguous()
+        wp = (torch.randn(kp * B, spec.n_classes, generator=g) / B).to(dev)
+        z_m, g_m = eng.hip.vjp(xang, th, wp)
+        ref = HipProgram(eng.ops, eng.coef, spec.n_qubits, spec.readout, dev, n_theta=spec.n_theta,
+                         state_dtype="fp32", jit=False, x_width=spec.x_width)
+        z_r, g_r = ref.vjp(xang, th, wp)
+        res["max_abs_err_expz"] = float((z_m - z_r).abs().max())
+        res["max_abs_err_grad"] = float((g_m - g_r).abs().max())
+        res["rms_err_expz"] = float((z_m - z_r).pow(2).mean().sqrt())
+        res["rms_err_grad"] = float((g_m - g_r).pow(2).mean().sqrt())
     print(json.dumps(res), flush=True)
 
 

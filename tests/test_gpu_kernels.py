@@ -425,3 +425,41 @@ def test_dp_client_norms_ride_in_round_buffer(cuda):
     for key in ("norm_p10", "norm_p50", "norm_p90"):
         assert abs(hc[key] - hg[key]) < 1e-3 * max(1.0, hc[key]), (key, hc[key], hg[key])
     assert all(0.0 <= h["clip_frac"] <= 1.0 for h in gpu["history"])
+
+
+def test_fused_adam_in_grad_reduce_bitwise(cuda):
+    """MFMA engine: the Adam step fused into hea_grad_reduce (the client's last block updates its row) gives bitwise
+    the parameters, moments and step counters of the separate qfx_adam launch, over several steps with clients that
+    drop out (active 0: row untouched, counter unchanged)."""
+    from qfedx_amd.fl.optim import BatchedOptimizer
+    from qfedx_amd.models.vqc import VQCSpec
+    from qfedx_amd.ops.engine import VQCEngine
+    spec = VQCSpec(n_qubits=12, n_layers=2, n_classes=3)
+    eng = VQCEngine(spec, cuda, "hip", "mfma")
+    assert getattr(eng.hip, "fuses_optimizer", False)
+    K, B = 5, 8
+    g = torch.Generator().manual_seed(7)
+    xs = [spec.encode_features(torch.rand(K, B, 12, generator=g)).to(cuda) for _ in range(3)]
+    ys = [torch.randint(0, 3, (K, B), generator=g).to(cuda) for _ in range(3)]
+    w = torch.full((K, B), 1.0 / B, device=cuda)
+    acts = [torch.tensor(a, dtype=torch.float32, device=cuda) for a in ([1, 1, 1, 1, 1], [1, 0, 1, 1, 0], [0, 0, 1, 1, 0])]
+    p0 = torch.stack([spec.init_params(k) for k in range(K)]).to(cuda)
+    outs = []
+    for fused in (False, True):
+        p = p0.clone()
+        opt = BatchedOptimizer("adam", p.shape, cuda, 0.05, backend="hip")
+        grads = []
+        for s in range(3):
+            res = eng.loss_and_grads(xs[s], ys[s], w, p, "adjoint", fused_opt=(opt, acts[s]) if fused else None)
+            assert res.get("opt_done", False) == fused
+            if not fused:
+                opt.step(p, res["grad"], acts[s])
+            grads.append(res["grad"].clone())
+        torch.cuda.synchronize()
+        outs.append((p, opt.m, opt.v, opt.t, grads))
+    (pa, ma, va, ta, ga), (pb, mb, vb, tb, gb) = outs
+    for a, b in zip(ga, gb):
+        assert torch.equal(a, b)
+    assert torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(va, vb) and torch.equal(ta, tb)
+    assert ta.tolist() == [2, 1, 3, 3, 1]
+    assert not torch.equal(pa[0], p0[0]) and torch.equal(pa[1], pb[1])
