@@ -4,6 +4,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
@@ -118,7 +119,8 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.lam_in = (adjoint && a.load_lam) ? dp<uint32_t>(lam_in, torch::kInt32, "lam_in", states) : nullptr;
   a.lam_out = (adjoint && a.store_lam) ? dp<uint32_t>(lam_out, torch::kInt32, "lam_out", states) : nullptr;
   need(a.x_stride >= a.n, "x stride must cover n feature angles");
-  a.xang = a.gen ? dp<float>(xang, torch::kFloat32, "xang", S / a.in_rep * a.x_stride) : nullptr;   // layer-1 only
+  // layer-1 factors: the product-state generation (forward gen passes) and OP_L1PROD (adjoint passes)
+  a.xang = (a.gen || adjoint) ? dp<float>(xang, torch::kFloat32, "xang", S / a.in_rep * a.x_stride) : nullptr;
   a.params = dp<float>(params, torch::kFloat32, "params", K * a.p_stride);
   a.frags = a.n_slots ? (const void*)dp<int32_t>(frags, torch::kInt32, "frags", K * a.n_slots * 4 * 128 * 4) : nullptr;
   a.wread = adjoint ? dp<float>(wread, torch::kFloat32, "wread", S * a.C) : nullptr;
@@ -147,8 +149,19 @@ void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64
   for (int64_t o = 0; o < ops.size(0); ++o) {
     const int* w = ow + o * 128;
     const int code = w[0];
-    need(code >= 1 && code <= 8, "unknown op code");
+    need(code >= 1 && code <= 9, "unknown op code");
     need(adjoint || code == 1 || code == 7, "adjoint op in a forward pass");
+    if (code == 9) {   // OP_L1PROD: the program's last op; entries = tile bit | group << 8 | index << 16
+      need(o == ops.size(0) - 1, "the layer-1 product-state op must be the last op");
+      need(w[2] >= 1 && w[2] <= 16 && w[2] <= t, "layer-1 qubit count out of range");
+      int groups = 0;
+      for (int e = 0; e < w[2]; ++e) {
+        need((w[20 + e] & 255) < t && ((w[20 + e] >> 16) & 255) < 4, "layer-1 entry out of range");
+        groups = std::max(groups, ((w[20 + e] >> 8) & 255) + 1);
+      }
+      need(w[100] >= 0 && w[100] + groups <= n_gradops, "layer-1 gradient records out of range");
+      continue;
+    }
     if (code <= 3 || code == 8) need(w[1] >= 0 && w[1] < n_slots, "op names a missing unitary slot");
     if (code <= 5 || code == 8) {
       need(w[2] >= 0 && w[2] <= 4, "group size out of range");

@@ -47,7 +47,7 @@ namespace hea {
 
 constexpr int OPW = 128;
 enum { OP_APPLY = 1, OP_UNAPPLY_PSI = 2, OP_UNAPPLY_LAM = 3, OP_GRAD = 4, OP_GRAD_L1 = 5, OP_OBS = 6, OP_READOUT = 7,
-       OP_BACK = 8 };
+       OP_BACK = 8, OP_L1PROD = 9 };
 enum { W_CODE = 0, W_SLOT = 1, W_NREAL = 2, W_FLAGS = 3, W_RFULL = 4, W_RT = 8, W_TH = 12, W_PH = 16, W_OFF = 20,
        W_BL = 36, W_BH = 68, W_GIDX = 100 };
 constexpr double FIX = 4294967296.0;   // 2^32: fixed point of the scaled gradient partial traces
@@ -848,6 +848,178 @@ __device__ __forceinline__ uint32_t op_fo_global(const int* ow, uint32_t fixed) 
   return (uint32_t)ow[W_OFF + fpb];
 }
 
+// ------------------------------------------------------------------------------------------- layer-1 gradients
+// OP_L1PROD: the 2 x 2 cross matrices n_q[y][x] = sum_rest psi[y, rest] conj(lambda[x, rest]) of EVERY layer-1 qubit
+// of the tile in one op, at the end of the last adjoint pass (every later gate un-applied, so psi is the layer-1
+// product state (x) w_q, known in closed form).  Then n_q[y][x] = w_q[y] conj(mu_q[x]) with
+//     mu_q[x] = sum_{z: z_q = x} lambda[z] prod_{p != q} conj(w_p[z_p])
+// a leave-one-out contraction of lambda with the conjugate factors: lambda is read once, psi not at all (it need not
+// be un-applied by the pass's last group op), no MFMA and no atomics - one op instead of one GRAD_L1 op (tile read,
+// cross-matrix MFMAs, 80 fixed-point atomics, region flush) per layer-1 group.
+// Thread u < U = T / 16 owns amplitudes tau = u + U j, j < 16: tile bits [0, t - 4) are the thread bits ("lo"), the
+// top 4 the register bits ("hi").  With f_i = conj(w of tile bit i), Hb[j] = outer * prod_hi f and A_u = prod_lo f:
+//   c_u = sum_j lambda[u, j] Hb[j]     -> lo bit i:  mu[x] = sum_{u: u_i = x} c_u prod_{lo i' != i} f_i'[u_i']
+//   r_j = sum_u lambda[u, j] A_u       -> hi bit k:  mu[x] = outer sum_{j: j_k = x} r_j prod_{hi k' != k} f_k'[j_k']
+// The per-thread terms are summed in fixed order through the (dead) tile image, so the result is deterministic;
+// slab entries are the exact 2^-32 fixed point of the true cross matrix, as reduce_region writes them.
+// Record: W_NREAL = number of layer-1 qubits; word W_OFF + e = tile bit | group << 8 | index in group << 16;
+// group g's slab row is W_GIDX + g.  sc: >= 96 float2 of scratch LDS.
+template <int NT, int TB, bool PL>
+__device__ __forceinline__ void l1prod_op(uint32_t* tile, const PassArgs& a, const int* opw, int tid, int s, int k,
+                                       uint32_t fixed, float rho, long long* slab, float2* sc) {
+  const int t = a.t, U = 1 << (t - 4), nlo = t - 4;
+  float2* fw = sc;            // [32][2] true layer-1 factors w_q (memory bit q)
+  float2* hb = sc + 64;       // [16] outer * prod_hi conj(w)
+  float2* rj = sc + 80;       // [16] r_j
+  __shared__ float2 outer_s;
+  __shared__ int emap[TMAX];  // tile bit -> record entry, or -1
+  // ---- factors (wave 0: lane q computes qubit q's pair; the out-of-tile product over the wave)
+  if (tid < 64) {
+    float2 w[2] = {make_float2(1.f, 0.f), make_float2(1.f, 0.f)};
+    const float* prm = a.params + (size_t)k * a.p_stride;
+    if (tid < a.n) {
+      l1_factor(a.xang[(size_t)s * a.x_stride + tid], prm[2 * tid], prm[2 * tid + 1], a.feature, w);
+      fw[2 * tid] = w[0];
+      fw[2 * tid + 1] = w[1];
+    }
+    const bool outq = tid < a.n && !(tid < a.c || (tid >= a.lo && tid < a.hi));
+    const float2 w0 = w[0], w1 = w[1];
+    float2 f = outq ? (((fixed >> (tid & 31)) & 1) ? w1 : w0) : make_float2(1.f, 0.f);
+    f.y = -f.y;                                          // conj
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) f = cmul(f, make_float2(__shfl_xor(f.x, off, 64), __shfl_xor(f.y, off, 64)));
+    if (tid == 0) outer_s = f;
+    if (tid < TMAX) emap[tid] = -1;
+  }
+  lds_barrier();
+  if (tid < opw[W_NREAL]) emap[opw[W_OFF + tid] & 255] = tid;
+  auto mbit = [&](int i) { return i < a.c ? i : a.lo + i - a.c; };   // memory bit (= layer-1 qubit) of tile bit i
+  auto fconj = [&](int i, int b) { const float2 v = fw[2 * mbit(i) + b]; return make_float2(v.x, -v.y); };
+  if (tid < 16) {
+    float2 v = outer_s;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) v = cmul(v, fconj(nlo + kk, (tid >> kk) & 1));
+    hb[tid] = v;
+  }
+  lds_barrier();
+  // ---- r's terms lambda[u, j] A_u: every lambda word is read by exactly one thread, so thread u overwrites its own
+  // 16 (psi, lambda) slots with them right away (no barrier, no registers held); c_u accumulates on the way
+  float2 c = make_float2(0.f, 0.f);
+  const bool act = tid < U;
+  const uint32_t h0 = swz(a, (uint32_t)tid >> 5);
+  // tau = u + U j: u < U and U j share no bits, so h(tau >> 5) = h(u >> 5) ^ h((U j) >> 5) (h is linear)
+  auto slot = [&](int j) { return ((uint32_t)tid + (uint32_t)U * j) ^ (h0 ^ swz(a, ((uint32_t)U * (uint32_t)j) >> 5)); };
+  if (act) {
+    float2 A = make_float2(1.f, 0.f);
+    for (int i = 0; i < nlo; ++i) A = cmul(A, fconj(i, (tid >> i) & 1));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t w = slot(j);
+      const uint32_t lw = PL ? tile[lam_word<TB>() + w] : lds_ld2(tile, 8u * w).y;
+      const float2 lam = unpack_h2(lw), h = hb[j];
+      c = make_float2(c.x + lam.x * h.x - lam.y * h.y, c.y + lam.x * h.y + lam.y * h.x);
+      const float2 pv = cmul(lam, A);
+      if constexpr (PL) {
+        tile[w] = __float_as_uint(pv.x);
+        tile[lam_word<TB>() + w] = __float_as_uint(pv.y);
+      } else {
+        lds_st2(tile, 8u * w, make_uint2(__float_as_uint(pv.x), __float_as_uint(pv.y)));
+      }
+    }
+  }
+  lds_barrier();
+  auto pget = [&](uint32_t u, int j) {              // thread u's r term of register bit pattern j
+    const uint32_t hu = swz(a, u >> 5) ^ swz(a, ((uint32_t)U * (uint32_t)j) >> 5);
+    const uint32_t w = (u + (uint32_t)U * j) ^ hu;
+    if constexpr (PL)
+      return make_float2(__uint_as_float(tile[w]), __uint_as_float(tile[lam_word<TB>() + w]));
+    const uint2 v = lds_ld2(tile, 8u * w);
+    return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+  };
+  // r_j: thread (j, l < 32) sums u = l, l + 32, ... then a fixed xor tree over the 32 lanes
+  {
+    const int j = tid >> 5, l = tid & 31;
+    float2 v = make_float2(0.f, 0.f);
+    if (j < 16)
+      for (int m = l; m < U; m += 32) {
+        const float2 e = pget((uint32_t)m, j);
+        v = make_float2(v.x + e.x, v.y + e.y);
+      }
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) {
+      const float ox = __shfl_xor(v.x, off, 64), oy = __shfl_xor(v.y, off, 64);
+      v = (l & off) ? make_float2(ox + v.x, oy + v.y) : make_float2(v.x + ox, v.y + oy);
+    }
+    if (j < 16 && l == 0) rj[j] = v;
+  }
+  lds_barrier();                                     // r terms read: the image is free for the lo terms
+  float2* scr = (float2*)tile;                       // [t - 4][U] lo terms T_i
+  if (act) {
+    // T_i = c_u prod_{lo i' != i} f_i' (prefix x suffix products)
+    float2 pre[TMAX - 3];
+    pre[0] = make_float2(1.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < TMAX - 4; ++i) pre[i + 1] = i < nlo ? cmul(pre[i], fconj(i, (tid >> i) & 1)) : pre[i];
+    float2 suf = make_float2(1.f, 0.f);
+#pragma unroll
+    for (int i = TMAX - 5; i >= 0; --i) {
+      if (i < nlo) {
+        scr[i * U + tid] = cmul(c, cmul(pre[i], suf));
+        suf = cmul(fconj(i, (tid >> i) & 1), suf);
+      }
+    }
+  }
+  lds_barrier();
+  const double nsc = (double)rho / (double)a.scale * FIX;   // lambda image -> true units, 2^-32 fixed point
+  // lo bins: thread (i, x, l < 16) sums T[i][u] over u with u_i = x (entries m = l, l + 16, ...), xor tree over 16
+  float2 mu_lo = make_float2(0.f, 0.f);
+  const int bi = tid >> 5, bx = (tid >> 4) & 1, bl = tid & 15;
+  if (bi < nlo) {
+    const uint32_t lowm = (1u << bi) - 1u;
+    for (int m = bl; m < (U >> 1); m += 16) {
+      const uint32_t u = (((uint32_t)m & ~lowm) << 1) | ((uint32_t)bx << bi) | ((uint32_t)m & lowm);
+      const float2 tv = scr[bi * U + u];
+      mu_lo = make_float2(mu_lo.x + tv.x, mu_lo.y + tv.y);
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1) {
+    const float ox = __shfl_xor(mu_lo.x, off, 64), oy = __shfl_xor(mu_lo.y, off, 64);
+    mu_lo = (bl & off) ? make_float2(ox + mu_lo.x, oy + mu_lo.y) : make_float2(mu_lo.x + ox, mu_lo.y + oy);
+  }
+  auto write_n = [&](int tb, int x, float2 mu) {          // n[y][x] = w[y] conj(mu), y = 0, 1
+    const int e = emap[tb];
+    if (e < 0) return;
+    const int rec = opw[W_OFF + e], g = (rec >> 8) & 255, jq = (rec >> 16) & 255;
+    long long* row = slab + (size_t)(opw[W_GIDX] + g) * 32 + 8 * jq;
+#pragma unroll
+    for (int y = 0; y < 2; ++y) {
+      const float2 w = fw[2 * mbit(tb) + y];
+      const double re = (double)w.x * mu.x + (double)w.y * mu.y, im = (double)w.y * mu.x - (double)w.x * mu.y;
+      row[4 * y + 2 * x] = __double2ll_rn(re * nsc);
+      row[4 * y + 2 * x + 1] = __double2ll_rn(im * nsc);
+    }
+  };
+  if (bi < nlo && bl == 0) write_n(bi, bx, mu_lo);
+  // hi bits: thread (k < 4, x, jj < 8): term r_j prod_{k' != k} f(j_k'), j = jj with bit x inserted at k; tree over 8
+  if (tid < 64) {
+    const int kk = tid >> 4, x = (tid >> 3) & 1, jj = tid & 7;
+    const int lowm = (1 << kk) - 1;
+    const int j = ((jj & ~lowm) << 1) | (x << kk) | (jj & lowm);
+    float2 v = rj[j];
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2)
+      if (k2 != kk) v = cmul(v, fconj(nlo + k2, (j >> k2) & 1));
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+      const float ox = __shfl_xor(v.x, off, 64), oy = __shfl_xor(v.y, off, 64);
+      v = (jj & off) ? make_float2(ox + v.x, oy + v.y) : make_float2(v.x + ox, v.y + oy);
+    }
+    const float2 o = outer_s;
+    if (jj == 0) write_n(nlo + kk, x, cmul(v, o));
+  }
+}
+
 // ------------------------------------------------------------------------------------------- forward pass
 // One workgroup per tile of 2^t <= 2^14 amplitudes: 8 waves and 64 KB of LDS, so two workgroups share a CU and
 // one's tile load overlaps the other's group ops (minimum waves per SIMD 4: <= 128 VGPRs).
@@ -1257,7 +1429,11 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   HEA_MARK();
   int ngrad = 0;
   int pending = -1;                                    // ring: region of the previous op, if a gradient op
-  for (int o = 0; o < a.nops; ++o) {
+  // A layer-1 product-state op (always the program's last) runs after the op loop, where none of the loop's values
+  // are live: inside the loop its code pushed the group ops' register allocation into spills.
+  const bool l1last = a.nops > 0 && a.ops[(size_t)(a.nops - 1) * OPW + W_CODE] == OP_L1PROD;
+  const int nloop = l1last ? a.nops - 1 : a.nops;
+  for (int o = 0; o < nloop; ++o) {
     // op o's record and fragments were written during op o - 1; the other buffers were last read at the
     // start of op o - 1, which every wave has finished at this barrier, so op o + 1's go there right away
     if (QFX_HEA_ABLATE && (a.ablate & 1) && o > 0)
@@ -1282,8 +1458,11 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
     }
     const int code = opw[W_CODE];
 #if QFX_CHECKS_ON
-    QFX_DCHECK(code >= OP_APPLY && code <= OP_BACK && code != OP_READOUT);
-    if (code != OP_OBS) {
+    QFX_DCHECK(code >= OP_APPLY && code <= OP_L1PROD && code != OP_READOUT);
+    if (code == OP_L1PROD) {
+      QFX_DCHECK(opw[W_NREAL] >= 1 && opw[W_NREAL] <= a.t && fidx_s[o] == -1 && o == a.nops - 1);
+      for (int e = 0; e < opw[W_NREAL]; ++e) QFX_DCHECK((opw[W_OFF + e] & 255) < a.t);
+    } else if (code != OP_OBS) {
       QFX_DCHECK(opw[W_NREAL] >= 0 && opw[W_NREAL] <= 4);
       QFX_DCHECK((uint32_t)opw[W_OFF + (lane & 15)] < (uint32_t)T);
       QFX_DCHECK((uint32_t)opw[W_BL + (lane & 31)] < (uint32_t)T);
@@ -1299,6 +1478,7 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
 #endif
     if (code == OP_OBS) {
       obs_op<NCK, NT, TB, PL>(tile, opw, tid, T, fixed, rsc);
+
     } else if (code == OP_UNAPPLY_PSI || code == OP_APPLY) {
       // U^H (or, re-applying a recomputed last pass, U) on the psi plane
       group_apply<1, NW, true, 0, TB, PL>(tile, F, opw, fo_s[o], lane, wave, nbw);
@@ -1359,6 +1539,13 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
     if (pending >= 0 && wave == NW - 1 && lane < 32) reduce_region(pending, lane);
   } else {
     for (int e = tid; e < ngrad * 32; e += NT) reduce_region(e >> 5, e & 31);
+  }
+  if (l1last) {
+    QFX_DCHECK(!a.store_lam);
+    // the pass's last op: the fragment slots are free (no unitary here, none prefetched after it); its record was
+    // staged during op nops - 2 (or before the loop)
+    lds_barrier();
+    l1prod_op<NT, TB, PL>(tile, a, opw2[(a.nops - 1) & 1], tid, s, k, fixed, rsc[CMAX], slab, (float2*)&frag_s[0][0]);
   }
   if (a.store_lam) store_lam_il<NT, TB, PL>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
   HEA_MARK();

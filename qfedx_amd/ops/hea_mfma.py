@@ -56,6 +56,9 @@ _NO_KEYS = torch.zeros(0, dtype=torch.int64)
 _NODBG = torch.zeros(0, dtype=torch.int64)     # no phase timestamps
 
 
+FUSED_ADAM_MAX_BLOCKS = 256   # hea_grad_reduce blocks (clients x gradient ops) up to which Adam is fused
+
+
 class HeaMfmaProgram:
     def __init__(self, spec, device, tile_bits: int | None = None, adj_tile_bits: int | None = None):
         if not eligible(spec):
@@ -551,8 +554,14 @@ class HeaMfmaProgram:
         grad = torch.empty_like(p)
         n = self._chunks(K, B) if noise is None else 1
         adam = None
-        if (fused_opt is not None and n == 1 and self.n_gradops > 0 and p.data_ptr() == params.data_ptr()
-                and os.environ.get("QFEDX_FUSED_ADAM", "1") != "0"):
+        # Auto: fused only while the reduction has at most one block per CU.  Every block publishes its gradient
+        # entries with one agent-scope release (an L2 writeback here): at 16q x 64 clients (832 blocks) the fused
+        # launch took 33.6 us against 13 + 5.4 us for the two launches; at the 8-client share (104 blocks) it saves
+        # a launch (round 387 -> 382 us; profiles/r3_fused_adam_ab.txt).  QFEDX_FUSED_ADAM=1 / 0 forces it on / off.
+        mode = os.environ.get("QFEDX_FUSED_ADAM", "auto")
+        want = mode == "1" or (mode == "auto" and K * self.n_gradops <= FUSED_ADAM_MAX_BLOCKS)
+        if (want and fused_opt is not None and n == 1 and self.n_gradops > 0
+                and p.data_ptr() == params.data_ptr()):
             adam = fused_opt[0].fused_adam(p, fused_opt[1])
         if n == 1:
             self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=adam)
