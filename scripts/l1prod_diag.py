@@ -17,7 +17,7 @@ def main():
     dev = torch.device("cuda", 0)
     n, L = int(sys.argv[1]), int(sys.argv[2])
     spec = VQCSpec(n, L, 3)
-    K, B = 3, 4
+    K, B = (int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (3, 4)
     x, params, wr = _inputs(spec, K, B, seed=11)
     xx, th, ww = x.to(dev), params[:, : spec.n_theta].to(dev), wr.to(dev)
     prog = HeaMfmaProgram(spec, dev)
@@ -28,7 +28,7 @@ def main():
         slabs.append(prog._ws["gslab"].clone().view(K * B, prog.slab_tiles, prog.n_gradops, 32).cpu())
     d = (slabs[0] != slabs[1]) | (slabs[0] != slabs[2])
     idx = d.nonzero()
-    print(json.dumps({"n": n, "n_gradops": prog.n_gradops, "slab_tiles": prog.slab_tiles, "ndiff": int(d.sum()),
+    print(json.dumps({"K": K, "B": B, "wgs": K * B << (n - prog.adj_tile_bits), "n": n, "n_gradops": prog.n_gradops, "slab_tiles": prog.slab_tiles, "ndiff": int(d.sum()),
                       "by_record": torch.bincount(idx[:, 2], minlength=prog.n_gradops).tolist() if len(idx) else [],
                       "by_slot": torch.bincount(idx[:, 3], minlength=32).tolist() if len(idx) else [],
                       "by_tile": torch.bincount(idx[:, 1], minlength=prog.slab_tiles).tolist()[:16] if len(idx) else [],
