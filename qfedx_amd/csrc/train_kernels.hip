@@ -479,10 +479,12 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
   const double SC = 4294967296.0;
   const int el = threadIdx.x % FA_E, grp = threadIdx.x / FA_E;
   const long e = (long)blockIdx.x * FA_E + el;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    // the weight sum: lane-strided over the clients (one dependent global load per client made a serial loop the
+    // launch's long pole at 64 clients), then an integer wave sum - exact, so the split changes no bit
     long long ws = 0;
     int wsat = 0;
-    for (int k = 0; k < K; ++k) {
+    for (int k = threadIdx.x; k < K; k += 64) {
       if (sa.seeds) {                  // the weight is element P of the client's masked vector
         const double v = weights[k] * sa.scale, lim = (double)(sa.mask >> 1);
         if (!(fabs(v) <= lim)) ++wsat;
@@ -493,8 +495,15 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
       if (!(fabs(v) <= FA_SAT)) ++wsat;
       ws += llrint(fmin(fmax(v, -FA_SAT), FA_SAT));
     }
-    out[P] = ws;
-    if (wsat && sat) atomicAdd((unsigned long long*)sat, (unsigned long long)wsat);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      ws += __shfl_xor(ws, off, 64);
+      wsat += __shfl_xor(wsat, off, 64);
+    }
+    if (threadIdx.x == 0) {
+      out[P] = ws;
+      if (wsat && sat) atomicAdd((unsigned long long*)sat, (unsigned long long)wsat);
+    }
   }
   long long acc = 0;
   int nsat = 0;
