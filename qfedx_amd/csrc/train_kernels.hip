@@ -347,20 +347,24 @@ struct RoundPack {          // metrics of the round epilogue (buf == nullptr: no
 };
 
 __device__ __forceinline__ void round_pack_block(const RoundPack& rp, int P) {
+  // the first 256 threads of the block (the fedavg launch's pack block has more; they only join the barriers)
   __shared__ double red[4][256];
   const int t = threadIdx.x;
+  const bool on = t < 256;
   double ls = 0.0, cs = 0.0, ns = 0.0, as = 0.0;
-  for (int i = t; i < rp.n; i += 256) {
+  for (int i = t; on && i < rp.n; i += 256) {
     const double nv = (double)rp.nvalid[i], ac = (double)rp.act[i];
     ls += (double)rp.loss[i] * nv;
     cs += (double)rp.correct[i] * ac;
     ns += nv;
     as += ac;
   }
-  red[0][t] = ls;
-  red[1][t] = cs;
-  red[2][t] = ns;
-  red[3][t] = as;
+  if (on) {
+    red[0][t] = ls;
+    red[1][t] = cs;
+    red[2][t] = ns;
+    red[3][t] = as;
+  }
   __syncthreads();
   for (int h = 128; h > 0; h >>= 1) {
     if (t < h)
@@ -368,14 +372,15 @@ __device__ __forceinline__ void round_pack_block(const RoundPack& rp, int P) {
     __syncthreads();
   }
   if (t < 4) rp.buf[P + 1 + t] = llrint(red[t][0] * 4294967296.0);
-  if (rp.norms)
+  if (rp.norms && on)
     for (int k = t; k < rp.K; k += 256) rp.buf[P + 6 + rp.cid[k]] = llrint(rp.norms[k] * 4294967296.0);
 }
 
 // out[e] = sum_k round(2^32 * w_k * priv(wrap(theta_k[e] - theta_g[e]))), out[P] = sum_k round(2^32 w_k)
 // Each client's term is rounded to fixed point BEFORE the sum: integer addition is associative, so the
 // aggregate is bitwise identical for any sharding of clients over GPUs (and equal to the CPU path).
-constexpr int FA_E = 64, FA_G = 4;   // fedavg reduce: parameters per block (one wave row) x client groups per block
+constexpr int FA_E = 64, FA_G = 16;  // fedavg reduce: parameters per block (one wave row) x client groups per block
+// (16 groups: a 64-client round has every client row in flight at once; 4 left the launch latency-bound)
 constexpr int FA_U = 4;              // client rows in flight per thread
 
 // Pairwise-mask secure aggregation inside the reduce (privacy/secure_agg.py is the host protocol and
