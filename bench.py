@@ -123,7 +123,7 @@ def make_config(args):
     cfg.model.n_layers = args.layers
     cfg.model.n_classes = args.classes
     cfg.model.readout_scale = 3.0
-    cfg.model.state_dtype = "mfma" if args.engine == "mfma" else "fp32"
+    cfg.model.state_dtype = {"mfma": "mfma", "mfma_bf16": "bf16"}.get(args.engine, "fp32")
     cfg.train.batch_size = args.batch
     cfg.train.local_steps = args.local_steps
     cfg.train.learning_rate = 0.05
@@ -176,8 +176,9 @@ def main():
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (auto: nccl = RCCL on GPUs, gloo on CPU); gloo on GPUs lets "
                          "several ranks share one GPU in tests")
-    ap.add_argument("--engine", default="mfma", choices=["mfma", "valu"],
-                    help="mfma: fp16-state MFMA group-unitary engine (ops/hea_mfma.py); valu: fp32 pass engine")
+    ap.add_argument("--engine", default="mfma", choices=["mfma", "mfma_bf16", "valu"],
+                    help="mfma: fp16-state MFMA group-unitary engine (ops/hea_mfma.py); mfma_bf16: the same engine "
+                         "with bf16 state storage; valu: fp32 pass engine")
     ap.add_argument("--precision-check", type=int, default=1,
                     help="after timing, one untimed VJP on the fp32 VALU engine at the bench shape: report the "
                          "MFMA engine's max abs <Z> / gradient differences (0 = skip)")
@@ -198,7 +199,13 @@ def main():
     value = local_steps_total / dt
     rounds_per_s = args.steps / dt
     # label what actually ran: the MFMA engine exists only on the HIP backend (ops/engine.py)
-    mfma = backend == "hip" and getattr(runner.adapter, "state_dtype", "") in ("mfma", "fp16")
+    sdt = getattr(runner.adapter, "state_dtype", "")
+    mfma = backend == "hip" and sdt in ("mfma", "fp16", "mfma_bf16")
+    import torch.distributed as tdist
+    from qfedx_amd.parallel.dist import max_over_ranks
+    rccl_ws = tdist.get_world_size() if tdist.is_initialized() else 0
+    fallbacks = max_over_ranks(float(getattr(runner.adapter.trainer, "capture_fallbacks", 0)), world)
+    graph_comm = runner.graph_comm_mode if fallbacks == 0 else "mixed"
     engine = "mfma" if mfma else ("valu" if backend == "hip" else backend)
     if world.is_main:
         rec = {
@@ -212,7 +219,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp16-state/fp32-accumulate (MFMA)" if mfma else "fp32",
+            "dtype": (("bf16" if sdt == "mfma_bf16" else "fp16") + "-state/fp32-accumulate (MFMA)") if mfma else "fp32",
             "engine": engine,
             "data": "synthetic non-IID (Dirichlet alpha=0.5) client shards, random-init VQC",
             "rounds_per_sec": round(rounds_per_s, 4),
@@ -220,6 +227,11 @@ def main():
             "backend": backend,
             "test_acc_after": round(ev["test_acc"], 4),
             "dist_backend": world.backend,
+            # ranks in the process group as torch.distributed sees it (0: no group) and whether the round's
+            # all-reduce ran captured in the round hipGraph on every rank (agreed at startup; "mixed" if a later
+            # shape had to fall back to an eager collective on some rank)
+            "rccl_world_size": rccl_ws,
+            "graph_comm": graph_comm,
             "host_ms_per_round": round(getattr(runner, "host_ms", 0.0), 4),   # enqueue time (GPU runs behind)
             **phases,
             **prec,

@@ -31,9 +31,15 @@ SUITE = {
     "vqc24q_ps256_mfma": ("configs/baseline5_24q_256clients_paramshift_shots.yaml", ["model.state_dtype=mfma"],
                           "client local-steps/sec (24-qubit VQC x 256 clients, param-shift + shots, fp16 MFMA engine)",
                           None),
+    # config 2 as written (state_dtype: bf16) runs the bf16 MFMA engine (csrc/hea_mfma_bf16.hip)
     "vqc16q_bf16_8": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1"],
                       "client local-steps/sec (16-qubit VQC bf16 state x 8 clients)", None),
-    "vqc16q_bf16_8_mfma": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1", "model.state_dtype=mfma"],
+    "vqc16q_bf16_8_mfma": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1"],
+                           "client local-steps/sec (16-qubit VQC bf16 state x 8 clients, bf16 MFMA engine)", None),
+    "vqc16q_bf16_8_valu": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1",
+                                                                        "model.state_dtype=bf16_valu"],
+                           "client local-steps/sec (16-qubit VQC bf16 state x 8 clients, VALU pass engine)", None),
+    "vqc16q_fp16_8_mfma": ("configs/baseline2_16q_bf16_8clients.yaml", ["train.local_steps=1", "model.state_dtype=mfma"],
                            "client local-steps/sec (16-qubit VQC x 8 clients, fp16 MFMA engine in place of bf16 "
                            "storage)", None),
     "vqc16q_64": ("configs/headline_16q_64clients.yaml", ["model.state_dtype=fp32"],
@@ -96,6 +102,7 @@ def main():
             "ms_per_step": round(1e3 * dt / args.steps, 3), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": round(value / ref, 2) if ref else None,
             "dtype": {"bf16": "bf16-state/fp32-compute", "mfma": "fp16-state/fp32-accumulate (MFMA)",
+                      "mfma_bf16": "bf16-state/fp32-accumulate (MFMA)",
                       "fp16": "fp16-state/fp32-accumulate (MFMA)"}.get(
                           getattr(runner.adapter, "state_dtype", cfg.model.state_dtype)
                           if backend == "hip" else "fp32", "fp32"),   # the MFMA/bf16 engines exist only on HIP

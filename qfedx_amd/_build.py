@@ -57,6 +57,19 @@ def _hash(paths) -> str:
     return h.hexdigest()
 
 
+def _local_includes(src: str) -> list:
+    """Non-header sources ``src`` pulls in with #include "..." (hea_mfma_bf16.hip includes hea_mfma.hip): part of
+    its rebuild key (the *.h headers are hashed for every object anyway)."""
+    import re
+    out = []
+    with open(src) as f:
+        for m in re.finditer(r'^\s*#include\s+"([^"]+)"', f.read(), re.M):
+            p = os.path.join(os.path.dirname(src), m.group(1))
+            if os.path.exists(p) and not p.endswith(".h"):
+                out.append(p)
+    return out
+
+
 def _run(cmd):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -86,7 +99,7 @@ def build(verbose: bool = False, force: bool = False, debug=None) -> str:
     hh = _hash(headers)
     for src in hips:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-        key = _hash([src]) + hh + ARCH + " ".join(extra)
+        key = _hash([src] + _local_includes(src)) + hh + ARCH + " ".join(extra)
         objs.append(obj)
         if stamps.get(obj) != key or not os.path.exists(obj):
             cmd = ["hipcc", "-c", "-fPIC", "-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fno-gpu-rdc",

@@ -46,8 +46,9 @@ class ModelConfig:
     entangler: str = "chain"            # chain | ring | none
     readout_scale: float = 1.0          # initial a in logit = a<Z> + b
     init_std: float = 0.1
-    state_dtype: str = "auto"           # auto (mfma when eligible on HIP, else fp32) | fp32 | bf16 (VALU pass
-                                        # engine storage) | mfma (fp16 MFMA engine, hardware-efficient ansatz)
+    state_dtype: str = "auto"           # auto (mfma when eligible on HIP, else fp32) | fp32 | mfma (fp16 MFMA engine,
+                                        # hardware-efficient ansatz) | bf16 (bf16 MFMA engine when eligible, else
+                                        # bf16 storage on the VALU pass engine) | bf16_valu
     simulator: str = "statevector"      # statevector | mps (tensor network past statevector memory) | density
                                         # (exact Kraus channels, <= 10 qubits; auto for noise.kind=amplitude)
     mps_chi: int = 64                   # MPS bond-dimension cap (exact while the circuit's bound fits)
@@ -87,6 +88,7 @@ class PrivacyConfig:
     secure_agg: bool = False
     secagg_bits: int = 48               # fixed-point ring Z_{2^bits} for exact mask cancellation
     secagg_scale: float = 2.0 ** 24
+    secagg_graph: str = "full"          # full (every pair) | sparse (SecAgg+: 2 ceil(log2 K) neighbours, O(K log K))
     # testing/debug only: key DP noise and DP client sampling by the PUBLIC train.seed (reproducible
     # across runs and rank counts) instead of a per-run secret - voids the DP guarantee
     deterministic_noise: bool = False
@@ -120,9 +122,10 @@ class RuntimeConfig:
     use_graphs: bool = True            # hipGraph capture of the local round (HIP backend)
     graph_comm: bool = True            # capture the round's all-reduce + apply into that graph (RCCL / no group)
     timer_every: int = 0               # time the GPU phases every N-th round (0: 16 on GPU, every round on CPU)
-    log_client_norms: bool = True      # DP rounds: every client's pre-clip update norm reaches every rank in the
-                                       # round all-reduce (CC6); clip fraction + norm quantiles per round (not
-                                       # under SecAgg, where per-client statistics would leak)
+    log_client_norms: bool = False     # NON-PRIVATE debug diagnostic (DP rounds): every client's raw pre-clip update
+                                       # norm reaches every rank in the round all-reduce (CC6) and clip fraction +
+                                       # norm quantiles are logged; they are not noised nor charged to the
+                                       # accountant (never under SecAgg)
 
 
 @dataclass

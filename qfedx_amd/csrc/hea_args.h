@@ -30,6 +30,7 @@ struct HeaPassArgs {
   int in_rep;                // forward: shifted parameter rows per stored input sample (param-shift prefix reuse)
   int pair;                  // forward: two samples per workgroup on 2^13 tiles (hea_fwd2_kernel)
   int ablate;                // timing ablations (builds with QFX_HEA_ABLATE only; QFEDX_HEA_ABLATE bit mask)
+  uint32_t poison;           // diagnostics: != 0 fills every LDS word with this value at workgroup start
 };
 
 // Launch arguments of a fused Adam epilogue (m == nullptr: none).  cnt: one zero-initialised arrival counter per

@@ -21,6 +21,11 @@ int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, c
                         float* params, float* grad, int p_stride, const QfxAdamArgs* adam, hipStream_t st);
 int qfx_hea_args_size();
 int qfx_hea_check_status(hipStream_t st);
+// bf16 state storage (hea_mfma_bf16.hip)
+int qfx_hea_pass_bf16(int adjoint, const HeaPassArgs* args, int n_samples, hipStream_t st);
+int qfx_hea_frags_bf16(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
+                       hipStream_t st);
+int qfx_hea_check_status_bf16(hipStream_t st);
 }
 
 namespace {
@@ -45,19 +50,22 @@ void check(int rc, const char* what) {
   if (rc != 0) throw std::runtime_error(std::string(what) + " failed: " + std::to_string(rc));
 #if defined(QFX_DEVICE_CHECKS) && QFX_DEVICE_CHECKS
   // debug build: every launch is followed by a read of the device-check status word
-  const int line = qfx_hea_check_status(cur());
+  int line = qfx_hea_check_status(cur());
+  if (line == 0) line = qfx_hea_check_status_bf16(cur());
   if (line != 0)
     throw std::runtime_error(std::string(what) + ": device check failed at hea_mfma.hip:" + std::to_string(line));
 #endif
 }
 
 // geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
-//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, pair]
+//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, pair[, bf16]]
+// bf16 (optional, default 0): states and fragments in bf16 (hea_mfma_bf16.hip) instead of fp16
 void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<int64_t> geom, double scale, torch::Tensor psi_in,
               torch::Tensor psi_out, torch::Tensor lam_in, torch::Tensor lam_out, torch::Tensor xang,
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
               torch::Tensor gslab, torch::Tensor dbg) {
-  need(geom.size() == 28, "geometry vector must have 28 entries");
+  need(geom.size() == 28 || geom.size() == 29, "geometry vector must have 28 or 29 entries");
+  const bool bf16 = geom.size() == 29 && geom[28] != 0;
   HeaPassArgs a{};
   a.n = (int)geom[0];
   a.t = (int)geom[1];
@@ -86,6 +94,14 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
       ablate = e ? atoi(e) : 0;
     }
     a.ablate = ablate;
+    // QFEDX_HEA_POISON=<hex>: fill all of a pass kernel's LDS with this word before it starts (uninitialised-read
+    // diagnostics; results must not depend on it)
+    static long long poison = -1;
+    if (poison < 0) {
+      const char* e = getenv("QFEDX_HEA_POISON");
+      poison = e ? (long long)(strtoull(e, nullptr, 0) & 0xffffffffull) : 0;
+    }
+    a.poison = (uint32_t)poison;
   }
   a.n_gradops = (int)geom[25];
   a.in_rep = (int)geom[26];
@@ -129,7 +145,10 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.gslab = adjoint ? dp<long long>(gslab, torch::kInt64, "gslab", S * a.slab_tiles * a.n_gradops * 32) : nullptr;
   need(!adjoint || a.slab_tiles >= a.n_tiles, "gradient slab has fewer tiles than the pass");
   need(!a.gen || a.n <= 32, "product-state generation supports <= 32 qubits");
-  check(qfx_hea_pass(adjoint ? 1 : 0, &a, (int)S, cur()), "qfx_hea_pass");
+  if (bf16)
+    check(qfx_hea_pass_bf16(adjoint ? 1 : 0, &a, (int)S, cur()), "qfx_hea_pass_bf16");
+  else
+    check(qfx_hea_pass(adjoint ? 1 : 0, &a, (int)S, cur()), "qfx_hea_pass");
 }
 
 // Validate a pass program once (host copy) when it is built: slot / gradient-slot ranges and op kinds.
@@ -176,9 +195,9 @@ void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64
 }
 
 void hea_frags(torch::Tensor params, int64_t p_stride, torch::Tensor slot_tab, int64_t n_slots, int64_t K,
-               torch::Tensor frags) {
+               torch::Tensor frags, bool bf16) {
   need(slot_tab.scalar_type() == torch::kInt32 && slot_tab.numel() >= n_slots * 9, "slot table [n_slots, 9] int32");
-  check(qfx_hea_frags(dp<float>(params, torch::kFloat32, "params", K * p_stride), (int)p_stride,
+  check((bf16 ? qfx_hea_frags_bf16 : qfx_hea_frags)(dp<float>(params, torch::kFloat32, "params", K * p_stride), (int)p_stride,
                       dp<int>(slot_tab, torch::kInt32, "slot_tab", n_slots * 9), (int)n_slots, (int)K,
                       dp<int32_t>(frags, torch::kInt32, "frags", K * n_slots * 4 * 128 * 4), cur()),
         "qfx_hea_frags");
@@ -214,7 +233,8 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
 
 void register_hea(pybind11::module& m) {
   m.def("hea_pass", &hea_pass);
-  m.def("hea_frags", &hea_frags);
+  m.def("hea_frags", &hea_frags, pybind11::arg("params"), pybind11::arg("p_stride"), pybind11::arg("slot_tab"),
+        pybind11::arg("n_slots"), pybind11::arg("K"), pybind11::arg("frags"), pybind11::arg("bf16") = false);
   m.def("hea_check_ops", &hea_check_ops);
   m.def("hea_grad_reduce", &hea_grad_reduce, pybind11::arg("gslab"), pybind11::arg("slab_tiles"),
         pybind11::arg("n_gradops"), pybind11::arg("gmeta"), pybind11::arg("spc"), pybind11::arg("K"),

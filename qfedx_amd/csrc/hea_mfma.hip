@@ -22,6 +22,21 @@
 #include <cstdint>
 #include <cstdlib>
 
+// Storage type of the states and unitary fragments: fp16 (this translation unit) or bf16 (hea_mfma_bf16.hip includes
+// this file with QFX_HEA_BF16=1: the same kernels in namespace hea_bf16, entry points suffixed _bf16).  Only the
+// pack / unpack / MFMA / i-multiply primitives and the fragment split below depend on it.
+#ifndef QFX_HEA_BF16
+#define QFX_HEA_BF16 0
+#endif
+#if QFX_HEA_BF16
+#define HEA_NS hea_bf16
+#define HEA_EXT(name) name##_bf16
+#define qfx_check_word qfx_check_word_bf16
+#else
+#define HEA_NS hea
+#define HEA_EXT(name) name
+#endif
+
 #include "hea_args.h"
 #include "qfx_adam.h"
 #include "qfx_check.h"
@@ -42,8 +57,13 @@ __device__ unsigned int qfx_check_word = 0;
 #ifndef QFX_HEA_GATE_LO
 #define QFX_HEA_GATE_LO 1
 #endif
+// Phase timestamps (HEA_MARK, a.dbg) exist only in timing builds: in release builds the stamp pointer folds to null
+// and its bookkeeping (a pointer and a counter live across the op loop) leaves the kernels' scalar registers free.
+#ifndef QFX_HEA_MARKS
+#define QFX_HEA_MARKS QFX_HEA_ABLATE
+#endif
 
-namespace hea {
+namespace HEA_NS {
 
 constexpr int OPW = 128;
 enum { OP_APPLY = 1, OP_UNAPPLY_PSI = 2, OP_UNAPPLY_LAM = 3, OP_GRAD = 4, OP_GRAD_L1 = 5, OP_OBS = 6, OP_READOUT = 7,
@@ -76,21 +96,33 @@ __device__ __forceinline__ int red_slot(int e) {
   return e + (k < 4 ? k : 8);
 }
 
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+#if QFX_HEA_BF16
+typedef __bf16 st_t;
+#else
+typedef _Float16 st_t;
+#endif
+typedef st_t half8 __attribute__((ext_vector_type(8)));
+typedef st_t half2v __attribute__((ext_vector_type(2)));
+// 1.0 in the storage type, in the low / high half of a packed (re, im) word
+constexpr uint32_t ONE_LO = QFX_HEA_BF16 ? 0x00003F80u : 0x00003C00u;
+constexpr uint32_t ONE_HI = ONE_LO << 16;
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
 using PassArgs = HeaPassArgs;
 
 __device__ __forceinline__ uint32_t pack_h2(float re, float im) {
-  half2v h = {(_Float16)re, (_Float16)im};
+  half2v h = {(st_t)re, (st_t)im};
   return __builtin_bit_cast(uint32_t, h);
 }
 
 __device__ __forceinline__ float2 unpack_h2(uint32_t u) {
+#if QFX_HEA_BF16
+  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u));   // bf16 -> fp32 is a shift
+#else
   half2v h = __builtin_bit_cast(half2v, u);
   return make_float2((float)h.x, (float)h.y);
+#endif
 }
 
 __device__ __forceinline__ int par(uint32_t x) { return __builtin_popcount(x) & 1; }
@@ -101,13 +133,26 @@ __device__ __forceinline__ int par(uint32_t x) { return __builtin_popcount(x) & 
 // the s_barrier is sufficient; global results (gslab, stored tiles) are never read back inside the kernel.
 __device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Diagnostics (a.poison != 0, QFEDX_HEA_POISON): fill an LDS array with the poison word before the kernel touches it, so
+// a read of LDS this workgroup never wrote shows up as a result that depends on the poison value.
+template <typename T>
+__device__ __forceinline__ void poison_lds(T* p, int bytes, uint32_t v, int tid, int nt) {
+  uint32_t* w = (uint32_t*)p;
+  for (int i = tid; i < bytes / 4; i += nt) w[i] = v;
+}
+
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
 
 __device__ __forceinline__ f4 mfma(uint4 a, uint4 b, f4 c) {
+#if QFX_HEA_BF16
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), c, 0,
+                                                  0, 0);
+#else
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, a), __builtin_bit_cast(half8, b), c, 0,
                                                  0, 0);
+#endif
 }
 
 // memory index of tile position tau
@@ -292,9 +337,14 @@ __device__ __forceinline__ void lds_st(uint32_t* tile, uint32_t byte, uint32_t v
 
 // i * (re, im) = (-im, re) on a packed fp16 pair: dst.lo = src.hi * (-1), dst.hi = src.lo * 1
 __device__ __forceinline__ uint32_t mul_i(uint32_t v) {
+#if QFX_HEA_BF16
+  // no packed bf16 multiply: swap the halves (rotate by 16) and flip the sign of the new low half
+  return __builtin_amdgcn_alignbit(v, v, 16) ^ 0x00008000u;
+#else
   uint32_t r;
   __asm__("v_pk_mul_f16 %0, %1, %2 op_sel:[1,0] op_sel_hi:[0,1]" : "=v"(r) : "v"(v), "s"(0x3C00BC00u));
   return r;
+#endif
 }
 
 // Y = U X on the op's column blocks for NX targets (tile byte bases tb[x]) sharing the addressing.  Lane
@@ -334,8 +384,8 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
     uint32_t* im = (uint32_t*)&IIM;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      re[j] = cl == 4 * g4 + j ? 0x00003C00u : 0u;
-      im[j] = cl == 4 * g4 + j ? 0x3C000000u : 0u;
+      re[j] = cl == 4 * g4 + j ? ONE_LO : 0u;
+      im[j] = cl == 4 * g4 + j ? ONE_HI : 0u;
     }
   }
   const uint32_t bl = (uint32_t)opw[W_BL + (wave & 1) * 16 + cl];
@@ -369,7 +419,8 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
       const f4 pr = mfma(XL[0], IRE, z), pi = mfma(XL[0], IIM, z), lr = mfma(XL[1], IRE, z), li = mfma(XL[1], IIM, z);
       const uint4 A = make_uint4(pack_h2(pr[0], pi[0]), pack_h2(pr[1], pi[1]), pack_h2(pr[2], pi[2]), pack_h2(pr[3], pi[3]));
       const uint4 Br = make_uint4(pack_h2(lr[0], li[0]), pack_h2(lr[1], li[1]), pack_h2(lr[2], li[2]), pack_h2(lr[3], li[3]));
-      const uint4 Bi = make_uint4(mul_i(Br.x), mul_i(Br.y), mul_i(Br.z), mul_i(Br.w));
+      // i lambda = (-im, re), packed straight from the fp32 values (rounding is sign symmetric: exactly i Br)
+      const uint4 Bi = make_uint4(pack_h2(-li[0], lr[0]), pack_h2(-li[1], lr[1]), pack_h2(-li[2], lr[2]), pack_h2(-li[3], lr[3]));
       acc[0] = mfma(A, Br, acc[0]);
       acc[1] = mfma(A, Bi, acc[1]);
     }
@@ -511,21 +562,21 @@ __device__ __forceinline__ void group_back_t(uint32_t* tile, const uint4* F, con
   };
   auto compute_store = [&](int i, const uint4* X) {
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    f4 pr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[0]), z, 0, 0, 0);
-    f4 pi = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[1]), z, 0, 0, 0);
-    f4 lr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[0]), z, 0, 0, 0);
-    f4 li = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[1]), z, 0, 0, 0);
+    f4 pr = mfma(X[0], F[0], z);
+    f4 pi = mfma(X[0], F[1], z);
+    f4 lr = mfma(X[1], F[0], z);
+    f4 li = mfma(X[1], F[1], z);
     if (QFX_HEA_GATE_LO) {
-      pr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[2]), pr, 0, 0, 0);
-      pi = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[0]), __builtin_bit_cast(half8, F[3]), pi, 0, 0, 0);
-      lr = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[2]), lr, 0, 0, 0);
-      li = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(half8, X[1]), __builtin_bit_cast(half8, F[3]), li, 0, 0, 0);
+      pr = mfma(X[0], F[2], pr);
+      pi = mfma(X[0], F[3], pi);
+      lr = mfma(X[1], F[2], lr);
+      li = mfma(X[1], F[3], li);
     }
     // (re, im) of amplitude cl, columns 4 g4 + r: the stored values, the cross matrix's A (psi) and B (lambda,
     // i lambda = (-im, re): exactly i times the rounded lambda, rounding is sign symmetric)
     const uint4 P = make_uint4(pack_h2(pr[0], pi[0]), pack_h2(pr[1], pi[1]), pack_h2(pr[2], pi[2]), pack_h2(pr[3], pi[3]));
     const uint4 Lr = make_uint4(pack_h2(lr[0], li[0]), pack_h2(lr[1], li[1]), pack_h2(lr[2], li[2]), pack_h2(lr[3], li[3]));
-    const uint4 Li = make_uint4(mul_i(Lr.x), mul_i(Lr.y), mul_i(Lr.z), mul_i(Lr.w));
+    const uint4 Li = make_uint4(pack_h2(-li[0], lr[0]), pack_h2(-li[1], lr[1]), pack_h2(-li[2], lr[2]), pack_h2(-li[3], lr[3]));
     acc[0] = mfma(P, Lr, acc[0]);
     acc[1] = mfma(P, Li, acc[1]);
     const uint32_t bb = bh[i];
@@ -866,13 +917,13 @@ __device__ __forceinline__ uint32_t op_fo_global(const int* ow, uint32_t fixed) 
 // group g's slab row is W_GIDX + g.  sc: >= 96 float2 of scratch LDS.
 template <int NT, int TB, bool PL>
 __device__ __forceinline__ void l1prod_op(uint32_t* tile, const PassArgs& a, const int* opw, int tid, int s, int k,
-                                       uint32_t fixed, float rho, long long* slab, float2* sc) {
+                                       uint32_t fixed, float rho, long long* slab, float2* sc, int* emap,
+                                       float2& outer_s) {
   const int t = a.t, U = 1 << (t - 4), nlo = t - 4;
   float2* fw = sc;            // [32][2] true layer-1 factors w_q (memory bit q)
   float2* hb = sc + 64;       // [16] outer * prod_hi conj(w)
   float2* rj = sc + 80;       // [16] r_j
-  __shared__ float2 outer_s;
-  __shared__ int emap[TMAX];  // tile bit -> record entry, or -1
+  // emap [TMAX]: tile bit -> record entry, or -1; outer_s: product of the out-of-tile conj factors
   // ---- factors (wave 0: lane q computes qubit q's pair; the out-of-tile product over the wave)
   if (tid < 64) {
     float2 w[2] = {make_float2(1.f, 0.f), make_float2(1.f, 0.f)};
@@ -1048,7 +1099,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   const size_t N = (size_t)1 << a.n;
   const uint32_t fixed = tile_fixed(a, tile_id);
   const float* prm = a.params + (size_t)k * a.p_stride;
-  long long* dbg = (a.dbg && blockIdx.x < 8) ? a.dbg + blockIdx.x * 64 : nullptr;
+  long long* dbg = (QFX_HEA_MARKS && a.dbg && blockIdx.x < 8) ? a.dbg + blockIdx.x * 64 : nullptr;
   int ndbg = 0;
   HEA_MARK();
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
@@ -1360,6 +1411,8 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   __shared__ unsigned long long red64[NREG * RSTR];
   __shared__ int gmeta_s[NREG][2];                      // (slab index, nreal) of the region's gradient op
   __shared__ float rsc[CMAX + 2];
+  __shared__ int emap_s[TMAX];                          // OP_L1PROD: tile bit -> record entry
+  __shared__ float2 l1outer_s;                          // OP_L1PROD: out-of-tile conj factor product
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1368,12 +1421,25 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   const int T = 1 << a.t;
   const size_t N = (size_t)1 << a.n;
   const uint32_t fixed = tile_fixed(a, tile_id);
-  long long* dbg = (a.dbg && blockIdx.x < 8) ? a.dbg + blockIdx.x * 64 : nullptr;
+  long long* dbg = (QFX_HEA_MARKS && a.dbg && blockIdx.x < 8) ? a.dbg + blockIdx.x * 64 : nullptr;
   int ndbg = 0;
   HEA_MARK();
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
   long long* slab = a.gslab + ((size_t)s * a.slab_tiles + tile_id) * a.n_gradops * 32;
   QFX_DCHECK(tile_id < a.slab_tiles);
+  if (a.poison) {
+    poison_lds(tile, (int)sizeof(tile), a.poison, tid, NT);
+    poison_lds(&opw2[0][0], (int)sizeof(opw2), a.poison, tid, NT);
+    poison_lds(fidx_s, (int)sizeof(fidx_s), a.poison, tid, NT);
+    poison_lds(fo_s, (int)sizeof(fo_s), a.poison, tid, NT);
+    poison_lds(&frag_s[0][0], (int)sizeof(frag_s), a.poison, tid, NT);
+    poison_lds(red64, (int)sizeof(red64), a.poison, tid, NT);
+    poison_lds(&gmeta_s[0][0], (int)sizeof(gmeta_s), a.poison, tid, NT);
+    poison_lds(rsc, (int)sizeof(rsc), a.poison, tid, NT);
+    poison_lds(emap_s, (int)sizeof(emap_s), a.poison, tid, NT);
+    poison_lds(&l1outer_s, (int)sizeof(l1outer_s), a.poison, tid, NT);
+    lds_barrier();
+  }
 
   // op 0's record and fragments are requested before the tile load (their latency hides behind it)
   if (tid < a.nops) {
@@ -1545,7 +1611,8 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
     // the pass's last op: the fragment slots are free (no unitary here, none prefetched after it); its record was
     // staged during op nops - 2 (or before the loop)
     lds_barrier();
-    l1prod_op<NT, TB, PL>(tile, a, opw2[(a.nops - 1) & 1], tid, s, k, fixed, rsc[CMAX], slab, (float2*)&frag_s[0][0]);
+    l1prod_op<NT, TB, PL>(tile, a, opw2[(a.nops - 1) & 1], tid, s, k, fixed, rsc[CMAX], slab, (float2*)&frag_s[0][0],
+                          emap_s, l1outer_s);
   }
   if (a.store_lam) store_lam_il<NT, TB, PL>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
   HEA_MARK();
@@ -1577,7 +1644,7 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
   }
   // real output row r = 16 h + (lane & 15) is component cr = h (0 re, 1 im) of amplitude m' = lane & 15: a block's
   // result then holds the re and im of one amplitude in the same register of its two 16-row tiles
-  _Float16 hi[8], lo[8];
+  st_t hi[8], lo[8];
 #pragma unroll
   for (int jj = 0; jj < 8; ++jj) {
     const int kk = 8 * (lane >> 4) + jj;
@@ -1595,8 +1662,8 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
     }
     if (dag) v.y = -v.y;
     const float val = cr == 0 ? (ck == 0 ? v.x : -v.y) : (ck == 0 ? v.y : v.x);
-    hi[jj] = (_Float16)val;
-    lo[jj] = (_Float16)(val - (float)hi[jj]);
+    hi[jj] = (st_t)val;
+    lo[jj] = (st_t)(val - (float)hi[jj]);
   }
   uint4 H, Lw;
   uint32_t* hp = (uint32_t*)&H;
@@ -1621,6 +1688,7 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
 // from the complete gradient row (the readout-parameter entries were written by the readout launch before), with
 // the element update of qfx_adam_kernel (qfx_adam.h): bitwise the separate launch.  Every block has read its
 // parameters before it arrives.
+#if !QFX_HEA_BF16
 __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* __restrict__ gslab, int slab_tiles,
                                                               int n_gradops, const int* __restrict__ gmeta, int spc,
                                                               float* __restrict__ params,
@@ -1693,12 +1761,13 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     qfx_adam_elem(params, gi, ad.m, ad.v, ad.t_in, ad.t_out, ad.active, k, e, i == 0, ad.lr, ad.b1, ad.b2, ad.eps);
   }
 }
+#endif  // !QFX_HEA_BF16
 
-}  // namespace hea
+}  // namespace HEA_NS
 
-extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_samples, hipStream_t st) {
-  const hea::PassArgs& a = *args;
-  if (a.t > hea::TMAX || a.t < 8 || a.C > hea::CMAX || a.n > 30 || a.c < 2) return -2;
+extern "C" int HEA_EXT(qfx_hea_pass)(int adjoint, const HEA_NS::PassArgs* args, int n_samples, hipStream_t st) {
+  const HEA_NS::PassArgs& a = *args;
+  if (a.t > HEA_NS::TMAX || a.t < 8 || a.C > HEA_NS::CMAX || a.n > 30 || a.c < 2) return -2;
   const unsigned grid = (unsigned)((a.pair && !adjoint ? n_samples / 2 : n_samples) * a.n_tiles);
   if (grid == 0) return 0;
   static int planes = -1;   // adjoint LDS image: 0 interleaved (psi, lambda) pairs, 1 planes (QFEDX_HEA_PLANES)
@@ -1714,23 +1783,23 @@ extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_sample
 #define HEA_LAUNCH(NCK)                                                                                     \
   do {                                                                                                     \
     if (!adjoint && a.pair)                                                                                \
-      hipLaunchKernelGGL((hea::hea_fwd2_kernel<NCK>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);            \
-    else if (!adjoint && a.t == hea::TMAX)                                                                 \
-      hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK, true>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);       \
+      hipLaunchKernelGGL((HEA_NS::hea_fwd2_kernel<NCK>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);            \
+    else if (!adjoint && a.t == HEA_NS::TMAX)                                                                 \
+      hipLaunchKernelGGL((HEA_NS::hea_fwd_kernel<NCK, true>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);       \
     else if (!adjoint)                                                                                     \
-      hipLaunchKernelGGL((hea::hea_fwd_kernel<NCK, false>), dim3(grid), dim3(hea::NT_FWD), 0, st, a);      \
+      hipLaunchKernelGGL((HEA_NS::hea_fwd_kernel<NCK, false>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);      \
     else if (a.t <= 13 && planes)                                                                          \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, false, true, false>), dim3(grid), dim3(512), 0, st, a); \
+      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, true, false>), dim3(grid), dim3(512), 0, st, a); \
     else if (a.t <= 13 && fuse)                                                                            \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, false, false, true>), dim3(grid), dim3(512), 0, st, a); \
+      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, false, true>), dim3(grid), dim3(512), 0, st, a); \
     else if (a.t <= 13)                                                                                    \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 13, 8, false, false, false>), dim3(grid), dim3(512), 0, st, a); \
+      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, false, false>), dim3(grid), dim3(512), 0, st, a); \
     else if (fuse)                                                                                         \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14, 16, true, false, true>), dim3(grid), dim3(1024), 0, st, a); \
+      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 14, 16, true, false, true>), dim3(grid), dim3(1024), 0, st, a); \
     else                                                                                                   \
-      hipLaunchKernelGGL((hea::hea_adj_kernel<NCK, 14, 16, true, false, false>), dim3(grid), dim3(1024), 0, st, a); \
+      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 14, 16, true, false, false>), dim3(grid), dim3(1024), 0, st, a); \
   } while (0)
-  switch (hea::class_kernel(a.C)) {
+  switch (HEA_NS::class_kernel(a.C)) {
     case 1: HEA_LAUNCH(1); break;
     case 2: HEA_LAUNCH(2); break;
     case 3: HEA_LAUNCH(3); break;
@@ -1741,14 +1810,15 @@ extern "C" int qfx_hea_pass(int adjoint, const hea::PassArgs* args, int n_sample
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
+extern "C" int HEA_EXT(qfx_hea_frags)(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                              hipStream_t st) {
   if (n_slots == 0 || K == 0) return 0;
-  hipLaunchKernelGGL(hea::hea_frag_kernel, dim3(n_slots, K), dim3(256), 0, st, params, p_stride, slot_tab, n_slots,
+  hipLaunchKernelGGL(HEA_NS::hea_frag_kernel, dim3(n_slots, K), dim3(256), 0, st, params, p_stride, slot_tab, n_slots,
                      (uint4*)frags);
   return (int)hipGetLastError();
 }
 
+#if !QFX_HEA_BF16
 extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc,
                                    int K, float* params, float* grad, int p_stride, const QfxAdamArgs* adam,
                                    hipStream_t st) {
@@ -1756,16 +1826,17 @@ extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n
   if (n_gradops == 0) return adam && adam->m ? (int)hipErrorInvalidValue : 0;   // no block would run the epilogue
   QfxAdamArgs ad{};
   if (adam) ad = *adam;
-  hipLaunchKernelGGL(hea::hea_grad_reduce_kernel, dim3(K, n_gradops), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
+  hipLaunchKernelGGL(HEA_NS::hea_grad_reduce_kernel, dim3(K, n_gradops), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
                      gmeta, spc, params, grad, p_stride, ad);
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_hea_args_size() { return (int)sizeof(hea::PassArgs); }
+extern "C" int qfx_hea_args_size() { return (int)sizeof(HEA_NS::PassArgs); }
+#endif  // !QFX_HEA_BF16
 
 // Debug build: synchronise the stream and return (and clear) the first failed device-check line, 0 if none;
 // -1 in the release build (no checks compiled).
-extern "C" int qfx_hea_check_status(hipStream_t st) {
+extern "C" int HEA_EXT(qfx_hea_check_status)(hipStream_t st) {
 #if QFX_CHECKS_ON
   if (hipStreamSynchronize(st) != hipSuccess) return -2;
   unsigned int v = 0, z = 0;

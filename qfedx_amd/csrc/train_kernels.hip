@@ -400,31 +400,42 @@ struct SecAgg {
   double scale;
   long long mask;            // 2^bits - 1
   long long* masks;          // [K][P + 1] each client's total pair mask per element (qfx_secagg_mask_kernel)
+  int epb;                   // mask elements per Philox block: 2 (bits > 32, two words each) or 4 (bits <= 32)
 };
 
-// Every client's total pair mask, one thread per (client, element pair): one Philox block per peer yields the 48-bit
-// values of elements 2 b and 2 b + 1 (prg_mask's layout), so the K x N x (P + 1) / 2 generator calls - the work
-// each client would do on its own device - spread over the whole GPU.
+// Every client's total pair mask, one thread per (client, Philox block): one block per peer yields the values of
+// elements epb b .. epb b + epb - 1 in prg_mask's layout (bits > 32: two words per element, 2 elements; bits <= 32:
+// one word per element, 4 elements), so the K x N x (P + 1) / epb generator calls - the work each client would do on
+// its own device - spread over the whole GPU.
 __global__ void __launch_bounds__(256) qfx_secagg_mask_kernel(SecAgg sa, int P) {
   const int k = blockIdx.y;
-  const long b = (long)blockIdx.x * 256 + threadIdx.x;      // element pair
-  const long e0 = 2 * b;
+  const long b = (long)blockIdx.x * 256 + threadIdx.x;      // Philox block
+  const long e0 = (long)sa.epb * b;
   if (e0 > P) return;
   const uint32_t rnd = (uint32_t)sa.round[0];
-  long long a0 = 0, a1 = 0;
+  long long a[4] = {0, 0, 0, 0};
   for (int j = 0; j < sa.N; ++j) {
     const int sg = sa.sign[(size_t)k * sa.N + j];
     if (sg == 0) continue;
     const uint32_t* key = sa.seeds + ((size_t)k * sa.N + j) * 2;
     const u32x4 o = philox4x32_10({(uint32_t)b, (uint32_t)((uint64_t)b >> 32), rnd, 0x5ECu}, key[0], key[1]);
-    const long long m0 = (long long)(((uint64_t)o.y << 32 | o.x) & (uint64_t)sa.mask);
-    const long long m1 = (long long)(((uint64_t)o.w << 32 | o.z) & (uint64_t)sa.mask);
-    a0 += sg > 0 ? m0 : -m0;
-    a1 += sg > 0 ? m1 : -m1;
+    long long m[4];
+    if (sa.epb == 2) {
+      m[0] = (long long)(((uint64_t)o.y << 32 | o.x) & (uint64_t)sa.mask);
+      m[1] = (long long)(((uint64_t)o.w << 32 | o.z) & (uint64_t)sa.mask);
+      m[2] = m[3] = 0;
+    } else {
+      m[0] = (long long)((uint64_t)o.x & (uint64_t)sa.mask);
+      m[1] = (long long)((uint64_t)o.y & (uint64_t)sa.mask);
+      m[2] = (long long)((uint64_t)o.z & (uint64_t)sa.mask);
+      m[3] = (long long)((uint64_t)o.w & (uint64_t)sa.mask);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] += sg > 0 ? m[i] : -m[i];
   }
   long long* row = sa.masks + (size_t)k * (P + 1);
-  row[e0] = a0;
-  if (e0 + 1 <= P) row[e0 + 1] = a1;
+  for (int i = 0; i < sa.epb; ++i)
+    if (e0 + i <= P) row[e0 + i] = a[i];
 }
 
 __device__ __forceinline__ long long secagg_masks(const SecAgg& sa, int k, long e, int P) {
@@ -912,10 +923,12 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
     hipLaunchKernelGGL(qfx_delta_norm_final_kernel, dim3((K + 63) / 64), dim3(64), 0, st, partial, nc, K, norms);
   }
   const RoundPack rp{pack_buf, loss, correct, nvalid, act, n_metrics, (dp && norm_cid) ? norms : nullptr, norm_cid, K};
-  const SecAgg sa{sa_seeds, sa_sign, sa_round, sa_n, sa_scale, sa_seeds ? (1LL << sa_bits) - 1 : 0, sa_masks};
+  const int epb = sa_bits <= 32 ? 4 : 2;
+  const SecAgg sa{sa_seeds, sa_sign, sa_round, sa_n, sa_scale, sa_seeds ? (1LL << sa_bits) - 1 : 0, sa_masks, epb};
   if (sa_seeds) {
     if (!sa_masks) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(qfx_secagg_mask_kernel, dim3((unsigned)(((P + 2) / 2 + 255) / 256), (unsigned)K), dim3(256), 0,
+    const long nblk = (P + 1 + epb - 1) / epb;
+    hipLaunchKernelGGL(qfx_secagg_mask_kernel, dim3((unsigned)((nblk + 255) / 256), (unsigned)K), dim3(256), 0,
                        st, sa, P);
   }
   const unsigned blocks = (unsigned)((P + FA_E - 1) / FA_E) + (pack_buf ? 1u : 0u);

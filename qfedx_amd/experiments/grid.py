@@ -88,6 +88,8 @@ def summarize_run(cfg: ExperimentConfig, out: dict, run: Optional[dict] = None) 
         "rounds": len(hist), "wall_s": out.get("wall_s", 0.0),
         "gpu_hours": out.get("wall_s", 0.0) * ws / 3600.0 if str(out.get("device", "")).startswith("cuda") else 0.0,
         "comm_mb_per_round": (up + down) / n / 2 ** 20, "comm_mb_total": (up + down) / 2 ** 20,
+        # bytes each rank actually puts into the round's collective(s) (the all-reduce buffer as sized by the runner)
+        "collective_mb_per_round": sum(h.get("comm_bytes_per_rank", 0) for h in hist) / n / 2 ** 20,
         "n_params": P, "world_size": ws, "backend": out.get("backend"), "simulator": out.get("simulator"),
         "config": cfg.to_dict(),
     }

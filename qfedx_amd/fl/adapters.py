@@ -18,7 +18,16 @@ from .trainer import VQCClientTrainer
 def resolve_state_dtype(state_dtype: str, spec, backend: str, noise) -> str:
     """``auto``: the fp16 MFMA engine (ops/hea_mfma.py) on the HIP backend for the specs it covers (CNOT-chain
     or no entangler, angle features, >= 8 qubits, no gate noise; readout confusion and shots are applied by its
-    readout kernels), the fp32 VALU pass engine otherwise."""
+    readout kernels), the fp32 VALU pass engine otherwise.  ``bf16``: the bf16 MFMA engine (``mfma_bf16``) where the
+    MFMA engine applies, else bf16 storage on the VALU pass engine; ``bf16_valu`` forces the latter."""
+    if state_dtype == "bf16_valu":
+        return "bf16"
+    if state_dtype == "bf16":
+        if backend == "hip" and (noise is None or not noise.gate_noise):
+            from ..ops.hea_plan import eligible
+            if eligible(spec):
+                return "mfma_bf16"
+        return "bf16"
     if state_dtype != "auto":
         return state_dtype
     if backend == "hip" and (noise is None or not noise.gate_noise):

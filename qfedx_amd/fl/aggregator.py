@@ -97,7 +97,7 @@ class Aggregator:
                     from ..utils.device import h2d
                     parts = list(participants if participants is not None else client_ids)
                     n_all = max([self.num_clients] + [int(c) + 1 for c in parts + list(client_ids)])
-                    seeds, sign = self.secagg.round_tables(client_ids, parts, dropped or [], n_all)
+                    seeds, sign = self.secagg.round_tables(client_ids, parts, dropped or [], n_all, round_num)
                     secagg_tabs = (h2d(seeds, self.device), h2d(sign, self.device),
                                    h2d(torch.tensor([round_num], dtype=torch.int32), self.device))
                 sa = (*secagg_tabs, self.secagg.scale, self.secagg.bits)
@@ -138,7 +138,10 @@ class Aggregator:
             total = torch.remainder(total + sa.mask(weighted[k], int(cid), parts, round_num), sa.modulus)
         from ..privacy.secure_agg import prg_mask
         for d in dropped or []:
+            nb = set(sa.neighbors(int(d), parts, round_num))
             for cid in client_ids:
+                if int(cid) not in nb:
+                    continue
                 m = prg_mask(sa.registry.pair_seed(int(cid), int(d)), round_num, self.P + 1, sa.bits, delta.device)
                 total = total - m if int(cid) < int(d) else total + m
             total = torch.remainder(total, sa.modulus)

@@ -23,8 +23,8 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ..parallel.dist import (ShardedServerState, World, all_gather_cat, all_reduce_, barrier, broadcast_,
-                             shard_clients)
+from ..parallel.dist import (ShardedServerState, World, agree_graph_comm, all_gather_cat, all_reduce_, barrier,
+                             broadcast_, shard_clients)
 from ..privacy.accountant import RDPAccountant
 from ..privacy.dp import draw_noise_seed
 from ..privacy.secure_agg import SecureAggregator
@@ -92,7 +92,7 @@ class FederatedRunner:
         if p.secure_agg:
             # each client's DH secret comes from OS randomness on the rank hosting it; only public keys
             # are exchanged (all-gather), so no process holds another rank's client secrets
-            self.secagg = SecureAggregator(None, p.secagg_bits, p.secagg_scale)
+            self.secagg = SecureAggregator(None, p.secagg_bits, p.secagg_scale, getattr(p, "secagg_graph", "full"))
             self.secagg.setup(self.local_ids, world)
         self.aggregator = Aggregator(self.P, adapter.angle_mask(), device, backend, t.aggregate,
                                      t.wrap_angles, p.dp, p.clip_norm, p.noise_multiplier, p.secure_agg,
@@ -117,9 +117,18 @@ class FederatedRunner:
                                                  t.server_momentum)
         self.params = adapter.init_params(t.seed).to(device)
         broadcast_(self.params, world)                      # CC1: identical theta on all ranks
-        # CC6: per-client update norms in the round all-reduce (DP only: they drive the clipping)
+        # CC6: per-client update norms in the round all-reduce.  Opt-in NON-PRIVATE diagnostic: the raw pre-clip norms
+        # (and the clip fraction / quantiles logged from them) are computed from private data without noise and are
+        # not charged to the accountant, so a run that logs them is outside the epsilon it reports
         self.n_norm_slots = (self.num_clients if (p.dp and not p.secure_agg and
-                                                  getattr(cfg.runtime, "log_client_norms", True)) else 0)
+                                                  getattr(cfg.runtime, "log_client_norms", False)) else 0)
+        # CC2: the round's collective captured into the round hipGraph - decided ONCE, agreed by every rank (each
+        # rank captures and replays one all-reduce, compared bitwise with an eager one; fl/trainer.py keeps a per-shape
+        # eager fallback that preserves the collective order)
+        want = (bool(getattr(cfg.runtime, "graph_comm", True)) and backend == "hip" and self.server_opt is None
+                and torch.device(device).type == "cuda" and (not world.distributed or world.backend == "nccl"))
+        self.graph_comm = agree_graph_comm(world, want)
+        self.graph_comm_mode = ("captured" if self.graph_comm else "eager") if backend == "hip" else "none"
 
     # ------------------------------------------------------------------ eval
     @torch.no_grad()
@@ -233,7 +242,7 @@ class FederatedRunner:
                 # the round's tables; the fused reduce masks each client's ring element (K18), so the round stays
                 # one graph launch
                 extra["sa_seed"], extra["sa_sign"] = self.secagg.round_tables(ids, participants, dropped,
-                                                                              self.num_clients)
+                                                                              self.num_clients, r)
                 extra["sa_round"] = torch.full((len(ids),), r, dtype=torch.int32)
             if self.n_norm_slots and ids:
                 extra["cid"] = torch.tensor(ids, dtype=torch.int32)
@@ -260,8 +269,7 @@ class FederatedRunner:
                                  keys=tabs.get("dpkeys"), secagg_tabs=sa, norm_cid=tabs.get("cid"),
                                  pack=(buf, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
                                        tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)))
-            graph_comm = (getattr(self.cfg.runtime, "graph_comm", True)
-                          and (not self.world.distributed or self.world.backend == "nccl"))
+            graph_comm = self.graph_comm
             with self.timer.phase("local_train"):
                 res = trainer.run_round(self.store, local_alive, self.params, r, epilogue=epilogue,
                                         extra=extra or None, post=post if graph_comm else None)
@@ -298,6 +306,7 @@ class FederatedRunner:
                     nslots[torch.tensor(ids, device=dev)] = self.aggregator.last_norms.double().to(dev)
                 metrics = torch.cat([torch.stack([loss_sum, correct]).to(dev), host_m, sat, nslots])
         norms = None
+        comm_bytes = 0
         with self.timer.phase("comm"):
             if fast:
                 if res.get("post_done"):
@@ -307,6 +316,7 @@ class FederatedRunner:
                     self._flip ^= 1
                     post(v)
                 self._out_writes[v] += 1
+                comm_bytes = self._round_buf.numel() * 8
                 out = self._round_outs[v]
                 metrics = out[:5]                                     # + saturated fixed-point terms
                 norms = out[6:6 + NN] if NN else None
@@ -316,12 +326,15 @@ class FederatedRunner:
                 tail = torch.cat([contrib[P:P + 1].to(torch.int64),
                                   torch.round(metrics.double() * EXACT_SCALE).to(torch.int64)])
                 all_reduce_(tail, self.world)
+                # + the reduce-scatter of the padded update sums and the all-gather of the new parameter slices
+                comm_bytes = tail.numel() * 8 + 2 * self.server_opt.padded * 8
                 wsum = tail[0].double() / EXACT_SCALE
                 metrics = tail[1:].double() / EXACT_SCALE
                 self._set_params(self.server_opt.step(self.params, contrib[:P].to(torch.int64), wsum))
             elif p.secure_agg:
                 all_reduce_(contrib, self.world)          # int64 ring elements: exact, mod later
                 all_reduce_(metrics, self.world)
+                comm_bytes = contrib.numel() * contrib.element_size() + metrics.numel() * metrics.element_size()
                 mean_upd, wsum = self.aggregator.finalize(contrib)
                 self._set_params(self.aggregator.apply(self.params, mean_upd, wsum=wsum))
             else:
@@ -329,6 +342,7 @@ class FederatedRunner:
                 buf = torch.cat([contrib.to(torch.int64),
                                  torch.round(metrics.double() * EXACT_SCALE).to(torch.int64)])
                 all_reduce_(buf, self.world)
+                comm_bytes = buf.numel() * 8
                 mean_upd, wsum = self.aggregator.finalize(buf[: P + 1])
                 metrics = buf[P + 1:].double() / EXACT_SCALE
                 self._set_params(self.aggregator.apply(self.params, mean_upd, wsum=wsum))
@@ -343,7 +357,7 @@ class FederatedRunner:
                "_metrics": metrics, "_t0": t0,
                "_out_stamp": (v, self._out_writes[v]) if fast else None,
                "_norms": (norms, [c for c in participants if c not in dropped_set]) if norms is not None else None,
-               "comm_bytes_per_rank": int((self.P + 1 + 4) * 8),
+               "comm_bytes_per_rank": int(comm_bytes),
                "upload_bytes": int(len(participants) - len(dropped)) * (self.P + 1) * 4}
         if p.dp:
             rec["epsilon"] = self.accountant.get_epsilon(p.delta)
@@ -371,7 +385,8 @@ class FederatedRunner:
                 C = self.cfg.privacy.clip_norm
                 q = np.quantile(vals, [0.1, 0.5, 0.9])
                 rec.update({"clip_frac": float((vals > C).mean()), "norm_p10": float(q[0]), "norm_p50": float(q[1]),
-                            "norm_p90": float(q[2])})
+                            "norm_p90": float(q[2]),
+                            "norms_private": False})   # raw, un-noised statistics (runtime.log_client_norms)
         if len(m) > 4 and m[4] > 0:
             raise RuntimeError(f"round {rec['round']}: {int(m[4])} fixed-point FedAvg terms saturated at 2^53 "
                                "(|w * Delta| > 2^21): lower the aggregation weights (train.weighting=uniform) or "
@@ -416,5 +431,8 @@ class FederatedRunner:
         self.metrics.close()
         return {"model": self.adapter.state_dict(self.params), "params": self.params, "accuracies": accs,
                 "auc": auc,
-                "history": self.history, "wall_s": wall, "phases_ms": self.timer.resolve(),
+                "history": self.history, "wall_s": wall,
+                # mean ms per TIMED round of each phase and how many rounds were timed (on the GPU only every
+                # runtime.timer_every-th round is; raw totals would undercount the run by that factor)
+                "phases_ms_per_round": self.timer.per_phase(), "phase_rounds_timed": dict(self.timer.counts),
                 "epsilon": self.accountant.get_epsilon(self.cfg.privacy.delta) if self.cfg.privacy.dp else None}

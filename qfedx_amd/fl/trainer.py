@@ -433,10 +433,15 @@ class VQCClientTrainer:
                             out = body()
                             if ent["post_in_graph"]:
                                 post(v)
-                    except Exception:
+                    except Exception as exc:
                         if not ent["post_in_graph"]:
                             raise
-                        # the collective refused capture: graphs without it, post() runs eagerly
+                        # the collective refused capture although the ranks agreed it could be captured
+                        # (parallel/dist.py agree_graph_comm): graphs without it, post() runs eagerly right after
+                        # the replay - the same point of this rank's collective sequence, so ranks stay matched
+                        import warnings
+                        warnings.warn(f"round collective capture failed ({exc!r}); running it eagerly on this rank")
+                        self.capture_fallbacks = getattr(self, "capture_fallbacks", 0) + 1
                         self.graph_comm = False
                         ent["post_in_graph"] = False
                         torch.cuda.synchronize(dev)

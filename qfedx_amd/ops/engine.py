@@ -77,10 +77,10 @@ class VQCEngine:
             kraus = noise.kraus() if (noise is not None and noise.gate_noise) else None
             self.prog = DensityProgram(ops, coef, spec.n_qubits, spec.readout, self.device, kraus=kraus)
             self.hip = None
-        elif backend == "hip" and state_dtype in ("mfma", "fp16"):
-            # fp16 states + MFMA group unitaries (ops/hea_mfma.py) for the hardware-efficient ansatz
+        elif backend == "hip" and state_dtype in ("mfma", "fp16", "mfma_bf16"):
+            # fp16 (or bf16) states + MFMA group unitaries (ops/hea_mfma.py) for the hardware-efficient ansatz
             from .hea_mfma import HeaMfmaProgram
-            self.hip = HeaMfmaProgram(spec, self.device)
+            self.hip = HeaMfmaProgram(spec, self.device, storage="bf16" if state_dtype == "mfma_bf16" else "fp16")
             self.prog = TorchProgram(ops, coef, spec.n_qubits, self.device)
         elif backend == "hip":
             from .statevec_hip import HipProgram

@@ -60,7 +60,14 @@ FUSED_ADAM_MAX_BLOCKS = 256   # hea_grad_reduce blocks (clients x gradient ops) 
 
 
 class HeaMfmaProgram:
-    def __init__(self, spec, device, tile_bits: int | None = None, adj_tile_bits: int | None = None):
+    def __init__(self, spec, device, tile_bits: int | None = None, adj_tile_bits: int | None = None,
+                 storage: str = "fp16"):
+        """``storage``: fp16 (default) or bf16 (BASELINE config 2) amplitudes and unitary fragments
+        (csrc/hea_mfma_bf16.hip: v_mfma_f32_16x16x32_bf16, fp32 accumulation; 2^-9 per-op state rounding)."""
+        if storage not in ("fp16", "bf16"):
+            raise ValueError(f"MFMA engine storage must be fp16 | bf16, got {storage!r}")
+        self.storage = storage
+        self.bf16 = storage == "bf16"
         if not eligible(spec):
             raise ValueError("the MFMA engine covers angle-encoded RX/RZ + CNOT-chain VQCs with 8..30 qubits, "
                              "no gate noise and <= 8 classes")
@@ -197,12 +204,12 @@ class HeaMfmaProgram:
               pair: bool = False):
         return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
                 int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
-                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep), int(pair)]
+                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep), int(pair), int(self.bf16)]
 
     def _frags(self, params: torch.Tensor, K: int, tag: str = "") -> torch.Tensor:
         fr = self._buf(f"{tag}frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
         if self.n_slots:
-            ext().hea_frags(params, params.shape[1], self.slot_tab, self.n_slots, K, fr)
+            ext().hea_frags(params, params.shape[1], self.slot_tab, self.n_slots, K, fr, self.bf16)
         return fr
 
     def _forward(self, x, params, fr, K, B, part, store_last: bool = False, tag: str = "", after_first=None):

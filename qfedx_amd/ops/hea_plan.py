@@ -745,18 +745,33 @@ def _round16(z):
     return (z.real.astype(np.float16).astype(np.float64) + 1j * z.imag.astype(np.float16).astype(np.float64))
 
 
+def _bf16(x):
+    """float64 -> the bf16 value the kernel stores (fp32 first, then round-to-nearest-even to 8 significand bits,
+    as v_cvt_pk_bf16_f32 does)."""
+    u = np.asarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return u.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+def _round_bf16(z):
+    return _bf16(z.real) + 1j * _bf16(z.imag)
+
+
 def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp16: bool = False,
-            recompute_last: bool = False):
+            recompute_last: bool = False, storage: str | None = None):
     """Tile-exact execution of ``plan`` with the kernel's tables.
 
     xang [K, B, n] encoded feature angles, params [K, P] (theta first), wread [K, B, C] = dL/d<Z_c>.
     Returns expz [K, B, C] and (if wread is given) theta gradients [K, n_theta] summed over samples.
-    ``fp16`` rounds the stored amplitudes to half precision after every op (kernel storage format).
+    ``fp16`` rounds the stored amplitudes to half precision after every op (kernel storage format);
+    ``storage="bf16"`` to bf16 instead (the bf16 build, csrc/hea_mfma_bf16.hip).
     """
     n, t = plan.n, plan.t
     K, B, _ = xang.shape
     progs = pass_programs(plan, recompute_last=recompute_last)
-    rnd = _round16 if fp16 else (lambda z: z)
+    if storage is None:
+        storage = "fp16" if fp16 else "exact"
+    rnd = {"fp16": _round16, "bf16": _round_bf16, "exact": lambda z: z}[storage]
     scale = float(1 << (n // 2))
     expz = np.zeros((K, B, plan.C))
     grads = np.zeros((K, plan.n_theta))

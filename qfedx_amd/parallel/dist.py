@@ -244,3 +244,62 @@ class ShardedServerState:
         self.m = shard(sd["m"])
         if self.v is not None:
             self.v = shard(sd["v"])
+
+
+def graph_allreduce_selfcheck(world: World) -> bool:
+    """This rank's half of the captured-collective self-check: capture ONE all-reduce of a rank-dependent int64
+    buffer into a hipGraph.  Returns a callable that replays it and compares the result bitwise with an eager
+    all-reduce of the same buffer, or None when capture failed here.  The replay may only run once every rank has
+    captured (``agree_graph_comm``): a replay on some ranks alone would wait forever for the others."""
+    dev = world.device
+    x = torch.arange(4096, dtype=torch.int64, device=dev) * 7 + (world.rank + 1) * 1_000_003
+    try:
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):            # warm-up outside capture (communicator set up for this stream)
+            w = x.clone()
+            dist.all_reduce(w)
+        torch.cuda.current_stream(dev).wait_stream(side)
+        static = torch.zeros_like(x)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            dist.all_reduce(static)
+    except Exception:
+        return None
+
+    def replay_and_compare() -> bool:
+        eager = x.clone()
+        dist.all_reduce(eager)
+        static.copy_(x)
+        g.replay()
+        torch.cuda.synchronize(dev)
+        return bool(torch.equal(static, eager))
+    return replay_and_compare
+
+
+def _vote(ok: bool, world: World) -> bool:
+    """True iff every rank voted True (one eager MIN all-reduce)."""
+    if not world.distributed:
+        return ok
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64,
+                     device=world.device if world.backend == "nccl" else torch.device("cpu"))
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.item()))
+
+
+def agree_graph_comm(world: World, want: bool, probe=graph_allreduce_selfcheck) -> bool:
+    """Rank-agreed decision whether the round's collective is captured into the round hipGraph (CC2 on RCCL).
+
+    ``want`` must be the same on every rank (it comes from the shared config).  Each rank captures one all-reduce
+    (``probe``); the ranks vote, and only if ALL captured do they replay it and compare it bitwise with an eager
+    all-reduce, then vote again.  So either every rank captures its round collective or none does: a rank that
+    cannot capture never leaves the others replaying a collective it runs eagerly at another point of its stream.
+    Without a process group there is no collective in the graph and nothing to check."""
+    if not want:
+        return False
+    if not world.distributed:
+        return True
+    replay = probe(world)
+    if not _vote(replay is not None, world):
+        return False
+    return _vote(bool(replay()), world)

@@ -14,6 +14,13 @@ Protocol (Bonawitz et al. style, single round, honest-but-curious server):
     no float rounding), then decoded.
   * dropouts: if a masked client drops before its vector arrives, surviving peers reveal their pair
     seeds with the dropped client and the server removes the orphan masks (ROADMAP:91).
+  * mask graph: ``graph="full"`` (default) pairs every two participants - K (K - 1) / 2 pair masks per round, each
+    P elements long.  ``graph="sparse"`` is the SecAgg+ construction (Bell et al., CCS 2020): each participant pairs
+    only with its 2 ceil(log2 K) neighbours in a circulant graph over a round-keyed public permutation of the
+    participants, so the round generates O(K log K) masks instead of O(K^2).  Masks still cancel exactly and orphan
+    masks of dropped clients are removed the same way (only their graph neighbours reveal seeds).  The guarantee is
+    SecAgg+'s: the sum stays hidden unless the server corrupts or drops enough of a client's neighbourhood, a weaker
+    statement than the complete graph's.
 
 PRG = Philox4x32-10 keyed by the pair seed, counter = (element/4, round) - the same generator the
 HIP aggregation kernel uses on device: ``round_tables`` gives the fused FedAvg kernel
@@ -23,13 +30,23 @@ round, and the kernel masks each client's encoded update itself (the round stays
 from __future__ import annotations
 
 import hashlib
+import math
 import secrets
 from typing import Iterable, Optional
 
 import numpy as np
 import torch
 
-from ..utils.seeding import MASK32, derive_seed, philox4x32
+from ..utils.seeding import MASK32, derive_seed, np_rng, philox4x32
+
+GRAPH_KEY = 0x5EC6A   # the neighbour graph is public (a server could announce it): keyed by round, not by a secret
+
+
+def secagg_degree(k: int) -> int:
+    """SecAgg+ neighbours per participant among ``k``: 2 ceil(log2 k), at most k - 1 (then the graph is complete)."""
+    if k <= 1:
+        return 0
+    return min(k - 1, 2 * max(1, math.ceil(math.log2(k))))
 
 # RFC 3526 group 14 would be realistic; a 127-bit Mersenne prime keeps the simulation fast.
 _P = (1 << 127) - 1
@@ -112,11 +129,41 @@ def decode_fixed(v: torch.Tensor, scale: float, bits: int = 48) -> torch.Tensor:
 
 
 class SecureAggregator:
-    def __init__(self, session_seed: Optional[int] = None, bits: int = 48, scale: float = 2.0 ** 24):
+    def __init__(self, session_seed: Optional[int] = None, bits: int = 48, scale: float = 2.0 ** 24,
+                 graph: str = "full"):
+        if graph not in ("full", "sparse"):
+            raise ValueError(f"secagg graph must be full | sparse, got {graph!r}")
         self.registry = KeyRegistry(session_seed)
         self.bits = bits
         self.scale = scale
         self.modulus = 1 << bits
+        self.graph = graph
+        self._nb = (None, None)
+
+    def neighbors(self, client: int, participants: Iterable[int], round_num: int) -> list[int]:
+        """The peers ``client`` shares pair masks with this round (sorted).  Full graph: every other participant.
+        Sparse graph: the secagg_degree(K) / 2 predecessors and successors of ``client`` on a circle of the K
+        participants in a round-keyed public order - symmetric (j is i's neighbour iff i is j's), the same on every
+        rank without communication."""
+        client = int(client)
+        parts = tuple(sorted({int(c) for c in participants}))
+        if self.graph == "full" or secagg_degree(len(parts)) >= len(parts) - 1:
+            return [j for j in parts if j != client]
+        key = (parts, int(round_num))
+        if self._nb[0] != key:
+            K = len(parts)
+            order = [parts[i] for i in np_rng(GRAPH_KEY, "secagg_graph", int(round_num), K).permutation(K)]
+            pos = {c: i for i, c in enumerate(order)}
+            h = secagg_degree(K) // 2
+            self._nb = (key, {c: sorted({order[(pos[c] + d) % K] for d in range(1, h + 1)} |
+                                        {order[(pos[c] - d) % K] for d in range(1, h + 1)}) for c in parts})
+        return list(self._nb[1][client])
+
+    def table_width(self, num_clients: int) -> int:
+        """Peer columns of ``round_tables``: every client (full graph) or the largest neighbourhood any round
+        can have (sparse: the degree grows with the participant count, so this is its value at all clients - fixed,
+        so the round's hipGraph keeps one shape)."""
+        return num_clients if self.graph == "full" else max(1, secagg_degree(num_clients))
 
     def register(self, clients: Iterable[int]) -> None:
         for c in clients:
@@ -138,10 +185,7 @@ class SecureAggregator:
     def client_mask(self, client: int, participants: Iterable[int], round_num: int, P: int,
                     device="cpu") -> torch.Tensor:
         total = torch.zeros(P, dtype=torch.int64, device=device)
-        for j in participants:
-            j = int(j)
-            if j == client:
-                continue
+        for j in self.neighbors(client, participants, round_num):
             m = prg_mask(self.registry.pair_seed(client, j), round_num, P, self.bits, device)
             total = total + m if client < j else total - m
         return torch.remainder(total, self.modulus)
@@ -168,12 +212,15 @@ class SecureAggregator:
         return out
 
     def round_tables(self, clients: list[int], participants: Iterable[int], dropped: Iterable[int],
-                     num_clients: int) -> tuple[torch.Tensor, torch.Tensor]:
+                     num_clients: int, round_num: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
         """Device-kernel tables of one round for the masking clients ``clients`` (rows): pair-seed key words
-        int32 [K, N, 2] (lo, hi 32-bit halves) and mask signs int32 [K, N] over ALL N clients: +1 toward
-        participating peers j > i, -1 toward j < i, 0 for the client itself and non-participants.  A dropped
-        peer d's orphan mask is removed by the correction the survivors enable (``aggregate``); that exactly
-        cancels the survivor's mask toward d mod 2^bits, so its sign is 0 (net)."""
+        int32 [K, W, 2] (lo, hi 32-bit halves) and mask signs int32 [K, W], W = ``table_width``.  Full graph: column
+        j is client j; +1 toward participating peers j > i, -1 toward j < i, 0 for the client itself and
+        non-participants.  Sparse graph: row i lists its live neighbours (sign 0 pads).  A dropped peer d's orphan
+        mask is removed by the correction the survivors enable (``aggregate``); that exactly cancels the survivor's
+        mask toward d mod 2^bits, so its sign is 0 (net)."""
+        if self.graph == "sparse":
+            return self._sparse_tables(clients, participants, dropped, num_clients, round_num)
         K = len(clients)
         live = np.zeros(num_clients, dtype=bool)
         live[[int(c) for c in participants]] = True
@@ -186,15 +233,47 @@ class SecureAggregator:
         return (torch.from_numpy(words.view(np.int32).reshape(K, num_clients, 2).copy()),
                 torch.from_numpy(sign.reshape(K, num_clients)))
 
+    def _sparse_tables(self, clients, participants, dropped, num_clients, round_num):
+        W = self.table_width(num_clients)
+        parts = list(participants)
+        gone = {int(d) for d in dropped}
+        seeds = np.zeros((len(clients), W), dtype=np.uint64)
+        sign = np.zeros((len(clients), W), dtype=np.int32)
+        for r, c in enumerate(clients):
+            c = int(c)
+            live = [j for j in self.neighbors(c, parts, round_num) if j not in gone] if parts else []
+            if len(live) > W:
+                raise ValueError(f"client {c} has {len(live)} neighbours, table width {W}")
+            for col, j in enumerate(live):
+                seeds[r, col] = self.registry.pair_seed(c, j)
+                sign[r, col] = 1 if j > c else -1
+        words = np.stack([seeds & np.uint64(0xFFFFFFFF), seeds >> np.uint64(32)], -1).astype(np.uint32)
+        return (torch.from_numpy(words.view(np.int32).reshape(len(clients), W, 2).copy()),
+                torch.from_numpy(sign))
+
+    def orphan_pairs(self, survivors: Iterable[int], dropped: Iterable[int], participants: Iterable[int],
+                     round_num: int) -> list[tuple[int, int]]:
+        """(survivor i, dropped d) pairs whose seeds the survivors reveal: d is i's graph neighbour."""
+        parts = list(participants)
+        out = []
+        for d in dropped:
+            nb = set(self.neighbors(int(d), parts, round_num))
+            out += [(int(i), int(d)) for i in survivors if int(i) in nb]
+        return out
+
     def aggregate(self, masked: list[torch.Tensor], survivors: list[int], dropped: Optional[list[int]] = None,
                   round_num: int = 0) -> torch.Tensor:
         """Sum surviving masked vectors; remove orphan masks of ``dropped`` clients; decode."""
         total = torch.zeros_like(masked[0])
         for m in masked:
             total = torch.remainder(total + m, self.modulus)
+        parts = list(survivors) + list(dropped or [])
         for d in dropped or []:
-            # survivors reveal s_{i,d}: remove the mask each survivor i added toward d
+            # survivors reveal s_{i,d}: remove the mask each neighbouring survivor i added toward d
+            nb = set(self.neighbors(int(d), parts, round_num))
             for i in survivors:
+                if int(i) not in nb:
+                    continue
                 m = prg_mask(self.registry.pair_seed(i, d), round_num, total.numel(), self.bits, total.device)
                 total = total - m if i < d else total + m
             total = torch.remainder(total, self.modulus)

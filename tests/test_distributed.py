@@ -97,3 +97,49 @@ def test_sharded_server_state_checkpoint_resumes_at_other_world_size(tmp_path):
     _run(2, dict(num_rounds=2, checkpoint_every=1, checkpoint_dir=ck, **srv), tmp_path)
     resumed = run_experiment(small_cfg(num_rounds=4, checkpoint_every=1, checkpoint_dir=ck, resume=True, **srv))
     assert torch.equal(resumed["params"], full["params"])
+
+
+def _vote_worker(rank, world, port, votes, out_path):
+    """One rank of the captured-collective agreement: ``votes[rank]`` = (capture ok, replay matches eager)."""
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from qfedx_amd.parallel.dist import World, agree_graph_comm
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w = World(rank, world, rank, "gloo", torch.device("cpu"))
+    replayed = []
+
+    def probe(wd):                       # stands in for graph_allreduce_selfcheck (no capture on the CPU)
+        if not votes[rank][0]:
+            return None
+
+        def replay():
+            t = torch.ones(1)
+            dist.all_reduce(t)           # the replay is a collective: it must run on every rank or none
+            replayed.append(float(t))
+            return votes[rank][1]
+        return replay
+    res = agree_graph_comm(w, True, probe)
+    off = agree_graph_comm(w, False, probe)   # config says no: no collective, no probe
+    torch.save({"res": res, "off": off, "replayed": replayed}, f"{out_path}.{rank}")
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("votes,expect,replays", [
+    (((True, True), (True, True)), True, 1),      # every rank captured and the replay matched: captured
+    (((True, True), (False, True)), False, 0),    # rank 1 could not capture: NO rank replays, all run eagerly
+    (((True, True), (True, False)), False, 1),    # rank 1's replay differs from the eager all-reduce: all eager
+])
+def test_graph_comm_decision_is_rank_agreed(tmp_path, votes, expect, replays):
+    """Verdict r3 item 4a/b: whether the round collective is captured is decided once and by every rank.  A capture
+    failure (or a captured replay that differs bitwise from an eager all-reduce) on ONE of two gloo ranks makes both
+    ranks take the eager path; the self-check replay runs only when all ranks captured."""
+    out = str(tmp_path / "vote")
+    mp.spawn(_vote_worker, args=(2, _free_port(), votes, out), nprocs=2, join=True)
+    res = [torch.load(f"{out}.{r}", weights_only=True) for r in range(2)]
+    assert [r["res"] for r in res] == [expect, expect]
+    assert [r["off"] for r in res] == [False, False]
+    assert [len(r["replayed"]) for r in res] == [replays, replays]
+    assert all(v == 2.0 for r in res for v in r["replayed"])

@@ -285,13 +285,15 @@ def test_trainer_epilogue_and_extra_tables():
 
 
 def test_dp_rounds_log_client_norms_and_clip_fraction():
-    """CC6: under DP every round record carries the clip fraction and norm quantiles of the participating clients'
-    pre-clip update norms (gathered through the round's all-reduce buffer)."""
+    """CC6 (opt-in, non-private diagnostic): under DP with runtime.log_client_norms every round record carries the clip
+    fraction and norm quantiles of the participating clients' pre-clip update norms (gathered through the round's
+    all-reduce buffer), flagged norms_private=False; off by default."""
     cfg = small_cfg(num_rounds=3, dp=True, clip_norm=0.05, noise_multiplier=0.5, num_clients=5, client_fraction=1.0,
-                    deterministic_noise=True)
+                    deterministic_noise=True, log_client_norms=True)
     out = run_experiment(cfg)
     for h in out["history"]:
         assert 0.0 <= h["clip_frac"] <= 1.0 and h["norm_p10"] <= h["norm_p50"] <= h["norm_p90"]
     assert out["history"][0]["norm_p50"] > 0
-    cfg2 = small_cfg(num_rounds=1, dp=True, num_clients=3, log_client_norms=False)
+    assert all(h["norms_private"] is False for h in out["history"])
+    cfg2 = small_cfg(num_rounds=1, dp=True, num_clients=3)
     assert "clip_frac" not in run_experiment(cfg2)["history"][0]

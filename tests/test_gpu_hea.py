@@ -57,6 +57,36 @@ def test_hea_vjp_matches_dense(cuda, n, L, tile, chain, feat):
     np.testing.assert_allclose(g.cpu().numpy(), g_ref.numpy(), atol=4e-3 * scale)
 
 
+@pytest.mark.parametrize("n,L,tile", [(10, 3, 14), (12, 4, 9), (13, 3, 10), (16, 3, 14)])
+def test_hea_vjp_matches_dense_bf16(cuda, n, L, tile):
+    """bf16 MFMA engine (BASELINE config 2, csrc/hea_mfma_bf16.hip): <Z> and gradients against the float64 oracle,
+    within 3x the error of the tile-exact emulator with bf16 rounding after every op (+ 5e-4 for the fp32 MFMA
+    accumulation and the hi + lo bf16 gate split, which the emulator does not model); plus the fp16 engine's
+    results are closer to the oracle (11 vs 8 significand bits)."""
+    from qfedx_amd.ops import hea_plan as hp
+    spec = VQCSpec(n, L, 3)
+    prog = HeaMfmaProgram(spec, cuda, tile_bits=tile, storage="bf16")
+    K, B = 2, 3
+    x, params, wr = _inputs(spec, K, B)
+    ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
+    ez_e, g_e = hp.emulate(prog.plan, x.double().numpy(), params.double().numpy(), wr.double().numpy(), storage="bf16")
+    z, g = prog.vjp(x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda))
+    z16, g16 = HeaMfmaProgram(spec, cuda, tile_bits=tile).vjp(x.to(cuda), params[:, : spec.n_theta].to(cuda),
+                                                                wr.to(cuda))
+    torch.cuda.synchronize()
+    zr = ez_ref.numpy()
+    ez_err = np.abs(ez_e - zr).max()
+    g_err = np.abs(g_e - g_ref.numpy()).max()
+    err_z = np.abs(z.cpu().reshape(K, B, -1).numpy() - zr).max()
+    err_g = np.abs(g.cpu().numpy() - g_ref.numpy()).max()
+    assert err_z <= 3 * ez_err + 5e-4, (err_z, ez_err)
+    assert err_g <= 3 * g_err + 5e-4, (err_g, g_err)
+    assert np.abs(z16.cpu().reshape(K, B, -1).numpy() - zr).max() < err_z
+    # deterministic: a second call is bitwise the first
+    z2, g2 = prog.vjp(x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda))
+    assert torch.equal(z, z2) and torch.equal(g, g2)
+
+
 def test_hea_train_step_matches_valu_engine(cuda):
     """Loss, a/b and theta gradients of a 16-qubit 3-layer step vs the fp32 VALU engine."""
     spec = VQCSpec(16, 3, 3, readout_scale=2.0)

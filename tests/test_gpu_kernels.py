@@ -366,12 +366,37 @@ def test_padded_inactive_client_rows_mfma(cuda):
     assert not loss_pad[:, 3].any() and not corr_pad[:, 3].any()
 
 
-@pytest.mark.parametrize("dp", [False, True])
-def test_secagg_masks_in_fused_reduce_match_host_protocol(cuda, dp):
+def test_secagg_sparse_graph_in_fused_reduce_match_host_protocol(cuda):
+    """SecAgg+ neighbour graph on the device: the mask kernel walks each client's compact neighbour table (width
+    secagg_degree(N)) and the masked local sum is bitwise the host protocol's, dropped neighbours included."""
+    from qfedx_amd.fl.aggregator import Aggregator
+    from qfedx_amd.privacy.secure_agg import SecureAggregator
+    K, P, N = 6, 257, 64
+    g = torch.Generator().manual_seed(9)
+    tk = torch.randn(K, P, generator=g) * 0.3
+    tg = torch.randn(P, generator=g)
+    w = torch.rand(K, generator=g).double() * 40 + 1
+    ids = [3, 8, 11, 20, 29, 40]
+    participants = sorted(set(ids) | {1, 2, 7, 9, 14, 25, 33, 38, 41, 47, 50, 52, 55, 58, 60, 63})
+    dropped = [7, 25, 50]
+    sa = SecureAggregator(123, graph="sparse")
+    assert len(sa.neighbors(3, participants, 4)) < len(participants) - 1
+    kw = dict(dp=False, seed=5, secure_agg=True, secagg=sa, num_clients=N)
+    cpu = Aggregator(P, torch.zeros(P), "cpu", "torch", wrap=False, **kw)
+    gpu = Aggregator(P, torch.zeros(P), cuda, "hip", wrap=False, **kw)
+    a = cpu.local_reduce(tk, tg, w, 4, ids, participants=participants, dropped=dropped)
+    b = gpu.local_reduce(tk.to(cuda), tg.to(cuda), w.to(cuda), 4, ids, participants=participants, dropped=dropped)
+    m = (1 << sa.bits) - 1
+    assert torch.equal(b.cpu() & m, a & m)
+
+
+@pytest.mark.parametrize("dp,bits", [(False, 48), (True, 48), (False, 32), (True, 32)])
+def test_secagg_masks_in_fused_reduce_match_host_protocol(cuda, dp, bits):
     """SecAgg on the device (K18): the fused FedAvg kernel masks every local client's ring element with the pairwise
     Philox masks itself.  Without DP the masked local sum is bitwise the host SecureAggregator's (mod 2^48),
     including the orphan-mask correction of dropped peers on and off this rank; with DP (and angle wrap) the decoded
-    update matches to fixed-point resolution.  The round-apply kernel decodes the ring sum like finalize + apply."""
+    update matches to fixed-point resolution.  The round-apply kernel decodes the ring sum like finalize + apply.
+    At bits <= 32 the device mask uses prg_mask's one-word-per-element layout (4 elements per Philox block)."""
     from qfedx_amd.fl.aggregator import Aggregator
     from qfedx_amd.ops._ext import ext
     from qfedx_amd.privacy.secure_agg import SecureAggregator
@@ -386,7 +411,7 @@ def test_secagg_masks_in_fused_reduce_match_host_protocol(cuda, dp):
     ids = [3, 8, 11, 20, 29]                      # this rank's surviving clients
     participants = [1, 2, 3, 7, 8, 11, 20, 25, 29]
     dropped = [7, 25]                             # 7 was local, 25 on another rank
-    sa = SecureAggregator(123)
+    sa = SecureAggregator(123, bits=bits, scale=2.0 ** 24 if bits > 32 else 2.0 ** 16)
     kw = dict(dp=dp, clip_norm=0.9, noise_multiplier=0.7, seed=5, secure_agg=True, secagg=sa, num_clients=N)
     cpu = Aggregator(P, mask, "cpu", "torch", wrap=dp, **kw)
     gpu = Aggregator(P, mask, cuda, "hip", wrap=dp, **kw)
@@ -416,7 +441,7 @@ def test_dp_client_norms_ride_in_round_buffer(cuda):
     from qfedx_amd.api import run_experiment
     from qfedx_amd.parallel.dist import init_distributed
     kw = dict(num_rounds=2, dp=True, clip_norm=0.05, noise_multiplier=0.5, num_clients=5, deterministic_noise=True,
-              optimizer="sgd")
+              optimizer="sgd", log_client_norms=True)
     cpu = run_experiment(small_cfg(**kw))
     dev = torch.device("cuda", 0)
     gpu = run_experiment(small_cfg(device="cuda", backend="hip", **kw), world=init_distributed(dev), device=dev,

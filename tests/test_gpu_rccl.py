@@ -64,5 +64,32 @@ def test_bench_rccl_single_rank():
     assert len(recs) == 1
     rec = recs[0]
     assert rec["dist_backend"] == "nccl" and rec["engine"] == "mfma" and rec["value"] > 0
+    # the startup self-check (one captured all-reduce replay == an eager one) passed: the round collective runs
+    # inside the round hipGraph on the RCCL communicator torch.distributed reports
+    assert rec["rccl_world_size"] == 1 and rec["graph_comm"] == "captured", rec
     assert rec["comm_ms"] >= 0 and rec["local_train_ms"] > 0
     assert rec["max_abs_err_expz"] < 5e-3 and rec["max_abs_err_grad"] < 5e-3 * max(1.0, rec["max_abs_grad"])
+
+
+_SELFCHECK = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from qfedx_amd.parallel.dist import init_distributed, shutdown, graph_allreduce_selfcheck, agree_graph_comm
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+world = init_distributed(dev, "nccl")
+replay = graph_allreduce_selfcheck(world)
+ok1 = replay is not None and replay()
+ok2 = agree_graph_comm(world, True)
+shutdown(world)
+print("RESULT", int(ok1), int(ok2))
+"""
+
+
+def test_captured_allreduce_selfcheck_rccl():
+    """The startup self-check on a real RCCL communicator: one all-reduce captured in a hipGraph, replayed, equals an
+    eager all-reduce bitwise, and the (one-rank) vote agrees on capturing the round collective."""
+    r = subprocess.run([sys.executable, "-c", _SELFCHECK.format(root=ROOT)], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "RESULT 1 1" in r.stdout, r.stdout[-2000:]

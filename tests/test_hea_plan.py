@@ -49,6 +49,35 @@ def test_emulated_plan_matches_dense(n, L, t, chain, feat):
         np.testing.assert_array_equal(gr4, gr3)
 
 
+def test_bf16_rounding_matches_hardware_conversion():
+    """_bf16 is round-to-nearest-even on the fp32 bits (v_cvt_pk_bf16_f32): ties go to the even significand."""
+    x = np.array([1.0, 1.0 + 2 ** -8, 1.0 + 3 * 2 ** -8, 1.0 + 2 ** -9, -1.5 - 2 ** -9, 3.0e38, 1e-40], np.float64)
+    got = hp._bf16(x)
+    assert got[0] == 1.0
+    assert got[1] == 1.0                       # 1 + 2^-8 is a tie between 1 and 1 + 2^-7: to even (1)
+    assert got[2] == 1.0 + 2 ** -6             # 1 + 3 2^-8 tie: to even (1 + 2^-6)
+    assert got[3] == 1.0 and got[4] == -1.5
+    assert np.isfinite(got[5]) and abs(got[6]) < 1e-38
+
+
+@pytest.mark.parametrize("n,L,t", [(10, 3, 8), (12, 3, 9), (11, 2, 10)])
+def test_emulated_bf16_storage_error_band(n, L, t):
+    """bf16 state storage (BASELINE config 2) on the tile-exact emulator: errors vs the float64 dense oracle are
+    above fp16's (8 vs 11 significand bits) and inside the band the bf16 GPU tests use (tests/test_gpu_hea.py)."""
+    spec = VQCSpec(n, L, 3)
+    plan = hp.build_plan(n, L, spec.readout, True, "ry", tile_bits=t)
+    g = torch.Generator().manual_seed(n + L)
+    x = torch.rand(2, 2, n, generator=g, dtype=torch.float64) * 3
+    params = torch.randn(2, spec.n_params, generator=g, dtype=torch.float64)
+    wr = torch.randn(2, 2, 3, generator=g, dtype=torch.float64)
+    ez, gr = _dense(spec, x, params, wr)
+    e16, g16 = hp.emulate(plan, x.numpy(), params.numpy(), wr.numpy(), storage="fp16")
+    eb, gb = hp.emulate(plan, x.numpy(), params.numpy(), wr.numpy(), storage="bf16")
+    sc = max(1.0, np.abs(gr).max())
+    assert np.abs(eb - ez).max() < 2.5e-2 and np.abs(gb - gr).max() < 3e-2 * sc
+    assert np.abs(eb - ez).max() > np.abs(e16 - ez).max()
+
+
 @pytest.mark.parametrize("n,L,passes", [(16, 3, 2), (16, 2, 2), (20, 2, 2), (20, 3, 2), (24, 2, 3), (12, 3, 1)])
 def test_plan_shapes(n, L, passes):
     plan = hp.build_plan(n, L, [0, 1, 2])
