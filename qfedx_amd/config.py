@@ -76,6 +76,7 @@ class TrainConfig:
     server_lr: float = 1.0
     server_momentum: float = 0.9
     eval_every: int = 1
+    fuse_optimizer: bool = True         # HIP CFed: SGD-momentum step fused into the gradient kernels (csrc/cnn_args.h)
     seed: int = 42
 
 

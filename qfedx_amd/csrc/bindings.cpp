@@ -401,7 +401,7 @@ void batch_gather(torch::Tensor X, torch::Tensor Y, torch::Tensor lid, torch::Te
 void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<torch::Tensor> m,
                     c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> t, torch::Tensor X, torch::Tensor Y,
                     torch::Tensor lid, torch::Tensor idx, int64_t mode, double alpha, torch::Tensor x_out,
-                    torch::Tensor y_out) {
+                    torch::Tensor y_out, bool rows) {
   need(theta, torch::kFloat32, "theta");
   need(params, torch::kFloat32, "params");
   const int64_t K = params.size(0), P = params.size(1);
@@ -425,7 +425,9 @@ void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<tor
   if (idx.size(1) != K || lid.numel() != K || x_out.dim() != 4 || x_out.size(0) != S || x_out.size(1) != K ||
       x_out.size(2) != B || x_out.size(3) < F || y_out.numel() < S * K * B || mode < 0 || mode > 2)
     throw std::invalid_argument("round_prologue: output shapes / mode");
-  check(qfx_launch_round_prologue(ptr<float>(theta), (int)K, (int)P, ptr<float>(params), ptr<float>(mt), ptr<float>(vt),
+  // rows = false: params only gives the [K, P] shape (the first local step reads theta; CFed fused SGD)
+  check(qfx_launch_round_prologue(ptr<float>(theta), (int)K, (int)P, rows ? ptr<float>(params) : nullptr, ptr<float>(mt),
+                                  ptr<float>(vt),
                                   ptr<float>(tt), tt.defined() ? (int)tt.numel() : 0, ptr<float>(X),
                                   ptr<long long>(Y), ptr<long long>(lid), ptr<long long>(idx), (int)S, (int)B,
                                   (long)X.size(1), (int)F, (int)mode, (float)alpha, ptr<float>(x_out),
@@ -597,7 +599,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("flag") = py::none());
   m.def("batch_plan", &qfx_runtime::batch_plan);
   m.def("batch_gather", &batch_gather);
-  m.def("round_prologue", &round_prologue);
+  m.def("round_prologue", &round_prologue, pybind11::arg("theta"), pybind11::arg("params"), pybind11::arg("m"),
+        pybind11::arg("v"), pybind11::arg("t"), pybind11::arg("X"), pybind11::arg("Y"), pybind11::arg("lid"),
+        pybind11::arg("idx"), pybind11::arg("mode"), pybind11::arg("alpha"), pybind11::arg("x_out"),
+        pybind11::arg("y_out"), pybind11::arg("rows") = true);
   m.def("amp_scratch", &amp_scratch);
   m.def("readout_noise", &readout_noise);
   m.def("philox_uniform", &philox_uniform);

@@ -17,6 +17,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "cnn_args.h"
 #include "philox.h"
 
 namespace qfx {
@@ -40,6 +41,23 @@ constexpr int K2 = 400;            // conv2 reduction (ci,dy,dx)
 struct CnnOff {                    // float offsets of the tensors inside one client's parameter row
   int w1, b1, w2, b2;
 };
+
+// One gradient entry of client k (row stride P) into its sink (cnn_args.h): the gradient row, or the fused SGD step.
+__device__ __forceinline__ void sink_put(const CnnSgd& sg, int P, int k, long e, float g) {
+  if (!sg.pout) {
+    sg.grad[(size_t)k * P + e] = g;
+    return;
+  }
+  const float pin = sg.pin[(size_t)k * sg.pstride + e];
+  float out = pin;
+  if (sg.act[k] != 0.f) {
+    const bool first = sg.t_in[k] == 0.f;   // the momentum buffer is the gradient on the first step (never read)
+    const float b = first ? g : fmaf(sg.mu, sg.buf[(size_t)k * P + e], g);
+    if (sg.keep) sg.buf[(size_t)k * P + e] = b;
+    out = pin - sg.lr * b;
+  }
+  sg.pout[(size_t)k * P + e] = out;
+}
 
 // --------------------------------------------------------------------------------------------
 // layout probe: D[16x16] = A[16xK] B[Kx16] with one wave (tests pin the MFMA operand layout)
@@ -641,8 +659,8 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
   }
 }
 
-// grad[k][dst(e)] = sum_g part[k*G + g][e]   (fixed order over groups)
-__global__ void cnn_reduce(const float* __restrict__ part, int G, float* __restrict__ grad, int P, CnnOff off) {
+// grad[k][dst(e)] = sum_g part[k*G + g][e]   (fixed order over groups), into the gradient sink
+__global__ void cnn_reduce(const float* __restrict__ part, int G, CnnSgd sg, int P, CnnOff off) {
   const int k = blockIdx.y;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= PART) return;
@@ -653,7 +671,7 @@ __global__ void cnn_reduce(const float* __restrict__ part, int G, float* __restr
   else if (e < C2 * K2 + C2) dst = off.b2 + (e - C2 * K2);
   else if (e < C2 * K2 + C2 + C1 * K1) dst = off.w1 + (e - C2 * K2 - C2);
   else dst = off.b1 + (e - C2 * K2 - C2 - C1 * K1);
-  grad[(size_t)k * P + dst] = sacc;
+  sink_put(sg, P, k, dst, sacc);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -676,11 +694,11 @@ constexpr int HG = (CMAXC * HID + CMAXC + 255) / 256;   // fc2 gradient entries 
 __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, int off_b1,
                                                 const float* __restrict__ mask, const long long* __restrict__ dkeys,
                                                 unsigned drop_stream, float drop_p, float drop_scale,
-                                                const float* __restrict__ params, int P, int off_w, int off_b,
-                                                int C, int B, const long long* __restrict__ y,
+                                                const float* __restrict__ params, long pstride, int P, int off_w,
+                                                int off_b, int C, int B, const long long* __restrict__ y,
                                                 const float* __restrict__ wts, float* __restrict__ dh1,
                                                 float* __restrict__ dlog, float* __restrict__ loss,
-                                                float* __restrict__ correct, float* __restrict__ grad) {
+                                                float* __restrict__ correct, CnnSgd sg) {
   __shared__ float Ws[CMAXC * HID];
   __shared__ float bs[CMAXC];
   __shared__ float b1s[HID];               // fc1 bias
@@ -689,7 +707,7 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
   __shared__ float dl[HB][CMAXC + 1];      // logits, then weighted dlogits
   __shared__ float lsb[HB], csb[HB];       // per-sample weighted loss / correct flag
   const int k = blockIdx.x, tid = threadIdx.x;
-  const float* prow = params + (size_t)k * P;
+  const float* prow = params + (size_t)k * pstride;
   for (int e = tid; e < C * HID; e += 256) Ws[e] = prow[off_w + e];
   if (tid < C) bs[tid] = prow[off_b + tid];
   if (tid < HID) b1s[tid] = prow[off_b1 + tid];
@@ -772,16 +790,19 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
     if (tid < HID)   // fc1 bias gradient: sum over samples of dh1 (fixed order)
       for (int b = 0; b < nb; ++b) db1 += hv[b][tid];
   }
-  if (tid < HID) grad[(size_t)k * P + off_b1 + tid] = db1;
+  // the fc2 weights / biases and the fc1 bias were staged in LDS before the chunk loop: an in-place SGD step of the
+  // same row (sg.pin == params) cannot race this block's reads
+  if (tid < HID) sink_put(sg, P, k, off_b1 + tid, db1);
 #pragma unroll
   for (int m = 0; m < HG; ++m) {
     const int e = tid + m * 256;
-    if (e < C * HID) grad[(size_t)k * P + off_w + e] = gacc[m];
-    else if (e < C * HID + C) grad[(size_t)k * P + off_b + (e - C * HID)] = gacc[m];
+    if (e < C * HID) sink_put(sg, P, k, off_w + e, gacc[m]);
+    else if (e < C * HID + C) sink_put(sg, P, k, off_b + (e - C * HID), gacc[m]);
   }
   if (tid == 0) {
     loss[k] = lsum;
     correct[k] = csum;
+    if (sg.pout) sg.t_out[k] = sg.t_in[k] + sg.act[k];
   }
 }
 
@@ -793,7 +814,7 @@ __global__ void __launch_bounds__(256) cnn_head(const float* __restrict__ h1, in
 // all 40 loads of a chunk in flight before its MFMAs.  Bandwidth-bound: pool2 read + gradient write once.
 // --------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) cnn_fc1_wgrad(const float* __restrict__ dh1, const float* __restrict__ pool2,
-                                                     int B, float* __restrict__ grad, int P, int off_w1) {
+                                                     int B, CnnSgd sg, int P, int off_w1) {
   const int k = blockIdx.y, c0 = blockIdx.x * 64;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -817,12 +838,12 @@ __global__ void __launch_bounds__(256) cnn_fc1_wgrad(const float* __restrict__ d
 #pragma unroll
       for (int nt = 0; nt < 4; ++nt) acc[nt] = mfma(a[ks], b[ks][nt], acc[nt]);
   }
-  float* g = grad + (size_t)k * P + off_w1 + (size_t)(wave * 16 + 4 * kq) * F1IN + c0 + i;
+  const long e0 = off_w1 + (long)(wave * 16 + 4 * kq) * F1IN + c0 + i;
 #pragma unroll
   for (int nt = 0; nt < 4; ++nt)
     if (c0 + nt * 16 + i < F1IN)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) g[(size_t)r * F1IN + nt * 16] = acc[nt][r];
+      for (int r = 0; r < 4; ++r) sink_put(sg, P, k, e0 + (long)r * F1IN + nt * 16, acc[nt][r]);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1055,9 +1076,11 @@ static int bwd_bs(int /*K*/, int B) {
   return bs;
 }
 
-extern "C" int qfx_cnn_backward(const float* X, const float* params, int P, int K, int B, const int* off4,
-                                const float* pool1, const uint8_t* am1, const float* pool2, const uint8_t* am2,
-                                const float* dP2, float* part, float* grad, hipStream_t st) {
+// params: read rows with stride pstride (0: every client reads theta); gradients (row stride P) into the sink
+extern "C" int qfx_cnn_backward(const float* X, const float* params, int pstride, int P, int K, int B,
+                                const int* off4, const float* pool1, const uint8_t* am1, const float* pool2,
+                                const uint8_t* am2, const float* dP2, float* part, const CnnSgd* sink,
+                                hipStream_t st) {
   const int bs = bwd_bs(K, B), G = (B + bs - 1) / bs;
   const CnnOff off{off4[0], off4[1], off4[2], off4[3]};
   static bool attr = false;
@@ -1065,27 +1088,27 @@ extern "C" int qfx_cnn_backward(const float* X, const float* params, int P, int 
     (void)hipFuncSetAttribute((const void*)cnn_bwd, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bwd_lds());
     attr = true;
   }
-  hipLaunchKernelGGL(cnn_bwd, dim3(K * G), dim3(NT), bwd_lds(), st, X, params, P, B, G, off, pool1, am1, pool2, am2,
-                     dP2, bs, part);
-  hipLaunchKernelGGL(cnn_reduce, dim3((PART + 255) / 256, K), dim3(256), 0, st, part, G, grad, P, off);
+  hipLaunchKernelGGL(cnn_bwd, dim3(K * G), dim3(NT), bwd_lds(), st, X, params, pstride, B, G, off, pool1, am1, pool2,
+                     am2, dP2, bs, part);
+  hipLaunchKernelGGL(cnn_reduce, dim3((PART + 255) / 256, K), dim3(256), 0, st, part, G, *sink, P, off);
   return (int)hipGetLastError();
 }
 
 extern "C" int qfx_cnn_head(const float* h1, int off_b1, const float* mask, const long long* dkeys,
-                            unsigned drop_stream, float drop_p, float drop_scale, const float* params, int P, int off_w,
-                            int off_b, int C, int K, int B, const long long* y, const float* wts, float* dh1,
-                            float* dlog, float* loss, float* correct, float* grad, hipStream_t st) {
+                            unsigned drop_stream, float drop_p, float drop_scale, const float* params, int pstride,
+                            int P, int off_w, int off_b, int C, int K, int B, const long long* y, const float* wts,
+                            float* dh1, float* dlog, float* loss, float* correct, const CnnSgd* sink, hipStream_t st) {
   if (C > CMAXC) return -2;
   if (!mask && !dkeys) return -3;
   hipLaunchKernelGGL(cnn_head, dim3(K), dim3(256), 0, st, h1, off_b1, mask, dkeys, drop_stream, drop_p, drop_scale,
-                     params, P, off_w, off_b, C, B, y, wts, dh1, dlog, loss, correct, grad);
+                     params, (long)pstride, P, off_w, off_b, C, B, y, wts, dh1, dlog, loss, correct, *sink);
   return (int)hipGetLastError();
 }
 
-extern "C" int qfx_cnn_fc1_wgrad(const float* dh1, const float* pool2, int K, int B, float* grad, int P, int off_w1,
-                                 hipStream_t st) {
+extern "C" int qfx_cnn_fc1_wgrad(const float* dh1, const float* pool2, int K, int B, const CnnSgd* sink, int P,
+                                 int off_w1, hipStream_t st) {
   if (K <= 0 || B <= 0) return 0;
-  hipLaunchKernelGGL(cnn_fc1_wgrad, dim3((F1IN + 63) / 64, K), dim3(256), 0, st, dh1, pool2, B, grad, P, off_w1);
+  hipLaunchKernelGGL(cnn_fc1_wgrad, dim3((F1IN + 63) / 64, K), dim3(256), 0, st, dh1, pool2, B, *sink, P, off_w1);
   return (int)hipGetLastError();
 }
 

@@ -26,6 +26,8 @@ int qfx_hea_pass_bf16(int adjoint, const HeaPassArgs* args, int n_samples, hipSt
 int qfx_hea_frags_bf16(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                        hipStream_t st);
 int qfx_hea_check_status_bf16(hipStream_t st);
+int qfx_hea_set_knob(const char* name, int value);
+int qfx_hea_set_knob_bf16(const char* name, int value);
 }
 
 namespace {
@@ -236,6 +238,11 @@ void register_hea(pybind11::module& m) {
   m.def("hea_frags", &hea_frags, pybind11::arg("params"), pybind11::arg("p_stride"), pybind11::arg("slot_tab"),
         pybind11::arg("n_slots"), pybind11::arg("K"), pybind11::arg("frags"), pybind11::arg("bf16") = false);
   m.def("hea_check_ops", &hea_check_ops);
+  // launch-variant knobs of both storage builds (planes | fuse | adj_waves); returns the previous fp16-build value
+  m.def("hea_set_knob", [](const std::string& name, int value) {
+    qfx_hea_set_knob_bf16(name.c_str(), value);
+    return qfx_hea_set_knob(name.c_str(), value);
+  });
   m.def("hea_grad_reduce", &hea_grad_reduce, pybind11::arg("gslab"), pybind11::arg("slab_tiles"),
         pybind11::arg("n_gradops"), pybind11::arg("gmeta"), pybind11::arg("spc"), pybind11::arg("K"),
         pybind11::arg("params"), pybind11::arg("grad"), pybind11::arg("p_stride"),

@@ -21,6 +21,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 
 // Storage type of the states and unitary fragments: fp16 (this translation unit) or bf16 (hea_mfma_bf16.hip includes
 // this file with QFX_HEA_BF16=1: the same kernels in namespace hea_bf16, entry points suffixed _bf16).  Only the
@@ -56,6 +57,10 @@ __device__ unsigned int qfx_check_word = 0;
 // only (fp16-rounded gate: half the apply MFMAs).
 #ifndef QFX_HEA_GATE_LO
 #define QFX_HEA_GATE_LO 1
+#endif
+// LDS poison fill (a.poison, QFEDX_HEA_POISON): compiled in unless -DQFX_HEA_POISON=0
+#ifndef QFX_HEA_POISON
+#define QFX_HEA_POISON 1
 #endif
 // Phase timestamps (HEA_MARK, a.dbg) exist only in timing builds: in release builds the stamp pointer folds to null
 // and its bookkeeping (a pointer and a counter live across the op loop) leaves the kernels' scalar registers free.
@@ -419,8 +424,11 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
       const f4 pr = mfma(XL[0], IRE, z), pi = mfma(XL[0], IIM, z), lr = mfma(XL[1], IRE, z), li = mfma(XL[1], IIM, z);
       const uint4 A = make_uint4(pack_h2(pr[0], pi[0]), pack_h2(pr[1], pi[1]), pack_h2(pr[2], pi[2]), pack_h2(pr[3], pi[3]));
       const uint4 Br = make_uint4(pack_h2(lr[0], li[0]), pack_h2(lr[1], li[1]), pack_h2(lr[2], li[2]), pack_h2(lr[3], li[3]));
-      // i lambda = (-im, re), packed straight from the fp32 values (rounding is sign symmetric: exactly i Br)
+#if QFX_HEA_BF16   // i lambda = (-im, re) packed straight from fp32 (rounding is sign symmetric: exactly i Br)
       const uint4 Bi = make_uint4(pack_h2(-li[0], lr[0]), pack_h2(-li[1], lr[1]), pack_h2(-li[2], lr[2]), pack_h2(-li[3], lr[3]));
+#else
+      const uint4 Bi = make_uint4(mul_i(Br.x), mul_i(Br.y), mul_i(Br.z), mul_i(Br.w));
+#endif
       acc[0] = mfma(A, Br, acc[0]);
       acc[1] = mfma(A, Bi, acc[1]);
     }
@@ -576,7 +584,11 @@ __device__ __forceinline__ void group_back_t(uint32_t* tile, const uint4* F, con
     // i lambda = (-im, re): exactly i times the rounded lambda, rounding is sign symmetric)
     const uint4 P = make_uint4(pack_h2(pr[0], pi[0]), pack_h2(pr[1], pi[1]), pack_h2(pr[2], pi[2]), pack_h2(pr[3], pi[3]));
     const uint4 Lr = make_uint4(pack_h2(lr[0], li[0]), pack_h2(lr[1], li[1]), pack_h2(lr[2], li[2]), pack_h2(lr[3], li[3]));
+#if QFX_HEA_BF16   // i lambda = (-im, re) packed straight from fp32 (one cvt; the bf16 mul_i is two instructions)
     const uint4 Li = make_uint4(pack_h2(-li[0], lr[0]), pack_h2(-li[1], lr[1]), pack_h2(-li[2], lr[2]), pack_h2(-li[3], lr[3]));
+#else              // (the packed form pushed the fp16 kernels' register allocation into spills)
+    const uint4 Li = make_uint4(mul_i(Lr.x), mul_i(Lr.y), mul_i(Lr.z), mul_i(Lr.w));
+#endif
     acc[0] = mfma(P, Lr, acc[0]);
     acc[1] = mfma(P, Li, acc[1]);
     const uint32_t bb = bh[i];
@@ -1427,7 +1439,7 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
   long long* slab = a.gslab + ((size_t)s * a.slab_tiles + tile_id) * a.n_gradops * 32;
   QFX_DCHECK(tile_id < a.slab_tiles);
-  if (a.poison) {
+  if (QFX_HEA_POISON && a.poison) {
     poison_lds(tile, (int)sizeof(tile), a.poison, tid, NT);
     poison_lds(&opw2[0][0], (int)sizeof(opw2), a.poison, tid, NT);
     poison_lds(fidx_s, (int)sizeof(fidx_s), a.poison, tid, NT);
@@ -1763,23 +1775,40 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
 }
 #endif  // !QFX_HEA_BF16
 
+// Launch-variant knobs (A/B in one process: scripts/hea_ab.py): defaults from the environment, settable at run time.
+enum { K_PLANES = 0, K_FUSE = 1, K_ADJ_WAVES = 2, K_COUNT = 3 };
+static int knob_v[K_COUNT] = {-1, -1, -1};
+inline int knob(int k) {
+  if (knob_v[k] < 0) {
+    static const char* env[K_COUNT] = {"QFEDX_HEA_PLANES", "QFEDX_HEA_FUSE", "QFEDX_HEA_ADJ_WAVES"};
+    static const int dflt[K_COUNT] = {0, 1, 8};
+    const char* e = getenv(env[k]);
+    knob_v[k] = e ? atoi(e) : dflt[k];
+  }
+  return knob_v[k];
+}
+
 }  // namespace HEA_NS
+
+// name: planes | fuse | adj_waves (4 or 8: waves of a 2^13 adjoint workgroup); returns the previous value, -1 unknown
+extern "C" int HEA_EXT(qfx_hea_set_knob)(const char* name, int value) {
+  static const char* names[HEA_NS::K_COUNT] = {"planes", "fuse", "adj_waves"};
+  for (int k = 0; k < HEA_NS::K_COUNT; ++k)
+    if (strcmp(name, names[k]) == 0) {
+      const int prev = HEA_NS::knob(k);
+      HEA_NS::knob_v[k] = value;
+      return prev;
+    }
+  return -1;
+}
 
 extern "C" int HEA_EXT(qfx_hea_pass)(int adjoint, const HEA_NS::PassArgs* args, int n_samples, hipStream_t st) {
   const HEA_NS::PassArgs& a = *args;
   if (a.t > HEA_NS::TMAX || a.t < 8 || a.C > HEA_NS::CMAX || a.n > 30 || a.c < 2) return -2;
   const unsigned grid = (unsigned)((a.pair && !adjoint ? n_samples / 2 : n_samples) * a.n_tiles);
   if (grid == 0) return 0;
-  static int planes = -1;   // adjoint LDS image: 0 interleaved (psi, lambda) pairs, 1 planes (QFEDX_HEA_PLANES)
-  if (planes < 0) {
-    const char* e = getenv("QFEDX_HEA_PLANES");
-    planes = e ? (atoi(e) != 0) : 0;
-  }
-  static int fuse = -1;     // BACK ops: cross matrix from the apply's registers (QFEDX_HEA_FUSE, default on)
-  if (fuse < 0) {
-    const char* e = getenv("QFEDX_HEA_FUSE");
-    fuse = e ? (atoi(e) != 0) : 1;
-  }
+  const int planes = HEA_NS::knob(HEA_NS::K_PLANES), fuse = HEA_NS::knob(HEA_NS::K_FUSE);
+  const int wv4 = HEA_NS::knob(HEA_NS::K_ADJ_WAVES) == 4;
 #define HEA_LAUNCH(NCK)                                                                                     \
   do {                                                                                                     \
     if (!adjoint && a.pair)                                                                                \
@@ -1790,6 +1819,8 @@ extern "C" int HEA_EXT(qfx_hea_pass)(int adjoint, const HEA_NS::PassArgs* args, 
       hipLaunchKernelGGL((HEA_NS::hea_fwd_kernel<NCK, false>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);      \
     else if (a.t <= 13 && planes)                                                                          \
       hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, true, false>), dim3(grid), dim3(512), 0, st, a); \
+    else if (a.t <= 13 && fuse && wv4)                                                                     \
+      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 4, false, false, true>), dim3(grid), dim3(256), 0, st, a); \
     else if (a.t <= 13 && fuse)                                                                            \
       hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, false, true>), dim3(grid), dim3(512), 0, st, a); \
     else if (a.t <= 13)                                                                                    \

@@ -738,7 +738,7 @@ extern "C" int qfx_launch_sgdm(float* p, const float* g, float* buf, const float
 struct RoundInit {
   const float* theta;
   int K, P;
-  float *params, *m, *v, *t;   // m / v / t may be null
+  float *params, *m, *v, *t;   // params / m / v / t may be null (params: the first local step reads theta directly)
   int nt;
 };
 
@@ -749,7 +749,7 @@ __device__ __forceinline__ void round_init_chunk(const RoundInit& ri, int k, int
   for (int u = 0; u < SG_U; ++u) {
     const int e = e0 + u * 256;
     if (e < ri.P) {
-      ri.params[row + e] = ri.theta[e];
+      if (ri.params) ri.params[row + e] = ri.theta[e];
       if (ri.m) ri.m[row + e] = 0.f;
       if (ri.v) ri.v[row + e] = 0.f;
     }
@@ -889,11 +889,15 @@ extern "C" int qfx_launch_round_prologue(const float* theta, int K, int P, float
                                          const long long* idx, int steps, int B, long nmax, int F, int mode,
                                          float alpha, float* xo, int x_stride, long long* yo, hipStream_t st) {
   if (K <= 0 || P <= 0) return 0;
-  const int chunks = (P + SG_E - 1) / SG_E;
-  const long blocks = (long)K * chunks + (long)steps * K * B;
+  // without client rows or moments to set, only the step counters need a block (chunk 0 of row 0)
+  const bool rows = params || m || v;
+  const int chunks = rows ? (P + SG_E - 1) / SG_E : (t ? 1 : 0);
+  const int kinit = rows ? K : (t ? 1 : 0);
+  const long blocks = (long)kinit * chunks + (long)steps * K * B;
   if (blocks > 0x7fffffffL) return (int)hipErrorInvalidValue;
+  if (blocks == 0) return 0;
   hipLaunchKernelGGL(qfx_round_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                     RoundInit{theta, K, P, params, m, v, t, nt}, chunks,
+                     RoundInit{theta, kinit, P, params, m, v, t, nt}, chunks,
                      BatchGather{X, Y, lid, idx, K, B, nmax, F, mode, alpha, xo, x_stride, yo});
   return (int)hipGetLastError();
 }

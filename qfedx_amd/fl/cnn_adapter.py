@@ -29,9 +29,11 @@ class CNNClientTrainer:
             from ..ops.cnn_hip import HipTinyCNN
             self._hip = HipTinyCNN(num_classes, self.device)
 
-    def loss_and_grads(self, params, xb, yb, wts, mask, loss_out=None, correct_out=None):
+    def loss_and_grads(self, params, xb, yb, wts, mask, loss_out=None, correct_out=None, sgd=None):
         if self._hip is not None:
-            return self._hip.loss_and_grads(params, xb, yb, wts, mask, loss_out, correct_out)
+            return self._hip.loss_and_grads(params, xb, yb, wts, mask, loss_out, correct_out, sgd=sgd)
+        if sgd is not None:
+            raise ValueError("the fused SGD step exists on the HIP backend only")
         p = params.detach().requires_grad_(True)
         logits = tc.batched_forward(p, xb, self.C, mask)
         nll = F.cross_entropy(logits.reshape(-1, self.C), yb.reshape(-1), reduction="none").reshape(yb.shape)
@@ -75,6 +77,11 @@ class CNNClientTrainer:
         loss_all = torch.empty(S, K, dtype=torch.float32, device=self.device)
         correct_all = torch.empty(S, K, dtype=torch.float32, device=self.device)
         fused = self.backend == "hip" and store.X.is_cuda
+        # SGD-momentum fused into the gradient-producing kernels (HIP): the round's first step reads theta broadcast
+        # and writes the stepped client rows, so no row init, no gradient buffer and no optimizer launch
+        fuse_sgd = fused and self._hip is not None and opt.kind in ("sgd", "sgdm", "spsa") and \
+            getattr(cfg, "fuse_optimizer", True)
+        theta_dev = theta_g.to(self.device).float().contiguous()
         upfront = False
         if fused:   # minibatches gathered straight from the device store by slot (no per-round shard copy)
             from ..ops._ext import ext
@@ -90,10 +97,10 @@ class CNNClientTrainer:
             rows = dv["lid"][:, None]
         if upfront:
             m, v, t = opt.init_state()
-            ext().round_prologue(theta_g.to(self.device).float().contiguous(), params, m, v, t, Xf, store.y,
-                                 dv["lid"], dv["idx"].contiguous(), 2, 1.0, xbuf, ybuf)
+            ext().round_prologue(theta_dev, params, m, v, t, Xf, store.y, dv["lid"], dv["idx"].contiguous(), 2, 1.0,
+                                 xbuf, ybuf, rows=not fuse_sgd)
         else:
-            opt.init_round(params, theta_g.to(self.device).float())
+            opt.init_round(params, theta_dev)
         for s in range(S):
             if upfront:
                 xb, yb = xbuf[s].view(K, B, *img), ybuf.view(S, K, B)[s]
@@ -107,8 +114,13 @@ class CNNClientTrainer:
                 mask = ("philox", dv["dkeys"], s, 0.5)
             else:
                 mask = tc.dropout_masks(cids, cfg.batch_size, cfg.seed, round_num, s, self.device)
-            res = self.loss_and_grads(params, xb, yb, dv["wts"][s], mask, loss_all[s], correct_all[s])
-            opt.step(params, res["grad"], dv["act"][s], last=s == S - 1)
+            if fuse_sgd:
+                sgd = dict(opt.fused_sgdm(last=s == S - 1), pout=params, act=dv["act"][s])
+                pin = theta_dev.expand(K, P) if s == 0 else params
+                res = self.loss_and_grads(pin, xb, yb, dv["wts"][s], mask, loss_all[s], correct_all[s], sgd=sgd)
+            else:
+                res = self.loss_and_grads(params, xb, yb, dv["wts"][s], mask, loss_all[s], correct_all[s])
+                opt.step(params, res["grad"], dv["act"][s], last=s == S - 1)
             if res["loss"].data_ptr() != loss_all[s].data_ptr():    # portable path: separate outputs
                 loss_all[s].copy_(res["loss"])
                 correct_all[s].copy_(res["correct"])

@@ -80,6 +80,19 @@ class BatchedOptimizer:
         return ([self.m, self.v, t_in, t_out, active.float().contiguous()],
                 [float(self.lr), float(self.b1), float(self.b2), float(self.eps)])
 
+    def fused_sgdm(self, last: bool = False) -> Optional[dict]:
+        """Hand this step's SGD-momentum update to the kernels that produce the gradient (the CFed step kernels'
+        sink, csrc/cnn_args.h): returns the state they update (momentum rows, step-counter ping-pong, lr, mu, keep)
+        and does ``step``'s bookkeeping, or None when that path does not apply (not HIP SGD)."""
+        if self.kind not in ("sgd", "sgdm", "spsa") or self.backend != "hip" or not self.m.is_cuda:
+            return None
+        if not self._fresh:
+            raise RuntimeError("BatchedOptimizer(zero_init=False): call init_round() or reset() first")
+        t_in, t_out = self._t[self._phase], self._t[1 - self._phase]
+        self._phase ^= 1
+        return {"buf": self.m, "t_in": t_in, "t_out": t_out, "lr": float(self.lr), "mu": float(self.momentum),
+                "keep": not last}
+
     @torch.no_grad()
     def step(self, params: torch.Tensor, grads: torch.Tensor, active: Optional[torch.Tensor] = None,
              last: bool = False) -> None:

@@ -8,9 +8,14 @@ One local step of K clients x B samples:
                         would depend on how clients are sharded over ranks)
   3. ``cnn_head``     - fc1 partials (fixed order) + bias + ReLU + keyed dropout + fc2 + weighted CE, dlogits, fc2
                         grads, dL/dh1, fc1 bias grad
-  4. fc1 backward     - ``cnn_fc1_wgrad`` (weight grad into the gradient rows) + ``cnn_fc1_dgrad`` (dL/dpool2)
+  4. fc1 backward     - ``cnn_fc1_dgrad`` (dL/dpool2) then ``cnn_fc1_wgrad`` (weight grad into the gradient rows)
   5. ``cnn_backward`` - unpool + ReLU masks, conv2 weight/input grads, conv1 weight grads (MFMA),
                         deterministic fixed-order reduction into the flat [K, P] gradient
+With ``sgd`` (``loss_and_grads``) the local SGD-momentum step is fused into the kernels that produce the gradient
+entries (head: fc2 + fc1 bias, fc1_wgrad: fc1 weights, the conv reduction: conv weights + biases; cnn_args.h): the
+gradient is never written or re-read and no optimizer launch runs.  The first local step of a round may read the
+global parameters broadcast (``theta.expand(K, P)``, row stride 0) and write the stepped client rows, so the round
+prologue sets no per-client rows.
 No autograd graph, no per-client Python loop, no library kernels; every buffer is sized [K, ...] once per shape.
 Evaluation (reference ``evaluate_model``, ``Classical_FL.py:83-102``) runs the same conv + fc1 kernels and
 ``cnn_eval_head`` (logits, fused CE / argmax-hit sums).
@@ -83,18 +88,27 @@ class HipTinyCNN:
     @torch.no_grad()
     def loss_and_grads(self, params: torch.Tensor, xb: torch.Tensor, yb: torch.Tensor, wts: torch.Tensor,
                        mask, loss_out: torch.Tensor | None = None,
-                       correct_out: torch.Tensor | None = None) -> dict:
+                       correct_out: torch.Tensor | None = None, sgd: dict | None = None) -> dict:
         """``mask``: [K, B, 64] dropout mask, ``None`` (no dropout) or ``("philox", keys, stream, p)`` - per-client
         device Philox keys [K, 2] from which the head draws the inverted-dropout mask itself (u >= p kept x
         1/(1-p): ``tinycnn.dropout_masks``' exact values).  ``loss_out`` / ``correct_out``: optional contiguous fp32 [K] rows the head
-        writes into directly."""
+        writes into directly.  ``sgd``: fuse the local SGD-momentum step (dict pout, buf, t_in, t_out, act, lr, mu,
+        keep; cnn_args.h): ``params`` are the rows read (``theta.expand(K, P)`` on a round's first step) and the
+        stepped rows go to ``pout``; the returned ``grad`` is then None."""
         C = ext()
-        params = params.float().contiguous()
+        if params.stride(0) != 0:
+            params = params.float().contiguous()
         K, B = xb.shape[:2]
         S = K * B
         Xf, pool1, am1, pool2, am2 = self.conv_forward(params, xb)
         h1 = self._fc1(params, pool2, K, B)                            # partial sums; the head adds them + bias
-        grad = torch.empty(K, self.P, dtype=torch.float32, device=self.device)   # every entry is written below
+        if sgd is None:
+            grad = torch.empty(K, self.P, dtype=torch.float32, device=self.device)   # every entry is written below
+            sk = hy = None
+        else:
+            grad = torch.empty(0, 0, dtype=torch.float32, device=self.device)
+            sk = [params, sgd["pout"], sgd["buf"], sgd["t_in"], sgd["t_out"], sgd["act"].float().contiguous()]
+            hy = [float(sgd["lr"]), float(sgd["mu"]), 1.0 if sgd["keep"] else 0.0]
         dh1 = self._buf("dh1", (K, B, 64))
         dlog = self._buf("dlog", (S, 16))
         loss = loss_out if loss_out is not None else torch.empty(K, dtype=torch.float32, device=self.device)
@@ -107,11 +121,12 @@ class HipTinyCNN:
             m = mask.float().contiguous() if mask is not None else torch.ones(K, B, 64, device=self.device)
             dk, dst, dp, ds = None, 0, 0.0, 1.0
         C.cnn_head(h1, self.fc1b, m, dk, dst, dp, ds, params, self.fc2w, self.fc2b, self.C, K, B, yb.reshape(S).long().contiguous(),
-                   wts.reshape(S).float().contiguous(), dh1, dlog, loss, correct, grad)
-        C.cnn_fc1_wgrad(dh1, pool2, K, B, grad, self.fc1w)      # written straight into the gradient rows
+                   wts.reshape(S).float().contiguous(), dh1, dlog, loss, correct, grad, sk, hy)
+        # dL/dpool2 reads the fc1 weights BEFORE the weight-gradient launch may step them in place (fused SGD)
         dP2 = self._buf("dP2", (S, 1568))
         C.cnn_fc1_dgrad(dh1, params, self.fc1w, K, B, dP2)
+        C.cnn_fc1_wgrad(dh1, pool2, K, B, grad, self.fc1w, sk, hy)      # straight into the gradient rows / step
         G = C.cnn_bwd_groups(K, B)
         part = self._buf("part", (K * G, C.cnn_partial_size()))
-        C.cnn_backward(Xf, params, K, B, self.off_conv, pool1, am1, pool2, am2, dP2, part, grad)
-        return {"loss": loss, "grad": grad, "correct": correct}
+        C.cnn_backward(Xf, params, K, B, self.off_conv, pool1, am1, pool2, am2, dP2, part, grad, sk, hy)
+        return {"loss": loss, "grad": grad if sgd is None else None, "correct": correct}

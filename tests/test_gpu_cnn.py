@@ -103,6 +103,45 @@ def test_cfed_federated_run_hip_matches_cpu(cuda):
     assert abs(gpu["accuracies"][-1] - cpu["accuracies"][-1]) < 0.02
 
 
+@pytest.mark.parametrize("local_epochs,momentum", [(1, 0.9), (2, 0.5)])
+def test_cfed_fused_sgd_step_bitwise(cuda, local_epochs, momentum):
+    """The SGD-momentum step fused into the gradient-producing kernels (cnn_args.h; the first local step reading theta
+    broadcast, no row init, no gradient buffer, no optimizer launch) is bitwise the separate qfx_sgdm launch: several
+    local steps with unequal non-IID shards (rows going inactive), momentum carried across steps."""
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.config import ExperimentConfig
+    from qfedx_amd.parallel.dist import init_distributed
+
+    def cfg(fuse):
+        c = ExperimentConfig()
+        c.model.kind = "tinycnn"
+        c.data.num_clients = 5
+        c.data.samples_per_client = 48
+        c.data.partition_type = "non_iid"
+        c.data.test_samples = 64
+        c.train.num_rounds = 2
+        c.train.local_epochs = local_epochs
+        c.train.optimizer = "sgd"
+        c.train.momentum = momentum
+        c.train.learning_rate = 0.05
+        c.train.batch_size = 16
+        c.train.aggregate = "weights"
+        c.train.wrap_angles = False
+        c.train.fuse_optimizer = fuse
+        c.runtime.device = "cuda"
+        c.runtime.backend = "hip"
+        c.runtime.log_every = 100
+        return c
+
+    dev = torch.device("cuda", 0)
+    a = run_experiment(cfg(True), world=init_distributed(dev), device=dev, backend="hip")
+    b = run_experiment(cfg(False), world=init_distributed(dev), device=dev, backend="hip")
+    assert torch.equal(a["params"], b["params"])
+    assert a["accuracies"] == b["accuracies"]
+    assert [h["train_loss"] for h in a["history"]] == [h["train_loss"] for h in b["history"]]
+    assert max(h["local_steps"] for h in a["history"]) > 5         # several steps per client per round
+
+
 def test_head_dropout_from_uniforms_matches_mask(cuda):
     """The head drawing the inverted-dropout mask from the clients' Philox keys gives bit-identical results to the
     materialised ``dropout_masks`` tensor."""
