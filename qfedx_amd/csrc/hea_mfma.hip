@@ -340,6 +340,13 @@ __device__ __forceinline__ void lds_st(uint32_t* tile, uint32_t byte, uint32_t v
 }
 
 
+// (int)floor(x + 0.5f) in one instruction (round half up; the compiler's rint + convert is two)
+__device__ __forceinline__ int cvt_rpi(float x) {
+  int r;
+  __asm__("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 // i * (re, im) = (-im, re) on a packed fp16 pair: dst.lo = src.hi * (-1), dst.hi = src.lo * 1
 __device__ __forceinline__ uint32_t mul_i(uint32_t v) {
 #if QFX_HEA_BF16
@@ -965,23 +972,34 @@ __device__ __forceinline__ void l1prod_op(uint32_t* tile, const PassArgs& a, con
     hb[tid] = v;
   }
   lds_barrier();
-  // ---- r's terms lambda[u, j] A_u: every lambda word is read by exactly one thread, so thread u overwrites its own
-  // 16 (psi, lambda) slots with them right away (no barrier, no registers held); c_u accumulates on the way
+  // ---- r's terms lambda[u, j] A_u: every lambda word is read by exactly one thread; all of them are read (and c_u
+  // accumulated) before a barrier, then thread u writes its 16 terms over its own (psi, lambda) slots
   float2 c = make_float2(0.f, 0.f);
   const bool act = tid < U;
   const uint32_t h0 = swz(a, (uint32_t)tid >> 5);
   // tau = u + U j: u < U and U j share no bits, so h(tau >> 5) = h(u >> 5) ^ h((U j) >> 5) (h is linear)
   auto slot = [&](int j) { return ((uint32_t)tid + (uint32_t)U * j) ^ (h0 ^ swz(a, ((uint32_t)U * (uint32_t)j) >> 5)); };
+  float2 A = make_float2(1.f, 0.f);
+  uint32_t lw[16];
   if (act) {
-    float2 A = make_float2(1.f, 0.f);
     for (int i = 0; i < nlo; ++i) A = cmul(A, fconj(i, (tid >> i) & 1));
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const uint32_t w = slot(j);
-      const uint32_t lw = PL ? tile[lam_word<TB>() + w] : lds_ld2(tile, 8u * w).y;
-      const float2 lam = unpack_h2(lw), h = hb[j];
+      lw[j] = PL ? tile[lam_word<TB>() + w] : lds_ld2(tile, 8u * w).y;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float2 lam = unpack_h2(lw[j]), h = hb[j];
       c = make_float2(c.x + lam.x * h.x - lam.y * h.y, c.y + lam.x * h.y + lam.y * h.x);
-      const float2 pv = cmul(lam, A);
+    }
+  }
+  lds_barrier();
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t w = slot(j);
+      const float2 pv = cmul(unpack_h2(lw[j]), A);
       if constexpr (PL) {
         tile[w] = __float_as_uint(pv.x);
         tile[lam_word<TB>() + w] = __float_as_uint(pv.y);
@@ -1507,6 +1525,18 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   HEA_MARK();
   int ngrad = 0;
   int pending = -1;                                    // ring: region of the previous op, if a gradient op
+  // Partial-trace entries this lane adds per gradient op: lane (g4, cl) holds N[4 g4 + i][cl]; byte i of epi is the
+  // entry's region slot (b == a -> b, b ^ a == e_j -> 16 + 16 j + b, skewed by red_slot) or 0xFF if no partial
+  // trace uses it.  One VGPR for the whole op loop (the per-op predicates had been SGPR pairs spilled to VGPR lanes,
+  // and the four slot addresses four more VGPRs).
+  uint32_t epi = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15, d = bb ^ aa;
+    const uint32_t sl = __builtin_popcount(d) <= 1 ? (uint32_t)red_slot(d == 0 ? (int)bb : 16 + 16 * __builtin_ctz(d) + (int)bb)
+                                                    : 0xFFu;
+    epi |= sl << (8 * i);
+  }
   // A layer-1 product-state op (always the program's last) runs after the op loop, where none of the loop's values
   // are live: inside the loop its code pushed the group ops' register allocation into spills.
   const bool l1last = a.nops > 0 && a.ops[(size_t)(a.nops - 1) * OPW + W_CODE] == OP_L1PROD;
@@ -1591,16 +1621,19 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
       const int reg = RING ? ngrad & 1 : ngrad;
       const float sc = rsc[CMAX + 1];
       unsigned long long* rg = red64 + reg * RSTR;
+      // opaque to the optimiser: kept packed in one VGPR (hoisted out of the op loop, the per-entry predicates and
+      // slot addresses had taken eight SGPRs - spilled to VGPR lanes - and four VGPRs)
+      uint32_t ep = epi;
+      __asm__ volatile("" : "+v"(ep));
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const uint32_t bb = 4u * (lane >> 4) + i, aa = lane & 15, d = bb ^ aa;
         if (QFX_HEA_ABLATE && (a.ablate & 2)) break;
-        if (__builtin_popcount(d) <= 1) {
-          const int e = d == 0 ? (int)bb : 16 + 16 * (__builtin_ctz(d)) + (int)bb;
-          // round to nearest: truncation would bias every add toward zero, and a tile's sum has thousands
-          const uint32_t lo = (uint32_t)(int)__builtin_rintf(accR[i] * sc) + PK_BIAS,
-                         hi = (uint32_t)(int)__builtin_rintf(accI[i] * sc) + PK_BIAS;
-          atomicAdd(&rg[red_slot(e)], ((unsigned long long)hi << 32) | lo);
+        const uint32_t sl = (ep >> (8 * i)) & 0xFFu;
+        if (sl != 0xFFu) {
+          // round half up (floor(x + 0.5), one instruction): unbiased for these continuous values - truncation biased
+          // every add toward zero, and a tile's sum has thousands
+          const uint32_t lo = (uint32_t)cvt_rpi(accR[i] * sc) + PK_BIAS, hi = (uint32_t)cvt_rpi(accI[i] * sc) + PK_BIAS;
+          atomicAdd(&rg[sl], ((unsigned long long)hi << 32) | lo);
         }
       }
       if (tid == 0) {
@@ -1776,12 +1809,12 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
 #endif  // !QFX_HEA_BF16
 
 // Launch-variant knobs (A/B in one process: scripts/hea_ab.py): defaults from the environment, settable at run time.
-enum { K_PLANES = 0, K_FUSE = 1, K_ADJ_WAVES = 2, K_COUNT = 3 };
-static int knob_v[K_COUNT] = {-1, -1, -1};
+enum { K_PLANES = 0, K_FUSE = 1, K_ADJ_WAVES = 2, K_FULL13 = 3, K_COUNT = 4 };
+static int knob_v[K_COUNT] = {-1, -1, -1, -1};
 inline int knob(int k) {
   if (knob_v[k] < 0) {
-    static const char* env[K_COUNT] = {"QFEDX_HEA_PLANES", "QFEDX_HEA_FUSE", "QFEDX_HEA_ADJ_WAVES"};
-    static const int dflt[K_COUNT] = {0, 1, 8};
+    static const char* env[K_COUNT] = {"QFEDX_HEA_PLANES", "QFEDX_HEA_FUSE", "QFEDX_HEA_ADJ_WAVES", "QFEDX_HEA_FULL13"};
+    static const int dflt[K_COUNT] = {0, 1, 8, 0};
     const char* e = getenv(env[k]);
     knob_v[k] = e ? atoi(e) : dflt[k];
   }
@@ -1790,9 +1823,9 @@ inline int knob(int k) {
 
 }  // namespace HEA_NS
 
-// name: planes | fuse | adj_waves (4 or 8: waves of a 2^13 adjoint workgroup); returns the previous value, -1 unknown
+// name: planes | fuse | adj_waves (4 or 8: waves of a 2^13 adjoint workgroup) | full13; returns the previous value, -1 unknown
 extern "C" int HEA_EXT(qfx_hea_set_knob)(const char* name, int value) {
-  static const char* names[HEA_NS::K_COUNT] = {"planes", "fuse", "adj_waves"};
+  static const char* names[HEA_NS::K_COUNT] = {"planes", "fuse", "adj_waves", "full13"};
   for (int k = 0; k < HEA_NS::K_COUNT; ++k)
     if (strcmp(name, names[k]) == 0) {
       const int prev = HEA_NS::knob(k);
@@ -1809,6 +1842,8 @@ extern "C" int HEA_EXT(qfx_hea_pass)(int adjoint, const HEA_NS::PassArgs* args, 
   if (grid == 0) return 0;
   const int planes = HEA_NS::knob(HEA_NS::K_PLANES), fuse = HEA_NS::knob(HEA_NS::K_FUSE);
   const int wv4 = HEA_NS::knob(HEA_NS::K_ADJ_WAVES) == 4;
+  // full13: the 2^13 adjoint with a compile-time column-block count (t == 13: no per-block bounds branches)
+  const int full13 = HEA_NS::knob(HEA_NS::K_FULL13);
 #define HEA_LAUNCH(NCK)                                                                                     \
   do {                                                                                                     \
     if (!adjoint && a.pair)                                                                                \
@@ -1821,6 +1856,8 @@ extern "C" int HEA_EXT(qfx_hea_pass)(int adjoint, const HEA_NS::PassArgs* args, 
       hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, true, false>), dim3(grid), dim3(512), 0, st, a); \
     else if (a.t <= 13 && fuse && wv4)                                                                     \
       hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 4, false, false, true>), dim3(grid), dim3(256), 0, st, a); \
+    else if (a.t == 13 && fuse && full13)                                                                  \
+      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, true, false, true>), dim3(grid), dim3(512), 0, st, a); \
     else if (a.t <= 13 && fuse)                                                                            \
       hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, false, true>), dim3(grid), dim3(512), 0, st, a); \
     else if (a.t <= 13)                                                                                    \

@@ -629,7 +629,9 @@ def pass_programs(plan: HEAPlan, meta: list | None = None, recompute_last: bool 
         prod = l1prod and j == 0 and bool(p.l1)
         for i, g in enumerate(rev):
             # gradient cross matrix + U^H on lambda (and on psi while it is still needed further back)
-            psi_needed = i < len(rev) - 1 or (bool(p.l1) and not prod)
+            # (QFEDX_HEA_L1PROD_PSI=1, diagnostics: the last group op still un-applies psi under OP_L1PROD)
+            keep_psi = os.environ.get("QFEDX_HEA_L1PROD_PSI", "0") == "1"
+            psi_needed = i < len(rev) - 1 or (bool(p.l1) and (not prod or keep_psi))
             flags = (F_BACK_PSI | (F_BACK_TRANS if trans else 0)) if psi_needed else 0
             adj.append(group_table(plan, p, g, OP_BACK, flags))
         if not prod:

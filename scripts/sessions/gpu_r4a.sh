@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method threa
   "tests/test_gpu_kernels.py::test_secagg_sparse_graph_in_fused_reduce_match_host_protocol" \
   "tests/test_gpu_kernels.py::test_secagg_masks_in_fused_reduce_match_host_protocol" > gpurun_out/r4a_tests.log 2>&1
 rc=$?; grep -E "PASS|FAIL|Error|passed|failed" gpurun_out/r4a_tests.log | tail -20; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python -u scripts/hea_ab.py --variants "w8:adj_waves=8,w4:adj_waves=4,bf16w8:storage=bf16;adj_waves=8" > gpurun_out/r4a_ab.log 2>&1 || { tail -20 gpurun_out/r4a_ab.log; exit 1; }
+timeout -k 10 400 python -u scripts/hea_ab.py --variants "w8:adj_waves=8,w8f:adj_waves=8;full13=1,w4:adj_waves=4;full13=0,bf16w8:storage=bf16;adj_waves=8;full13=0" > gpurun_out/r4a_ab.log 2>&1 || { tail -20 gpurun_out/r4a_ab.log; exit 1; }
 tail -1 gpurun_out/r4a_ab.log
 STEPS=10 WARMUP=3 bash scripts/gpu_suite.sh vqc16q_bf16_8 vqc16q_fp16_8_mfma cfed128 || exit 1
 for p in 0 0x7e007e00 0x3c003c00; do
