@@ -649,7 +649,9 @@ __device__ __forceinline__ void dma_frags(const PassArgs& a, int k, int fi, int 
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)(slot + 64 * j);
-    __asm__ volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(fr + 64 * j),
+    // s_nop: an LDS DMA reads M0 one wait state after an SALU write of it (the compiler's hazard recognizer does
+    // not look inside this asm statement)
+    __asm__ volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(fr + 64 * j),
                      "s"(__builtin_amdgcn_readfirstlane(lds))
                      : "memory", "m0");
   }

@@ -54,12 +54,14 @@ def main():
     variants = parse_variants(args.variants)
     progs = {}
     for name, knobs in variants:
+        # plan-level variants are fixed when the program is built: l1prod=0/1 (OP_L1PROD for the last pass)
+        os.environ["QFEDX_HEA_L1PROD"] = knobs.get("l1prod", "0")
         progs[name] = HeaMfmaProgram(spec, dev, storage=knobs.get("storage", "fp16"))
     C = ext()
 
     def set_knobs(knobs):
         for k, v in knobs.items():
-            if k != "storage":
+            if k not in ("storage", "l1prod"):
                 C.hea_set_knob(k, int(v))
 
     def prep(prog):
