@@ -52,6 +52,15 @@ SUITE = {
                               None),
     "cfed128_secagg": ("configs/baseline4_cfed_128clients.yaml", ["train.local_steps=1", "privacy.secure_agg=true"],
                        "client local-steps/sec (CFed TinyCNN x 128 clients, batch 32, SecAgg on the device)", 258.0),
+    "cfed128_secagg_sparse": ("configs/baseline4_cfed_128clients.yaml",
+                              ["train.local_steps=1", "privacy.secure_agg=true", "privacy.secagg_graph=sparse"],
+                              "client local-steps/sec (CFed TinyCNN x 128 clients, batch 32, SecAgg+ sparse "
+                              "neighbour masks on the device)", 258.0),
+    "vqc16q_64_mfma_secagg_sparse": ("configs/headline_16q_64clients.yaml",
+                                     ["model.state_dtype=mfma", "privacy.secure_agg=true",
+                                      "privacy.secagg_graph=sparse"],
+                                     "client local-steps/sec (16-qubit VQC x 64 clients, SecAgg+ sparse neighbour "
+                                     "masks on the device)", None),
     "vqc20q_dp64_mfma": ("configs/baseline3_20q_dp_64clients.yaml", ["model.state_dtype=mfma"],
                          "client local-steps/sec (20-qubit VQC x 64 non-IID clients, DP, fp16 MFMA engine)", None),
     "vqc48q_mps64": ("configs/mps_48q_64clients.yaml", [],

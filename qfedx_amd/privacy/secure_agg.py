@@ -93,8 +93,16 @@ class KeyRegistry:
             if self.session_seed is None:
                 raise KeyError(f"no public key registered for client {peer}")
             self.register(peer)
-        shared = pow(self.public[peer], self._sk[me], _P)
-        return _hash_int(shared)
+        # pair seeds do not depend on the round: one modular exponentiation per (client, peer, peer key), cached
+        # (the sparse graph re-pairs clients every round, so its tables would otherwise pay one per edge per round)
+        cache = self.__dict__.setdefault("_pair_cache", {})
+        pk = self.public[peer]
+        hit = cache.get((me, peer))
+        if hit is not None and hit[0] == pk and hit[1] == self._sk[me]:
+            return hit[2]
+        seed = _hash_int(pow(pk, self._sk[me], _P))
+        cache[(me, peer)] = (pk, self._sk[me], seed)
+        return seed
 
 
 def prg_mask(pair_seed: int, round_num: int, P: int, bits: int = 48, device="cpu") -> torch.Tensor:
@@ -149,6 +157,10 @@ class SecureAggregator:
         parts = tuple(sorted({int(c) for c in participants}))
         if self.graph == "full" or secagg_degree(len(parts)) >= len(parts) - 1:
             return [j for j in parts if j != client]
+        return list(self._neighbor_map(parts, round_num)[client])
+
+    def _neighbor_map(self, parts: tuple, round_num: int) -> dict:
+        """client -> sorted sparse-graph neighbours for the sorted participant tuple ``parts`` (cached per round)."""
         key = (parts, int(round_num))
         if self._nb[0] != key:
             K = len(parts)
@@ -157,7 +169,7 @@ class SecureAggregator:
             h = secagg_degree(K) // 2
             self._nb = (key, {c: sorted({order[(pos[c] + d) % K] for d in range(1, h + 1)} |
                                         {order[(pos[c] - d) % K] for d in range(1, h + 1)}) for c in parts})
-        return list(self._nb[1][client])
+        return self._nb[1]
 
     def table_width(self, num_clients: int) -> int:
         """Peer columns of ``round_tables``: every client (full graph) or the largest neighbourhood any round
@@ -237,16 +249,37 @@ class SecureAggregator:
         W = self.table_width(num_clients)
         parts = list(participants)
         gone = {int(d) for d in dropped}
-        seeds = np.zeros((len(clients), W), dtype=np.uint64)
-        sign = np.zeros((len(clients), W), dtype=np.int32)
-        for r, c in enumerate(clients):
-            c = int(c)
-            live = [j for j in self.neighbors(c, parts, round_num) if j not in gone] if parts else []
-            if len(live) > W:
-                raise ValueError(f"client {c} has {len(live)} neighbours, table width {W}")
-            for col, j in enumerate(live):
-                seeds[r, col] = self.registry.pair_seed(c, j)
-                sign[r, col] = 1 if j > c else -1
+        # the graph is re-drawn every round, so over a run every pair is used: the clients' full seed rows are
+        # derived once (cached, as for the full graph) and each round only gathers its neighbours' columns
+        full = self.seed_matrix(clients, num_clients)
+        pt = np.asarray(sorted({int(c) for c in parts}), dtype=np.int64)
+        cl = np.asarray([int(c) for c in clients], dtype=np.int64)
+        K = len(pt)
+        if K == 0:
+            nb = np.full((len(cl), 0), -1, dtype=np.int64)
+        elif secagg_degree(K) >= K - 1:
+            nb = np.where((pt[None, :] != cl[:, None]) & np.isin(cl, pt)[:, None], pt[None, :], -1)   # all others
+        else:
+            # the round's circle (as _neighbor_map): h predecessors and successors of each client, vectorised
+            order = pt[np_rng(GRAPH_KEY, "secagg_graph", int(round_num), K).permutation(K)]
+            pos = np.zeros(max(int(pt.max()), int(cl.max(initial=0))) + 1, dtype=np.int64)
+            pos[order] = np.arange(K)
+            h = secagg_degree(K) // 2
+            d = np.concatenate([np.arange(1, h + 1), -np.arange(1, h + 1)])
+            nb = np.sort(order[(pos[cl][:, None] + d[None, :]) % K], axis=1)
+            nb = np.where(np.isin(cl, pt)[:, None], nb, -1)                  # non-participants mask nothing
+        if len(gone):
+            nb = np.where(np.isin(nb, np.asarray(sorted(gone), dtype=np.int64)), -1, nb)
+        # live neighbours first (ascending), -1 pads
+        key = np.where(nb < 0, np.iinfo(np.int64).max, nb)
+        nb = np.take_along_axis(nb, np.argsort(key, axis=1, kind="stable"), axis=1)
+        cnt = (nb >= 0).sum(1)
+        if len(cnt) and int(cnt.max()) > W:
+            raise ValueError(f"a client has {int(cnt.max())} live neighbours, table width {W}")
+        nb = nb[:, :W] if nb.shape[1] >= W else np.pad(nb, ((0, 0), (0, W - nb.shape[1])), constant_values=-1)
+        ok = nb >= 0
+        seeds = np.where(ok, np.take_along_axis(full, np.where(ok, nb, 0), axis=1), np.uint64(0)).astype(np.uint64)
+        sign = np.where(ok, np.where(nb > cl[:, None], 1, -1), 0).astype(np.int32)
         words = np.stack([seeds & np.uint64(0xFFFFFFFF), seeds >> np.uint64(32)], -1).astype(np.uint32)
         return (torch.from_numpy(words.view(np.int32).reshape(len(clients), W, 2).copy()),
                 torch.from_numpy(sign))
