@@ -31,6 +31,16 @@ struct HeaPassArgs {
   int pair;                  // forward: two samples per workgroup on 2^13 tiles (hea_fwd2_kernel)
   int ablate;                // timing ablations (builds with QFX_HEA_ABLATE only; QFEDX_HEA_ABLATE bit mask)
   uint32_t poison;           // diagnostics: != 0 fills every LDS word with this value at workgroup start
+  // Fused readout (first adjoint pass, noiseless): every workgroup computes its sample's <Z>, cross entropy and
+  // dL/d<Z> from the readout partials (part, ro_tps tiles) instead of reading wread; the tile-0 workgroup writes
+  // ro_expz / ro_w [S][C] (the later passes' wread) and the per-sample reduction record ro_rec [S][2C + 2]
+  // (dl_c z_c, dl_c, loss term, hit) that hea_grad_reduce sums per client.
+  int ro_fuse, ro_tps;
+  const long long* ro_y;
+  const float* ro_wts;
+  float* ro_expz;
+  float* ro_w;
+  float* ro_rec;
 };
 
 // Launch arguments of a fused Adam epilogue (m == nullptr: none).  cnt: one zero-initialised arrival counter per
@@ -43,4 +53,13 @@ struct QfxAdamArgs {
   const float* active;
   unsigned* cnt;
   float lr, b1, b2, eps;
+};
+
+// Per-client readout reduction in hea_grad_reduce (fused readout): one more block per client sums its samples' ro_rec
+// records in sample order into the loss / hit outputs and the readout-parameter gradients (a, b) of grad.
+struct QfxReadoutRed {
+  const float* rec;          // [S][2C + 2] (nullptr: no readout block)
+  float* loss;               // [K]
+  float* correct;            // [K]
+  int C, n_theta;
 };

@@ -18,7 +18,8 @@ int qfx_hea_pass(int adjoint, const HeaPassArgs* args, int n_samples, hipStream_
 int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                   hipStream_t st);
 int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc, int K,
-                        float* params, float* grad, int p_stride, const QfxAdamArgs* adam, hipStream_t st);
+                        float* params, float* grad, int p_stride, const QfxAdamArgs* adam,
+                        const QfxReadoutRed* readout, hipStream_t st);
 int qfx_hea_args_size();
 int qfx_hea_check_status(hipStream_t st);
 // bf16 state storage (hea_mfma_bf16.hip)
@@ -65,7 +66,8 @@ void check(int rc, const char* what) {
 void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<int64_t> geom, double scale, torch::Tensor psi_in,
               torch::Tensor psi_out, torch::Tensor lam_in, torch::Tensor lam_out, torch::Tensor xang,
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
-              torch::Tensor gslab, torch::Tensor dbg) {
+              torch::Tensor gslab, torch::Tensor dbg, c10::optional<std::vector<torch::Tensor>> readout,
+              int64_t ro_tps) {
   need(geom.size() == 28 || geom.size() == 29, "geometry vector must have 28 or 29 entries");
   const bool bf16 = geom.size() == 29 && geom[28] != 0;
   HeaPassArgs a{};
@@ -141,9 +143,27 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.xang = (a.gen || adjoint) ? dp<float>(xang, torch::kFloat32, "xang", S / a.in_rep * a.x_stride) : nullptr;
   a.params = dp<float>(params, torch::kFloat32, "params", K * a.p_stride);
   a.frags = a.n_slots ? (const void*)dp<int32_t>(frags, torch::kInt32, "frags", K * a.n_slots * 4 * 128 * 4) : nullptr;
-  a.wread = adjoint ? dp<float>(wread, torch::kFloat32, "wread", S * a.C) : nullptr;
   a.part = dp<float>(part, torch::kFloat32, "part", 0);
-  if (a.part) need(part.numel() >= S * a.n_tiles * a.C, "part buffer too small");
+  if (readout && !readout->empty()) {
+    // fused readout (first adjoint pass): readout = (y int64 [S], wts [S], expz [S, C], w_out [S, C],
+    // rec [S, 2C + 2]); part holds the readout pass's [S, ro_tps, C] partials
+    const auto& r = *readout;
+    need(adjoint && !a.load_lam && r.size() == 5 && ro_tps >= 1, "fused readout: first adjoint pass, 5 tensors");
+    need(ro_tps * a.C <= 64, "fused readout: at most 64 readout partials per sample (one per lane)");
+    need(a.part && part.numel() >= S * ro_tps * a.C, "fused readout: part buffer too small");
+    a.ro_fuse = 1;
+    a.ro_tps = (int)ro_tps;
+    a.ro_y = dp<long long>(r[0], torch::kInt64, "ro_y", S);
+    a.ro_wts = dp<float>(r[1], torch::kFloat32, "ro_wts", S);
+    a.ro_expz = dp<float>(r[2], torch::kFloat32, "ro_expz", S * a.C);
+    a.ro_w = dp<float>(r[3], torch::kFloat32, "ro_w", S * a.C);
+    a.ro_rec = dp<float>(r[4], torch::kFloat32, "ro_rec", S * (2 * a.C + 2));
+    need(a.n_theta + 2 * a.C <= a.p_stride, "fused readout: readout parameters past the parameter row");
+    a.wread = nullptr;
+  } else {
+    a.wread = adjoint ? dp<float>(wread, torch::kFloat32, "wread", S * a.C) : nullptr;
+    if (a.part) need(part.numel() >= S * a.n_tiles * a.C, "part buffer too small");
+  }
   a.gslab = adjoint ? dp<long long>(gslab, torch::kInt64, "gslab", S * a.slab_tiles * a.n_gradops * 32) : nullptr;
   need(!adjoint || a.slab_tiles >= a.n_tiles, "gradient slab has fewer tiles than the pass");
   need(!a.gen || a.n <= 32, "product-state generation supports <= 32 qubits");
@@ -207,9 +227,23 @@ void hea_frags(torch::Tensor params, int64_t p_stride, torch::Tensor slot_tab, i
 
 // adam: optional (m, v, t_in, t_out, active, cnt) device tensors [K, P] / [K] (cnt int32, zero-initialised) and
 // lr, b1, b2, eps: the clients' Adam step fused into the reduction (the last block of each client updates its row)
+// readout: optional (rec [K * spc, 2C + 2], loss [K], correct [K]) of a fused-readout step and ro_c = C, ro_ntheta:
+// one more block per client reduces the records into loss / correct and the readout-parameter gradients
 void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops, torch::Tensor gmeta, int64_t spc,
                      int64_t K, torch::Tensor params, torch::Tensor grad, int64_t p_stride,
-                     c10::optional<std::vector<torch::Tensor>> adam, c10::optional<std::vector<double>> hyper) {
+                     c10::optional<std::vector<torch::Tensor>> adam, c10::optional<std::vector<double>> hyper,
+                     c10::optional<std::vector<torch::Tensor>> readout, int64_t ro_c, int64_t ro_ntheta) {
+  QfxReadoutRed ro{};
+  if (readout && !readout->empty()) {
+    const auto& r = *readout;
+    need(r.size() == 3 && ro_c >= 1 && ro_c <= 8 && ro_ntheta + 2 * ro_c <= p_stride,
+         "grad_reduce: readout = (rec, loss, correct) with 1..8 classes inside the parameter row");
+    ro.rec = dp<float>(r[0], torch::kFloat32, "rec", K * spc * (2 * ro_c + 2));
+    ro.loss = dp<float>(r[1], torch::kFloat32, "loss", K);
+    ro.correct = dp<float>(r[2], torch::kFloat32, "correct", K);
+    ro.C = (int)ro_c;
+    ro.n_theta = (int)ro_ntheta;
+  }
   QfxAdamArgs ad{};
   if (adam && !adam->empty()) {
     const auto& a = *adam;
@@ -222,19 +256,23 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
     ad.active = dp<float>(a[4], torch::kFloat32, "active", K);
     ad.cnt = dp<unsigned>(a[5], torch::kInt32, "cnt", K);
     ad.lr = (float)(*hyper)[0], ad.b1 = (float)(*hyper)[1], ad.b2 = (float)(*hyper)[2], ad.eps = (float)(*hyper)[3];
-    need(n_gradops > 0, "grad_reduce: fused Adam needs at least one gradient op");
+    need(n_gradops > 0 || ro.rec, "grad_reduce: fused Adam needs at least one reduction block");
   }
   check(qfx_hea_grad_reduce(dp<long long>(gslab, torch::kInt64, "gslab", K * spc * slab_tiles * n_gradops * 32),
                             (int)slab_tiles, (int)n_gradops, dp<int>(gmeta, torch::kInt32, "gmeta", n_gradops * 10),
                             (int)spc, (int)K, dp<float>(params, torch::kFloat32, "params", K * p_stride),
-                            dp<float>(grad, torch::kFloat32, "grad", K * p_stride), (int)p_stride, &ad, cur()),
+                            dp<float>(grad, torch::kFloat32, "grad", K * p_stride), (int)p_stride, &ad, &ro, cur()),
         "qfx_hea_grad_reduce");
 }
 
 }  // namespace
 
 void register_hea(pybind11::module& m) {
-  m.def("hea_pass", &hea_pass);
+  m.def("hea_pass", &hea_pass, pybind11::arg("adjoint"), pybind11::arg("ops"), pybind11::arg("fidx"),
+        pybind11::arg("geom"), pybind11::arg("scale"), pybind11::arg("psi_in"), pybind11::arg("psi_out"),
+        pybind11::arg("lam_in"), pybind11::arg("lam_out"), pybind11::arg("xang"), pybind11::arg("params"),
+        pybind11::arg("frags"), pybind11::arg("wread"), pybind11::arg("part"), pybind11::arg("gslab"),
+        pybind11::arg("dbg"), pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_tps") = 0);
   m.def("hea_frags", &hea_frags, pybind11::arg("params"), pybind11::arg("p_stride"), pybind11::arg("slot_tab"),
         pybind11::arg("n_slots"), pybind11::arg("K"), pybind11::arg("frags"), pybind11::arg("bf16") = false);
   m.def("hea_check_ops", &hea_check_ops);
@@ -246,7 +284,8 @@ void register_hea(pybind11::module& m) {
   m.def("hea_grad_reduce", &hea_grad_reduce, pybind11::arg("gslab"), pybind11::arg("slab_tiles"),
         pybind11::arg("n_gradops"), pybind11::arg("gmeta"), pybind11::arg("spc"), pybind11::arg("K"),
         pybind11::arg("params"), pybind11::arg("grad"), pybind11::arg("p_stride"),
-        pybind11::arg("adam") = pybind11::none(), pybind11::arg("hyper") = pybind11::none());
+        pybind11::arg("adam") = pybind11::none(), pybind11::arg("hyper") = pybind11::none(),
+        pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_c") = 0, pybind11::arg("ro_ntheta") = 0);
   m.def("hea_args_size", []() { return qfx_hea_args_size(); });
   // -1: release build (no device checks); 0: no failure since the last read; else the failing source line
   m.def("hea_check_status", []() { return qfx_hea_check_status(cur()); });

@@ -39,6 +39,7 @@
 #endif
 
 #include "hea_args.h"
+#include "qfx_readout.h"
 #include "qfx_adam.h"
 #include "qfx_check.h"
 
@@ -1481,14 +1482,79 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
   if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
+  // Fused readout (the last wave): its lanes load the sample's readout partials, label, loss weight and readout
+  // parameters BEFORE the tile load is issued, so their latency overlaps the tile's; lane 0 sums the partials in tile
+  // order after the load (the readout kernel's order and arithmetic, qfx_readout.h).
+  const bool ro_wave = a.ro_fuse && wave == NW - 1;
+  const int ro_np = a.ro_fuse ? a.ro_tps * a.C : 0;   // partials per sample (<= 64: host-checked)
+  float ro_v = 0.f, ro_ab = 0.f, ro_ws = 0.f;
+  int ro_yy = 0;
+  if (ro_wave) {
+    if (lane < ro_np) ro_v = a.part[(size_t)s * ro_np + lane];
+    if (lane < 2 * a.C) ro_ab = a.params[(size_t)k * a.p_stride + a.n_theta + lane];
+    if (lane == 0) {
+      ro_ws = a.ro_wts[s];
+      ro_yy = (int)a.ro_y[s];
+    }
+  }
   if (!(QFX_HEA_ABLATE && (a.ablate & 32)))
     load_tile_il<NT, TB, PL>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
                          h_q, fixed);
-  if (tid == 0) {
+
+  if (a.ro_fuse ? tid == NT - 64 : tid == 0) {
+    float wv[CMAX];
+    if (a.ro_fuse) {
+      // lane 0 of the last wave: partials and parameters gathered from its wave's lanes (one load round trip); every
+      // per-class array is indexed by unrolled constants (a run-time class index would put them in scratch)
+      float z[qfx_ro::RO_CMAX], ra[2 * qfx_ro::RO_CMAX], dl[qfx_ro::RO_CMAX], lterm, hit;
+#pragma unroll
+      for (int c = 0; c < qfx_ro::RO_CMAX; ++c) z[c] = 0.f;
+      for (int u = 0; u < a.ro_tps; ++u) {
+#pragma unroll
+        for (int c = 0; c < qfx_ro::RO_CMAX; ++c)
+          if (c < a.C) z[c] += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ro_v), u * a.C + c));
+      }
+#pragma unroll
+      for (int c = 0; c < 2 * qfx_ro::RO_CMAX; ++c)
+        ra[c] = c < 2 * a.C ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ro_ab), c)) : 0.f;
+      float rb[qfx_ro::RO_CMAX];
+#pragma unroll
+      for (int c = 0; c < qfx_ro::RO_CMAX; ++c) rb[c] = c < a.C ? __int_as_float(__builtin_amdgcn_readlane(
+                                                                 __float_as_int(ro_ab), a.C + c)) : 0.f;
+      qfx_ro::ce_sample(z, ra, rb, a.C, ro_yy, ro_ws, dl, lterm, hit);
+      const bool out = tile_id == 0;
+      float* rec = a.ro_rec + (size_t)s * (2 * a.C + 2);
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) {
+        if (c >= a.C) break;
+        wv[c] = dl[c] * ra[c];
+        if (out) {
+          a.ro_expz[(size_t)s * a.C + c] = z[c];
+          a.ro_w[(size_t)s * a.C + c] = wv[c];
+          rec[c] = dl[c] * z[c];
+          rec[a.C + c] = dl[c];
+        }
+      }
+      if (out) {
+        rec[2 * a.C] = lterm;
+        rec[2 * a.C + 1] = hit;
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) {
+        if (c >= a.C) break;
+        wv[c] = a.wread[(size_t)s * a.C + c];
+      }
+    }
     float rho = 0.f;
-    for (int c = 0; c < a.C; ++c) rho = fmaxf(rho, fabsf(a.wread[(size_t)s * a.C + c]));
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c) {
+      if (c >= a.C) break;
+      rho = fmaxf(rho, fabsf(wv[c]));
+    }
     if (rho == 0.f) rho = 1.f;
-    for (int c = 0; c < NCK; ++c) rsc[c] = c < a.C ? a.wread[(size_t)s * a.C + c] / rho : 0.f;
+#pragma unroll
+    for (int c = 0; c < NCK; ++c) rsc[c] = c < a.C ? wv[c] / rho : 0.f;
     rsc[CMAX] = rho;
     rsc[CMAX + 1] = PK_SCALE / (a.scale * a.scale);
   }
@@ -1739,52 +1805,80 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
 __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* __restrict__ gslab, int slab_tiles,
                                                               int n_gradops, const int* __restrict__ gmeta, int spc,
                                                               float* __restrict__ params,
-                                                              float* __restrict__ grad, int p_stride, QfxAdamArgs ad) {
+                                                              float* __restrict__ grad, int p_stride, QfxAdamArgs ad,
+                                                              QfxReadoutRed ro) {
   // 8 groups of 32 lanes split the client's (sample, tile) rows; 4 independent loads in flight per lane; the
   // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
   const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
-  const int* m = gmeta + g * 10;
-  // m[1]: nreal in bits 0..3; bit 4 = cross matrix taken at the op INPUT (transposed BACK ops)
-  const int nt = m[0], nreal = m[1] & 15, inside = (m[1] >> 4) & 1;
-  const int R = spc * nt;
-  __shared__ long long part[8][32];
-  __shared__ double pt[32];
-  long long acc[4] = {0, 0, 0, 0};
-  auto row = [&](int r) -> long long {
-    const int s = k * spc + r / nt, t = r % nt;
-    return gslab[(((size_t)s * slab_tiles + t) * n_gradops + g) * 32 + lane];
-  };
-  int r = grp;
-  for (; r + 24 < R; r += 32) {
-    acc[0] += row(r);
-    acc[1] += row(r + 8);
-    acc[2] += row(r + 16);
-    acc[3] += row(r + 24);
-  }
-  for (; r < R; r += 8) acc[0] += row(r);
-  part[grp][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-  __syncthreads();
-  if (tid < 32) {
-    long long v = 0;
-    for (int j = 0; j < 8; ++j) v += part[j][tid];
-    pt[tid] = (double)v / FIX;
-  }
-  __syncthreads();
-  if (tid < nreal) {
-    const double* p = pt + 8 * tid;
-    const float* prm = params + (size_t)k * p_stride;
-    if (inside) {
-      // at the op input: d/dtheta = Im<lam|X|psi> = Im(n01 + n10);
-      // d/dphi = Im<lam|RX^H Z RX|psi> = cos(theta) Im(n00 - n11) + sin(theta) Re(n01 - n10)
-      const double th = prm[m[2 + tid]];
-      const double ct = cos(th), st = sin(th);
-      grad[(size_t)k * p_stride + m[2 + tid]] = (float)(p[3] + p[5]);
-      grad[(size_t)k * p_stride + m[6 + tid]] = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
-    } else {
-      const double ph = prm[m[6 + tid]];
-      const double cp = cos(ph), sp = sin(ph);
-      grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
-      grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
+  if (g == n_gradops) {
+    // fused readout: the client's per-sample records summed in sample order (thread j sums samples j, j + 256, ...;
+    // then a fixed-order tree): loss, hits, and the readout gradients d/da_c = sum dl_c z_c, d/db_c = sum dl_c
+    __shared__ float rs[256];
+    const int NV = 2 * ro.C + 2;
+    for (int q = 0; q < NV; ++q) {
+      float v = 0.f;
+      for (int j = tid; j < spc; j += 256) v += ro.rec[((size_t)k * spc + j) * NV + q];
+      rs[tid] = v;
+      __syncthreads();
+      for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) rs[tid] += rs[tid + w];
+        __syncthreads();
+      }
+      if (tid == 0) {
+        const float tot = rs[0];
+        if (q < 2 * ro.C)
+          grad[(size_t)k * p_stride + ro.n_theta + q] = tot;
+        else if (q == 2 * ro.C)
+          ro.loss[k] = tot;
+        else
+          ro.correct[k] = tot;
+      }
+      __syncthreads();
+    }
+  } else {
+    const int* m = gmeta + g * 10;
+    // m[1]: nreal in bits 0..3; bit 4 = cross matrix taken at the op INPUT (transposed BACK ops)
+    const int nt = m[0], nreal = m[1] & 15, inside = (m[1] >> 4) & 1;
+    const int R = spc * nt;
+    __shared__ long long part[8][32];
+    __shared__ double pt[32];
+    long long acc[4] = {0, 0, 0, 0};
+    auto row = [&](int r) -> long long {
+      const int s = k * spc + r / nt, t = r % nt;
+      return gslab[(((size_t)s * slab_tiles + t) * n_gradops + g) * 32 + lane];
+    };
+    int r = grp;
+    for (; r + 24 < R; r += 32) {
+      acc[0] += row(r);
+      acc[1] += row(r + 8);
+      acc[2] += row(r + 16);
+      acc[3] += row(r + 24);
+    }
+    for (; r < R; r += 8) acc[0] += row(r);
+    part[grp][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
+    if (tid < 32) {
+      long long v = 0;
+      for (int j = 0; j < 8; ++j) v += part[j][tid];
+      pt[tid] = (double)v / FIX;
+    }
+    __syncthreads();
+    if (tid < nreal) {
+      const double* p = pt + 8 * tid;
+      const float* prm = params + (size_t)k * p_stride;
+      if (inside) {
+        // at the op input: d/dtheta = Im<lam|X|psi> = Im(n01 + n10);
+        // d/dphi = Im<lam|RX^H Z RX|psi> = cos(theta) Im(n00 - n11) + sin(theta) Re(n01 - n10)
+        const double th = prm[m[2 + tid]];
+        const double ct = cos(th), st = sin(th);
+        grad[(size_t)k * p_stride + m[2 + tid]] = (float)(p[3] + p[5]);
+        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
+      } else {
+        const double ph = prm[m[6 + tid]];
+        const double cp = cos(ph), sp = sin(ph);
+        grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
+        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
+      }
     }
   }
   if (!ad.m) return;
@@ -1796,7 +1890,7 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   if (tid == 0) {
     __threadfence();
     const unsigned prev = atomicAdd(&ad.cnt[k], 1u);
-    last_s = prev == (unsigned)(n_gradops - 1);
+    last_s = prev == (unsigned)(gridDim.y - 1);
     if (last_s) ad.cnt[k] = 0u;                       // ready for the next launch
   }
   __syncthreads();
@@ -1891,13 +1985,16 @@ extern "C" int HEA_EXT(qfx_hea_frags)(const float* params, int p_stride, const i
 #if !QFX_HEA_BF16
 extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc,
                                    int K, float* params, float* grad, int p_stride, const QfxAdamArgs* adam,
-                                   hipStream_t st) {
+                                   const QfxReadoutRed* readout, hipStream_t st) {
   if (K == 0) return 0;
-  if (n_gradops == 0) return adam && adam->m ? (int)hipErrorInvalidValue : 0;   // no block would run the epilogue
+  QfxReadoutRed ro{};
+  if (readout) ro = *readout;
+  const int rows = n_gradops + (ro.rec ? 1 : 0);
+  if (rows == 0) return adam && adam->m ? (int)hipErrorInvalidValue : 0;   // no block would run the epilogue
   QfxAdamArgs ad{};
   if (adam) ad = *adam;
-  hipLaunchKernelGGL(HEA_NS::hea_grad_reduce_kernel, dim3(K, n_gradops), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
-                     gmeta, spc, params, grad, p_stride, ad);
+  hipLaunchKernelGGL(HEA_NS::hea_grad_reduce_kernel, dim3(K, rows), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
+                     gmeta, spc, params, grad, p_stride, ad, ro);
   return (int)hipGetLastError();
 }
 

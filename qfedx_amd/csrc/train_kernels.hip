@@ -15,6 +15,7 @@
 #include "philox.h"
 #include "qfx_adam.h"
 #include "qfx_plan.h"
+#include "qfx_readout.h"
 
 namespace qfx {
 
@@ -48,25 +49,6 @@ __device__ __forceinline__ void block_sum(float (&v)[NV], float* sm) {
   for (int i = 0; i < NV; ++i) v[i] = sm[i * 4 + 0] + sm[i * 4 + 1] + sm[i * 4 + 2] + sm[i * 4 + 3];
 }
 
-// zs[c] = sum_u part[s][u][c] in tile order.  Loads are issued in batches of 8 tiles (predicated) so
-// their latencies overlap instead of serialising one dependent load per tile.
-__device__ __forceinline__ void tile_sums(const float* __restrict__ part, long s, int tps, int C, float (&zs)[CMAX]) {
-#pragma unroll
-  for (int c = 0; c < CMAX; ++c) zs[c] = 0.f;
-  const float* base = part + (size_t)s * tps * C;
-  for (int u0 = 0; u0 < tps; u0 += 8) {
-    float v[8][CMAX];
-#pragma unroll
-    for (int du = 0; du < 8; ++du)
-#pragma unroll
-      for (int c = 0; c < CMAX; ++c) v[du][c] = (u0 + du < tps && c < C) ? base[(size_t)(u0 + du) * C + c] : 0.f;
-#pragma unroll
-    for (int du = 0; du < 8; ++du)
-#pragma unroll
-      for (int c = 0; c < CMAX; ++c) zs[c] += v[du][c];
-  }
-}
-
 // one block per client: <Z_c> = sum of tile partials; logits a<Z>+b; CE; dL/d<Z>; grads of a, b
 __global__ void __launch_bounds__(256) qfx_readout_ce_kernel(
     const float* __restrict__ part, int tps, int C, int spc, const long long* __restrict__ y,
@@ -85,44 +67,28 @@ __global__ void __launch_bounds__(256) qfx_readout_ce_kernel(
   for (int i = 0; i < 2 * CMAX + 2; ++i) acc[i] = 0.f;
   for (int j = threadIdx.x; j < spc; j += 256) {
     const long s = (long)k * spc + j;
-    float z[CMAX], lg[CMAX];
-    float m = -INFINITY;
-    float zs[CMAX];
-    tile_sums(part, s, tps, C, zs);
+    float z[CMAX], zs[CMAX];
+    qfx_ro::tile_sums(part, s, tps, C, zs);
 #pragma unroll
     for (int c = 0; c < CMAX; ++c) {
-      if (c >= C) break;
-      float t = zs[c];
-      if (noisy) t = noisy_z(t, nz.p01, nz.p10, nz.shots, k0, k1, nz.stream, ((uint64_t)j * C + c) * (uint64_t)nz.shots);
+      float t = c < C ? zs[c] : 0.f;
+      if (noisy && c < C) t = noisy_z(t, nz.p01, nz.p10, nz.shots, k0, k1, nz.stream, ((uint64_t)j * C + c) * (uint64_t)nz.shots);
       z[c] = t;
-      lg[c] = fmaf(a[c], t, b[c]);
-      m = fmaxf(m, lg[c]);
     }
-    float se = 0.f;
-    int am = 0;
-#pragma unroll
-    for (int c = 0; c < CMAX; ++c) {
-      if (c >= C) break;
-      se += expf(lg[c] - m);
-      if (lg[c] > lg[am]) am = c;
-    }
-    const float lse = m + logf(se);
     const int yy = (int)y[s];
     const float ws = wts[s];
-    float ly = 0.f;
+    float dl[CMAX], lterm, hit;
+    qfx_ro::ce_sample(z, a, b, C, yy, ws, dl, lterm, hit);
 #pragma unroll
     for (int c = 0; c < CMAX; ++c) {
       if (c >= C) break;
-      if (c == yy) ly = lg[c];
-      const float p = expf(lg[c] - lse);
-      const float dl = (p - (c == yy ? 1.f : 0.f)) * ws;
       expz[(size_t)s * C + c] = z[c];
-      w_out[(size_t)s * C + c] = dl * a[c] * gscale;
-      acc[c] += dl * z[c];
-      acc[CMAX + c] += dl;
+      w_out[(size_t)s * C + c] = dl[c] * a[c] * gscale;
+      acc[c] += dl[c] * z[c];
+      acc[CMAX + c] += dl[c];
     }
-    acc[2 * CMAX] += ws * (lse - ly);
-    acc[2 * CMAX + 1] += (am == yy && ws > 0.f) ? 1.f : 0.f;
+    acc[2 * CMAX] += lterm;
+    acc[2 * CMAX + 1] += hit;
   }
   block_sum<2 * CMAX + 2>(acc, sm);
   if (threadIdx.x == 0) {

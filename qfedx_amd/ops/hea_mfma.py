@@ -245,7 +245,10 @@ class HeaMfmaProgram:
             stored += [stored[R]] * (J - 1 - R)
         return stored
 
-    def _adjoint(self, x, params, fr, K, B, stored, wread, gslab, tag: str = ""):
+    def _adjoint(self, x, params, fr, K, B, stored, wread, gslab, tag: str = "", readout=None):
+        """Adjoint passes, last pass first.  ``readout`` = (part, y, wts, expz, rec): the first adjoint pass computes
+        every sample's readout and dL/d<Z> itself (fused readout; ``wread`` is then its output, read by the later
+        passes) instead of taking ``wread`` from the readout kernel."""
         C = ext()
         S = K * B
         N = S << self.n
@@ -257,8 +260,13 @@ class HeaMfmaProgram:
             _, _, adj, p = self.passes[j]
             lam_out = self._buf(f"{tag}lam{j % 2}", N, torch.int32) if j > 0 else empty
             geom = self._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, x.shape[1], K)
-            C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
-                       params, fr, wread, fempty, gslab, _NODBG)
+            if readout is not None and j == J - 1:
+                part, yy, ww, expz, rec = readout
+                C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
+                           params, fr, fempty, part, gslab, _NODBG, [yy, ww, expz, wread, rec], self.tiles_last)
+            else:
+                C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
+                           params, fr, wread, fempty, gslab, _NODBG)
             lam_in = lam_out
 
     def _prep(self, xang, params):
@@ -524,20 +532,32 @@ class HeaMfmaProgram:
         wread = self._buf(f"{tag}wread", S * self.C, torch.float32)
         gslab = self._buf(f"{tag}gslab", S * self.slab_tiles * self.n_gradops * 32, torch.int64)
         stored = self._forward(x, p, fr, K, B, part, store_last=True, tag=tag, after_first=after_first)
-        if noise is None:
-            C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss, correct,
-                         grad, True, 0.0, 0.0, 0, _NO_KEYS, 0)
+        # Fused readout (noiseless steps; QFEDX_FUSED_READOUT=0 keeps the separate kernel): the first adjoint pass
+        # computes each sample's <Z>, cross entropy and dL/d<Z> from the readout partials, and the gradient
+        # reduction sums the clients' loss, hits and readout gradients - one launch fewer per local step.
+        fuse_ro = (noise is None and os.environ.get("QFEDX_FUSED_READOUT", "1") != "0"
+                   and self.tiles_last * self.C <= 64)
+        ro = None
+        if fuse_ro:
+            rec = self._buf(f"{tag}rorec", S * (2 * self.C + 2), torch.float32)
+            ro = [rec, loss, correct]
+            self._adjoint(x, p, fr, K, B, stored, wread, gslab, tag, readout=(part, yy, ww, expz, rec))
         else:
-            from .statevec_hip import _keys
-            C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss, correct,
-                         grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
-        self._adjoint(x, p, fr, K, B, stored, wread, gslab, tag)
+            if noise is None:
+                C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
+                             correct, grad, True, 0.0, 0.0, 0, _NO_KEYS, 0)
+            else:
+                from .statevec_hip import _keys
+                C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
+                             correct, grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
+            self._adjoint(x, p, fr, K, B, stored, wread, gslab, tag)
         if adam is None:
-            C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1])
+            C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1],
+                              None, None, ro, self.C, self.n_theta)
         else:
             cnt = self._zbuf(f"{tag}adamcnt", K, torch.int32)
             C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1],
-                              adam[0] + [cnt], adam[1])
+                              adam[0] + [cnt], adam[1], ro, self.C, self.n_theta)
 
     def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
                        out_correct=None, init: torch.Tensor | None = None, fused_opt=None) -> dict:
@@ -566,7 +586,9 @@ class HeaMfmaProgram:
         # launch took 33.6 us against 13 + 5.4 us for the two launches; at the 8-client share (104 blocks) it saves
         # a launch (round 387 -> 382 us; profiles/r3_fused_adam_ab.txt).  QFEDX_FUSED_ADAM=1 / 0 forces it on / off.
         mode = os.environ.get("QFEDX_FUSED_ADAM", "auto")
-        want = mode == "1" or (mode == "auto" and K * self.n_gradops <= FUSED_ADAM_MAX_BLOCKS)
+        ro_rows = 1 if (noise is None and os.environ.get("QFEDX_FUSED_READOUT", "1") != "0"
+                        and self.tiles_last * self.C <= 64) else 0
+        want = mode == "1" or (mode == "auto" and K * (self.n_gradops + ro_rows) <= FUSED_ADAM_MAX_BLOCKS)
         if (want and fused_opt is not None and n == 1 and self.n_gradops > 0
                 and p.data_ptr() == params.data_ptr()):
             adam = fused_opt[0].fused_adam(p, fused_opt[1])

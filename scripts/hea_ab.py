@@ -61,7 +61,9 @@ def main():
 
     def set_knobs(knobs):
         for k, v in knobs.items():
-            if k not in ("storage", "l1prod"):
+            if k.startswith("env."):           # run-time environment switches, e.g. env.QFEDX_FUSED_READOUT=0
+                os.environ[k[4:]] = v
+            elif k not in ("storage", "l1prod"):
                 C.hea_set_knob(k, int(v))
 
     def prep(prog):

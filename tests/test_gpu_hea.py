@@ -229,3 +229,35 @@ def test_paired_forward_matches_single_sample_kernel(cuda, n, L):
     ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
     np.testing.assert_allclose(z2.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
     np.testing.assert_allclose(g2.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
+
+
+@pytest.mark.parametrize("n,K,B,C", [(16, 8, 32, 3), (12, 5, 7, 4), (10, 3, 4, 8)])
+def test_fused_readout_matches_readout_kernel(cuda, monkeypatch, n, K, B, C):
+    """The first adjoint pass computing each sample's readout, cross entropy and dL/d<Z> itself (and hea_grad_reduce
+    the clients' loss, hits and readout gradients) matches the separate readout kernel: <Z> and the theta gradients
+    bitwise (same per-sample arithmetic, shared qfx_readout.h), the per-client sums to fp32 reassociation; the
+    fused path is deterministic."""
+    spec = VQCSpec(n, 3, C, readout_scale=2.0)
+    g = torch.Generator().manual_seed(5)
+    xang = spec.encode_features(torch.rand(K, B, n, generator=g)).to(cuda)
+    y = torch.randint(0, C, (K, B), generator=g).to(cuda)
+    w = (torch.rand(K, B, generator=g) / B).to(cuda)
+    params = torch.stack([spec.init_params(k) for k in range(K)])
+    params = (params + 0.3 * torch.randn(params.shape, generator=g)).to(cuda)
+
+    def run(fused):
+        monkeypatch.setenv("QFEDX_FUSED_READOUT", "1" if fused else "0")
+        prog = HeaMfmaProgram(spec, cuda)
+        out = prog.loss_and_grads(xang, y, w, params, spec)
+        torch.cuda.synchronize()
+        return {k: v.clone() for k, v in out.items()}
+
+    ref, got, again = run(False), run(True), run(True)
+    assert torch.equal(got["expz"], ref["expz"])
+    nt = spec.n_theta
+    assert torch.equal(got["grad"][:, :nt], ref["grad"][:, :nt])
+    torch.testing.assert_close(got["grad"][:, nt:], ref["grad"][:, nt:], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(got["loss"], ref["loss"], rtol=1e-5, atol=1e-6)
+    assert torch.equal(got["correct"], ref["correct"])
+    for k in ("loss", "correct", "grad", "expz"):
+        assert torch.equal(got[k], again[k]), k
