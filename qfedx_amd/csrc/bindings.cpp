@@ -91,7 +91,8 @@ int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned
                       float clip, float sigma, long long* out, long long* pack_buf, const float* loss,
                       const float* correct, const float* nvalid, const float* act, int n_metrics, long long* sat,
                       const uint32_t* sa_seeds, const int* sa_sign, const int* sa_round, int sa_n, double sa_scale,
-                      int sa_bits, long long* sa_masks, const int* norm_cid, hipStream_t st);
+                      int sa_bits, long long* sa_masks, const int* norm_cid, float* fa_theta, double* fa_out,
+                      unsigned* fa_cnt, int fa_bits, double fa_ring_scale, int fa_n_norms, hipStream_t st);
 }
 
 namespace qfx_runtime {
@@ -443,7 +444,9 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
             torch::Tensor out, torch::Tensor pack_buf, torch::Tensor loss, torch::Tensor correct,
             torch::Tensor nvalid, torch::Tensor act, torch::Tensor sat, c10::optional<torch::Tensor> sa_seeds,
             c10::optional<torch::Tensor> sa_sign, c10::optional<torch::Tensor> sa_round, double sa_scale,
-            int64_t sa_bits, c10::optional<torch::Tensor> sa_masks, c10::optional<torch::Tensor> norm_cid) {
+            int64_t sa_bits, c10::optional<torch::Tensor> sa_masks, c10::optional<torch::Tensor> norm_cid,
+            c10::optional<torch::Tensor> fa_theta, c10::optional<torch::Tensor> fa_out,
+            c10::optional<torch::Tensor> fa_cnt, int64_t fa_bits, double fa_scale, int64_t fa_n_norms) {
   need(theta_k, torch::kFloat32, "theta_k");
   need(sat, torch::kInt64, "sat");
   if (sat.numel() < 1) throw std::invalid_argument("fedavg: sat counter missing");
@@ -490,6 +493,18 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
     need(*norm_cid, torch::kInt32, "norm_cid");
     if (!pack || !dp || norm_cid->numel() < K) throw std::invalid_argument("fedavg: norm slots need pack + DP + [K] ids");
   }
+  // single-rank round: the launch's last block also applies the round (round_apply's work) to fa_theta [P], writing
+  // the [6 + n_norms] outputs to fa_out; fa_cnt is an int32 [1] zeroed arrival counter (self-resetting)
+  const bool fa = fa_theta.has_value() && fa_theta->defined();
+  if (fa) {
+    if (!pack || !fa_out.has_value() || !fa_cnt.has_value()) throw std::invalid_argument("fedavg: fused apply needs pack, out, counter");
+    need(*fa_theta, torch::kFloat32, "fa_theta");
+    need(*fa_out, torch::kFloat64, "fa_out");
+    need(*fa_cnt, torch::kInt32, "fa_cnt");
+    if (fa_theta->numel() != P || fa_out->numel() < 6 + fa_n_norms || fa_cnt->numel() < 1 || fa_n_norms < 0 ||
+        pack_buf.numel() < P + 6 + fa_n_norms || fa_bits < 0 || fa_bits > 62)
+      throw std::invalid_argument("fedavg: fused apply sizes");
+  }
   check(qfx_launch_fedavg(ptr<float>(theta_k), ptr<float>(theta_g), ptr<unsigned char>(angle_mask),
                           ptr<double>(weights), ptr<double>(norms), ptr<uint32_t>(keys), K, P, wrap ? 1 : 0,
                           dp ? 1 : 0, (float)clip, (float)sigma, ptr<long long>(out),
@@ -498,7 +513,10 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
                           pack ? ptr<float>(act) : nullptr, (int)n, ptr<long long>(sat),
                           sa ? ptr<uint32_t>(*sa_seeds) : nullptr, sa ? ptr<int>(*sa_sign) : nullptr,
                           sa ? ptr<int>(*sa_round) : nullptr, sa_n, sa_scale, (int)sa_bits,
-                          sa ? ptr<long long>(*sa_masks) : nullptr, nc ? ptr<int>(*norm_cid) : nullptr, cur_stream()),
+                          sa ? ptr<long long>(*sa_masks) : nullptr, nc ? ptr<int>(*norm_cid) : nullptr,
+                          fa ? ptr<float>(*fa_theta) : nullptr, fa ? ptr<double>(*fa_out) : nullptr,
+                          fa ? ptr<unsigned>(*fa_cnt) : nullptr, (int)fa_bits, fa_scale, (int)fa_n_norms,
+                          cur_stream()),
         "qfx_fedavg");
 }
 

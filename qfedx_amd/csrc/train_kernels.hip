@@ -442,16 +442,134 @@ __device__ __forceinline__ long long fedavg_term(float x, double tg, bool wr, in
   return llrint(v);
 }
 
+// round epilogue 2 for one entry e of the all-reduced buffer (qfx_round_apply_kernel below, or the last block of a
+// single-rank FedAvg reduce, FusedApply):
+// theta += lr * (sum w Delta) / (sum w) in float64, rounded to fp32 - the same operations as Aggregator.finalize +
+// apply; rounds with zero total weight keep theta.
+//   out[0..3] = metrics, out[4] = saturated FedAvg terms over all ranks (buf[P + 5], which this zeroes for the next
+//   round: nothing else reads it, and the next round's reduce runs after it), out[5] = weight sum
+// With SecAgg (bits > 0) the update and weight entries are ring elements: reduced mod 2^bits, read as signed and
+// divided by the SecAgg scale (decode_fixed); the metric tail stays plain 2^32 fixed point.  ``ld`` loads an entry
+// of buf (a device-coherent load when other blocks of the same launch wrote it).
+__device__ __forceinline__ double ring_decode(long long v, int bits, double scale) {
+  const long long m = (1LL << bits) - 1;
+  long long u = v & m;
+  if (u >> (bits - 1)) u -= (1LL << bits);
+  return (double)u / scale;
+}
+
+template <typename Ld>
+__device__ __forceinline__ void round_apply_elem(long long* buf, int P, float* theta, double lr, double* out, int bits,
+                                                 double ring_scale, int n_norms, long e, double wsum, Ld ld) {
+  const double SC = 4294967296.0;
+  if (e < P) {
+    const long long b = ld(e);
+    const double upd = bits ? ring_decode(b, bits, ring_scale) : (double)b / SC;
+    const double mean = upd / fmax(wsum, 1e-300);
+    const double th = (double)theta[e];
+    theta[e] = wsum > 0.0 ? (float)(th + lr * mean) : (float)th;
+  } else if (e < P + 6) {
+    const int j = (int)(e - P);
+    if (j < 4) {
+      out[j] = (double)ld(P + 1 + j) / SC;
+    } else if (j == 4) {
+      out[j] = (double)ld(P + 5);
+      buf[P + 5] = 0;
+    } else {
+      out[j] = wsum;
+    }
+  } else if (e < P + 6 + n_norms) {    // CC6 per-client norm slots: read out, zeroed for the next round
+    const int j = (int)(e - P);
+    out[j] = (double)ld(P + j) / SC;
+    buf[P + j] = 0;
+  }
+}
+
+// A single-rank round has no collective between the reduce and the apply, so the reduce launch applies it too (one
+// launch fewer per round): every parameter block knows the (exact, integer) weight sum - it is K loads - and applies
+// its own entries right after forming them; the last arriving block reads out the metric / norm tail.  Under SecAgg
+// the weight sum carries the masks, so only block 0 forms it and the last block applies every entry.
+// theta == nullptr: not fused.
+struct FusedApply {
+  float* theta;
+  double* out;
+  unsigned* cnt;           // arrival counter, reset by the last block
+  int bits, n_norms;
+  double ring_scale, lr;
+};
+
+// Arrival of one block of a FusedApply launch; the last one applies entries [params_done ? P : 0, P + 6 + n_norms).
+// ``release``: the block wrote what the last block reads (buffer entries, the metric pack, saturation counts) - its
+// stores are in this XCD's L2 after the barrier and one agent-scope release publishes them before the arrival (the
+// hea_grad_reduce Adam protocol).  A release is an L2 writeback on this chip, so blocks with nothing to publish (the
+// parameter blocks that applied their own entries) skip it.  ``ws``: the weight sum when every block knows it.
+__device__ __forceinline__ void fused_apply_tail(const FusedApply& fa, long long* buf, int P, bool params_done,
+                                                 bool release, long long ws) {
+  __shared__ int last_s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (release) __threadfence();
+    const unsigned prev = atomicAdd(fa.cnt, 1u);
+    last_s = prev == gridDim.x - 1;
+    if (last_s) *fa.cnt = 0u;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  auto ld = [buf](long i) { return __hip_atomic_load(&buf[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  const double wsum = params_done ? (double)ws / 4294967296.0
+                                  : (fa.bits ? ring_decode(ld(P), fa.bits, fa.ring_scale) : (double)ld(P) / 4294967296.0);
+  for (long e = (params_done ? P : 0) + threadIdx.x; e < (long)P + 6 + fa.n_norms; e += blockDim.x)
+    round_apply_elem(buf, P, fa.theta, fa.lr, fa.out, fa.bits, fa.ring_scale, fa.n_norms, e, wsum, ld);
+}
+
+// the weight sum (wave 0): lane-strided over the clients (one dependent global load per client made a serial loop
+// the launch's long pole at 64 clients), then an integer wave sum - exact, so the split changes no bit.  Under
+// SecAgg the weight is element P of each client's masked vector.
+__device__ __forceinline__ long long weight_sum_wave(const double* __restrict__ weights, int K, int P,
+                                                     const SecAgg& sa, int& wsat) {
+  const double SC = 4294967296.0;
+  long long ws = 0;
+  wsat = 0;
+  for (int k = threadIdx.x; k < K; k += 64) {
+    if (sa.seeds) {
+      const double v = weights[k] * sa.scale, lim = (double)(sa.mask >> 1);
+      if (!(fabs(v) <= lim)) ++wsat;
+      ws += ((long long)llrint(fmin(fmax(v, -lim), lim)) & sa.mask) + secagg_masks(sa, k, P, P);
+      continue;
+    }
+    const double v = weights[k] * SC;
+    if (!(fabs(v) <= FA_SAT)) ++wsat;
+    ws += llrint(fmin(fmax(v, -FA_SAT), FA_SAT));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    ws += __shfl_xor(ws, off, 64);
+    wsat += __shfl_xor(wsat, off, 64);
+  }
+  return ws;
+}
+
 __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
-    const float* __restrict__ theta_k, const float* __restrict__ theta_g,
+    const float* __restrict__ theta_k, const float* theta_g,     // theta_g may be fa.theta (applied in place)
     const unsigned char* __restrict__ angle_mask, const double* __restrict__ weights,
     const double* __restrict__ norms, const uint32_t* __restrict__ keys, int K, int P, int wrap,
     int dp, float clip, float sigma, long long* __restrict__ out, RoundPack rp, long long* __restrict__ sat,
-    SecAgg sa) {
+    SecAgg sa, FusedApply fa) {
+  const bool own_apply = fa.theta && !sa.seeds;       // every parameter block applies its own entries (FusedApply)
+  __shared__ long long ws_s;
   // the block past the parameter blocks (launched only with rp.buf) packs the round metrics into the tail of
   // the all-reduce buffer: the parameter blocks write out[0..P], the pack block out[P+1..P+4]
   if (blockIdx.x == gridDim.x - 1 && rp.buf != nullptr) {
     round_pack_block(rp, P);
+    if (fa.theta) {
+      if (own_apply && threadIdx.x < 64) {
+        int wsat;
+        const long long ws = weight_sum_wave(weights, K, P, sa, wsat);
+        if (threadIdx.x == 0) ws_s = ws;
+      }
+      __syncthreads();
+      fused_apply_tail(fa, rp.buf, P, own_apply, true, ws_s);
+    }
     return;
   }
   // thread (group g, lane el): parameter e = block * FA_E + el (a wave reads 256 contiguous bytes of a client
@@ -461,31 +579,17 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
   const double SC = 4294967296.0;
   const int el = threadIdx.x % FA_E, grp = threadIdx.x / FA_E;
   const long e = (long)blockIdx.x * FA_E + el;
-  if (blockIdx.x == 0 && threadIdx.x < 64) {
-    // the weight sum: lane-strided over the clients (one dependent global load per client made a serial loop the
-    // launch's long pole at 64 clients), then an integer wave sum - exact, so the split changes no bit
-    long long ws = 0;
-    int wsat = 0;
-    for (int k = threadIdx.x; k < K; k += 64) {
-      if (sa.seeds) {                  // the weight is element P of the client's masked vector
-        const double v = weights[k] * sa.scale, lim = (double)(sa.mask >> 1);
-        if (!(fabs(v) <= lim)) ++wsat;
-        ws += ((long long)llrint(fmin(fmax(v, -lim), lim)) & sa.mask) + secagg_masks(sa, k, P, P);
-        continue;
-      }
-      const double v = weights[k] * SC;
-      if (!(fabs(v) <= FA_SAT)) ++wsat;
-      ws += llrint(fmin(fmax(v, -FA_SAT), FA_SAT));
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      ws += __shfl_xor(ws, off, 64);
-      wsat += __shfl_xor(wsat, off, 64);
-    }
+  int wsat = 0;
+  if ((blockIdx.x == 0 || own_apply) && threadIdx.x < 64) {
+    const long long ws = weight_sum_wave(weights, K, P, sa, wsat);
     if (threadIdx.x == 0) {
-      out[P] = ws;
-      if (wsat && sat) atomicAdd((unsigned long long*)sat, (unsigned long long)wsat);
+      ws_s = ws;
+      if (blockIdx.x == 0) {
+        out[P] = ws;
+        if (wsat && sat) atomicAdd((unsigned long long*)sat, (unsigned long long)wsat);
+      }
     }
+    if (blockIdx.x != 0) wsat = 0;
   }
   long long acc = 0;
   int nsat = 0;
@@ -513,50 +617,26 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
     long long v = 0;
     for (int j = 0; j < FA_G; ++j) v += part[j][el];
     out[e] = v;
+    if (own_apply)        // ws_s was stored before the barrier above
+      round_apply_elem(out, P, fa.theta, fa.lr, fa.out, 0, 1.0, 0, e, (double)ws_s / SC, [v](long) { return v; });
+  }
+  if (fa.theta) {
+    // the last block reads this block's buffer entries only when it applies them (SecAgg); saturation counts it
+    // always reads
+    const bool counted = __syncthreads_or((nsat || wsat) ? 1 : 0);
+    fused_apply_tail(fa, rp.buf, P, own_apply, !own_apply || counted, ws_s);
   }
 }
 
 // round epilogue 1 on its own (the HIP round path packs in the FedAvg launch's last block instead)
 __global__ void __launch_bounds__(256) qfx_round_pack_kernel(RoundPack rp, int P) { round_pack_block(rp, P); }
 
-// round epilogue 2 (after the all-reduce): theta += lr * (sum w Delta) / (sum w) in float64, rounded to
-// fp32 - the same operations as Aggregator.finalize + apply; rounds with zero total weight keep theta.
-//   out[0..3] = metrics, out[4] = saturated FedAvg terms over all ranks (buf[P + 5], which this launch zeroes for
-//   the next round: nothing else reads it, and the next round's reduce runs after it), out[5] = weight sum
-// With SecAgg (bits > 0) the update and weight entries are ring elements: reduced mod 2^bits, read as signed and
-// divided by the SecAgg scale (decode_fixed); the metric tail stays plain 2^32 fixed point.
-__device__ __forceinline__ double ring_decode(long long v, int bits, double scale) {
-  const long long m = (1LL << bits) - 1;
-  long long u = v & m;
-  if (u >> (bits - 1)) u -= (1LL << bits);
-  return (double)u / scale;
-}
-
+// round epilogue 2 (after the all-reduce): round_apply_elem per entry
 __global__ void qfx_round_apply_kernel(long long* __restrict__ buf, int P, float* __restrict__ theta, double lr,
                                        double* __restrict__ out, int bits, double ring_scale, int n_norms) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const double SC = 4294967296.0;
-  const double wsum = bits ? ring_decode(buf[P], bits, ring_scale) : (double)buf[P] / SC;
-  if (e < P) {
-    const double upd = bits ? ring_decode(buf[e], bits, ring_scale) : (double)buf[e] / SC;
-    const double mean = upd / fmax(wsum, 1e-300);
-    const double th = (double)theta[e];
-    theta[e] = wsum > 0.0 ? (float)(th + lr * mean) : (float)th;
-  } else if (e < P + 6) {
-    const int j = (int)(e - P);
-    if (j < 4) {
-      out[j] = (double)buf[P + 1 + j] / SC;
-    } else if (j == 4) {
-      out[j] = (double)buf[P + 5];
-      buf[P + 5] = 0;
-    } else {
-      out[j] = wsum;
-    }
-  } else if (e < P + 6 + n_norms) {    // CC6 per-client norm slots: read out, zeroed for the next round
-    const int j = (int)(e - P);
-    out[j] = (double)buf[P + j] / SC;
-    buf[P + j] = 0;
-  }
+  const double wsum = bits ? ring_decode(buf[P], bits, ring_scale) : (double)buf[P] / 4294967296.0;
+  round_apply_elem(buf, P, theta, lr, out, bits, ring_scale, n_norms, e, wsum, [buf](long i) { return buf[i]; });
 }
 
 // Parameter-shift combine (ops/hea_mfma.py HeaMfmaProgram.param_shift): for client k and parameter j, the exact
@@ -884,7 +964,8 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                                  const float* loss, const float* correct, const float* nvalid, const float* act,
                                  int n_metrics, long long* sat, const uint32_t* sa_seeds, const int* sa_sign,
                                  const int* sa_round, int sa_n, double sa_scale, int sa_bits, long long* sa_masks,
-                                 const int* norm_cid, hipStream_t st) {
+                                 const int* norm_cid, float* fa_theta, double* fa_out, unsigned* fa_cnt,
+                                 int fa_bits, double fa_ring_scale, int fa_n_norms, hipStream_t st) {
   if (dp) {   // clipping needs the per-client norms; without DP they are not computed
     const int nc = (P + NORM_CHUNK - 1) / NORM_CHUNK;
     double* partial = norms + K;   // scratch tail of the norms buffer: K * nc doubles
@@ -902,7 +983,13 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                        st, sa, P);
   }
   const unsigned blocks = (unsigned)((P + FA_E - 1) / FA_E) + (pack_buf ? 1u : 0u);
+  // the fused apply reads the whole [P + 6 + n_norms] buffer this launch writes: it needs the pack block and the
+  // buffer head to be this launch's output
+  if (fa_theta && (!pack_buf || !fa_out || !fa_cnt || out != pack_buf || fa_bits < 0 || fa_bits > 62 ||
+                   fa_n_norms < 0 || (fa_bits != 0) != (sa_seeds != nullptr)))
+    return (int)hipErrorInvalidValue;
+  const FusedApply fa{fa_theta, fa_out, fa_cnt, fa_bits, fa_n_norms, fa_ring_scale, 1.0};
   hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3(blocks), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
-                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out, rp, sat, sa);
+                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out, rp, sat, sa, fa);
   return (int)hipGetLastError();
 }

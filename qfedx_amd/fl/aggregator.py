@@ -76,14 +76,17 @@ class Aggregator:
                      round_num: int, client_ids: list, participants: Optional[list] = None,
                      dropped: Optional[list] = None, out: Optional[torch.Tensor] = None,
                      keys: Optional[torch.Tensor] = None, pack: Optional[tuple] = None,
-                     secagg_tabs: Optional[tuple] = None, norm_cid: Optional[torch.Tensor] = None) -> torch.Tensor:
+                     secagg_tabs: Optional[tuple] = None, norm_cid: Optional[torch.Tensor] = None,
+                     apply: Optional[tuple] = None) -> torch.Tensor:
         """This rank's contribution [P+1] = [sum_k w_k priv(Delta_k) | sum_k w_k].
 
         float64 normally; int64 ring elements (mod 2^bits, masked) under secure aggregation.
         ``dropped`` clients (subset of participants, possibly on other ranks) had agreed masks but
         never deliver: survivors on this rank add the orphan-mask corrections.
         ``pack`` (HIP fast path only): (buf, loss, correct, nvalid, act) - the same launch also packs the round
-        metrics into the tail of the all-reduce buffer ``buf`` whose head is ``out``.
+        metrics into the tail of the all-reduce buffer ``buf`` whose head is ``out``.  ``apply`` (with ``pack``,
+        single-rank rounds): the same launch also applies the round to the global params
+        (``fedavg_hip.fused_local_reduce``).
         """
         if self.backend == "hip":
             from ..ops import fedavg_hip
@@ -105,12 +108,12 @@ class Aggregator:
                 theta_k, theta_g, weights, self._mask_u8, client_ids, round_num, self.seed,
                 wrap=self.wrap, dp=self.dp, clip_norm=self.clip_norm,
                 noise_multiplier=self.noise_multiplier, out=out, keys=keys, pack=pack, secagg=sa,
-                norm_cid=norm_cid)
+                norm_cid=norm_cid, apply=apply)
             self.last_norms = norms
             self.last_saturation = sat
             return out
-        if pack is not None:
-            raise ValueError("the metric pack is fused into the HIP reduce only")
+        if pack is not None or apply is not None:
+            raise ValueError("the metric pack and the apply are fused into the HIP reduce only")
         delta = theta_k.double() - theta_g.double()[None, :]
         if self.wrap:
             delta = torch.where(self.angle_mask[None, :], wrap_angles(delta), delta)

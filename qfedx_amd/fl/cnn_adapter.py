@@ -125,7 +125,7 @@ class CNNClientTrainer:
                 loss_all[s].copy_(res["loss"])
                 correct_all[s].copy_(res["correct"])
         if epilogue is not None:
-            epilogue(params, dict(dv, loss=loss_all, correct=correct_all), theta_g.to(self.device).float())
+            epilogue(params, dict(dv, loss=loss_all, correct=correct_all, eager=True), theta_g.to(self.device).float())
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
                 "lid": dv["lid"], "weights": dv["w"], "samples": float(nvalid.sum()), "steps": int(sum(plan.steps_per_client)),
                 "client_ids": cids, "n_samples": store.counts[li].to(torch.float64)}

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import json
 import math
+import os
 import time
 from typing import Optional
 
@@ -35,6 +36,11 @@ from ..utils.seeding import generator, np_rng
 from ..utils.timing import PhaseTimer
 from .aggregator import EXACT_SCALE, Aggregator
 from .trainer import ShardStore
+
+# single-rank rounds apply the update inside the FedAvg reduce launch (FusedApply: every block arrives on one counter)
+# up to this many buffer entries: past it the arrivals, one same-address atomic per 64-parameter block, cost more
+# than the round_apply launch they save (CFed TinyCNN, 128 clients: +9 us per round, profiles/r4_round_structure_ab.txt)
+FUSED_APPLY_MAX = 4096
 
 
 def sample_participants(num_clients: int, fraction: float, seed: int, round_num: int,
@@ -255,20 +261,38 @@ class FederatedRunner:
             ring = (p.secagg_bits, p.secagg_scale) if p.secure_agg else (0, 1.0)
             world, params_g, outs = self.world, self.params, self._round_outs
 
+            fused = self.__dict__.setdefault("_apply_fused", {})
+
             def post(v):
                 # ONE collective per round (CC2+CC3), then finalize + apply in place; captured into the round
-                # graph (variant v writes metrics buffer v) when the collective allows it
+                # graph (variant v writes metrics buffer v) when the collective allows it.  A single-rank round whose
+                # epilogue already applied (variant v, in the same capture) has nothing left to do.
+                if fused.pop("variant", None) == v:
+                    return
                 all_reduce_(buf, world)
                 from ..ops._ext import ext
                 ext().round_apply(buf, P, params_g, 1.0, outs[v], *ring, NN)
 
             def epilogue(params_k, tabs, theta):
-                # one launch: the fused reduce writes the buffer head, its last block packs the metrics
+                # one launch: the fused reduce writes the buffer head, its last block packs the metrics.  Single
+                # rank, with post(v) known to follow (captured right behind it: tabs["variant"] = v; eager: the
+                # variant post will take) the same launch also applies the round (no collective in between), one
+                # launch fewer per round
                 sa = (tabs["sa_seed"], tabs["sa_sign"], tabs["sa_round"]) if "sa_seed" in tabs else None
+                v = tabs.get("variant", self._flip if tabs.get("eager") else None)
+                apply = None
+                fused.pop("variant", None)
+                if (v is not None and not world.distributed and P + 6 + NN <= FUSED_APPLY_MAX
+                        and os.environ.get("QFEDX_FUSED_APPLY", "1") != "0"
+                        and theta.data_ptr() == params_g.data_ptr()):
+                    if getattr(self, "_apply_cnt", None) is None:
+                        self._apply_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+                    apply = (params_g, outs[v], self._apply_cnt, *ring, NN)
+                    fused["variant"] = v
                 agg.local_reduce(params_k, theta, tabs.get("fw", tabs["w"]), r, ids, out=buf[: P + 1],
                                  keys=tabs.get("dpkeys"), secagg_tabs=sa, norm_cid=tabs.get("cid"),
                                  pack=(buf, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
-                                       tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)))
+                                       tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)), apply=apply)
             graph_comm = self.graph_comm
             with self.timer.phase("local_train"):
                 res = trainer.run_round(self.store, local_alive, self.params, r, epilogue=epilogue,

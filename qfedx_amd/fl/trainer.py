@@ -361,8 +361,8 @@ class VQCClientTrainer:
             params, loss_all, correct_all = self._body(store.X, store.y, dv["lid"], theta, dv["idx"],
                                                        dv["wts"], dv["act"], plan.max_steps, round_num, method,
                                                        traj_keys, ro_keys)
-            if epilogue is not None:
-                epilogue(params, dict(dv, loss=loss_all, correct=correct_all), theta)
+            if epilogue is not None:    # eager: ``post`` (if any) runs right after, on the caller's side
+                epilogue(params, dict(dv, loss=loss_all, correct=correct_all, eager=True), theta)
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
                 "lid": dv["lid"], "weights": dv["w"], "post_done": post_v is not None, "post_variant": post_v,
                 **common}
@@ -408,10 +408,14 @@ class VQCClientTrainer:
             args = (store.X, store.y, dv["lid"], ent["theta"], dv["idx"], dv["wts"], dv["act"], plan.max_steps,
                     round_num, "adjoint")
 
-            def body():
+            def body(variant=None):
+                # ``variant``: set when post(variant) is captured right behind the epilogue (it may fold into it)
                 out = self._body(*args)
                 if epilogue is not None:
-                    epilogue(out[0], dict(dv, loss=out[1], correct=out[2]), ent["theta"])
+                    tabs = dict(dv, loss=out[1], correct=out[2])
+                    if variant is not None:
+                        tabs["variant"] = variant
+                    epilogue(out[0], tabs, ent["theta"])
                 return out
             # the graph owns its workspaces: eager calls (evaluation) can never regrow/free them
             ent["ws"] = {}
@@ -430,7 +434,7 @@ class VQCClientTrainer:
                     try:
                         with torch.cuda.graph(g):
                             E.host_upload(ent["pin"][v][: up.nbytes], pack, ent["ctr"], ent["flag"])
-                            out = body()
+                            out = body(v if ent["post_in_graph"] else None)
                             if ent["post_in_graph"]:
                                 post(v)
                     except Exception as exc:

@@ -29,7 +29,8 @@ def dp_noise_keys(client_ids, round_num, seed) -> torch.Tensor:
 
 
 def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp, clip_norm,
-                       noise_multiplier, out=None, keys=None, pack=None, sat=None, secagg=None, norm_cid=None):
+                       noise_multiplier, out=None, keys=None, pack=None, sat=None, secagg=None, norm_cid=None,
+                       apply=None):
     """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as exact int64 fixed point (scale 2^32)
     [P+1] (per-client terms rounded before the sum -> rank-count invariant), plus norms [K].
     ``angle_mask`` uint8 [P] on the device; ``out`` an optional int64 [P+1] destination (e.g. the head
@@ -44,6 +45,9 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
     [P + 1] head holds SecAgg ring elements instead, each client's term masked in the kernel
     (``SecureAggregator.round_tables``).  ``norm_cid`` (device int32 [K] global client ids; needs ``pack`` and
     DP): the pack block scatters the clients' pre-clip norms into ``buf[P + 6 + id]`` (CC6).
+    ``apply`` = (theta [P] float32, outs float64 [6 + n_norms], counter int32 [1] zeroed, bits, ring scale,
+    n_norms): single-rank rounds (no collective between reduce and apply) - the launch's last block also does
+    ``round_apply``'s work (needs ``pack``).
     Returns (out, norms, sat)."""
     K, P = theta_k.shape
     dev = theta_k.device
@@ -74,5 +78,5 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
                  *((secagg[0].contiguous(), secagg[1].contiguous(), secagg[2].contiguous(), float(secagg[3]),
                     int(secagg[4]), torch.empty(K * (P + 1), dtype=torch.int64, device=dev))
                    if secagg is not None else (None, None, None, 1.0, 48, None)),
-                 norm_cid)
+                 norm_cid, *(apply if apply is not None else (None, None, None, 0, 1.0, 0)))
     return out, (norms[:K] if dp else None), sat

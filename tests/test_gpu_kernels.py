@@ -264,6 +264,44 @@ def test_fedavg_launch_packs_round_metrics(cuda, dp):
     assert bufs[0][P + 5] == 0
 
 
+@pytest.mark.parametrize("dp,P", [(False, 300), (True, 300), (False, 5000)])
+def test_fedavg_fused_apply_matches_round_apply(cuda, dp, P):
+    """Single-rank rounds: the FedAvg reduce whose last arriving block applies the round == reduce + round_apply
+    (bitwise params, metrics, saturation count, weight sum and CC6 norm slots), twice in a row (the arrival counter
+    resets itself)."""
+    from qfedx_amd.ops import fedavg_hip
+    from qfedx_amd.ops._ext import ext
+    K, n, NN = 6, 24, 9 if dp else 0
+    g = torch.Generator().manual_seed(P + dp)
+    mask = (torch.arange(P) < P // 2).to(torch.uint8).to(cuda)
+    cid = torch.tensor([0, 2, 3, 5, 7, 8], dtype=torch.int32).to(cuda) if dp else None
+    keys = torch.randint(0, 2 ** 31 - 1, (K, 2), generator=g, dtype=torch.int64).to(torch.int32).to(cuda)
+    theta0 = torch.randn(P, generator=g).to(cuda)
+    thetas, outs = {}, {}
+    cnt = torch.zeros(1, dtype=torch.int32, device=cuda)
+    for fused in (True, False):
+        gg = torch.Generator().manual_seed(7)
+        theta = theta0.clone()
+        buf = torch.zeros(P + 6 + NN, dtype=torch.int64, device=cuda)
+        res = []
+        for r in range(2):
+            tk = (theta[None] + torch.randn(K, P, generator=gg).to(cuda) * 0.1).contiguous()
+            w = (torch.rand(K, generator=gg).double() + 0.5).to(cuda)
+            mets = [torch.rand(n, generator=gg).to(cuda) for _ in range(4)]
+            out = torch.full((6 + NN,), -1.0, dtype=torch.float64, device=cuda)
+            fedavg_hip.fused_local_reduce(tk, theta, w, mask, list(range(K)), r, 9, True, dp, 0.8, 1.1,
+                                          out=buf[: P + 1], keys=keys, pack=(buf, *mets), norm_cid=cid,
+                                          apply=(theta, out, cnt, 0, 1.0, NN) if fused else None)
+            if not fused:
+                ext().round_apply(buf, P, theta, 1.0, out, 0, 1.0, NN)
+            res.append(out.cpu())
+        thetas[fused], outs[fused] = theta.cpu(), res
+    assert torch.equal(thetas[True], thetas[False]) and not torch.equal(thetas[True], theta0.cpu())
+    for a, b in zip(outs[True], outs[False]):
+        assert torch.equal(a, b)
+    assert int(cnt.item()) == 0
+
+
 def test_fedavg_saturation_is_counted_not_wrapped(cuda):
     """A fixed-point term past 2^53 (w * Delta > 2^21) is clamped and counted; round_apply reports the count
     and zeroes the counter for the next round."""
@@ -432,6 +470,15 @@ def test_secagg_masks_in_fused_reduce_match_host_protocol(cuda, dp, bits):
     ext().round_apply(buf, P, theta, 1.0, out, sa.bits, sa.scale, 0)
     ref = gpu.apply(tg.to(cuda), mb.to(cuda), wsum=wb)
     assert torch.equal(theta, ref) and abs(out[5].item() - float(wb)) < 1e-12
+    # single rank: the same reduce launch applies the ring sum itself (its last block, FusedApply) == round_apply
+    buf2 = torch.zeros(P + 6, dtype=torch.int64, device=cuda)
+    theta2 = tg.to(cuda).clone()
+    out2 = torch.zeros(6, dtype=torch.float64, device=cuda)
+    mets = [torch.zeros(4, device=cuda) for _ in range(4)]
+    cnt = torch.zeros(1, dtype=torch.int32, device=cuda)
+    gpu.local_reduce(tk.to(cuda), theta2, w.to(cuda), 4, ids, participants=participants, dropped=dropped,
+                     out=buf2[: P + 1], pack=(buf2, *mets), apply=(theta2, out2, cnt, sa.bits, sa.scale, 0))
+    assert torch.equal(theta2, theta) and out2[5].item() == out[5].item() and int(cnt.item()) == 0
 
 
 def test_dp_client_norms_ride_in_round_buffer(cuda):
