@@ -111,6 +111,25 @@ def test_fused_fedavg_reduce_matches_torch(cuda, dp):
     assert torch.allclose(a, b, atol=1e-6, rtol=1e-6), (a - b).abs().max()
 
 
+@pytest.mark.parametrize("K,P", [(150, 20000), (150, 20003), (37, 16385), (64, 300), (130, 113859), (20, 9001)])
+def test_fedavg_fixed_point_sum_exact(cuda, K, P):
+    """The FedAvg reduce's int64 sums equal the host's exact fixed-point sums bitwise, over client counts that take
+    every client-batch path (4 rows in flight per thread, single rows) and the CFed TinyCNN's vector length."""
+    import numpy as np
+    from qfedx_amd.ops import fedavg_hip
+    g = torch.Generator().manual_seed(K + P)
+    tk = torch.randn(K, P, generator=g) * 0.2
+    tg = torch.randn(P, generator=g)
+    w = torch.rand(K, generator=g).double() * 30 + 0.5
+    mask = torch.zeros(P, dtype=torch.uint8, device=cuda)
+    out, _, sat = fedavg_hip.fused_local_reduce(tk.to(cuda), tg.to(cuda), w.to(cuda), mask, list(range(K)), 0, 0,
+                                                False, False, 1.0, 0.0)
+    d = tk.double().numpy() - tg.double().numpy()[None, :]
+    terms = np.rint(w.numpy()[:, None] * d * 4294967296.0).astype(np.int64)
+    ref = np.concatenate([terms.sum(0), [np.rint(w.numpy() * 4294967296.0).astype(np.int64).sum()]])
+    assert np.array_equal(out.cpu().numpy(), ref) and int(sat.item()) == 0
+
+
 @pytest.mark.parametrize("fraction,sampling,dp", [(1.0, "fixed", False), (0.5, "fixed", False),
                                                   (0.5, "poisson", False), (0.5, "poisson", True)])
 def test_graph_round_matches_eager(cuda, fraction, sampling, dp):
