@@ -236,6 +236,9 @@ class FederatedRunner:
             # arguments.
             if getattr(self, "_round_buf", None) is None:
                 self._round_buf = torch.zeros(P + 6 + self.n_norm_slots, dtype=torch.int64, device=dev)
+                # FusedApply arrival counter (self-resetting); allocated here, eagerly: created inside the round
+                # graph's capture, its zero fill would become a node replayed every round
+                self._apply_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
             buf = self._round_buf
             extra = {}
             if p.dp and ids:
@@ -285,8 +288,6 @@ class FederatedRunner:
                 if (v is not None and not world.distributed and P + 6 + NN <= FUSED_APPLY_MAX
                         and os.environ.get("QFEDX_FUSED_APPLY", "1") != "0"
                         and theta.data_ptr() == params_g.data_ptr()):
-                    if getattr(self, "_apply_cnt", None) is None:
-                        self._apply_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
                     apply = (params_g, outs[v], self._apply_cnt, *ring, NN)
                     fused["variant"] = v
                 agg.local_reduce(params_k, theta, tabs.get("fw", tabs["w"]), r, ids, out=buf[: P + 1],
