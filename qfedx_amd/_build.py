@@ -2,7 +2,9 @@
 
 ``QFEDX_DEBUG=1`` (or ``python -m qfedx_amd._build --debug``) builds the separate debug extension
 ``qfedx_amd._qfedx_C_debug`` with device-side bounds checks (``csrc/qfx_check.h``) into ``build/qfx_debug``;
-``QFEDX_DEBUG=1`` at run time makes ``ops/_ext.py`` load it instead of the release one.
+``QFEDX_DEBUG=1`` at run time makes ``ops/_ext.py`` load it instead of the release one.  ``--stamps``
+(``QFEDX_STAMPS=1``) likewise builds / loads ``qfedx_amd._qfedx_C_stamps``: the MFMA pass kernels with per-wave
+s_memtime phase stamps (``-DQFX_HEA_STAMPS=1``, stall attribution: scripts/hea_stamps.py), never the release path.
 
 Device code (``csrc/*.hip``) is compiled by ``hipcc --offload-arch=gfx950``; host bindings
 (``csrc/*.cpp``: planner + pybind11/torch glue) by g++ against torch's headers; everything is linked
@@ -26,11 +28,25 @@ CSRC = os.path.join(HERE, "csrc")
 ARCH = os.environ.get("QFEDX_ARCH", "gfx950")
 
 
+def variant(debug=None) -> str:
+    """release | debug | stamps (``debug``: True / False forces debug / release; None reads the environment)."""
+    if debug is not None:
+        return "debug" if debug else "release"
+    if os.environ.get("QFEDX_DEBUG", "0") == "1":
+        return "debug"
+    if os.environ.get("QFEDX_STAMPS", "0") == "1":
+        return "stamps"
+    return "release"
+
+
+_VARIANTS = {"release": ("qfx", "_qfedx_C", []), "debug": ("qfx_debug", "_qfedx_C_debug", ["-DQFX_DEVICE_CHECKS=1"]),
+             "stamps": ("qfx_stamps", "_qfedx_C_stamps", ["-DQFX_HEA_STAMPS=1"])}
+
+
 def _mode(debug):
-    if debug is None:
-        debug = os.environ.get("QFEDX_DEBUG", "0") == "1"
-    return (os.path.join(HERE, "..", "build", "qfx_debug" if debug else "qfx"),
-            "_qfedx_C_debug" if debug else "_qfedx_C", bool(debug))
+    v = debug if isinstance(debug, str) else variant(debug)
+    d, name, flags = _VARIANTS[v]
+    return os.path.join(HERE, "..", "build", d), name, flags
 
 
 def ext_path(debug=None) -> str:
@@ -78,10 +94,9 @@ def _run(cmd):
 
 
 def build(verbose: bool = False, force: bool = False, debug=None) -> str:
-    BUILD, EXT_NAME, dbg = _mode(debug)
+    BUILD, EXT_NAME, checks = _mode(debug)
     os.makedirs(BUILD, exist_ok=True)
-    checks = ["-DQFX_DEVICE_CHECKS=1"] if dbg else []
-    extra = os.environ.get("QFEDX_EXTRA_HIPFLAGS", "").split()   # e.g. -DQFX_HEA_ABLATE=1 (timing builds)
+    extra = os.environ.get("QFEDX_EXTRA_HIPFLAGS", "").split()   # e.g. -DQFX_HEA_GATE_LO=0 (A/B builds)
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     hips = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     cpps = sorted(glob.glob(os.path.join(CSRC, "*.cpp")))
@@ -125,7 +140,7 @@ def build(verbose: bool = False, force: bool = False, debug=None) -> str:
                 stamps[obj] = key
                 if verbose:
                     print("compiled", os.path.basename(obj))
-    out = ext_path(dbg)
+    out = ext_path(debug)
     link_key = _hash(objs) if all(os.path.exists(o) for o in objs) else ""
     if jobs or stamps.get("__link__") != link_key or not os.path.exists(out):
         cmd = ["hipcc", "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", out + ".tmp",
@@ -143,5 +158,6 @@ def build(verbose: bool = False, force: bool = False, debug=None) -> str:
 
 
 if __name__ == "__main__":
-    p = build(verbose=True, force="--force" in sys.argv, debug=True if "--debug" in sys.argv else None)
+    v = "debug" if "--debug" in sys.argv else ("stamps" if "--stamps" in sys.argv else None)
+    p = build(verbose=True, force="--force" in sys.argv, debug=v)
     print(p)

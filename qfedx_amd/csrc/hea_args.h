@@ -3,6 +3,9 @@
 #pragma once
 #include <cstdint>
 
+// Rows of the stall-attribution buffer (stamps build): STAMP_WG = 2048 workgroups x up to 16 waves.
+constexpr int HEA_STAMP_ROWS = 2048 * 16;
+
 struct HeaPassArgs {
   const int* ops;            // [nops][128] op records (hea_plan.py)
   const int* fidx;           // [nops] unitary fragment index (slot * 4 + 0 | 2) or -1
@@ -26,11 +29,8 @@ struct HeaPassArgs {
   int slab_tiles;
   int n_gradops;
   int hrow[5];               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
-  long long* dbg;            // optional phase timestamps (s_memtime) of workgroups < 8, [8][64]
+  long long* dbg;            // stamps build only (QFX_HEA_STAMPS): per-wave phase cycles, [HEA_STAMP_ROWS][16]
   int in_rep;                // forward: shifted parameter rows per stored input sample (param-shift prefix reuse)
-  int pair;                  // forward: two samples per workgroup on 2^13 tiles (hea_fwd2_kernel)
-  int ablate;                // timing ablations (builds with QFX_HEA_ABLATE only; QFEDX_HEA_ABLATE bit mask)
-  uint32_t poison;           // diagnostics: != 0 fills every LDS word with this value at workgroup start
   // Fused readout (first adjoint pass, noiseless): every workgroup computes its sample's <Z>, cross entropy and
   // dL/d<Z> from the readout partials (part, ro_tps tiles) instead of reading wread; the tile-0 workgroup writes
   // ro_expz / ro_w [S][C] (the later passes' wread) and the per-sample reduction record ro_rec [S][2C + 2]

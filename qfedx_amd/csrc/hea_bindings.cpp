@@ -27,8 +27,6 @@ int qfx_hea_pass_bf16(int adjoint, const HeaPassArgs* args, int n_samples, hipSt
 int qfx_hea_frags_bf16(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                        hipStream_t st);
 int qfx_hea_check_status_bf16(hipStream_t st);
-int qfx_hea_set_knob(const char* name, int value);
-int qfx_hea_set_knob_bf16(const char* name, int value);
 }
 
 namespace {
@@ -61,15 +59,16 @@ void check(int rc, const char* what) {
 }
 
 // geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
-//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, pair[, bf16]]
-// bf16 (optional, default 0): states and fragments in bf16 (hea_mfma_bf16.hip) instead of fp16
+//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, bf16]
+// bf16: states and fragments in bf16 (hea_mfma_bf16.hip) instead of fp16.  dbg: the stall-attribution buffer of the
+// stamps build (int64 [HEA_STAMP_ROWS * 16]; empty otherwise)
 void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<int64_t> geom, double scale, torch::Tensor psi_in,
               torch::Tensor psi_out, torch::Tensor lam_in, torch::Tensor lam_out, torch::Tensor xang,
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
               torch::Tensor gslab, torch::Tensor dbg, c10::optional<std::vector<torch::Tensor>> readout,
               int64_t ro_tps) {
-  need(geom.size() == 28 || geom.size() == 29, "geometry vector must have 28 or 29 entries");
-  const bool bf16 = geom.size() == 29 && geom[28] != 0;
+  need(geom.size() == 28, "geometry vector must have 28 entries");
+  const bool bf16 = geom[27] != 0;
   HeaPassArgs a{};
   a.n = (int)geom[0];
   a.t = (int)geom[1];
@@ -91,27 +90,11 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.n_slots = (int)geom[17];
   a.slab_tiles = (int)geom[18];
   const int64_t K = geom[19];
-  {
-    static int ablate = -1;    // only the QFX_HEA_ABLATE timing builds read it
-    if (ablate < 0) {
-      const char* e = getenv("QFEDX_HEA_ABLATE");
-      ablate = e ? atoi(e) : 0;
-    }
-    a.ablate = ablate;
-    // QFEDX_HEA_POISON=<hex>: fill all of a pass kernel's LDS with this word before it starts (uninitialised-read
-    // diagnostics; results must not depend on it)
-    static long long poison = -1;
-    if (poison < 0) {
-      const char* e = getenv("QFEDX_HEA_POISON");
-      poison = e ? (long long)(strtoull(e, nullptr, 0) & 0xffffffffull) : 0;
-    }
-    a.poison = (uint32_t)poison;
-  }
   a.n_gradops = (int)geom[25];
   a.in_rep = (int)geom[26];
-  a.pair = (int)geom[27];
   a.scale = (float)scale;
-  a.dbg = dbg.defined() && dbg.numel() >= 8 * 64 ? dp<long long>(dbg, torch::kInt64, "dbg", 8 * 64) : nullptr;
+  a.dbg = dbg.defined() && dbg.numel() > 0 ? dp<long long>(dbg, torch::kInt64, "dbg", (int64_t)HEA_STAMP_ROWS * 16)
+                                           : nullptr;
   for (int b = 0; b < 5; ++b) {
     a.hrow[b] = (int)geom[20 + b];
     need(a.hrow[b] >= 0 && a.hrow[b] < (1 << (a.t - 5)), "swizzle row reads past the tile bits");
@@ -131,7 +114,6 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.fidx = a.nops ? dp<int>(fidx, torch::kInt32, "fidx", a.nops) : nullptr;
   need(a.in_rep >= 1 && (!adjoint || a.in_rep == 1) && K % a.in_rep == 0,
        "in_rep: forward only, parameter rows a multiple of it");
-  need(!a.pair || (!adjoint && a.t == 13 && a.spc % 2 == 0), "paired forward: forward passes on 2^13 tiles, even spc");
   const int64_t states = S << a.n;
   a.psi_in = a.gen ? nullptr : dp<uint32_t>(psi_in, torch::kInt32, "psi_in", states / a.in_rep);
   need(!(adjoint && a.store_psi), "adjoint passes store lambda only");
@@ -139,8 +121,8 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.lam_in = (adjoint && a.load_lam) ? dp<uint32_t>(lam_in, torch::kInt32, "lam_in", states) : nullptr;
   a.lam_out = (adjoint && a.store_lam) ? dp<uint32_t>(lam_out, torch::kInt32, "lam_out", states) : nullptr;
   need(a.x_stride >= a.n, "x stride must cover n feature angles");
-  // layer-1 factors: the product-state generation (forward gen passes) and OP_L1PROD (adjoint passes)
-  a.xang = (a.gen || adjoint) ? dp<float>(xang, torch::kFloat32, "xang", S / a.in_rep * a.x_stride) : nullptr;
+  // layer-1 factors: the product-state generation (forward gen passes)
+  a.xang = a.gen ? dp<float>(xang, torch::kFloat32, "xang", S / a.in_rep * a.x_stride) : nullptr;
   a.params = dp<float>(params, torch::kFloat32, "params", K * a.p_stride);
   a.frags = a.n_slots ? (const void*)dp<int32_t>(frags, torch::kInt32, "frags", K * a.n_slots * 4 * 128 * 4) : nullptr;
   a.part = dp<float>(part, torch::kFloat32, "part", 0);
@@ -184,33 +166,23 @@ void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64
        ops.is_contiguous(), "ops must be a contiguous host int32 [nops, 128] tensor");
   const int* ow = ops.data_ptr<int>();
   int ngrad = 0;
-  for (int64_t o = 0; o < ops.size(0); ++o) ngrad += (ow[o * 128] == 4 || ow[o * 128] == 5 || ow[o * 128] == 8);
+  // op codes (hea_plan.py): 1 APPLY, 5 GRAD_L1, 6 OBS, 7 READOUT, 8 BACK
+  for (int64_t o = 0; o < ops.size(0); ++o) ngrad += (ow[o * 128] == 5 || ow[o * 128] == 8);
   need(ngrad <= 12, "at most 12 gradient ops per pass program");
   need(ops.size(0) <= 128, "at most 128 ops per pass program");
   for (int64_t o = 0; o < ops.size(0); ++o) {
     const int* w = ow + o * 128;
     const int code = w[0];
-    need(code >= 1 && code <= 9, "unknown op code");
-    need(adjoint || code == 1 || code == 7, "adjoint op in a forward pass");
-    if (code == 9) {   // OP_L1PROD: the program's last op; entries = tile bit | group << 8 | index << 16
-      need(o == ops.size(0) - 1, "the layer-1 product-state op must be the last op");
-      need(w[2] >= 1 && w[2] <= 16 && w[2] <= t, "layer-1 qubit count out of range");
-      int groups = 0;
-      for (int e = 0; e < w[2]; ++e) {
-        need((w[20 + e] & 255) < t && ((w[20 + e] >> 16) & 255) < 4, "layer-1 entry out of range");
-        groups = std::max(groups, ((w[20 + e] >> 8) & 255) + 1);
-      }
-      need(w[100] >= 0 && w[100] + groups <= n_gradops, "layer-1 gradient records out of range");
-      continue;
-    }
-    if (code <= 3 || code == 8) need(w[1] >= 0 && w[1] < n_slots, "op names a missing unitary slot");
-    if (code <= 5 || code == 8) {
+    need(code == 1 || code == 5 || code == 6 || code == 7 || code == 8, "unknown op code");
+    need(adjoint ? (code == 5 || code == 6 || code == 8) : (code == 1 || code == 7), "op kind not valid in this pass");
+    if (code == 1 || code == 8) need(w[1] >= 0 && w[1] < n_slots, "op names a missing unitary slot");
+    if (code == 1 || code == 5 || code == 8) {
       need(w[2] >= 0 && w[2] <= 4, "group size out of range");
       for (int j = 0; j < w[2]; ++j)
         need(w[12 + j] >= 0 && w[12 + j] < n_theta && w[16 + j] >= 0 && w[16 + j] < n_theta,
              "gradient slot out of range");
       for (int i = 20; i < 100; ++i) need(w[i] >= 0 && w[i] < (1 << t), "tile address out of range");
-      if (code >= 4 && code != 6 && code != 7) need(w[100] >= 0 && w[100] < n_gradops, "gradient op index out of range");
+      if (code != 1) need(w[100] >= 0 && w[100] < n_gradops, "gradient op index out of range");
     }
     if (code == 6 || code == 7) need(w[2] >= 1 && w[2] <= 8, "observable count out of range");
   }
@@ -276,17 +248,13 @@ void register_hea(pybind11::module& m) {
   m.def("hea_frags", &hea_frags, pybind11::arg("params"), pybind11::arg("p_stride"), pybind11::arg("slot_tab"),
         pybind11::arg("n_slots"), pybind11::arg("K"), pybind11::arg("frags"), pybind11::arg("bf16") = false);
   m.def("hea_check_ops", &hea_check_ops);
-  // launch-variant knobs of both storage builds (planes | fuse | adj_waves); returns the previous fp16-build value
-  m.def("hea_set_knob", [](const std::string& name, int value) {
-    qfx_hea_set_knob_bf16(name.c_str(), value);
-    return qfx_hea_set_knob(name.c_str(), value);
-  });
   m.def("hea_grad_reduce", &hea_grad_reduce, pybind11::arg("gslab"), pybind11::arg("slab_tiles"),
         pybind11::arg("n_gradops"), pybind11::arg("gmeta"), pybind11::arg("spc"), pybind11::arg("K"),
         pybind11::arg("params"), pybind11::arg("grad"), pybind11::arg("p_stride"),
         pybind11::arg("adam") = pybind11::none(), pybind11::arg("hyper") = pybind11::none(),
         pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_c") = 0, pybind11::arg("ro_ntheta") = 0);
   m.def("hea_args_size", []() { return qfx_hea_args_size(); });
+  m.attr("HEA_STAMP_ROWS") = HEA_STAMP_ROWS;
   // -1: release build (no device checks); 0: no failure since the last read; else the failing source line
   m.def("hea_check_status", []() { return qfx_hea_check_status(cur()); });
 }

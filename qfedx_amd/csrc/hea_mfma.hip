@@ -47,33 +47,25 @@
 __device__ unsigned int qfx_check_word = 0;
 #endif
 
-// Timing ablations (scripts/gpu_ab_*.sh): a build with -DQFX_HEA_ABLATE=1 skips parts of every op by the bit mask
-// QFEDX_HEA_ABLATE (1 op barriers, 2 gradient atomics, 4 cross matrices, 8 unitary applications, 16 gradient-region
-// flushes, 32 the adjoint tile load, 64 next-op record / fragment staging).  Results are wrong in such a build;
-// release builds compile the checks out.
-#ifndef QFX_HEA_ABLATE
-#define QFX_HEA_ABLATE 0
-#endif
 // Gate precision: 1 (default) applies every unitary as its fp16 hi + lo halves (exact to ~2^-22), 0 as the hi half
 // only (fp16-rounded gate: half the apply MFMAs).
 #ifndef QFX_HEA_GATE_LO
 #define QFX_HEA_GATE_LO 1
 #endif
-// LDS poison fill (a.poison, QFEDX_HEA_POISON): compiled in unless -DQFX_HEA_POISON=0
-#ifndef QFX_HEA_POISON
-#define QFX_HEA_POISON 1
-#endif
-// Phase timestamps (HEA_MARK, a.dbg) exist only in timing builds: in release builds the stamp pointer folds to null
-// and its bookkeeping (a pointer and a counter live across the op loop) leaves the kernels' scalar registers free.
-#ifndef QFX_HEA_MARKS
-#define QFX_HEA_MARKS QFX_HEA_ABLATE
+// Stall attribution (diagnostic build only: python -m qfedx_amd._build --stamps -> _qfedx_C_stamps, -DQFX_HEA_STAMPS=1).
+// Every wave of the first STAMP_WG workgroups of a pass adds the s_memtime cycles of each phase (enum Ph) into its own
+// row of a.dbg; scripts/hea_stamps.py turns the rows into the per-op-phase table.  In the release build no stamp
+// executes and the bookkeeping folds away.
+#ifndef QFX_HEA_STAMPS
+#define QFX_HEA_STAMPS 0
 #endif
 
 namespace HEA_NS {
 
 constexpr int OPW = 128;
-enum { OP_APPLY = 1, OP_UNAPPLY_PSI = 2, OP_UNAPPLY_LAM = 3, OP_GRAD = 4, OP_GRAD_L1 = 5, OP_OBS = 6, OP_READOUT = 7,
-       OP_BACK = 8, OP_L1PROD = 9 };
+// (codes 2, 3, 4 and 9 were measured-and-rejected variants: un-apply-only ops of a recomputed last pass, the
+// cross-only gradient op of the non-fused BACK form, the layer-1 product-state op; docs/ARCHITECTURE.md keeps the A/Bs)
+enum { OP_APPLY = 1, OP_GRAD_L1 = 5, OP_OBS = 6, OP_READOUT = 7, OP_BACK = 8 };
 enum { W_CODE = 0, W_SLOT = 1, W_NREAL = 2, W_FLAGS = 3, W_RFULL = 4, W_RT = 8, W_TH = 12, W_PH = 16, W_OFF = 20,
        W_BL = 36, W_BH = 68, W_GIDX = 100 };
 constexpr double FIX = 4294967296.0;   // 2^32: fixed point of the scaled gradient partial traces
@@ -139,13 +131,56 @@ __device__ __forceinline__ int par(uint32_t x) { return __builtin_popcount(x) & 
 // the s_barrier is sufficient; global results (gslab, stored tiles) are never read back inside the kernel.
 __device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// Diagnostics (a.poison != 0, QFEDX_HEA_POISON): fill an LDS array with the poison word before the kernel touches it, so
-// a read of LDS this workgroup never wrote shows up as a result that depends on the poison value.
-template <typename T>
-__device__ __forceinline__ void poison_lds(T* p, int bytes, uint32_t v, int tid, int nt) {
-  uint32_t* w = (uint32_t*)p;
-  for (int i = tid; i < bytes / 4; i += nt) w[i] = v;
-}
+// Stall-attribution phases: per wave, the cycles between consecutive marks go to the phase named by the LATER mark.
+//   PRO     kernel start -> tile-load issue (record / fragment staging, readout inputs)
+//   LOAD    tile load or product-state generation, up to the first op barrier's arrival
+//   BAR     op barriers: arrival -> release (waiting for the slowest wave of the workgroup)
+//   SETUP   after release: fragment registers, next op's record / fragment DMA, gradient-region flush
+//   BACK    adjoint BACK op bodies (LDS reads, MFMAs, writes)      GRADL1  cross-matrix-only (layer-1) op bodies
+//   APPLY   forward group-op bodies                                OTHER   OBS / READOUT op bodies
+//   EPI     gradient epilogue (fixed-point packing, u64 LDS atomics)
+//   TAIL    after the op loop: last barrier, region reduction, tile store
+// Slots NPH - 2 / NPH - 1 hold the op count and the wave's total cycles.
+enum { PH_PRO = 0, PH_LOAD, PH_BAR, PH_SETUP, PH_BACK, PH_GRADL1, PH_APPLY, PH_OTHER, PH_EPI, PH_TAIL, NPH = 16 };
+constexpr int STAMP_WG = HEA_STAMP_ROWS / 16;   // workgroups stamped per pass (a.dbg: STAMP_WG x waves x NPH u64)
+struct Stamps {
+  unsigned long long acc[PH_TAIL + 1];
+  unsigned long long t0, last;
+  int nops;
+  __device__ __forceinline__ static unsigned long long now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    __asm__ volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+  }
+  __device__ __forceinline__ void init() {
+    if constexpr (QFX_HEA_STAMPS) {
+#pragma unroll
+      for (int i = 0; i <= PH_TAIL; ++i) acc[i] = 0;
+      nops = 0;
+      t0 = last = now();
+    }
+  }
+  __device__ __forceinline__ void mark(int ph) {
+    if constexpr (QFX_HEA_STAMPS) {
+      const unsigned long long t = now();
+      acc[ph] += t - last;
+      last = t;
+    }
+  }
+  // lane 0 of every wave of the first STAMP_WG workgroups writes its row
+  __device__ __forceinline__ void write(long long* dbg, int nw, int wave, int lane) {
+    if constexpr (QFX_HEA_STAMPS) {
+      if (!dbg || blockIdx.x >= (unsigned)STAMP_WG || lane != 0) return;
+      long long* row = dbg + ((size_t)blockIdx.x * nw + wave) * NPH;
+#pragma unroll
+      for (int i = 0; i <= PH_TAIL; ++i) row[i] = (long long)acc[i];
+      row[NPH - 2] = nops;
+      row[NPH - 1] = (long long)(last - t0);
+    }
+  }
+};
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
@@ -225,18 +260,12 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
   }
 }
 
-// Adjoint LDS image, two layouts (template PL; QFEDX_HEA_PLANES selects):
-//   PL = false, interleaved: word 2w = psi, 2w + 1 = lambda of swizzled amplitude w.  One ds_read_b64 /
-//     ds_write_b64 moves an amplitude's (psi, lambda) pair: half the LDS instructions of two b32 accesses (the
-//     LDS issue rate, not bandwidth, bounds this kernel: PMC WAIT_INST_LDS), at a v_mov per dword splitting the
-//     pairs into MFMA operands.
-//   PL = true, planes: psi at word w, lambda at word lam_word<TB>() + w = 2^TB + 4 + w.  psi and lambda of one
-//     amplitude share one address VGPR (constant instruction offset) and land where the MFMA operands want them;
-//     the 4-word skew keeps the compiler from fusing the pair into a ds_read2st64_b32 (split again by v_movs).
-// Without a lambda input the lambda words are zeroed (the observable op writes them).
-template <int TB>
-__host__ __device__ constexpr uint32_t lam_word() { return (1u << TB) + 4u; }
-template <int NT, int TB, bool PL>
+// Adjoint LDS image, interleaved: word 2w = psi, 2w + 1 = lambda of swizzled amplitude w.  One ds_read_b64 /
+// ds_write_b64 moves an amplitude's (psi, lambda) pair: half the LDS instructions of two b32 accesses (the LDS
+// issue rate, not bandwidth, bounds this kernel: PMC WAIT_INST_LDS), at a v_mov per dword splitting the pairs into
+// MFMA operands.  (Separate psi / lambda planes halve the bank conflicts but double the LDS instructions: measured
+// slower, round 3.)  Without a lambda input the lambda words are zeroed (the observable op writes them).
+template <int NT, int TB>
 __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* psrc, const uint32_t* lsrc,
                                              uint32_t* tile, int tid, int T, uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
@@ -256,40 +285,31 @@ __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* 
       const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
       const uint32_t w0 = (q ^ h) & ~3u;
       const uint4 pv = quad_perm(v[i], h & 3u), lv = quad_perm(l[i], h & 3u);
-      if constexpr (PL) {
-        *(uint4*)&tile[w0] = pv;
-        *(uint4*)&tile[lam_word<TB>() + w0] = lv;
-      } else {
-        *(uint4*)&tile[2 * w0] = make_uint4(pv.x, lv.x, pv.y, lv.y);
-        *(uint4*)&tile[2 * w0 + 4] = make_uint4(pv.z, lv.z, pv.w, lv.w);
-      }
+      *(uint4*)&tile[2 * w0] = make_uint4(pv.x, lv.x, pv.y, lv.y);
+      *(uint4*)&tile[2 * w0 + 4] = make_uint4(pv.z, lv.z, pv.w, lv.w);
     }
   }
 }
 
-template <int NT, int TB, bool PL>
+template <int NT, int TB>
 __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, const uint32_t* tile, int tid, int T,
                                              uint32_t h_q, uint32_t fixed) {
-  if constexpr (PL) {
-    store_tile<NT, TB>(a, dst, tile + lam_word<TB>(), tid, T, h_q, fixed);
-  } else {
-    constexpr int MQ = (1 << TB) / (4 * NT);
-    uint4 v[MQ];
+  constexpr int MQ = (1 << TB) / (4 * NT);
+  uint4 v[MQ];
 #pragma unroll
-    for (int i = 0; i < MQ; ++i) {
-      const uint32_t q = 4u * (tid + NT * i);
-      if (q < (uint32_t)T) {
-        const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
-        const uint32_t w0 = 2u * ((q ^ h) & ~3u);
-        const uint4 a0 = *(const uint4*)&tile[w0], a1 = *(const uint4*)&tile[w0 + 4];
-        v[i] = quad_perm(make_uint4(a0.y, a0.w, a1.y, a1.w), h & 3u);
-      }
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) {
+      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
+      const uint32_t w0 = 2u * ((q ^ h) & ~3u);
+      const uint4 a0 = *(const uint4*)&tile[w0], a1 = *(const uint4*)&tile[w0 + 4];
+      v[i] = quad_perm(make_uint4(a0.y, a0.w, a1.y, a1.w), h & 3u);
     }
+  }
 #pragma unroll
-    for (int i = 0; i < MQ; ++i) {
-      const uint32_t q = 4u * (tid + NT * i);
-      if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
-    }
+  for (int i = 0; i < MQ; ++i) {
+    const uint32_t q = 4u * (tid + NT * i);
+    if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
   }
 }
 
@@ -360,39 +380,32 @@ __device__ __forceinline__ uint32_t mul_i(uint32_t v) {
 #endif
 }
 
-// Y = U X on the op's column blocks for NX targets (tile byte bases tb[x]) sharing the addressing.  Lane
-// (g4, cl) owns column cl of a 16-column block: it reads amplitudes m = 4 g4 .. 4 g4 + 3 (B operand,
-// k = 2m + re/im) and writes the same amplitudes back (row 4 g4 + i of output tile 0 / 1 = re / im of m' = 4 g4 + i).
-// A wave's blocks are blk = wave + NW i (i < nbw <= MAXB, fully unrolled): (blk & 1) = (wave & 1), so the
-// block bases are BL[lane] ^ BH[blk >> 1] precomputed in registers.  Blocks go in pairs (independent MFMA
-// chains) and the next pair's operands are read before the current pair is written (disjoint blocks).
-//   IL = false: forward psi image, NX = 1.
-//   IL = true : interleaved adjoint image; NX = 2 applies U to psi and lambda (one b64 read / write per
-//               amplitude pair), NX = 1 to component SEL only (pairs read, single dwords written).
-//   CROSS (interleaved adjoint image only): also accumulate the op's gradient cross matrix N = sum psi lambda^H
-//               from the SAME registers (the group_cross reads saved): an MFMA against the constant identity
-//               fragments IRE / IIM (exact in fp16) transposes each block's psi and lambda so the column index
-//               lands in registers - lane cl then holds (re, im) of amplitude cl for columns 4 g4 .. 4 g4 + 3, packed
-//               as the K = 32 operand of one MFMA that sums over columns (accR: B = lambda, accI: B = i lambda).
-//               Accumulator layout as group_cross: lane (g4, cl) holds N[4 g4 + i][cl].
-template <int NX, int NW, bool IL, int SEL, int TB = TMAX, bool PL = false, bool CROSS = false>
+// Y = U X on the op's column blocks.  Lane (g4, cl) owns column cl of a 16-column block: it reads amplitudes
+// m = 4 g4 .. 4 g4 + 3 (B operand, k = 2m + re/im) and writes the same amplitudes back (row 4 g4 + i of output tile
+// 0 / 1 = re / im of m' = 4 g4 + i).  A wave's blocks are blk = wave + NW i (i < nbw <= MAXB, fully unrolled):
+// (blk & 1) = (wave & 1), so the block bases are BL[lane] ^ BH[blk >> 1] precomputed in registers.  Blocks go in
+// pairs (independent MFMA chains).
+//   ADJ = false: forward psi image; the next pair's operands are read before the current pair is written.
+//   ADJ = true : interleaved adjoint image, U applied to lambda only (a pass's last BACK op when psi is no longer
+//                needed), plus the op's gradient cross matrix N = sum psi lambda^H from the SAME registers: an MFMA
+//                against the constant identity fragments IRE / IIM (exact in fp16) transposes each block's psi and
+//                lambda so the column index lands in registers - lane cl then holds (re, im) of amplitude cl for
+//                columns 4 g4 .. 4 g4 + 3, packed as the K = 32 operand of one MFMA that sums over columns
+//                (acc[0]: B = lambda, acc[1]: B = i lambda).  Accumulator layout as group_cross: lane (g4, cl)
+//                holds N[4 g4 + i][cl].
+template <int NW, bool ADJ, int TB = TMAX>
 __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, const int* opw, uint32_t fo, int lane,
                                             int wave, int nbw, f4* acc = nullptr) {
   constexpr int MAXB = (1 << (TB - 8)) / NW;   // column blocks per wave per op (t = 14: 64 blocks)
-  constexpr bool PAIR = IL && !PL;             // interleaved adjoint image: (psi, lambda) word pairs
-  static_assert(!CROSS || PAIR, "the fused cross matrix reads the interleaved image");
-  constexpr int NL = CROSS ? 2 : NX;           // registers loaded per block: psi and lambda for the cross
-  constexpr int SH = PAIR ? 3 : 2;
-  constexpr uint32_t LP = 4u * lam_word<TB>();  // lambda plane (planes image), bytes
-  static_assert(IL || NX == 1, "the forward image holds psi only");
+  constexpr int NL = ADJ ? 2 : 1;              // registers loaded per block: psi and lambda for the cross
+  constexpr int SH = ADJ ? 3 : 2;
   const int g4 = lane >> 4, cl = lane & 15;
   uint32_t oin[4];
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) oin[jj] = ((uint32_t)opw[W_OFF + 4 * g4 + jj] ^ fo) << SH;
-  // CROSS: identity fragments (rows: re of amplitude n, then im), built here so they are not live across the
-  // kernel's op loop
+  // identity fragments (rows: re of amplitude n, then im), built here so they are not live across the op loop
   uint4 IRE = {}, IIM = {};
-  if constexpr (CROSS) {
+  if constexpr (ADJ) {
     uint32_t* re = (uint32_t*)&IRE;
     uint32_t* im = (uint32_t*)&IIM;
 #pragma unroll
@@ -405,30 +418,19 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
   uint32_t base[MAXB];
 #pragma unroll
   for (int i = 0; i < MAXB; ++i) base[i] = (bl ^ (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)]) << SH;
-  // plane x of the image: psi (0) or lambda (1); a forward image has psi only
   auto load = [&](uint32_t b, uint4* X) {
     const uint32_t a0 = b ^ oin[0], a1 = b ^ oin[1], a2 = b ^ oin[2], a3 = b ^ oin[3];
-    if constexpr (PAIR) {
+    if constexpr (ADJ) {
       const uint2 p0 = lds_ld2(tile, a0), p1 = lds_ld2(tile, a1), p2 = lds_ld2(tile, a2), p3 = lds_ld2(tile, a3);
-      if constexpr (NL == 2) {
-        X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
-        X[1] = make_uint4(p0.y, p1.y, p2.y, p3.y);
-      } else if constexpr (SEL == 0) {
-        X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
-      } else {
-        X[0] = make_uint4(p0.y, p1.y, p2.y, p3.y);
-      }
+      X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
+      X[1] = make_uint4(p0.y, p1.y, p2.y, p3.y);
     } else {
-#pragma unroll
-      for (int x = 0; x < NX; ++x) {
-        const uint32_t pl = (NX == 2 ? x : (IL ? SEL : 0)) ? LP : 0u;
-        X[x] = make_uint4(lds_ld(tile, a0 + pl), lds_ld(tile, a1 + pl), lds_ld(tile, a2 + pl), lds_ld(tile, a3 + pl));
-      }
+      X[0] = make_uint4(lds_ld(tile, a0), lds_ld(tile, a1), lds_ld(tile, a2), lds_ld(tile, a3));
     }
   };
   auto compute_store = [&](uint32_t b, const uint4* XL) {
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    if constexpr (CROSS) {
+    if constexpr (ADJ) {
       const f4 pr = mfma(XL[0], IRE, z), pi = mfma(XL[0], IIM, z), lr = mfma(XL[1], IRE, z), li = mfma(XL[1], IIM, z);
       const uint4 A = make_uint4(pack_h2(pr[0], pi[0]), pack_h2(pr[1], pi[1]), pack_h2(pr[2], pi[2]), pack_h2(pr[3], pi[3]));
       const uint4 Br = make_uint4(pack_h2(lr[0], li[0]), pack_h2(lr[1], li[1]), pack_h2(lr[2], li[2]), pack_h2(lr[3], li[3]));
@@ -440,38 +442,21 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
       acc[0] = mfma(A, Br, acc[0]);
       acc[1] = mfma(A, Bi, acc[1]);
     }
-    // the apply targets among the loaded registers: both, or component SEL (psi 0 / lambda 1)
-    const uint4* X = (CROSS && NX == 1) ? XL + SEL : XL;
-    f4 d0[NX], d1[NX];
-#pragma unroll
-    for (int x = 0; x < NX; ++x) {
-      d0[x] = mfma(F[0], X[x], z);
-      d1[x] = mfma(F[1], X[x], z);
-      if (QFX_HEA_GATE_LO) {
-        d0[x] = mfma(F[2], X[x], d0[x]);
-        d1[x] = mfma(F[3], X[x], d1[x]);
-      }
+    const uint4 X = XL[NL - 1];                   // the apply target: psi (forward) or lambda (adjoint)
+    f4 d0 = mfma(F[0], X, z), d1 = mfma(F[1], X, z);
+    if (QFX_HEA_GATE_LO) {
+      d0 = mfma(F[2], X, d0);
+      d1 = mfma(F[3], X, d1);
     }
-    // output amplitude 4 g4 + i = (tile 0, tile 1) register i, written where it was read
-    if constexpr (PAIR && NX == 2) {
+    // output amplitude 4 g4 + i = (tile 0, tile 1) register i, written where it was read (adjoint: the lambda word)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        lds_st2(tile, b ^ oin[i], make_uint2(pack_h2(d0[0][i], d1[0][i]), pack_h2(d0[1][i], d1[1][i])));
-    } else {
-#pragma unroll
-      for (int x = 0; x < NX; ++x) {
-        const uint32_t pl = PAIR ? 4u * SEL : ((NX == 2 ? x : (IL ? SEL : 0)) ? LP : 0u);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          lds_st(tile, ((b ^ oin[i]) ^ (PAIR ? pl : 0u)) + (PAIR ? 0u : pl), pack_h2(d0[x][i], d1[x][i]));
-      }
-    }
+    for (int i = 0; i < 4; ++i) lds_st(tile, (b ^ oin[i]) ^ (ADJ ? 4u : 0u), pack_h2(d0[i], d1[i]));
   };
   if (nbw <= 0) return;
   uint4 B0[NL], B1[NL];
   load(base[0], B0);
   if (nbw > 1) load(base[1], B1);
-  constexpr bool PREFETCH = !CROSS;             // the fused cross needs the registers of the prefetched pair
+  constexpr bool PREFETCH = !ADJ;               // the fused cross needs the registers of the prefetched pair
 #pragma unroll
   for (int p = 0; p < MAXB; p += 2) {
     if (p >= nbw) break;
@@ -498,33 +483,25 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
 // Gradient cross matrix N[b][a] += sum_col psi[b][col] conj(lam[a][col]) over the op's column blocks:
 // K = 16 columns x (re, im), lane (g4, cl) reads amplitude m = cl of columns 4 g4 .. 4 g4 + 3; accR / accI
 // end up holding N[4 g4 + i][cl] (real / imaginary).
-template <int NW, int TB = TMAX, bool PL = false>
+template <int NW, int TB = TMAX>
 __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw, uint32_t fo, int lane, int wave,
                                             int nbw, f4& accR, f4& accI) {
   constexpr int MAXB = (1 << (TB - 8)) / NW;
   const int g4 = lane >> 4, cl = lane & 15;
-  constexpr uint32_t LP = 4u * lam_word<TB>();
-  constexpr int SH = PL ? 2 : 3;
   const uint32_t om = (uint32_t)opw[W_OFF + cl] ^ fo;
   uint32_t gb[4];
 #pragma unroll
-  for (int jj = 0; jj < 4; ++jj) gb[jj] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + jj] ^ om) << SH;
+  for (int jj = 0; jj < 4; ++jj) gb[jj] = ((uint32_t)opw[W_BL + (wave & 1) * 16 + 4 * g4 + jj] ^ om) << 3;
 #pragma unroll
   for (int i = 0; i < MAXB; ++i) {
     if (i >= nbw) break;
-    const uint32_t bh = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << SH;
+    const uint32_t bh = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << 3;
     uint32_t pv[4], lv[4];
 #pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {            // psi and lambda of one amplitude: one b64 pair or two planes
-      const uint32_t ad = gb[jj] ^ bh;
-      if constexpr (PL) {
-        pv[jj] = lds_ld(tile, ad);
-        lv[jj] = lds_ld(tile, ad + LP);
-      } else {
-        const uint2 v = lds_ld2(tile, ad);
-        pv[jj] = v.x;
-        lv[jj] = v.y;
-      }
+    for (int jj = 0; jj < 4; ++jj) {            // psi and lambda of one amplitude: one b64 pair
+      const uint2 v = lds_ld2(tile, gb[jj] ^ bh);
+      pv[jj] = v.x;
+      lv[jj] = v.y;
     }
     const uint4 A = make_uint4(pv[0], pv[1], pv[2], pv[3]);
     const uint4 Br = make_uint4(lv[0], lv[1], lv[2], lv[3]);
@@ -546,12 +523,11 @@ __device__ __forceinline__ void group_cross(const uint32_t* tile, const int* opw
 // hea_grad_reduce applies the input-side generators (X, and RX^H Z RX = cos(theta) Z + sin(theta) Y).  The
 // results go back amplitude-major: lane (g4, cl) writes amplitude cl of columns 4 g4 .. 4 g4 + 3, one 16-lane
 // b64 store group = 16 amplitudes of one column (the planner keeps their pair banks distinct).
-template <int NW, int TB, bool PL>
+template <int NW, int TB>
 __device__ __forceinline__ void group_back_t(uint32_t* tile, const uint4* F, const int* opw, uint32_t fo, int lane,
                                              int wave, int nbw, f4* acc) {
   constexpr int MAXB = (1 << (TB - 8)) / NW;
-  constexpr int SH = PL ? 2 : 3;
-  constexpr uint32_t LP = 4u * lam_word<TB>();
+  constexpr int SH = 3;
   const int g4 = lane >> 4, cl = lane & 15;
   // load address of block i, amplitude 4 g4 + j: lo[j] ^ bh[i]; store address of column 4 g4 + r: ost[r] ^ bh[i]
   uint32_t lo[4], ost[4], bh[MAXB];
@@ -565,16 +541,10 @@ __device__ __forceinline__ void group_back_t(uint32_t* tile, const uint4* F, con
   for (int i = 0; i < MAXB; ++i) bh[i] = (uint32_t)opw[W_BH + ((wave + NW * i) >> 1)] << SH;
   auto load = [&](int i, uint4* X) {
     const uint32_t b = bh[i];
-    if constexpr (PL) {
-      X[0] = make_uint4(lds_ld(tile, b ^ lo[0]), lds_ld(tile, b ^ lo[1]), lds_ld(tile, b ^ lo[2]), lds_ld(tile, b ^ lo[3]));
-      X[1] = make_uint4(lds_ld(tile, (b ^ lo[0]) + LP), lds_ld(tile, (b ^ lo[1]) + LP), lds_ld(tile, (b ^ lo[2]) + LP),
-                        lds_ld(tile, (b ^ lo[3]) + LP));
-    } else {
-      const uint2 p0 = lds_ld2(tile, b ^ lo[0]), p1 = lds_ld2(tile, b ^ lo[1]), p2 = lds_ld2(tile, b ^ lo[2]),
-                  p3 = lds_ld2(tile, b ^ lo[3]);
-      X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
-      X[1] = make_uint4(p0.y, p1.y, p2.y, p3.y);
-    }
+    const uint2 p0 = lds_ld2(tile, b ^ lo[0]), p1 = lds_ld2(tile, b ^ lo[1]), p2 = lds_ld2(tile, b ^ lo[2]),
+                p3 = lds_ld2(tile, b ^ lo[3]);
+    X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
+    X[1] = make_uint4(p0.y, p1.y, p2.y, p3.y);
   };
   auto compute_store = [&](int i, const uint4* X) {
     const f4 z = {0.f, 0.f, 0.f, 0.f};
@@ -604,18 +574,12 @@ __device__ __forceinline__ void group_back_t(uint32_t* tile, const uint4* F, con
     const uint32_t* Lw = (const uint32_t*)&Lr;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint32_t ad = ost[r] ^ bb;
-      if constexpr (PL) {
-        lds_st(tile, ad, Pw[r]);
-        lds_st(tile, ad + LP, Lw[r]);
-      } else {
-        // psi and lambda words from two unpaired registers in one ds_write2_b32 (a b64 store needs them
-        // adjacent, and the cross-matrix operands need each of psi and lambda in four adjacent registers: the
-        // compiler merges two dword stores into a b64 with two v_movs).  Issued as asm, the store is unknown
-        // to the wait-count pass; LDS operations complete in order, so its waits only become conservative.
-        const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)((char*)tile + ad);
-        __asm__ volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(Pw[r]), "v"(Lw[r]) : "memory");
-      }
+      // psi and lambda words from two unpaired registers in one ds_write2_b32 (a b64 store needs them adjacent,
+      // and the cross-matrix operands need each of psi and lambda in four adjacent registers: the compiler merges
+      // two dword stores into a b64 with two v_movs).  Issued as asm, the store is unknown to the wait-count pass;
+      // LDS operations complete in order, so its waits only become conservative.
+      const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)((char*)tile + (ost[r] ^ bb));
+      __asm__ volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(Pw[r]), "v"(Lw[r]) : "memory");
     }
   };
   // one block at a time with the next block's reads in flight (four independent MFMA chains per block; a pair of
@@ -759,91 +723,8 @@ __device__ __forceinline__ void readout_op(const uint32_t* psi_t, const PassArgs
   }
 }
 
-// <Z_c> partial sums of a PAIRED forward tile (two samples of one client interleaved: word 2w = sample A,
-// 2w + 1 = sample B of swizzled amplitude w; one b64 read per amplitude pair), written for both samples.
-template <int NC, int NT, int TB>
-__device__ __forceinline__ void readout_pair_op(const uint32_t* tile, const PassArgs& a, const int* opw, int tid,
-                                                int lane, int wave, int T, uint32_t fixed, float* red, size_t pidxA,
-                                                size_t pidxB) {
-  constexpr int QI = (1 << TB) / NT, NW = NT / 64;
-  constexpr int CH = QI < RCH ? QI : RCH;
-  const int iters = T >= NT ? T / NT : 1;
-  const ClassSigns<NC, CH> cs = class_signs<NC, NT, CH, TB>(opw, tid, fixed, iters);
-  float acc[2][NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) acc[0][c] = acc[1][c] = 0.f;
-#pragma unroll 1
-  for (int i0 = 0; i0 < QI; i0 += CH) {
-    if (i0 >= iters) break;
-    uint2 v[CH];
-#pragma unroll
-    for (int j = 0; j < CH; ++j) v[j] = *(const uint2*)&tile[2 * ((tid + NT * (i0 + j)) & (T - 1))];
-    float sum[2][NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) sum[0][c] = sum[1][c] = 0.f;
-#pragma unroll
-    for (int j = 0; j < CH; ++j) {
-      const float2 fa = unpack_h2(v[j].x), fb = unpack_h2(v[j].y);
-      const float pa = fa.x * fa.x + fa.y * fa.y, pb = fb.x * fb.x + fb.y * fb.y;
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        sum[0][c] += cs.mul(pa, j, c);
-        sum[1][c] += cs.mul(pb, j, c);
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const bool f = cs.flip(c, i0 / CH);
-      acc[0][c] += f ? -sum[0][c] : sum[0][c];
-      acc[1][c] += f ? -sum[1][c] : sum[1][c];
-    }
-  }
-#pragma unroll
-  for (int x = 0; x < 2; ++x)
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      float v = tid < T ? acc[x][c] : 0.f;
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      if (lane == 0) red[(x * NW + wave) * CMAX + c] = v;
-    }
-  lds_barrier();
-  if (tid < 2 * a.C) {
-    const int x = tid / a.C, c = tid - x * a.C;
-    float v = 0.f;
-    for (int w = 0; w < NW; ++w) v += red[(x * NW + w) * CMAX + c];
-    a.part[(x ? pidxB : pidxA) + c] = v / (a.scale * a.scale);
-  }
-}
-
-// Paired image store: sample A (even words) and sample B (odd words) of every amplitude to their states.
-template <int NT, int TB>
-__device__ __forceinline__ void store_pair_il(const PassArgs& a, uint32_t* dstA, uint32_t* dstB, const uint32_t* tile,
-                                              int tid, int T, uint32_t h_q, uint32_t fixed) {
-  constexpr int MQ = (1 << TB) / (4 * NT);
-  uint4 va[MQ], vb[MQ];
-#pragma unroll
-  for (int i = 0; i < MQ; ++i) {
-    const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) {
-      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
-      const uint32_t w0 = 2u * ((q ^ h) & ~3u);
-      const uint4 a0 = *(const uint4*)&tile[w0], a1 = *(const uint4*)&tile[w0 + 4];
-      va[i] = quad_perm(make_uint4(a0.x, a0.z, a1.x, a1.z), h & 3u);
-      vb[i] = quad_perm(make_uint4(a0.y, a0.w, a1.y, a1.w), h & 3u);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < MQ; ++i) {
-    const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) {
-      *(uint4*)&dstA[mem_of(q, a, fixed)] = va[i];
-      *(uint4*)&dstB[mem_of(q, a, fixed)] = vb[i];
-    }
-  }
-}
-
-// Adjoint seed lambda = sum_c r_c Z_c psi on the adjoint image (psi plane word w, lambda plane word 2^TB + w).
-template <int NC, int NT, int TB = TMAX, bool PL = false>
+// Adjoint seed lambda = sum_c r_c Z_c psi on the interleaved adjoint image (psi word 2w, lambda word 2w + 1).
+template <int NC, int NT, int TB = TMAX>
 __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, int T, uint32_t fixed,
                                        const float* rsc_s) {
   constexpr int QI = (1 << TB) / NT;
@@ -858,7 +739,7 @@ __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, 
     if (i0 >= iters) break;
     uint32_t v[CH];
 #pragma unroll
-    for (int j = 0; j < CH; ++j) v[j] = tile[(PL ? 1 : 2) * ((tid + NT * (i0 + j)) & (T - 1))];   // in bounds
+    for (int j = 0; j < CH; ++j) v[j] = tile[2 * ((tid + NT * (i0 + j)) & (T - 1))];   // in bounds
     float rr[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) rr[c] = cs.flip(c, i0 / CH) ? -r[c] : r[c];
@@ -869,7 +750,7 @@ __device__ __forceinline__ void obs_op(uint32_t* tile, const int* opw, int tid, 
       for (int c = 0; c < NC; ++c) fsum += cs.mul(rr[c], j, c);
       const float2 f = unpack_h2(v[j]);
       const int w = tid + NT * (i0 + j);
-      if (i0 + j < iters && w < T) tile[PL ? lam_word<TB>() + w : 2 * w + 1] = pack_h2(fsum * f.x, fsum * f.y);
+      if (i0 + j < iters && w < T) tile[2 * w + 1] = pack_h2(fsum * f.x, fsum * f.y);
     }
   }
 }
@@ -896,13 +777,6 @@ __device__ __forceinline__ void op_barrier(int wave) {
   __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Phase timestamps of workgroups < 8 (scripts/hea_ablate.py): one per phase, read back as cycle deltas.
-#define HEA_MARK()                                                                                   \
-  do {                                                                                               \
-    if (dbg && tid == 0 && ndbg < 64) dbg[ndbg] = (long long)__builtin_readcyclecounter();           \
-    ++ndbg;                                                                                          \
-  } while (0)
-
 // Memory bits of tile tile_id outside the tile.
 __device__ __forceinline__ uint32_t tile_fixed(const PassArgs& a, int tile_id) {
   const int w1 = a.lo - a.c;
@@ -919,189 +793,6 @@ __device__ __forceinline__ uint32_t op_fo_global(const int* ow, uint32_t fixed) 
   for (int j = 0; j < 4; ++j)
     if (j < nreal) fpb |= par(fixed & (uint32_t)ow[W_RFULL + j]) << j;
   return (uint32_t)ow[W_OFF + fpb];
-}
-
-// ------------------------------------------------------------------------------------------- layer-1 gradients
-// OP_L1PROD: the 2 x 2 cross matrices n_q[y][x] = sum_rest psi[y, rest] conj(lambda[x, rest]) of EVERY layer-1 qubit
-// of the tile in one op, at the end of the last adjoint pass (every later gate un-applied, so psi is the layer-1
-// product state (x) w_q, known in closed form).  Then n_q[y][x] = w_q[y] conj(mu_q[x]) with
-//     mu_q[x] = sum_{z: z_q = x} lambda[z] prod_{p != q} conj(w_p[z_p])
-// a leave-one-out contraction of lambda with the conjugate factors: lambda is read once, psi not at all (it need not
-// be un-applied by the pass's last group op), no MFMA and no atomics - one op instead of one GRAD_L1 op (tile read,
-// cross-matrix MFMAs, 80 fixed-point atomics, region flush) per layer-1 group.
-// Thread u < U = T / 16 owns amplitudes tau = u + U j, j < 16: tile bits [0, t - 4) are the thread bits ("lo"), the
-// top 4 the register bits ("hi").  With f_i = conj(w of tile bit i), Hb[j] = outer * prod_hi f and A_u = prod_lo f:
-//   c_u = sum_j lambda[u, j] Hb[j]     -> lo bit i:  mu[x] = sum_{u: u_i = x} c_u prod_{lo i' != i} f_i'[u_i']
-//   r_j = sum_u lambda[u, j] A_u       -> hi bit k:  mu[x] = outer sum_{j: j_k = x} r_j prod_{hi k' != k} f_k'[j_k']
-// The per-thread terms are summed in fixed order through the (dead) tile image, so the result is deterministic;
-// slab entries are the exact 2^-32 fixed point of the true cross matrix, as reduce_region writes them.
-// Record: W_NREAL = number of layer-1 qubits; word W_OFF + e = tile bit | group << 8 | index in group << 16;
-// group g's slab row is W_GIDX + g.  sc: >= 96 float2 of scratch LDS.
-template <int NT, int TB, bool PL>
-__device__ __forceinline__ void l1prod_op(uint32_t* tile, const PassArgs& a, const int* opw, int tid, int s, int k,
-                                       uint32_t fixed, float rho, long long* slab, float2* sc, int* emap,
-                                       float2& outer_s) {
-  const int t = a.t, U = 1 << (t - 4), nlo = t - 4;
-  float2* fw = sc;            // [32][2] true layer-1 factors w_q (memory bit q)
-  float2* hb = sc + 64;       // [16] outer * prod_hi conj(w)
-  float2* rj = sc + 80;       // [16] r_j
-  // emap [TMAX]: tile bit -> record entry, or -1; outer_s: product of the out-of-tile conj factors
-  // ---- factors (wave 0: lane q computes qubit q's pair; the out-of-tile product over the wave)
-  if (tid < 64) {
-    float2 w[2] = {make_float2(1.f, 0.f), make_float2(1.f, 0.f)};
-    const float* prm = a.params + (size_t)k * a.p_stride;
-    if (tid < a.n) {
-      l1_factor(a.xang[(size_t)s * a.x_stride + tid], prm[2 * tid], prm[2 * tid + 1], a.feature, w);
-      fw[2 * tid] = w[0];
-      fw[2 * tid + 1] = w[1];
-    }
-    const bool outq = tid < a.n && !(tid < a.c || (tid >= a.lo && tid < a.hi));
-    const float2 w0 = w[0], w1 = w[1];
-    float2 f = outq ? (((fixed >> (tid & 31)) & 1) ? w1 : w0) : make_float2(1.f, 0.f);
-    f.y = -f.y;                                          // conj
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) f = cmul(f, make_float2(__shfl_xor(f.x, off, 64), __shfl_xor(f.y, off, 64)));
-    if (tid == 0) outer_s = f;
-    if (tid < TMAX) emap[tid] = -1;
-  }
-  lds_barrier();
-  if (tid < opw[W_NREAL]) emap[opw[W_OFF + tid] & 255] = tid;
-  auto mbit = [&](int i) { return i < a.c ? i : a.lo + i - a.c; };   // memory bit (= layer-1 qubit) of tile bit i
-  auto fconj = [&](int i, int b) { const float2 v = fw[2 * mbit(i) + b]; return make_float2(v.x, -v.y); };
-  if (tid < 16) {
-    float2 v = outer_s;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) v = cmul(v, fconj(nlo + kk, (tid >> kk) & 1));
-    hb[tid] = v;
-  }
-  lds_barrier();
-  // ---- r's terms lambda[u, j] A_u: every lambda word is read by exactly one thread; all of them are read (and c_u
-  // accumulated) before a barrier, then thread u writes its 16 terms over its own (psi, lambda) slots
-  float2 c = make_float2(0.f, 0.f);
-  const bool act = tid < U;
-  const uint32_t h0 = swz(a, (uint32_t)tid >> 5);
-  // tau = u + U j: u < U and U j share no bits, so h(tau >> 5) = h(u >> 5) ^ h((U j) >> 5) (h is linear)
-  auto slot = [&](int j) { return ((uint32_t)tid + (uint32_t)U * j) ^ (h0 ^ swz(a, ((uint32_t)U * (uint32_t)j) >> 5)); };
-  float2 A = make_float2(1.f, 0.f);
-  uint32_t lw[16];
-  if (act) {
-    for (int i = 0; i < nlo; ++i) A = cmul(A, fconj(i, (tid >> i) & 1));
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t w = slot(j);
-      lw[j] = PL ? tile[lam_word<TB>() + w] : lds_ld2(tile, 8u * w).y;
-    }
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float2 lam = unpack_h2(lw[j]), h = hb[j];
-      c = make_float2(c.x + lam.x * h.x - lam.y * h.y, c.y + lam.x * h.y + lam.y * h.x);
-    }
-  }
-  lds_barrier();
-  if (act) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t w = slot(j);
-      const float2 pv = cmul(unpack_h2(lw[j]), A);
-      if constexpr (PL) {
-        tile[w] = __float_as_uint(pv.x);
-        tile[lam_word<TB>() + w] = __float_as_uint(pv.y);
-      } else {
-        lds_st2(tile, 8u * w, make_uint2(__float_as_uint(pv.x), __float_as_uint(pv.y)));
-      }
-    }
-  }
-  lds_barrier();
-  auto pget = [&](uint32_t u, int j) {              // thread u's r term of register bit pattern j
-    const uint32_t hu = swz(a, u >> 5) ^ swz(a, ((uint32_t)U * (uint32_t)j) >> 5);
-    const uint32_t w = (u + (uint32_t)U * j) ^ hu;
-    if constexpr (PL)
-      return make_float2(__uint_as_float(tile[w]), __uint_as_float(tile[lam_word<TB>() + w]));
-    const uint2 v = lds_ld2(tile, 8u * w);
-    return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
-  };
-  // r_j: thread (j, l < 32) sums u = l, l + 32, ... then a fixed xor tree over the 32 lanes
-  {
-    const int j = tid >> 5, l = tid & 31;
-    float2 v = make_float2(0.f, 0.f);
-    if (j < 16)
-      for (int m = l; m < U; m += 32) {
-        const float2 e = pget((uint32_t)m, j);
-        v = make_float2(v.x + e.x, v.y + e.y);
-      }
-#pragma unroll
-    for (int off = 1; off < 32; off <<= 1) {
-      const float ox = __shfl_xor(v.x, off, 64), oy = __shfl_xor(v.y, off, 64);
-      v = (l & off) ? make_float2(ox + v.x, oy + v.y) : make_float2(v.x + ox, v.y + oy);
-    }
-    if (j < 16 && l == 0) rj[j] = v;
-  }
-  lds_barrier();                                     // r terms read: the image is free for the lo terms
-  float2* scr = (float2*)tile;                       // [t - 4][U] lo terms T_i
-  if (act) {
-    // T_i = c_u prod_{lo i' != i} f_i' (prefix x suffix products)
-    float2 pre[TMAX - 3];
-    pre[0] = make_float2(1.f, 0.f);
-#pragma unroll
-    for (int i = 0; i < TMAX - 4; ++i) pre[i + 1] = i < nlo ? cmul(pre[i], fconj(i, (tid >> i) & 1)) : pre[i];
-    float2 suf = make_float2(1.f, 0.f);
-#pragma unroll
-    for (int i = TMAX - 5; i >= 0; --i) {
-      if (i < nlo) {
-        scr[i * U + tid] = cmul(c, cmul(pre[i], suf));
-        suf = cmul(fconj(i, (tid >> i) & 1), suf);
-      }
-    }
-  }
-  lds_barrier();
-  const double nsc = (double)rho / (double)a.scale * FIX;   // lambda image -> true units, 2^-32 fixed point
-  // lo bins: thread (i, x, l < 16) sums T[i][u] over u with u_i = x (entries m = l, l + 16, ...), xor tree over 16
-  float2 mu_lo = make_float2(0.f, 0.f);
-  const int bi = tid >> 5, bx = (tid >> 4) & 1, bl = tid & 15;
-  if (bi < nlo) {
-    const uint32_t lowm = (1u << bi) - 1u;
-    for (int m = bl; m < (U >> 1); m += 16) {
-      const uint32_t u = (((uint32_t)m & ~lowm) << 1) | ((uint32_t)bx << bi) | ((uint32_t)m & lowm);
-      const float2 tv = scr[bi * U + u];
-      mu_lo = make_float2(mu_lo.x + tv.x, mu_lo.y + tv.y);
-    }
-  }
-#pragma unroll
-  for (int off = 1; off < 16; off <<= 1) {
-    const float ox = __shfl_xor(mu_lo.x, off, 64), oy = __shfl_xor(mu_lo.y, off, 64);
-    mu_lo = (bl & off) ? make_float2(ox + mu_lo.x, oy + mu_lo.y) : make_float2(mu_lo.x + ox, mu_lo.y + oy);
-  }
-  auto write_n = [&](int tb, int x, float2 mu) {          // n[y][x] = w[y] conj(mu), y = 0, 1
-    const int e = emap[tb];
-    if (e < 0) return;
-    const int rec = opw[W_OFF + e], g = (rec >> 8) & 255, jq = (rec >> 16) & 255;
-    long long* row = slab + (size_t)(opw[W_GIDX] + g) * 32 + 8 * jq;
-#pragma unroll
-    for (int y = 0; y < 2; ++y) {
-      const float2 w = fw[2 * mbit(tb) + y];
-      const double re = (double)w.x * mu.x + (double)w.y * mu.y, im = (double)w.y * mu.x - (double)w.x * mu.y;
-      row[4 * y + 2 * x] = __double2ll_rn(re * nsc);
-      row[4 * y + 2 * x + 1] = __double2ll_rn(im * nsc);
-    }
-  };
-  if (bi < nlo && bl == 0) write_n(bi, bx, mu_lo);
-  // hi bits: thread (k < 4, x, jj < 8): term r_j prod_{k' != k} f(j_k'), j = jj with bit x inserted at k; tree over 8
-  if (tid < 64) {
-    const int kk = tid >> 4, x = (tid >> 3) & 1, jj = tid & 7;
-    const int lowm = (1 << kk) - 1;
-    const int j = ((jj & ~lowm) << 1) | (x << kk) | (jj & lowm);
-    float2 v = rj[j];
-#pragma unroll
-    for (int k2 = 0; k2 < 4; ++k2)
-      if (k2 != kk) v = cmul(v, fconj(nlo + k2, (j >> k2) & 1));
-#pragma unroll
-    for (int off = 1; off < 8; off <<= 1) {
-      const float ox = __shfl_xor(v.x, off, 64), oy = __shfl_xor(v.y, off, 64);
-      v = (jj & off) ? make_float2(ox + v.x, oy + v.y) : make_float2(v.x + ox, v.y + oy);
-    }
-    const float2 o = outer_s;
-    if (jj == 0) write_n(nlo + kk, x, cmul(v, o));
-  }
 }
 
 // ------------------------------------------------------------------------------------------- forward pass
@@ -1132,9 +823,8 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   const size_t N = (size_t)1 << a.n;
   const uint32_t fixed = tile_fixed(a, tile_id);
   const float* prm = a.params + (size_t)k * a.p_stride;
-  long long* dbg = (QFX_HEA_MARKS && a.dbg && blockIdx.x < 8) ? a.dbg + blockIdx.x * 64 : nullptr;
-  int ndbg = 0;
-  HEA_MARK();
+  Stamps st;
+  st.init();
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
 
   // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op); op 0's
@@ -1146,6 +836,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
   if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
+  st.mark(PH_PRO);
 
   // ---------------------------------------------------------------- initial psi tile
   if (a.gen) {
@@ -1169,7 +860,6 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
       if (tid == 0) outer_s = make_float2(a.scale * f.x, a.scale * f.y);
     }
     lds_barrier();
-    HEA_MARK();
     const int ta = a.t >> 1, tb = a.t - ta;
     constexpr int JMAX = TMAX - (TMAX >> 1);
     const bool lowt = tid < (1 << ta), hight = tid >= 256 && tid < 256 + (1 << tb);
@@ -1191,7 +881,6 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
         tabB[i] = v;
     }
     lds_barrier();
-    HEA_MARK();
     const uint32_t am = (1u << ta) - 1u;
     // quad q = tid + NT i holds LDS words 4q .. 4q+3 = amplitudes tau_e = (4q + e) ^ h, h = h(q >> 3);
     // the swizzle only flips bits < 5 and ta >= 4, so the four words share one high-half factor.  Table reads
@@ -1225,16 +914,16 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   // ---------------------------------------------------------------- op list
   const int ncol = T >> 4, nblk = ncol >> 4;
   const int nbw = FULL ? (1 << (TMAX - 8)) / NW : (wave < nblk ? (nblk - wave + NW - 1) / NW : 0);   // (uniform)
+  st.mark(PH_LOAD);
   lds_barrier_dma();
-  HEA_MARK();
+  st.mark(PH_BAR);
   for (int o = 0; o < a.nops; ++o) {
     // op o's record and fragments were written during op o - 1; the other buffers were last read at the
     // start of op o - 1, which every wave has finished at this barrier, so op o + 1's go there right away
-    if (QFX_HEA_ABLATE && (a.ablate & 1) && o > 0)
-      lds_barrier_wave();
-    else
+    if (o > 0) {
       op_barrier(wave);
-    HEA_MARK();
+      st.mark(PH_BAR);
+    }
     const int* opw = opw2[o & 1];
     uint4 F[4];
     if (fidx_s[o] >= 0) {
@@ -1259,160 +948,21 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
       QFX_DCHECK(opw[W_NREAL] >= 1 && opw[W_NREAL] <= a.C);
     }
 #endif
+    st.mark(PH_SETUP);
     if (code == OP_APPLY) {
-      group_apply<1, NW, false, 0>(psi_t, F, opw, fo_s[o], lane, wave, nbw);
+      group_apply<NW, false>(psi_t, F, opw, fo_s[o], lane, wave, nbw);
+      st.mark(PH_APPLY);
     } else if (code == OP_READOUT) {
       const size_t pidx = ((size_t)s * a.n_tiles + tile_id) * a.C;
       readout_op<NCK, NT>(psi_t, a, opw, tid, lane, wave, T, fixed, red, pidx);
+      st.mark(PH_OTHER);
     }
+    if constexpr (QFX_HEA_STAMPS) ++st.nops;
   }
   lds_barrier();
-  HEA_MARK();
   if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
-  HEA_MARK();
-}
-
-// ------------------------------------------------------------------------------------------- paired forward
-// Two samples of one client per workgroup on 2^13-amplitude tiles of the adjoint's plan (same passes, groups and
-// slots), interleaved like the adjoint image: every group op moves (sample A, sample B) amplitude pairs with one
-// ds_read_b64 / ds_write_b64 and applies U to both (the same client unitary), so a tile costs half the LDS
-// instructions per amplitude of the single-sample 2^14 forward at the same 64 KB of LDS and amplitudes per
-// workgroup.  Samples s = 2 * pair and s + 1 (spc even: a pair never straddles two clients).
-template <int NCK>
-__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd2_kernel(PassArgs a) {
-  constexpr int NT = NT_FWD, NW = NT / 64, TB = 13;
-  __shared__ __attribute__((aligned(16))) uint32_t tile[2 << TB];   // (A, B) fp16 (re, im) pairs, swizzled
-  __shared__ int opw2[2][OPW];
-  __shared__ int fidx_s[MAXOPS];
-  __shared__ uint32_t fo_s[MAXOPS];
-  __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];
-  __shared__ float red[2 * NW * CMAX];
-  __shared__ float2 wv[2][32][2];
-  __shared__ float2 tabA[2][128];
-  __shared__ float2 tabB[2][128];
-  __shared__ float2 outer_s[2];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int sp = blockIdx.x / a.n_tiles, tile_id = blockIdx.x % a.n_tiles;
-  const int s = 2 * sp;                                 // sample A; sample B = s + 1 (same client)
-  const int k = s / a.spc;
-  const int s_in = a.in_rep > 1 ? (s / (a.in_rep * a.spc)) * a.spc + s % a.spc : s;
-  const int T = 1 << a.t;
-  const size_t N = (size_t)1 << a.n;
-  const uint32_t fixed = tile_fixed(a, tile_id);
-  const float* prm = a.params + (size_t)k * a.p_stride;
-  const uint32_t h_q = swz(a, (uint32_t)tid >> 3);
-
-  if (tid < a.nops) {
-    fidx_s[tid] = a.fidx[tid];
-    fo_s[tid] = op_fo_global(a.ops + (size_t)tid * OPW, fixed);
-  }
-  if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
-  int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
-  if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
-
-  if (a.gen) {
-    // layer-1 product states of both samples: wave x computes sample x's qubit factors and outer factor
-    if (wave < 2) {
-      const int x = wave;
-      float2 w[2] = {make_float2(1.f, 0.f), make_float2(1.f, 0.f)};
-      if (lane < a.n) {
-        l1_factor(a.xang[(size_t)(s_in + x) * a.x_stride + lane], prm[2 * lane], prm[2 * lane + 1], a.feature, w);
-        wv[x][lane][0] = w[0];
-        wv[x][lane][1] = w[1];
-      }
-      const bool outq = lane < a.n && !(lane < a.c || (lane >= a.lo && lane < a.hi));
-      const float2 w0 = w[0], w1 = w[1];
-      float2 f = outq ? (((fixed >> (lane & 31)) & 1) ? w1 : w0) : make_float2(1.f, 0.f);
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) f = cmul(f, make_float2(__shfl_xor(f.x, off, 64), __shfl_xor(f.y, off, 64)));
-      if (lane == 0) outer_s[x] = make_float2(a.scale * f.x, a.scale * f.y);
-    }
-    lds_barrier();
-    const int ta = a.t >> 1, tb = a.t - ta;
-    constexpr int JMAX = TB - (TB >> 1);
-    {
-      // threads [0, 256) build sample A's half tables, [256, 512) sample B's
-      const int x = tid >> 8, u = tid & 255;
-      const bool lowt = u < (1 << ta), hight = u >= 128 && u < 128 + (1 << tb);
-      if (lowt || hight) {
-        const int i = lowt ? u : u - 128, j0 = lowt ? 0 : ta, nj = lowt ? ta : tb;
-        float2 fac[JMAX];
-#pragma unroll
-        for (int j = 0; j < JMAX; ++j) {
-          const int tj = j0 + j, mb = tj < a.c ? tj : a.lo + tj - a.c;
-          fac[j] = wv[x][j < nj ? mb : 0][(i >> j) & 1];
-        }
-        float2 v = lowt ? make_float2(1.f, 0.f) : outer_s[x];
-#pragma unroll
-        for (int j = 0; j < JMAX; ++j)
-          if (j < nj) v = cmul(v, fac[j]);
-        if (lowt)
-          tabA[x][i] = v;
-        else
-          tabB[x][i] = v;
-      }
-    }
-    lds_barrier();
-    const uint32_t am = (1u << ta) - 1u;
-    constexpr int QI = (1 << TB) / (4 * NT);
-    uint4 oa[QI], ob[QI];
-#pragma unroll
-    for (int i = 0; i < QI; ++i) {
-      const uint32_t q = (uint32_t)(tid + NT * i);
-      const uint32_t qq = 4 * q < (uint32_t)T ? q : 0u;
-      const uint32_t h = h_q ^ swz(a, (uint32_t)(4 * NT / 32) * i);
-      const float2 va = tabB[0][((4 * qq) ^ h) >> ta], vbb = tabB[1][((4 * qq) ^ h) >> ta];
-      uint32_t* wa = (uint32_t*)&oa[i];
-      uint32_t* wb = (uint32_t*)&ob[i];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const uint32_t ix = ((4 * qq + e) ^ h) & am;
-        const float2 v0 = cmul(tabA[0][ix], va), v1 = cmul(tabA[1][ix], vbb);
-        wa[e] = pack_h2(v0.x, v0.y);
-        wb[e] = pack_h2(v1.x, v1.y);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < QI; ++i) {
-      const uint32_t q = (uint32_t)(tid + NT * i);
-      if (4 * q < (uint32_t)T) {
-        *(uint4*)&tile[8 * q] = make_uint4(oa[i].x, ob[i].x, oa[i].y, ob[i].y);
-        *(uint4*)&tile[8 * q + 4] = make_uint4(oa[i].z, ob[i].z, oa[i].w, ob[i].w);
-      }
-    }
-  } else {
-    load_tile_il<NT, TB, false>(a, a.psi_in + (size_t)s_in * N, a.psi_in + (size_t)(s_in + 1) * N, tile, tid, T,
-                                h_q, fixed);
-  }
-
-  constexpr int NBW = (1 << (TB - 8)) / NW;            // t == 13 (host-checked): 4 column blocks per wave
-  lds_barrier_dma();
-  for (int o = 0; o < a.nops; ++o) {
-    op_barrier(wave);
-    const int* opw = opw2[o & 1];
-    uint4 F[4];
-    if (fidx_s[o] >= 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) F[i] = frag_s[o & 1][64 * i + lane];
-    }
-    if (o + 1 < a.nops) {
-      if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
-      if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
-      dma_frags(a, k, fidx_s[o + 1], lane, wave, frag_s[(o + 1) & 1]);
-    }
-    const int code = opw[W_CODE];
-    QFX_DCHECK(code == OP_APPLY || code == OP_READOUT);
-    if (code == OP_APPLY) {
-      group_apply<2, NW, true, 0, TB, false>(tile, F, opw, fo_s[o], lane, wave, NBW);   // U on both samples
-    } else if (code == OP_READOUT) {
-      readout_pair_op<NCK, NT, TB>(tile, a, opw, tid, lane, wave, T, fixed, red,
-                                   ((size_t)s * a.n_tiles + tile_id) * a.C, ((size_t)(s + 1) * a.n_tiles + tile_id) * a.C);
-    }
-  }
-  lds_barrier();
-  if (a.store_psi) store_pair_il<NT, TB>(a, a.psi_out + (size_t)s * N, a.psi_out + (size_t)(s + 1) * N, tile, tid, T, h_q, fixed);
+  st.mark(PH_TAIL);
+  st.write(a.dbg, NW, wave, lane);
 }
 
 // ------------------------------------------------------------------------------------------- adjoint pass
@@ -1426,14 +976,14 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd2_kernel(PassArgs a) {
 // zeroes it, while the other waves go on with the op (its region is next used two gradient ops later, after
 // at least one more barrier).  Measured: spreading that flush over all waves delays every wave by its LDS
 // round trip and was slower (16q adjoint 0.67 -> 0.72 ms).
-// WV = waves per workgroup: 2^(TB - 10) gives 4 column blocks per wave per op (the round-2 layout); fewer waves
-// give each wave more blocks per op, amortising the per-op setup / epilogue over more MFMAs.
-template <int NCK, int TB, int WV, bool FULL, bool PL, bool FUSE>
-__global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(PassArgs a) {
-  constexpr int NT = 64 * WV, NW = WV;
+// 2^(TB - 10) waves give each wave 4 column blocks per op (a 4-wave 2^13 workgroup with 8 blocks per wave halves the
+// per-op setup per MFMA but halves the waves per SIMD: measured 18% slower, round 4).
+template <int NCK, int TB, bool FULL>
+__global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_adj_kernel(PassArgs a) {
+  constexpr int NT = 1 << (TB - 4), NW = NT / 64;
   static_assert(NW % 2 == 0 && (1 << (TB - 8)) % NW == 0, "column blocks per wave must be whole, block pairs aligned");
   // (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
-  __shared__ __attribute__((aligned(16))) uint32_t tile[PL ? lam_word<TB>() + (1 << TB) : (2 << TB)];
+  __shared__ __attribute__((aligned(16))) uint32_t tile[2 << TB];
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
   __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
   __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (op_fo_global)
@@ -1444,8 +994,6 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   __shared__ unsigned long long red64[NREG * RSTR];
   __shared__ int gmeta_s[NREG][2];                      // (slab index, nreal) of the region's gradient op
   __shared__ float rsc[CMAX + 2];
-  __shared__ int emap_s[TMAX];                          // OP_L1PROD: tile bit -> record entry
-  __shared__ float2 l1outer_s;                          // OP_L1PROD: out-of-tile conj factor product
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1454,25 +1002,11 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   const int T = 1 << a.t;
   const size_t N = (size_t)1 << a.n;
   const uint32_t fixed = tile_fixed(a, tile_id);
-  long long* dbg = (QFX_HEA_MARKS && a.dbg && blockIdx.x < 8) ? a.dbg + blockIdx.x * 64 : nullptr;
-  int ndbg = 0;
-  HEA_MARK();
+  Stamps st;
+  st.init();
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
   long long* slab = a.gslab + ((size_t)s * a.slab_tiles + tile_id) * a.n_gradops * 32;
   QFX_DCHECK(tile_id < a.slab_tiles);
-  if (QFX_HEA_POISON && a.poison) {
-    poison_lds(tile, (int)sizeof(tile), a.poison, tid, NT);
-    poison_lds(&opw2[0][0], (int)sizeof(opw2), a.poison, tid, NT);
-    poison_lds(fidx_s, (int)sizeof(fidx_s), a.poison, tid, NT);
-    poison_lds(fo_s, (int)sizeof(fo_s), a.poison, tid, NT);
-    poison_lds(&frag_s[0][0], (int)sizeof(frag_s), a.poison, tid, NT);
-    poison_lds(red64, (int)sizeof(red64), a.poison, tid, NT);
-    poison_lds(&gmeta_s[0][0], (int)sizeof(gmeta_s), a.poison, tid, NT);
-    poison_lds(rsc, (int)sizeof(rsc), a.poison, tid, NT);
-    poison_lds(emap_s, (int)sizeof(emap_s), a.poison, tid, NT);
-    poison_lds(&l1outer_s, (int)sizeof(l1outer_s), a.poison, tid, NT);
-    lds_barrier();
-  }
 
   // op 0's record and fragments are requested before the tile load (their latency hides behind it)
   if (tid < a.nops) {
@@ -1497,9 +1031,9 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
       ro_yy = (int)a.ro_y[s];
     }
   }
-  if (!(QFX_HEA_ABLATE && (a.ablate & 32)))
-    load_tile_il<NT, TB, PL>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
-                         h_q, fixed);
+  st.mark(PH_PRO);
+  load_tile_il<NT, TB>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T, h_q,
+                       fixed);
 
   if (a.ro_fuse ? tid == NT - 64 : tid == 0) {
     float wv[CMAX];
@@ -1589,8 +1123,9 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
   // FULL (t == TB): every wave owns exactly (2^(TB - 8)) / NW column blocks - a compile-time count, so the block
   // loops of the group ops carry no bounds checks or branches
   const int nbw = FULL ? (1 << (TB - 8)) / NW : (wave < nblk ? (nblk - wave + NW - 1) / NW : 0);
+  st.mark(PH_LOAD);
   lds_barrier_dma();
-  HEA_MARK();
+  st.mark(PH_BAR);
   int ngrad = 0;
   int pending = -1;                                    // ring: region of the previous op, if a gradient op
   // Partial-trace entries this lane adds per gradient op: lane (g4, cl) holds N[4 g4 + i][cl]; byte i of epi is the
@@ -1605,81 +1140,62 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
                                                     : 0xFFu;
     epi |= sl << (8 * i);
   }
-  // A layer-1 product-state op (always the program's last) runs after the op loop, where none of the loop's values
-  // are live: inside the loop its code pushed the group ops' register allocation into spills.
-  const bool l1last = a.nops > 0 && a.ops[(size_t)(a.nops - 1) * OPW + W_CODE] == OP_L1PROD;
-  const int nloop = l1last ? a.nops - 1 : a.nops;
-  for (int o = 0; o < nloop; ++o) {
+  for (int o = 0; o < a.nops; ++o) {
     // op o's record and fragments were written during op o - 1; the other buffers were last read at the
     // start of op o - 1, which every wave has finished at this barrier, so op o + 1's go there right away
-    if (QFX_HEA_ABLATE && (a.ablate & 1) && o > 0)
-      lds_barrier_wave();
-    else
+    if (o > 0) {
       op_barrier(wave);
-    HEA_MARK();
+      st.mark(PH_BAR);
+    }
     if (RING && pending >= 0) {
-      if (wave == NW - 1 && !(QFX_HEA_ABLATE && (a.ablate & 16))) flush(pending);
+      if (wave == NW - 1) flush(pending);
       pending = -1;
     }
-    const int* opw = opw2[(QFX_HEA_ABLATE && (a.ablate & 64)) ? 0 : (o & 1)];   // ablation: op 0's record
+    const int* opw = opw2[o & 1];
     uint4 F[4];
     if (fidx_s[o] >= 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) F[i] = frag_s[o & 1][64 * i + lane];
     }
-    if (o + 1 < a.nops && !(QFX_HEA_ABLATE && (a.ablate & 64))) {
+    if (o + 1 < a.nops) {
       if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
       if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
       dma_frags(a, k, fidx_s[o + 1], lane, wave, frag_s[(o + 1) & 1]);
     }
     const int code = opw[W_CODE];
 #if QFX_CHECKS_ON
-    QFX_DCHECK(code >= OP_APPLY && code <= OP_L1PROD && code != OP_READOUT);
-    if (code == OP_L1PROD) {
-      QFX_DCHECK(opw[W_NREAL] >= 1 && opw[W_NREAL] <= a.t && fidx_s[o] == -1 && o == a.nops - 1);
-      for (int e = 0; e < opw[W_NREAL]; ++e) QFX_DCHECK((opw[W_OFF + e] & 255) < a.t);
-    } else if (code != OP_OBS) {
+    QFX_DCHECK(code == OP_BACK || code == OP_GRAD_L1 || code == OP_OBS);
+    if (code != OP_OBS) {
       QFX_DCHECK(opw[W_NREAL] >= 0 && opw[W_NREAL] <= 4);
       QFX_DCHECK((uint32_t)opw[W_OFF + (lane & 15)] < (uint32_t)T);
       QFX_DCHECK((uint32_t)opw[W_BL + (lane & 31)] < (uint32_t)T);
       QFX_DCHECK((uint32_t)opw[W_BH + (lane & 31)] < (uint32_t)T);
       // -1 = no unitary (cross-matrix-only gradient ops); every op that applies one names a fragment
       QFX_DCHECK(fidx_s[o] >= -1 && fidx_s[o] < 4 * a.n_slots);
-      QFX_DCHECK(fidx_s[o] >= 0 || code == OP_GRAD || code == OP_GRAD_L1);
-      if (code != OP_UNAPPLY_PSI && code != OP_UNAPPLY_LAM && code != OP_APPLY)
-        QFX_DCHECK(opw[W_GIDX] >= 0 && opw[W_GIDX] < a.n_gradops);
+      QFX_DCHECK(fidx_s[o] >= 0 || code == OP_GRAD_L1);
+      QFX_DCHECK(opw[W_GIDX] >= 0 && opw[W_GIDX] < a.n_gradops);
     } else {
       QFX_DCHECK(opw[W_NREAL] >= 1 && opw[W_NREAL] <= a.C);
     }
 #endif
+    st.mark(PH_SETUP);
     if (code == OP_OBS) {
-      obs_op<NCK, NT, TB, PL>(tile, opw, tid, T, fixed, rsc);
-
-    } else if (code == OP_UNAPPLY_PSI || code == OP_APPLY) {
-      // U^H (or, re-applying a recomputed last pass, U) on the psi plane
-      group_apply<1, NW, true, 0, TB, PL>(tile, F, opw, fo_s[o], lane, wave, nbw);
-    } else if (code == OP_UNAPPLY_LAM) {
-      group_apply<1, NW, true, 1, TB, PL>(tile, F, opw, fo_s[o], lane, wave, nbw);
-    } else if (code == OP_BACK || code == OP_GRAD || code == OP_GRAD_L1) {
+      obs_op<NCK, NT, TB>(tile, opw, tid, T, fixed, rsc);
+      st.mark(PH_OTHER);
+    } else {   // OP_BACK / OP_GRAD_L1
       const uint32_t fo = fo_s[o];
       f4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      if (code == OP_BACK && (opw[W_FLAGS] & F_BACK_TRANS)) {
+      if (code == OP_BACK && (opw[W_FLAGS] & F_BACK_PSI)) {
         // U^H on psi and lambda, cross matrix at the op input from the results (hea_grad_reduce: input side)
-        group_back_t<NW, TB, PL>(tile, F, opw, fo, lane, wave, nbw, acc2);
-      } else if (FUSE && code == OP_BACK) {
-        // cross matrix from the apply's own registers (one pass over the blocks, no group_cross reads)
-        if (opw[W_FLAGS] & F_BACK_PSI)
-          group_apply<2, NW, true, 0, TB, PL, FUSE>(tile, F, opw, fo, lane, wave, nbw, acc2);
-        else
-          group_apply<1, NW, true, 1, TB, PL, FUSE>(tile, F, opw, fo, lane, wave, nbw, acc2);
+        group_back_t<NW, TB>(tile, F, opw, fo, lane, wave, nbw, acc2);
+        st.mark(PH_BACK);
+      } else if (code == OP_BACK) {
+        // U^H on lambda only, cross matrix from the apply's own registers (one pass over the blocks)
+        group_apply<NW, true, TB>(tile, F, opw, fo, lane, wave, nbw, acc2);
+        st.mark(PH_BACK);
       } else {
-        if (!(QFX_HEA_ABLATE && (a.ablate & 4))) group_cross<NW, TB, PL>(tile, opw, fo, lane, wave, nbw, acc2[0], acc2[1]);
-        if (code == OP_BACK && !(QFX_HEA_ABLATE && (a.ablate & 8))) {
-          if (opw[W_FLAGS] & F_BACK_PSI)
-            group_apply<2, NW, true, 0, TB, PL>(tile, F, opw, fo, lane, wave, nbw);
-          else
-            group_apply<1, NW, true, 1, TB, PL>(tile, F, opw, fo, lane, wave, nbw);
-        }
+        group_cross<NW, TB>(tile, opw, fo, lane, wave, nbw, acc2[0], acc2[1]);
+        st.mark(PH_GRADL1);
       }
       const f4 accR = acc2[0], accI = acc2[1];
       // Cross-wave sum of the partial-trace entries of N / rho into the op's region: packed biased fixed point
@@ -1695,7 +1211,6 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
       __asm__ volatile("" : "+v"(ep));
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (QFX_HEA_ABLATE && (a.ablate & 2)) break;
         const uint32_t sl = (ep >> (8 * i)) & 0xFFu;
         if (sl != 0xFFu) {
           // round half up (floor(x + 0.5), one instruction): unbiased for these continuous values - truncation biased
@@ -1710,27 +1225,20 @@ __global__ void __launch_bounds__(64 * WV, (64 * WV * 2) / 256) hea_adj_kernel(P
       }
       pending = reg;
       ++ngrad;
+      st.mark(PH_EPI);
     }
+    if constexpr (QFX_HEA_STAMPS) ++st.nops;
   }
   lds_barrier();
-  HEA_MARK();
   if (RING) {
     if (pending >= 0 && wave == NW - 1 && lane < 32) reduce_region(pending, lane);
   } else {
     for (int e = tid; e < ngrad * 32; e += NT) reduce_region(e >> 5, e & 31);
   }
-  if (l1last) {
-    QFX_DCHECK(!a.store_lam);
-    // the pass's last op: the fragment slots are free (no unitary here, none prefetched after it); its record was
-    // staged during op nops - 2 (or before the loop)
-    lds_barrier();
-    l1prod_op<NT, TB, PL>(tile, a, opw2[(a.nops - 1) & 1], tid, s, k, fixed, rsc[CMAX], slab, (float2*)&frag_s[0][0],
-                          emap_s, l1outer_s);
-  }
-  if (a.store_lam) store_lam_il<NT, TB, PL>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
-  HEA_MARK();
+  if (a.store_lam) store_lam_il<NT, TB>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
+  st.mark(PH_TAIL);
+  st.write(a.dbg, NW, wave, lane);
 }
-#undef HEA_MARK
 
 // Unitary fragments: per (client, slot) U and U^H in the real 32 x 32 embedding, laid out as the MFMA
 // A operand of v_mfma_f32_16x16x32_f16 (lane l: row 16h + (l & 15), k = 8 (l >> 4) .. +7), hi and lo fp16.
@@ -1904,64 +1412,24 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
 }
 #endif  // !QFX_HEA_BF16
 
-// Launch-variant knobs (A/B in one process: scripts/hea_ab.py): defaults from the environment, settable at run time.
-enum { K_PLANES = 0, K_FUSE = 1, K_ADJ_WAVES = 2, K_FULL13 = 3, K_COUNT = 4 };
-static int knob_v[K_COUNT] = {-1, -1, -1, -1};
-inline int knob(int k) {
-  if (knob_v[k] < 0) {
-    static const char* env[K_COUNT] = {"QFEDX_HEA_PLANES", "QFEDX_HEA_FUSE", "QFEDX_HEA_ADJ_WAVES", "QFEDX_HEA_FULL13"};
-    static const int dflt[K_COUNT] = {0, 1, 8, 0};
-    const char* e = getenv(env[k]);
-    knob_v[k] = e ? atoi(e) : dflt[k];
-  }
-  return knob_v[k];
-}
-
 }  // namespace HEA_NS
-
-// name: planes | fuse | adj_waves (4 or 8: waves of a 2^13 adjoint workgroup) | full13; returns the previous value, -1 unknown
-extern "C" int HEA_EXT(qfx_hea_set_knob)(const char* name, int value) {
-  static const char* names[HEA_NS::K_COUNT] = {"planes", "fuse", "adj_waves", "full13"};
-  for (int k = 0; k < HEA_NS::K_COUNT; ++k)
-    if (strcmp(name, names[k]) == 0) {
-      const int prev = HEA_NS::knob(k);
-      HEA_NS::knob_v[k] = value;
-      return prev;
-    }
-  return -1;
-}
 
 extern "C" int HEA_EXT(qfx_hea_pass)(int adjoint, const HEA_NS::PassArgs* args, int n_samples, hipStream_t st) {
   const HEA_NS::PassArgs& a = *args;
   if (a.t > HEA_NS::TMAX || a.t < 8 || a.C > HEA_NS::CMAX || a.n > 30 || a.c < 2) return -2;
-  const unsigned grid = (unsigned)((a.pair && !adjoint ? n_samples / 2 : n_samples) * a.n_tiles);
+  const unsigned grid = (unsigned)(n_samples * a.n_tiles);
   if (grid == 0) return 0;
-  const int planes = HEA_NS::knob(HEA_NS::K_PLANES), fuse = HEA_NS::knob(HEA_NS::K_FUSE);
-  const int wv4 = HEA_NS::knob(HEA_NS::K_ADJ_WAVES) == 4;
-  // full13: the 2^13 adjoint with a compile-time column-block count (t == 13: no per-block bounds branches)
-  const int full13 = HEA_NS::knob(HEA_NS::K_FULL13);
-#define HEA_LAUNCH(NCK)                                                                                     \
-  do {                                                                                                     \
-    if (!adjoint && a.pair)                                                                                \
-      hipLaunchKernelGGL((HEA_NS::hea_fwd2_kernel<NCK>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);            \
-    else if (!adjoint && a.t == HEA_NS::TMAX)                                                                 \
-      hipLaunchKernelGGL((HEA_NS::hea_fwd_kernel<NCK, true>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);       \
-    else if (!adjoint)                                                                                     \
-      hipLaunchKernelGGL((HEA_NS::hea_fwd_kernel<NCK, false>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);      \
-    else if (a.t <= 13 && planes)                                                                          \
-      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, true, false>), dim3(grid), dim3(512), 0, st, a); \
-    else if (a.t <= 13 && fuse && wv4)                                                                     \
-      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 4, false, false, true>), dim3(grid), dim3(256), 0, st, a); \
-    else if (a.t == 13 && fuse && full13)                                                                  \
-      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, true, false, true>), dim3(grid), dim3(512), 0, st, a); \
-    else if (a.t <= 13 && fuse)                                                                            \
-      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, false, true>), dim3(grid), dim3(512), 0, st, a); \
-    else if (a.t <= 13)                                                                                    \
-      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, 8, false, false, false>), dim3(grid), dim3(512), 0, st, a); \
-    else if (fuse)                                                                                         \
-      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 14, 16, true, false, true>), dim3(grid), dim3(1024), 0, st, a); \
-    else                                                                                                   \
-      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 14, 16, true, false, false>), dim3(grid), dim3(1024), 0, st, a); \
+  // adjoint: 2^13 tiles (8 waves, two workgroups per CU) up to t = 13, else one 16-wave 2^14 workgroup per CU
+#define HEA_LAUNCH(NCK)                                                                                      \
+  do {                                                                                                      \
+    if (!adjoint && a.t == HEA_NS::TMAX)                                                                     \
+      hipLaunchKernelGGL((HEA_NS::hea_fwd_kernel<NCK, true>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);        \
+    else if (!adjoint)                                                                                      \
+      hipLaunchKernelGGL((HEA_NS::hea_fwd_kernel<NCK, false>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);       \
+    else if (a.t <= 13)                                                                                     \
+      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, false>), dim3(grid), dim3(512), 0, st, a);         \
+    else                                                                                                    \
+      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 14, true>), dim3(grid), dim3(1024), 0, st, a);         \
   } while (0)
   switch (HEA_NS::class_kernel(a.C)) {
     case 1: HEA_LAUNCH(1); break;

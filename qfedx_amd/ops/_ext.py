@@ -4,7 +4,7 @@ On a GPU box the HIP path is mandatory: if the extension cannot be imported, ``e
 instead of silently falling back to the torch reference path.  ``QFEDX_AUTOBUILD=1`` builds it on
 first use (hipcc, gfx950) when the shared object is missing.  ``QFEDX_DEBUG=1`` loads the debug build
 ``qfedx_amd._qfedx_C_debug`` (device-side bounds checks that raise after the failing launch; build it with
-``python -m qfedx_amd._build --debug``).
+``python -m qfedx_amd._build --debug``); ``QFEDX_STAMPS=1`` the stall-attribution build ``_qfedx_C_stamps``.
 """
 from __future__ import annotations
 
@@ -18,14 +18,14 @@ def ext():
     global _EXT
     if _EXT is not None:
         return _EXT
-    debug = os.environ.get("QFEDX_DEBUG", "0") == "1"
-    name = "qfedx_amd._qfedx_C_debug" if debug else "qfedx_amd._qfedx_C"
+    from .. import _build
+    v = _build.variant()
+    name = "qfedx_amd." + _build._VARIANTS[v][1]
     try:
         _EXT = importlib.import_module(name)
     except ImportError as e:
         if os.environ.get("QFEDX_AUTOBUILD", "0") == "1":
-            from .. import _build
-            _build.build(debug=debug)
+            _build.build(debug=v)
             _EXT = importlib.import_module(name)
         else:
             raise RuntimeError(

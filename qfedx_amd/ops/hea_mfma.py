@@ -26,7 +26,6 @@ import torch
 from ._ext import ext
 from .hea_plan import OP_APPLY, OP_READOUT, TILE_BITS, W_CODE, build_plan, eligible, obs_table, pass_programs
 
-HEA_CHUNKS = 1       # client chunks per training step on staggered streams (A/B: scripts/hea_kbench.py)
 ADJ_TILE_BITS = 13   # adjoint tiles: 2^13 amplitudes x (psi, lambda) = 64 KB of LDS -> two workgroups per CU
 
 
@@ -43,17 +42,17 @@ _FEATURE = {"ry": 0, "rx": 1, "rz": 2}
 
 def _frag_index(ops: np.ndarray) -> torch.Tensor:
     """Per op the unitary fragment it multiplies by (slot * 4 + 0: U, + 2: U^H) or -1 (prefetch table)."""
-    from .hea_plan import OP_APPLY, OP_BACK, OP_UNAPPLY_LAM, OP_UNAPPLY_PSI, W_CODE, W_SLOT
+    from .hea_plan import OP_APPLY, OP_BACK, W_CODE, W_SLOT
     out = np.full(len(ops), -1, dtype=np.int32)
     for i, w in enumerate(ops):
         code = int(w[W_CODE])
         if code == OP_APPLY:
             out[i] = 4 * int(w[W_SLOT])
-        elif code in (OP_UNAPPLY_PSI, OP_UNAPPLY_LAM, OP_BACK):
+        elif code == OP_BACK:
             out[i] = 4 * int(w[W_SLOT]) + 2
     return torch.from_numpy(out)
 _NO_KEYS = torch.zeros(0, dtype=torch.int64)
-_NODBG = torch.zeros(0, dtype=torch.int64)     # no phase timestamps
+_NODBG = torch.zeros(0, dtype=torch.int64)     # no stall-attribution buffer (stamps build only)
 
 
 FUSED_ADAM_MAX_BLOCKS = 256   # hea_grad_reduce blocks (clients x gradient ops) up to which Adam is fused
@@ -99,13 +98,7 @@ class HeaMfmaProgram:
         self.n_slots = self.plan.n_slots
         self.passes = []
         gmeta = []
-        # Paired forward (QFEDX_HEA_FWD_PAIR=1, opt-in): when the adjoint runs its own 2^13 plan, the forward runs
-        # that plan too, two samples of a client per workgroup (hea_fwd2_kernel; an odd sample count falls back to
-        # one sample per 2^13 tile).  Measured even with the 2^14 one-sample forward at 16q (fwd0 +1%, fwd1 -2%):
-        # the forward is not LDS-issue bound, so the long-tested 2^14 path stays the default.
-        self.fwd_pair = (plan_a is not self.plan and self.adj_tile_bits == 13
-                         and os.environ.get("QFEDX_HEA_FWD_PAIR", "0") == "1")
-        fplan = plan_a if self.fwd_pair else self.plan
+        fplan = self.plan
         progs_f = pass_programs(fplan, [])
         # Forward passes after the last one that applies a unitary are identities on the state (they exist for
         # the adjoint's layer-1 gradient tiles, e.g. every pass of an L = 1 circuit): the forward stops at that
@@ -113,12 +106,7 @@ class HeaMfmaProgram:
         applies = [j for j, (_, fwd, _) in enumerate(progs_f) if any(int(w[W_CODE]) == OP_APPLY for w in fwd)]
         self.fwd_last = applies[-1] if applies else 0
         J = len(progs_f)
-        # QFEDX_HEA_RECOMPUTE=1: the adjoint of the last pass re-applies that pass's groups in-tile from its stored
-        # INPUT, so the forward's last pass only reads out.  Needs a stored input (J >= 2) and a last pass that
-        # applies groups.  Opt-in: at 16q the saved state write did not shorten the forward pass, and the
-        # re-applied groups lengthened the adjoint one.
-        self.recompute = (J >= 2 and self.fwd_last == J - 1 and os.environ.get("QFEDX_HEA_RECOMPUTE", "0") == "1")
-        progs_a = pass_programs(plan_a, gmeta, recompute_last=self.recompute)
+        progs_a = pass_programs(plan_a, gmeta)
         self.n_gradops = len(gmeta)
         if self.fwd_last < J - 1:
             pr, fr_ops, ar = progs_f[self.fwd_last]
@@ -154,15 +142,9 @@ class HeaMfmaProgram:
         self.scale = float(1 << (self.n // 2))
         self.feature = _FEATURE[spec.feature_map.lower()]
         self._ws = {}
-        self.pair_kernel = True
         self._ps_budget = None
         if self.device.type == "cuda":
             self._shift_budget()      # query free HBM now, never inside a graph capture
-
-    def _paired(self, B: int) -> bool:
-        """Forward passes on the two-sample kernel (``pair_kernel = False`` keeps the one-sample 2^13 kernel on the
-        same plan: bitwise the same results, used by the tests)."""
-        return self.fwd_pair and self.pair_kernel and B % 2 == 0
 
     # ------------------------------------------------------------------ workspaces
     @contextlib.contextmanager
@@ -200,11 +182,10 @@ class HeaMfmaProgram:
         """Tiles per sample of the pass that reads out <Z> (the last forward pass that runs)."""
         return 1 << (self.n - self.passes[self.fwd_last][0].t)
 
-    def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K, in_rep: int = 1,
-              pair: bool = False):
+    def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K, in_rep: int = 1):
         return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
                 int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
-                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep), int(pair), int(self.bf16)]
+                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep), int(self.bf16)]
 
     def _frags(self, params: torch.Tensor, K: int, tag: str = "") -> torch.Tensor:
         fr = self._buf(f"{tag}frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
@@ -212,11 +193,10 @@ class HeaMfmaProgram:
             ext().hea_frags(params, params.shape[1], self.slot_tab, self.n_slots, K, fr, self.bf16)
         return fr
 
-    def _forward(self, x, params, fr, K, B, part, store_last: bool = False, tag: str = "", after_first=None):
+    def _forward(self, x, params, fr, K, B, part, store_last: bool = False, tag: str = "", dbg=None):
         """Forward passes up to the readout pass ``fwd_last``; returns the stored pass outputs (all of them with
         ``store_last``: the adjoint starts each pass from its output; identity passes after ``fwd_last`` alias
-        its output).  ``tag`` names this client chunk's workspaces; ``after_first()`` runs right after the
-        first pass is queued."""
+        its output).  ``tag`` names the workspaces; ``dbg`` (stamps build): per-pass stall-attribution buffers."""
         C = ext()
         S = K * B
         N = S << self.n
@@ -226,26 +206,21 @@ class HeaMfmaProgram:
         J, R = self.n_passes, self.fwd_last
         for j in range(R + 1):
             p, fwd = self.passes[j][0], self.passes[j][1]
-            keep = j < R or (store_last and not self.recompute)
+            keep = j < R or store_last
             # evaluation only needs the previous pass output: two ping-pong buffers instead of one per pass
             name = f"{tag}psi{j}" if store_last else f"{tag}pe{j % 2}"
             out = self._buf(name, N, torch.int32) if keep else empty
             psi_in = stored[-1] if j > 0 else empty
-            geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K,
-                              pair=self._paired(B))
+            geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K)
             C.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
-                       part if j == R else fempty, fempty, _NODBG)
-            if j == 0 and after_first is not None:
-                after_first()
+                       part if j == R else fempty, fempty, dbg[f"fwd{j}"] if dbg else _NODBG)
             if keep:
                 stored.append(out)
-        if store_last and self.recompute:
-            stored.append(stored[R - 1])             # the last adjoint pass starts from its pass's input
-        elif store_last:
+        if store_last:
             stored += [stored[R]] * (J - 1 - R)
         return stored
 
-    def _adjoint(self, x, params, fr, K, B, stored, wread, gslab, tag: str = "", readout=None):
+    def _adjoint(self, x, params, fr, K, B, stored, wread, gslab, tag: str = "", readout=None, dbg=None):
         """Adjoint passes, last pass first.  ``readout`` = (part, y, wts, expz, rec): the first adjoint pass computes
         every sample's readout and dL/d<Z> itself (fused readout; ``wread`` is then its output, read by the later
         passes) instead of taking ``wread`` from the readout kernel."""
@@ -263,10 +238,11 @@ class HeaMfmaProgram:
             if readout is not None and j == J - 1:
                 part, yy, ww, expz, rec = readout
                 C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
-                           params, fr, fempty, part, gslab, _NODBG, [yy, ww, expz, wread, rec], self.tiles_last)
+                           params, fr, fempty, part, gslab, dbg[f"adj{j}"] if dbg else _NODBG,
+                           [yy, ww, expz, wread, rec], self.tiles_last)
             else:
                 C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
-                           params, fr, wread, fempty, gslab, _NODBG)
+                           params, fr, wread, fempty, gslab, dbg[f"adj{j}"] if dbg else _NODBG)
             lam_in = lam_out
 
     def _prep(self, xang, params):
@@ -494,8 +470,7 @@ class HeaMfmaProgram:
             keep = jj < R
             out = self._buf(f"pbpsi{(jj - j) % 2}", N, torch.int32) if keep else empty
             first = jj == j
-            geom = self._geom(p, jj == 0, False, keep, False, B, ps, S, xs.shape[1], Kr, nr if first else 1,
-                              pair=self._paired(B))
+            geom = self._geom(p, jj == 0, False, keep, False, B, ps, S, xs.shape[1], Kr, nr if first else 1)
             E.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, xs, thr, fr, fempty,
                        part if jj == R else fempty, fempty, _NODBG)
             psi_in = out
@@ -504,44 +479,34 @@ class HeaMfmaProgram:
         return z.view(na, nr, B, self.C)
 
     # ------------------------------------------------------------------ train step
-    def _chunks(self, K: int, B: int) -> int:
-        """Client chunks of a training step (``QFEDX_HEA_CHUNKS`` overrides).  Chunk i runs on its own stream
-        and starts once chunk i-1's first forward pass is queued, so HBM-bound forward passes of one chunk
-        overlap the LDS/MFMA-bound adjoint passes of another and no pass drains the GPU by itself."""
-        env = os.environ.get("QFEDX_HEA_CHUNKS")
-        n = int(env) if env else HEA_CHUNKS
-        return max(1, min(n, K))
-
-    def _stream(self, i: int) -> torch.cuda.Stream:
-        streams = self.__dict__.setdefault("_streams", [])
-        while len(streams) <= i:
-            streams.append(torch.cuda.Stream(device=self.device))
-        return streams[i]
-
     fuses_optimizer = True    # VQCEngine: loss_and_grads(fused_opt=...) may run the Adam step in the reduction
 
-    def _step(self, x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, tag="", after_first=None,
-              adam=None):
-        """Forward, readout + CE, adjoint and gradient reduction of clients [0, K) of the given row slices.
+    def _fused_readout(self, noise) -> bool:
+        """Noiseless steps compute the readout in the first adjoint pass (``QFEDX_FUSED_READOUT=0`` keeps the
+        separate readout kernel; bench A/B)."""
+        return (noise is None and os.environ.get("QFEDX_FUSED_READOUT", "1") != "0"
+                and self.tiles_last * self.C <= 64)
+
+    def _step(self, x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=None, dbg=None):
+        """Forward, readout + CE, adjoint and gradient reduction of clients [0, K).
         ``adam`` = (tensors, hyper) from ``BatchedOptimizer.fused_adam``: the clients' Adam step runs in the
-        gradient reduction's epilogue (one launch fewer per local step)."""
+        gradient reduction's epilogue (one launch fewer per local step).  ``dbg``: stall-attribution buffers per
+        pass (``stamp_buffers``, stamps build only)."""
         C = ext()
         S = K * B
-        fr = self._frags(p, K, tag)
-        part = self._buf(f"{tag}part", S * self.tiles_last * self.C, torch.float32)
-        wread = self._buf(f"{tag}wread", S * self.C, torch.float32)
-        gslab = self._buf(f"{tag}gslab", S * self.slab_tiles * self.n_gradops * 32, torch.int64)
-        stored = self._forward(x, p, fr, K, B, part, store_last=True, tag=tag, after_first=after_first)
-        # Fused readout (noiseless steps; QFEDX_FUSED_READOUT=0 keeps the separate kernel): the first adjoint pass
-        # computes each sample's <Z>, cross entropy and dL/d<Z> from the readout partials, and the gradient
-        # reduction sums the clients' loss, hits and readout gradients - one launch fewer per local step.
-        fuse_ro = (noise is None and os.environ.get("QFEDX_FUSED_READOUT", "1") != "0"
-                   and self.tiles_last * self.C <= 64)
+        fr = self._frags(p, K)
+        part = self._buf("part", S * self.tiles_last * self.C, torch.float32)
+        wread = self._buf("wread", S * self.C, torch.float32)
+        gslab = self._buf("gslab", S * self.slab_tiles * self.n_gradops * 32, torch.int64)
+        stored = self._forward(x, p, fr, K, B, part, store_last=True, dbg=dbg)
+        # Fused readout: the first adjoint pass computes each sample's <Z>, cross entropy and dL/d<Z> from the readout
+        # partials, and the gradient reduction sums the clients' loss, hits and readout gradients - one launch fewer
+        # per local step.
         ro = None
-        if fuse_ro:
-            rec = self._buf(f"{tag}rorec", S * (2 * self.C + 2), torch.float32)
+        if self._fused_readout(noise):
+            rec = self._buf("rorec", S * (2 * self.C + 2), torch.float32)
             ro = [rec, loss, correct]
-            self._adjoint(x, p, fr, K, B, stored, wread, gslab, tag, readout=(part, yy, ww, expz, rec))
+            self._adjoint(x, p, fr, K, B, stored, wread, gslab, readout=(part, yy, ww, expz, rec), dbg=dbg)
         else:
             if noise is None:
                 C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
@@ -550,25 +515,28 @@ class HeaMfmaProgram:
                 from .statevec_hip import _keys
                 C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
                              correct, grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
-            self._adjoint(x, p, fr, K, B, stored, wread, gslab, tag)
+            self._adjoint(x, p, fr, K, B, stored, wread, gslab, dbg=dbg)
         if adam is None:
             C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1],
                               None, None, ro, self.C, self.n_theta)
         else:
-            cnt = self._zbuf(f"{tag}adamcnt", K, torch.int32)
+            cnt = self._zbuf("adamcnt", K, torch.int32)
             C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1],
                               adam[0] + [cnt], adam[1], ro, self.C, self.n_theta)
 
-    def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
-                       out_correct=None, init: torch.Tensor | None = None, fused_opt=None) -> dict:
-        """One adjoint training step (same contract as ``HipProgram.loss_and_grads``).
+    def stamp_buffers(self) -> dict:
+        """Zeroed stall-attribution buffers, one per pass launch (``fwd{j}``, ``adj{j}``), for the stamps build
+        (``QFEDX_STAMPS=1``, scripts/hea_stamps.py)."""
+        rows = int(getattr(ext(), "HEA_STAMP_ROWS", 0)) * 16
+        names = [f"fwd{j}" for j in range(self.fwd_last + 1)] + [f"adj{j}" for j in range(self.n_passes)]
+        return {nm: torch.zeros(rows, dtype=torch.int64, device=self.device) for nm in names}
 
-        Clients are independent within a step, so the step runs as ``_chunks`` client chunks on staggered
-        streams (fork/join events; captured into the round's hipGraph as parallel branches).  Every chunk
-        writes only its own client rows, so results are bitwise those of one chunk.
-        ``fused_opt`` = (BatchedOptimizer, active): on one chunk, with params updated in place (a contiguous fp32
-        tensor) and HIP Adam, the optimizer step runs in the gradient reduction's epilogue and the result says
-        ``opt_done``; otherwise the caller steps the optimizer itself."""
+    def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
+                       out_correct=None, init: torch.Tensor | None = None, fused_opt=None, dbg=None) -> dict:
+        """One adjoint training step (same contract as ``HipProgram.loss_and_grads``).
+        ``fused_opt`` = (BatchedOptimizer, active): with params updated in place (a contiguous fp32 tensor) and HIP
+        Adam, the optimizer step runs in the gradient reduction's epilogue and the result says ``opt_done``;
+        otherwise the caller steps the optimizer itself."""
         if init is not None:
             raise ValueError("the MFMA engine starts from the angle feature map (no initial states)")
         x, p, K, B = self._prep(xang, params)
@@ -579,59 +547,16 @@ class HeaMfmaProgram:
         loss = torch.empty(K, dtype=torch.float32, device=self.device) if out_loss is None else out_loss
         correct = torch.empty(K, dtype=torch.float32, device=self.device) if out_correct is None else out_correct
         grad = torch.empty_like(p)
-        n = self._chunks(K, B) if noise is None else 1
         adam = None
-        # Auto: fused only while the reduction has at most one block per CU.  Every block publishes its gradient
-        # entries with one agent-scope release (an L2 writeback here): at 16q x 64 clients (832 blocks) the fused
-        # launch took 33.6 us against 13 + 5.4 us for the two launches; at the 8-client share (104 blocks) it saves
-        # a launch (round 387 -> 382 us; profiles/r3_fused_adam_ab.txt).  QFEDX_FUSED_ADAM=1 / 0 forces it on / off.
-        mode = os.environ.get("QFEDX_FUSED_ADAM", "auto")
-        ro_rows = 1 if (noise is None and os.environ.get("QFEDX_FUSED_READOUT", "1") != "0"
-                        and self.tiles_last * self.C <= 64) else 0
-        want = mode == "1" or (mode == "auto" and K * (self.n_gradops + ro_rows) <= FUSED_ADAM_MAX_BLOCKS)
-        if (want and fused_opt is not None and n == 1 and self.n_gradops > 0
-                and p.data_ptr() == params.data_ptr()):
+        # Fused only while the reduction has at most one block per CU.  Every block publishes its gradient entries
+        # with one agent-scope release (an L2 writeback here): at 16q x 64 clients (832 blocks) the fused launch took
+        # 33.6 us against 13 + 5.4 us for the two launches; at the 8-client share (104 blocks) it saves a launch
+        # (round 387 -> 382 us; profiles/r3_fused_adam_ab.txt).
+        ro_rows = 1 if self._fused_readout(noise) else 0
+        want = K * (self.n_gradops + ro_rows) <= FUSED_ADAM_MAX_BLOCKS
+        if want and fused_opt is not None and self.n_gradops > 0 and p.data_ptr() == params.data_ptr():
             adam = fused_opt[0].fused_adam(p, fused_opt[1])
-        if n == 1:
-            self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=adam)
-        else:
-            bounds = [(i * K) // n for i in range(n + 1)]
-            cur = torch.cuda.current_stream(self.device)
-            C = self.C
-            # size every chunk's workspaces on the launching stream before forking (nothing allocates on a branch)
-            for i in range(n):
-                k0, k1 = bounds[i], bounds[i + 1]
-                Si = (k1 - k0) * B
-                self._buf(f"c{i}frags", max((k1 - k0) * self.n_slots * 4 * 128 * 4, 1), torch.int32)
-                for name, numel, dt in ((f"c{i}part", Si * self.tiles_last * C, torch.float32),
-                                        (f"c{i}wread", Si * C, torch.float32),
-                                        (f"c{i}gslab", Si * self.slab_tiles * self.n_gradops * 32, torch.int64)):
-                    self._buf(name, numel, dt)
-                for j in range(self.fwd_last + (0 if self.recompute else 1)):
-                    self._buf(f"c{i}psi{j}", Si << self.n, torch.int32)
-                for j in range(min(2, self.n_passes - 1)):
-                    self._buf(f"c{i}lam{j}", Si << self.n, torch.int32)
-            gates = [torch.cuda.Event() for _ in range(n - 1)]
-            for i in range(n):
-                k0, k1 = bounds[i], bounds[i + 1]
-                st = cur if i == 0 else self._stream(i - 1)
-                if i > 0:
-                    st.wait_event(gates[i - 1])         # after chunk i-1's first pass (and all prior work)
-                rec = (lambda e=gates[i]: e.record()) if i < n - 1 else None
-                r0, r1 = k0 * B, k1 * B
-                with torch.cuda.stream(st):
-                    self._step(x[r0:r1], p[k0:k1], yy[r0:r1], ww[r0:r1], k1 - k0, B, loss[k0:k1],
-                               correct[k0:k1], grad[k0:k1], expz[r0 * C:r1 * C], None, None, step, f"c{i}", rec)
-                if i > 0:
-                    # allocated on the launching stream, used on this side stream: a later regrow of a workspace
-                    # must not hand its memory out while the side stream may still read it
-                    for name, t in self._ws.items():
-                        if name.startswith(f"c{i}"):
-                            t.record_stream(st)
-                    for t in (x, p, yy, ww, loss, correct, grad, expz):
-                        t.record_stream(st)
-            for i in range(n - 1):
-                cur.wait_stream(self._stream(i))
+        self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=adam, dbg=dbg)
         res = {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}
         if adam is not None:
             res["opt_done"] = True

@@ -34,8 +34,6 @@ tests hold against a dense simulation, and the HIP kernel is tested against both
 from __future__ import annotations
 
 import copy
-import math
-import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -45,11 +43,11 @@ TILE_BITS = 14             # 2^14 fp16 complex amplitudes = 64 KB of LDS per sta
 MIN_CONTIG = 5             # contiguous low bits in a strided tile (32 amplitudes = 128 B)
 
 # op codes (kept in sync with csrc/hea_mfma.hip)
-OP_APPLY, OP_UNAPPLY_PSI, OP_UNAPPLY_LAM, OP_GRAD, OP_GRAD_L1, OP_OBS, OP_READOUT, OP_BACK, OP_L1PROD = 1, 2, 3, 4, 5, 6, 7, 8, 9
+OP_APPLY, OP_GRAD_L1, OP_OBS, OP_READOUT, OP_BACK = 1, 5, 6, 7, 8
 OP_WORDS = 128
 W_CODE, W_SLOT, W_NREAL, W_FLAGS, W_RFULL, W_RT, W_TH, W_PH, W_OFF, W_BL, W_BH = 0, 1, 2, 3, 4, 8, 12, 16, 20, 36, 68
-F_BACK_PSI = 1             # OP_BACK also un-applies the group on psi (still needed further back)
-F_BACK_TRANS = 2           # OP_BACK (with F_BACK_PSI) in the transposed form: cross matrix at the op input
+F_BACK_PSI = 1             # OP_BACK also un-applies the group on psi (still needed further back), in the transposed
+                           # form (group_back_t): its cross matrix is taken at the op INPUT
 W_GIDX = 100               # gradient ops: global index of the op's partial-trace record in the slab
 MAX_CLASSES = 8
 BANK_BITS = 5              # ds_read_b32 / ds_write_b32: bank = dword address % 32 per 32-lane half
@@ -185,8 +183,6 @@ def build_plan(n: int, L: int, readout, chain: bool = True, feature: str = "ry",
     pass) and the trimmed plan (a non-final pass defers each layer's ragged tail so its groups are full
     4-qubit unitaries) and keeps the one with fewer passes, then fewer group ops: for 16q x 3L the trimmed
     plan runs 8 group ops instead of 10 in the same two passes."""
-    if trim is None and os.environ.get("QFEDX_HEA_TRIM", "auto") in ("0", "1"):   # A/B timing override
-        trim = os.environ["QFEDX_HEA_TRIM"] == "1"
     key = (n, L, tuple(readout), chain, feature, tile_bits, swizzle)
     if trim is None and key in _PLAN_CACHE:          # the candidate search runs once per circuit shape
         return copy.deepcopy(_PLAN_CACHE[key])
@@ -562,54 +558,12 @@ def obs_table(plan: HEAPlan, p: Pass, code: int) -> np.ndarray:
     return w
 
 
-def _trans_default() -> bool:
-    """Transposed BACK ops (``F_BACK_TRANS``, kernel ``group_back_t``): on unless QFEDX_HEA_TRANS=0 (A/B)."""
-    return os.environ.get("QFEDX_HEA_TRANS", "1") != "0"
-
-
-def _l1prod_default() -> bool:
-    """Layer-1 gradients of the last adjoint pass from the closed-form product state (``OP_L1PROD``): opt-in
-    (QFEDX_HEA_L1PROD=1).  On the GPU it matched the dense oracle and was deterministic at 16q, but at 20q x 2L the
-    first vjp call of a fresh program differed from later identical calls in ~20% of workgroups (the lambda image it
-    reads was identical; the cross-thread reductions of its terms were not) - cause not found yet, so the per-group
-    GRAD_L1 ops stay the default (docs/ARCHITECTURE.md, open items)."""
-    return os.environ.get("QFEDX_HEA_L1PROD", "0") == "1"
-
-
-def l1prod_table(plan: HEAPlan, p: Pass, gidx0: int) -> np.ndarray:
-    """OP_L1PROD record: every layer-1 qubit of pass ``p``'s l1 groups, word W_OFF + e = tile bit | group << 8 |
-    index in group << 16; group g's partial traces go to slab row W_GIDX + g (= gidx0 + g)."""
-    w = np.zeros(OP_WORDS, dtype=np.int64)
-    w[W_CODE] = OP_L1PROD
-    w[W_SLOT] = -1
-    ents = []
-    for g, grp in enumerate(p.l1):
-        for j, q in enumerate(grp.qubits):
-            tb = p.bits.index(q)           # layer 1 acts in frame 0: qubit q is memory bit q
-            ents.append(tb | (g << 8) | (j << 16))
-    if len(ents) > 16:
-        raise ValueError("OP_L1PROD: at most 16 layer-1 qubits per tile")
-    w[W_NREAL] = len(ents)
-    w[W_OFF:W_OFF + len(ents)] = ents
-    w[W_GIDX] = gidx0
-    return w
-
-
-def pass_programs(plan: HEAPlan, meta: list | None = None, recompute_last: bool = False, trans: bool | None = None,
-                  l1prod: bool | None = None):
+def pass_programs(plan: HEAPlan, meta: list | None = None):
     """Forward and adjoint op lists per pass: list of (Pass, fwd_ops [k, OP_WORDS], adj_ops).  ``meta``
-    (optional list) receives one row per gradient op: [tiles of its pass, nreal, theta slots x4, phi slots x4].
-    ``recompute_last``: the last pass's adjoint starts from that pass's INPUT and re-applies its groups in-tile
-    before the observable op, so the forward's last pass never stores its output (one state write and read of
-    HBM per sample saved for a few in-tile group ops).  ``trans``: BACK ops that un-apply psi too run transposed
-    (``F_BACK_TRANS``): their cross matrix is taken at the op input, flagged for hea_grad_reduce by bit 4 of the
-    meta row's nreal word.  ``l1prod``: the LAST adjoint pass (pass 0, where every later gate is un-applied and psi is
-    the layer-1 product state) measures all its layer-1 qubits in one ``OP_L1PROD`` op from lambda and the closed-form
-    factors (same gradient records as the per-group GRAD_L1 ops, psi never needed after the pass's last group op)."""
-    if trans is None:
-        trans = _trans_default()
-    if l1prod is None:
-        l1prod = _l1prod_default()
+    (optional list) receives one row per gradient op: [tiles of its pass, nreal | inside << 4, theta slots x4,
+    phi slots x4].  BACK ops that un-apply psi too run transposed (``group_back_t``): their cross matrix is taken at
+    the op input (``inside``, hea_grad_reduce applies the input-side generators); a pass's last BACK op, when psi is
+    no longer needed, un-applies lambda only and takes the cross matrix at its output."""
     out = []
     gidx = [0]
     gmeta = meta if meta is not None else []
@@ -618,39 +572,20 @@ def pass_programs(plan: HEAPlan, meta: list | None = None, recompute_last: bool 
         fwd = [group_table(plan, p, g, OP_APPLY) for g in p.groups]
         if j == J - 1:
             fwd.append(obs_table(plan, p, OP_READOUT))
-        # the adjoint of pass j starts from pass j's stored OUTPUT (or, recomputing the last pass, its input) and
-        # walks back
-        adj = []
-        if j == J - 1 and recompute_last:
-            adj = [group_table(plan, p, g, OP_APPLY) for g in p.groups]
-        if j == J - 1:
-            adj.append(obs_table(plan, p, OP_OBS))
+        # the adjoint of pass j starts from pass j's stored OUTPUT and walks back
+        adj = [obs_table(plan, p, OP_OBS)] if j == J - 1 else []
         rev = list(reversed(p.groups))
-        prod = l1prod and j == 0 and bool(p.l1)
         for i, g in enumerate(rev):
             # gradient cross matrix + U^H on lambda (and on psi while it is still needed further back)
-            # (QFEDX_HEA_L1PROD_PSI=1, diagnostics: the last group op still un-applies psi under OP_L1PROD)
-            keep_psi = os.environ.get("QFEDX_HEA_L1PROD_PSI", "0") == "1"
-            psi_needed = i < len(rev) - 1 or (bool(p.l1) and (not prod or keep_psi))
-            flags = (F_BACK_PSI | (F_BACK_TRANS if trans else 0)) if psi_needed else 0
-            adj.append(group_table(plan, p, g, OP_BACK, flags))
-        if not prod:
-            for g in p.l1:
-                adj.append(group_table(plan, p, g, OP_GRAD_L1))
+            psi_needed = i < len(rev) - 1 or bool(p.l1)
+            adj.append(group_table(plan, p, g, OP_BACK, F_BACK_PSI if psi_needed else 0))
+        for g in p.l1:
+            adj.append(group_table(plan, p, g, OP_GRAD_L1))
         for w in adj:
-            if w[W_CODE] in (OP_BACK, OP_GRAD, OP_GRAD_L1):
+            if w[W_CODE] in (OP_BACK, OP_GRAD_L1):
                 w[W_GIDX] = gidx[0]
-                inside = 16 if (int(w[W_CODE]) == OP_BACK and int(w[W_FLAGS]) & F_BACK_TRANS) else 0
+                inside = 16 if (int(w[W_CODE]) == OP_BACK and int(w[W_FLAGS]) & F_BACK_PSI) else 0
                 gmeta.append([1 << (plan.n - p.t), int(w[W_NREAL]) | inside] + [int(v) for v in w[W_TH:W_TH + 4]] +
-                             [int(v) for v in w[W_PH:W_PH + 4]])
-                gidx[0] += 1
-        if prod:
-            # one gradient record per layer-1 group, as its GRAD_L1 op would have had (cross matrix at the output of
-            # the layer-1 rotations), filled by the single product-state op
-            adj.append(l1prod_table(plan, p, gidx[0]))
-            for g in p.l1:
-                w = group_table(plan, p, g, OP_GRAD_L1)
-                gmeta.append([1 << (plan.n - p.t), int(w[W_NREAL])] + [int(v) for v in w[W_TH:W_TH + 4]] +
                              [int(v) for v in w[W_PH:W_PH + 4]])
                 gidx[0] += 1
         out.append((p, np.stack(fwd) if fwd else np.zeros((0, OP_WORDS), np.int64),
@@ -760,7 +695,7 @@ def _round_bf16(z):
 
 
 def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp16: bool = False,
-            recompute_last: bool = False, storage: str | None = None):
+            storage: str | None = None):
     """Tile-exact execution of ``plan`` with the kernel's tables.
 
     xang [K, B, n] encoded feature angles, params [K, P] (theta first), wread [K, B, C] = dL/d<Z_c>.
@@ -770,7 +705,7 @@ def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp1
     """
     n, t = plan.n, plan.t
     K, B, _ = xang.shape
-    progs = pass_programs(plan, recompute_last=recompute_last)
+    progs = pass_programs(plan)
     if storage is None:
         storage = "fp16" if fp16 else "exact"
     rnd = {"fp16": _round16, "bf16": _round_bf16, "exact": lambda z: z}[storage]
@@ -791,7 +726,6 @@ def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp1
             psi0 = np.full(1 << n, scale, dtype=np.complex128)
             for q in range(n):
                 psi0 = psi0 * np.array(wv[q])[(idx >> q) & 1]
-            psi0_exact = psi0
             psi0 = rnd(psi0)
             stored = [psi0]
             # forward passes
@@ -824,8 +758,7 @@ def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp1
             lam = None
             for j in range(len(progs) - 1, -1, -1):
                 p, _, adj = progs[j]
-                # output of forward pass j (its input when the last pass is recomputed in-tile)
-                psi_in = stored[j] if (recompute_last and j == len(progs) - 1) else stored[j + 1]
+                psi_in = stored[j + 1]                        # output of forward pass j
                 lam_out = np.zeros(1 << n, dtype=np.complex128)
                 sg_w = np.array([sigma(p.H, int(x)) for x in range(1 << p.t)])
                 for tid in range(1 << (n - p.t)):
@@ -844,33 +777,16 @@ def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp1
                             lm = rnd((rr @ sg) * ps)
                             continue
                         a = _addr(w, p.t, fixed)
-                        if code == OP_BACK and int(w[W_FLAGS]) & F_BACK_TRANS:
+                        if code == OP_BACK and int(w[W_FLAGS]) & F_BACK_PSI:
                             # transposed BACK: U^H on both, cross matrix of the rounded input states
                             Uh = Us[int(w[W_SLOT])].conj().T
                             lm[a] = rnd((Uh @ lm[a].T).T)
                             ps[a] = rnd((Uh @ ps[a].T).T)
                             _grad(w, ps[a], lm[a], th, grads[k], gfac, inside=True)
-                        elif code == OP_BACK:
+                        elif code == OP_BACK:           # lambda only, cross matrix at the op output
                             _grad(w, ps[a], lm[a], th, grads[k], gfac)
-                            Uh = Us[int(w[W_SLOT])].conj().T
-                            lm[a] = rnd((Uh @ lm[a].T).T)
-                            if int(w[W_FLAGS]) & F_BACK_PSI:
-                                ps[a] = rnd((Uh @ ps[a].T).T)
-                        elif code == OP_APPLY:
-                            ps[a] = rnd((Us[int(w[W_SLOT])] @ ps[a].T).T)
-                        elif code == OP_UNAPPLY_PSI:
-                            ps[a] = rnd((Us[int(w[W_SLOT])].conj().T @ ps[a].T).T)
-                        elif code == OP_UNAPPLY_LAM:
                             lm[a] = rnd((Us[int(w[W_SLOT])].conj().T @ lm[a].T).T)
-                        elif code == OP_L1PROD:
-                            # every layer-1 group of the tile against the exact (scaled) product state
-                            pr = np.empty_like(ps)
-                            pr[sg_w] = psi0_exact[mem]
-                            for g in p.l1:
-                                wg = group_table(plan, p, g, OP_GRAD_L1)
-                                ag = _addr(wg, p.t, fixed)
-                                _grad(wg, pr[ag], lm[ag], th, grads[k], gfac)
-                        else:   # OP_GRAD / OP_GRAD_L1
+                        else:   # OP_GRAD_L1
                             _grad(w, ps[a], lm[a], th, grads[k], gfac)
                     lam_out[mem] = lm[sg_w]
                 lam = lam_out

@@ -1,10 +1,10 @@
-"""Interleaved A/B of MFMA-engine launch variants in ONE process (guide rule: perf deltas from interleaved rounds on
-one device).  Variants are runtime knobs of the pass launcher (``hea_set_knob``: adj_waves 8 | 4, planes, fuse) and
-the state storage (fp16 | bf16).  Each round times every variant's full local step (frags, forward, readout, adjoint,
-gradient reduction) and its adjoint passes alone; prints per-variant median / min ms over the rounds as JSON.
+"""Interleaved A/B of MFMA-engine variants in ONE process (guide rule: perf deltas from interleaved rounds on one
+device).  Variants are run-time environment switches (``env.NAME=value``, e.g. env.QFEDX_FUSED_READOUT=0) and the state
+storage (fp16 | bf16).  Each round times every variant's full local step (frags, forward, readout, adjoint, gradient
+reduction) and its adjoint passes alone; prints per-variant median / min ms over the rounds as JSON.
 
 python scripts/hea_ab.py [--qubits 16 --layers 3 --clients 64 --batch 32 --rounds 7 --iters 10]
-                         [--variants "w8:adj_waves=8,w4:adj_waves=4,bf16w8:storage=bf16"]
+                         [--variants "fp16:storage=fp16,bf16:storage=bf16"]
 """
 import argparse
 import json
@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--variants", default="w8:adj_waves=8,w4:adj_waves=4")
+    ap.add_argument("--variants", default="fp16:storage=fp16,bf16:storage=bf16")
     args = ap.parse_args()
     import torch
     from qfedx_amd.models.vqc import VQCSpec
@@ -54,17 +54,13 @@ def main():
     variants = parse_variants(args.variants)
     progs = {}
     for name, knobs in variants:
-        # plan-level variants are fixed when the program is built: l1prod=0/1 (OP_L1PROD for the last pass)
-        os.environ["QFEDX_HEA_L1PROD"] = knobs.get("l1prod", "0")
         progs[name] = HeaMfmaProgram(spec, dev, storage=knobs.get("storage", "fp16"))
-    C = ext()
+    ext()
 
     def set_knobs(knobs):
         for k, v in knobs.items():
             if k.startswith("env."):           # run-time environment switches, e.g. env.QFEDX_FUSED_READOUT=0
                 os.environ[k[4:]] = v
-            elif k not in ("storage", "l1prod"):
-                C.hea_set_knob(k, int(v))
 
     def prep(prog):
         xx = x.reshape(S, -1).float().contiguous()
