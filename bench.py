@@ -52,6 +52,7 @@ def timed_rounds(cfg, device, backend, world, warmup: int, steps: int, counts: l
     t0 = time.perf_counter()
     for r in range(warmup, warmup + steps):
         rec = runner.run_round(r, sync=False)
+        runner.comm_bytes = rec.get("comm_bytes_per_rank", 0)
         if counts is not None:
             counts.append(rec["participants"] - rec["dropped"])
     # host time to build and enqueue a round, without the time it waited for the GPU to free a pinned buffer
@@ -192,6 +193,10 @@ def main():
     cfg = make_config(args)
     device, backend, world = setup(cfg)
     runner, dt = timed_rounds(cfg, device, backend, world, args.warmup, args.steps)
+    # clients trained by each rank (the 8-GPU operating point is 8 of the 64 headline clients per rank)
+    from qfedx_amd.parallel.dist import all_gather_cat
+    per_rank = [int(v) for v in all_gather_cat(torch.tensor([len(runner.local_ids)], dtype=torch.int64,
+                                                             device=device), world).cpu().tolist()]
     phases = phase_ms(runner, world, args.steps)
     ev = runner.evaluate()
     prec = precision_check(runner, args.batch) if (args.precision_check and device.type == "cuda") else {}
@@ -233,6 +238,9 @@ def main():
             "rccl_world_size": rccl_ws,
             "graph_comm": graph_comm,
             "host_ms_per_round": round(getattr(runner, "host_ms", 0.0), 4),   # enqueue time (GPU runs behind)
+            "clients_per_rank": per_rank,
+            # bytes each rank all-reduces per round: ONE fused [exact int64 update | weight | metrics] buffer
+            "allreduce_bytes_per_round": int(getattr(runner, "comm_bytes", 0)),
             **phases,
             **prec,
             "config": {

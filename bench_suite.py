@@ -61,8 +61,16 @@ SUITE = {
                                       "privacy.secagg_graph=sparse"],
                                      "client local-steps/sec (16-qubit VQC x 64 clients, SecAgg+ sparse neighbour "
                                      "masks on the device)", None),
-    "vqc20q_dp64_mfma": ("configs/baseline3_20q_dp_64clients.yaml", ["model.state_dtype=mfma"],
+    # DP lines key their noise by the public seed (privacy.deterministic_noise: reproducible accuracy; NOT private)
+    "vqc20q_dp64_mfma": ("configs/baseline3_20q_dp_64clients.yaml",
+                         ["model.state_dtype=mfma", "privacy.deterministic_noise=true"],
                          "client local-steps/sec (20-qubit VQC x 64 non-IID clients, DP, fp16 MFMA engine)", None),
+    # distributed DP: each client adds sigma^2 C^2 / m, the SecAgg sum carries the accounted sigma C
+    "vqc20q_ddp64_mfma": ("configs/baseline3_20q_dp_64clients.yaml",
+                          ["model.state_dtype=mfma", "privacy.deterministic_noise=true",
+                           "privacy.noise_mode=distributed", "privacy.secure_agg=true"],
+                          "client local-steps/sec (20-qubit VQC x 64 non-IID clients, distributed DP + SecAgg, "
+                          "fp16 MFMA engine)", None),
     "vqc48q_mps64": ("configs/mps_48q_64clients.yaml", [],
                      "client local-steps/sec (48-qubit VQC x 64 clients, MPS tensor-network backend)", None),
     "vqc4q_2_cpu": ("configs/baseline1_4q_2clients_cpu.yaml", ["train.local_steps=1"],
@@ -127,6 +135,12 @@ def main():
                        "secure_agg": cfg.privacy.secure_agg,
                        "shots": cfg.noise.shots},
         }
+        if cfg.privacy.dp:
+            rec["dp"] = {"noise_mode": cfg.privacy.noise_mode, "noise_multiplier": cfg.privacy.noise_multiplier,
+                         "clip_norm": cfg.privacy.clip_norm, "delta": cfg.privacy.delta,
+                         "rounds_accounted": len(runner.accountant.history) if hasattr(runner.accountant, "history")
+                         else None, "epsilon": round(float(runner.accountant.get_epsilon(cfg.privacy.delta)), 4),
+                         "deterministic_noise": cfg.privacy.deterministic_noise}
         eng = getattr(runner.adapter, "engine", None)
         if kind == "vqc" and backend == "hip":
             from bench import precision_check

@@ -90,6 +90,13 @@ class PrivacyConfig:
     secagg_bits: int = 48               # fixed-point ring Z_{2^bits} for exact mask cancellation
     secagg_scale: float = 2.0 ** 24
     secagg_graph: str = "full"          # full (every pair) | sparse (SecAgg+: 2 ceil(log2 K) neighbours, O(K log K))
+    # a round is aborted (no update aggregated) if a surviving participant has fewer live mask neighbours than this;
+    # 0 = auto: half its graph degree (sparse, SecAgg+), 1 (full graph)
+    secagg_min_live: int = 0
+    # local: every client adds N(0, sigma^2 C^2) (ROADMAP.md:50-51; the sum carries sqrt(m) sigma C);
+    # distributed: every client adds N(0, sigma^2 C^2 / m) for the round's m live participants, so the SecAgg sum
+    # carries exactly the sigma C the accountant charges (distributed DP: needs secure_agg to hide each share)
+    noise_mode: str = "local"
     # testing/debug only: key DP noise and DP client sampling by the PUBLIC train.seed (reproducible
     # across runs and rank counts) instead of a per-run secret - voids the DP guarantee
     deterministic_noise: bool = False

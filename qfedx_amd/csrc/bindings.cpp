@@ -92,7 +92,8 @@ int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned
                       const float* correct, const float* nvalid, const float* act, int n_metrics, long long* sat,
                       const uint32_t* sa_seeds, const int* sa_sign, const int* sa_round, int sa_n, double sa_scale,
                       int sa_bits, long long* sa_masks, const int* norm_cid, float* fa_theta, double* fa_out,
-                      unsigned* fa_cnt, int fa_bits, double fa_ring_scale, int fa_n_norms, hipStream_t st);
+                      unsigned* fa_cnt, int fa_bits, double fa_ring_scale, int fa_n_norms, const float* dp_scale,
+                      hipStream_t st);
 }
 
 namespace qfx_runtime {
@@ -446,7 +447,8 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
             c10::optional<torch::Tensor> sa_sign, c10::optional<torch::Tensor> sa_round, double sa_scale,
             int64_t sa_bits, c10::optional<torch::Tensor> sa_masks, c10::optional<torch::Tensor> norm_cid,
             c10::optional<torch::Tensor> fa_theta, c10::optional<torch::Tensor> fa_out,
-            c10::optional<torch::Tensor> fa_cnt, int64_t fa_bits, double fa_scale, int64_t fa_n_norms) {
+            c10::optional<torch::Tensor> fa_cnt, int64_t fa_bits, double fa_scale, int64_t fa_n_norms,
+            c10::optional<torch::Tensor> dp_scale) {
   need(theta_k, torch::kFloat32, "theta_k");
   need(sat, torch::kInt64, "sat");
   if (sat.numel() < 1) throw std::invalid_argument("fedavg: sat counter missing");
@@ -493,6 +495,12 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
     need(*norm_cid, torch::kInt32, "norm_cid");
     if (!pack || !dp || norm_cid->numel() < K) throw std::invalid_argument("fedavg: norm slots need pack + DP + [K] ids");
   }
+  // distributed DP: per-client noise scale [K] float32 (the round's 1 / sqrt(live participants))
+  const bool ds = dp_scale.has_value() && dp_scale->defined() && dp_scale->numel() > 0;
+  if (ds) {
+    need(*dp_scale, torch::kFloat32, "dp_scale");
+    if (!dp || dp_scale->numel() < K) throw std::invalid_argument("fedavg: dp_scale needs DP and [K] entries");
+  }
   // single-rank round: the launch's last block also applies the round (round_apply's work) to fa_theta [P], writing
   // the [6 + n_norms] outputs to fa_out; fa_cnt is an int32 [1] zeroed arrival counter (self-resetting)
   const bool fa = fa_theta.has_value() && fa_theta->defined();
@@ -516,7 +524,7 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
                           sa ? ptr<long long>(*sa_masks) : nullptr, nc ? ptr<int>(*norm_cid) : nullptr,
                           fa ? ptr<float>(*fa_theta) : nullptr, fa ? ptr<double>(*fa_out) : nullptr,
                           fa ? ptr<unsigned>(*fa_cnt) : nullptr, (int)fa_bits, fa_scale, (int)fa_n_norms,
-                          cur_stream()),
+                          ds ? ptr<float>(*dp_scale) : nullptr, cur_stream()),
         "qfx_fedavg");
 }
 

@@ -1305,10 +1305,11 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
 //   d/dtheta = Im(e^{-i phi} n10 + e^{i phi} n01),   d/dphi = Im(n00 - n11).
 //
 // Optional Adam epilogue (ad.m != nullptr; the local optimizer step fused into this launch): the last of a client's
-// n_gradops blocks to finish - arrival counter ad.cnt[k], reset by that block - updates the client's parameter row
-// from the complete gradient row (the readout-parameter entries were written by the readout launch before), with
-// the element update of qfx_adam_kernel (qfx_adam.h): bitwise the separate launch.  Every block has read its
-// parameters before it arrives.
+// gridDim.y blocks to finish - arrival counter ad.cnt[k], reset by that block - updates the client's parameter row
+// from the complete gradient row, with the element update of qfx_adam_kernel (qfx_adam.h): bitwise the separate
+// launch.  The arrivals are the n_gradops gradient-record blocks PLUS, with the fused readout, the g == n_gradops
+// block that writes the readout-parameter gradients: the Adam step must wait for all gridDim.y = n_gradops + 1 of
+// them (the launcher sizes the grid so).  Every block has read its parameters before it arrives.
 #if !QFX_HEA_BF16
 __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* __restrict__ gslab, int slab_tiles,
                                                               int n_gradops, const int* __restrict__ gmeta, int spc,
@@ -1403,6 +1404,11 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   }
   __syncthreads();
   if (!last_s) return;
+  if (tid == 0) {                                     // consumer side: one agent-scope acquire, drained
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
   for (int i = tid; i < p_stride; i += 256) {
     const long e = (long)k * p_stride + i;
     // device-coherent load: other blocks (other CUs) wrote these entries

@@ -413,8 +413,8 @@ __device__ __forceinline__ long long secagg_masks(const SecAgg& sa, int k, long 
 // sample-count weights times a diverged CNN delta) is clamped and counted in *nsat instead of wrapping in llrint.
 constexpr double FA_SAT = 9007199254740992.0;
 __device__ __forceinline__ long long fedavg_term(float x, double tg, bool wr, int k, long e, const double* weights,
-                                                 const double* norms, const uint32_t* keys, int dp, float clip,
-                                                 float sigma, int& nsat, const SecAgg& sa, int sa_P) {
+                                                 const double* norms, const uint32_t* keys, const float* dps, int dp,
+                                                 float clip, float sigma, int& nsat, const SecAgg& sa, int sa_P) {
   const double SC = 4294967296.0;
   double d = (double)x - tg;
   if (wr) d = wrap_pi(d);
@@ -422,8 +422,10 @@ __device__ __forceinline__ long long fedavg_term(float x, double tg, bool wr, in
     const double n = norms[k];
     const double sc = fmin(1.0, (double)clip / fmax(n, 1e-12));
     d = d * sc;
+    // dps: per-client noise scale of the round (distributed DP: 1 / sqrt(live participants)), else 1
     if (sigma > 0.f)
-      d += (double)sigma * (double)clip * (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
+      d += (double)sigma * (dps ? (double)dps[k] : 1.0) * (double)clip *
+           (double)philox_normal_at((uint64_t)e, keys[2 * k], keys[2 * k + 1], 0u);
   }
   if (sa.seeds) {                      // SecAgg ring element: held to +-2^(bits - 1) before it wraps
     double v = weights[k] * d * sa.scale;
@@ -515,6 +517,13 @@ __device__ __forceinline__ void fused_apply_tail(const FusedApply& fa, long long
   }
   __syncthreads();
   if (!last_s) return;
+  // consumer side of the hand-off (every other block released its entries before its arrival): one agent-scope
+  // acquire, drained, before any thread of the last block reads them (HIP / AMDGPU memory model)
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
   auto ld = [buf](long i) { return __hip_atomic_load(&buf[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   const double wsum = params_done ? (double)ws / 4294967296.0
                                   : (fa.bits ? ring_decode(ld(P), fa.bits, fa.ring_scale) : (double)ld(P) / 4294967296.0);
@@ -552,8 +561,8 @@ __device__ __forceinline__ long long weight_sum_wave(const double* __restrict__ 
 __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
     const float* __restrict__ theta_k, const float* theta_g,     // theta_g may be fa.theta (applied in place)
     const unsigned char* __restrict__ angle_mask, const double* __restrict__ weights,
-    const double* __restrict__ norms, const uint32_t* __restrict__ keys, int K, int P, int wrap,
-    int dp, float clip, float sigma, long long* __restrict__ out, RoundPack rp, long long* __restrict__ sat,
+    const double* __restrict__ norms, const uint32_t* __restrict__ keys, const float* __restrict__ dps, int K, int P,
+    int wrap, int dp, float clip, float sigma, long long* __restrict__ out, RoundPack rp, long long* __restrict__ sat,
     SecAgg sa, FusedApply fa) {
   const bool own_apply = fa.theta && !sa.seeds;       // every parameter block applies its own entries (FusedApply)
   __shared__ long long ws_s;
@@ -603,10 +612,11 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
       for (int u = 0; u < FA_U; ++u) x[u] = theta_k[(size_t)(k + u * FA_G) * P + e];
 #pragma unroll
       for (int u = 0; u < FA_U; ++u)
-        acc += fedavg_term(x[u], tg, wr, k + u * FA_G, e, weights, norms, keys, dp, clip, sigma, nsat, sa, P);
+        acc += fedavg_term(x[u], tg, wr, k + u * FA_G, e, weights, norms, keys, dps, dp, clip, sigma, nsat, sa, P);
     }
     for (; k < K; k += FA_G)
-      acc += fedavg_term(theta_k[(size_t)k * P + e], tg, wr, k, e, weights, norms, keys, dp, clip, sigma, nsat, sa, P);
+      acc += fedavg_term(theta_k[(size_t)k * P + e], tg, wr, k, e, weights, norms, keys, dps, dp, clip, sigma, nsat, sa,
+                         P);
   }
   // saturated terms are counted (an integer: the count is exact in any order); the host raises on a nonzero
   // count when it reads the round's metrics back (self-cleaning: round_apply zeroes it after the all-reduce)
@@ -965,7 +975,8 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                                  int n_metrics, long long* sat, const uint32_t* sa_seeds, const int* sa_sign,
                                  const int* sa_round, int sa_n, double sa_scale, int sa_bits, long long* sa_masks,
                                  const int* norm_cid, float* fa_theta, double* fa_out, unsigned* fa_cnt,
-                                 int fa_bits, double fa_ring_scale, int fa_n_norms, hipStream_t st) {
+                                 int fa_bits, double fa_ring_scale, int fa_n_norms, const float* dp_scale,
+                                 hipStream_t st) {
   if (dp) {   // clipping needs the per-client norms; without DP they are not computed
     const int nc = (P + NORM_CHUNK - 1) / NORM_CHUNK;
     double* partial = norms + K;   // scratch tail of the norms buffer: K * nc doubles
@@ -990,6 +1001,7 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
     return (int)hipErrorInvalidValue;
   const FusedApply fa{fa_theta, fa_out, fa_cnt, fa_bits, fa_n_norms, fa_ring_scale, 1.0};
   hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3(blocks), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
-                     angle_mask, weights, norms, keys, K, P, wrap, dp, clip, sigma, out, rp, sat, sa, fa);
+                     angle_mask, weights, norms, keys, dp ? dp_scale : nullptr, K, P, wrap, dp, clip, sigma, out, rp,
+                     sat, sa, fa);
   return (int)hipGetLastError();
 }

@@ -50,6 +50,13 @@ def federated_averaging(client_updates):
     return out
 
 
+def _scale_table(dp_scale, K: int, device):
+    """The HIP reduce's per-client noise-scale table: None (local DP), a device table as given, or a float broadcast."""
+    if dp_scale is None or torch.is_tensor(dp_scale):
+        return dp_scale
+    return torch.full((K,), float(dp_scale), dtype=torch.float32, device=device)
+
+
 class Aggregator:
     def __init__(self, n_params: int, angle_mask: Optional[torch.Tensor], device, backend: str = "torch",
                  aggregate: str = "delta", wrap: bool = True, dp: bool = False, clip_norm: float = 1.0,
@@ -77,7 +84,7 @@ class Aggregator:
                      dropped: Optional[list] = None, out: Optional[torch.Tensor] = None,
                      keys: Optional[torch.Tensor] = None, pack: Optional[tuple] = None,
                      secagg_tabs: Optional[tuple] = None, norm_cid: Optional[torch.Tensor] = None,
-                     apply: Optional[tuple] = None) -> torch.Tensor:
+                     apply: Optional[tuple] = None, dp_scale=None) -> torch.Tensor:
         """This rank's contribution [P+1] = [sum_k w_k priv(Delta_k) | sum_k w_k].
 
         float64 normally; int64 ring elements (mod 2^bits, masked) under secure aggregation.
@@ -86,7 +93,8 @@ class Aggregator:
         ``pack`` (HIP fast path only): (buf, loss, correct, nvalid, act) - the same launch also packs the round
         metrics into the tail of the all-reduce buffer ``buf`` whose head is ``out``.  ``apply`` (with ``pack``,
         single-rank rounds): the same launch also applies the round to the global params
-        (``fedavg_hip.fused_local_reduce``).
+        (``fedavg_hip.fused_local_reduce``).  ``dp_scale``: the round's per-client noise factor
+        (``privacy.dp.noise_scale``; distributed DP) - a float, or a device float32 [K] table on the HIP path.
         """
         if self.backend == "hip":
             from ..ops import fedavg_hip
@@ -108,7 +116,7 @@ class Aggregator:
                 theta_k, theta_g, weights, self._mask_u8, client_ids, round_num, self.seed,
                 wrap=self.wrap, dp=self.dp, clip_norm=self.clip_norm,
                 noise_multiplier=self.noise_multiplier, out=out, keys=keys, pack=pack, secagg=sa,
-                norm_cid=norm_cid, apply=apply)
+                norm_cid=norm_cid, apply=apply, dp_scale=_scale_table(dp_scale, len(client_ids), self.device))
             self.last_norms = norms
             self.last_saturation = sat
             return out
@@ -118,8 +126,9 @@ class Aggregator:
         if self.wrap:
             delta = torch.where(self.angle_mask[None, :], wrap_angles(delta), delta)
         if self.dp:
+            sk = 1.0 if dp_scale is None else float(dp_scale if not torch.is_tensor(dp_scale) else dp_scale.reshape(-1)[0])
             delta, norms = clip_and_noise(delta, self.clip_norm, self.noise_multiplier, self.seed,
-                                          round_num, client_ids)
+                                          round_num, client_ids, scale_k=sk)
             self.last_norms = norms
         else:
             self.last_norms = delta.norm(dim=-1)
@@ -136,6 +145,7 @@ class Aggregator:
             return torch.round(v).to(torch.int64).sum(0)
         sa = self.secagg
         parts = list(participants if participants is not None else client_ids)
+        sa._require_ok(parts, dropped or [], round_num)        # no survivor may be left without live mask neighbours
         total = torch.zeros(self.P + 1, dtype=torch.int64, device=delta.device)
         for k, cid in enumerate(client_ids):
             total = torch.remainder(total + sa.mask(weighted[k], int(cid), parts, round_num), sa.modulus)

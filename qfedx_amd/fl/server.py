@@ -27,7 +27,7 @@ import torch
 from ..parallel.dist import (ShardedServerState, World, agree_graph_comm, all_gather_cat, all_reduce_, barrier,
                              broadcast_, shard_clients)
 from ..privacy.accountant import RDPAccountant
-from ..privacy.dp import draw_noise_seed
+from ..privacy.dp import noise_scale, draw_noise_seed
 from ..privacy.secure_agg import SecureAggregator
 from ..utils.device import h2d
 from ..utils.checkpoint import latest_checkpoint, load_checkpoint, save_checkpoint
@@ -94,11 +94,17 @@ class FederatedRunner:
         if sampling not in ("fixed", "poisson"):
             raise ValueError(f"train.sampling must be auto | fixed | poisson, got {t.sampling!r}")
         self.poisson = sampling == "poisson"
+        noise_scale(getattr(p, "noise_mode", "local"), 1)           # validates privacy.noise_mode
+        if p.dp and getattr(p, "noise_mode", "local") == "distributed" and not p.secure_agg:
+            # each client's share of the noise is too small to protect its update on its own: only the SecAgg sum
+            # (which the server sees instead of the shares) carries the accounted sigma C
+            raise ValueError("privacy.noise_mode=distributed needs privacy.secure_agg=true")
         self.secagg = None
         if p.secure_agg:
             # each client's DH secret comes from OS randomness on the rank hosting it; only public keys
             # are exchanged (all-gather), so no process holds another rank's client secrets
-            self.secagg = SecureAggregator(None, p.secagg_bits, p.secagg_scale, getattr(p, "secagg_graph", "full"))
+            self.secagg = SecureAggregator(None, p.secagg_bits, p.secagg_scale, getattr(p, "secagg_graph", "full"),
+                                           getattr(p, "secagg_min_live", 0))
             self.secagg.setup(self.local_ids, world)
         self.aggregator = Aggregator(self.P, adapter.angle_mask(), device, backend, t.aggregate,
                                      t.wrap_angles, p.dp, p.clip_norm, p.noise_multiplier, p.secure_agg,
@@ -218,6 +224,14 @@ class FederatedRunner:
         participants = sample_participants(self.num_clients, t.client_fraction,
                                            self.noise_seed if p.dp else t.seed, r, self.poisson)
         dropped = sample_dropouts(participants, t.dropout_prob, t.seed, r)
+        # SecAgg+ abort (Bell et al.): a survivor left with fewer than the threshold of live mask neighbours would be
+        # unmasked by the orphan-mask removal, so the round aggregates nothing.  The decision uses public data only
+        # (participants, dropouts, the round-keyed graph): every rank takes it alike and still posts its (zero)
+        # contribution to the one collective.
+        sa_abort = bool(p.secure_agg and self.secagg is not None and participants
+                        and not self.secagg.round_ok(participants, dropped, r))
+        if sa_abort:
+            dropped = list(participants)
         dropped_set = set(dropped)
         part_set = set(participants)
         local_part = [i for i, c in enumerate(self.local_ids) if c in part_set]
@@ -226,6 +240,10 @@ class FederatedRunner:
         dev = self.device
         P = self.P
         ids = [self.local_ids[i] for i in local_alive]
+        # distributed DP: each client's share of the noise is N(0, sigma^2 C^2 / m) for the round's m live participants
+        # (public: every rank knows the participant set and the dropouts), so the SecAgg sum carries exactly sigma C
+        dp_mode = getattr(p, "noise_mode", "local")
+        dp_scale = noise_scale(dp_mode, len(participants) - len(dropped)) if (p.dp and dp_mode != "local") else None
         fast = self.backend == "hip" and self.server_opt is None
         trainer = self.adapter.trainer
         if fast:
@@ -246,6 +264,8 @@ class FederatedRunner:
                 extra["dpkeys"] = dp_noise_keys(ids, r, self.noise_seed)
             if t.weighting == "uniform":
                 extra["fw"] = torch.ones(len(ids), dtype=torch.float64)
+            if dp_scale is not None and ids:
+                extra["dpscale"] = torch.full((len(ids),), dp_scale, dtype=torch.float32)
             if p.secure_agg and ids:
                 # SecAgg on the device: every local client's pair-seed keys and mask signs for this round ride with
                 # the round's tables; the fused reduce masks each client's ring element (K18), so the round stays
@@ -293,7 +313,8 @@ class FederatedRunner:
                 agg.local_reduce(params_k, theta, tabs.get("fw", tabs["w"]), r, ids, out=buf[: P + 1],
                                  keys=tabs.get("dpkeys"), secagg_tabs=sa, norm_cid=tabs.get("cid"),
                                  pack=(buf, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
-                                       tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)), apply=apply)
+                                       tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)), apply=apply,
+                                 dp_scale=tabs.get("dpscale"))
             graph_comm = self.graph_comm
             with self.timer.phase("local_train"):
                 res = trainer.run_round(self.store, local_alive, self.params, r, epilogue=epilogue,
@@ -314,7 +335,8 @@ class FederatedRunner:
                     w = self._counts_dev[res["lid"]]
                 if local_alive:
                     contrib = self.aggregator.local_reduce(res["params"], self.params, w, r, ids,
-                                                           participants=participants, dropped=dropped)
+                                                           participants=participants, dropped=dropped,
+                                                           dp_scale=dp_scale)
                 else:
                     contrib = torch.zeros(P + 1, dtype=torch.int64, device=dev)
                 loss_sum = (res["loss"].double() * res["nvalid"].double()).sum()
@@ -378,7 +400,7 @@ class FederatedRunner:
             # drawn without replacement is accounted conservatively with no amplification (q = 1)
             q = min(1.0, t.client_fraction) if self.poisson else 1.0
             self.accountant.step(q, p.noise_multiplier, 1)
-        rec = {"round": r + 1, "participants": len(participants), "dropped": len(dropped),
+        rec = {"round": r + 1, "participants": len(participants), "dropped": len(dropped), "secagg_aborted": sa_abort,
                "_metrics": metrics, "_t0": t0,
                "_out_stamp": (v, self._out_writes[v]) if fast else None,
                "_norms": (norms, [c for c in participants if c not in dropped_set]) if norms is not None else None,

@@ -30,7 +30,7 @@ def dp_noise_keys(client_ids, round_num, seed) -> torch.Tensor:
 
 def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_num, seed, wrap, dp, clip_norm,
                        noise_multiplier, out=None, keys=None, pack=None, sat=None, secagg=None, norm_cid=None,
-                       apply=None):
+                       apply=None, dp_scale=None):
     """[sum_k w_k priv(wrap(theta_k - theta_g)) | sum_k w_k] as exact int64 fixed point (scale 2^32)
     [P+1] (per-client terms rounded before the sum -> rank-count invariant), plus norms [K].
     ``angle_mask`` uint8 [P] on the device; ``out`` an optional int64 [P+1] destination (e.g. the head
@@ -47,7 +47,8 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
     DP): the pack block scatters the clients' pre-clip norms into ``buf[P + 6 + id]`` (CC6).
     ``apply`` = (theta [P] float32, outs float64 [6 + n_norms], counter int32 [1] zeroed, bits, ring scale,
     n_norms): single-rank rounds (no collective between reduce and apply) - the launch's last block also does
-    ``round_apply``'s work (needs ``pack``).
+    ``round_apply``'s work (needs ``pack``).  ``dp_scale`` (device float32 [K], DP only): per-client factor on the
+    noise std (distributed DP: 1 / sqrt(live participants), uploaded with the round's tables).
     Returns (out, norms, sat)."""
     K, P = theta_k.shape
     dev = theta_k.device
@@ -78,5 +79,6 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
                  *((secagg[0].contiguous(), secagg[1].contiguous(), secagg[2].contiguous(), float(secagg[3]),
                     int(secagg[4]), torch.empty(K * (P + 1), dtype=torch.int64, device=dev))
                    if secagg is not None else (None, None, None, 1.0, 48, None)),
-                 norm_cid, *(apply if apply is not None else (None, None, None, 0, 1.0, 0)))
+                 norm_cid, *(apply if apply is not None else (None, None, None, 0, 1.0, 0)),
+                 dp_scale.float().contiguous() if (dp and dp_scale is not None) else None)
     return out, (norms[:K] if dp else None), sat

@@ -25,7 +25,7 @@ from __future__ import annotations
 import datetime
 import os
 from dataclasses import dataclass
-from typing import Optional
+from typing import Callable, Optional
 
 import torch
 import torch.distributed as dist
@@ -66,6 +66,16 @@ def init_distributed(device: torch.device, backend: str = "auto", timeout_s: int
         backend = "nccl" if device.type == "cuda" else "gloo"
     if backend == "nccl" and device.type != "cuda":
         raise ValueError("dist_backend=nccl (RCCL) needs a GPU device")
+    if backend == "nccl":
+        # RCCL runs one rank per GPU: more local ranks than visible GPUs would put two ranks on one device (the
+        # device map takes LOCAL_RANK modulo the count) and fail deep inside communicator setup.  device_count()
+        # does not initialise the GPU.
+        ngpu = torch.cuda.device_count()
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
+        if local >= ngpu or lws > ngpu:
+            raise RuntimeError(f"dist_backend=nccl (RCCL) needs one GPU per rank: LOCAL_RANK={local} of "
+                               f"{lws} local ranks, but {ngpu} GPU(s) visible; launch at most {ngpu} ranks per node "
+                               "or use dist_backend=gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if "MASTER_PORT" not in os.environ:
         if ws > 1:
@@ -246,7 +256,7 @@ class ShardedServerState:
             self.v = shard(sd["v"])
 
 
-def graph_allreduce_selfcheck(world: World) -> bool:
+def graph_allreduce_selfcheck(world: World) -> Optional[Callable[[], bool]]:
     """This rank's half of the captured-collective self-check: capture ONE all-reduce of a rank-dependent int64
     buffer into a hipGraph.  Returns a callable that replays it and compares the result bitwise with an eager
     all-reduce of the same buffer, or None when capture failed here.  The replay may only run once every rank has
@@ -302,4 +312,9 @@ def agree_graph_comm(world: World, want: bool, probe=graph_allreduce_selfcheck) 
     replay = probe(world)
     if not _vote(replay is not None, world):
         return False
-    return _vote(bool(replay()), world)
+    # a replay that raises on one rank must still reach the second vote, or the other ranks block in it forever
+    try:
+        ok = bool(replay())
+    except Exception:                       # noqa: BLE001 - any failure means: do not capture the collective
+        ok = False
+    return _vote(ok, world)

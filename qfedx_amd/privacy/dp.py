@@ -44,13 +44,28 @@ def dp_noise(P: int, seed: int, round_num: int, client: int, device="cpu") -> to
     return philox_normal(P, key).to(device)
 
 
+def noise_scale(mode: str, live: int) -> float:
+    """Per-client factor on the noise std sigma C.  ``local`` (ROADMAP.md:50-51): 1 - every client adds the full
+    N(0, sigma^2 C^2), so a sum of m clients carries sigma C sqrt(m).  ``distributed``: 1 / sqrt(m) for the round's m
+    live participants - the (SecAgg-hidden) sum carries exactly the N(0, sigma^2 C^2) the accountant charges for
+    sensitivity C, while no single share is private on its own."""
+    if mode == "local":
+        return 1.0
+    if mode == "distributed":
+        return 1.0 / float(max(1, live)) ** 0.5
+    raise ValueError(f"privacy.noise_mode must be local | distributed, got {mode!r}")
+
+
 def clip_and_noise(deltas: torch.Tensor, clip_norm: float, noise_multiplier: float, seed: int,
-                   round_num: int, client_ids, add_noise: bool = True) -> tuple[torch.Tensor, torch.Tensor]:
-    """Torch reference of the fused DP step.  Returns (privatised deltas [K,P], pre-clip norms [K])."""
+                   round_num: int, client_ids, add_noise: bool = True,
+                   scale_k: float = 1.0) -> tuple[torch.Tensor, torch.Tensor]:
+    """Torch reference of the fused DP step (``scale_k``: ``noise_scale`` of the round).  Returns (privatised
+    deltas [K,P], pre-clip norms [K])."""
     scale, norms = clip_factors(deltas, clip_norm)
     out = deltas * scale[:, None]
     if add_noise and noise_multiplier > 0:
-        std = noise_multiplier * clip_norm
+        # the same float32 factor the device kernel multiplies by (sigma x dps[k] x C)
+        std = float(noise_multiplier) * float(torch.tensor(scale_k, dtype=torch.float32)) * clip_norm
         noise = torch.stack([dp_noise(deltas.shape[1], seed, round_num, int(c), deltas.device)
                              for c in client_ids])
         out = out + std * noise.to(out.dtype)

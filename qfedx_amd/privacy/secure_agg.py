@@ -21,6 +21,11 @@ Protocol (Bonawitz et al. style, single round, honest-but-curious server):
     masks of dropped clients are removed the same way (only their graph neighbours reveal seeds).  The guarantee is
     SecAgg+'s: the sum stays hidden unless the server corrupts or drops enough of a client's neighbourhood, a weaker
     statement than the complete graph's.
+  * live-neighbour threshold: a surviving participant whose mask neighbours all dropped would send its ring element
+    with no mask left in it (after the orphan masks are removed the server holds that client's update).  Every
+    surviving participant must therefore keep at least ``min_live`` live neighbours (default: half its degree on the
+    sparse graph, as SecAgg+ requires; one on the complete graph); otherwise the round is aborted (``SecAggAbort``)
+    - ``round_tables`` and ``aggregate`` refuse it, and the server skips the round's aggregation on every rank.
 
 PRG = Philox4x32-10 keyed by the pair seed, counter = (element/4, round) - the same generator the
 HIP aggregation kernel uses on device: ``round_tables`` gives the fused FedAvg kernel
@@ -40,6 +45,10 @@ import torch
 from ..utils.seeding import MASK32, derive_seed, np_rng, philox4x32
 
 GRAPH_KEY = 0x5EC6A   # the neighbour graph is public (a server could announce it): keyed by round, not by a secret
+
+
+class SecAggAbort(ValueError):
+    """The round's surviving participants do not keep enough live mask neighbours: aggregating would unmask one."""
 
 
 def secagg_degree(k: int) -> int:
@@ -138,7 +147,7 @@ def decode_fixed(v: torch.Tensor, scale: float, bits: int = 48) -> torch.Tensor:
 
 class SecureAggregator:
     def __init__(self, session_seed: Optional[int] = None, bits: int = 48, scale: float = 2.0 ** 24,
-                 graph: str = "full"):
+                 graph: str = "full", min_live: int = 0):
         if graph not in ("full", "sparse"):
             raise ValueError(f"secagg graph must be full | sparse, got {graph!r}")
         self.registry = KeyRegistry(session_seed)
@@ -146,7 +155,44 @@ class SecureAggregator:
         self.scale = scale
         self.modulus = 1 << bits
         self.graph = graph
+        self.min_live = int(min_live)
         self._nb = (None, None)
+
+    def live_threshold(self, num_participants: int) -> int:
+        """Live mask neighbours every surviving participant must keep (``min_live``, or auto: half the sparse
+        graph's degree, rounded up, as SecAgg+ requires; one on the complete graph)."""
+        if self.min_live > 0:
+            return self.min_live
+        if self.graph == "sparse" and secagg_degree(num_participants) < num_participants - 1:
+            return max(1, (secagg_degree(num_participants) + 1) // 2)
+        return 1
+
+    def live_counts(self, participants: Iterable[int], dropped: Iterable[int], round_num: int) -> dict:
+        """survivor -> number of its mask neighbours that survived the round."""
+        parts = sorted({int(c) for c in participants})
+        gone = {int(d) for d in dropped}
+        surv = [c for c in parts if c not in gone]
+        if self.graph == "full" or secagg_degree(len(parts)) >= len(parts) - 1:
+            return {c: len(surv) - 1 for c in surv}           # complete graph: every other survivor
+        nb = self._neighbor_map(tuple(parts), round_num)
+        return {c: sum(1 for j in nb[c] if j not in gone) for c in surv}
+
+    def round_ok(self, participants: Iterable[int], dropped: Iterable[int], round_num: int) -> bool:
+        """Every surviving participant keeps at least ``live_threshold`` live neighbours (public information: the
+        participant set, the dropouts and the round-keyed graph, so every rank decides alike)."""
+        parts = sorted({int(c) for c in participants})
+        cnt = self.live_counts(parts, dropped, round_num)
+        t = self.live_threshold(len(parts))
+        return all(v >= t for v in cnt.values())
+
+    def _require_ok(self, participants, dropped, round_num) -> None:
+        if not self.round_ok(participants, dropped, round_num):
+            parts = sorted({int(c) for c in participants})
+            cnt = self.live_counts(parts, dropped, round_num)
+            t = self.live_threshold(len(parts))
+            low = sorted(c for c, v in cnt.items() if v < t)
+            raise SecAggAbort(f"round {round_num}: survivors {low[:8]} keep fewer than {t} live mask neighbours; "
+                              "aggregating would expose their updates")
 
     def neighbors(self, client: int, participants: Iterable[int], round_num: int) -> list[int]:
         """The peers ``client`` shares pair masks with this round (sorted).  Full graph: every other participant.
@@ -231,6 +277,7 @@ class SecureAggregator:
         non-participants.  Sparse graph: row i lists its live neighbours (sign 0 pads).  A dropped peer d's orphan
         mask is removed by the correction the survivors enable (``aggregate``); that exactly cancels the survivor's
         mask toward d mod 2^bits, so its sign is 0 (net)."""
+        self._require_ok(participants, dropped, round_num)
         if self.graph == "sparse":
             return self._sparse_tables(clients, participants, dropped, num_clients, round_num)
         K = len(clients)
@@ -296,7 +343,9 @@ class SecureAggregator:
 
     def aggregate(self, masked: list[torch.Tensor], survivors: list[int], dropped: Optional[list[int]] = None,
                   round_num: int = 0) -> torch.Tensor:
-        """Sum surviving masked vectors; remove orphan masks of ``dropped`` clients; decode."""
+        """Sum surviving masked vectors; remove orphan masks of ``dropped`` clients; decode.  Refuses a round in
+        which a survivor kept fewer than ``live_threshold`` live neighbours (``SecAggAbort``)."""
+        self._require_ok(list(survivors) + list(dropped or []), dropped or [], round_num)
         total = torch.zeros_like(masked[0])
         for m in masked:
             total = torch.remainder(total + m, self.modulus)

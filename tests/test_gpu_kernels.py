@@ -554,3 +554,47 @@ def test_fused_adam_in_grad_reduce_bitwise(cuda):
     assert torch.equal(pa, pb) and torch.equal(ma, mb) and torch.equal(va, vb) and torch.equal(ta, tb)
     assert ta.tolist() == [2, 1, 3, 3, 1]
     assert not torch.equal(pa[0], p0[0]) and torch.equal(pa[1], pb[1])
+
+
+def test_secagg_sparse_federated_hip_run_matches_plain(cuda):
+    """the end-to-end sparse (SecAgg+) path on the HIP round graph - server round_tables -> device mask
+    kernel -> fused reduce with the single-rank FusedApply - with 20 clients (a true circulant graph: degree 10 < 19)
+    and dropouts decodes to the plain HIP aggregate; a round whose dropouts would isolate a survivor is aborted."""
+    from tests.test_fl import small_cfg
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.parallel.dist import init_distributed
+    from qfedx_amd.privacy.secure_agg import SecureAggregator
+    assert len(SecureAggregator(0, graph="sparse").neighbors(0, range(20), 0)) < 19
+    dev = torch.device("cuda", 0)
+    kw = dict(num_rounds=1, n_qubits=6, num_clients=20, samples_per_client=16, dropout_prob=0.2, device="cuda",
+              backend="hip")
+    plain = run_experiment(small_cfg(**kw), world=init_distributed(dev), device=dev, backend="hip")
+    sec = run_experiment(small_cfg(secure_agg=True, secagg_graph="sparse", **kw), world=init_distributed(dev),
+                         device=dev, backend="hip")
+    assert sec["history"][0]["dropped"] > 0 and not sec["history"][0]["secagg_aborted"]
+    assert torch.allclose(plain["params"].cpu(), sec["params"].cpu(), atol=1e-5)
+
+
+@pytest.mark.parametrize("scale", [None, 0.25])
+def test_fused_reduce_dp_noise_scale_matches_host(cuda, scale):
+    """Distributed DP on the device: the fused reduce multiplies each client's noise std by its dp_scale entry
+    (uploaded per round); the decoded update matches the torch reference clip_and_noise(scale_k) to fixed point."""
+    from qfedx_amd.fl.aggregator import Aggregator
+    K, P = 6, 513
+    g = torch.Generator().manual_seed(3)
+    tk = torch.randn(K, P, generator=g) * 0.3
+    tg = torch.randn(P, generator=g)
+    w = torch.ones(K, dtype=torch.float64)
+    ids = [0, 3, 4, 7, 9, 12]
+    kw = dict(dp=True, clip_norm=0.8, noise_multiplier=1.3, seed=21)
+    cpu = Aggregator(P, torch.zeros(P), "cpu", "torch", wrap=False, **kw)
+    gpu = Aggregator(P, torch.zeros(P), cuda, "hip", wrap=False, **kw)
+    a = cpu.local_reduce(tk, tg, w, 2, ids, dp_scale=scale)
+    tab = None if scale is None else torch.full((K,), scale, dtype=torch.float32, device=cuda)
+    b = gpu.local_reduce(tk.to(cuda), tg.to(cuda), w.to(cuda), 2, ids, dp_scale=tab)
+    ma, _ = cpu.finalize(a)
+    mb, _ = gpu.finalize(b.cpu())
+    assert torch.allclose(ma, mb, atol=1e-6)
+    if scale is not None:                       # and it is not the unscaled noise
+        full = gpu.finalize(gpu.local_reduce(tk.to(cuda), tg.to(cuda), w.to(cuda), 2, ids).cpu())[0]
+        assert not torch.allclose(full, mb, atol=1e-3)

@@ -249,10 +249,108 @@ def test_secagg_sparse_round_tables_reproduce_host_masks():
 
 
 def test_secagg_sparse_federated_run_matches_plain():
-    """A federated round with the sparse mask graph (and dropouts) decodes to the plain aggregate."""
+    """A federated round with the sparse mask graph (20 clients: a true circulant graph, degree 10 < 19) and dropouts
+    decodes to the plain aggregate (one round: across rounds the clients' Adam steps amplify the 2^-24 ring
+    quantisation on parameters whose gradient is ~0, so later rounds are not comparable to 1e-5)."""
     from qfedx_amd.api import run_experiment
+    from qfedx_amd.privacy.secure_agg import SecureAggregator
     from tests.test_fl import small_cfg
-    kw = dict(num_rounds=1, num_clients=9, dropout_prob=0.3)
+    sa = SecureAggregator(0, graph="sparse")
+    assert all(len(sa.neighbors(c, range(20), 0)) < 19 for c in range(20))
+    kw = dict(num_rounds=1, num_clients=20, samples_per_client=16, dropout_prob=0.2)
     plain = run_experiment(small_cfg(**kw))
     sec = run_experiment(small_cfg(secure_agg=True, secagg_graph="sparse", **kw))
+    assert sum(h["dropped"] for h in sec["history"]) > 0
+    assert not any(h["secagg_aborted"] for h in sec["history"])
     assert torch.allclose(plain["params"], sec["params"], atol=1e-5)
+
+
+def _isolating_dropouts(sa, parts, r):
+    """Drop every sparse-graph neighbour of the first participant (which survives)."""
+    return sorted(sa.neighbors(parts[0], parts, r))
+
+
+def test_secagg_refuses_survivor_without_live_neighbours():
+    """a survivor all of whose mask neighbours dropped would send its ring element unmasked once the
+    orphan masks are removed.  round_tables / aggregate refuse the round (SecAggAbort); below the threshold too."""
+    from qfedx_amd.privacy.secure_agg import SecAggAbort, SecureAggregator, secagg_degree
+    N, r, P = 32, 3, 8
+    sa = SecureAggregator(11, graph="sparse")
+    parts = list(range(N))
+    iso = _isolating_dropouts(sa, parts, r)
+    assert 0 < len(iso) < N - 1
+    assert sa.live_counts(parts, iso, r)[parts[0]] == 0 and not sa.round_ok(parts, iso, r)
+    with pytest.raises(SecAggAbort):
+        sa.round_tables([parts[0]], parts, iso, N, r)
+    surv = [c for c in parts if c not in iso]
+    masked = [sa.mask(torch.randn(P), c, parts, r) for c in surv]
+    with pytest.raises(SecAggAbort):
+        sa.aggregate(masked, surv, iso, r)
+    # half the degree must stay live (SecAgg+ threshold); one neighbour short of it is refused as well
+    t = sa.live_threshold(N)
+    assert t == (secagg_degree(N) + 1) // 2
+    nb = sa.neighbors(parts[0], parts, r)
+    short = nb[: len(nb) - t + 1]
+    assert sa.live_counts(parts, short, r)[parts[0]] == t - 1 and not sa.round_ok(parts, short, r)
+    assert sa.round_ok(parts, nb[: len(nb) - t], r)
+    # complete graph: a lone survivor is refused, two are fine
+    full = SecureAggregator(11)
+    assert not full.round_ok([1, 2, 3], [2, 3], r) and full.round_ok([1, 2, 3], [3], r)
+
+
+def test_secagg_abort_skips_round_on_every_rank_path(monkeypatch):
+    """The server aborts a round whose dropouts isolate a survivor: nothing is aggregated (theta unchanged) and the
+    record says so; the next round proceeds."""
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.fl import server as srv
+    from qfedx_amd.privacy.secure_agg import SecureAggregator
+    from tests.test_fl import small_cfg
+    sa = SecureAggregator(0, graph="sparse")
+    real = srv.sample_dropouts
+
+    def drops(participants, prob, seed, r):
+        return _isolating_dropouts(sa, sorted(participants), r) if r == 0 else real(participants, prob, seed, r)
+
+    monkeypatch.setattr(srv, "sample_dropouts", drops)
+    kw = dict(num_rounds=2, num_clients=20, samples_per_client=16)
+    cfg = small_cfg(secure_agg=True, secagg_graph="sparse", **kw)
+    out0 = run_experiment(small_cfg(secure_agg=True, secagg_graph="sparse", **dict(kw, num_rounds=0)))
+    out = run_experiment(cfg)
+    h = out["history"]
+    assert h[0]["secagg_aborted"] and h[0]["dropped"] == h[0]["participants"]
+    assert not h[1]["secagg_aborted"]
+    one = run_experiment(small_cfg(secure_agg=True, secagg_graph="sparse", **dict(kw, num_rounds=1)))
+    assert torch.equal(one["params"], out0["params"])    # the aborted round left theta unchanged
+
+
+def test_distributed_dp_noise_scale_and_learning():
+    """Verdict r4 item 6: privacy.noise_mode=distributed - each client adds N(0, sigma^2 C^2 / m) for the round's m
+    live participants, so the SecAgg sum carries exactly the sigma C the accountant charges (local mode: sigma C
+    sqrt(m)).  A 20q-shaped DP config (64 -> 32 clients, half sampled, small circuit) learns over round 0 in
+    distributed mode; the mode needs SecAgg."""
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.privacy.dp import noise_scale
+    from tests.test_fl import small_cfg
+    assert noise_scale("local", 16) == 1.0 and noise_scale("distributed", 16) == 0.25
+    with pytest.raises(ValueError):
+        noise_scale("other", 4)
+    kw = dict(num_rounds=12, num_clients=32, samples_per_client=32, client_fraction=0.5, dp=True, noise_multiplier=1.0,
+              clip_norm=1.0, deterministic_noise=True, noise_mode="distributed", n_qubits=6, n_layers=2,
+              test_samples=256, batch_size=16, learning_rate=0.05, local_steps=1)
+    with pytest.raises(ValueError, match="secure_agg"):
+        run_experiment(small_cfg(**kw))
+    out = run_experiment(small_cfg(secure_agg=True, **kw))
+    acc = out["accuracies"]
+    assert acc[-1] > acc[0] + 0.05 and sum(acc[-3:]) > sum(acc[:3])
+    again = run_experiment(small_cfg(secure_agg=True, **kw))          # reproducible (deterministic noise)
+    assert torch.equal(again["params"], out["params"])
+
+
+def test_distributed_dp_sum_carries_accounted_noise():
+    """The aggregate noise of m clients' shares has std sigma C (distributed) vs sigma C sqrt(m) (local)."""
+    from qfedx_amd.privacy.dp import clip_and_noise, noise_scale
+    m, P = 16, 20000
+    d = torch.zeros(m, P, dtype=torch.float64)
+    for mode, want in (("local", m ** 0.5), ("distributed", 1.0)):
+        out, _ = clip_and_noise(d, 1.0, 1.0, 7, 0, list(range(m)), scale_k=noise_scale(mode, m))
+        assert abs(float(out.sum(0).std()) / want - 1.0) < 0.03
