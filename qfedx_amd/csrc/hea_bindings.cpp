@@ -109,9 +109,9 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   need(ops.dim() == 2 && ops.size(1) == 128 && ops.scalar_type() == torch::kInt32 && ops.is_cuda(),
        "ops must be int32 [nops, 128] on the device");
   a.nops = (int)ops.size(0);
-  need(a.nops <= 128, "at most 128 ops per pass program");
+  need(a.nops <= 32, "at most 32 ops per pass program");
   a.ops = dp<int>(ops, torch::kInt32, "ops", 0);
-  a.fidx = a.nops ? dp<int>(fidx, torch::kInt32, "fidx", a.nops) : nullptr;
+  a.fidx = a.nops ? dp<int>(fidx, torch::kInt32, "fidx", 2 * a.nops) : nullptr;
   need(a.in_rep >= 1 && (!adjoint || a.in_rep == 1) && K % a.in_rep == 0,
        "in_rep: forward only, parameter rows a multiple of it");
   const int64_t states = S << a.n;
@@ -158,31 +158,47 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
 // Validate a pass program once (host copy) when it is built: slot / gradient-slot ranges and op kinds.
 void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64_t n_theta, bool adjoint, int64_t t,
                    int64_t n_gradops) {
-  need(fidx.scalar_type() == torch::kInt32 && !fidx.is_cuda() && fidx.numel() == ops.size(0),
-       "fidx must be a host int32 [nops] tensor");
+  need(fidx.scalar_type() == torch::kInt32 && !fidx.is_cuda() && fidx.is_contiguous() && fidx.numel() == 2 * ops.size(0),
+       "fidx must be a host int32 [nops, 2] tensor");
   const int* fi = fidx.data_ptr<int>();
-  for (int64_t o = 0; o < ops.size(0); ++o) need(fi[o] >= -1 && fi[o] < 4 * n_slots, "fragment index out of range");
+  for (int64_t o = 0; o < 2 * ops.size(0); ++o) need(fi[o] >= -1 && fi[o] < 4 * n_slots, "fragment index out of range");
   need(ops.dim() == 2 && ops.size(1) == 128 && ops.scalar_type() == torch::kInt32 && !ops.is_cuda() &&
        ops.is_contiguous(), "ops must be a contiguous host int32 [nops, 128] tensor");
   const int* ow = ops.data_ptr<int>();
   int ngrad = 0;
-  // op codes (hea_plan.py): 1 APPLY, 5 GRAD_L1, 6 OBS, 7 READOUT, 8 BACK
-  for (int64_t o = 0; o < ops.size(0); ++o) ngrad += (ow[o * 128] == 5 || ow[o * 128] == 8);
+  // op codes (hea_plan.py): 1 APPLY, 2 APPLY2, 3 BACK2, 4 GRAD2 (chained pairs), 5 GRAD_L1, 6 OBS, 7 READOUT, 8 BACK
+  for (int64_t o = 0; o < ops.size(0); ++o) {
+    const int c = ow[o * 128];
+    ngrad += (c == 5 || c == 8) ? 1 : (c == 3 || c == 4) ? 2 : 0;
+  }
   need(ngrad <= 12, "at most 12 gradient ops per pass program");
-  need(ops.size(0) <= 128, "at most 128 ops per pass program");
+  need(ops.size(0) <= 32, "at most 32 ops per pass program");
   for (int64_t o = 0; o < ops.size(0); ++o) {
     const int* w = ow + o * 128;
     const int code = w[0];
-    need(code == 1 || code == 5 || code == 6 || code == 7 || code == 8, "unknown op code");
-    need(adjoint ? (code == 5 || code == 6 || code == 8) : (code == 1 || code == 7), "op kind not valid in this pass");
-    if (code == 1 || code == 8) need(w[1] >= 0 && w[1] < n_slots, "op names a missing unitary slot");
-    if (code == 1 || code == 5 || code == 8) {
-      need(w[2] >= 0 && w[2] <= 4, "group size out of range");
+    const bool pair = code >= 2 && code <= 4;
+    need(code >= 1 && code <= 8, "unknown op code");
+    need(adjoint ? (code >= 3 && code <= 6) || code == 8 : (code == 1 || code == 2 || code == 7),
+         "op kind not valid in this pass");
+    if (code == 1 || code == 2 || code == 3 || code == 8) need(w[1] >= 0 && w[1] < n_slots, "op names a missing unitary slot");
+    if (code == 2 || code == 3) need(w[102] >= 0 && w[102] < n_slots, "pair op names a missing unitary slot");
+    // fragment indices must be the op's own slots (the kernel DMAs them)
+    if (code == 1 || code == 2) need(fi[2 * o] == 4 * w[1], "fragment index / slot mismatch");
+    if (code == 3 || code == 8) need(fi[2 * o] == 4 * w[1] + 2, "fragment index / slot mismatch");
+    if (code == 2) need(fi[2 * o + 1] == 4 * w[102], "fragment index / slot mismatch");
+    if (code == 3) need(fi[2 * o + 1] == 4 * w[102] + 2, "fragment index / slot mismatch");
+    if (!pair) need(fi[2 * o + 1] == -1, "a single op has one fragment set");
+    if (code != 6 && code != 7) {
+      need(pair ? w[2] == 4 : (w[2] >= 0 && w[2] <= 4), "group size out of range");
       for (int j = 0; j < w[2]; ++j)
         need(w[12 + j] >= 0 && w[12 + j] < n_theta && w[16 + j] >= 0 && w[16 + j] < n_theta,
              "gradient slot out of range");
       for (int i = 20; i < 100; ++i) need(w[i] >= 0 && w[i] < (1 << t), "tile address out of range");
-      if (code != 1) need(w[100] >= 0 && w[100] < n_gradops, "gradient op index out of range");
+      if (pair)
+        for (int i = 104; i < 120; ++i) need(w[i] >= 0 && w[i] < (1 << t), "tile address out of range");
+      if (pair) need(t >= 11, "pair ops need tiles of >= 2^11 amplitudes");
+      if (code != 1 && code != 2) need(w[100] >= 0 && w[100] < n_gradops, "gradient op index out of range");
+      if (code == 3 || code == 4) need(w[101] >= 0 && w[101] < n_gradops, "gradient op index out of range");
     }
     if (code == 6 || code == 7) need(w[2] >= 1 && w[2] <= 8, "observable count out of range");
   }

@@ -63,11 +63,12 @@ __device__ unsigned int qfx_check_word = 0;
 namespace HEA_NS {
 
 constexpr int OPW = 128;
-// (codes 2, 3, 4 and 9 were measured-and-rejected variants: un-apply-only ops of a recomputed last pass, the
-// cross-only gradient op of the non-fused BACK form, the layer-1 product-state op; docs/ARCHITECTURE.md keeps the A/Bs)
-enum { OP_APPLY = 1, OP_GRAD_L1 = 5, OP_OBS = 6, OP_READOUT = 7, OP_BACK = 8 };
+// APPLY2 / BACK2 / GRAD2: chained pairs of two commuting 4-qubit groups X, Y of one layer (group_pair_*)
+enum { OP_APPLY = 1, OP_APPLY2 = 2, OP_BACK2 = 3, OP_GRAD2 = 4, OP_GRAD_L1 = 5, OP_OBS = 6, OP_READOUT = 7, OP_BACK = 8 };
 enum { W_CODE = 0, W_SLOT = 1, W_NREAL = 2, W_FLAGS = 3, W_RFULL = 4, W_RT = 8, W_TH = 12, W_PH = 16, W_OFF = 20,
-       W_BL = 36, W_BH = 68, W_GIDX = 100 };
+       W_BL = 36, W_BH = 68, W_GIDX = 100,
+       // pair records (hea_plan.pair_table): group Y's row masks in the W_RT words, its records / OFF table here
+       W_RFULL2 = 8, W_GIDX2 = 101, W_SLOT2 = 102, W_OFF2 = 104 };
 constexpr double FIX = 4294967296.0;   // 2^32: fixed point of the scaled gradient partial traces
 constexpr int F_BACK_PSI = 1;
 constexpr int F_BACK_TRANS = 2;   // OP_BACK (with F_BACK_PSI) in the transposed form: cross matrix at the op input
@@ -75,7 +76,7 @@ constexpr int TMAX = 14;
 constexpr int NT_FWD = 512;    // forward: 8 waves, 64 KB LDS -> 2 workgroups per CU
 constexpr int NT_ADJ = 1024;   // adjoint: 16 waves, 128 KB LDS (psi + lambda) -> 1 workgroup per CU
 constexpr int CMAX = 8;
-constexpr int MAXOPS = 128;    // ops per pass program (host-checked)
+constexpr int MAXOPS = 32;     // ops per pass program (host-checked)
 constexpr int MAXGRAD = 12;    // gradient ops per pass program (host-checked)
 // Per gradient op, 80 cross-matrix entries e = 16 k + b (k = 0: b == a, k = 1 + j: b ^ a = e_j), each one u64
 // LDS atomic holding (re, im) as two biased 32-bit fixed-point halves (PK_*).  A half-wave's active lanes add
@@ -403,15 +404,19 @@ __device__ __forceinline__ void group_apply(uint32_t* tile, const uint4* F, cons
   uint32_t oin[4];
 #pragma unroll
   for (int jj = 0; jj < 4; ++jj) oin[jj] = ((uint32_t)opw[W_OFF + 4 * g4 + jj] ^ fo) << SH;
-  // identity fragments (rows: re of amplitude n, then im), built here so they are not live across the op loop
+  // identity fragments (rows: re of amplitude n, then im), built here from an opaque copy of the lane index so the
+  // compiler cannot hoist them out of the kernel's op loop (hoisted, they were spilled to scratch there)
   uint4 IRE = {}, IIM = {};
   if constexpr (ADJ) {
+    int ln = lane;
+    __asm__ volatile("" : "+v"(ln));
+    const int dg = (ln & 15) - 4 * (ln >> 4);
     uint32_t* re = (uint32_t*)&IRE;
     uint32_t* im = (uint32_t*)&IIM;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      re[j] = cl == 4 * g4 + j ? ONE_LO : 0u;
-      im[j] = cl == 4 * g4 + j ? ONE_HI : 0u;
+      re[j] = dg == j ? ONE_LO : 0u;
+      im[j] = dg == j ? ONE_HI : 0u;
     }
   }
   const uint32_t bl = (uint32_t)opw[W_BL + (wave & 1) * 16 + cl];
@@ -598,27 +603,215 @@ __device__ __forceinline__ void group_back_t(uint32_t* tile, const uint4* F, con
   }
 }
 
-// An op's unitary fragments (4 x 64 lanes x 16 B = 4 KB, contiguous in global memory) go to an LDS slot by
-// direct global -> LDS DMA (global_load_lds_dwordx4, 1 KB per wave-instruction), issued one op ahead by wave 0
-// alone (four instructions): no VGPRs are held for the prefetch, and the other waves never wait on vector memory
-// at an op barrier (the wave that flushes gradient partials to the slab must not wait for those stores there).
+// An op's unitary fragments go to an LDS slot by direct global -> LDS DMA (global_load_lds_dwordx4, 1 KB per
+// wave-instruction), issued one op ahead by wave 0 alone: no VGPRs are held for the prefetch, and the other waves
+// never wait on vector memory at an op barrier (the wave that flushes gradient partials to the slab must not wait
+// for those stores there).  Only the re rows (hi and lo halves, 2 KB per group) travel: the im rows of the real
+// embedding are i times them per (re, im) word (frag_regs).  A pair op's second group fills the slot's upper half.
 // The LDS base of a wave-instruction is wave-uniform (M0); the DMA is complete once wave 0 has passed
 // s_waitcnt vmcnt(0) (op_barrier).
-__device__ __forceinline__ void dma_frags(const PassArgs& a, int k, int fi, int lane, int wave, uint4* slot) {
-  if (fi < 0 || wave != 0) return;
-  const uint4* fr = (const uint4*)a.frags + ((size_t)k * a.n_slots * 4 + fi) * 128 + lane;
-  // Issued as inline asm: the compiler's wait-count pass cannot tell which LDS bytes a builtin DMA writes (no
-  // alias scopes reach codegen), so it waited for the DMA before the op's first LDS store or atomic and exposed
-  // the fragment latency in every op.  The slot is only read after op_barrier's vmcnt(0) + barrier, and a
-  // vector-memory op unknown to the pass can only make its other waits longer, never shorter.
+__device__ __forceinline__ void dma_frags(const PassArgs& a, int k, const int* fi, int lane, int wave, uint4* slot) {
+  if (wave != 0) return;
+#pragma unroll
+  for (int g = 0; g < 2; ++g) {
+    if (fi[g] < 0) continue;
+    const uint4* fr = (const uint4*)a.frags + ((size_t)k * a.n_slots * 4 + fi[g]) * 128 + lane;
+    // Issued as inline asm: the compiler's wait-count pass cannot tell which LDS bytes a builtin DMA writes (no
+    // alias scopes reach codegen), so it waited for the DMA before the op's first LDS store or atomic and exposed
+    // the fragment latency in every op.  The slot is only read after op_barrier's vmcnt(0) + barrier, and a
+    // vector-memory op unknown to the pass can only make its other waits longer, never shorter.
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {                 // hi re rows (f), lo re rows (f + 1: 128 uint4 further)
+      const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)(slot + 128 * g + 64 * j);
+      // s_nop: an LDS DMA reads M0 one wait state after an SALU write of it (the compiler's hazard recognizer does
+      // not look inside this asm statement)
+      __asm__ volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(fr + 128 * j),
+                       "s"(__builtin_amdgcn_readfirstlane(lds))
+                       : "memory", "m0");
+    }
+  }
+}
+
+// Fragment registers of group g of the slot: F[0] / F[2] = hi / lo re rows, F[1] / F[3] = hi / lo im rows.  Row
+// (re, m') of the real 32 x 32 embedding holds (Re U, -Im U) per (re, im) column pair, row (im, m') (Im U, Re U): the
+// im row's word is i times the re row's word, exactly (a sign flip and a swap; hi / lo halves alike).
+__device__ __forceinline__ void frag_regs(const uint4* slot, int g, int lane, uint4* F) {
+  F[0] = slot[128 * g + lane];
+  F[2] = slot[128 * g + 64 + lane];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const uint4 v = F[2 * h];
+    F[2 * h + 1] = make_uint4(mul_i(v.x), mul_i(v.y), mul_i(v.z), mul_i(v.w));
+  }
+}
+
+// ------------------------------------------------------------------------------------------- chained pair ops
+// A block is one coset of span(X, Y) in the tile: 256 amplitudes at  base ^ OFF_X[x] ^ OFF_Y[y] ^ fo.  Lane
+// (g4, cl) first holds (x = 4 g4 + j, y = cl) in register j - the operand layout of X's product over x with y as the
+// column.  X runs in the TRANSPOSED form (state block as the A operand, fragments as B): the result lands with the
+// lane holding x = cl for y = 4 g4 + i in register i, which is exactly the operand layout of Y's product over y with x
+// as the column.  So the pair's second product needs no data movement at all: one LDS read and one write of the
+// coset per pair (and one op barrier), against two of each for two single ops.  The state is rounded to the
+// storage type between the two products, as the LDS store between two single ops rounds it.
+
+// Per-lane address words of a pair op (byte offsets, SH = log2 bytes per amplitude image entry):
+//   xa[j] = (x = 4 g4 + j, y = cl),   ya[j] = (x = cl, y = 4 g4 + j)
+template <int SH>
+__device__ __forceinline__ void pair_addrs(const int* opw, uint32_t fo, int lane, uint32_t* xa, uint32_t* ya) {
+  const int g4 = lane >> 4, cl = lane & 15;
+  const uint32_t ox = (uint32_t)opw[W_OFF + cl], oy = (uint32_t)opw[W_OFF2 + cl];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint4*)(slot + 64 * j);
-    // s_nop: an LDS DMA reads M0 one wait state after an SALU write of it (the compiler's hazard recognizer does
-    // not look inside this asm statement)
-    __asm__ volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(fr + 64 * j),
-                     "s"(__builtin_amdgcn_readfirstlane(lds))
-                     : "memory", "m0");
+    xa[j] = ((uint32_t)opw[W_OFF + 4 * g4 + j] ^ oy ^ fo) << SH;
+    ya[j] = (ox ^ (uint32_t)opw[W_OFF2 + 4 * g4 + j] ^ fo) << SH;
+  }
+}
+
+// block blk's coset base (byte offset)
+template <int SH>
+__device__ __forceinline__ uint32_t pair_base(const int* opw, int blk) {
+  return ((uint32_t)opw[W_BL + (blk & 31)] ^ (uint32_t)opw[W_BH + (blk >> 5)]) << SH;
+}
+
+__device__ __forceinline__ uint4 pack4(const f4& re, const f4& im) {
+  return make_uint4(pack_h2(re[0], im[0]), pack_h2(re[1], im[1]), pack_h2(re[2], im[2]), pack_h2(re[3], im[3]));
+}
+
+// Forward pair: Y U_Y (U_X X) on the psi image.  Read at (x = 4 g4 + j, y = cl), written at (x = cl, y = 4 g4 + i).
+// A wave owns blocks blk = wave + NW i; the next block's reads are issued before the current block computes (all of
+// a block's addresses belong to its coset, so blocks are disjoint).
+template <int NW, int TB>
+__device__ __forceinline__ void group_pair_fwd(uint32_t* tile, const uint4* FX, const uint4* FY, const int* opw,
+                                               uint32_t fo, int lane, int wave, int nbw) {
+  constexpr int MAXB = (1 << (TB - 8)) / NW;
+  uint32_t xa[4], ya[4];
+  pair_addrs<2>(opw, fo, lane, xa, ya);
+  auto load = [&](int i) {
+    const uint32_t b = pair_base<2>(opw, wave + NW * i);
+    return make_uint4(lds_ld(tile, b ^ xa[0]), lds_ld(tile, b ^ xa[1]), lds_ld(tile, b ^ xa[2]), lds_ld(tile, b ^ xa[3]));
+  };
+  if (nbw <= 0) return;
+  uint4 X = load(0);
+#pragma unroll
+  for (int i = 0; i < MAXB; ++i) {
+    if (i >= nbw) break;
+    uint4 Xn = X;
+    if (i + 1 < MAXB && i + 1 < nbw) Xn = load(i + 1 < MAXB ? i + 1 : 0);
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    f4 pr = mfma(X, FX[0], z), pi = mfma(X, FX[1], z);          // X transposed: lane holds x = cl, y = 4 g4 + r
+    if (QFX_HEA_GATE_LO) {
+      pr = mfma(X, FX[2], pr);
+      pi = mfma(X, FX[3], pi);
+    }
+    const uint4 P = pack4(pr, pi);
+    f4 d0 = mfma(FY[0], P, z), d1 = mfma(FY[1], P, z);           // Y over y, column x = cl
+    if (QFX_HEA_GATE_LO) {
+      d0 = mfma(FY[2], P, d0);
+      d1 = mfma(FY[3], P, d1);
+    }
+    const uint32_t b = pair_base<2>(opw, wave + NW * i);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) lds_st(tile, b ^ ya[r], pack_h2(d0[r], d1[r]));
+    X = Xn;
+  }
+}
+
+// Adjoint pair: U_X^H then U_Y^H on psi and lambda (interleaved image), both transposed, each op's gradient cross
+// matrix taken from its rounded results (the op input side, as group_back_t): acc[0..1] for X, acc[2..3] for Y.  Read
+// and written at the same addresses (x = 4 g4 + j, y = cl): after Y the lane holds y = cl for x = 4 g4 + r.
+template <int NW, int TB>
+__device__ __forceinline__ void group_pair_back(uint32_t* tile, const uint4* FX, const uint4* FY, const int* opw,
+                                                uint32_t fo, int lane, int wave, int nbw, f4* acc) {
+  constexpr int MAXB = (1 << (TB - 8)) / NW;
+  uint32_t xa[4], ya[4];
+  pair_addrs<3>(opw, fo, lane, xa, ya);
+  auto load = [&](int i, uint4* X) {
+    const uint32_t b = pair_base<3>(opw, wave + NW * i);
+    const uint2 p0 = lds_ld2(tile, b ^ xa[0]), p1 = lds_ld2(tile, b ^ xa[1]), p2 = lds_ld2(tile, b ^ xa[2]),
+                p3 = lds_ld2(tile, b ^ xa[3]);
+    X[0] = make_uint4(p0.x, p1.x, p2.x, p3.x);
+    X[1] = make_uint4(p0.y, p1.y, p2.y, p3.y);
+  };
+  // one transposed un-apply of both states + the cross matrix of the results.  The im-row fragments are formed
+  // here from the re rows (frag_regs' identity, 4 VALU each): two groups' full fragment sets held across the block
+  // loop pushed the kernel past 128 VGPRs into scratch.
+  auto imrow = [](uint4 v) {        // opaque copy first: hoisted out of the block loop, the im rows stay live again
+    __asm__ volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+    return make_uint4(mul_i(v.x), mul_i(v.y), mul_i(v.z), mul_i(v.w));
+  };
+  auto back = [&](const uint4& Ps, const uint4& Ls, const uint4* F, f4* ac, uint4& Po, uint4& Lo) {
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    uint4 Fi = imrow(F[0]);
+    f4 pr = mfma(Ps, F[0], z), pi = mfma(Ps, Fi, z), lr = mfma(Ls, F[0], z), li = mfma(Ls, Fi, z);
+    if (QFX_HEA_GATE_LO) {
+      Fi = imrow(F[2]);
+      pr = mfma(Ps, F[2], pr);
+      pi = mfma(Ps, Fi, pi);
+      lr = mfma(Ls, F[2], lr);
+      li = mfma(Ls, Fi, li);
+    }
+    Po = pack4(pr, pi);
+    Lo = pack4(lr, li);
+#if QFX_HEA_BF16
+    const uint4 Li = make_uint4(pack_h2(-li[0], lr[0]), pack_h2(-li[1], lr[1]), pack_h2(-li[2], lr[2]), pack_h2(-li[3], lr[3]));
+#else
+    const uint4 Li = make_uint4(mul_i(Lo.x), mul_i(Lo.y), mul_i(Lo.z), mul_i(Lo.w));
+#endif
+    ac[0] = mfma(Po, Lo, ac[0]);
+    ac[1] = mfma(Po, Li, ac[1]);
+  };
+  if (nbw <= 0) return;
+  uint4 Xc[2];
+  load(0, Xc);
+#pragma unroll
+  for (int i = 0; i < MAXB; ++i) {
+    if (i >= nbw) break;
+    uint4 P1, L1, P2, L2;
+    back(Xc[0], Xc[1], FX, acc, P1, L1);
+    // the next block's reads go into the registers X's products have just consumed (a separate prefetch set pushed
+    // the kernel past 128 VGPRs into scratch); they stay in flight during Y's products and the writes
+    if (i + 1 < MAXB && i + 1 < nbw) load(i + 1 < MAXB ? i + 1 : 0, Xc);
+    back(P1, L1, FY, acc + 2, P2, L2);
+    const uint32_t b = pair_base<3>(opw, wave + NW * i);
+    const uint32_t* Pw = (const uint32_t*)&P2;
+    const uint32_t* Lw = (const uint32_t*)&L2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      // (psi, lambda) of one amplitude from two unpaired registers in one ds_write2_b32 (as group_back_t)
+      const uint32_t la = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)((char*)tile + (b ^ xa[r]));
+      __asm__ volatile("ds_write2_b32 %0, %1, %2 offset1:1" ::"v"(la), "v"(Pw[r]), "v"(Lw[r]) : "memory");
+    }
+  }
+}
+
+// Cross-matrix-only pair (layer-1 gradient groups): N_X from the reads at (x = cl, y = 4 g4 + j) (columns y in K),
+// N_Y from (x = 4 g4 + j, y = cl); read-only, so both address patterns read the same coset with no barrier between.
+template <int NW, int TB>
+__device__ __forceinline__ void group_pair_cross(const uint32_t* tile, const int* opw, uint32_t fo, int lane, int wave,
+                                                 int nbw, f4* acc) {
+  constexpr int MAXB = (1 << (TB - 8)) / NW;
+  uint32_t xa[4], ya[4];
+  pair_addrs<3>(opw, fo, lane, xa, ya);
+#pragma unroll
+  for (int i = 0; i < MAXB; ++i) {
+    if (i >= nbw) break;
+    const uint32_t b = pair_base<3>(opw, wave + NW * i);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const uint32_t* ad = g == 0 ? ya : xa;
+      uint32_t pv[4], lv[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint2 v = lds_ld2(tile, b ^ ad[j]);
+        pv[j] = v.x;
+        lv[j] = v.y;
+      }
+      const uint4 A = make_uint4(pv[0], pv[1], pv[2], pv[3]);
+      const uint4 Br = make_uint4(lv[0], lv[1], lv[2], lv[3]);
+      const uint4 Bi = make_uint4(mul_i(lv[0]), mul_i(lv[1]), mul_i(lv[2]), mul_i(lv[3]));
+      acc[2 * g] = mfma(A, Br, acc[2 * g]);
+      acc[2 * g + 1] = mfma(A, Bi, acc[2 * g + 1]);
+    }
   }
 }
 
@@ -787,12 +980,18 @@ __device__ __forceinline__ uint32_t tile_fixed(const PassArgs& a, int tile_id) {
 // op of the pass once per workgroup (lane o, straight from the global records, behind the tile load): inside the
 // op loop it was a dependent chain of nreal LDS reads per op and wave.
 __device__ __forceinline__ uint32_t op_fo_global(const int* ow, uint32_t fixed) {
+  const int code = ow[W_CODE];
+  if (code == OP_OBS || code == OP_READOUT) return 0u;
+  const bool pair = code == OP_APPLY2 || code == OP_BACK2 || code == OP_GRAD2;
   const int nreal = ow[W_NREAL];
-  int fpb = 0;
+  int fpb = 0, fpy = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < 4; ++j) {
     if (j < nreal) fpb |= par(fixed & (uint32_t)ow[W_RFULL + j]) << j;
-  return (uint32_t)ow[W_OFF + fpb];
+    if (pair) fpy |= par(fixed & (uint32_t)ow[W_RFULL2 + j]) << j;
+  }
+  // a pair's OFF tables are linear: one word for both groups' fixed-bit offsets
+  return (uint32_t)ow[W_OFF + fpb] ^ (pair ? (uint32_t)ow[W_OFF2 + fpy] : 0u);
 }
 
 // ------------------------------------------------------------------------------------------- forward pass
@@ -803,7 +1002,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   constexpr int NT = NT_FWD, NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint32_t psi_t[1 << TMAX];   // fp16 (re, im), swizzled
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
-  __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
+  __shared__ int fidx_s[MAXOPS][2];                     // per-op fragment indices (pair ops: two), staged once
   __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (op_fo_global)
   __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];   // op unitary fragments, double buffered
   __shared__ float red[NW * CMAX];
@@ -830,12 +1029,13 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   // op records and unitary fragments are prefetched one op ahead (their global latency hides behind an op); op 0's
   // are requested before the initial tile, so their latency hides behind the tile load / layer-1 generation
   if (tid < a.nops) {                            // LDS copies: the prefetch below never waits on a global load
-    fidx_s[tid] = a.fidx[tid];
+    fidx_s[tid][0] = a.fidx[2 * tid];
+    fidx_s[tid][1] = a.fidx[2 * tid + 1];
     fo_s[tid] = op_fo_global(a.ops + (size_t)tid * OPW, fixed);
   }
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
-  if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
+  if (a.nops > 0) dma_frags(a, k, a.fidx, lane, wave, frag_s[0]);
   st.mark(PH_PRO);
 
   // ---------------------------------------------------------------- initial psi tile
@@ -925,11 +1125,9 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
       st.mark(PH_BAR);
     }
     const int* opw = opw2[o & 1];
-    uint4 F[4];
-    if (fidx_s[o] >= 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) F[i] = frag_s[o & 1][64 * i + lane];
-    }
+    uint4 F[4], FY[4];
+    if (fidx_s[o][0] >= 0) frag_regs(frag_s[o & 1], 0, lane, F);
+    if (fidx_s[o][1] >= 0) frag_regs(frag_s[o & 1], 1, lane, FY);
     if (o + 1 < a.nops) {
       if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
       if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
@@ -937,13 +1135,17 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
     }
     const int code = opw[W_CODE];
 #if QFX_CHECKS_ON
-    QFX_DCHECK(code == OP_APPLY || code == OP_READOUT);
-    if (code == OP_APPLY) {
+    QFX_DCHECK(code == OP_APPLY || code == OP_APPLY2 || code == OP_READOUT);
+    if (code != OP_READOUT) {
       QFX_DCHECK(opw[W_NREAL] >= 0 && opw[W_NREAL] <= 4);
       QFX_DCHECK((uint32_t)opw[W_OFF + (lane & 15)] < (uint32_t)T);
       QFX_DCHECK((uint32_t)opw[W_BL + (lane & 31)] < (uint32_t)T);
       QFX_DCHECK((uint32_t)opw[W_BH + (lane & 31)] < (uint32_t)T);
-      QFX_DCHECK(fidx_s[o] >= 0 && fidx_s[o] < 4 * a.n_slots);
+      QFX_DCHECK(fidx_s[o][0] >= 0 && fidx_s[o][0] < 4 * a.n_slots);
+      if (code == OP_APPLY2) {
+        QFX_DCHECK((uint32_t)opw[W_OFF2 + (lane & 15)] < (uint32_t)T);
+        QFX_DCHECK(fidx_s[o][1] >= 0 && fidx_s[o][1] < 4 * a.n_slots && a.t >= 11);
+      }
     } else {
       QFX_DCHECK(opw[W_NREAL] >= 1 && opw[W_NREAL] <= a.C);
     }
@@ -951,6 +1153,9 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
     st.mark(PH_SETUP);
     if (code == OP_APPLY) {
       group_apply<NW, false>(psi_t, F, opw, fo_s[o], lane, wave, nbw);
+      st.mark(PH_APPLY);
+    } else if (code == OP_APPLY2) {
+      group_pair_fwd<NW, TMAX>(psi_t, F, FY, opw, fo_s[o], lane, wave, nbw);
       st.mark(PH_APPLY);
     } else if (code == OP_READOUT) {
       const size_t pidx = ((size_t)s * a.n_tiles + tile_id) * a.C;
@@ -985,12 +1190,13 @@ __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_
   // (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
   __shared__ __attribute__((aligned(16))) uint32_t tile[2 << TB];
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
-  __shared__ int fidx_s[MAXOPS];                        // per-op fragment index (staged once)
+  __shared__ int fidx_s[MAXOPS][2];                     // per-op fragment indices (pair ops: two), staged once
   __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (op_fo_global)
   __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];   // op unitary fragments, double buffered
   // the 80 cross-matrix entries a partial trace can use (b = a, and b = a ^ e_j) x (re, im), 2^-32 fixed point
   constexpr bool RING = TB < 14;
-  constexpr int NREG = RING ? 2 : MAXGRAD;
+  // ring of 4 regions: an op uses at most two (pair ops), so consecutive ops never share one
+  constexpr int NREG = RING ? 4 : MAXGRAD;
   __shared__ unsigned long long red64[NREG * RSTR];
   __shared__ int gmeta_s[NREG][2];                      // (slab index, nreal) of the region's gradient op
   __shared__ float rsc[CMAX + 2];
@@ -1010,12 +1216,13 @@ __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_
 
   // op 0's record and fragments are requested before the tile load (their latency hides behind it)
   if (tid < a.nops) {
-    fidx_s[tid] = a.fidx[tid];
+    fidx_s[tid][0] = a.fidx[2 * tid];
+    fidx_s[tid][1] = a.fidx[2 * tid + 1];
     fo_s[tid] = op_fo_global(a.ops + (size_t)tid * OPW, fixed);
   }
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
-  if (a.nops > 0) dma_frags(a, k, a.fidx[0], lane, wave, frag_s[0]);
+  if (a.nops > 0) dma_frags(a, k, a.fidx, lane, wave, frag_s[0]);
   // Fused readout (the last wave): its lanes load the sample's readout partials, label, loss weight and readout
   // parameters BEFORE the tile load is issued, so their latency overlaps the tile's; lane 0 sums the partials in tile
   // order after the load (the readout kernel's order and arithmetic, qfx_readout.h).
@@ -1127,7 +1334,7 @@ __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_
   lds_barrier_dma();
   st.mark(PH_BAR);
   int ngrad = 0;
-  int pending = -1;                                    // ring: region of the previous op, if a gradient op
+  int pending = -1, npend = 0;                         // ring: first region / count of the previous op's regions
   // Partial-trace entries this lane adds per gradient op: lane (g4, cl) holds N[4 g4 + i][cl]; byte i of epi is the
   // entry's region slot (b == a -> b, b ^ a == e_j -> 16 + 16 j + b, skewed by red_slot) or 0xFF if no partial
   // trace uses it.  One VGPR for the whole op loop (the per-op predicates had been SGPR pairs spilled to VGPR lanes,
@@ -1147,16 +1354,15 @@ __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_
       op_barrier(wave);
       st.mark(PH_BAR);
     }
-    if (RING && pending >= 0) {
-      if (wave == NW - 1) flush(pending);
-      pending = -1;
+    if (RING && npend > 0) {                           // one wave per region, the last waves
+      for (int q = 0; q < npend; ++q)
+        if (wave == NW - 1 - q) flush((pending + q) & (NREG - 1));
+      npend = 0;
     }
     const int* opw = opw2[o & 1];
-    uint4 F[4];
-    if (fidx_s[o] >= 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) F[i] = frag_s[o & 1][64 * i + lane];
-    }
+    uint4 F[4], FY[4];
+    if (fidx_s[o][0] >= 0) frag_regs(frag_s[o & 1], 0, lane, F);
+    if (fidx_s[o][1] >= 0) frag_regs(frag_s[o & 1], 1, lane, FY);
     if (o + 1 < a.nops) {
       if (tid < OPW) opw2[(o + 1) & 1][tid] = nxt;
       if (o + 2 < a.nops && tid < OPW) nxt = a.ops[(size_t)(o + 2) * OPW + tid];
@@ -1164,16 +1370,22 @@ __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_
     }
     const int code = opw[W_CODE];
 #if QFX_CHECKS_ON
-    QFX_DCHECK(code == OP_BACK || code == OP_GRAD_L1 || code == OP_OBS);
+    QFX_DCHECK(code == OP_BACK || code == OP_GRAD_L1 || code == OP_OBS || code == OP_BACK2 || code == OP_GRAD2);
     if (code != OP_OBS) {
+      const bool pr2 = code == OP_BACK2 || code == OP_GRAD2;
       QFX_DCHECK(opw[W_NREAL] >= 0 && opw[W_NREAL] <= 4);
       QFX_DCHECK((uint32_t)opw[W_OFF + (lane & 15)] < (uint32_t)T);
       QFX_DCHECK((uint32_t)opw[W_BL + (lane & 31)] < (uint32_t)T);
       QFX_DCHECK((uint32_t)opw[W_BH + (lane & 31)] < (uint32_t)T);
       // -1 = no unitary (cross-matrix-only gradient ops); every op that applies one names a fragment
-      QFX_DCHECK(fidx_s[o] >= -1 && fidx_s[o] < 4 * a.n_slots);
-      QFX_DCHECK(fidx_s[o] >= 0 || code == OP_GRAD_L1);
+      QFX_DCHECK(fidx_s[o][0] >= -1 && fidx_s[o][0] < 4 * a.n_slots);
+      QFX_DCHECK(fidx_s[o][0] >= 0 || code == OP_GRAD_L1 || code == OP_GRAD2);
       QFX_DCHECK(opw[W_GIDX] >= 0 && opw[W_GIDX] < a.n_gradops);
+      if (pr2) {
+        QFX_DCHECK((uint32_t)opw[W_OFF2 + (lane & 15)] < (uint32_t)T && a.t >= 11);
+        QFX_DCHECK(opw[W_GIDX2] >= 0 && opw[W_GIDX2] < a.n_gradops);
+        QFX_DCHECK(code == OP_GRAD2 || (fidx_s[o][1] >= 0 && fidx_s[o][1] < 4 * a.n_slots));
+      }
     } else {
       QFX_DCHECK(opw[W_NREAL] >= 1 && opw[W_NREAL] <= a.C);
     }
@@ -1182,56 +1394,71 @@ __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_
     if (code == OP_OBS) {
       obs_op<NCK, NT, TB>(tile, opw, tid, T, fixed, rsc);
       st.mark(PH_OTHER);
-    } else {   // OP_BACK / OP_GRAD_L1
+    } else {   // OP_BACK / OP_GRAD_L1 / OP_BACK2 / OP_GRAD2
       const uint32_t fo = fo_s[o];
-      f4 acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      f4 acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      int ng = 1;
       if (code == OP_BACK && (opw[W_FLAGS] & F_BACK_PSI)) {
         // U^H on psi and lambda, cross matrix at the op input from the results (hea_grad_reduce: input side)
-        group_back_t<NW, TB>(tile, F, opw, fo, lane, wave, nbw, acc2);
+        group_back_t<NW, TB>(tile, F, opw, fo, lane, wave, nbw, acc);
         st.mark(PH_BACK);
       } else if (code == OP_BACK) {
         // U^H on lambda only, cross matrix from the apply's own registers (one pass over the blocks)
-        group_apply<NW, true, TB>(tile, F, opw, fo, lane, wave, nbw, acc2);
+        group_apply<NW, true, TB>(tile, F, opw, fo, lane, wave, nbw, acc);
         st.mark(PH_BACK);
+      } else if (code == OP_BACK2) {
+        group_pair_back<NW, TB>(tile, F, FY, opw, fo, lane, wave, nbw, acc);
+        ng = 2;
+        st.mark(PH_BACK);
+      } else if (code == OP_GRAD2) {
+        group_pair_cross<NW, TB>(tile, opw, fo, lane, wave, nbw, acc);
+        ng = 2;
+        st.mark(PH_GRADL1);
       } else {
-        group_cross<NW, TB>(tile, opw, fo, lane, wave, nbw, acc2[0], acc2[1]);
+        group_cross<NW, TB>(tile, opw, fo, lane, wave, nbw, acc[0], acc[1]);
         st.mark(PH_GRADL1);
       }
-      const f4 accR = acc2[0], accI = acc2[1];
-      // Cross-wave sum of the partial-trace entries of N / rho into the op's region: packed biased fixed point
+      // Cross-wave sum of the partial-trace entries of N / rho into the op's region(s): packed biased fixed point
       // (PK_*), one u64 LDS atomic per entry.  Integer addition is associative, so the sums are bitwise
       // independent of the order the waves (and, in hea_grad_reduce, samples and tiles) arrive.
       // Lane (g4, cl) holds N[4 g4 + i][cl]; entry slot: b == a -> b, b ^ a == e_j -> 16 + 16 j + b.
-      const int reg = RING ? ngrad & 1 : ngrad;
       const float sc = rsc[CMAX + 1];
-      unsigned long long* rg = red64 + reg * RSTR;
       // opaque to the optimiser: kept packed in one VGPR (hoisted out of the op loop, the per-entry predicates and
       // slot addresses had taken eight SGPRs - spilled to VGPR lanes - and four VGPRs)
       uint32_t ep = epi;
       __asm__ volatile("" : "+v"(ep));
+      if (RING) pending = ngrad & (NREG - 1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t sl = (ep >> (8 * i)) & 0xFFu;
-        if (sl != 0xFFu) {
-          // round half up (floor(x + 0.5), one instruction): unbiased for these continuous values - truncation biased
-          // every add toward zero, and a tile's sum has thousands
-          const uint32_t lo = (uint32_t)cvt_rpi(accR[i] * sc) + PK_BIAS, hi = (uint32_t)cvt_rpi(accI[i] * sc) + PK_BIAS;
-          atomicAdd(&rg[sl], ((unsigned long long)hi << 32) | lo);
+      for (int g = 0; g < 2; ++g) {
+        if (g >= ng) break;
+        const int reg = RING ? ngrad & (NREG - 1) : ngrad;
+        unsigned long long* rg = red64 + reg * RSTR;
+        const f4 accR = acc[2 * g], accI = acc[2 * g + 1];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t sl = (ep >> (8 * i)) & 0xFFu;
+          if (sl != 0xFFu) {
+            // round half up (floor(x + 0.5), one instruction): unbiased for these continuous values - truncation
+            // biased every add toward zero, and a tile's sum has thousands
+            const uint32_t lo = (uint32_t)cvt_rpi(accR[i] * sc) + PK_BIAS, hi = (uint32_t)cvt_rpi(accI[i] * sc) + PK_BIAS;
+            atomicAdd(&rg[sl], ((unsigned long long)hi << 32) | lo);
+          }
         }
+        if (tid == 0) {
+          gmeta_s[reg][0] = opw[g ? W_GIDX2 : W_GIDX];
+          gmeta_s[reg][1] = opw[W_NREAL];
+        }
+        ++ngrad;
       }
-      if (tid == 0) {
-        gmeta_s[reg][0] = opw[W_GIDX];
-        gmeta_s[reg][1] = opw[W_NREAL];
-      }
-      pending = reg;
-      ++ngrad;
+      npend = ng;
       st.mark(PH_EPI);
     }
     if constexpr (QFX_HEA_STAMPS) ++st.nops;
   }
   lds_barrier();
   if (RING) {
-    if (pending >= 0 && wave == NW - 1 && lane < 32) reduce_region(pending, lane);
+    for (int q = 0; q < npend; ++q)
+      if (wave == NW - 1 - q && lane < 32) reduce_region((pending + q) & (NREG - 1), lane);
   } else {
     for (int e = tid; e < ngrad * 32; e += NT) reduce_region(e >> 5, e & 31);
   }

@@ -41,16 +41,21 @@ _FEATURE = {"ry": 0, "rx": 1, "rz": 2}
 
 
 def _frag_index(ops: np.ndarray) -> torch.Tensor:
-    """Per op the unitary fragment it multiplies by (slot * 4 + 0: U, + 2: U^H) or -1 (prefetch table)."""
-    from .hea_plan import OP_APPLY, OP_BACK, W_CODE, W_SLOT
-    out = np.full(len(ops), -1, dtype=np.int32)
+    """Per op the unitary fragments it multiplies by (slot * 4 + 0: U, + 2: U^H; a pair op names its two groups'),
+    -1 for none: int32 [nops, 2] (prefetch table)."""
+    from .hea_plan import OP_APPLY, OP_APPLY2, OP_BACK, OP_BACK2, W_CODE, W_SLOT, W_SLOT2
+    out = np.full((len(ops), 2), -1, dtype=np.int32)
     for i, w in enumerate(ops):
         code = int(w[W_CODE])
-        if code == OP_APPLY:
-            out[i] = 4 * int(w[W_SLOT])
-        elif code == OP_BACK:
-            out[i] = 4 * int(w[W_SLOT]) + 2
-    return torch.from_numpy(out)
+        if code in (OP_APPLY, OP_APPLY2):
+            out[i, 0] = 4 * int(w[W_SLOT])
+        elif code in (OP_BACK, OP_BACK2):
+            out[i, 0] = 4 * int(w[W_SLOT]) + 2
+        if code == OP_APPLY2:
+            out[i, 1] = 4 * int(w[W_SLOT2])
+        elif code == OP_BACK2:
+            out[i, 1] = 4 * int(w[W_SLOT2]) + 2
+    return torch.from_numpy(out).contiguous()
 _NO_KEYS = torch.zeros(0, dtype=torch.int64)
 _NODBG = torch.zeros(0, dtype=torch.int64)     # no stall-attribution buffer (stamps build only)
 

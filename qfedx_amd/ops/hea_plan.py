@@ -34,6 +34,7 @@ tests hold against a dense simulation, and the HIP kernel is tested against both
 from __future__ import annotations
 
 import copy
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -44,8 +45,14 @@ MIN_CONTIG = 5             # contiguous low bits in a strided tile (32 amplitude
 
 # op codes (kept in sync with csrc/hea_mfma.hip)
 OP_APPLY, OP_GRAD_L1, OP_OBS, OP_READOUT, OP_BACK = 1, 5, 6, 7, 8
+# chained pairs of two commuting 4-qubit groups X, Y of one layer on the 256-amplitude cosets of span(X, Y): one LDS
+# read and write of the coset per pair, one op barrier (see pair_table)
+OP_APPLY2, OP_BACK2, OP_GRAD2 = 2, 3, 4
+PAIR_CODES = (OP_APPLY2, OP_BACK2, OP_GRAD2)
 OP_WORDS = 128
 W_CODE, W_SLOT, W_NREAL, W_FLAGS, W_RFULL, W_RT, W_TH, W_PH, W_OFF, W_BL, W_BH = 0, 1, 2, 3, 4, 8, 12, 16, 20, 36, 68
+# pair records: the second group's rows in the W_RT words, and
+W_RFULL2, W_GIDX2, W_SLOT2, W_OFF2, W_TH2, W_PH2 = 8, 101, 102, 104, 120, 124
 F_BACK_PSI = 1             # OP_BACK also un-applies the group on psi (still needed further back), in the transposed
                            # form (group_back_t): its cross matrix is taken at the op INPUT
 W_GIDX = 100               # gradient ops: global index of the op's partial-trace record in the slab
@@ -543,6 +550,66 @@ def group_table(plan: HEAPlan, p: Pass, g: Group, code: int, flags: int = 0) -> 
     return w
 
 
+def pairable(plan: HEAPlan, p: Pass, gx: Group, gy: Group) -> bool:
+    """Two rotation groups can run as one chained pair op: one layer (so one CNOT frame: each group's row masks
+    annihilate the other's vectors and their 8 vectors are independent), 4 real qubits each, and at least one
+    256-amplitude coset per... tile of 2^t >= 2^11 (8 cosets: one per wave of a forward workgroup at least)."""
+    return (gx.layer == gy.layer and gx.layer >= 1 and len(gx.qubits) == GROUP and len(gy.qubits) == GROUP
+            and p.t >= 11 and not set(gx.qubits) & set(gy.qubits))
+
+
+def pair_table(plan: HEAPlan, p: Pass, gx: Group, gy: Group, code: int, flags: int = 0) -> np.ndarray:
+    """Record of a chained pair op: group X runs first, then Y (X, Y commute).  A block is one coset of span(X, Y)
+    in the tile, 256 amplitudes at  addr(x, y) = base ^ OFF_X[x] ^ OFF_Y[y] ^ fo  with x, y the two groups' logical
+    coordinates (the OFF tables are linear, so the tile's fixed-bit offset is one word fo = OFF_X[fpX] ^ OFF_Y[fpY]).
+    Block bases BL[blk & 31] ^ BH[blk >> 5] = d ^ OFF_X[bits_X(d)] ^ OFF_Y[bits_Y(d)] for a deposit d of the block
+    index into the tile bits outside both groups' pivots (logical coordinates 0 in both groups).  The kernel chains
+    the two 16 x 16 products in registers: X in the transposed MFMA form leaves each lane holding its x-amplitude of 4
+    y-columns, which is exactly the operand layout of Y's product over y (csrc/hea_mfma.hip, group_pair)."""
+    if not pairable(plan, p, gx, gy):
+        raise ValueError("groups cannot be paired")
+    n, t = plan.n, p.t
+    w = np.zeros(OP_WORDS, dtype=np.int64)
+    w[W_CODE] = code
+    w[W_FLAGS] = flags
+    w[W_NREAL] = GROUP
+    geo = []
+    for g, (wr, wth, wph, woff, wsl) in ((gx, (W_RFULL, W_TH, W_PH, W_OFF, W_SLOT)),
+                                          (gy, (W_RFULL2, W_TH2, W_PH2, W_OFF2, W_SLOT2))):
+        allv, rfull, rt, off, _, bits, _ = _group_geom(plan, p, g)
+        geo.append((allv, off, bits))
+        w[wsl] = g.slot
+        for j in range(GROUP):
+            w[wr + j] = rfull[j]
+            w[wth + j] = plan.theta_slot(g.layer, g.qubits[j])
+            w[wph + j] = plan.theta_slot(g.layer, g.qubits[j]) + 1
+        for m in range(16):
+            w[woff + m] = sigma(p.H, off[m])
+    piv = set(_pivots(geo[0][0] + geo[1][0]))
+    order = [b for b in range(t) if b not in piv]
+    assert len(order) == t - 2 * GROUP
+    (_, offx, bitsx), (_, offy, bitsy) = geo
+
+    def rep(d):
+        return d ^ offx[bitsx(d)] ^ offy[bitsy(d)]
+    for i in range(32):
+        lo = hi = 0
+        for j in range(5):
+            if (i >> j) & 1:
+                if j < len(order):
+                    lo |= 1 << order[j]
+                if 5 + j < len(order):
+                    hi |= 1 << order[5 + j]
+        w[W_BL + i] = sigma(p.H, rep(lo))
+        w[W_BH + i] = sigma(p.H, rep(hi))
+    return w
+
+
+def _pair_default() -> bool:
+    """Chained pair ops (QFEDX_HEA_PAIR=0 plans every group op alone: A/B)."""
+    return os.environ.get("QFEDX_HEA_PAIR", "1") != "0"
+
+
 def obs_table(plan: HEAPlan, p: Pass, code: int) -> np.ndarray:
     w = np.zeros(OP_WORDS, dtype=np.int64)
     w[W_CODE] = code
@@ -558,36 +625,73 @@ def obs_table(plan: HEAPlan, p: Pass, code: int) -> np.ndarray:
     return w
 
 
-def pass_programs(plan: HEAPlan, meta: list | None = None):
+def _pairs(plan: HEAPlan, p: Pass, groups: list, pair: bool) -> list:
+    """Greedy left-to-right grouping of consecutive pairable groups: [(g,), (g, h), ...]."""
+    out, i = [], 0
+    while i < len(groups):
+        if pair and i + 1 < len(groups) and pairable(plan, p, groups[i], groups[i + 1]):
+            out.append((groups[i], groups[i + 1]))
+            i += 2
+        else:
+            out.append((groups[i],))
+            i += 1
+    return out
+
+
+def pass_programs(plan: HEAPlan, meta: list | None = None, pair: bool | None = None):
     """Forward and adjoint op lists per pass: list of (Pass, fwd_ops [k, OP_WORDS], adj_ops).  ``meta``
-    (optional list) receives one row per gradient op: [tiles of its pass, nreal | inside << 4, theta slots x4,
+    (optional list) receives one row per gradient (group) op: [tiles of its pass, nreal | inside << 4, theta slots x4,
     phi slots x4].  BACK ops that un-apply psi too run transposed (``group_back_t``): their cross matrix is taken at
     the op input (``inside``, hea_grad_reduce applies the input-side generators); a pass's last BACK op, when psi is
-    no longer needed, un-applies lambda only and takes the cross matrix at its output."""
+    no longer needed, un-applies lambda only and takes the cross matrix at its output.  ``pair`` (default on,
+    QFEDX_HEA_PAIR): consecutive groups of one layer run as chained pair ops (``pair_table``) - the forward pairs
+    (g_i, g_i+1) of the pass order, the adjoint the same pairs in reverse, and the layer-1 gradient groups in pairs
+    - with the gradient records in the order of the unpaired program."""
+    if pair is None:
+        pair = _pair_default()
     out = []
     gidx = [0]
     gmeta = meta if meta is not None else []
     J = len(plan.passes)
+
+    def meta_row(w, x: str):
+        th, ph = (W_TH, W_PH) if x == "x" else (W_TH2, W_PH2)
+        inside = 16 if (int(w[W_CODE]) in (OP_BACK, OP_BACK2) and int(w[W_FLAGS]) & F_BACK_PSI) else 0
+        gmeta.append([1 << (plan.n - p.t), int(w[W_NREAL]) | inside] + [int(v) for v in w[th:th + 4]] +
+                     [int(v) for v in w[ph:ph + 4]])
     for j, p in enumerate(plan.passes):
-        fwd = [group_table(plan, p, g, OP_APPLY) for g in p.groups]
+        units = _pairs(plan, p, p.groups, pair)
+        fwd = [group_table(plan, p, u[0], OP_APPLY) if len(u) == 1 else pair_table(plan, p, u[0], u[1], OP_APPLY2)
+               for u in units]
         if j == J - 1:
             fwd.append(obs_table(plan, p, OP_READOUT))
-        # the adjoint of pass j starts from pass j's stored OUTPUT and walks back
+        # the adjoint of pass j starts from pass j's stored OUTPUT and walks back; a forward pair (g, h) un-applies h
+        # first, then g
         adj = [obs_table(plan, p, OP_OBS)] if j == J - 1 else []
-        rev = list(reversed(p.groups))
-        for i, g in enumerate(rev):
+        for i, u in enumerate(reversed(units)):
             # gradient cross matrix + U^H on lambda (and on psi while it is still needed further back)
-            psi_needed = i < len(rev) - 1 or bool(p.l1)
-            adj.append(group_table(plan, p, g, OP_BACK, F_BACK_PSI if psi_needed else 0))
-        for g in p.l1:
-            adj.append(group_table(plan, p, g, OP_GRAD_L1))
+            psi_needed = i < len(units) - 1 or bool(p.l1)
+            if len(u) == 2 and psi_needed:
+                adj.append(pair_table(plan, p, u[1], u[0], OP_BACK2, F_BACK_PSI))
+            elif len(u) == 2:                   # the pass's last pair without psi: two single ops
+                adj.append(group_table(plan, p, u[1], OP_BACK, F_BACK_PSI))
+                adj.append(group_table(plan, p, u[0], OP_BACK, 0))
+            else:
+                adj.append(group_table(plan, p, u[0], OP_BACK, F_BACK_PSI if psi_needed else 0))
+        for u in _pairs(plan, p, p.l1, pair):
+            adj.append(group_table(plan, p, u[0], OP_GRAD_L1) if len(u) == 1 else
+                       pair_table(plan, p, u[0], u[1], OP_GRAD2))
         for w in adj:
-            if w[W_CODE] in (OP_BACK, OP_GRAD_L1):
+            code = int(w[W_CODE])
+            if code in (OP_BACK, OP_GRAD_L1):
                 w[W_GIDX] = gidx[0]
-                inside = 16 if (int(w[W_CODE]) == OP_BACK and int(w[W_FLAGS]) & F_BACK_PSI) else 0
-                gmeta.append([1 << (plan.n - p.t), int(w[W_NREAL]) | inside] + [int(v) for v in w[W_TH:W_TH + 4]] +
-                             [int(v) for v in w[W_PH:W_PH + 4]])
+                meta_row(w, "x")
                 gidx[0] += 1
+            elif code in (OP_BACK2, OP_GRAD2):
+                w[W_GIDX], w[W_GIDX2] = gidx[0], gidx[0] + 1
+                meta_row(w, "x")
+                meta_row(w, "y")
+                gidx[0] += 2
         out.append((p, np.stack(fwd) if fwd else np.zeros((0, OP_WORDS), np.int64),
                     np.stack(adj) if adj else np.zeros((0, OP_WORDS), np.int64)))
     return out
@@ -644,6 +748,29 @@ def _addr(w, t, fixed):
     off = w[W_OFF:W_OFF + 16]
     base = w[W_BL + (col & 31)] ^ w[W_BH + (col >> 5)] ^ off[fp]
     return base[:, None] ^ off[None, :]
+
+
+def _pair_addr(w, t, fixed):
+    """[blocks, 16 (x), 16 (y)] tile addresses of a pair record's cosets, computed as the kernel does."""
+    fo = 0
+    for off, rows in ((W_OFF, W_RFULL), (W_OFF2, W_RFULL2)):
+        fp = 0
+        for j in range(GROUP):
+            fp |= parity(fixed & int(w[rows + j])) << j
+        fo ^= int(w[off + fp])
+    blk = np.arange(1 << (t - 2 * GROUP))
+    base = w[W_BL + (blk & 31)] ^ w[W_BH + (blk >> 5)] ^ fo
+    return base[:, None, None] ^ w[W_OFF:W_OFF + 16][None, :, None] ^ w[W_OFF2:W_OFF2 + 16][None, None, :]
+
+
+def _pair_half(w, which: str):
+    """A single-op view (W_NREAL, W_TH, W_PH, W_GIDX) of group X or Y of a pair record (emulator)."""
+    v = np.array(w, copy=True)
+    if which == "y":
+        v[W_TH:W_TH + 4] = w[W_TH2:W_TH2 + 4]
+        v[W_PH:W_PH + 4] = w[W_PH2:W_PH2 + 4]
+        v[W_SLOT] = w[W_SLOT2]
+    return v
 
 
 def _grad(w, ps, lm, th, gk, gfac, inside: bool = False):
@@ -743,6 +870,10 @@ def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp1
                         if w[W_CODE] == OP_APPLY:
                             a = _addr(w, p.t, fixed)
                             tile[a] = rnd((Us[int(w[W_SLOT])] @ tile[a].T).T)
+                        elif w[W_CODE] == OP_APPLY2:         # X along x, rounded, then Y along y
+                            a = _pair_addr(w, p.t, fixed)
+                            v = np.einsum("ij,bjy->biy", Us[int(w[W_SLOT])], tile[a])
+                            tile[a] = rnd(np.einsum("ij,bxj->bxi", Us[int(w[W_SLOT2])], rnd(v)))
                         elif w[W_CODE] == OP_READOUT:
                             sg = _signs(w, p.t, fixed, plan.C)
                             expz[k, b] += sg @ (np.abs(tile) ** 2) / scale ** 2
@@ -775,6 +906,26 @@ def emulate(plan: HEAPlan, xang: np.ndarray, params: np.ndarray, wread=None, fp1
                         if code == OP_OBS:
                             sg = _signs(w, p.t, fixed, plan.C)
                             lm = rnd((rr @ sg) * ps)
+                            continue
+                        if code == OP_BACK2:
+                            # X then Y, each transposed: U^H on both states, cross matrix of the rounded results
+                            a = _pair_addr(w, p.t, fixed)
+                            P, Lm = ps[a], lm[a]
+                            Uh = Us[int(w[W_SLOT])].conj().T
+                            P, Lm = rnd(np.einsum("ij,bjy->biy", Uh, P)), rnd(np.einsum("ij,bjy->biy", Uh, Lm))
+                            _grad(w, P.transpose(0, 2, 1).reshape(-1, 16), Lm.transpose(0, 2, 1).reshape(-1, 16),
+                                  th, grads[k], gfac, inside=True)
+                            Uh = Us[int(w[W_SLOT2])].conj().T
+                            P, Lm = rnd(np.einsum("ij,bxj->bxi", Uh, P)), rnd(np.einsum("ij,bxj->bxi", Uh, Lm))
+                            _grad(_pair_half(w, "y"), P.reshape(-1, 16), Lm.reshape(-1, 16), th, grads[k], gfac,
+                                  inside=True)
+                            ps[a], lm[a] = P, Lm
+                            continue
+                        if code == OP_GRAD2:
+                            a = _pair_addr(w, p.t, fixed)
+                            _grad(w, ps[a].transpose(0, 2, 1).reshape(-1, 16), lm[a].transpose(0, 2, 1).reshape(-1, 16),
+                                  th, grads[k], gfac)
+                            _grad(_pair_half(w, "y"), ps[a].reshape(-1, 16), lm[a].reshape(-1, 16), th, grads[k], gfac)
                             continue
                         a = _addr(w, p.t, fixed)
                         if code == OP_BACK and int(w[W_FLAGS]) & F_BACK_PSI:

@@ -228,3 +228,31 @@ def test_fused_readout_matches_readout_kernel(cuda, monkeypatch, n, K, B, C):
     assert torch.equal(got["correct"], ref["correct"])
     for k in ("loss", "correct", "grad", "expz"):
         assert torch.equal(got[k], again[k]), k
+
+
+@pytest.mark.parametrize("n,L,tile", [(16, 3, 14), (12, 3, 11), (20, 2, 14)])
+def test_pair_ops_match_unpaired_kernels(cuda, monkeypatch, n, L, tile):
+    """Chained pair ops (APPLY2 / BACK2 / GRAD2) on the GPU against the unpaired program (QFEDX_HEA_PAIR=0) on the
+    same plan: <Z> and gradients agree to fp32-accumulation rounding (the pair chains its second product in registers;
+    the state is rounded to fp16 at the same points), both match the dense oracle, and the pair program is
+    deterministic."""
+    spec = VQCSpec(n, L, 3)
+    K, B = 3, 4
+    x, params, wr = _inputs(spec, K, B, seed=n + L)
+    xx, th, ww = x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda)
+    monkeypatch.setenv("QFEDX_HEA_PAIR", "1")
+    pp = HeaMfmaProgram(spec, cuda, tile_bits=tile)
+    codes = {int(c) for p in pp.passes for c in list(p[1][0][:, 0].cpu()) + list(p[2][0][:, 0].cpu())}
+    assert codes & {2, 3}, codes
+    z1, g1 = pp.vjp(xx, th, ww)
+    z1b, g1b = pp.vjp(xx, th, ww)
+    monkeypatch.setenv("QFEDX_HEA_PAIR", "0")
+    p0 = HeaMfmaProgram(spec, cuda, tile_bits=tile)
+    z0, g0 = p0.vjp(xx, th, ww)
+    torch.cuda.synchronize()
+    assert torch.equal(z1, z1b) and torch.equal(g1, g1b)
+    np.testing.assert_allclose(z1.cpu().numpy(), z0.cpu().numpy(), atol=2e-5)
+    np.testing.assert_allclose(g1.cpu().numpy(), g0.cpu().numpy(), atol=2e-4 * max(1.0, float(g0.abs().max())))
+    ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
+    np.testing.assert_allclose(z1.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
+    np.testing.assert_allclose(g1.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))

@@ -183,3 +183,44 @@ def test_pi_identity_of_shifted_expectations():
         m = 0.5 * (z[0, :, c] + z[1, :, c])
         np.testing.assert_allclose(z[2, :, c].numpy(), (m + gg).numpy(), atol=1e-10)
         np.testing.assert_allclose(z[3, :, c].numpy(), (m - gg).numpy(), atol=1e-10)
+
+
+@pytest.mark.parametrize("n,L,t", [(12, 3, 11), (14, 2, 12), (16, 3, 14), (16, 3, 13), (13, 4, 11)])
+def test_pair_ops_emulated_match_dense_and_unpaired(n, L, t):
+    """Chained pair ops (APPLY2 / BACK2 / GRAD2, hea_plan.pair_table): emulated tile by tile with the pair records'
+    coset addressing they give the dense float64 results, and in the fp16 storage format they round at exactly the
+    points the unpaired program rounds (bitwise the same expectations and gradients)."""
+    spec = VQCSpec(n, L, 3)
+    plan = hp.build_plan(n, L, spec.readout, True, "ry", tile_bits=t)
+    progs = hp.pass_programs(plan, pair=True)
+    codes = {int(w[hp.W_CODE]) for _, f, a in progs for w in list(f) + list(a)}
+    assert hp.OP_APPLY2 in codes and hp.OP_BACK2 in codes
+    g = torch.Generator().manual_seed(n * 7 + L)
+    x = torch.rand(2, 2, n, generator=g, dtype=torch.float64) * 3
+    params = torch.randn(2, spec.n_params, generator=g, dtype=torch.float64)
+    wr = torch.randn(2, 2, 3, generator=g, dtype=torch.float64)
+    ez, gr = _dense(spec, x, params, wr)
+    ez2, gr2 = hp.emulate(plan, x.numpy(), params.numpy(), wr.numpy())
+    np.testing.assert_allclose(ez2, ez, atol=1e-12)
+    np.testing.assert_allclose(gr2, gr, atol=1e-12)
+    import os
+    ez3, gr3 = hp.emulate(plan, x.numpy(), params.numpy(), wr.numpy(), fp16=True)
+    os.environ["QFEDX_HEA_PAIR"] = "0"
+    try:
+        assert not {int(w[hp.W_CODE]) for _, f, a in hp.pass_programs(plan) for w in list(f) + list(a)} & set(hp.PAIR_CODES)
+        ez4, gr4 = hp.emulate(plan, x.numpy(), params.numpy(), wr.numpy(), fp16=True)
+    finally:
+        del os.environ["QFEDX_HEA_PAIR"]
+    np.testing.assert_array_equal(ez3, ez4)
+    np.testing.assert_allclose(gr3, gr4, atol=1e-12)
+
+
+def test_pair_gradient_records_keep_unpaired_order():
+    """A pair op carries two gradient records in the unpaired program's order (the slab layout and hea_grad_reduce
+    are unchanged): same gmeta rows with and without pairing."""
+    spec = VQCSpec(16, 3, 3)
+    plan = hp.build_plan(16, 3, spec.readout, True, "ry", tile_bits=13)
+    m1, m0 = [], []
+    hp.pass_programs(plan, m1, pair=True)
+    hp.pass_programs(plan, m0, pair=False)
+    assert m1 == m0 and len(m1) > 0

@@ -202,6 +202,12 @@ def test_secagg_sparse_graph_cancels_with_dropouts(k, seed):
     masked = {c: sa.mask(ups[c], c, parts, round_num=4) for c in parts}
     dropped = parts[1::5] if k > 2 else []
     survivors = [c for c in parts if c not in dropped]
+    if not sa.round_ok(parts, dropped, 4):
+        # a survivor kept fewer live neighbours than the SecAgg+ threshold: the round is refused, never unmasked
+        from qfedx_amd.privacy.secure_agg import SecAggAbort
+        with pytest.raises(SecAggAbort):
+            sa.aggregate([masked[c] for c in survivors], survivors, dropped, round_num=4)
+        return
     total = sa.aggregate([masked[c] for c in survivors], survivors, dropped, round_num=4)
     assert torch.allclose(total, sum(ups[c] for c in survivors), atol=1e-5)
     assert len(sa.orphan_pairs(survivors, dropped, parts, 4)) <= deg * len(dropped)
