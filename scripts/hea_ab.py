@@ -53,14 +53,16 @@ def main():
     params = torch.stack([spec.init_params(k) for k in range(K)]).to(dev)
     variants = parse_variants(args.variants)
     progs = {}
-    for name, knobs in variants:
-        progs[name] = HeaMfmaProgram(spec, dev, storage=knobs.get("storage", "fp16"))
-    ext()
 
     def set_knobs(knobs):
         for k, v in knobs.items():
-            if k.startswith("env."):           # run-time environment switches, e.g. env.QFEDX_FUSED_READOUT=0
+            if k.startswith("env."):           # environment switches, e.g. env.QFEDX_FUSED_READOUT=0
                 os.environ[k[4:]] = v
+
+    for name, knobs in variants:
+        set_knobs(knobs)                       # plan-level switches (QFEDX_HEA_PAIR) act when the program is built
+        progs[name] = HeaMfmaProgram(spec, dev, storage=knobs.get("storage", "fp16"))
+    ext()
 
     def prep(prog):
         xx = x.reshape(S, -1).float().contiguous()

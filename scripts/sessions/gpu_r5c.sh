@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 5, call 3: chained pair ops -- MFMA-engine GPU tests first (pair vs unpaired, dense oracle), then the full GPU
+# suite, the headline + 8-client bench, pair A/B (QFEDX_HEA_PAIR) interleaved, stall attribution.
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r5c
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  timeout -k 10 "$secs" "$@" > "gpurun_out/r5c/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"; tail -3 "gpurun_out/r5c/$name.log" | cut -c1-700
+  [ $rc -eq 0 ] || exit $rc
+}
+step hea_tests 400 python -u -m pytest tests/test_gpu_hea.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+step bench64 300 python bench.py --steps 20 --warmup 3
+step share8 300 python bench.py --steps 30 --warmup 5 --clients 8
+step ab_pair64 300 python -u scripts/hea_ab.py --rounds 7 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=1"
+step ab_pair8 300 python -u scripts/hea_ab.py --rounds 7 --clients 8 --iters 30 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=1"
+step stamps64 300 python -u scripts/hea_stamps.py --clients 64 --out gpurun_out/r5c/stamps64.jsonl
