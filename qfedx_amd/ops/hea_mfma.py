@@ -24,7 +24,7 @@ import numpy as np
 import torch
 
 from ._ext import ext
-from .hea_plan import OP_APPLY, OP_READOUT, TILE_BITS, W_CODE, build_plan, eligible, obs_table, pass_programs
+from .hea_plan import OP_APPLY, OP_APPLY2, OP_READOUT, TILE_BITS, W_CODE, build_plan, eligible, obs_table, pass_programs
 
 ADJ_TILE_BITS = 13   # adjoint tiles: 2^13 amplitudes x (psi, lambda) = 64 KB of LDS -> two workgroups per CU
 
@@ -108,7 +108,8 @@ class HeaMfmaProgram:
         # Forward passes after the last one that applies a unitary are identities on the state (they exist for
         # the adjoint's layer-1 gradient tiles, e.g. every pass of an L = 1 circuit): the forward stops at that
         # pass, reads out there, and later passes' stored outputs alias its output.
-        applies = [j for j, (_, fwd, _) in enumerate(progs_f) if any(int(w[W_CODE]) == OP_APPLY for w in fwd)]
+        applies = [j for j, (_, fwd, _) in enumerate(progs_f)
+                   if any(int(w[W_CODE]) in (OP_APPLY, OP_APPLY2) for w in fwd)]
         self.fwd_last = applies[-1] if applies else 0
         J = len(progs_f)
         progs_a = pass_programs(plan_a, gmeta)

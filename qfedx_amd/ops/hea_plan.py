@@ -605,9 +605,10 @@ def pair_table(plan: HEAPlan, p: Pass, gx: Group, gy: Group, code: int, flags: i
     return w
 
 
-def _pair_default() -> bool:
-    """Chained pair ops (QFEDX_HEA_PAIR=0 plans every group op alone: A/B)."""
-    return os.environ.get("QFEDX_HEA_PAIR", "1") != "0"
+def _pair_default() -> int:
+    """Chained pair ops: QFEDX_HEA_PAIR bit mask of the kinds planned as pairs (1 APPLY2, 2 BACK2, 4 GRAD2; default 7,
+    0 plans every group op alone: A/B)."""
+    return int(os.environ.get("QFEDX_HEA_PAIR", "7"))
 
 
 def obs_table(plan: HEAPlan, p: Pass, code: int) -> np.ndarray:
@@ -649,6 +650,7 @@ def pass_programs(plan: HEAPlan, meta: list | None = None, pair: bool | None = N
     - with the gradient records in the order of the unpaired program."""
     if pair is None:
         pair = _pair_default()
+    pair = 7 if pair is True else (0 if pair is False else int(pair))
     out = []
     gidx = [0]
     gmeta = meta if meta is not None else []
@@ -660,9 +662,13 @@ def pass_programs(plan: HEAPlan, meta: list | None = None, pair: bool | None = N
         gmeta.append([1 << (plan.n - p.t), int(w[W_NREAL]) | inside] + [int(v) for v in w[th:th + 4]] +
                      [int(v) for v in w[ph:ph + 4]])
     for j, p in enumerate(plan.passes):
-        units = _pairs(plan, p, p.groups, pair)
-        fwd = [group_table(plan, p, u[0], OP_APPLY) if len(u) == 1 else pair_table(plan, p, u[0], u[1], OP_APPLY2)
-               for u in units]
+        units = _pairs(plan, p, p.groups, bool(pair & 3))
+        fwd = []
+        for u in units:
+            if len(u) == 2 and pair & 1:
+                fwd.append(pair_table(plan, p, u[0], u[1], OP_APPLY2))
+            else:
+                fwd += [group_table(plan, p, g, OP_APPLY) for g in u]
         if j == J - 1:
             fwd.append(obs_table(plan, p, OP_READOUT))
         # the adjoint of pass j starts from pass j's stored OUTPUT and walks back; a forward pair (g, h) un-applies h
@@ -671,14 +677,14 @@ def pass_programs(plan: HEAPlan, meta: list | None = None, pair: bool | None = N
         for i, u in enumerate(reversed(units)):
             # gradient cross matrix + U^H on lambda (and on psi while it is still needed further back)
             psi_needed = i < len(units) - 1 or bool(p.l1)
-            if len(u) == 2 and psi_needed:
+            if len(u) == 2 and psi_needed and pair & 2:
                 adj.append(pair_table(plan, p, u[1], u[0], OP_BACK2, F_BACK_PSI))
-            elif len(u) == 2:                   # the pass's last pair without psi: two single ops
+            elif len(u) == 2:                   # unpaired, or the pass's last pair without psi: two single ops
                 adj.append(group_table(plan, p, u[1], OP_BACK, F_BACK_PSI))
-                adj.append(group_table(plan, p, u[0], OP_BACK, 0))
+                adj.append(group_table(plan, p, u[0], OP_BACK, F_BACK_PSI if psi_needed else 0))
             else:
                 adj.append(group_table(plan, p, u[0], OP_BACK, F_BACK_PSI if psi_needed else 0))
-        for u in _pairs(plan, p, p.l1, pair):
+        for u in _pairs(plan, p, p.l1, bool(pair & 4)):
             adj.append(group_table(plan, p, u[0], OP_GRAD_L1) if len(u) == 1 else
                        pair_table(plan, p, u[0], u[1], OP_GRAD2))
         for w in adj:

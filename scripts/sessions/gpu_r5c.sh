@@ -15,6 +15,6 @@ step hea_tests 400 python -u -m pytest tests/test_gpu_hea.py -x -q --timeout 120
 step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 step bench64 300 python bench.py --steps 20 --warmup 3
 step share8 300 python bench.py --steps 30 --warmup 5 --clients 8
-step ab_pair64 300 python -u scripts/hea_ab.py --rounds 7 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=1"
-step ab_pair8 300 python -u scripts/hea_ab.py --rounds 7 --clients 8 --iters 30 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=1"
+step ab_pair64 300 python -u scripts/hea_ab.py --rounds 7 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=7"
+step ab_pair8 300 python -u scripts/hea_ab.py --rounds 7 --clients 8 --iters 30 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=7"
 step stamps64 300 python -u scripts/hea_stamps.py --clients 64 --out gpurun_out/r5c/stamps64.jsonl

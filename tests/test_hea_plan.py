@@ -224,3 +224,17 @@ def test_pair_gradient_records_keep_unpaired_order():
     hp.pass_programs(plan, m1, pair=True)
     hp.pass_programs(plan, m0, pair=False)
     assert m1 == m0 and len(m1) > 0
+
+
+def test_pair_only_pass_counts_as_applying():
+    """A forward pass whose only group ops are chained pairs still applies unitaries: the forward reads out at the
+    last such pass (20q x 2L: pass 1 is [APPLY2, READOUT]; counting single APPLY ops only stopped the forward one
+    pass early, which <Z> of the low readout qubits could not see)."""
+    import torch
+    from qfedx_amd.ops.hea_mfma import HeaMfmaProgram
+    spec = VQCSpec(20, 2, 3)
+    plan = hp.build_plan(20, 2, spec.readout, True, "ry", tile_bits=14)
+    progs = hp.pass_programs(plan)
+    assert [int(w[hp.W_CODE]) for w in progs[-1][1]] == [hp.OP_APPLY2, hp.OP_READOUT]
+    prog = HeaMfmaProgram(spec, torch.device("cpu"))
+    assert prog.fwd_last == len(prog.passes) - 1
