@@ -488,10 +488,29 @@ def _best_cols(H, allv, dirs, stores: bool = True):
     return best
 
 
-def layout_pass(plan: HEAPlan, p: Pass, seed: int = 0, tries: int = 48) -> None:
-    """Pick the pass' LDS swizzle rows H and every group's column bits (bank-conflict search)."""
+def _pair_score(H, vx: list, vy: list, rotation: bool) -> int:
+    """Conflict-free access patterns of a chained pair op (X, Y) under swizzle H.  A 32-lane half reads / writes
+    (x = 4 g4 + j, y = cl) or (x = cl, y = 4 g4 + j): 32 banks when X's bit-2 vector and Y's four vectors (or the
+    reverse) are independent in the 5 bank bits.  The forward pair (X, Y) reads the first pattern and writes the
+    second; the adjoint pair runs (Y, X) and reads and writes the second pattern, its ds_write2_b32 pairs in 16-lane
+    groups (X's four vectors independent in bank bits mod 16); a cross-only pair reads both patterns."""
+    bx, by = [_bank(H, v) for v in vx], [_bank(H, v) for v in vy]
+    a = int(_rank([bx[2]] + by) == 5)
+    b = int(_rank([by[2]] + bx) == 5)
+    if not rotation:
+        return a + b
+    return a + b + int(_rank([v & 15 for v in bx]) == 4)
+
+
+def layout_pass(plan: HEAPlan, p: Pass, seed: int = 0, tries: int = 256) -> None:
+    """Pick the pass' LDS swizzle rows H and every group's column bits (bank-conflict search), scoring the chained
+    pair ops the planner will form (``_pairs``) as well."""
     groups = p.groups + p.l1
     geoms = [_group_geom(plan, p, g) for g in groups]
+    vec = {(g.layer, tuple(g.qubits)): geo[0] for g, geo in zip(groups, geoms)}
+    pairs = [(u, True) for u in _pairs(plan, p, p.groups, True) if len(u) == 2]
+    pairs += [(u, False) for u in _pairs(plan, p, p.l1, True) if len(u) == 2]
+    full = FULL_SCORE * len(groups) + sum(3 if rot else 2 for _, rot in pairs)
     hb = max(p.t - BANK_BITS, 0)
     rng = np.random.default_rng(1234 + seed)
     best = None
@@ -502,12 +521,15 @@ def layout_pass(plan: HEAPlan, p: Pass, seed: int = 0, tries: int = 48) -> None:
             sc, c = _best_cols(H, allv, dirs, gi < len(p.groups))
             cols.append(c)
             score += sc
+        for (g, h), rot in pairs:
+            score += _pair_score(H, vec[(g.layer, tuple(g.qubits))], vec[(h.layer, tuple(h.qubits))], rot)
         if best is None or score > best[0]:
             best = (score, H, cols)
-        if score == FULL_SCORE * len(groups):
+        if score == full:
             break
     p.H = best[1]
     p.cols = {(g.layer, tuple(g.qubits)): c for g, c in zip(groups, best[2])}
+    p.layout_score = (best[0], full)
 
 
 def group_table(plan: HEAPlan, p: Pass, g: Group, code: int, flags: int = 0) -> np.ndarray:

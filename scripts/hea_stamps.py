@@ -36,7 +36,7 @@ def main():
     from qfedx_amd.models.vqc import VQCSpec
     from qfedx_amd.ops._ext import ext
     from qfedx_amd.ops.hea_mfma import HeaMfmaProgram
-    from qfedx_amd.ops.hea_plan import OP_BACK, OP_GRAD_L1, W_CODE
+    from qfedx_amd.ops.hea_plan import OP_BACK, OP_BACK2, OP_GRAD2, OP_GRAD_L1, W_CODE
 
     E = ext()
     assert getattr(E, "__name__", "").endswith("_stamps"), "needs the stamps build (QFEDX_STAMPS=1)"
@@ -68,8 +68,8 @@ def main():
             continue
         tot = rows[:, 15].mean()
         mean = {ph: float(rows[:, i].mean()) for i, ph in enumerate(PH)}
-        n_back = sum(c == OP_BACK for c in codes)
-        n_l1 = sum(c == OP_GRAD_L1 for c in codes)
+        n_back = sum(c in (OP_BACK, OP_BACK2) for c in codes)        # op records (a pair record = one body)
+        n_l1 = sum(c in (OP_GRAD_L1, OP_GRAD2) for c in codes)
         rec = {"pass": name, "t": p.t, "waves_per_wg": nw, "waves_stamped": int(len(rows)), "ops": len(codes),
                "op_codes": codes, "cycles_per_wave": round(tot), "phase_cycles": {k: round(v) for k, v in mean.items()},
                "phase_share": {k: round(v / tot, 4) for k, v in mean.items()},

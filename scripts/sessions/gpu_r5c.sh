@@ -18,3 +18,4 @@ step share8 300 python bench.py --steps 30 --warmup 5 --clients 8
 step ab_pair64 300 python -u scripts/hea_ab.py --rounds 7 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=7"
 step ab_pair8 300 python -u scripts/hea_ab.py --rounds 7 --clients 8 --iters 30 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=7"
 step stamps64 300 python -u scripts/hea_stamps.py --clients 64 --out gpurun_out/r5c/stamps64.jsonl
+step prof_bench 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5c/prof -o bench -- python3 bench.py --steps 10 --warmup 3

@@ -240,7 +240,7 @@ def test_pair_ops_match_unpaired_kernels(cuda, monkeypatch, n, L, tile):
     K, B = 3, 4
     x, params, wr = _inputs(spec, K, B, seed=n + L)
     xx, th, ww = x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda)
-    monkeypatch.setenv("QFEDX_HEA_PAIR", "1")
+    monkeypatch.setenv("QFEDX_HEA_PAIR", "7")
     pp = HeaMfmaProgram(spec, cuda, tile_bits=tile)
     codes = {int(c) for p in pp.passes for c in list(p[1][0][:, 0].cpu()) + list(p[2][0][:, 0].cpu())}
     assert codes & {2, 3}, codes
