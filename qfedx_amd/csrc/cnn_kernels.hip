@@ -129,13 +129,30 @@ __device__ __forceinline__ float relu_pool(f4 acc, float bias, int& arg) {
 //          w/2's last m-tile (window 48); the two halves are summed in fixed order afterwards.
 // --------------------------------------------------------------------------------------------
 constexpr int FSG = 4;             // samples per forward workgroup
-constexpr int CSF = 328;           // LDS stride of one padded 18x18 pool1 map (== 8 mod 32)
+constexpr int CSF = 336;           // LDS stride of one padded 18x18 pool1 map (== 16 mod 32, see fwd_win)
 constexpr int W2F = 402;           // LDS stride of W2 reordered as w2f[o][tap*16 + ci] (== 18 mod 32)
+constexpr int IRF = 46;            // LDS row stride of a padded forward image (32 used): conv1's A reads of 4
+                                   // windows x 2 rows x 2 taps average 1.19-way vs 2.24-way at stride 32
 static_assert(FSG * 2 == NW, "conv2 partial m-tile: one (sample, half) per wave");
+
+// conv2 (forward) m-tile slot (tile * 4 + j, slot 48 = the partial tile) -> pooled window wy * 7 + wx.  A 32-lane
+// half of an A read touches 4 windows x 4 positions of two channels CSF apart: with window origins o = 36 wy + 2 wx,
+// positions {0, 1, 18, 19} and CSF == 16 (mod 32) its 32 banks are distinct iff the 4 windows share the parity of wx
+// and have distinct (2 wy + wx) mod 8.  Tiles 0-6 are the even-wx windows of one row, tiles 7-11 the odd-wx triple
+// of rows 0-4 plus one odd window of rows 5 / 6 (packed 6-bit ids), window 43 = (6, 1) is left for the partial
+// tile.  In plain row order two windows of a tile collide and every A read of the round-4 kernel was 2-way
+// (PMC: 44% of the kernel's LDS cycles were conflict cycles).
+__device__ __forceinline__ int fwd_win(int slot) {
+  const int t = slot >> 2, j = slot & 3;
+  if (slot >= Q2 * Q2 - 1) return 43;
+  if (t < 7) return t * Q2 + 2 * j;
+  if (j < 3) return (t - 7) * Q2 + 2 * j + 1;
+  return (0x2D9A4BE8u >> (6 * (t - 7))) & 63;   // 40, 47, 36, 38, 45
+}
 
 // conv2 (forward) GEMM row -> offset of its 5x5 window origin in the padded 18-wide map
 __device__ __forceinline__ int fwd_q2(int row) {
-  const int w = min(row >> 2, Q2 * Q2 - 1), pos = row & 3;   // rows past window 48 clamp (dropped later)
+  const int w = fwd_win(min(row >> 2, Q2 * Q2 - 1)), pos = row & 3;   // rows past slot 48 clamp (dropped later)
   return (2 * (w / Q2) + (pos >> 1)) * P1P + 2 * (w % Q2) + (pos & 1);
 }
 
@@ -204,7 +221,7 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
   float* b1s = w1s + C1 * K1P;              // [16]
   float* b2s = b1s + C1;                    // [32]
   float* img = b2s + C2;                    // [FSG][32*32] zero-padded images
-  float* p1s = img + FSG * IMGP * IMGP;     // [FSG][16][328] zero-padded pool1
+  float* p1s = img + FSG * IMGP * IRF;      // [FSG][16][CSF] zero-padded pool1
   float* red = img;                         // [FSG][2 halves][32 o][4]: window-48 partials (images dead)
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -224,7 +241,7 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
   if (tid < C2) b2s[tid] = prow[off.b2 + tid];
   {
     constexpr int NU = FSG * IMGP * IMGP / NT;
-    static_assert(NU * NT == FSG * IMGP * IMGP, "whole image rows per thread");
+    static_assert(NU * NT == FSG * IMGP * IMGP && IMGP == 32, "whole image rows per thread");
     float v[NU];
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
@@ -233,7 +250,10 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
       v[u] = (s < ns && y >= 0 && y < IMG && x >= 0 && x < IMG) ? X[((size_t)k * B + s0 + s) * IMG * IMG + y * IMG + x] : 0.f;
     }
 #pragma unroll
-    for (int u = 0; u < NU; ++u) img[tid + u * NT] = v[u];
+    for (int u = 0; u < NU; ++u) {
+      const int e = tid + u * NT, r = e & (IMGP * IMGP - 1);
+      img[(e >> 10) * IMGP * IRF + (r >> 5) * IRF + (r & 31)] = v[u];
+    }
   }
   for (int e = tid; e < FSG * C1 * CSF; e += NT) p1s[e] = 0.f;
   __syncthreads();
@@ -246,7 +266,7 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
     for (int ks = 0; ks < K1P / 4; ++ks) {
       const int kk = ks * 4 + kq;
       bw[ks] = w1s[i * K1P + kk];
-      toff[ks] = kk < K1 ? (kk / 5) * IMGP + kk % 5 : 0;   // w1s is zero there
+      toff[ks] = kk < K1 ? (kk / 5) * IRF + kk % 5 : 0;   // w1s is zero there
     }
     const int nu = ns * 49;
     for (int u = wave; u < nu; u += 2 * NW) {
@@ -256,7 +276,7 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
       for (int h = 0; h < 2; ++h) {
         const int uu = h ? u1 : u, s = uu / 49, mt = uu - s * 49;
         const int w = mt * 4 + (i >> 2), pos = i & 3;
-        ub[h] = s * IMGP * IMGP + (2 * (w / Q1) + (pos >> 1)) * IMGP + 2 * (w % Q1) + (pos & 1);
+        ub[h] = s * IMGP * IRF + (2 * (w / Q1) + (pos >> 1)) * IRF + 2 * (w % Q1) + (pos & 1);
       }
       float av[2][K1P / 4];
 #pragma unroll
@@ -298,7 +318,7 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
     fwd_conv2<3>(sm, aoff, boff, 0, 25, acc);
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      const int wo = (mt0 + m) * 4 + kq;
+      const int wo = fwd_win((mt0 + m) * 4 + kq);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int o = h * 16 + i;
@@ -333,7 +353,7 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
     for (int r = 0; r < 4; ++r) v[r] = red[((s * 2) * C2 + o) * 4 + r] + red[((s * 2 + 1) * C2 + o) * 4 + r];
     int arg;
     const float best = relu_pool(v, b2s[o], arg);
-    const size_t so = ((size_t)k * B + s0 + s) * C2 * Q2 * Q2 + o * Q2 * Q2 + Q2 * Q2 - 1;
+    const size_t so = ((size_t)k * B + s0 + s) * C2 * Q2 * Q2 + o * Q2 * Q2 + fwd_win(Q2 * Q2 - 1);
     pool2[so] = best;
     am2[so] = (uint8_t)arg;
   }
@@ -1035,8 +1055,9 @@ __global__ void __launch_bounds__(256) cnn_eval_head(const float* __restrict__ h
   }
 }
 
+static_assert((C2 * W2F + C1 * K1P + C1 + C2 + FSG * IMGP * IRF + FSG * C1 * CSF) * 4 <= 160 * 1024, "cnn_fwd LDS");
 size_t fwd_lds() {
-  return (size_t)(C2 * W2F + C1 * K1P + C1 + C2 + FSG * IMGP * IMGP + FSG * C1 * CSF) * 4;
+  return (size_t)(C2 * W2F + C1 * K1P + C1 + C2 + FSG * IMGP * IRF + FSG * C1 * CSF) * 4;
 }
 size_t bwd_lds() {
   return (size_t)(C1 * W2R + (C2 + C1) * CS + 2 * C1 * DPS + 2 * IMGP * IMS + 256 + 256) * 4 + 2 * C1 * DPS;
