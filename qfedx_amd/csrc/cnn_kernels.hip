@@ -158,6 +158,8 @@ __device__ __forceinline__ int fwd_q2(int row) {
 
 // W2 [o][ci][tap] of one client row -> LDS at dst[o*so + ci*sc + tap*st]: all 25 loads of a thread are issued
 // before any store (a plain strided loop waits on each load in turn: one workgroup per CU hides nothing)
+// (PERM: channel o goes to column 4 (o % 8) + o / 8, the dgrad B layout of cnn_bwd)
+template <bool PERM = false>
 __device__ __forceinline__ void stage_w2(const float* __restrict__ w2g, float* dst, int so, int sc, int st, int tid) {
   constexpr int NU = (C2 * K2 + NT - 1) / NT;
   float v[NU];
@@ -171,7 +173,7 @@ __device__ __forceinline__ void stage_w2(const float* __restrict__ w2g, float* d
     const int e = tid + u * NT;
     if (e < C2 * K2) {
       const int o = e / K2, rem = e - o * K2, ci = rem / 25, r = rem - ci * 25;
-      dst[o * so + ci * sc + r * st] = v[u];
+      dst[(PERM ? 4 * (o & 7) + (o >> 3) : o) * so + ci * sc + r * st] = v[u];
     }
   }
 }
@@ -386,6 +388,22 @@ constexpr int IMS = 37;            // LDS row stride of the padded image
 constexpr int NT2 = 26;            // conv2 wgrad n-tiles (25 taps + ones)
 constexpr int PART = C2 * K2 + C2 + C1 * K1 + C1;
 
+// conv2 dgrad GEMM row (m-tile * 16 + row) -> dp1 pixel p = 14 y + x.  A 32-lane half of an A read touches 16 pixels
+// (lane i) of two channels 8 CS apart (o = oc + 8 kq; 8 CS == 16 mod 32): its banks are distinct iff the 16 pixels'
+// map offsets 18 y + x are distinct mod 16, i.e. (2 y + x) mod 16.  Tile t holds the t-th pixel (in row order) of
+// every residue class; rows 192..195 (partial m-tile 12) the four classes that have a 13th.  In plain row order
+// (16 consecutive pixels) every A read was 2-way (PMC: 29% of the kernel's LDS cycles were conflict cycles).
+__constant__ uint8_t kDgPix[H2 * H2] = {
+    0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 26, 27, 40, 41, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23,
+    24, 25, 38, 39, 52, 53, 54, 55, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 50, 51, 64, 65, 66, 67, 68, 69, 42, 43,
+    44, 45, 46, 47, 48, 49, 62, 63, 76, 77, 78, 79, 80, 81, 82, 83, 56, 57, 58, 59, 60, 61, 74, 75, 88, 89, 90, 91,
+    92, 93, 94, 95, 96, 97, 70, 71, 72, 73, 86, 87, 100, 101, 102, 103, 104, 105, 106, 107, 108, 109, 110, 111, 84, 85, 98, 99,
+    112, 113, 114, 115, 116, 117, 118, 119, 120, 121, 122, 123, 124, 125, 138, 139, 152, 153, 126, 127, 128, 129, 130, 131, 132, 133, 134, 135,
+    136, 137, 150, 151, 164, 165, 166, 167, 140, 141, 142, 143, 144, 145, 146, 147, 148, 149, 162, 163, 176, 177, 178, 179, 180, 181, 154, 155,
+    156, 157, 158, 159, 160, 161, 174, 175, 188, 189, 190, 191, 192, 193, 194, 195, 168, 169, 170, 171, 172, 173, 186, 187, 182, 183, 184, 185,
+};
+__device__ __forceinline__ int dg_pix(int row) { return kDgPix[min(row, H2 * H2 - 1)]; }
+
 // conv2 wgrad over the 49 k-steps of one sample: acc[j] += A(o rows) x B(n-tile j)
 template <int NJ>
 struct WgradSet {
@@ -428,7 +446,7 @@ __device__ __forceinline__ void bwd_dgrad2(const float* sm, const int (&aoff)[NM
         for (int m = 0; m < NM; ++m) {
           const float* ap = sm + (aoff[m] - ro);
 #pragma unroll
-          for (int oc = 0; oc < 8; ++oc) st.a[m][oc] = ap[4 * oc * CS];
+          for (int oc = 0; oc < 8; ++oc) st.a[m][oc] = ap[oc * CS];   // channel oc + 8 kq (kq in aoff)
         }
       },
       [&](const DgradSet<NM>& st) {
@@ -449,8 +467,8 @@ struct C1Set {
 __device__ __forceinline__ void bwd_dp1_store(float* dp1, const float* p1s, int mt, f4 acc, int i, int kq) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int p = mt * 16 + 4 * kq + r;
-    if (p < H2 * H2) dp1[i * DPS + p] = p1s[i * CS + q14(p) + 2 * P1P + 2] > 0.f ? acc[r] : 0.f;
+    const int row = mt * 16 + 4 * kq + r, p = dg_pix(row);
+    if (row < H2 * H2) dp1[i * DPS + p] = p1s[i * CS + q14(p) + 2 * P1P + 2] > 0.f ? acc[r] : 0.f;
   }
 }
 
@@ -526,7 +544,7 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
                                               const uint8_t* __restrict__ am2, const float* __restrict__ dP2,
                                               int bs, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* w2r = sm;                          // [16][802]: w2r[ci][tap*32 + o] = W2[o][ci][tap]
+  float* w2r = sm;                          // [16][802]: w2r[ci][tap*32 + 4 (o % 8) + o / 8] = W2[o][ci][tap]
   float* dc2 = w2r + C1 * W2R;              // [32][338] padded dL/d conv2-output (post-unpool, ReLU-masked)
   float* p1s = dc2 + C2 * CS;               // [16][338] padded pool1 (conv2 input)
   // conv1 wgrad of sample s runs during sample s+1's conv2 work: its inputs are double buffered (index s & 1)
@@ -544,7 +562,7 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
   const float* prow = params + (size_t)k * P;
   const int i = lane & 15, kq = lane >> 4;
 
-  stage_w2(prow + off.w2, w2r, 1, W2R, 32, tid);   // w2r[ci][tap*32 + o]
+  stage_w2<true>(prow + off.w2, w2r, 1, W2R, 32, tid);
   for (int e = tid; e < (C2 + C1) * CS; e += NT) dc2[e] = 0.f;   // dc2 and p1s are contiguous
   for (int e = tid; e < 2 * IMGP * IMS; e += NT) imgb[e] = 0.f;
   if (tid < 256) ones[tid] = 1.f;
@@ -563,7 +581,7 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
 #pragma unroll
   for (int j = 0; j < 7; ++j) wacc[j] = f4{0.f, 0.f, 0.f, 0.f};
   f4 c1acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-  const int dboff = (int)(w2r - sm) + i * W2R + kq;   // dgrad B: w2r[i][tap*32 + 4*oc + kq]
+  const int dboff = (int)(w2r - sm) + i * W2R + kq;   // dgrad B: w2r[i][tap*32 + 4*oc + kq] = W2[oc + 8 kq][i][tap]
   __syncthreads();
 
   // conv1 wgrad (dC1 = unpool1(dp1) on the fly; K = 784 split across the 8 waves) of one finished sample
@@ -608,21 +626,21 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
     // ---- conv2 dgrad -> dp1
     if (wave < 4) {
       const int mt0 = 2 * wave;
-      const int aoff[2] = {(int)(dc2 - sm) + kq * CS + q14(mt0 * 16 + i) + 4 * P1P + 4,
-                           (int)(dc2 - sm) + kq * CS + q14(mt0 * 16 + 16 + i) + 4 * P1P + 4};
+      const int aoff[2] = {(int)(dc2 - sm) + 8 * kq * CS + q14(dg_pix(mt0 * 16 + i)) + 4 * P1P + 4,
+                           (int)(dc2 - sm) + 8 * kq * CS + q14(dg_pix(mt0 * 16 + 16 + i)) + 4 * P1P + 4};
       f4 acc[2][2] = {};
       bwd_dgrad2<2>(sm, aoff, dboff, 0, 25, acc);
       bwd_dp1_store(dp1, p1s, mt0, acc[0][0] + acc[0][1], i, kq);
       bwd_dp1_store(dp1, p1s, mt0 + 1, acc[1][0] + acc[1][1], i, kq);
     } else {
       const int mt = 4 + wave;
-      const int aoff[1] = {(int)(dc2 - sm) + kq * CS + q14(mt * 16 + i) + 4 * P1P + 4};
+      const int aoff[1] = {(int)(dc2 - sm) + 8 * kq * CS + q14(dg_pix(mt * 16 + i)) + 4 * P1P + 4};
       f4 acc[1][2] = {};
       bwd_dgrad2<1>(sm, aoff, dboff, 0, 25, acc);
       bwd_dp1_store(dp1, p1s, mt, acc[0][0] + acc[0][1], i, kq);
       // m-tile 12: rows 192..195 valid (rows past 195 read a clamped in-range row and are dropped)
       const int w4 = wave - 4;
-      const int aoff12[1] = {(int)(dc2 - sm) + kq * CS + q14(min(192 + i, H2 * H2 - 1)) + 4 * P1P + 4};
+      const int aoff12[1] = {(int)(dc2 - sm) + 8 * kq * CS + q14(dg_pix(192 + i)) + 4 * P1P + 4};
       f4 acc12[1][2] = {};
       bwd_dgrad2<1>(sm, aoff12, dboff, w4 == 0 ? 0 : 1 + 6 * w4, 7 + 6 * w4, acc12);
       if (kq == 0) {
@@ -638,11 +656,12 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
     // m-tile 12 partials in fixed wave order -> dp1 rows 192..195.  The ReLU mask is read before the barrier:
     // after it the other waves may already restage p1s for the next sample.
     const int r12 = tid >> 4, ci12 = tid & 15;
-    const bool m12 = tid < 64 && p1s[ci12 * CS + q14(192 + r12) + 2 * P1P + 2] > 0.f;
+    const int p12 = dg_pix(192 + r12);
+    const bool m12 = tid < 64 && p1s[ci12 * CS + q14(p12) + 2 * P1P + 2] > 0.f;
     __syncthreads();
     if (tid < 64) {
       const float v = ((red12[tid] + red12[64 + tid]) + red12[128 + tid]) + red12[192 + tid];
-      dp1[ci12 * DPS + 192 + r12] = m12 ? v : 0.f;
+      dp1[ci12 * DPS + p12] = m12 ? v : 0.f;
     }
   }
   __syncthreads();   // the last sample's dp1 rows 192..195
