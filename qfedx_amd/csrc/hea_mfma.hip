@@ -1547,29 +1547,28 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
   const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
   if (g == n_gradops) {
-    // fused readout: the client's per-sample records summed in sample order (thread j sums samples j, j + 256, ...;
-    // then a fixed-order tree): loss, hits, and the readout gradients d/da_c = sum dl_c z_c, d/db_c = sum dl_c
+    // fused readout: the client's per-sample records summed in a fixed order - loss, hits, and the readout gradients
+    // d/da_c = sum dl_c z_c, d/db_c = sum dl_c.  Thread t < GS * NV sums value q = t % NV of samples t / NV + GS i
+    // (its loads are contiguous across threads and all in flight), then thread q sums the GS partials in order.
+    // (A loop over q with a load and a tree per value serialised NV global round trips: this block was the
+    // straggler of the 8-client reduction.)
     __shared__ float rs[256];
-    const int NV = 2 * ro.C + 2;
-    for (int q = 0; q < NV; ++q) {
-      float v = 0.f;
-      for (int j = tid; j < spc; j += 256) v += ro.rec[((size_t)k * spc + j) * NV + q];
-      rs[tid] = v;
-      __syncthreads();
-      for (int w = 128; w > 0; w >>= 1) {
-        if (tid < w) rs[tid] += rs[tid + w];
-        __syncthreads();
-      }
-      if (tid == 0) {
-        const float tot = rs[0];
-        if (q < 2 * ro.C)
-          grad[(size_t)k * p_stride + ro.n_theta + q] = tot;
-        else if (q == 2 * ro.C)
-          ro.loss[k] = tot;
-        else
-          ro.correct[k] = tot;
-      }
-      __syncthreads();
+    const int NV = 2 * ro.C + 2, GS = 256 / NV;
+    const float* rec = ro.rec + (size_t)k * spc * NV;
+    float v = 0.f;
+    if (tid < GS * NV)
+      for (int j = tid / NV; j < spc; j += GS) v += rec[j * NV + tid % NV];
+    rs[tid] = v;
+    __syncthreads();
+    if (tid < NV) {
+      float tot = 0.f;
+      for (int j = 0; j < GS; ++j) tot += rs[j * NV + tid];
+      if (tid < 2 * ro.C)
+        grad[(size_t)k * p_stride + ro.n_theta + tid] = tot;
+      else if (tid == 2 * ro.C)
+        ro.loss[k] = tot;
+      else
+        ro.correct[k] = tot;
     }
   } else {
     const int* m = gmeta + g * 10;

@@ -15,3 +15,10 @@ step gpu_tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeou
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step bench 600 python bench.py --steps 20 --warmup 3
 step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o bench -- python3 bench.py --steps 10 --warmup 2
+# end-of-round suite: every BASELINE config line (config 5 = vqc24q_ps256_mfma), 10 timed rounds each
+for c in cfed128 cfed128_epoch cfed128_secagg cfed128_secagg_sparse vqc16q_64_mfma vqc16q_64_mfma_secagg \
+         vqc16q_64_mfma_secagg_sparse vqc16q_bf16_8_mfma vqc16q_fp16_8_mfma vqc20q_dp64_mfma vqc20q_ddp64_mfma \
+         vqc24q_ps256_mfma vqc48q_mps64; do
+  step suite_$c 600 python bench_suite.py --config $c --steps 10 --warmup 2
+  grep '"metric"' gpurun_out/suite_$c.log >> gpurun_out/suite_lines.jsonl
+done
