@@ -4,3 +4,4 @@
 // fp32's exponent range, so the scale is harmless); the per-op rounding of the state is 2^-9 instead of 2^-12.
 #define QFX_HEA_BF16 1
 #include "hea_mfma.hip"
+#include "hea_step.hip"

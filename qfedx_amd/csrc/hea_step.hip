@@ -1,0 +1,213 @@
+// Per-step kernels of the MFMA statevector engine (passes: hea_mfma.hip): the unitary fragments of every (client,
+// slot) before a step, and the fixed-order gradient reduction of the pass kernels' slab (with the fused readout
+// sums and the optional fused Adam step).  hea_mfma_bf16.hip includes this file for the bf16 fragment build.
+#include "hea_common.h"
+
+namespace HEA_NS {
+
+// Unitary fragments: per (client, slot) U and U^H in the real 32 x 32 embedding, laid out as the MFMA
+// A operand of v_mfma_f32_16x16x32_f16 (lane l: row 16h + (l & 15), k = 8 (l >> 4) .. +7), hi and lo fp16.
+// Rows are ordered (component, amplitude): row 16 h + m' is the re (h = 0) or im (h = 1) part of output m'.
+// The same registers are the B operand of the transposed product X^T M^T (group_back_t).
+// frags[((k * n_slots + slot) * 4 + f) * 128 + h * 64 + lane], f = 0 U hi, 1 U lo, 2 U^H hi, 3 U^H lo.
+__global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__ params, int p_stride,
+                                                       const int* __restrict__ slot_tab, int n_slots,
+                                                       uint4* __restrict__ frags) {
+  const int slot = blockIdx.x, k = blockIdx.y;
+  const int t = threadIdx.x, dag = t >> 7, h = (t >> 6) & 1, lane = t & 63;
+  const int* st = slot_tab + slot * 9;
+  const int nreal = st[0];
+  const float* prm = params + (size_t)k * p_stride;
+  // per qubit j: RZ(ph) RX(th) = [[e- c, -i e- s], [-i e+ s, e+ c]], e-+ = cp -+ i sp (identity past nreal)
+  float cj[4], sj[4], cpj[4], spj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    cj[j] = 1.f, sj[j] = 0.f, cpj[j] = 1.f, spj[j] = 0.f;
+    if (j < nreal) {
+      __sincosf(0.5f * prm[st[1 + j]], &sj[j], &cj[j]);
+      __sincosf(0.5f * prm[st[5 + j]], &spj[j], &cpj[j]);
+    }
+  }
+  // real output row r = 16 h + (lane & 15) is component cr = h (0 re, 1 im) of amplitude m' = lane & 15: a block's
+  // result then holds the re and im of one amplitude in the same register of its two 16-row tiles
+  st_t hi[8], lo[8];
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int kk = 8 * (lane >> 4) + jj;
+    const int mp = lane & 15, cr = h, m = kk >> 1, ck = kk & 1;
+    const int row = dag ? m : mp, colm = dag ? mp : m;   // U^H[mp][m] = conj(U[m][mp])
+    float2 v = make_float2(1.f, 0.f);
+    // entry (row_j, col_j) of qubit j's 2 x 2 factor, formed arithmetically (a run-time index into a table of
+    // the four entries put it in scratch): diagonal (cp c, +-sp c), off-diagonal (+-sp s, -cp s), sign + for row 1
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool rb = (row >> j) & 1, cb = (colm >> j) & 1;
+      const float e = rb ? spj[j] : -spj[j];
+      const float2 f = rb == cb ? make_float2(cpj[j] * cj[j], e * cj[j]) : make_float2(e * sj[j], -cpj[j] * sj[j]);
+      v = cmul(v, f);
+    }
+    if (dag) v.y = -v.y;
+    const float val = cr == 0 ? (ck == 0 ? v.x : -v.y) : (ck == 0 ? v.y : v.x);
+    hi[jj] = (st_t)val;
+    lo[jj] = (st_t)(val - (float)hi[jj]);
+  }
+  uint4 H, Lw;
+  uint32_t* hp = (uint32_t*)&H;
+  uint32_t* lp = (uint32_t*)&Lw;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    half2v a2 = {hi[2 * i], hi[2 * i + 1]}, b2 = {lo[2 * i], lo[2 * i + 1]};
+    hp[i] = __builtin_bit_cast(uint32_t, a2);
+    lp[i] = __builtin_bit_cast(uint32_t, b2);
+  }
+  uint4* base = frags + ((size_t)(k * n_slots + slot) * 4 + 2 * dag) * 128;
+  base[h * 64 + lane] = H;
+  base[128 + h * 64 + lane] = Lw;
+}
+
+// Per client and gradient op: exact int64 sums of the 32 partial-trace slots over the client's samples and
+// the op's tiles, then per real qubit j (slots 8j + 4y + 2x + comp = n_j[y][x].(re, im))
+//   d/dtheta = Im(e^{-i phi} n10 + e^{i phi} n01),   d/dphi = Im(n00 - n11).
+//
+// Optional Adam epilogue (ad.m != nullptr; the local optimizer step fused into this launch): the last of a client's
+// gridDim.y blocks to finish - arrival counter ad.cnt[k], reset by that block - updates the client's parameter row
+// from the complete gradient row, with the element update of qfx_adam_kernel (qfx_adam.h): bitwise the separate
+// launch.  The arrivals are the n_gradops gradient-record blocks PLUS, with the fused readout, the g == n_gradops
+// block that writes the readout-parameter gradients: the Adam step must wait for all gridDim.y = n_gradops + 1 of
+// them (the launcher sizes the grid so).  Every block has read its parameters before it arrives.
+#if !QFX_HEA_BF16
+__global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* __restrict__ gslab, int slab_tiles,
+                                                              int n_gradops, const int* __restrict__ gmeta, int spc,
+                                                              float* __restrict__ params,
+                                                              float* __restrict__ grad, int p_stride, QfxAdamArgs ad,
+                                                              QfxReadoutRed ro) {
+  // 8 groups of 32 lanes split the client's (sample, tile) rows; 4 independent loads in flight per lane; the
+  // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
+  const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
+  if (g == n_gradops) {
+    // fused readout: the client's per-sample records summed in a fixed order - loss, hits, and the readout gradients
+    // d/da_c = sum dl_c z_c, d/db_c = sum dl_c.  Thread t < GS * NV sums value q = t % NV of samples t / NV + GS i
+    // (its loads are contiguous across threads and all in flight), then thread q sums the GS partials in order.
+    // (A loop over q with a load and a tree per value serialised NV global round trips: this block was the
+    // straggler of the 8-client reduction.)
+    __shared__ float rs[256];
+    const int NV = 2 * ro.C + 2, GS = 256 / NV;
+    const float* rec = ro.rec + (size_t)k * spc * NV;
+    float v = 0.f;
+    if (tid < GS * NV)
+      for (int j = tid / NV; j < spc; j += GS) v += rec[j * NV + tid % NV];
+    rs[tid] = v;
+    __syncthreads();
+    if (tid < NV) {
+      float tot = 0.f;
+      for (int j = 0; j < GS; ++j) tot += rs[j * NV + tid];
+      if (tid < 2 * ro.C)
+        grad[(size_t)k * p_stride + ro.n_theta + tid] = tot;
+      else if (tid == 2 * ro.C)
+        ro.loss[k] = tot;
+      else
+        ro.correct[k] = tot;
+    }
+  } else {
+    const int* m = gmeta + g * 10;
+    // m[1]: nreal in bits 0..3; bit 4 = cross matrix taken at the op INPUT (transposed BACK ops)
+    const int nt = m[0], nreal = m[1] & 15, inside = (m[1] >> 4) & 1;
+    const int R = spc * nt;
+    __shared__ long long part[8][32];
+    __shared__ double pt[32];
+    long long acc[4] = {0, 0, 0, 0};
+    auto row = [&](int r) -> long long {
+      const int s = k * spc + r / nt, t = r % nt;
+      return gslab[(((size_t)s * slab_tiles + t) * n_gradops + g) * 32 + lane];
+    };
+    int r = grp;
+    for (; r + 24 < R; r += 32) {
+      acc[0] += row(r);
+      acc[1] += row(r + 8);
+      acc[2] += row(r + 16);
+      acc[3] += row(r + 24);
+    }
+    for (; r < R; r += 8) acc[0] += row(r);
+    part[grp][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    __syncthreads();
+    if (tid < 32) {
+      long long v = 0;
+      for (int j = 0; j < 8; ++j) v += part[j][tid];
+      pt[tid] = (double)v / FIX;
+    }
+    __syncthreads();
+    if (tid < nreal) {
+      const double* p = pt + 8 * tid;
+      const float* prm = params + (size_t)k * p_stride;
+      if (inside) {
+        // at the op input: d/dtheta = Im<lam|X|psi> = Im(n01 + n10);
+        // d/dphi = Im<lam|RX^H Z RX|psi> = cos(theta) Im(n00 - n11) + sin(theta) Re(n01 - n10)
+        const double th = prm[m[2 + tid]];
+        const double ct = cos(th), st = sin(th);
+        grad[(size_t)k * p_stride + m[2 + tid]] = (float)(p[3] + p[5]);
+        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
+      } else {
+        const double ph = prm[m[6 + tid]];
+        const double cp = cos(ph), sp = sin(ph);
+        grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
+        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
+      }
+    }
+  }
+  if (!ad.m) return;
+  __shared__ int last_s;
+  // The block's gradient stores are complete in L2 after the barrier; ONE agent-scope release (thread 0) makes
+  // them visible across XCDs before the arrival.  A release is an L2 writeback on this chip: issued by every
+  // thread it made the launch 7x slower (16q x 64 clients: 13 -> 98 us).
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(&ad.cnt[k], 1u);
+    last_s = prev == (unsigned)(gridDim.y - 1);
+    if (last_s) ad.cnt[k] = 0u;                       // ready for the next launch
+  }
+  __syncthreads();
+  if (!last_s) return;
+  if (tid == 0) {                                     // consumer side: one agent-scope acquire, drained
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  for (int i = tid; i < p_stride; i += 256) {
+    const long e = (long)k * p_stride + i;
+    // device-coherent load: other blocks (other CUs) wrote these entries
+    const float gi = __hip_atomic_load(&grad[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    qfx_adam_elem(params, gi, ad.m, ad.v, ad.t_in, ad.t_out, ad.active, k, e, i == 0, ad.lr, ad.b1, ad.b2, ad.eps);
+  }
+}
+#endif  // !QFX_HEA_BF16
+
+}  // namespace HEA_NS
+
+extern "C" int HEA_EXT(qfx_hea_frags)(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
+                             hipStream_t st) {
+  if (n_slots == 0 || K == 0) return 0;
+  hipLaunchKernelGGL(HEA_NS::hea_frag_kernel, dim3(n_slots, K), dim3(256), 0, st, params, p_stride, slot_tab, n_slots,
+                     (uint4*)frags);
+  return (int)hipGetLastError();
+}
+
+#if !QFX_HEA_BF16
+extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc,
+                                   int K, float* params, float* grad, int p_stride, const QfxAdamArgs* adam,
+                                   const QfxReadoutRed* readout, hipStream_t st) {
+  if (K == 0) return 0;
+  QfxReadoutRed ro{};
+  if (readout) ro = *readout;
+  const int rows = n_gradops + (ro.rec ? 1 : 0);
+  if (rows == 0) return adam && adam->m ? (int)hipErrorInvalidValue : 0;   // no block would run the epilogue
+  QfxAdamArgs ad{};
+  if (adam) ad = *adam;
+  hipLaunchKernelGGL(HEA_NS::hea_grad_reduce_kernel, dim3(K, rows), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
+                     gmeta, spc, params, grad, p_stride, ad, ro);
+  return (int)hipGetLastError();
+}
+
+extern "C" int qfx_hea_args_size() { return (int)sizeof(HEA_NS::PassArgs); }
+#endif  // !QFX_HEA_BF16
+
