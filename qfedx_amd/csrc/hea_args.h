@@ -43,6 +43,17 @@ struct HeaPassArgs {
   float* ro_rec;
 };
 
+// Chained passes in one launch (hea_fwd_chain / hea_adj_chain): npass pass argument blocks run as one dataflow
+// over per-sample completion counters; pass j's blocks are items [start[j], start[j + 1]).  sync: a zeroed device
+// buffer of 3 + (npass - 1) * S words owned by the caller (layout in hea_mfma.hip, chain_begin).
+constexpr int HEA_MAXCHAIN = 4;
+struct HeaChainArgs {
+  HeaPassArgs p[HEA_MAXCHAIN];
+  int start[HEA_MAXCHAIN + 1];
+  int npass, S;
+  unsigned* sync;
+};
+
 // Launch arguments of a fused Adam epilogue (m == nullptr: none).  cnt: one zero-initialised arrival counter per
 // client (the client's last block resets it).
 struct QfxAdamArgs {

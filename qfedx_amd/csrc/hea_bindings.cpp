@@ -15,6 +15,7 @@
 
 extern "C" {
 int qfx_hea_pass(int adjoint, const HeaPassArgs* args, int n_samples, hipStream_t st);
+int qfx_hea_chain(int adjoint, const HeaChainArgs* chain, hipStream_t st);
 int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                   hipStream_t st);
 int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc, int K,
@@ -24,6 +25,7 @@ int qfx_hea_args_size();
 int qfx_hea_check_status(hipStream_t st);
 // bf16 state storage (hea_mfma_bf16.hip)
 int qfx_hea_pass_bf16(int adjoint, const HeaPassArgs* args, int n_samples, hipStream_t st);
+int qfx_hea_chain_bf16(int adjoint, const HeaChainArgs* chain, hipStream_t st);
 int qfx_hea_frags_bf16(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                        hipStream_t st);
 int qfx_hea_check_status_bf16(hipStream_t st);
@@ -66,7 +68,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
               torch::Tensor psi_out, torch::Tensor lam_in, torch::Tensor lam_out, torch::Tensor xang,
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
               torch::Tensor gslab, torch::Tensor dbg, c10::optional<std::vector<torch::Tensor>> readout,
-              int64_t ro_tps) {
+              int64_t ro_tps, c10::optional<torch::Tensor> chain, int64_t chain_idx) {
   need(geom.size() == 28, "geometry vector must have 28 entries");
   const bool bf16 = geom[27] != 0;
   HeaPassArgs a{};
@@ -149,10 +151,42 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.gslab = adjoint ? dp<long long>(gslab, torch::kInt64, "gslab", S * a.slab_tiles * a.n_gradops * 32) : nullptr;
   need(!adjoint || a.slab_tiles >= a.n_tiles, "gradient slab has fewer tiles than the pass");
   need(!a.gen || a.n <= 32, "product-state generation supports <= 32 qubits");
+  if (chain && chain->defined()) {   // staged for hea_chain (one launch for several passes), not launched here
+    need(!chain->is_cuda() && chain->scalar_type() == torch::kUInt8 && chain->is_contiguous() &&
+             chain->numel() >= (int64_t)sizeof(HeaChainArgs) && chain_idx >= 0 && chain_idx < HEA_MAXCHAIN,
+         "chain: host uint8 buffer of sizeof(HeaChainArgs), index < HEA_MAXCHAIN");
+    reinterpret_cast<HeaChainArgs*>(chain->data_ptr<uint8_t>())->p[chain_idx] = a;
+    return;
+  }
   if (bf16)
     check(qfx_hea_pass_bf16(adjoint ? 1 : 0, &a, (int)S, cur()), "qfx_hea_pass_bf16");
   else
     check(qfx_hea_pass(adjoint ? 1 : 0, &a, (int)S, cur()), "qfx_hea_pass");
+}
+
+// Launch the npass passes staged in `chain` (hea_pass(..., chain, j)) as one dataflow launch over S samples.  sync:
+// zeroed int32 device words, 3 + (npass - 1) S of them, private to this chain shape (hea_mfma.hip, chain_begin).
+// Returns the sync word counting dependency waits that gave up (nonzero = the launch's numbers are wrong) only when
+// `check` is set (it synchronises the stream).
+int64_t hea_chain(bool adjoint, torch::Tensor chain, int64_t npass, int64_t S, torch::Tensor sync, bool bf16, bool check_sync) {
+  need(!chain.is_cuda() && chain.scalar_type() == torch::kUInt8 && chain.numel() >= (int64_t)sizeof(HeaChainArgs),
+       "chain: host uint8 buffer of sizeof(HeaChainArgs)");
+  need(npass >= 1 && npass <= HEA_MAXCHAIN, "1..HEA_MAXCHAIN chained passes");
+  HeaChainArgs c = *reinterpret_cast<const HeaChainArgs*>(chain.data_ptr<uint8_t>());
+  c.npass = (int)npass;
+  c.S = (int)S;
+  c.start[0] = 0;
+  for (int j = 0; j < npass; ++j) {
+    need(c.p[j].ops != nullptr || c.p[j].nops == 0, "chain: pass not staged");
+    c.start[j + 1] = c.start[j] + (int)(S * c.p[j].n_tiles);
+  }
+  c.sync = reinterpret_cast<unsigned*>(dp<int32_t>(sync, torch::kInt32, "sync", 3 + (npass - 1) * S));
+  if (bf16)
+    check(qfx_hea_chain_bf16(adjoint ? 1 : 0, &c, cur()), "qfx_hea_chain_bf16");
+  else
+    check(qfx_hea_chain(adjoint ? 1 : 0, &c, cur()), "qfx_hea_chain");
+  if (!check_sync) return 0;
+  return sync.narrow(0, 2, 1).cpu().item<int32_t>();
 }
 
 // Validate a pass program once (host copy) when it is built: slot / gradient-slot ranges and op kinds.
@@ -260,7 +294,11 @@ void register_hea(pybind11::module& m) {
         pybind11::arg("geom"), pybind11::arg("scale"), pybind11::arg("psi_in"), pybind11::arg("psi_out"),
         pybind11::arg("lam_in"), pybind11::arg("lam_out"), pybind11::arg("xang"), pybind11::arg("params"),
         pybind11::arg("frags"), pybind11::arg("wread"), pybind11::arg("part"), pybind11::arg("gslab"),
-        pybind11::arg("dbg"), pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_tps") = 0);
+        pybind11::arg("dbg"), pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_tps") = 0,
+        pybind11::arg("chain") = pybind11::none(), pybind11::arg("chain_idx") = 0);
+  m.def("hea_chain", &hea_chain, pybind11::arg("adjoint"), pybind11::arg("chain"), pybind11::arg("npass"),
+        pybind11::arg("S"), pybind11::arg("sync"), pybind11::arg("bf16") = false, pybind11::arg("check") = false);
+  m.attr("HEA_CHAIN_BYTES") = (int)sizeof(HeaChainArgs);
   m.def("hea_frags", &hea_frags, pybind11::arg("params"), pybind11::arg("p_stride"), pybind11::arg("slot_tab"),
         pybind11::arg("n_slots"), pybind11::arg("K"), pybind11::arg("frags"), pybind11::arg("bf16") = false);
   m.def("hea_check_ops", &hea_check_ops);

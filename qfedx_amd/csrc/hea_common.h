@@ -155,10 +155,10 @@ struct Stamps {
     }
   }
   // lane 0 of every wave of the first STAMP_WG workgroups writes its row
-  __device__ __forceinline__ void write(long long* dbg, int nw, int wave, int lane) {
+  __device__ __forceinline__ void write(long long* dbg, int bid, int nw, int wave, int lane) {
     if constexpr (QFX_HEA_STAMPS) {
-      if (!dbg || blockIdx.x >= (unsigned)STAMP_WG || lane != 0) return;
-      long long* row = dbg + ((size_t)blockIdx.x * nw + wave) * NPH;
+      if (!dbg || bid >= STAMP_WG || lane != 0) return;
+      long long* row = dbg + ((size_t)bid * nw + wave) * NPH;
 #pragma unroll
       for (int i = 0; i <= PH_TAIL; ++i) row[i] = (long long)acc[i];
       row[NPH - 2] = nops;

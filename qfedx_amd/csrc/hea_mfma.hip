@@ -825,8 +825,9 @@ __device__ __forceinline__ uint32_t op_fo_global(const int* ow, uint32_t fixed) 
 // ------------------------------------------------------------------------------------------- forward pass
 // One workgroup per tile of 2^t <= 2^14 amplitudes: 8 waves and 64 KB of LDS, so two workgroups share a CU and
 // one's tile load overlaps the other's group ops (minimum waves per SIMD 4: <= 128 VGPRs).
+// (a device function: the plain launch runs one pass, hea_fwd_chain several; bid = the pass' block index)
 template <int NCK, bool FULL>
-__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
+__device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
   constexpr int NT = NT_FWD, NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint32_t psi_t[1 << TMAX];   // fp16 (re, im), swizzled
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
@@ -841,7 +842,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int s = blockIdx.x / a.n_tiles, tile_id = blockIdx.x % a.n_tiles;
+  const int s = bid / a.n_tiles, tile_id = bid % a.n_tiles;
   const int k = s / a.spc;
   // in_rep > 1: in_rep consecutive parameter rows (clients) share each input sample - a parameter-shift branch
   // starts from the stored unshifted state of its client's sample (sample s reads input row s_in)
@@ -995,7 +996,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
   lds_barrier();
   if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
   st.mark(PH_TAIL);
-  st.write(a.dbg, NW, wave, lane);
+  st.write(a.dbg, bid, NW, wave, lane);
 }
 
 // ------------------------------------------------------------------------------------------- adjoint pass
@@ -1012,7 +1013,7 @@ __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) {
 // 2^(TB - 10) waves give each wave 4 column blocks per op (a 4-wave 2^13 workgroup with 8 blocks per wave halves the
 // per-op setup per MFMA but halves the waves per SIMD: measured 18% slower, round 4).
 template <int NCK, int TB, bool FULL>
-__global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_adj_kernel(PassArgs a) {
+__device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
   constexpr int NT = 1 << (TB - 4), NW = NT / 64;
   static_assert(NW % 2 == 0 && (1 << (TB - 8)) % NW == 0, "column blocks per wave must be whole, block pairs aligned");
   // (psi, lambda) pairs (fp16 re, im), swizzled; 16-byte aligned for the b64 / b128 accesses
@@ -1031,7 +1032,7 @@ __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int s = blockIdx.x / a.n_tiles, tile_id = blockIdx.x % a.n_tiles;
+  const int s = bid / a.n_tiles, tile_id = bid % a.n_tiles;
   const int k = s / a.spc;
   const int T = 1 << a.t;
   const size_t N = (size_t)1 << a.n;
@@ -1292,38 +1293,144 @@ __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_
   }
   if (a.store_lam) store_lam_il<NT, TB>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
   st.mark(PH_TAIL);
-  st.write(a.dbg, NW, wave, lane);
+  st.write(a.dbg, bid, NW, wave, lane);
+}
+
+// ------------------------------------------------------------------------------------------- launches
+template <int NCK, bool FULL>
+__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) { fwd_pass<NCK, FULL>(a, blockIdx.x); }
+
+template <int NCK, int TB, bool FULL>
+__global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_adj_kernel(PassArgs a) {
+  adj_pass<NCK, TB, FULL>(a, blockIdx.x);
+}
+
+// Chained passes: the forward passes (or the adjoint passes) of one step in ONE launch, a dataflow over per-sample
+// completion counters instead of a kernel boundary per pass.  A block takes the next work item from a ticket counter
+// (items in pass order, so every item a block waits for was taken earlier by a running block: no deadlock), waits
+// until all tiles of its sample in the previous pass are done, and runs the pass body.  The next pass' first tiles
+// thus start while the previous pass' last ones drain, and a step has one launch per direction (at the 8-client share
+// the passes run 2 / 4 generations of workgroups, so each pass boundary left the chip ramping down and up).
+//   sync[0] ticket, sync[1] finished blocks, sync[2] spin timeouts (a wait past ~1 s gives up: wrong numbers and a
+//   nonzero word, never a hang), sync[3 + j S + s] finished tiles of pass j for sample s.  The launch's last block
+//   zeroes every counter but sync[2] (the buffer starts zeroed).
+// A producer publishes its tile / slab stores with one agent-scope release (its tile lives in another XCD's L2) and
+// its consumers acquire before loading.
+__device__ __forceinline__ int chain_begin(const HeaChainArgs& c, int& pj) {
+  __shared__ int item_s[2];
+  if (threadIdx.x == 0) {
+    const int item = (int)atomicAdd(&c.sync[0], 1u);
+    int j = 0;
+    while (j + 1 < c.npass && item >= c.start[j + 1]) ++j;
+    if (j > 0) {
+      const int s = (item - c.start[j]) / c.p[j].n_tiles;
+      const unsigned* cnt = c.sync + 3 + (size_t)(j - 1) * c.S + s;
+      const unsigned need = (unsigned)c.p[j - 1].n_tiles;
+      for (int it = 0; __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need; ++it) {
+        if (it == (1 << 24)) {
+          atomicAdd(&c.sync[2], 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    item_s[0] = item - c.start[j];
+    item_s[1] = j;
+  }
+  __syncthreads();
+  pj = item_s[1];
+  return item_s[0];
+}
+
+__device__ __forceinline__ void chain_end(const HeaChainArgs& c, int j, int bid) {
+  __shared__ int last_s;
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile / slab stores complete in L2
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();                                     // one agent-scope release for the block
+    if (j + 1 < c.npass) atomicAdd(&c.sync[3 + (size_t)j * c.S + bid / c.p[j].n_tiles], 1u);
+    last_s = atomicAdd(&c.sync[1], 1u) == (unsigned)c.start[c.npass] - 1u;
+  }
+  __syncthreads();
+  if (!last_s) return;
+  const int nc = 3 + (c.npass - 1) * c.S;                // every other block has finished: reset for the next launch
+  for (int e = threadIdx.x; e < nc; e += blockDim.x)
+    if (e != 2) c.sync[e] = 0u;
+}
+
+template <int NCK, bool FULL>
+__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_chain(HeaChainArgs c) {
+  int j;
+  const int bid = chain_begin(c, j);
+  fwd_pass<NCK, FULL>(c.p[j], bid);
+  chain_end(c, j, bid);
+}
+
+template <int NCK, int TB, bool FULL>
+__global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_adj_chain(HeaChainArgs c) {
+  int j;
+  const int bid = chain_begin(c, j);
+  adj_pass<NCK, TB, FULL>(c.p[j], bid);
+  chain_end(c, j, bid);
 }
 
 }  // namespace HEA_NS
 
+// adjoint: 2^13 tiles (8 waves, two workgroups per CU) up to t = 13, else one 16-wave 2^14 workgroup per CU
+#define HEA_LAUNCH(NCK, KF, KA, ARG)                                                                         \
+  do {                                                                                                      \
+    if (!adjoint && t == HEA_NS::TMAX)                                                                       \
+      hipLaunchKernelGGL((HEA_NS::KF<NCK, true>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, ARG);             \
+    else if (!adjoint)                                                                                      \
+      hipLaunchKernelGGL((HEA_NS::KF<NCK, false>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, ARG);            \
+    else if (t <= 13)                                                                                       \
+      hipLaunchKernelGGL((HEA_NS::KA<NCK, 13, false>), dim3(grid), dim3(512), 0, st, ARG);                   \
+    else                                                                                                    \
+      hipLaunchKernelGGL((HEA_NS::KA<NCK, 14, true>), dim3(grid), dim3(1024), 0, st, ARG);                   \
+  } while (0)
+#define HEA_SWITCH(KF, KA, ARG)                 \
+  switch (HEA_NS::class_kernel(C)) {            \
+    case 1: HEA_LAUNCH(1, KF, KA, ARG); break;  \
+    case 2: HEA_LAUNCH(2, KF, KA, ARG); break;  \
+    case 3: HEA_LAUNCH(3, KF, KA, ARG); break;  \
+    case 4: HEA_LAUNCH(4, KF, KA, ARG); break;  \
+    default: HEA_LAUNCH(8, KF, KA, ARG); break; \
+  }
+
+static bool hea_args_ok(const HEA_NS::PassArgs& a) {
+  return !(a.t > HEA_NS::TMAX || a.t < 8 || a.C > HEA_NS::CMAX || a.n > 30 || a.c < 2);
+}
+
 extern "C" int HEA_EXT(qfx_hea_pass)(int adjoint, const HEA_NS::PassArgs* args, int n_samples, hipStream_t st) {
   const HEA_NS::PassArgs& a = *args;
-  if (a.t > HEA_NS::TMAX || a.t < 8 || a.C > HEA_NS::CMAX || a.n > 30 || a.c < 2) return -2;
+  if (!hea_args_ok(a)) return -2;
   const unsigned grid = (unsigned)(n_samples * a.n_tiles);
   if (grid == 0) return 0;
-  // adjoint: 2^13 tiles (8 waves, two workgroups per CU) up to t = 13, else one 16-wave 2^14 workgroup per CU
-#define HEA_LAUNCH(NCK)                                                                                      \
-  do {                                                                                                      \
-    if (!adjoint && a.t == HEA_NS::TMAX)                                                                     \
-      hipLaunchKernelGGL((HEA_NS::hea_fwd_kernel<NCK, true>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);        \
-    else if (!adjoint)                                                                                      \
-      hipLaunchKernelGGL((HEA_NS::hea_fwd_kernel<NCK, false>), dim3(grid), dim3(HEA_NS::NT_FWD), 0, st, a);       \
-    else if (a.t <= 13)                                                                                     \
-      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 13, false>), dim3(grid), dim3(512), 0, st, a);         \
-    else                                                                                                    \
-      hipLaunchKernelGGL((HEA_NS::hea_adj_kernel<NCK, 14, true>), dim3(grid), dim3(1024), 0, st, a);         \
-  } while (0)
-  switch (HEA_NS::class_kernel(a.C)) {
-    case 1: HEA_LAUNCH(1); break;
-    case 2: HEA_LAUNCH(2); break;
-    case 3: HEA_LAUNCH(3); break;
-    case 4: HEA_LAUNCH(4); break;
-    default: HEA_LAUNCH(8); break;
-  }
-#undef HEA_LAUNCH
+  const int t = a.t, C = a.C;
+  HEA_SWITCH(hea_fwd_kernel, hea_adj_kernel, a);
   return (int)hipGetLastError();
 }
+
+// Chained passes (one launch): every pass must select the same kernel instance (direction, tile class, class count).
+extern "C" int HEA_EXT(qfx_hea_chain)(int adjoint, const HeaChainArgs* chain, hipStream_t st) {
+  const HeaChainArgs& c = *chain;
+  if (c.npass < 1 || c.npass > HEA_MAXCHAIN || !c.sync || c.start[0] != 0) return -2;
+  const int t = c.p[0].t, C = c.p[0].C;
+  for (int j = 0; j < c.npass; ++j) {
+    const HEA_NS::PassArgs& a = c.p[j];
+    const bool same = adjoint ? ((a.t <= 13) == (t <= 13)) : ((a.t == HEA_NS::TMAX) == (t == HEA_NS::TMAX));
+    if (!hea_args_ok(a) || !same || HEA_NS::class_kernel(a.C) != HEA_NS::class_kernel(C) ||
+        c.start[j + 1] - c.start[j] != c.S * a.n_tiles)
+      return -2;
+  }
+  const unsigned grid = (unsigned)c.start[c.npass];
+  if (grid == 0) return 0;
+  HEA_SWITCH(hea_fwd_chain, hea_adj_chain, c);
+  return (int)hipGetLastError();
+}
+#undef HEA_SWITCH
+#undef HEA_LAUNCH
 
 
 // Debug build: synchronise the stream and return (and clear) the first failed device-check line, 0 if none;

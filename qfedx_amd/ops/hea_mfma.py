@@ -61,6 +61,13 @@ _NODBG = torch.zeros(0, dtype=torch.int64)     # no stall-attribution buffer (st
 
 
 FUSED_ADAM_MAX_BLOCKS = 256   # hea_grad_reduce blocks (clients x gradient ops) up to which Adam is fused
+HEA_MAXCHAIN = 4              # passes per chained launch (csrc/hea_args.h)
+
+
+def _chain_default() -> bool:
+    """Chained pass launches (hea_chain: one dataflow launch per direction instead of one per pass);
+    ``QFEDX_HEA_CHAIN=0`` launches every pass on its own."""
+    return os.environ.get("QFEDX_HEA_CHAIN", "1") != "0"
 
 
 class HeaMfmaProgram:
@@ -149,6 +156,8 @@ class HeaMfmaProgram:
         self.feature = _FEATURE[spec.feature_map.lower()]
         self._ws = {}
         self._ps_budget = None
+        self.chain = _chain_default()
+        self._chain_args = {}     # host staging buffers of the chained launches (HeaChainArgs bytes)
         if self.device.type == "cuda":
             self._shift_budget()      # query free HBM now, never inside a graph capture
 
@@ -210,18 +219,22 @@ class HeaMfmaProgram:
         empty = torch.empty(0, dtype=torch.int32, device=self.device)
         fempty = torch.empty(0, dtype=torch.float32, device=self.device)
         J, R = self.n_passes, self.fwd_last
+        chain = self._chain_buf("f", [self.passes[j][0] for j in range(R + 1)], False)
         for j in range(R + 1):
             p, fwd = self.passes[j][0], self.passes[j][1]
             keep = j < R or store_last
-            # evaluation only needs the previous pass output: two ping-pong buffers instead of one per pass
-            name = f"{tag}psi{j}" if store_last else f"{tag}pe{j % 2}"
+            # evaluation only needs the previous pass output: two ping-pong buffers instead of one per pass (a chained
+            # launch keeps every pass output: pass j + 1 may start while pass j - 1's output is still being read)
+            name = f"{tag}psi{j}" if (store_last or chain is not None) else f"{tag}pe{j % 2}"
             out = self._buf(name, N, torch.int32) if keep else empty
             psi_in = stored[-1] if j > 0 else empty
             geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K)
             C.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
-                       part if j == R else fempty, fempty, dbg[f"fwd{j}"] if dbg else _NODBG)
+                       part if j == R else fempty, fempty, dbg[f"fwd{j}"] if dbg else _NODBG, None, 0, chain, j)
             if keep:
                 stored.append(out)
+        if chain is not None:
+            C.hea_chain(False, chain, R + 1, S, self._zbuf(f"{tag}fsync", 3 + R * S, torch.int32), self.bf16)
         if store_last:
             stored += [stored[R]] * (J - 1 - R)
         return stored
@@ -237,19 +250,40 @@ class HeaMfmaProgram:
         fempty = torch.empty(0, dtype=torch.float32, device=self.device)
         J = self.n_passes
         lam_in = empty
-        for j in range(J - 1, -1, -1):
+        chain = self._chain_buf("a", [self.passes[j][3] for j in range(J - 1, -1, -1)], True)
+        for i, j in enumerate(range(J - 1, -1, -1)):
             _, _, adj, p = self.passes[j]
-            lam_out = self._buf(f"{tag}lam{j % 2}", N, torch.int32) if j > 0 else empty
+            # (chained: one lambda buffer per pass, as in the forward)
+            lam_out = self._buf(f"{tag}lam{j if chain is not None else j % 2}", N, torch.int32) if j > 0 else empty
             geom = self._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, x.shape[1], K)
             if readout is not None and j == J - 1:
                 part, yy, ww, expz, rec = readout
                 C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
                            params, fr, fempty, part, gslab, dbg[f"adj{j}"] if dbg else _NODBG,
-                           [yy, ww, expz, wread, rec], self.tiles_last)
+                           [yy, ww, expz, wread, rec], self.tiles_last, chain, i)
             else:
                 C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
-                           params, fr, wread, fempty, gslab, dbg[f"adj{j}"] if dbg else _NODBG)
+                           params, fr, wread, fempty, gslab, dbg[f"adj{j}"] if dbg else _NODBG, None, 0, chain, i)
             lam_in = lam_out
+        if chain is not None:
+            C.hea_chain(True, chain, J, S, self._zbuf(f"{tag}async", 3 + (J - 1) * S, torch.int32), self.bf16)
+
+    def chain_timeouts(self) -> int:
+        """Dependency waits of chained launches that gave up (sync word 2 of every chain's counters; must be 0)."""
+        return sum(int(t[2]) for name, t in self._ws.items() if name.endswith(("fsync", "async")) and t.numel() > 2)
+
+    def _chain_buf(self, kind: str, ps: list, adjoint: bool):
+        """Host staging buffer for a chained launch of passes ``ps`` (in launch order), or None when they launch one
+        by one: chaining off, a single pass, more than HEA_MAXCHAIN, or passes of different kernel instances."""
+        if not self.chain or not (2 <= len(ps) <= HEA_MAXCHAIN):
+            return None
+        cls = {p.t <= 13 for p in ps} if adjoint else {p.t == 14 for p in ps}
+        if len(cls) != 1:
+            return None
+        buf = self._chain_args.get(kind)
+        if buf is None:
+            buf = self._chain_args[kind] = torch.zeros(int(ext().HEA_CHAIN_BYTES), dtype=torch.uint8)
+        return buf
 
     def _prep(self, xang, params):
         K, B, F = xang.shape
