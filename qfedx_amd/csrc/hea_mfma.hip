@@ -46,18 +46,45 @@ __device__ __forceinline__ uint4 quad_perm(uint4 v, uint32_t r) {
   return v;
 }
 
+// Global tile words of one sample.  CH (chained launches, hea_fwd_chain / hea_adj_chain): a tile crosses workgroups -
+// and XCDs - inside one launch, so its copies are write-through sc1 stores and L1-bypassing sc1 loads through a buffer
+// descriptor: no release or acquire fence on either side (cdna_hip_programming.md Guideline 16, R1).  An agent-scope
+// release per producer block (an L2 writeback) and an acquire per consumer made the chained launches 1.8x slower.
+template <bool CH>
+struct GTile {
+  const uint32_t* base;
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ GTile(const uint32_t* b, size_t words) : base(b) {
+    if constexpr (CH) {   // descriptor from provably wave-uniform words (no waterfall loop around each access)
+      const uint64_t u = (uint64_t)(uintptr_t)b;
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+      r = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)(words * 4),
+                                            0x00020000);
+    }
+  }
+  __device__ __forceinline__ uint4 ld(uint32_t w) const {
+    if constexpr (CH) return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(w * 4), 0, 16));
+    else return *(const uint4*)&base[w];
+  }
+  __device__ __forceinline__ void st(uint32_t w, uint4 v) const {
+    if constexpr (CH) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, (int)(w * 4), 0, 16);
+    else *(uint4*)&base[w] = v;
+  }
+};
+
 // Global [mem order] <-> LDS [swizzled] tile copies: quad q = 4 (tid + NT i) of the tile sits at LDS dword
 // (q ^ h) & ~3 with its dwords permuted by h & 3, h = h(q >> 5) = h(tid >> 3) ^ h(4 NT / 32 * i).  All of a
 // thread's global loads are issued before its LDS writes.
-template <int NT, int TB = TMAX>
+template <int NT, int TB = TMAX, bool CH = false>
 __device__ __forceinline__ void load_tile(const PassArgs& a, const uint32_t* src, uint32_t* dst, int tid, int T,
                                           uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
+  const GTile<CH> g(src, (size_t)1 << a.n);
   uint4 v[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) v[i] = *(const uint4*)&src[mem_of(q, a, fixed)];
+    if (q < (uint32_t)T) v[i] = g.ld(mem_of(q, a, fixed));
   }
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -69,10 +96,11 @@ __device__ __forceinline__ void load_tile(const PassArgs& a, const uint32_t* src
   }
 }
 
-template <int NT, int TB = TMAX>
+template <int NT, int TB = TMAX, bool CH = false>
 __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, const uint32_t* src, int tid, int T,
                                            uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
+  const GTile<CH> g(dst, (size_t)1 << a.n);
   uint4 v[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -85,7 +113,7 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
+    if (q < (uint32_t)T) g.st(mem_of(q, a, fixed), v[i]);
   }
 }
 
@@ -94,17 +122,18 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
 // issue rate, not bandwidth, bounds this kernel: PMC WAIT_INST_LDS), at a v_mov per dword splitting the pairs into
 // MFMA operands.  (Separate psi / lambda planes halve the bank conflicts but double the LDS instructions: measured
 // slower, round 3.)  Without a lambda input the lambda words are zeroed (the observable op writes them).
-template <int NT, int TB>
+template <int NT, int TB, bool CH = false>
 __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* psrc, const uint32_t* lsrc,
                                              uint32_t* tile, int tid, int T, uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
+  const GTile<CH> gp(psrc, (size_t)1 << a.n), gl(lsrc, (size_t)1 << a.n);
   uint4 v[MQ], l[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
     if (q < (uint32_t)T) {
-      v[i] = *(const uint4*)&psrc[mem_of(q, a, fixed)];
-      l[i] = lsrc ? *(const uint4*)&lsrc[mem_of(q, a, fixed)] : make_uint4(0u, 0u, 0u, 0u);
+      v[i] = gp.ld(mem_of(q, a, fixed));
+      l[i] = lsrc ? gl.ld(mem_of(q, a, fixed)) : make_uint4(0u, 0u, 0u, 0u);
     }
   }
 #pragma unroll
@@ -120,10 +149,11 @@ __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* 
   }
 }
 
-template <int NT, int TB>
+template <int NT, int TB, bool CH = false>
 __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, const uint32_t* tile, int tid, int T,
                                              uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
+  const GTile<CH> g(dst, (size_t)1 << a.n);
   uint4 v[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -138,7 +168,7 @@ __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, c
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
+    if (q < (uint32_t)T) g.st(mem_of(q, a, fixed), v[i]);
   }
 }
 
@@ -826,7 +856,7 @@ __device__ __forceinline__ uint32_t op_fo_global(const int* ow, uint32_t fixed) 
 // One workgroup per tile of 2^t <= 2^14 amplitudes: 8 waves and 64 KB of LDS, so two workgroups share a CU and
 // one's tile load overlaps the other's group ops (minimum waves per SIMD 4: <= 128 VGPRs).
 // (a device function: the plain launch runs one pass, hea_fwd_chain several; bid = the pass' block index)
-template <int NCK, bool FULL>
+template <int NCK, bool FULL, bool CH>
 __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
   constexpr int NT = NT_FWD, NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint32_t psi_t[1 << TMAX];   // fp16 (re, im), swizzled
@@ -937,7 +967,7 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
       if (4 * q < (uint32_t)T) *(uint4*)&psi_t[4 * q] = out[i];
     }
   } else {
-    load_tile<NT>(a, a.psi_in + (size_t)s_in * N, psi_t, tid, T, h_q, fixed);
+    load_tile<NT, TMAX, CH>(a, a.psi_in + (size_t)s_in * N, psi_t, tid, T, h_q, fixed);
   }
 
   // ---------------------------------------------------------------- op list
@@ -994,7 +1024,7 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
     if constexpr (QFX_HEA_STAMPS) ++st.nops;
   }
   lds_barrier();
-  if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
+  if (a.store_psi) store_tile<NT, TMAX, CH>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
   st.mark(PH_TAIL);
   st.write(a.dbg, bid, NW, wave, lane);
 }
@@ -1012,7 +1042,7 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
 // round trip and was slower (16q adjoint 0.67 -> 0.72 ms).
 // 2^(TB - 10) waves give each wave 4 column blocks per op (a 4-wave 2^13 workgroup with 8 blocks per wave halves the
 // per-op setup per MFMA but halves the waves per SIMD: measured 18% slower, round 4).
-template <int NCK, int TB, bool FULL>
+template <int NCK, int TB, bool FULL, bool CH>
 __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
   constexpr int NT = 1 << (TB - 4), NW = NT / 64;
   static_assert(NW % 2 == 0 && (1 << (TB - 8)) % NW == 0, "column blocks per wave must be whole, block pairs aligned");
@@ -1068,8 +1098,8 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
     }
   }
   st.mark(PH_PRO);
-  load_tile_il<NT, TB>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T, h_q,
-                       fixed);
+  load_tile_il<NT, TB, CH>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
+                           h_q, fixed);
 
   if (a.ro_fuse ? tid == NT - 64 : tid == 0) {
     float wv[CMAX];
@@ -1100,7 +1130,10 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
         wv[c] = dl[c] * ra[c];
         if (out) {
           a.ro_expz[(size_t)s * a.C + c] = z[c];
-          a.ro_w[(size_t)s * a.C + c] = wv[c];
+          if constexpr (CH)   // read by this launch's later passes (write-through, as the tiles)
+            __hip_atomic_store(&a.ro_w[(size_t)s * a.C + c], wv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            a.ro_w[(size_t)s * a.C + c] = wv[c];
           rec[c] = dl[c] * z[c];
           rec[a.C + c] = dl[c];
         }
@@ -1113,7 +1146,8 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
 #pragma unroll
       for (int c = 0; c < CMAX; ++c) {
         if (c >= a.C) break;
-        wv[c] = a.wread[(size_t)s * a.C + c];
+        wv[c] = CH ? __hip_atomic_load(&a.wread[(size_t)s * a.C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                   : a.wread[(size_t)s * a.C + c];
       }
     }
     float rho = 0.f;
@@ -1291,18 +1325,18 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
   } else {
     for (int e = tid; e < ngrad * 32; e += NT) reduce_region(e >> 5, e & 31);
   }
-  if (a.store_lam) store_lam_il<NT, TB>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
+  if (a.store_lam) store_lam_il<NT, TB, CH>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
   st.mark(PH_TAIL);
   st.write(a.dbg, bid, NW, wave, lane);
 }
 
 // ------------------------------------------------------------------------------------------- launches
 template <int NCK, bool FULL>
-__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) { fwd_pass<NCK, FULL>(a, blockIdx.x); }
+__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) { fwd_pass<NCK, FULL, false>(a, blockIdx.x); }
 
 template <int NCK, int TB, bool FULL>
 __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_adj_kernel(PassArgs a) {
-  adj_pass<NCK, TB, FULL>(a, blockIdx.x);
+  adj_pass<NCK, TB, FULL, false>(a, blockIdx.x);
 }
 
 // Chained passes: the forward passes (or the adjoint passes) of one step in ONE launch, a dataflow over per-sample
@@ -1314,8 +1348,9 @@ __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_
 //   sync[0] ticket, sync[1] finished blocks, sync[2] spin timeouts (a wait past ~1 s gives up: wrong numbers and a
 //   nonzero word, never a hang), sync[3 + j S + s] finished tiles of pass j for sample s.  The launch's last block
 //   zeroes every counter but sync[2] (the buffer starts zeroed).
-// A producer publishes its tile / slab stores with one agent-scope release (its tile lives in another XCD's L2) and
-// its consumers acquire before loading.
+// Hand-off without fences (cdna guide Guideline 16, R1): a producer's handed-off bytes (its tile, and the fused
+// readout's dL/d<Z>) are sc1 write-through stores that every wave drains before the block's barrier, then ONE lane adds
+// to the counter; the consumer polls it relaxed and reads those bytes only with sc1 loads.
 __device__ __forceinline__ int chain_begin(const HeaChainArgs& c, int& pj) {
   __shared__ int item_s[2];
   if (threadIdx.x == 0) {
@@ -1333,7 +1368,9 @@ __device__ __forceinline__ int chain_begin(const HeaChainArgs& c, int& pj) {
         }
         __builtin_amdgcn_s_sleep(2);
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      // every load of handed-off bytes is an sc1 load (GTile<true>, wread): no agent acquire, only keep the
+      // compiler from hoisting loads above the poll
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     item_s[0] = item - c.start[j];
     item_s[1] = j;
@@ -1345,10 +1382,10 @@ __device__ __forceinline__ int chain_begin(const HeaChainArgs& c, int& pj) {
 
 __device__ __forceinline__ void chain_end(const HeaChainArgs& c, int j, int bid) {
   __shared__ int last_s;
-  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's tile / slab stores complete in L2
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 tile stores complete (every storing wave)
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();                                     // one agent-scope release for the block
+    // the tile went out by write-through sc1 stores, drained by every wave above
     if (j + 1 < c.npass) atomicAdd(&c.sync[3 + (size_t)j * c.S + bid / c.p[j].n_tiles], 1u);
     last_s = atomicAdd(&c.sync[1], 1u) == (unsigned)c.start[c.npass] - 1u;
   }
@@ -1363,7 +1400,7 @@ template <int NCK, bool FULL>
 __global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_chain(HeaChainArgs c) {
   int j;
   const int bid = chain_begin(c, j);
-  fwd_pass<NCK, FULL>(c.p[j], bid);
+  fwd_pass<NCK, FULL, true>(c.p[j], bid);
   chain_end(c, j, bid);
 }
 
@@ -1371,7 +1408,7 @@ template <int NCK, int TB, bool FULL>
 __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_adj_chain(HeaChainArgs c) {
   int j;
   const int bid = chain_begin(c, j);
-  adj_pass<NCK, TB, FULL>(c.p[j], bid);
+  adj_pass<NCK, TB, FULL, true>(c.p[j], bid);
   chain_end(c, j, bid);
 }
 
@@ -1420,7 +1457,7 @@ extern "C" int HEA_EXT(qfx_hea_chain)(int adjoint, const HeaChainArgs* chain, hi
   for (int j = 0; j < c.npass; ++j) {
     const HEA_NS::PassArgs& a = c.p[j];
     const bool same = adjoint ? ((a.t <= 13) == (t <= 13)) : ((a.t == HEA_NS::TMAX) == (t == HEA_NS::TMAX));
-    if (!hea_args_ok(a) || !same || HEA_NS::class_kernel(a.C) != HEA_NS::class_kernel(C) ||
+    if (!hea_args_ok(a) || !same || a.n > 28 ||   // (buffer descriptors span one sample: < 2^31 bytes) HEA_NS::class_kernel(a.C) != HEA_NS::class_kernel(C) ||
         c.start[j + 1] - c.start[j] != c.S * a.n_tiles)
       return -2;
   }

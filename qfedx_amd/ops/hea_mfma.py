@@ -275,7 +275,7 @@ class HeaMfmaProgram:
     def _chain_buf(self, kind: str, ps: list, adjoint: bool):
         """Host staging buffer for a chained launch of passes ``ps`` (in launch order), or None when they launch one
         by one: chaining off, a single pass, more than HEA_MAXCHAIN, or passes of different kernel instances."""
-        if not self.chain or not (2 <= len(ps) <= HEA_MAXCHAIN):
+        if not self.chain or not (2 <= len(ps) <= HEA_MAXCHAIN) or self.n > 28:
             return None
         cls = {p.t <= 13 for p in ps} if adjoint else {p.t == 14 for p in ps}
         if len(cls) != 1:

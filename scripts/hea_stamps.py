@@ -79,9 +79,18 @@ def main():
                           "EPI": round(mean["EPI"] / max(1, n_back + n_l1)) if (n_back + n_l1) else None},
                # barrier wait spread: the slowest wave of a workgroup waits least
                "bar_wave_p10_p90": [round(float(np.percentile(rows[:, 2], 10))), round(float(np.percentile(rows[:, 2], 90)))]}
+        # per wave index (which waves the others wait for at the barriers): mean cycles of each phase
+        ww = buf.view(-1, nw, 16).cpu().numpy().astype(np.float64)
+        ww = ww[ww[:, :, 15].min(axis=1) > 0]
+        rec["per_wave"] = {ph: [round(float(v)) for v in ww[:, :, i].mean(axis=0)] for i, ph in enumerate(PH)
+                           if ww[:, :, i].mean() > 0}
         lines.append(rec)
         print(json.dumps(rec), flush=True)
     print()
+    for r in lines:
+        print(f"{r['pass']} per wave index (mean cycles):")
+        for ph, v in r["per_wave"].items():
+            print(f"  {ph:7s} " + " ".join(f"{x:6d}" for x in v))
     print(f"{'pass':6s} {'cyc/wave':>9s} " + " ".join(f"{ph:>7s}" for ph in PH))
     for r in lines:
         print(f"{r['pass']:6s} {r['cycles_per_wave']:9d} " + " ".join(f"{100 * r['phase_share'][ph]:6.1f}%" for ph in PH))
