@@ -8,7 +8,8 @@ constexpr int HEA_STAMP_ROWS = 2048 * 16;
 
 struct HeaPassArgs {
   const int* ops;            // [nops][128] op records (hea_plan.py)
-  const int* fidx;           // [nops] unitary fragment index (slot * 4 + 0 | 2) or -1
+  const int* fidx;           // [nops][2] unitary fragment indices (slot * 4 + 0 | 2) or -1
+  const uint32_t* fo_tab;    // [n_tiles][nops] per-op OFF base of each tile (hea_plan.fo_table)
   int nops;
   int n, t, c, lo, hi, n_tiles;   // tile = memory bits [0, c) u [lo, hi), 2^(n - t) tiles per sample
   int gen, load_lam, store_psi, store_lam;
@@ -28,6 +29,7 @@ struct HeaPassArgs {
   long long* gslab;          // [S][slab_tiles][n_gradops][32] 2^-32 fixed-point partial traces
   int slab_tiles;
   int n_gradops;
+  int n_regions;             // adjoint: gradient records of this pass program (LDS partial-trace regions it fills)
   int hrow[5];               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
   long long* dbg;            // stamps build only (QFX_HEA_STAMPS): per-wave phase cycles, [HEA_STAMP_ROWS][16]
   int in_rep;                // forward: shifted parameter rows per stored input sample (param-shift prefix reuse)
@@ -41,17 +43,6 @@ struct HeaPassArgs {
   float* ro_expz;
   float* ro_w;
   float* ro_rec;
-};
-
-// Chained passes in one launch (hea_fwd_chain / hea_adj_chain): npass pass argument blocks run as one dataflow
-// over per-sample completion counters; pass j's blocks are items [start[j], start[j + 1]).  sync: a zeroed device
-// buffer of 3 + (npass - 1) * S words owned by the caller (layout in hea_mfma.hip, chain_begin).
-constexpr int HEA_MAXCHAIN = 4;
-struct HeaChainArgs {
-  HeaPassArgs p[HEA_MAXCHAIN];
-  int start[HEA_MAXCHAIN + 1];
-  int npass, S;
-  unsigned* sync;
 };
 
 // Launch arguments of a fused Adam epilogue (m == nullptr: none).  cnt: one zero-initialised arrival counter per

@@ -15,7 +15,6 @@
 
 extern "C" {
 int qfx_hea_pass(int adjoint, const HeaPassArgs* args, int n_samples, hipStream_t st);
-int qfx_hea_chain(int adjoint, const HeaChainArgs* chain, hipStream_t st);
 int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                   hipStream_t st);
 int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc, int K,
@@ -25,7 +24,6 @@ int qfx_hea_args_size();
 int qfx_hea_check_status(hipStream_t st);
 // bf16 state storage (hea_mfma_bf16.hip)
 int qfx_hea_pass_bf16(int adjoint, const HeaPassArgs* args, int n_samples, hipStream_t st);
-int qfx_hea_chain_bf16(int adjoint, const HeaChainArgs* chain, hipStream_t st);
 int qfx_hea_frags_bf16(const float* params, int p_stride, const int* slot_tab, int n_slots, int K, void* frags,
                        hipStream_t st);
 int qfx_hea_check_status_bf16(hipStream_t st);
@@ -61,15 +59,16 @@ void check(int rc, const char* what) {
 }
 
 // geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
-//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, bf16]
+//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, bf16, n_regions]
 // bf16: states and fragments in bf16 (hea_mfma_bf16.hip) instead of fp16.  dbg: the stall-attribution buffer of the
 // stamps build (int64 [HEA_STAMP_ROWS * 16]; empty otherwise)
-void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<int64_t> geom, double scale, torch::Tensor psi_in,
+void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, torch::Tensor fo, std::vector<int64_t> geom, double scale,
+              torch::Tensor psi_in,
               torch::Tensor psi_out, torch::Tensor lam_in, torch::Tensor lam_out, torch::Tensor xang,
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
               torch::Tensor gslab, torch::Tensor dbg, c10::optional<std::vector<torch::Tensor>> readout,
-              int64_t ro_tps, c10::optional<torch::Tensor> chain, int64_t chain_idx) {
-  need(geom.size() == 28, "geometry vector must have 28 entries");
+              int64_t ro_tps) {
+  need(geom.size() == 29, "geometry vector must have 29 entries");
   const bool bf16 = geom[27] != 0;
   HeaPassArgs a{};
   a.n = (int)geom[0];
@@ -94,6 +93,8 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   const int64_t K = geom[19];
   a.n_gradops = (int)geom[25];
   a.in_rep = (int)geom[26];
+  a.n_regions = (int)geom[28];
+  need(a.n_regions >= 0 && a.n_regions <= 2 * 32, "gradient regions per pass out of range");
   a.scale = (float)scale;
   a.dbg = dbg.defined() && dbg.numel() > 0 ? dp<long long>(dbg, torch::kInt64, "dbg", (int64_t)HEA_STAMP_ROWS * 16)
                                            : nullptr;
@@ -114,6 +115,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   need(a.nops <= 32, "at most 32 ops per pass program");
   a.ops = dp<int>(ops, torch::kInt32, "ops", 0);
   a.fidx = a.nops ? dp<int>(fidx, torch::kInt32, "fidx", 2 * a.nops) : nullptr;
+  a.fo_tab = a.nops ? reinterpret_cast<const uint32_t*>(dp<int>(fo, torch::kInt32, "fo", (int64_t)a.n_tiles * a.nops)) : nullptr;
   need(a.in_rep >= 1 && (!adjoint || a.in_rep == 1) && K % a.in_rep == 0,
        "in_rep: forward only, parameter rows a multiple of it");
   const int64_t states = S << a.n;
@@ -151,42 +153,10 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, std::vector<i
   a.gslab = adjoint ? dp<long long>(gslab, torch::kInt64, "gslab", S * a.slab_tiles * a.n_gradops * 32) : nullptr;
   need(!adjoint || a.slab_tiles >= a.n_tiles, "gradient slab has fewer tiles than the pass");
   need(!a.gen || a.n <= 32, "product-state generation supports <= 32 qubits");
-  if (chain && chain->defined()) {   // staged for hea_chain (one launch for several passes), not launched here
-    need(!chain->is_cuda() && chain->scalar_type() == torch::kUInt8 && chain->is_contiguous() &&
-             chain->numel() >= (int64_t)sizeof(HeaChainArgs) && chain_idx >= 0 && chain_idx < HEA_MAXCHAIN,
-         "chain: host uint8 buffer of sizeof(HeaChainArgs), index < HEA_MAXCHAIN");
-    reinterpret_cast<HeaChainArgs*>(chain->data_ptr<uint8_t>())->p[chain_idx] = a;
-    return;
-  }
   if (bf16)
     check(qfx_hea_pass_bf16(adjoint ? 1 : 0, &a, (int)S, cur()), "qfx_hea_pass_bf16");
   else
     check(qfx_hea_pass(adjoint ? 1 : 0, &a, (int)S, cur()), "qfx_hea_pass");
-}
-
-// Launch the npass passes staged in `chain` (hea_pass(..., chain, j)) as one dataflow launch over S samples.  sync:
-// zeroed int32 device words, 3 + (npass - 1) S of them, private to this chain shape (hea_mfma.hip, chain_begin).
-// Returns the sync word counting dependency waits that gave up (nonzero = the launch's numbers are wrong) only when
-// `check` is set (it synchronises the stream).
-int64_t hea_chain(bool adjoint, torch::Tensor chain, int64_t npass, int64_t S, torch::Tensor sync, bool bf16, bool check_sync) {
-  need(!chain.is_cuda() && chain.scalar_type() == torch::kUInt8 && chain.numel() >= (int64_t)sizeof(HeaChainArgs),
-       "chain: host uint8 buffer of sizeof(HeaChainArgs)");
-  need(npass >= 1 && npass <= HEA_MAXCHAIN, "1..HEA_MAXCHAIN chained passes");
-  HeaChainArgs c = *reinterpret_cast<const HeaChainArgs*>(chain.data_ptr<uint8_t>());
-  c.npass = (int)npass;
-  c.S = (int)S;
-  c.start[0] = 0;
-  for (int j = 0; j < npass; ++j) {
-    need(c.p[j].ops != nullptr || c.p[j].nops == 0, "chain: pass not staged");
-    c.start[j + 1] = c.start[j] + (int)(S * c.p[j].n_tiles);
-  }
-  c.sync = reinterpret_cast<unsigned*>(dp<int32_t>(sync, torch::kInt32, "sync", 3 + (npass - 1) * S));
-  if (bf16)
-    check(qfx_hea_chain_bf16(adjoint ? 1 : 0, &c, cur()), "qfx_hea_chain_bf16");
-  else
-    check(qfx_hea_chain(adjoint ? 1 : 0, &c, cur()), "qfx_hea_chain");
-  if (!check_sync) return 0;
-  return sync.narrow(0, 2, 1).cpu().item<int32_t>();
 }
 
 // Validate a pass program once (host copy) when it is built: slot / gradient-slot ranges and op kinds.
@@ -290,15 +260,11 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
 }  // namespace
 
 void register_hea(pybind11::module& m) {
-  m.def("hea_pass", &hea_pass, pybind11::arg("adjoint"), pybind11::arg("ops"), pybind11::arg("fidx"),
+  m.def("hea_pass", &hea_pass, pybind11::arg("adjoint"), pybind11::arg("ops"), pybind11::arg("fidx"), pybind11::arg("fo"),
         pybind11::arg("geom"), pybind11::arg("scale"), pybind11::arg("psi_in"), pybind11::arg("psi_out"),
         pybind11::arg("lam_in"), pybind11::arg("lam_out"), pybind11::arg("xang"), pybind11::arg("params"),
         pybind11::arg("frags"), pybind11::arg("wread"), pybind11::arg("part"), pybind11::arg("gslab"),
-        pybind11::arg("dbg"), pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_tps") = 0,
-        pybind11::arg("chain") = pybind11::none(), pybind11::arg("chain_idx") = 0);
-  m.def("hea_chain", &hea_chain, pybind11::arg("adjoint"), pybind11::arg("chain"), pybind11::arg("npass"),
-        pybind11::arg("S"), pybind11::arg("sync"), pybind11::arg("bf16") = false, pybind11::arg("check") = false);
-  m.attr("HEA_CHAIN_BYTES") = (int)sizeof(HeaChainArgs);
+        pybind11::arg("dbg"), pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_tps") = 0);
   m.def("hea_frags", &hea_frags, pybind11::arg("params"), pybind11::arg("p_stride"), pybind11::arg("slot_tab"),
         pybind11::arg("n_slots"), pybind11::arg("K"), pybind11::arg("frags"), pybind11::arg("bf16") = false);
   m.def("hea_check_ops", &hea_check_ops);

@@ -46,45 +46,18 @@ __device__ __forceinline__ uint4 quad_perm(uint4 v, uint32_t r) {
   return v;
 }
 
-// Global tile words of one sample.  CH (chained launches, hea_fwd_chain / hea_adj_chain): a tile crosses workgroups -
-// and XCDs - inside one launch, so its copies are write-through sc1 stores and L1-bypassing sc1 loads through a buffer
-// descriptor: no release or acquire fence on either side (cdna_hip_programming.md Guideline 16, R1).  An agent-scope
-// release per producer block (an L2 writeback) and an acquire per consumer made the chained launches 1.8x slower.
-template <bool CH>
-struct GTile {
-  const uint32_t* base;
-  __amdgpu_buffer_rsrc_t r;
-  __device__ __forceinline__ GTile(const uint32_t* b, size_t words) : base(b) {
-    if constexpr (CH) {   // descriptor from provably wave-uniform words (no waterfall loop around each access)
-      const uint64_t u = (uint64_t)(uintptr_t)b;
-      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
-      r = __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0, (int)(words * 4),
-                                            0x00020000);
-    }
-  }
-  __device__ __forceinline__ uint4 ld(uint32_t w) const {
-    if constexpr (CH) return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(w * 4), 0, 16));
-    else return *(const uint4*)&base[w];
-  }
-  __device__ __forceinline__ void st(uint32_t w, uint4 v) const {
-    if constexpr (CH) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), r, (int)(w * 4), 0, 16);
-    else *(uint4*)&base[w] = v;
-  }
-};
-
 // Global [mem order] <-> LDS [swizzled] tile copies: quad q = 4 (tid + NT i) of the tile sits at LDS dword
 // (q ^ h) & ~3 with its dwords permuted by h & 3, h = h(q >> 5) = h(tid >> 3) ^ h(4 NT / 32 * i).  All of a
 // thread's global loads are issued before its LDS writes.
-template <int NT, int TB = TMAX, bool CH = false>
+template <int NT, int TB = TMAX>
 __device__ __forceinline__ void load_tile(const PassArgs& a, const uint32_t* src, uint32_t* dst, int tid, int T,
                                           uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
-  const GTile<CH> g(src, (size_t)1 << a.n);
   uint4 v[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) v[i] = g.ld(mem_of(q, a, fixed));
+    if (q < (uint32_t)T) v[i] = *(const uint4*)&src[mem_of(q, a, fixed)];
   }
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -96,11 +69,10 @@ __device__ __forceinline__ void load_tile(const PassArgs& a, const uint32_t* src
   }
 }
 
-template <int NT, int TB = TMAX, bool CH = false>
+template <int NT, int TB = TMAX>
 __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, const uint32_t* src, int tid, int T,
                                            uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
-  const GTile<CH> g(dst, (size_t)1 << a.n);
   uint4 v[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -113,7 +85,7 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) g.st(mem_of(q, a, fixed), v[i]);
+    if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
   }
 }
 
@@ -122,18 +94,17 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
 // issue rate, not bandwidth, bounds this kernel: PMC WAIT_INST_LDS), at a v_mov per dword splitting the pairs into
 // MFMA operands.  (Separate psi / lambda planes halve the bank conflicts but double the LDS instructions: measured
 // slower, round 3.)  Without a lambda input the lambda words are zeroed (the observable op writes them).
-template <int NT, int TB, bool CH = false>
+template <int NT, int TB>
 __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* psrc, const uint32_t* lsrc,
                                              uint32_t* tile, int tid, int T, uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
-  const GTile<CH> gp(psrc, (size_t)1 << a.n), gl(lsrc, (size_t)1 << a.n);
   uint4 v[MQ], l[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
     if (q < (uint32_t)T) {
-      v[i] = gp.ld(mem_of(q, a, fixed));
-      l[i] = lsrc ? gl.ld(mem_of(q, a, fixed)) : make_uint4(0u, 0u, 0u, 0u);
+      v[i] = *(const uint4*)&psrc[mem_of(q, a, fixed)];
+      l[i] = lsrc ? *(const uint4*)&lsrc[mem_of(q, a, fixed)] : make_uint4(0u, 0u, 0u, 0u);
     }
   }
 #pragma unroll
@@ -149,11 +120,10 @@ __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* 
   }
 }
 
-template <int NT, int TB, bool CH = false>
+template <int NT, int TB>
 __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, const uint32_t* tile, int tid, int T,
                                              uint32_t h_q, uint32_t fixed) {
   constexpr int MQ = (1 << TB) / (4 * NT);
-  const GTile<CH> g(dst, (size_t)1 << a.n);
   uint4 v[MQ];
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -168,7 +138,7 @@ __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, c
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) g.st(mem_of(q, a, fixed), v[i]);
+    if (q < (uint32_t)T) *(uint4*)&dst[mem_of(q, a, fixed)] = v[i];
   }
 }
 
@@ -815,9 +785,6 @@ __host__ __device__ constexpr int class_kernel(int C) { return C <= 4 ? C : 8; }
 // This wave's own LDS operations complete (no workgroup barrier).
 __device__ __forceinline__ void lds_barrier_wave() { __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-__device__ __forceinline__ void lds_barrier_dma() {
-  __asm__ volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 // Op barrier: wave 0 (the fragment DMA) and waves 0..1 (the next op record's global load, tid < OPW) wait for their
 // vector memory; every other wave only for its LDS operations.  A wave that stored gradient partials to the slab
@@ -834,9 +801,11 @@ __device__ __forceinline__ uint32_t tile_fixed(const PassArgs& a, int tile_id) {
   return ((uint32_t)(tile_id & ((1 << w1) - 1)) << a.c) | ((uint32_t)(tile_id >> w1) << a.hi);
 }
 
-// The op's OFF base for the tile's fixed bits (their parities with the op's frame row masks), computed for every
-// op of the pass once per workgroup (lane o, straight from the global records, behind the tile load): inside the
-// op loop it was a dependent chain of nreal LDS reads per op and wave.
+// The op's OFF base for the tile's fixed bits (their parities with the op's frame row masks).  The kernels read it from
+// the host table (PassArgs::fo_tab, hea_plan.fo_table: one load per op); the debug build checks the table against this.
+// Computed in the kernel it was a dependent chain of record loads on wave 0 before its share of the tile load (stall
+// table, round 5: wave 0's prologue 5-10K cycles against < 1K for the other waves, every wave waiting at the first
+// barrier).
 __device__ __forceinline__ uint32_t op_fo_global(const int* ow, uint32_t fixed) {
   const int code = ow[W_CODE];
   if (code == OP_OBS || code == OP_READOUT) return 0u;
@@ -855,14 +824,13 @@ __device__ __forceinline__ uint32_t op_fo_global(const int* ow, uint32_t fixed) 
 // ------------------------------------------------------------------------------------------- forward pass
 // One workgroup per tile of 2^t <= 2^14 amplitudes: 8 waves and 64 KB of LDS, so two workgroups share a CU and
 // one's tile load overlaps the other's group ops (minimum waves per SIMD 4: <= 128 VGPRs).
-// (a device function: the plain launch runs one pass, hea_fwd_chain several; bid = the pass' block index)
-template <int NCK, bool FULL, bool CH>
+template <int NCK, bool FULL>
 __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
   constexpr int NT = NT_FWD, NW = NT / 64;
   __shared__ __attribute__((aligned(16))) uint32_t psi_t[1 << TMAX];   // fp16 (re, im), swizzled
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
   __shared__ int fidx_s[MAXOPS][2];                     // per-op fragment indices (pair ops: two), staged once
-  __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (op_fo_global)
+  __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (fo_tab)
   __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];   // op unitary fragments, double buffered
   __shared__ float red[NW * CMAX];
   __shared__ float2 wv[32][2];
@@ -890,7 +858,8 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
   if (tid < a.nops) {                            // LDS copies: the prefetch below never waits on a global load
     fidx_s[tid][0] = a.fidx[2 * tid];
     fidx_s[tid][1] = a.fidx[2 * tid + 1];
-    fo_s[tid] = op_fo_global(a.ops + (size_t)tid * OPW, fixed);
+    fo_s[tid] = a.fo_tab[(size_t)tile_id * a.nops + tid];
+    QFX_DCHECK(fo_s[tid] == op_fo_global(a.ops + (size_t)tid * OPW, fixed));
   }
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
@@ -967,14 +936,14 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
       if (4 * q < (uint32_t)T) *(uint4*)&psi_t[4 * q] = out[i];
     }
   } else {
-    load_tile<NT, TMAX, CH>(a, a.psi_in + (size_t)s_in * N, psi_t, tid, T, h_q, fixed);
+    load_tile<NT>(a, a.psi_in + (size_t)s_in * N, psi_t, tid, T, h_q, fixed);
   }
 
   // ---------------------------------------------------------------- op list
   const int ncol = T >> 4, nblk = ncol >> 4;
   const int nbw = FULL ? (1 << (TMAX - 8)) / NW : (wave < nblk ? (nblk - wave + NW - 1) / NW : 0);   // (uniform)
   st.mark(PH_LOAD);
-  lds_barrier_dma();
+  op_barrier(wave);   // (waves 0-1 wait for op 0's fragment DMA and record loads; the readout wave's stores never)
   st.mark(PH_BAR);
   for (int o = 0; o < a.nops; ++o) {
     // op o's record and fragments were written during op o - 1; the other buffers were last read at the
@@ -1024,7 +993,7 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
     if constexpr (QFX_HEA_STAMPS) ++st.nops;
   }
   lds_barrier();
-  if (a.store_psi) store_tile<NT, TMAX, CH>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
+  if (a.store_psi) store_tile<NT>(a, a.psi_out + (size_t)s * N, psi_t, tid, T, h_q, fixed);
   st.mark(PH_TAIL);
   st.write(a.dbg, bid, NW, wave, lane);
 }
@@ -1042,7 +1011,7 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
 // round trip and was slower (16q adjoint 0.67 -> 0.72 ms).
 // 2^(TB - 10) waves give each wave 4 column blocks per op (a 4-wave 2^13 workgroup with 8 blocks per wave halves the
 // per-op setup per MFMA but halves the waves per SIMD: measured 18% slower, round 4).
-template <int NCK, int TB, bool FULL, bool CH>
+template <int NCK, int TB, bool FULL>
 __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
   constexpr int NT = 1 << (TB - 4), NW = NT / 64;
   static_assert(NW % 2 == 0 && (1 << (TB - 8)) % NW == 0, "column blocks per wave must be whole, block pairs aligned");
@@ -1050,12 +1019,15 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
   __shared__ __attribute__((aligned(16))) uint32_t tile[2 << TB];
   __shared__ int opw2[2][OPW];                          // op records, double buffered (one barrier per op)
   __shared__ int fidx_s[MAXOPS][2];                     // per-op fragment indices (pair ops: two), staged once
-  __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (op_fo_global)
+  __shared__ uint32_t fo_s[MAXOPS];                     // per-op OFF base of this tile (fo_tab)
   __shared__ __attribute__((aligned(16))) uint4 frag_s[2][256];   // op unitary fragments, double buffered
   // the 80 cross-matrix entries a partial trace can use (b = a, and b = a ^ e_j) x (re, im), 2^-32 fixed point
-  constexpr bool RING = TB < 14;
-  // ring of 4 regions: an op uses at most two (pair ops), so consecutive ops never share one
-  constexpr int NREG = RING ? 4 : MAXGRAD;
+  // One region per gradient record of the pass, reduced by all waves after the op loop - up to NREG (2^13 tiles: 9,
+  // which still fits two workgroups per CU).  A pass with more records cycles through a ring of 4 regions instead,
+  // one wave flushing a region at the start of the op after its use (an op uses at most two, so consecutive ops never
+  // share one) - that flush put the flushing wave on every barrier's critical path (stall table, round 5).
+  constexpr int NREG = TB < 14 ? 9 : MAXGRAD;
+  const bool ring = TB < 14 && a.n_regions > NREG;   // (2^14 tiles: MAXGRAD regions, never a ring)
   __shared__ unsigned long long red64[NREG * RSTR];
   __shared__ int gmeta_s[NREG][2];                      // (slab index, nreal) of the region's gradient op
   __shared__ float rsc[CMAX + 2];
@@ -1077,7 +1049,8 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
   if (tid < a.nops) {
     fidx_s[tid][0] = a.fidx[2 * tid];
     fidx_s[tid][1] = a.fidx[2 * tid + 1];
-    fo_s[tid] = op_fo_global(a.ops + (size_t)tid * OPW, fixed);
+    fo_s[tid] = a.fo_tab[(size_t)tile_id * a.nops + tid];
+    QFX_DCHECK(fo_s[tid] == op_fo_global(a.ops + (size_t)tid * OPW, fixed));
   }
   if (tid < OPW && a.nops > 0) opw2[0][tid] = a.ops[tid];
   int nxt = (tid < OPW && a.nops > 1) ? a.ops[OPW + tid] : 0;
@@ -1098,8 +1071,8 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
     }
   }
   st.mark(PH_PRO);
-  load_tile_il<NT, TB, CH>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T,
-                           h_q, fixed);
+  load_tile_il<NT, TB>(a, a.psi_in + (size_t)s * N, a.load_lam ? a.lam_in + (size_t)s * N : nullptr, tile, tid, T, h_q,
+                       fixed);
 
   if (a.ro_fuse ? tid == NT - 64 : tid == 0) {
     float wv[CMAX];
@@ -1130,10 +1103,7 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
         wv[c] = dl[c] * ra[c];
         if (out) {
           a.ro_expz[(size_t)s * a.C + c] = z[c];
-          if constexpr (CH)   // read by this launch's later passes (write-through, as the tiles)
-            __hip_atomic_store(&a.ro_w[(size_t)s * a.C + c], wv[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else
-            a.ro_w[(size_t)s * a.C + c] = wv[c];
+          a.ro_w[(size_t)s * a.C + c] = wv[c];
           rec[c] = dl[c] * z[c];
           rec[a.C + c] = dl[c];
         }
@@ -1146,8 +1116,7 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
 #pragma unroll
       for (int c = 0; c < CMAX; ++c) {
         if (c >= a.C) break;
-        wv[c] = CH ? __hip_atomic_load(&a.wread[(size_t)s * a.C + c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                   : a.wread[(size_t)s * a.C + c];
+        wv[c] = a.wread[(size_t)s * a.C + c];
       }
     }
     float rho = 0.f;
@@ -1162,7 +1131,7 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
     rsc[CMAX] = rho;
     rsc[CMAX + 1] = PK_SCALE / (a.scale * a.scale);
   }
-  for (int e = tid; e < NREG * RSTR; e += NT) red64[e] = 0ull;
+  for (int e = tid; e < (ring ? 4 : min(a.n_regions, NREG)) * RSTR; e += NT) red64[e] = 0ull;
 
   // Partial traces of a finished gradient op's region (read after a barrier): output r = (j, y, x, comp) sums the
   // 8 entries with b_j = y, a_j = x (the whole workgroup at the end of the pass, or lanes 0..31 of the flushing
@@ -1194,7 +1163,7 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
   // loops of the group ops carry no bounds checks or branches
   const int nbw = FULL ? (1 << (TB - 8)) / NW : (wave < nblk ? (nblk - wave + NW - 1) / NW : 0);
   st.mark(PH_LOAD);
-  lds_barrier_dma();
+  op_barrier(wave);   // (waves 0-1 wait for op 0's fragment DMA and record loads; the readout wave's stores never)
   st.mark(PH_BAR);
   int ngrad = 0;
   int pending = -1, npend = 0;                         // ring: first region / count of the previous op's regions
@@ -1217,9 +1186,9 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
       op_barrier(wave);
       st.mark(PH_BAR);
     }
-    if (RING && npend > 0) {                           // one wave per region, the last waves
+    if (ring && npend > 0) {                           // one wave per region, the last waves
       for (int q = 0; q < npend; ++q)
-        if (wave == NW - 1 - q) flush((pending + q) & (NREG - 1));
+        if (wave == NW - 1 - q) flush((pending + q) & 3);
       npend = 0;
     }
     const int* opw = opw2[o & 1];
@@ -1290,11 +1259,11 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
       // slot addresses had taken eight SGPRs - spilled to VGPR lanes - and four VGPRs)
       uint32_t ep = epi;
       __asm__ volatile("" : "+v"(ep));
-      if (RING) pending = ngrad & (NREG - 1);
+      if (ring) pending = ngrad & 3;
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
         if (g >= ng) break;
-        const int reg = RING ? ngrad & (NREG - 1) : ngrad;
+        const int reg = ring ? ngrad & 3 : ngrad;
         unsigned long long* rg = red64 + reg * RSTR;
         const f4 accR = acc[2 * g], accI = acc[2 * g + 1];
 #pragma unroll
@@ -1319,97 +1288,24 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
     if constexpr (QFX_HEA_STAMPS) ++st.nops;
   }
   lds_barrier();
-  if (RING) {
+  if (ring) {
     for (int q = 0; q < npend; ++q)
-      if (wave == NW - 1 - q && lane < 32) reduce_region((pending + q) & (NREG - 1), lane);
+      if (wave == NW - 1 - q && lane < 32) reduce_region((pending + q) & 3, lane);
   } else {
     for (int e = tid; e < ngrad * 32; e += NT) reduce_region(e >> 5, e & 31);
   }
-  if (a.store_lam) store_lam_il<NT, TB, CH>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
+  if (a.store_lam) store_lam_il<NT, TB>(a, a.lam_out + (size_t)s * N, tile, tid, T, h_q, fixed);
   st.mark(PH_TAIL);
   st.write(a.dbg, bid, NW, wave, lane);
 }
 
 // ------------------------------------------------------------------------------------------- launches
 template <int NCK, bool FULL>
-__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) { fwd_pass<NCK, FULL, false>(a, blockIdx.x); }
+__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_kernel(PassArgs a) { fwd_pass<NCK, FULL>(a, blockIdx.x); }
 
 template <int NCK, int TB, bool FULL>
 __global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_adj_kernel(PassArgs a) {
-  adj_pass<NCK, TB, FULL, false>(a, blockIdx.x);
-}
-
-// Chained passes: the forward passes (or the adjoint passes) of one step in ONE launch, a dataflow over per-sample
-// completion counters instead of a kernel boundary per pass.  A block takes the next work item from a ticket counter
-// (items in pass order, so every item a block waits for was taken earlier by a running block: no deadlock), waits
-// until all tiles of its sample in the previous pass are done, and runs the pass body.  The next pass' first tiles
-// thus start while the previous pass' last ones drain, and a step has one launch per direction (at the 8-client share
-// the passes run 2 / 4 generations of workgroups, so each pass boundary left the chip ramping down and up).
-//   sync[0] ticket, sync[1] finished blocks, sync[2] spin timeouts (a wait past ~1 s gives up: wrong numbers and a
-//   nonzero word, never a hang), sync[3 + j S + s] finished tiles of pass j for sample s.  The launch's last block
-//   zeroes every counter but sync[2] (the buffer starts zeroed).
-// Hand-off without fences (cdna guide Guideline 16, R1): a producer's handed-off bytes (its tile, and the fused
-// readout's dL/d<Z>) are sc1 write-through stores that every wave drains before the block's barrier, then ONE lane adds
-// to the counter; the consumer polls it relaxed and reads those bytes only with sc1 loads.
-__device__ __forceinline__ int chain_begin(const HeaChainArgs& c, int& pj) {
-  __shared__ int item_s[2];
-  if (threadIdx.x == 0) {
-    const int item = (int)atomicAdd(&c.sync[0], 1u);
-    int j = 0;
-    while (j + 1 < c.npass && item >= c.start[j + 1]) ++j;
-    if (j > 0) {
-      const int s = (item - c.start[j]) / c.p[j].n_tiles;
-      const unsigned* cnt = c.sync + 3 + (size_t)(j - 1) * c.S + s;
-      const unsigned need = (unsigned)c.p[j - 1].n_tiles;
-      for (int it = 0; __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need; ++it) {
-        if (it == (1 << 24)) {
-          atomicAdd(&c.sync[2], 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      // every load of handed-off bytes is an sc1 load (GTile<true>, wread): no agent acquire, only keep the
-      // compiler from hoisting loads above the poll
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    item_s[0] = item - c.start[j];
-    item_s[1] = j;
-  }
-  __syncthreads();
-  pj = item_s[1];
-  return item_s[0];
-}
-
-__device__ __forceinline__ void chain_end(const HeaChainArgs& c, int j, int bid) {
-  __shared__ int last_s;
-  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 tile stores complete (every storing wave)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // the tile went out by write-through sc1 stores, drained by every wave above
-    if (j + 1 < c.npass) atomicAdd(&c.sync[3 + (size_t)j * c.S + bid / c.p[j].n_tiles], 1u);
-    last_s = atomicAdd(&c.sync[1], 1u) == (unsigned)c.start[c.npass] - 1u;
-  }
-  __syncthreads();
-  if (!last_s) return;
-  const int nc = 3 + (c.npass - 1) * c.S;                // every other block has finished: reset for the next launch
-  for (int e = threadIdx.x; e < nc; e += blockDim.x)
-    if (e != 2) c.sync[e] = 0u;
-}
-
-template <int NCK, bool FULL>
-__global__ void __launch_bounds__(NT_FWD, 4) hea_fwd_chain(HeaChainArgs c) {
-  int j;
-  const int bid = chain_begin(c, j);
-  fwd_pass<NCK, FULL, true>(c.p[j], bid);
-  chain_end(c, j, bid);
-}
-
-template <int NCK, int TB, bool FULL>
-__global__ void __launch_bounds__(1 << (TB - 4), (1 << (TB - 4)) * 2 / 256) hea_adj_chain(HeaChainArgs c) {
-  int j;
-  const int bid = chain_begin(c, j);
-  adj_pass<NCK, TB, FULL, true>(c.p[j], bid);
-  chain_end(c, j, bid);
+  adj_pass<NCK, TB, FULL>(a, blockIdx.x);
 }
 
 }  // namespace HEA_NS
@@ -1449,23 +1345,6 @@ extern "C" int HEA_EXT(qfx_hea_pass)(int adjoint, const HEA_NS::PassArgs* args, 
   return (int)hipGetLastError();
 }
 
-// Chained passes (one launch): every pass must select the same kernel instance (direction, tile class, class count).
-extern "C" int HEA_EXT(qfx_hea_chain)(int adjoint, const HeaChainArgs* chain, hipStream_t st) {
-  const HeaChainArgs& c = *chain;
-  if (c.npass < 1 || c.npass > HEA_MAXCHAIN || !c.sync || c.start[0] != 0) return -2;
-  const int t = c.p[0].t, C = c.p[0].C;
-  for (int j = 0; j < c.npass; ++j) {
-    const HEA_NS::PassArgs& a = c.p[j];
-    const bool same = adjoint ? ((a.t <= 13) == (t <= 13)) : ((a.t == HEA_NS::TMAX) == (t == HEA_NS::TMAX));
-    if (!hea_args_ok(a) || !same || a.n > 28 ||   // (buffer descriptors span one sample: < 2^31 bytes) HEA_NS::class_kernel(a.C) != HEA_NS::class_kernel(C) ||
-        c.start[j + 1] - c.start[j] != c.S * a.n_tiles)
-      return -2;
-  }
-  const unsigned grid = (unsigned)c.start[c.npass];
-  if (grid == 0) return 0;
-  HEA_SWITCH(hea_fwd_chain, hea_adj_chain, c);
-  return (int)hipGetLastError();
-}
 #undef HEA_SWITCH
 #undef HEA_LAUNCH
 

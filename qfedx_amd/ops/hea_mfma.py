@@ -24,7 +24,8 @@ import numpy as np
 import torch
 
 from ._ext import ext
-from .hea_plan import OP_APPLY, OP_APPLY2, OP_READOUT, TILE_BITS, W_CODE, build_plan, eligible, obs_table, pass_programs
+from .hea_plan import (OP_APPLY, OP_APPLY2, OP_BACK, OP_BACK2, OP_GRAD2, OP_GRAD_L1, OP_READOUT, TILE_BITS, W_CODE, build_plan, eligible, fo_table, obs_table,
+                       pass_programs)
 
 ADJ_TILE_BITS = 13   # adjoint tiles: 2^13 amplitudes x (psi, lambda) = 64 KB of LDS -> two workgroups per CU
 
@@ -61,13 +62,6 @@ _NODBG = torch.zeros(0, dtype=torch.int64)     # no stall-attribution buffer (st
 
 
 FUSED_ADAM_MAX_BLOCKS = 256   # hea_grad_reduce blocks (clients x gradient ops) up to which Adam is fused
-HEA_MAXCHAIN = 4              # passes per chained launch (csrc/hea_args.h)
-
-
-def _chain_default() -> bool:
-    """Chained pass launches (hea_chain: one dataflow launch per direction instead of one per pass);
-    ``QFEDX_HEA_CHAIN=0`` launches every pass on its own."""
-    return os.environ.get("QFEDX_HEA_CHAIN", "1") != "0"
 
 
 class HeaMfmaProgram:
@@ -126,14 +120,19 @@ class HeaMfmaProgram:
             fr_ops = np.concatenate([fr_ops, obs_table(fplan, pr, OP_READOUT)[None]], 0)
             progs_f = [(p, f if j < self.fwd_last else (fr_ops if j == self.fwd_last else f[:0]), a)
                        for j, (p, f, a) in enumerate(progs_f)]
+        self.n_regions = []       # per pass: gradient records of its adjoint program (LDS regions)
         for (p, fwd, _), (pa, _, adj) in zip(progs_f, progs_a):
             f = torch.from_numpy(fwd.astype(np.int32)).contiguous()
             a = torch.from_numpy(adj.astype(np.int32)).contiguous()
             ff, fa = _frag_index(fwd), _frag_index(adj)
             C.hea_check_ops(f, ff, self.n_slots, self.n_theta, False, p.t, self.n_gradops)
             C.hea_check_ops(a, fa, self.n_slots, self.n_theta, True, pa.t, self.n_gradops)
-            self.passes.append((p, (f.to(self.device), ff.to(self.device)), (a.to(self.device), fa.to(self.device)),
-                                pa))
+            self.n_regions.append(sum(2 if int(w[W_CODE]) in (OP_BACK2, OP_GRAD2) else
+                                      int(int(w[W_CODE]) in (OP_BACK, OP_GRAD_L1)) for w in adj))
+            of = torch.from_numpy(fo_table(fwd, p, self.n).reshape(-1)).to(self.device)
+            oa = torch.from_numpy(fo_table(adj, pa, self.n).reshape(-1)).to(self.device)
+            self.passes.append((p, (f.to(self.device), ff.to(self.device), of),
+                                (a.to(self.device), fa.to(self.device), oa), pa))
         slot_tab = np.zeros((max(self.n_slots, 1), 9), dtype=np.int32)
         owner = np.zeros(self.n_theta, dtype=np.int32)
         for p in self.plan.passes:
@@ -156,8 +155,9 @@ class HeaMfmaProgram:
         self.feature = _FEATURE[spec.feature_map.lower()]
         self._ws = {}
         self._ps_budget = None
-        self.chain = _chain_default()
-        self._chain_args = {}     # host staging buffers of the chained launches (HeaChainArgs bytes)
+        # noiseless steps compute the readout in the first adjoint pass (profiles/r5_fused_readout_ab.txt: a tie at 64
+        # clients, -2.7% at 8); the readout kernel runs for readout noise - and for tests comparing the two (False)
+        self.fused_readout = True
         if self.device.type == "cuda":
             self._shift_budget()      # query free HBM now, never inside a graph capture
 
@@ -197,10 +197,12 @@ class HeaMfmaProgram:
         """Tiles per sample of the pass that reads out <Z> (the last forward pass that runs)."""
         return 1 << (self.n - self.passes[self.fwd_last][0].t)
 
-    def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K, in_rep: int = 1):
+    def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K, in_rep: int = 1,
+              n_regions: int = 0):
         return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
                 int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
-                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep), int(self.bf16)]
+                self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep), int(self.bf16),
+                                                                 int(n_regions)]
 
     def _frags(self, params: torch.Tensor, K: int, tag: str = "") -> torch.Tensor:
         fr = self._buf(f"{tag}frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
@@ -219,22 +221,18 @@ class HeaMfmaProgram:
         empty = torch.empty(0, dtype=torch.int32, device=self.device)
         fempty = torch.empty(0, dtype=torch.float32, device=self.device)
         J, R = self.n_passes, self.fwd_last
-        chain = self._chain_buf("f", [self.passes[j][0] for j in range(R + 1)], False)
         for j in range(R + 1):
             p, fwd = self.passes[j][0], self.passes[j][1]
             keep = j < R or store_last
-            # evaluation only needs the previous pass output: two ping-pong buffers instead of one per pass (a chained
-            # launch keeps every pass output: pass j + 1 may start while pass j - 1's output is still being read)
-            name = f"{tag}psi{j}" if (store_last or chain is not None) else f"{tag}pe{j % 2}"
+            # evaluation only needs the previous pass output: two ping-pong buffers instead of one per pass
+            name = f"{tag}psi{j}" if store_last else f"{tag}pe{j % 2}"
             out = self._buf(name, N, torch.int32) if keep else empty
             psi_in = stored[-1] if j > 0 else empty
             geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K)
-            C.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
-                       part if j == R else fempty, fempty, dbg[f"fwd{j}"] if dbg else _NODBG, None, 0, chain, j)
+            C.hea_pass(False, fwd[0], fwd[1], fwd[2], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
+                       part if j == R else fempty, fempty, dbg[f"fwd{j}"] if dbg else _NODBG)
             if keep:
                 stored.append(out)
-        if chain is not None:
-            C.hea_chain(False, chain, R + 1, S, self._zbuf(f"{tag}fsync", 3 + R * S, torch.int32), self.bf16)
         if store_last:
             stored += [stored[R]] * (J - 1 - R)
         return stored
@@ -250,40 +248,20 @@ class HeaMfmaProgram:
         fempty = torch.empty(0, dtype=torch.float32, device=self.device)
         J = self.n_passes
         lam_in = empty
-        chain = self._chain_buf("a", [self.passes[j][3] for j in range(J - 1, -1, -1)], True)
-        for i, j in enumerate(range(J - 1, -1, -1)):
+        for j in range(J - 1, -1, -1):
             _, _, adj, p = self.passes[j]
-            # (chained: one lambda buffer per pass, as in the forward)
-            lam_out = self._buf(f"{tag}lam{j if chain is not None else j % 2}", N, torch.int32) if j > 0 else empty
-            geom = self._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, x.shape[1], K)
+            lam_out = self._buf(f"{tag}lam{j % 2}", N, torch.int32) if j > 0 else empty
+            geom = self._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, x.shape[1], K,
+                              n_regions=self.n_regions[j])
             if readout is not None and j == J - 1:
                 part, yy, ww, expz, rec = readout
-                C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
+                C.hea_pass(True, adj[0], adj[1], adj[2], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
                            params, fr, fempty, part, gslab, dbg[f"adj{j}"] if dbg else _NODBG,
-                           [yy, ww, expz, wread, rec], self.tiles_last, chain, i)
+                           [yy, ww, expz, wread, rec], self.tiles_last)
             else:
-                C.hea_pass(True, adj[0], adj[1], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
-                           params, fr, wread, fempty, gslab, dbg[f"adj{j}"] if dbg else _NODBG, None, 0, chain, i)
+                C.hea_pass(True, adj[0], adj[1], adj[2], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
+                           params, fr, wread, fempty, gslab, dbg[f"adj{j}"] if dbg else _NODBG)
             lam_in = lam_out
-        if chain is not None:
-            C.hea_chain(True, chain, J, S, self._zbuf(f"{tag}async", 3 + (J - 1) * S, torch.int32), self.bf16)
-
-    def chain_timeouts(self) -> int:
-        """Dependency waits of chained launches that gave up (sync word 2 of every chain's counters; must be 0)."""
-        return sum(int(t[2]) for name, t in self._ws.items() if name.endswith(("fsync", "async")) and t.numel() > 2)
-
-    def _chain_buf(self, kind: str, ps: list, adjoint: bool):
-        """Host staging buffer for a chained launch of passes ``ps`` (in launch order), or None when they launch one
-        by one: chaining off, a single pass, more than HEA_MAXCHAIN, or passes of different kernel instances."""
-        if not self.chain or not (2 <= len(ps) <= HEA_MAXCHAIN) or self.n > 28:
-            return None
-        cls = {p.t <= 13 for p in ps} if adjoint else {p.t == 14 for p in ps}
-        if len(cls) != 1:
-            return None
-        buf = self._chain_args.get(kind)
-        if buf is None:
-            buf = self._chain_args[kind] = torch.zeros(int(ext().HEA_CHAIN_BYTES), dtype=torch.uint8)
-        return buf
 
     def _prep(self, xang, params):
         K, B, F = xang.shape
@@ -511,7 +489,7 @@ class HeaMfmaProgram:
             out = self._buf(f"pbpsi{(jj - j) % 2}", N, torch.int32) if keep else empty
             first = jj == j
             geom = self._geom(p, jj == 0, False, keep, False, B, ps, S, xs.shape[1], Kr, nr if first else 1)
-            E.hea_pass(False, fwd[0], fwd[1], geom, self.scale, psi_in, out, empty, empty, xs, thr, fr, fempty,
+            E.hea_pass(False, fwd[0], fwd[1], fwd[2], geom, self.scale, psi_in, out, empty, empty, xs, thr, fr, fempty,
                        part if jj == R else fempty, fempty, _NODBG)
             psi_in = out
         z = self._buf("pbz", S * self.C, torch.float32)
@@ -522,10 +500,8 @@ class HeaMfmaProgram:
     fuses_optimizer = True    # VQCEngine: loss_and_grads(fused_opt=...) may run the Adam step in the reduction
 
     def _fused_readout(self, noise) -> bool:
-        """Noiseless steps compute the readout in the first adjoint pass (``QFEDX_FUSED_READOUT=0`` keeps the
-        separate readout kernel; bench A/B)."""
-        return (noise is None and os.environ.get("QFEDX_FUSED_READOUT", "1") != "0"
-                and self.tiles_last * self.C <= 64)
+        """Noiseless steps compute the readout in the first adjoint pass (``fused_readout``)."""
+        return noise is None and self.fused_readout and self.tiles_last * self.C <= 64
 
     def _step(self, x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=None, dbg=None):
         """Forward, readout + CE, adjoint and gradient reduction of clients [0, K).

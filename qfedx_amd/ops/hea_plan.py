@@ -767,6 +767,38 @@ def group_unitary(theta: np.ndarray, nreal: int, th_slots, ph_slots) -> np.ndarr
     return U
 
 
+def tile_fixed(p: Pass, n: int) -> np.ndarray:
+    """Memory bits outside the tile of every tile id of pass ``p`` (the kernels' tile_fixed): [2^(n - t)] uint32."""
+    tid = np.arange(1 << (n - p.t), dtype=np.uint64)
+    w1 = p.lo - p.c
+    return (((tid & ((1 << w1) - 1)) << p.c) | ((tid >> w1) << p.hi)).astype(np.uint32)
+
+
+def fo_table(ops: np.ndarray, p: Pass, n: int) -> np.ndarray:
+    """Per (tile, op) OFF base of a pass program: the op's OFF entry for the parities of the tile's fixed bits with
+    its frame row masks (pair records: both groups', XORed).  [n_tiles, nops] int32, read by every workgroup in its
+    prologue (one load per op instead of a dependent chain of record loads on one wave: round-5 stall table)."""
+    fixed = tile_fixed(p, n)
+    out = np.zeros((len(fixed), len(ops)), dtype=np.uint32)
+
+    def fp(rows, k):
+        v = np.zeros(len(fixed), dtype=np.uint32)
+        for j in range(k):
+            v |= ((np.bitwise_count(fixed & np.uint32(int(rows[j]) & 0xFFFFFFFF)) & 1).astype(np.uint32) << j)
+        return v
+
+    for o, w in enumerate(ops):
+        code = int(w[W_CODE])
+        if code in (OP_OBS, OP_READOUT):
+            continue
+        off = np.asarray(w[W_OFF:W_OFF + 16]).astype(np.uint32)
+        fo = off[fp(w[W_RFULL:W_RFULL + 4], int(w[W_NREAL]))]
+        if code in PAIR_CODES:
+            fo = fo ^ np.asarray(w[W_OFF2:W_OFF2 + 16]).astype(np.uint32)[fp(w[W_RFULL2:W_RFULL2 + 4], GROUP)]
+        out[:, o] = fo
+    return out.view(np.int32)
+
+
 def _addr(w, t, fixed):
     """[ncol, 16] tile addresses of (column, group coordinate m), computed as the kernel does."""
     col = np.arange(1 << (t - GROUP))

@@ -1,5 +1,5 @@
 """Interleaved A/B of MFMA-engine variants in ONE process (guide rule: perf deltas from interleaved rounds on one
-device).  Variants are run-time environment switches (``env.NAME=value``, e.g. env.QFEDX_FUSED_READOUT=0) and the state
+device).  Variants are run-time environment switches (``env.NAME=value``, e.g. env.QFEDX_HEA_PAIR=0) and the state
 storage (fp16 | bf16).  Each round times every variant's full local step (frags, forward, readout, adjoint, gradient
 reduction) and its adjoint passes alone; prints per-variant median / min ms over the rounds as JSON.
 
@@ -56,7 +56,7 @@ def main():
 
     def set_knobs(knobs):
         for k, v in knobs.items():
-            if k.startswith("env."):           # environment switches, e.g. env.QFEDX_FUSED_READOUT=0
+            if k.startswith("env."):           # environment switches, e.g. env.QFEDX_HEA_PAIR=0
                 os.environ[k[4:]] = v
 
     for name, knobs in variants:

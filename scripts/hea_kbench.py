@@ -85,17 +85,18 @@ def main():
         geom = prog._geom(p, j == 0, False, True, False, B, params.shape[1], S, xx.shape[1], K,
                           pair=prog._paired(B))
         nb = 4 * N * ((j > 0) + 1)
-        timeit(lambda: C.hea_pass(False, fwd[0], fwd[1], geom, prog.scale, psi_in, out, empty, empty, xx, params, fr, fempty,
+        timeit(lambda: C.hea_pass(False, fwd[0], fwd[1], fwd[2], geom, prog.scale, psi_in, out, empty, empty, xx, params, fr, fempty,
                                   part if j == R else fempty, fempty, _NODBG), f"fwd{j}", nb)
     lam = [prog._buf("lam0", N, torch.int32), prog._buf("lam1", N, torch.int32)]
     for j in range(J - 1, -1, -1):
         ent = prog.passes[j]                          # (fwd pass, fwd prog, adj prog[, adj pass]) (older trees: 3)
         adj, p = ent[2], ent[-1] if len(ent) > 3 else ent[0]
-        geom = prog._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, xx.shape[1], K)
+        geom = prog._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, xx.shape[1], K,
+                          n_regions=prog.n_regions[j])
         lin = lam[(j + 1) % 2] if j < J - 1 else empty
         lout = lam[j % 2] if j > 0 else empty
         nb = 4 * N * (1 + (j < J - 1) + (j > 0))
-        timeit(lambda: C.hea_pass(True, adj[0], adj[1], geom, prog.scale, stored[j], empty, lin, lout,
+        timeit(lambda: C.hea_pass(True, adj[0], adj[1], adj[2], geom, prog.scale, stored[j], empty, lin, lout,
                                   xx, params, fr, wread, fempty, gslab, _NODBG), f"adj{j}", nb)
     grad = torch.zeros(K, params.shape[1], device=dev)
     timeit(lambda: C.hea_grad_reduce(gslab, prog.slab_tiles, prog.n_gradops, prog.gmeta, B, K, params, grad,

@@ -213,8 +213,8 @@ def test_fused_readout_matches_readout_kernel(cuda, monkeypatch, n, K, B, C):
     params = (params + 0.3 * torch.randn(params.shape, generator=g)).to(cuda)
 
     def run(fused):
-        monkeypatch.setenv("QFEDX_FUSED_READOUT", "1" if fused else "0")
         prog = HeaMfmaProgram(spec, cuda)
+        prog.fused_readout = fused
         out = prog.loss_and_grads(xang, y, w, params, spec)
         torch.cuda.synchronize()
         return {k: v.clone() for k, v in out.items()}
@@ -256,32 +256,3 @@ def test_pair_ops_match_unpaired_kernels(cuda, monkeypatch, n, L, tile):
     ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
     np.testing.assert_allclose(z1.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
     np.testing.assert_allclose(g1.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
-
-
-@pytest.mark.parametrize("n,L,tile,K,B", [(16, 3, 14, 8, 32), (24, 3, 14, 2, 2), (20, 2, 14, 3, 8), (12, 3, 11, 5, 7)])
-def test_chained_pass_launch_is_bitwise_the_per_pass_launches(cuda, monkeypatch, n, L, tile, K, B):
-    """One dataflow launch per direction (hea_chain: the forward passes, then the adjoint passes, over per-sample
-    completion counters) computes bitwise what one launch per pass computes - <Z>, gradients, and the fused-readout
-    step's loss / hits / readout gradients - and no dependency wait gives up.  16q x 8 x 32 puts 1024 / 2048
-    workgroups per pass into 512 resident slots, so consumers really overtake the previous pass' stragglers."""
-    spec = VQCSpec(n, L, 3)
-    x, params, wr = _inputs(spec, K, B, seed=7 * n + L)
-    xx, th, ww = x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda)
-    g = torch.Generator().manual_seed(n)
-    y = torch.randint(0, 3, (K, B), generator=g).to(cuda)
-    wts = torch.full((K, B), 1.0 / B, device=cuda)
-    out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("QFEDX_HEA_CHAIN", mode)
-        prog = HeaMfmaProgram(spec, cuda, tile_bits=tile)
-        assert prog.chain == (mode == "1")
-        z, gr = prog.vjp(xx, th, ww)
-        st = prog.loss_and_grads(xx, y, wts, params.to(cuda), spec)
-        z2, gr2 = prog.vjp(xx, th, ww)                 # counters were reset by the previous launches' last blocks
-        torch.cuda.synchronize()
-        out[mode] = (z, gr, z2, gr2, st["loss"].clone(), st["correct"].clone(), st["grad"].clone())
-        if mode == "1":
-            assert prog.chain_timeouts() == 0
-            assert any(k.endswith("fsync") for k in prog._ws) or prog.fwd_last == 0
-    for a, b in zip(out["0"], out["1"]):
-        assert torch.equal(a, b)

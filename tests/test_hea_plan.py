@@ -238,3 +238,27 @@ def test_pair_only_pass_counts_as_applying():
     assert [int(w[hp.W_CODE]) for w in progs[-1][1]] == [hp.OP_APPLY2, hp.OP_READOUT]
     prog = HeaMfmaProgram(spec, torch.device("cpu"))
     assert prog.fwd_last == len(prog.passes) - 1
+
+
+@pytest.mark.parametrize("n,L,t", [(16, 3, 14), (16, 3, 13), (20, 2, 13), (12, 3, 10)])
+def test_fo_table_matches_per_tile_op_bases(n, L, t):
+    """The host table of per-(tile, op) OFF bases the pass kernels read in their prologue equals the kernels' former
+    in-kernel computation (parities of the tile's fixed bits with each op's frame row masks; pair records XOR both
+    groups' entries; OBS / READOUT 0) for every tile of every pass program."""
+    from qfedx_amd.models.vqc import VQCSpec
+    spec = VQCSpec(n, L, 3)
+    plan = hp.build_plan(n, L, spec.readout, True, "ry", tile_bits=t)
+    for p, fwd, adj in hp.pass_programs(plan, []):
+        for ops in (fwd, adj):
+            tab = hp.fo_table(ops, p, n).view(np.uint32)
+            for tile, fixed in enumerate(hp.tile_fixed(p, n)):
+                for o, w in enumerate(ops):
+                    code = int(w[hp.W_CODE])
+                    want = 0
+                    if code not in (hp.OP_OBS, hp.OP_READOUT):
+                        fp = sum(hp.parity(int(fixed) & int(w[hp.W_RFULL + j])) << j for j in range(int(w[hp.W_NREAL])))
+                        want = int(w[hp.W_OFF + fp])
+                        if code in hp.PAIR_CODES:
+                            fy = sum(hp.parity(int(fixed) & int(w[hp.W_RFULL2 + j])) << j for j in range(4))
+                            want ^= int(w[hp.W_OFF2 + fy])
+                    assert int(tab[tile, o]) == want
