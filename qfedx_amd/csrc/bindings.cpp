@@ -610,6 +610,7 @@ void dm_run(torch::Tensor gates, int64_t G, int64_t n, torch::Tensor rows, torch
         "qfx_dm_run");
 }
 void register_hea(pybind11::module& m);
+void register_mps(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "qfedx_amd native runtime: pass planner + gfx950 HIP kernels";
@@ -650,4 +651,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dm_gate_bytes", []() { return qfx_dm_gate_bytes(); });
   m.def("dm_lds_qubits", []() { return qfx_dm_lds_qubits(); });
   register_hea(m);
+  register_mps(m);
 }

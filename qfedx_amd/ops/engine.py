@@ -53,6 +53,7 @@ class VQCEngine:
     def __init__(self, spec: VQCSpec, device="cpu", backend: str = "torch", state_dtype: str = "fp32",
                  noise=None, mps_chi: int = 64):
         self.spec = spec
+        self.mps_hip = None
         self.noise = noise          # quantum.noise.NoiseModel or None
         self.device = torch.device(device)
         self.backend = backend
@@ -71,6 +72,11 @@ class VQCEngine:
                 raise ValueError("amplitude-encoded initial states need a dense 2^n vector (n <= 26 with mps)")
             self.prog = MPSProgram(ops, coef, spec.n_qubits, self.device, chi_max=mps_chi)
             self.hip = None
+            # the CNOT-chain VQC (<= 3 layers, exact at bond 8) runs on one HIP kernel per step on a GPU
+            from ..quantum.mps_chain import eligible as chain_ok
+            if self.device.type == "cuda" and chain_ok(spec) and noise is None:
+                from .mps_hip import MpsChainProgram
+                self.mps_hip = MpsChainProgram(spec, self.device)
         elif backend == "density":
             # exact density matrices with the Kraus gate channel (HIP kernel on a GPU, torch on CPU)
             from .density import DensityProgram
@@ -154,6 +160,8 @@ class VQCEngine:
                 raise ValueError("the density-matrix simulator starts from |0><0| (angle feature maps)")
             z = self.prog.expz(self._rows(xang, theta)).reshape(K, B, -1).float()
             return self._readout(z, readout_keys, step)
+        if self.mps_hip is not None and init is None:
+            return self._readout(self.mps_hip.expz(xang, theta), readout_keys, step)
         psi = self.prog.run(self._rows(xang, theta), state=self._init_rows(init))
         z = self.prog.expz(psi, self.spec.readout).reshape(K, B, -1).float()
         return self._readout(z, readout_keys, step)
@@ -210,6 +218,12 @@ class VQCEngine:
         P = spec.n_theta
         with torch.no_grad():
             rows = psi = None
+            if method == "adjoint" and self.mps_hip is not None and init is None:
+                # HIP column contraction (csrc/mps_chain.hip): <Z>, then the gradient sweep with dL/d<Z>
+                expz = self._readout(self.mps_hip.expz(xang, th), readout_keys, step)
+                loss, w, ga, gb, correct = ce_readout(expz, y, wmask, a, b)
+                gth = self.mps_hip.grads(xang, th, w)
+                return {"loss": loss, "grad": torch.cat([gth, ga, gb], -1), "correct": correct, "expz": expz}
             if (method == "adjoint" and self.backend == "mps" and self.prog.autograd_ok and init is None):
                 # one recorded MPS contraction: readout now, reverse-mode pull-back of dL/d<Z> below
                 rows = self._rows(xang, th)
