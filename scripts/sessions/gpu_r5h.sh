@@ -12,12 +12,9 @@ step() {  # step <name> <seconds> <cmd...>
   [ $rc -eq 0 ] || exit $rc
 }
 step hea_tests 400 python -u -m pytest tests/test_gpu_hea.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
-step hea_debug 300 env QFEDX_DEBUG=1 python -u -m pytest tests/test_gpu_hea.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider -k "dense or pair"
 step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 step bench64 300 python bench.py --steps 20 --warmup 3
 step share8 300 python bench.py --steps 30 --warmup 5 --clients 8
-step ab_pair64 300 python -u scripts/hea_ab.py --rounds 5 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=7"
-step ab_pair8 300 python -u scripts/hea_ab.py --rounds 5 --clients 8 --iters 30 --variants "single:env.QFEDX_HEA_PAIR=0,pair:env.QFEDX_HEA_PAIR=7"
 step stamps64 300 python -u scripts/hea_stamps.py --clients 64 --out gpurun_out/r5h/stamps64.jsonl
 step prof64 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5h/prof64 -o bench -- python3 bench.py --steps 10 --warmup 3
 step prof8 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r5h/prof8 -o bench -- python3 bench.py --steps 20 --warmup 3 --clients 8
