@@ -82,7 +82,7 @@ int qfx_launch_round_init(const float* theta, int K, int P, float* params, float
 int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
                               const float* X, const long long* Y, const long long* lid, const long long* idx,
                               int steps, int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride,
-                              long long* yo, hipStream_t st);
+                              long long* yo, const int* slot_tab, int n_slots, void* frags, int bf16, hipStream_t st);
 int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx, int K,
                             int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride, long long* yo,
                             hipStream_t st);
@@ -403,7 +403,7 @@ void batch_gather(torch::Tensor X, torch::Tensor Y, torch::Tensor lid, torch::Te
 void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<torch::Tensor> m,
                     c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> t, torch::Tensor X, torch::Tensor Y,
                     torch::Tensor lid, torch::Tensor idx, int64_t mode, double alpha, torch::Tensor x_out,
-                    torch::Tensor y_out, bool rows) {
+                    torch::Tensor y_out, bool rows, c10::optional<std::vector<torch::Tensor>> frag_job, bool frag_bf16) {
   need(theta, torch::kFloat32, "theta");
   need(params, torch::kFloat32, "params");
   const int64_t K = params.size(0), P = params.size(1);
@@ -427,13 +427,31 @@ void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<tor
   if (idx.size(1) != K || lid.numel() != K || x_out.dim() != 4 || x_out.size(0) != S || x_out.size(1) != K ||
       x_out.size(2) != B || x_out.size(3) < F || y_out.numel() < S * K * B || mode < 0 || mode > 2)
     throw std::invalid_argument("round_prologue: output shapes / mode");
+  // frag_job = (slot_tab int32 [n_slots, 9], frags int32 [n_slots * 4 * 128 * 4]): the MFMA engine's shared
+  // fragments of the round's first step, built from theta by extra blocks of the same launch
+  const int* slot_tab = nullptr;
+  void* frags = nullptr;
+  int n_slots = 0;
+  if (frag_job && !frag_job->empty()) {
+    if (frag_job->size() != 2) throw std::invalid_argument("round_prologue: frag_job = (slot_tab, frags)");
+    const torch::Tensor& stab = (*frag_job)[0];
+    const torch::Tensor& fr = (*frag_job)[1];
+    need(stab, torch::kInt32, "slot_tab");
+    need(fr, torch::kInt32, "frags");
+    if (stab.dim() != 2 || stab.size(1) != 9) throw std::invalid_argument("round_prologue: slot_tab [n_slots, 9]");
+    n_slots = (int)stab.size(0);
+    if (fr.numel() < (int64_t)n_slots * 4 * 128 * 4) throw std::invalid_argument("round_prologue: frags too small");
+    slot_tab = stab.data_ptr<int>();
+    frags = fr.data_ptr();
+  }
   // rows = false: params only gives the [K, P] shape (the first local step reads theta; CFed fused SGD)
   check(qfx_launch_round_prologue(ptr<float>(theta), (int)K, (int)P, rows ? ptr<float>(params) : nullptr, ptr<float>(mt),
                                   ptr<float>(vt),
                                   ptr<float>(tt), tt.defined() ? (int)tt.numel() : 0, ptr<float>(X),
                                   ptr<long long>(Y), ptr<long long>(lid), ptr<long long>(idx), (int)S, (int)B,
                                   (long)X.size(1), (int)F, (int)mode, (float)alpha, ptr<float>(x_out),
-                                  (int)x_out.size(3), ptr<long long>(y_out), cur_stream()),
+                                  (int)x_out.size(3), ptr<long long>(y_out), slot_tab, n_slots, frags,
+                                  frag_bf16 ? 1 : 0, cur_stream()),
         "qfx_round_prologue");
 }
 
@@ -629,7 +647,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("round_prologue", &round_prologue, pybind11::arg("theta"), pybind11::arg("params"), pybind11::arg("m"),
         pybind11::arg("v"), pybind11::arg("t"), pybind11::arg("X"), pybind11::arg("Y"), pybind11::arg("lid"),
         pybind11::arg("idx"), pybind11::arg("mode"), pybind11::arg("alpha"), pybind11::arg("x_out"),
-        pybind11::arg("y_out"), pybind11::arg("rows") = true);
+        pybind11::arg("y_out"), pybind11::arg("rows") = true, pybind11::arg("frag_job") = pybind11::none(),
+        pybind11::arg("frag_bf16") = false);
   m.def("amp_scratch", &amp_scratch);
   m.def("readout_noise", &readout_noise);
   m.def("philox_uniform", &philox_uniform);

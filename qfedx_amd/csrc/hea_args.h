@@ -22,8 +22,9 @@ struct HeaPassArgs {
   const float* xang;         // [S][x_stride] feature angles
   int x_stride;
   const float* params;       // [K][p_stride]
-  const void* frags;         // uint4 unitary fragments (hea_frag_kernel)
+  const void* frags;         // uint4 unitary fragments (hea_frag.h)
   int n_slots;
+  int frag_shared;           // 1: one fragment set for every client (a round's first step, built by the prologue)
   const float* wread;        // [S][C] dL/d<Z_c>
   float* part;               // [S][n_tiles][C] readout partials
   long long* gslab;          // [S][slab_tiles][n_gradops][32] 2^-32 fixed-point partial traces

@@ -59,7 +59,8 @@ void check(int rc, const char* what) {
 }
 
 // geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
-//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, bf16, n_regions]
+//         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, bf16, n_regions,
+//         frag_shared]
 // bf16: states and fragments in bf16 (hea_mfma_bf16.hip) instead of fp16.  dbg: the stall-attribution buffer of the
 // stamps build (int64 [HEA_STAMP_ROWS * 16]; empty otherwise)
 void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, torch::Tensor fo, std::vector<int64_t> geom, double scale,
@@ -68,7 +69,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, torch::Tensor
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
               torch::Tensor gslab, torch::Tensor dbg, c10::optional<std::vector<torch::Tensor>> readout,
               int64_t ro_tps) {
-  need(geom.size() == 29, "geometry vector must have 29 entries");
+  need(geom.size() == 30, "geometry vector must have 30 entries");
   const bool bf16 = geom[27] != 0;
   HeaPassArgs a{};
   a.n = (int)geom[0];
@@ -94,6 +95,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, torch::Tensor
   a.n_gradops = (int)geom[25];
   a.in_rep = (int)geom[26];
   a.n_regions = (int)geom[28];
+  a.frag_shared = geom[29] != 0 ? 1 : 0;
   need(a.n_regions >= 0 && a.n_regions <= 2 * 32, "gradient regions per pass out of range");
   a.scale = (float)scale;
   a.dbg = dbg.defined() && dbg.numel() > 0 ? dp<long long>(dbg, torch::kInt64, "dbg", (int64_t)HEA_STAMP_ROWS * 16)
@@ -128,7 +130,9 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, torch::Tensor
   // layer-1 factors: the product-state generation (forward gen passes)
   a.xang = a.gen ? dp<float>(xang, torch::kFloat32, "xang", S / a.in_rep * a.x_stride) : nullptr;
   a.params = dp<float>(params, torch::kFloat32, "params", K * a.p_stride);
-  a.frags = a.n_slots ? (const void*)dp<int32_t>(frags, torch::kInt32, "frags", K * a.n_slots * 4 * 128 * 4) : nullptr;
+  a.frags = a.n_slots ? (const void*)dp<int32_t>(frags, torch::kInt32, "frags",
+                                                  (a.frag_shared ? 1 : K) * a.n_slots * 4 * 128 * 4)
+                      : nullptr;
   a.part = dp<float>(part, torch::kFloat32, "part", 0);
   if (readout && !readout->empty()) {
     // fused readout (first adjoint pass): readout = (y int64 [S], wts [S], expz [S, C], w_out [S, C],

@@ -443,7 +443,7 @@ __device__ __forceinline__ void dma_frags(const PassArgs& a, int k, const int* f
 #pragma unroll
   for (int g = 0; g < 2; ++g) {
     if (fi[g] < 0) continue;
-    const uint4* fr = (const uint4*)a.frags + ((size_t)k * a.n_slots * 4 + fi[g]) * 128 + lane;
+    const uint4* fr = (const uint4*)a.frags + ((size_t)(a.frag_shared ? 0 : k) * a.n_slots * 4 + fi[g]) * 128 + lane;
     // Issued as inline asm: the compiler's wait-count pass cannot tell which LDS bytes a builtin DMA writes (no
     // alias scopes reach codegen), so it waited for the DMA before the op's first LDS store or atomic and exposed
     // the fragment latency in every op.  The slot is only read after op_barrier's vmcnt(0) + barrier, and a

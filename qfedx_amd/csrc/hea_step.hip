@@ -2,67 +2,17 @@
 // slot) before a step, and the fixed-order gradient reduction of the pass kernels' slab (with the fused readout
 // sums and the optional fused Adam step).  hea_mfma_bf16.hip includes this file for the bf16 fragment build.
 #include "hea_common.h"
+#include "hea_frag.h"
 
 namespace HEA_NS {
 
-// Unitary fragments: per (client, slot) U and U^H in the real 32 x 32 embedding, laid out as the MFMA
-// A operand of v_mfma_f32_16x16x32_f16 (lane l: row 16h + (l & 15), k = 8 (l >> 4) .. +7), hi and lo fp16.
-// Rows are ordered (component, amplitude): row 16 h + m' is the re (h = 0) or im (h = 1) part of output m'.
-// The same registers are the B operand of the transposed product X^T M^T (group_back_t).
-// frags[((k * n_slots + slot) * 4 + f) * 128 + h * 64 + lane], f = 0 U hi, 1 U lo, 2 U^H hi, 3 U^H lo.
+// Unitary fragments of every (client, slot): hea_frag.h (layout), one 256-thread block each.
 __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__ params, int p_stride,
                                                        const int* __restrict__ slot_tab, int n_slots,
                                                        uint4* __restrict__ frags) {
   const int slot = blockIdx.x, k = blockIdx.y;
-  const int t = threadIdx.x, dag = t >> 7, h = (t >> 6) & 1, lane = t & 63;
-  const int* st = slot_tab + slot * 9;
-  const int nreal = st[0];
-  const float* prm = params + (size_t)k * p_stride;
-  // per qubit j: RZ(ph) RX(th) = [[e- c, -i e- s], [-i e+ s, e+ c]], e-+ = cp -+ i sp (identity past nreal)
-  float cj[4], sj[4], cpj[4], spj[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    cj[j] = 1.f, sj[j] = 0.f, cpj[j] = 1.f, spj[j] = 0.f;
-    if (j < nreal) {
-      __sincosf(0.5f * prm[st[1 + j]], &sj[j], &cj[j]);
-      __sincosf(0.5f * prm[st[5 + j]], &spj[j], &cpj[j]);
-    }
-  }
-  // real output row r = 16 h + (lane & 15) is component cr = h (0 re, 1 im) of amplitude m' = lane & 15: a block's
-  // result then holds the re and im of one amplitude in the same register of its two 16-row tiles
-  st_t hi[8], lo[8];
-#pragma unroll
-  for (int jj = 0; jj < 8; ++jj) {
-    const int kk = 8 * (lane >> 4) + jj;
-    const int mp = lane & 15, cr = h, m = kk >> 1, ck = kk & 1;
-    const int row = dag ? m : mp, colm = dag ? mp : m;   // U^H[mp][m] = conj(U[m][mp])
-    float2 v = make_float2(1.f, 0.f);
-    // entry (row_j, col_j) of qubit j's 2 x 2 factor, formed arithmetically (a run-time index into a table of
-    // the four entries put it in scratch): diagonal (cp c, +-sp c), off-diagonal (+-sp s, -cp s), sign + for row 1
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool rb = (row >> j) & 1, cb = (colm >> j) & 1;
-      const float e = rb ? spj[j] : -spj[j];
-      const float2 f = rb == cb ? make_float2(cpj[j] * cj[j], e * cj[j]) : make_float2(e * sj[j], -cpj[j] * sj[j]);
-      v = cmul(v, f);
-    }
-    if (dag) v.y = -v.y;
-    const float val = cr == 0 ? (ck == 0 ? v.x : -v.y) : (ck == 0 ? v.y : v.x);
-    hi[jj] = (st_t)val;
-    lo[jj] = (st_t)(val - (float)hi[jj]);
-  }
-  uint4 H, Lw;
-  uint32_t* hp = (uint32_t*)&H;
-  uint32_t* lp = (uint32_t*)&Lw;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    half2v a2 = {hi[2 * i], hi[2 * i + 1]}, b2 = {lo[2 * i], lo[2 * i + 1]};
-    hp[i] = __builtin_bit_cast(uint32_t, a2);
-    lp[i] = __builtin_bit_cast(uint32_t, b2);
-  }
-  uint4* base = frags + ((size_t)(k * n_slots + slot) * 4 + 2 * dag) * 128;
-  base[h * 64 + lane] = H;
-  base[128 + h * 64 + lane] = Lw;
+  hea_frag::build<st_t>(params + (size_t)k * p_stride, slot_tab + slot * 9, threadIdx.x,
+                        frags + (size_t)(k * n_slots + slot) * 4 * 128);
 }
 
 // Per client and gradient op: exact int64 sums of the 32 partial-trace slots over the client's samples and

@@ -16,6 +16,7 @@
 #include "qfx_adam.h"
 #include "qfx_plan.h"
 #include "qfx_readout.h"
+#include "hea_frag.h"
 
 namespace qfx {
 
@@ -931,30 +932,54 @@ __global__ void __launch_bounds__(256) qfx_batch_gather_kernel(BatchGather g) { 
 // Round prologue in ONE launch: blocks [0, K * chunks) initialise the client rows / optimizer state (as
 // qfx_round_init_kernel), the rest gather and encode the minibatches of EVERY local step of the round (as
 // qfx_batch_gather_kernel over steps * K * B rows).  Neither part reads what the other writes.
-__global__ void __launch_bounds__(256) qfx_round_prologue_kernel(RoundInit ri, int chunks, BatchGather g) {
+// The MFMA engine's fragments of the round's first local step (every client row starts as theta): one shared set,
+// built from theta by n_slots extra blocks of the prologue launch (hea_frag.h) instead of a per-client frag launch.
+struct FragJob {
+  const int* slot_tab;    // [n_slots][9]
+  int n_slots;            // 0: none
+  uint4* frags;           // [n_slots][4][128]
+  int bf16;
+};
+
+__global__ void __launch_bounds__(256) qfx_round_prologue_kernel(RoundInit ri, int chunks, BatchGather g, FragJob fj,
+                                                                 long gather_blocks) {
   const int init_blocks = ri.K * chunks;
   if ((int)blockIdx.x < init_blocks) {
     round_init_chunk(ri, blockIdx.x / chunks, blockIdx.x % chunks);
     return;
   }
-  gather_row(g, (long)blockIdx.x - init_blocks);
+  const long b = (long)blockIdx.x - init_blocks;
+  if (b < gather_blocks) {
+    gather_row(g, b);
+    return;
+  }
+  const int slot = (int)(b - gather_blocks);
+  uint4* out = fj.frags + (size_t)slot * 4 * 128;
+  if (fj.bf16)
+    hea_frag::build<__bf16>(ri.theta, fj.slot_tab + slot * 9, threadIdx.x, out);
+  else
+    hea_frag::build<_Float16>(ri.theta, fj.slot_tab + slot * 9, threadIdx.x, out);
 }
 
 extern "C" int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, float* m, float* v, float* t,
                                          int nt, const float* X, const long long* Y, const long long* lid,
                                          const long long* idx, int steps, int B, long nmax, int F, int mode,
-                                         float alpha, float* xo, int x_stride, long long* yo, hipStream_t st) {
+                                         float alpha, float* xo, int x_stride, long long* yo, const int* slot_tab,
+                                         int n_slots, void* frags, int bf16, hipStream_t st) {
   if (K <= 0 || P <= 0) return 0;
+  if (n_slots < 0 || (n_slots > 0 && (!slot_tab || !frags))) return (int)hipErrorInvalidValue;
   // without client rows or moments to set, only the step counters need a block (chunk 0 of row 0)
   const bool rows = params || m || v;
   const int chunks = rows ? (P + SG_E - 1) / SG_E : (t ? 1 : 0);
   const int kinit = rows ? K : (t ? 1 : 0);
-  const long blocks = (long)kinit * chunks + (long)steps * K * B;
+  const long gather = (long)steps * K * B;
+  const long blocks = (long)kinit * chunks + gather + n_slots;
   if (blocks > 0x7fffffffL) return (int)hipErrorInvalidValue;
   if (blocks == 0) return 0;
   hipLaunchKernelGGL(qfx_round_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
                      RoundInit{theta, kinit, P, params, m, v, t, nt}, chunks,
-                     BatchGather{X, Y, lid, idx, K, B, nmax, F, mode, alpha, xo, x_stride, yo});
+                     BatchGather{X, Y, lid, idx, K, B, nmax, F, mode, alpha, xo, x_stride, yo},
+                     FragJob{slot_tab, n_slots, (uint4*)frags, bf16}, gather);
   return (int)hipGetLastError();
 }
 

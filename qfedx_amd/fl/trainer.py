@@ -264,10 +264,14 @@ class VQCClientTrainer:
             dummy = torch.zeros(K, BT, 0 if spec.noisy else 1, device=self.device) if spec.amplitude else None
         else:
             rows = lid[:, None]
+        fj = None
         if upfront:
             m, v, t = opt.init_state()
+            # the MFMA engine's first-step fragments come from theta in the same launch (every row starts as theta)
+            fj = self.engine.prologue_frag_job() if method == "adjoint" and noise is None else None
             ext().round_prologue(theta.float().contiguous(), params, m, v, t, X, Y, lid, idx_d.contiguous(), mode,
-                                 float(spec.alpha), xbuf, ybuf)
+                                 float(spec.alpha), xbuf, ybuf, frag_job=fj,
+                                 frag_bf16=bool(getattr(self.engine.hip, "bf16", False)))
         else:
             opt.init_round(params, theta.float())
         for s in range(steps):
@@ -292,7 +296,8 @@ class VQCClientTrainer:
             xang = self.engine.augment(xang, traj_keys, s)
             res = self.engine.loss_and_grads(xang, yb, ws, params, method, rng_keys=(cfg.seed, round_num, s),
                                              readout_keys=ro_keys, step=s, out_loss=loss_all[s],
-                                             out_correct=correct_all[s], init=init, fused_opt=(opt, act_d[s]))
+                                             out_correct=correct_all[s], init=init, fused_opt=(opt, act_d[s]),
+                                             shared_frags=fj[1] if (fj is not None and s == 0) else None)
             if not res.get("opt_done", False):      # the MFMA engine runs HIP Adam inside its gradient reduction
                 opt.step(params, res["grad"], act_d[s])
         return params, loss_all, correct_all

@@ -125,6 +125,11 @@ class VQCEngine:
                              f"{' + %d noise selectors' % self.spec.n_noise_ops if self.spec.noisy else ''}, "
                              f"got {xang.shape[-1]}; set data.n_features = model.n_qubits")
 
+    def prologue_frag_job(self):
+        """The MFMA engine's (slot_tab, frags) for the round prologue (None for every other engine)."""
+        job = getattr(self.hip, "prologue_frag_job", None)
+        return job() if job is not None else None
+
     def augment(self, xang: torch.Tensor, keys: Optional[torch.Tensor], step: int) -> torch.Tensor:
         """Append this step's noise-trajectory Pauli selectors to the encoded features [K, B, n]."""
         if not self.spec.noisy:
@@ -178,19 +183,21 @@ class VQCEngine:
                        rng_keys: tuple = (0,), readout_keys: Optional[torch.Tensor] = None,
                        step: int = 0, out_loss: Optional[torch.Tensor] = None,
                        out_correct: Optional[torch.Tensor] = None, init: Optional[torch.Tensor] = None,
-                       fused_opt=None) -> dict:
+                       fused_opt=None, shared_frags=None) -> dict:
         """Loss [K], gradient [K,P], correct [K] for [K,B] minibatches.  ``out_loss`` / ``out_correct``
         (optional [K] views, e.g. rows of a round buffer) receive the loss / hit counts in place.
         ``init`` = raw amplitudes [K,B,F<=2^n] or complex states (amplitude encoding; None otherwise).
         ``fused_opt`` = (BatchedOptimizer, active [K]): an engine that can fuse the local optimizer step into its
-        own launches (the MFMA engine: HIP Adam in the gradient reduction) does so and returns ``opt_done``."""
+        own launches (the MFMA engine: HIP Adam in the gradient reduction) does so and returns ``opt_done``.
+        ``shared_frags``: the MFMA engine's unitary fragments of this step, already built by the round prologue
+        (``prologue_frag_job``; a round's first step only, when every client row is the global vector)."""
         spec = self.spec
         self._check(xang, init)
         if self.backend == "hip" and method == "adjoint":
             nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
             if fused_opt is not None and getattr(self.hip, "fuses_optimizer", False):
                 return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step, out_loss,
-                                               out_correct, init, fused_opt=fused_opt)
+                                               out_correct, init, fused_opt=fused_opt, shared_frags=shared_frags)
             return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step, out_loss,
                                            out_correct, init)
         res = self._loss_and_grads(xang, y, wmask, params, method, spsa_c, rng_keys, readout_keys, step, init)

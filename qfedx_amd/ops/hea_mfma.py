@@ -198,11 +198,11 @@ class HeaMfmaProgram:
         return 1 << (self.n - self.passes[self.fwd_last][0].t)
 
     def _geom(self, p, gen, load_lam, store_psi, store_lam, B, p_stride, S, x_stride, K, in_rep: int = 1,
-              n_regions: int = 0):
+              n_regions: int = 0, shared: bool = False):
         return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
                 int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
                 self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep), int(self.bf16),
-                                                                 int(n_regions)]
+                                                                 int(n_regions), int(shared)]
 
     def _frags(self, params: torch.Tensor, K: int, tag: str = "") -> torch.Tensor:
         fr = self._buf(f"{tag}frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
@@ -210,7 +210,8 @@ class HeaMfmaProgram:
             ext().hea_frags(params, params.shape[1], self.slot_tab, self.n_slots, K, fr, self.bf16)
         return fr
 
-    def _forward(self, x, params, fr, K, B, part, store_last: bool = False, tag: str = "", dbg=None):
+    def _forward(self, x, params, fr, K, B, part, store_last: bool = False, tag: str = "", dbg=None,
+                 shared: bool = False):
         """Forward passes up to the readout pass ``fwd_last``; returns the stored pass outputs (all of them with
         ``store_last``: the adjoint starts each pass from its output; identity passes after ``fwd_last`` alias
         its output).  ``tag`` names the workspaces; ``dbg`` (stamps build): per-pass stall-attribution buffers."""
@@ -228,7 +229,7 @@ class HeaMfmaProgram:
             name = f"{tag}psi{j}" if store_last else f"{tag}pe{j % 2}"
             out = self._buf(name, N, torch.int32) if keep else empty
             psi_in = stored[-1] if j > 0 else empty
-            geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K)
+            geom = self._geom(p, j == 0, False, keep, False, B, params.shape[1], S, x.shape[1], K, shared=shared)
             C.hea_pass(False, fwd[0], fwd[1], fwd[2], geom, self.scale, psi_in, out, empty, empty, x, params, fr, fempty,
                        part if j == R else fempty, fempty, dbg[f"fwd{j}"] if dbg else _NODBG)
             if keep:
@@ -237,7 +238,8 @@ class HeaMfmaProgram:
             stored += [stored[R]] * (J - 1 - R)
         return stored
 
-    def _adjoint(self, x, params, fr, K, B, stored, wread, gslab, tag: str = "", readout=None, dbg=None):
+    def _adjoint(self, x, params, fr, K, B, stored, wread, gslab, tag: str = "", readout=None, dbg=None,
+                 shared: bool = False):
         """Adjoint passes, last pass first.  ``readout`` = (part, y, wts, expz, rec): the first adjoint pass computes
         every sample's readout and dL/d<Z> itself (fused readout; ``wread`` is then its output, read by the later
         passes) instead of taking ``wread`` from the readout kernel."""
@@ -252,7 +254,7 @@ class HeaMfmaProgram:
             _, _, adj, p = self.passes[j]
             lam_out = self._buf(f"{tag}lam{j % 2}", N, torch.int32) if j > 0 else empty
             geom = self._geom(p, False, j < J - 1, False, j > 0, B, params.shape[1], S, x.shape[1], K,
-                              n_regions=self.n_regions[j])
+                              n_regions=self.n_regions[j], shared=shared)
             if readout is not None and j == J - 1:
                 part, yy, ww, expz, rec = readout
                 C.hea_pass(True, adj[0], adj[1], adj[2], geom, self.scale, stored[j], empty, lam_in, lam_out, x,
@@ -503,18 +505,28 @@ class HeaMfmaProgram:
         """Noiseless steps compute the readout in the first adjoint pass (``fused_readout``)."""
         return noise is None and self.fused_readout and self.tiles_last * self.C <= 64
 
-    def _step(self, x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=None, dbg=None):
+    def prologue_frag_job(self):
+        """(slot_tab, frags) for the round prologue to build the first local step's fragments from the global
+        parameters (one shared set: every client row starts as theta), or None without unitary slots.  The trainer
+        then passes ``shared_frags=frags`` to that step's ``loss_and_grads`` (hea_frag.h; one launch fewer)."""
+        if not self.n_slots:
+            return None
+        return [self.slot_tab, self._buf("pfrags", self.n_slots * 4 * 128 * 4, torch.int32)]
+
+    def _step(self, x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=None, dbg=None,
+              shared_frags=None):
         """Forward, readout + CE, adjoint and gradient reduction of clients [0, K).
         ``adam`` = (tensors, hyper) from ``BatchedOptimizer.fused_adam``: the clients' Adam step runs in the
         gradient reduction's epilogue (one launch fewer per local step).  ``dbg``: stall-attribution buffers per
         pass (``stamp_buffers``, stamps build only)."""
         C = ext()
         S = K * B
-        fr = self._frags(p, K)
+        shared = shared_frags is not None
+        fr = shared_frags if shared else self._frags(p, K)
         part = self._buf("part", S * self.tiles_last * self.C, torch.float32)
         wread = self._buf("wread", S * self.C, torch.float32)
         gslab = self._buf("gslab", S * self.slab_tiles * self.n_gradops * 32, torch.int64)
-        stored = self._forward(x, p, fr, K, B, part, store_last=True, dbg=dbg)
+        stored = self._forward(x, p, fr, K, B, part, store_last=True, dbg=dbg, shared=shared)
         # Fused readout: the first adjoint pass computes each sample's <Z>, cross entropy and dL/d<Z> from the readout
         # partials, and the gradient reduction sums the clients' loss, hits and readout gradients - one launch fewer
         # per local step.
@@ -522,7 +534,8 @@ class HeaMfmaProgram:
         if self._fused_readout(noise):
             rec = self._buf("rorec", S * (2 * self.C + 2), torch.float32)
             ro = [rec, loss, correct]
-            self._adjoint(x, p, fr, K, B, stored, wread, gslab, readout=(part, yy, ww, expz, rec), dbg=dbg)
+            self._adjoint(x, p, fr, K, B, stored, wread, gslab, readout=(part, yy, ww, expz, rec), dbg=dbg,
+                          shared=shared)
         else:
             if noise is None:
                 C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
@@ -531,7 +544,7 @@ class HeaMfmaProgram:
                 from .statevec_hip import _keys
                 C.readout_ce(part, self.tiles_last, self.C, B, K, yy, ww, p, self.n_theta, expz, wread, loss,
                              correct, grad, True, noise.p01, noise.p10, noise.shots, _keys(keys, noise), int(step))
-            self._adjoint(x, p, fr, K, B, stored, wread, gslab, dbg=dbg)
+            self._adjoint(x, p, fr, K, B, stored, wread, gslab, dbg=dbg, shared=shared)
         if adam is None:
             C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1],
                               None, None, ro, self.C, self.n_theta)
@@ -548,7 +561,8 @@ class HeaMfmaProgram:
         return {nm: torch.zeros(rows, dtype=torch.int64, device=self.device) for nm in names}
 
     def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
-                       out_correct=None, init: torch.Tensor | None = None, fused_opt=None, dbg=None) -> dict:
+                       out_correct=None, init: torch.Tensor | None = None, fused_opt=None, dbg=None,
+                       shared_frags=None) -> dict:
         """One adjoint training step (same contract as ``HipProgram.loss_and_grads``).
         ``fused_opt`` = (BatchedOptimizer, active): with params updated in place (a contiguous fp32 tensor) and HIP
         Adam, the optimizer step runs in the gradient reduction's epilogue and the result says ``opt_done``;
@@ -572,7 +586,8 @@ class HeaMfmaProgram:
         want = K * (self.n_gradops + ro_rows) <= FUSED_ADAM_MAX_BLOCKS
         if want and fused_opt is not None and self.n_gradops > 0 and p.data_ptr() == params.data_ptr():
             adam = fused_opt[0].fused_adam(p, fused_opt[1])
-        self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=adam, dbg=dbg)
+        self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=adam, dbg=dbg,
+                   shared_frags=shared_frags)
         res = {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}
         if adam is not None:
             res["opt_done"] = True

@@ -598,3 +598,24 @@ def test_fused_reduce_dp_noise_scale_matches_host(cuda, scale):
     if scale is not None:                       # and it is not the unscaled noise
         full = gpu.finalize(gpu.local_reduce(tk.to(cuda), tg.to(cuda), w.to(cuda), 2, ids).cpu())[0]
         assert not torch.allclose(full, mb, atol=1e-3)
+
+
+def test_prologue_fragments_match_per_client_fragments(cuda, monkeypatch):
+    """The MFMA engine's first local step reads ONE fragment set built from theta by the round prologue launch
+    (hea_frag.h; every client row starts as theta) instead of the per-client fragment launch: the federated run is
+    bitwise the run with the prologue job disabled, over rounds of several local steps (later steps build
+    per-client fragments from the updated rows), graph-captured and eager."""
+    from tests.test_fl import small_cfg
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.ops.engine import VQCEngine
+    from qfedx_amd.parallel.dist import init_distributed
+    outs = []
+    for on in (True, False):
+        if not on:
+            monkeypatch.setattr(VQCEngine, "prologue_frag_job", lambda self: None)
+        cfg = small_cfg(num_rounds=3, n_qubits=12, n_layers=3, device="cuda", backend="hip", num_clients=5,
+                        local_epochs=2, state_dtype="mfma")
+        dev = torch.device("cuda", 0)
+        outs.append(run_experiment(cfg, world=init_distributed(dev), device=dev, backend="hip"))
+    assert torch.equal(outs[0]["params"], outs[1]["params"])
+    assert torch.equal(torch.tensor(outs[0]["accuracies"]), torch.tensor(outs[1]["accuracies"]))
