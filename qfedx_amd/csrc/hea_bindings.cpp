@@ -197,10 +197,17 @@ void hea_check_ops(torch::Tensor ops, torch::Tensor fidx, int64_t n_slots, int64
     if (code == 3) need(fi[2 * o + 1] == 4 * w[102] + 2, "fragment index / slot mismatch");
     if (!pair) need(fi[2 * o + 1] == -1, "a single op has one fragment set");
     if (code != 6 && code != 7) {
-      need(pair ? w[2] == 4 : (w[2] >= 0 && w[2] <= 4), "group size out of range");
+      // rotation pairs hold two 4-qubit groups; a layer-1 gradient pair (GRAD2) may have short groups (w[103]: Y's)
+      if (pair) need(code == 4 ? (w[2] >= 1 && w[2] <= 4 && w[103] >= 1 && w[103] <= 4) : (w[2] == 4 && w[103] == 4),
+                     "pair group sizes out of range");
+      else need(w[2] >= 0 && w[2] <= 4, "group size out of range");
       for (int j = 0; j < w[2]; ++j)
         need(w[12 + j] >= 0 && w[12 + j] < n_theta && w[16 + j] >= 0 && w[16 + j] < n_theta,
              "gradient slot out of range");
+      if (pair)
+        for (int j = 0; j < w[103]; ++j)
+          need(w[120 + j] >= 0 && w[120 + j] < n_theta && w[124 + j] >= 0 && w[124 + j] < n_theta,
+               "gradient slot out of range");
       for (int i = 20; i < 100; ++i) need(w[i] >= 0 && w[i] < (1 << t), "tile address out of range");
       if (pair)
         for (int i = 104; i < 120; ++i) need(w[i] >= 0 && w[i] < (1 << t), "tile address out of range");

@@ -52,7 +52,7 @@ enum { OP_APPLY = 1, OP_APPLY2 = 2, OP_BACK2 = 3, OP_GRAD2 = 4, OP_GRAD_L1 = 5, 
 enum { W_CODE = 0, W_SLOT = 1, W_NREAL = 2, W_FLAGS = 3, W_RFULL = 4, W_RT = 8, W_TH = 12, W_PH = 16, W_OFF = 20,
        W_BL = 36, W_BH = 68, W_GIDX = 100,
        // pair records (hea_plan.pair_table): group Y's row masks in the W_RT words, its records / OFF table here
-       W_RFULL2 = 8, W_GIDX2 = 101, W_SLOT2 = 102, W_OFF2 = 104 };
+       W_RFULL2 = 8, W_GIDX2 = 101, W_SLOT2 = 102, W_NREAL2 = 103, W_OFF2 = 104 };
 constexpr double FIX = 4294967296.0;   // 2^32: fixed point of the scaled gradient partial traces
 constexpr int F_BACK_PSI = 1;
 constexpr int F_BACK_TRANS = 2;   // OP_BACK (with F_BACK_PSI) in the transposed form: cross matrix at the op input

@@ -1278,7 +1278,7 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
         }
         if (tid == 0) {
           gmeta_s[reg][0] = opw[g ? W_GIDX2 : W_GIDX];
-          gmeta_s[reg][1] = opw[W_NREAL];
+          gmeta_s[reg][1] = opw[g ? W_NREAL2 : W_NREAL];   // (a layer-1 pair's groups may be short)
         }
         ++ngrad;
       }

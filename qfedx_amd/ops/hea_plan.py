@@ -52,7 +52,7 @@ PAIR_CODES = (OP_APPLY2, OP_BACK2, OP_GRAD2)
 OP_WORDS = 128
 W_CODE, W_SLOT, W_NREAL, W_FLAGS, W_RFULL, W_RT, W_TH, W_PH, W_OFF, W_BL, W_BH = 0, 1, 2, 3, 4, 8, 12, 16, 20, 36, 68
 # pair records: the second group's rows in the W_RT words, and
-W_RFULL2, W_GIDX2, W_SLOT2, W_OFF2, W_TH2, W_PH2 = 8, 101, 102, 104, 120, 124
+W_RFULL2, W_GIDX2, W_SLOT2, W_NREAL2, W_OFF2, W_TH2, W_PH2 = 8, 101, 102, 103, 104, 120, 124
 F_BACK_PSI = 1             # OP_BACK also un-applies the group on psi (still needed further back), in the transposed
                            # form (group_back_t): its cross matrix is taken at the op INPUT
 W_GIDX = 100               # gradient ops: global index of the op's partial-trace record in the slab
@@ -502,15 +502,34 @@ def _pair_score(H, vx: list, vy: list, rotation: bool) -> int:
     return a + b + int(_rank([v & 15 for v in bx]) == 4)
 
 
+def single_op_groups(plan: HEAPlan, p: Pass, mask: int) -> set:
+    """(layer, qubits) of the pass' groups that run as single ops in some program under pair mask ``mask``
+    (pass_programs): unpaired groups, both groups of a rotation pair when the forward or the adjoint splits it (the
+    adjoint's last pair when psi is no longer needed), and layer-1 groups outside a cross pair."""
+    out = set()
+    units = _pairs(plan, p, p.groups, bool(mask & 3))
+    for i, u in enumerate(units):
+        split = len(u) == 1 or not (mask & 1) or not (mask & 2) or (i == 0 and not p.l1)
+        if split:
+            out |= {(g.layer, tuple(g.qubits)) for g in u}
+    for u in _pairs(plan, p, p.l1, bool(mask & 4), cross=True):
+        if len(u) == 1:
+            out.add((u[0].layer, tuple(u[0].qubits)))
+    return out
+
+
 def layout_pass(plan: HEAPlan, p: Pass, seed: int = 0, tries: int = 256) -> None:
     """Pick the pass' LDS swizzle rows H and every group's column bits (bank-conflict search), scoring the chained
     pair ops the planner will form (``_pairs``) as well."""
     groups = p.groups + p.l1
     geoms = [_group_geom(plan, p, g) for g in groups]
     vec = {(g.layer, tuple(g.qubits)): geo[0] for g, geo in zip(groups, geoms)}
-    pairs = [(u, True) for u in _pairs(plan, p, p.groups, True) if len(u) == 2]
-    pairs += [(u, False) for u in _pairs(plan, p, p.l1, True) if len(u) == 2]
-    full = FULL_SCORE * len(groups) + sum(3 if rot else 2 for _, rot in pairs)
+    mask = _pair_default()
+    pairs = [(u, True) for u in _pairs(plan, p, p.groups, bool(mask & 3)) if len(u) == 2]
+    pairs += [(u, False) for u in _pairs(plan, p, p.l1, bool(mask & 4), cross=True) if len(u) == 2]
+    solo = single_op_groups(plan, p, mask)
+    single = [(g.layer, tuple(g.qubits)) in solo for g in groups]
+    full = FULL_SCORE * sum(single) + sum(3 if rot else 2 for _, rot in pairs)
     hb = max(p.t - BANK_BITS, 0)
     rng = np.random.default_rng(1234 + seed)
     best = None
@@ -520,7 +539,7 @@ def layout_pass(plan: HEAPlan, p: Pass, seed: int = 0, tries: int = 256) -> None
         for gi, (allv, _, _, _, _, _, dirs) in enumerate(geoms):
             sc, c = _best_cols(H, allv, dirs, gi < len(p.groups))
             cols.append(c)
-            score += sc
+            score += sc if single[gi] else 0
         for (g, h), rot in pairs:
             score += _pair_score(H, vec[(g.layer, tuple(g.qubits))], vec[(h.layer, tuple(h.qubits))], rot)
         if best is None or score > best[0]:
@@ -572,12 +591,15 @@ def group_table(plan: HEAPlan, p: Pass, g: Group, code: int, flags: int = 0) -> 
     return w
 
 
-def pairable(plan: HEAPlan, p: Pass, gx: Group, gy: Group) -> bool:
+def pairable(plan: HEAPlan, p: Pass, gx: Group, gy: Group, cross: bool = False) -> bool:
     """Two rotation groups can run as one chained pair op: one layer (so one CNOT frame: each group's row masks
     annihilate the other's vectors and their 8 vectors are independent), 4 real qubits each, and at least one
-    256-amplitude coset per... tile of 2^t >= 2^11 (8 cosets: one per wave of a forward workgroup at least)."""
-    return (gx.layer == gy.layer and gx.layer >= 1 and len(gx.qubits) == GROUP and len(gy.qubits) == GROUP
-            and p.t >= 11 and not set(gx.qubits) & set(gy.qubits))
+    256-amplitude coset per... tile of 2^t >= 2^11 (8 cosets: one per wave of a forward workgroup at least).
+    ``cross`` (layer-1 gradient pairs, OP_GRAD2: cross matrices only, no unitary): a group may be short - its padding
+    vectors (``_neutral_pads``) act as more column coordinates, and only its real qubits get partial traces."""
+    sizes_ok = (1 <= len(gx.qubits) <= GROUP and 1 <= len(gy.qubits) <= GROUP) if cross else \
+        (len(gx.qubits) == GROUP and len(gy.qubits) == GROUP)
+    return (gx.layer == gy.layer and gx.layer >= 1 and sizes_ok and p.t >= 11 and not set(gx.qubits) & set(gy.qubits))
 
 
 def pair_table(plan: HEAPlan, p: Pass, gx: Group, gy: Group, code: int, flags: int = 0) -> np.ndarray:
@@ -588,20 +610,22 @@ def pair_table(plan: HEAPlan, p: Pass, gx: Group, gy: Group, code: int, flags: i
     index into the tile bits outside both groups' pivots (logical coordinates 0 in both groups).  The kernel chains
     the two 16 x 16 products in registers: X in the transposed MFMA form leaves each lane holding its x-amplitude of 4
     y-columns, which is exactly the operand layout of Y's product over y (csrc/hea_mfma.hip, group_pair)."""
-    if not pairable(plan, p, gx, gy):
+    if not pairable(plan, p, gx, gy, cross=code == OP_GRAD2):
         raise ValueError("groups cannot be paired")
     n, t = plan.n, p.t
     w = np.zeros(OP_WORDS, dtype=np.int64)
     w[W_CODE] = code
     w[W_FLAGS] = flags
-    w[W_NREAL] = GROUP
+    w[W_NREAL], w[W_NREAL2] = len(gx.qubits), len(gy.qubits)
     geo = []
     for g, (wr, wth, wph, woff, wsl) in ((gx, (W_RFULL, W_TH, W_PH, W_OFF, W_SLOT)),
                                           (gy, (W_RFULL2, W_TH2, W_PH2, W_OFF2, W_SLOT2))):
         allv, rfull, rt, off, _, bits, _ = _group_geom(plan, p, g)
         geo.append((allv, off, bits))
         w[wsl] = g.slot
-        for j in range(GROUP):
+        w[wth:wth + GROUP] = -1                # (a short group's padding: no slots, row masks 0 - parity 0 always)
+        w[wph:wph + GROUP] = -1
+        for j in range(len(g.qubits)):
             w[wr + j] = rfull[j]
             w[wth + j] = plan.theta_slot(g.layer, g.qubits[j])
             w[wph + j] = plan.theta_slot(g.layer, g.qubits[j]) + 1
@@ -648,11 +672,11 @@ def obs_table(plan: HEAPlan, p: Pass, code: int) -> np.ndarray:
     return w
 
 
-def _pairs(plan: HEAPlan, p: Pass, groups: list, pair: bool) -> list:
+def _pairs(plan: HEAPlan, p: Pass, groups: list, pair: bool, cross: bool = False) -> list:
     """Greedy left-to-right grouping of consecutive pairable groups: [(g,), (g, h), ...]."""
     out, i = [], 0
     while i < len(groups):
-        if pair and i + 1 < len(groups) and pairable(plan, p, groups[i], groups[i + 1]):
+        if pair and i + 1 < len(groups) and pairable(plan, p, groups[i], groups[i + 1], cross):
             out.append((groups[i], groups[i + 1]))
             i += 2
         else:
@@ -679,9 +703,9 @@ def pass_programs(plan: HEAPlan, meta: list | None = None, pair: bool | None = N
     J = len(plan.passes)
 
     def meta_row(w, x: str):
-        th, ph = (W_TH, W_PH) if x == "x" else (W_TH2, W_PH2)
+        th, ph, nr = (W_TH, W_PH, W_NREAL) if x == "x" else (W_TH2, W_PH2, W_NREAL2)
         inside = 16 if (int(w[W_CODE]) in (OP_BACK, OP_BACK2) and int(w[W_FLAGS]) & F_BACK_PSI) else 0
-        gmeta.append([1 << (plan.n - p.t), int(w[W_NREAL]) | inside] + [int(v) for v in w[th:th + 4]] +
+        gmeta.append([1 << (plan.n - p.t), int(w[nr]) | inside] + [int(v) for v in w[th:th + 4]] +
                      [int(v) for v in w[ph:ph + 4]])
     for j, p in enumerate(plan.passes):
         units = _pairs(plan, p, p.groups, bool(pair & 3))
@@ -706,7 +730,7 @@ def pass_programs(plan: HEAPlan, meta: list | None = None, pair: bool | None = N
                 adj.append(group_table(plan, p, u[0], OP_BACK, F_BACK_PSI if psi_needed else 0))
             else:
                 adj.append(group_table(plan, p, u[0], OP_BACK, F_BACK_PSI if psi_needed else 0))
-        for u in _pairs(plan, p, p.l1, bool(pair & 4)):
+        for u in _pairs(plan, p, p.l1, bool(pair & 4), cross=True):
             adj.append(group_table(plan, p, u[0], OP_GRAD_L1) if len(u) == 1 else
                        pair_table(plan, p, u[0], u[1], OP_GRAD2))
         for w in adj:
@@ -827,6 +851,7 @@ def _pair_half(w, which: str):
     """A single-op view (W_NREAL, W_TH, W_PH, W_GIDX) of group X or Y of a pair record (emulator)."""
     v = np.array(w, copy=True)
     if which == "y":
+        v[W_NREAL] = w[W_NREAL2]
         v[W_TH:W_TH + 4] = w[W_TH2:W_TH2 + 4]
         v[W_PH:W_PH + 4] = w[W_PH2:W_PH2 + 4]
         v[W_SLOT] = w[W_SLOT2]

@@ -39,8 +39,9 @@ def test_kernel_matches_oracle(cuda, n, L, C, feat, ro):
 
 
 def test_48_qubits_match_torch_mps_and_train(cuda):
-    """The BASELINE MPS shape (48 qubits, 3 layers): <Z> and the engine's loss / gradients on the HIP kernel equal
-    the generic torch MPS backend (reverse-mode AD through its einsum network) to fp32 rounding."""
+    """The BASELINE MPS shape (48 qubits, 3 layers): the kernel's <Z> and gradients match the float64 oracle, and the
+    engine's loss / gradients on the HIP kernel equal the generic torch MPS backend (reverse-mode AD through its
+    complex64 einsum network) to fp32 accumulation over 48 sites."""
     from qfedx_amd.ops.engine import VQCEngine
     spec = VQCSpec(48, 3, 3, readout_scale=3.0)
     g = torch.Generator().manual_seed(3)
@@ -58,7 +59,18 @@ def test_48_qubits_match_torch_mps_and_train(cuda):
     ref = eng.loss_and_grads(xang, y, wm, params)
     ez_ref = eng.expz(xang, spec.split(params)[0])
     torch.cuda.synchronize()
-    np.testing.assert_allclose(ez.cpu().numpy(), ez_ref.cpu().numpy(), atol=2e-5)
-    np.testing.assert_allclose(fast["loss"].cpu().numpy(), ref["loss"].cpu().numpy(), rtol=1e-5, atol=1e-6)
-    np.testing.assert_allclose(fast["grad"].cpu().numpy(), ref["grad"].cpu().numpy(), atol=2e-5)
+    np.testing.assert_allclose(ez.cpu().numpy(), ez_ref.cpu().numpy(), atol=1e-4)
+    np.testing.assert_allclose(fast["loss"].cpu().numpy(), ref["loss"].cpu().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(fast["grad"].cpu().numpy(), ref["grad"].cpu().numpy(), atol=1e-4)
     assert torch.equal(fast["correct"], ref["correct"])
+    # two samples against the float64 oracle (the kernel's own error, not the difference of two fp32 paths)
+    th = spec.split(params)[0]
+    w = torch.randn(1, 2, 3, generator=g).to(cuda)
+    from qfedx_amd.ops.mps_hip import MpsChainProgram
+    kp = MpsChainProgram(spec, cuda)
+    z1 = kp.expz(xang[:1, :2].contiguous(), th[:1].contiguous())
+    g1 = kp.grads(xang[:1, :2].contiguous(), th[:1].contiguous(), w)
+    zo, go = chain_columns(xang[0, :2].double().cpu().numpy(), th[:1].double().cpu().numpy().repeat(2, 0), 48, 3,
+                           spec.readout, "ry", w[0].double().cpu().numpy())
+    np.testing.assert_allclose(z1[0].cpu().numpy(), zo, atol=2e-5)
+    np.testing.assert_allclose(g1[0].cpu().numpy(), go.sum(0), atol=5e-5)
