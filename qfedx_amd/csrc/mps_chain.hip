@@ -49,7 +49,7 @@ struct Col {
 
 __device__ __forceinline__ void build_col(const MpsArgs& g, const float* th, float xq, int q, int a, int b, Col& c) {
   float s0, c0;
-  __sincosf(0.5f * xq, &s0, &c0);
+  sincosf(0.5f * xq, &s0, &c0);   // (precise: the __sincosf error drifted the norm by ~3e-5 over 48 x 3 gates)
   if (g.feature == 1) {                    // rx
     c.v0 = make_float2(c0, 0.f);
     c.v1 = make_float2(0.f, -s0);
@@ -64,8 +64,8 @@ __device__ __forceinline__ void build_col(const MpsArgs& g, const float* th, flo
   for (int l = 0; l < 3; ++l) {
     if (l >= g.L) break;
     const int k = 2 * (l * g.n + q);
-    __sincosf(0.5f * th[k], &c.st[l], &c.ct[l]);
-    __sincosf(0.5f * th[k + 1], &c.sp[l], &c.cp[l]);
+    sincosf(0.5f * th[k], &c.st[l], &c.ct[l]);
+    sincosf(0.5f * th[k + 1], &c.sp[l], &c.cp[l]);
     c.vp[l][0] = c.v0;
     c.vp[l][1] = c.v1;
     // RX: [c, -i s; -i s, c]     (-i s z = (s z.y, -s z.x))
@@ -206,6 +206,9 @@ __global__ void __launch_bounds__(64 * WPB) mps_chain_kernel(MpsArgs g) {
     R[lane] = o;
     wave_lds();
   }
+  // <psi|psi> = Rp_0 (1 x 1): the readout is divided by it (exactly 1 up to fp32 rounding, as the torch MPS backend
+  // normalises), the gradients too (first order)
+  const float inv_norm = 1.f / R[0].x;
   // ---------------- readout <Z_c>: left sweep up to the last readout qubit
   float2* Lp = E1[wave];
   float2* LO = E2[wave];
@@ -309,8 +312,8 @@ __global__ void __launch_bounds__(64 * WPB) mps_chain_kernel(MpsArgs g) {
         if (l >= g.L) break;
         const float dt = wave_sum(part[2 * l]), dp = wave_sum(part[2 * l + 1]);
         if (lane == 0) {
-          gout[2 * (l * n + q)] = dt;      // (reverse_col already returns 2 Re)
-          gout[2 * (l * n + q) + 1] = dp;
+          gout[2 * (l * n + q)] = dt * inv_norm;      // (reverse_col already returns 2 Re)
+          gout[2 * (l * n + q) + 1] = dp * inv_norm;
         }
       }
     }
@@ -335,7 +338,7 @@ __global__ void __launch_bounds__(64 * WPB) mps_chain_kernel(MpsArgs g) {
   if (lane == 0) {
 #pragma unroll
     for (int i = 0; i < RMAX; ++i)
-      if (i < g.C) g.z[(size_t)s * g.C + i] = zc[i];
+      if (i < g.C) g.z[(size_t)s * g.C + i] = zc[i] * inv_norm;
   }
 }
 

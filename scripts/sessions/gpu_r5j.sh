@@ -11,7 +11,7 @@ step() {  # step <name> <seconds> <cmd...>
   echo "$name rc=$rc"; tail -3 "gpurun_out/r5j/$name.log" | cut -c1-600
   [ $rc -eq 0 ] || exit $rc
 }
-step hea_tests 400 python -u -m pytest tests/test_gpu_hea.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
+#step hea_tests 400 python -u -m pytest tests/test_gpu_hea.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider
 step gpu_tests 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider
 step bench64 300 python bench.py --steps 20 --warmup 3
 step share8 300 python bench.py --steps 30 --warmup 5 --clients 8
