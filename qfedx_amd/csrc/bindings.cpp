@@ -82,7 +82,8 @@ int qfx_launch_round_init(const float* theta, int K, int P, float* params, float
 int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, float* m, float* v, float* t, int nt,
                               const float* X, const long long* Y, const long long* lid, const long long* idx,
                               int steps, int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride,
-                              long long* yo, const int* slot_tab, int n_slots, void* frags, int bf16, hipStream_t st);
+                              long long* yo, const int* slot_tab, int n_slots, void* frags, int bf16, long long* zero,
+                              int nzero, hipStream_t st);
 int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx, int K,
                             int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride, long long* yo,
                             hipStream_t st);
@@ -403,7 +404,8 @@ void batch_gather(torch::Tensor X, torch::Tensor Y, torch::Tensor lid, torch::Te
 void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<torch::Tensor> m,
                     c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> t, torch::Tensor X, torch::Tensor Y,
                     torch::Tensor lid, torch::Tensor idx, int64_t mode, double alpha, torch::Tensor x_out,
-                    torch::Tensor y_out, bool rows, c10::optional<std::vector<torch::Tensor>> frag_job, bool frag_bf16) {
+                    torch::Tensor y_out, bool rows, c10::optional<std::vector<torch::Tensor>> frag_job, bool frag_bf16,
+                    c10::optional<torch::Tensor> zero) {
   need(theta, torch::kFloat32, "theta");
   need(params, torch::kFloat32, "params");
   const int64_t K = params.size(0), P = params.size(1);
@@ -444,6 +446,14 @@ void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<tor
     slot_tab = stab.data_ptr<int>();
     frags = fr.data_ptr();
   }
+  // zero: int64 entries the prologue zeroes (the all-reduce buffer head the MFMA engine's FedAvg tail adds into)
+  long long* zp = nullptr;
+  int64_t nz = 0;
+  if (zero && zero->defined() && zero->numel() > 0) {
+    need(*zero, torch::kInt64, "zero");
+    zp = zero->data_ptr<long long>();
+    nz = zero->numel();
+  }
   // rows = false: params only gives the [K, P] shape (the first local step reads theta; CFed fused SGD)
   check(qfx_launch_round_prologue(ptr<float>(theta), (int)K, (int)P, rows ? ptr<float>(params) : nullptr, ptr<float>(mt),
                                   ptr<float>(vt),
@@ -451,7 +461,7 @@ void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<tor
                                   ptr<long long>(Y), ptr<long long>(lid), ptr<long long>(idx), (int)S, (int)B,
                                   (long)X.size(1), (int)F, (int)mode, (float)alpha, ptr<float>(x_out),
                                   (int)x_out.size(3), ptr<long long>(y_out), slot_tab, n_slots, frags,
-                                  frag_bf16 ? 1 : 0, cur_stream()),
+                                  frag_bf16 ? 1 : 0, zp, (int)nz, cur_stream()),
         "qfx_round_prologue");
 }
 
@@ -648,7 +658,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("v"), pybind11::arg("t"), pybind11::arg("X"), pybind11::arg("Y"), pybind11::arg("lid"),
         pybind11::arg("idx"), pybind11::arg("mode"), pybind11::arg("alpha"), pybind11::arg("x_out"),
         pybind11::arg("y_out"), pybind11::arg("rows") = true, pybind11::arg("frag_job") = pybind11::none(),
-        pybind11::arg("frag_bf16") = false);
+        pybind11::arg("frag_bf16") = false, pybind11::arg("zero") = pybind11::none());
   m.def("amp_scratch", &amp_scratch);
   m.def("readout_noise", &readout_noise);
   m.def("philox_uniform", &philox_uniform);

@@ -58,6 +58,26 @@ struct QfxAdamArgs {
   float lr, b1, b2, eps;
 };
 
+// The round's FedAvg folded into hea_grad_reduce's Adam epilogue (a round's last local step, plain FedAvg: no DP, no
+// SecAgg; buf == nullptr: none).  The last block of client k, right after its Adam step, adds the client's exact
+// fixed-point terms round(2^32 w_k wrap(theta_k - theta_g)) and weight round(2^32 w_k) into the all-reduce buffer head
+// with int64 atomics (integer sums: any arrival order gives the same bits, as the FedAvg reduce's own sums), which the
+// round prologue zeroed; the last of the K client epilogues packs the round metrics and, on a single rank, applies
+// the round to theta_g (the FedAvg launch's FusedApply).
+struct QfxFedTail {
+  long long* buf;            // [P + 6 + n_norms] all-reduce buffer
+  const float* theta_g;      // [P]
+  const unsigned char* mask; // [P] angle mask (wrapped entries)
+  const double* weights;     // [K] FedAvg weights
+  int wrap;
+  const float *loss, *correct, *nvalid, *act;   // round metric tables (n_metrics entries each)
+  int n_metrics;
+  unsigned* cnt;             // zero-initialised arrival counter of the client epilogues (the last one resets it)
+  float* apply_theta;        // single rank: theta_g updated in place (nullptr: the all-reduce + apply follow)
+  double* apply_out;         // [6 + n_norms] metrics / saturation / weight sum read back by the host
+  int n_norms;
+};
+
 // Per-client readout reduction in hea_grad_reduce (fused readout): one more block per client sums its samples' ro_rec
 // records in sample order into the loss / hit outputs and the readout-parameter gradients (a, b) of grad.
 struct QfxReadoutRed {

@@ -19,7 +19,7 @@ int qfx_hea_frags(const float* params, int p_stride, const int* slot_tab, int n_
                   hipStream_t st);
 int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc, int K,
                         float* params, float* grad, int p_stride, const QfxAdamArgs* adam,
-                        const QfxReadoutRed* readout, hipStream_t st);
+                        const QfxReadoutRed* readout, const QfxFedTail* fed, hipStream_t st);
 int qfx_hea_args_size();
 int qfx_hea_check_status(hipStream_t st);
 // bf16 state storage (hea_mfma_bf16.hip)
@@ -235,7 +235,8 @@ void hea_frags(torch::Tensor params, int64_t p_stride, torch::Tensor slot_tab, i
 void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops, torch::Tensor gmeta, int64_t spc,
                      int64_t K, torch::Tensor params, torch::Tensor grad, int64_t p_stride,
                      c10::optional<std::vector<torch::Tensor>> adam, c10::optional<std::vector<double>> hyper,
-                     c10::optional<std::vector<torch::Tensor>> readout, int64_t ro_c, int64_t ro_ntheta) {
+                     c10::optional<std::vector<torch::Tensor>> readout, int64_t ro_c, int64_t ro_ntheta,
+                     c10::optional<std::vector<torch::Tensor>> fed, bool fed_wrap, int64_t fed_n_norms) {
   QfxReadoutRed ro{};
   if (readout && !readout->empty()) {
     const auto& r = *readout;
@@ -261,10 +262,41 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
     ad.lr = (float)(*hyper)[0], ad.b1 = (float)(*hyper)[1], ad.b2 = (float)(*hyper)[2], ad.eps = (float)(*hyper)[3];
     need(n_gradops > 0 || ro.rec, "grad_reduce: fused Adam needs at least one reduction block");
   }
+  // fed = (buf int64 [P + 6 + n_norms], theta_g f32 [P], mask u8 [P], weights f64 [K], loss, correct, nvalid, act
+  // f32 [n], cnt int32 [1][, apply_theta f32 [P], apply_out f64 [6 + n_norms]]): the round's FedAvg in the Adam
+  // epilogue (QfxFedTail)
+  QfxFedTail ft{};
+  const bool fused_fed = fed && !fed->empty();
+  if (fused_fed) {
+    const auto& f = *fed;
+    need((f.size() == 9 || f.size() == 11) && ad.m, "grad_reduce: fed = 9 or 11 tensors, with the fused Adam step");
+    need(fed_n_norms >= 0, "grad_reduce: fed norm slots");
+    ft.buf = dp<long long>(f[0], torch::kInt64, "fed buf", p_stride + 6 + fed_n_norms);
+    ft.theta_g = dp<float>(f[1], torch::kFloat32, "fed theta_g", p_stride);
+    need(f[2].defined() && f[2].is_cuda() && f[2].scalar_type() == torch::kUInt8 && f[2].numel() >= p_stride,
+         "grad_reduce: fed angle mask");
+    ft.mask = f[2].data_ptr<uint8_t>();
+    ft.weights = dp<double>(f[3], torch::kFloat64, "fed weights", K);
+    const int64_t nm = f[4].numel();
+    ft.loss = dp<float>(f[4], torch::kFloat32, "fed loss", nm);
+    ft.correct = dp<float>(f[5], torch::kFloat32, "fed correct", nm);
+    ft.nvalid = dp<float>(f[6], torch::kFloat32, "fed nvalid", nm);
+    ft.act = dp<float>(f[7], torch::kFloat32, "fed act", nm);
+    ft.n_metrics = (int)nm;
+    ft.cnt = dp<unsigned>(f[8], torch::kInt32, "fed cnt", 1);
+    ft.wrap = fed_wrap ? 1 : 0;
+    ft.n_norms = (int)fed_n_norms;
+    if (f.size() == 11) {
+      ft.apply_theta = dp<float>(f[9], torch::kFloat32, "fed apply theta", p_stride);
+      ft.apply_out = dp<double>(f[10], torch::kFloat64, "fed apply out", 6 + fed_n_norms);
+      need(ft.apply_theta == ft.theta_g, "grad_reduce: the single-rank apply updates theta_g in place");
+    }
+  }
   check(qfx_hea_grad_reduce(dp<long long>(gslab, torch::kInt64, "gslab", K * spc * slab_tiles * n_gradops * 32),
                             (int)slab_tiles, (int)n_gradops, dp<int>(gmeta, torch::kInt32, "gmeta", n_gradops * 10),
                             (int)spc, (int)K, dp<float>(params, torch::kFloat32, "params", K * p_stride),
-                            dp<float>(grad, torch::kFloat32, "grad", K * p_stride), (int)p_stride, &ad, &ro, cur()),
+                            dp<float>(grad, torch::kFloat32, "grad", K * p_stride), (int)p_stride, &ad, &ro,
+                            fused_fed ? &ft : nullptr, cur()),
         "qfx_hea_grad_reduce");
 }
 
@@ -283,7 +315,8 @@ void register_hea(pybind11::module& m) {
         pybind11::arg("n_gradops"), pybind11::arg("gmeta"), pybind11::arg("spc"), pybind11::arg("K"),
         pybind11::arg("params"), pybind11::arg("grad"), pybind11::arg("p_stride"),
         pybind11::arg("adam") = pybind11::none(), pybind11::arg("hyper") = pybind11::none(),
-        pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_c") = 0, pybind11::arg("ro_ntheta") = 0);
+        pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_c") = 0, pybind11::arg("ro_ntheta") = 0,
+        pybind11::arg("fed") = pybind11::none(), pybind11::arg("fed_wrap") = false, pybind11::arg("fed_n_norms") = 0);
   m.def("hea_args_size", []() { return qfx_hea_args_size(); });
   m.attr("HEA_STAMP_ROWS") = HEA_STAMP_ROWS;
   // -1: release build (no device checks); 0: no failure since the last read; else the failing source line

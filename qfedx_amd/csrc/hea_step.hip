@@ -3,6 +3,7 @@
 // sums and the optional fused Adam step).  hea_mfma_bf16.hip includes this file for the bf16 fragment build.
 #include "hea_common.h"
 #include "hea_frag.h"
+#include "qfx_fedavg.h"
 
 namespace HEA_NS {
 
@@ -30,7 +31,7 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
                                                               int n_gradops, const int* __restrict__ gmeta, int spc,
                                                               float* __restrict__ params,
                                                               float* __restrict__ grad, int p_stride, QfxAdamArgs ad,
-                                                              QfxReadoutRed ro) {
+                                                              QfxReadoutRed ro, QfxFedTail ft) {
   // 8 groups of 32 lanes split the client's (sample, tile) rows; 4 independent loads in flight per lane; the
   // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
   const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
@@ -129,6 +130,45 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     const float gi = __hip_atomic_load(&grad[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     qfx_adam_elem(params, gi, ad.m, ad.v, ad.t_in, ad.t_out, ad.active, k, e, i == 0, ad.lr, ad.b1, ad.b2, ad.eps);
   }
+  if (!ft.buf) return;
+  // ---- the round's FedAvg (QfxFedTail): client k's terms from the row this block just updated
+  const double SC = 4294967296.0;
+  int nsat = 0;
+  __syncthreads();                                     // the block's own Adam stores, visible to the block
+  for (int e = tid; e < p_stride; e += 256) {
+    double d = (double)params[(size_t)k * p_stride + e] - (double)ft.theta_g[e];
+    if (ft.wrap && ft.mask[e]) d = qfx::wrap_pi(d);
+    const long long v = qfx::fixed_term(ft.weights[k] * d * SC, nsat);
+    if (v) atomicAdd((unsigned long long*)&ft.buf[e], (unsigned long long)v);
+  }
+  if (tid == 0) {
+    const long long v = qfx::fixed_term(ft.weights[k] * SC, nsat);
+    if (v) atomicAdd((unsigned long long*)&ft.buf[p_stride], (unsigned long long)v);
+  }
+  if (nsat) atomicAdd((unsigned long long*)&ft.buf[p_stride + 5], (unsigned long long)nsat);   // saturated terms
+  __shared__ int flast_s;
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();                                   // this client's terms published before its arrival
+    flast_s = atomicAdd(ft.cnt, 1u) == gridDim.x - 1;
+    if (flast_s) *ft.cnt = 0u;
+  }
+  __syncthreads();
+  if (!flast_s) return;
+  if (tid == 0) {                                      // every client's terms and metrics: acquire, drained
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  qfx::round_pack_block(qfx::RoundPack{ft.buf, ft.loss, ft.correct, ft.nvalid, ft.act, ft.n_metrics, nullptr,
+                                       nullptr, 0},
+                        p_stride);
+  if (!ft.apply_theta) return;
+  __syncthreads();
+  auto ld = [&](long i) { return __hip_atomic_load(&ft.buf[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  const double wsum = (double)ld(p_stride) / SC;
+  for (long e = tid; e < (long)p_stride + 6 + ft.n_norms; e += 256)
+    qfx::round_apply_elem(ft.buf, p_stride, ft.apply_theta, 1.0, ft.apply_out, 0, 1.0, ft.n_norms, e, wsum, ld);
 }
 #endif  // !QFX_HEA_BF16
 
@@ -145,7 +185,7 @@ extern "C" int HEA_EXT(qfx_hea_frags)(const float* params, int p_stride, const i
 #if !QFX_HEA_BF16
 extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n_gradops, const int* gmeta, int spc,
                                    int K, float* params, float* grad, int p_stride, const QfxAdamArgs* adam,
-                                   const QfxReadoutRed* readout, hipStream_t st) {
+                                   const QfxReadoutRed* readout, const QfxFedTail* fed, hipStream_t st) {
   if (K == 0) return 0;
   QfxReadoutRed ro{};
   if (readout) ro = *readout;
@@ -153,8 +193,13 @@ extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n
   if (rows == 0) return adam && adam->m ? (int)hipErrorInvalidValue : 0;   // no block would run the epilogue
   QfxAdamArgs ad{};
   if (adam) ad = *adam;
+  QfxFedTail ftl{};
+  if (fed) {
+    if (!adam || !adam->m) return (int)hipErrorInvalidValue;   // the FedAvg tail runs in the Adam epilogue
+    ftl = *fed;
+  }
   hipLaunchKernelGGL(HEA_NS::hea_grad_reduce_kernel, dim3(K, rows), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
-                     gmeta, spc, params, grad, p_stride, ad, ro);
+                     gmeta, spc, params, grad, p_stride, ad, ro, ftl);
   return (int)hipGetLastError();
 }
 

@@ -296,18 +296,48 @@ class FederatedRunner:
                 from ..ops._ext import ext
                 ext().round_apply(buf, P, params_g, 1.0, outs[v], *ring, NN)
 
+            def apply_variant(tabs, theta):
+                """The metrics buffer variant whose post() the single-rank apply may fold into (None: no fold)."""
+                v = tabs.get("variant", self._flip if tabs.get("eager") else None)
+                if (v is not None and not world.distributed and P + 6 + NN <= FUSED_APPLY_MAX
+                        and os.environ.get("QFEDX_FUSED_APPLY", "1") != "0"
+                        and theta.data_ptr() == params_g.data_ptr()):
+                    return v
+                return None
+
+            def fused_tail(tabs, theta):
+                # plain FedAvg (no DP noise / clipping, no SecAgg masks) folded into the MFMA engine's fused Adam
+                # epilogue of the last local step (hea_step.hip, QfxFedTail): same fixed-point terms, int64 atomics
+                # into the zeroed buffer head, metrics packed and (single rank) the round applied by the last client
+                if p.dp or p.secure_agg or NN or agg.backend != "hip" or \
+                        os.environ.get("QFEDX_FED_TAIL", "1") == "0":
+                    return None
+                if getattr(agg, "_mask_u8", None) is None:
+                    agg._mask_u8 = agg.angle_mask.to(torch.uint8).contiguous()
+                if getattr(self, "_tail_cnt", None) is None:
+                    self._tail_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+                fed = [buf, theta, agg._mask_u8, tabs.get("fw", tabs["w"]), tabs["loss"].reshape(-1),
+                       tabs["correct"].reshape(-1), tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1),
+                       self._tail_cnt]
+                v = apply_variant(tabs, theta)
+                if v is not None:
+                    fed += [params_g, outs[v]]
+                return {"fed": fed, "wrap": bool(agg.wrap), "n_norms": NN, "zero": buf[: P + 1]}
+
             def epilogue(params_k, tabs, theta):
                 # one launch: the fused reduce writes the buffer head, its last block packs the metrics.  Single
                 # rank, with post(v) known to follow (captured right behind it: tabs["variant"] = v; eager: the
                 # variant post will take) the same launch also applies the round (no collective in between), one
-                # launch fewer per round
+                # launch fewer per round.  tabs["fed_done"]: the engine already ran all of it (fused_tail).
                 sa = (tabs["sa_seed"], tabs["sa_sign"], tabs["sa_round"]) if "sa_seed" in tabs else None
-                v = tabs.get("variant", self._flip if tabs.get("eager") else None)
+                v = apply_variant(tabs, theta)
                 apply = None
                 fused.pop("variant", None)
-                if (v is not None and not world.distributed and P + 6 + NN <= FUSED_APPLY_MAX
-                        and os.environ.get("QFEDX_FUSED_APPLY", "1") != "0"
-                        and theta.data_ptr() == params_g.data_ptr()):
+                if tabs.get("fed_done"):
+                    if v is not None:
+                        fused["variant"] = v
+                    return
+                if v is not None:
                     apply = (params_g, outs[v], self._apply_cnt, *ring, NN)
                     fused["variant"] = v
                 agg.local_reduce(params_k, theta, tabs.get("fw", tabs["w"]), r, ids, out=buf[: P + 1],
@@ -315,6 +345,7 @@ class FederatedRunner:
                                  pack=(buf, tabs["loss"].reshape(-1), tabs["correct"].reshape(-1),
                                        tabs["nvalid"].reshape(-1), tabs["act"].reshape(-1)), apply=apply,
                                  dp_scale=tabs.get("dpscale"))
+            epilogue.fused_tail = fused_tail
             graph_comm = self.graph_comm
             with self.timer.phase("local_train"):
                 res = trainer.run_round(self.store, local_alive, self.params, r, epilogue=epilogue,

@@ -212,6 +212,24 @@ def _native_runtime():
     return _NATIVE[0]
 
 
+def _tail(epilogue, dv, theta, variant=None, eager=False):
+    """The round epilogue's FedAvg as a ``fed_tail`` maker for the last local step (``epilogue.fused_tail``), or None.
+    The returned callable gets ``done = True`` when the engine ran the FedAvg itself (the epilogue then skips it)."""
+    make = getattr(epilogue, "fused_tail", None)
+    if make is None:
+        return None
+
+    def tail(loss_all, correct_all):
+        tabs = dict(dv, loss=loss_all, correct=correct_all)
+        if variant is not None:
+            tabs["variant"] = variant
+        if eager:
+            tabs["eager"] = True
+        return make(tabs, theta)
+    tail.done = False
+    return tail
+
+
 class VQCClientTrainer:
     """Runs one federated round of local training for a rank's clients (batched)."""
 
@@ -226,7 +244,7 @@ class VQCClientTrainer:
         return self.spec.encode_features(X)
 
     def _body(self, X, Y, lid, theta, idx_d, wts_d, act_d, steps: int, round_num: int, method: str,
-              traj_keys=None, ro_keys=None):
+              traj_keys=None, ro_keys=None, tail=None):
         """Device work of one round (capturable): local steps of all clients.
 
         ``X`` [Nc, Nmax, F] / ``Y`` [Nc, Nmax] are the whole device-resident client store and ``lid`` [K]
@@ -265,13 +283,20 @@ class VQCClientTrainer:
         else:
             rows = lid[:, None]
         fj = None
+        # ``tail(loss_all, correct_all)``: the round epilogue's FedAvg as a ``fed_tail`` for the last step's engine
+        # call (the MFMA engine folds it into its fused Adam epilogue); ``tail.done`` says the engine ran it
+        ft = tail(loss_all, correct_all) if (tail is not None and fused and method == "adjoint") else None
         if upfront:
             m, v, t = opt.init_state()
-            # the MFMA engine's first-step fragments come from theta in the same launch (every row starts as theta)
+            # the MFMA engine's first-step fragments come from theta in the same launch (every row starts as theta);
+            # the FedAvg tail's all-reduce buffer head is zeroed there too
             fj = self.engine.prologue_frag_job() if method == "adjoint" and noise is None else None
             ext().round_prologue(theta.float().contiguous(), params, m, v, t, X, Y, lid, idx_d.contiguous(), mode,
                                  float(spec.alpha), xbuf, ybuf, frag_job=fj,
-                                 frag_bf16=bool(getattr(self.engine.hip, "bf16", False)))
+                                 frag_bf16=bool(getattr(self.engine.hip, "bf16", False)),
+                                 zero=ft["zero"] if ft is not None else None)
+        elif ft is not None:
+            ft = None                                  # (the tail needs the prologue's zeroed buffer head)
         else:
             opt.init_round(params, theta.float())
         for s in range(steps):
@@ -297,7 +322,10 @@ class VQCClientTrainer:
             res = self.engine.loss_and_grads(xang, yb, ws, params, method, rng_keys=(cfg.seed, round_num, s),
                                              readout_keys=ro_keys, step=s, out_loss=loss_all[s],
                                              out_correct=correct_all[s], init=init, fused_opt=(opt, act_d[s]),
-                                             shared_frags=fj[1] if (fj is not None and s == 0) else None)
+                                             shared_frags=fj[1] if (fj is not None and s == 0) else None,
+                                             fed_tail=ft if s == steps - 1 else None)
+            if res.get("fed_done", False):
+                tail.done = True
             if not res.get("opt_done", False):      # the MFMA engine runs HIP Adam inside its gradient reduction
                 opt.step(params, res["grad"], act_d[s])
         return params, loss_all, correct_all
@@ -363,11 +391,13 @@ class VQCClientTrainer:
         else:
             dv = up.to_device(self.device)
             theta = theta_g.to(self.device)
+            tail = _tail(epilogue, dv, theta, eager=True)
             params, loss_all, correct_all = self._body(store.X, store.y, dv["lid"], theta, dv["idx"],
                                                        dv["wts"], dv["act"], plan.max_steps, round_num, method,
-                                                       traj_keys, ro_keys)
+                                                       traj_keys, ro_keys, tail=tail)
             if epilogue is not None:    # eager: ``post`` (if any) runs right after, on the caller's side
-                epilogue(params, dict(dv, loss=loss_all, correct=correct_all, eager=True), theta)
+                epilogue(params, dict(dv, loss=loss_all, correct=correct_all, eager=True,
+                                      fed_done=bool(tail and tail.done)), theta)
         return {"params": params, "loss": loss_all, "correct": correct_all, "nvalid": dv["nvalid"], "act": dv["act"],
                 "lid": dv["lid"], "weights": dv["w"], "post_done": post_v is not None, "post_variant": post_v,
                 **common}
@@ -415,9 +445,10 @@ class VQCClientTrainer:
 
             def body(variant=None):
                 # ``variant``: set when post(variant) is captured right behind the epilogue (it may fold into it)
-                out = self._body(*args)
+                tail = _tail(epilogue, dv, ent["theta"], variant=variant)
+                out = self._body(*args, tail=tail)
                 if epilogue is not None:
-                    tabs = dict(dv, loss=out[1], correct=out[2])
+                    tabs = dict(dv, loss=out[1], correct=out[2], fed_done=bool(tail and tail.done))
                     if variant is not None:
                         tabs["variant"] = variant
                     epilogue(out[0], tabs, ent["theta"])

@@ -183,21 +183,24 @@ class VQCEngine:
                        rng_keys: tuple = (0,), readout_keys: Optional[torch.Tensor] = None,
                        step: int = 0, out_loss: Optional[torch.Tensor] = None,
                        out_correct: Optional[torch.Tensor] = None, init: Optional[torch.Tensor] = None,
-                       fused_opt=None, shared_frags=None) -> dict:
+                       fused_opt=None, shared_frags=None, fed_tail=None) -> dict:
         """Loss [K], gradient [K,P], correct [K] for [K,B] minibatches.  ``out_loss`` / ``out_correct``
         (optional [K] views, e.g. rows of a round buffer) receive the loss / hit counts in place.
         ``init`` = raw amplitudes [K,B,F<=2^n] or complex states (amplitude encoding; None otherwise).
         ``fused_opt`` = (BatchedOptimizer, active [K]): an engine that can fuse the local optimizer step into its
         own launches (the MFMA engine: HIP Adam in the gradient reduction) does so and returns ``opt_done``.
         ``shared_frags``: the MFMA engine's unitary fragments of this step, already built by the round prologue
-        (``prologue_frag_job``; a round's first step only, when every client row is the global vector)."""
+        (``prologue_frag_job``; a round's first step only, when every client row is the global vector).
+        ``fed_tail``: the round's FedAvg to fold into this (last) step's fused Adam epilogue (``QfxFedTail``); the
+        result says ``fed_done`` when the engine did."""
         spec = self.spec
         self._check(xang, init)
         if self.backend == "hip" and method == "adjoint":
             nz = self.noise if (self.noise is not None and self.noise.readout_noise) else None
             if fused_opt is not None and getattr(self.hip, "fuses_optimizer", False):
                 return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step, out_loss,
-                                               out_correct, init, fused_opt=fused_opt, shared_frags=shared_frags)
+                                               out_correct, init, fused_opt=fused_opt, shared_frags=shared_frags,
+                                               fed_tail=fed_tail)
             return self.hip.loss_and_grads(xang, y, wmask, params, spec, nz, readout_keys, step, out_loss,
                                            out_correct, init)
         res = self._loss_and_grads(xang, y, wmask, params, method, spsa_c, rng_keys, readout_keys, step, init)

@@ -514,7 +514,7 @@ class HeaMfmaProgram:
         return [self.slot_tab, self._buf("pfrags", self.n_slots * 4 * 128 * 4, torch.int32)]
 
     def _step(self, x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=None, dbg=None,
-              shared_frags=None):
+              shared_frags=None, fed=None):
         """Forward, readout + CE, adjoint and gradient reduction of clients [0, K).
         ``adam`` = (tensors, hyper) from ``BatchedOptimizer.fused_adam``: the clients' Adam step runs in the
         gradient reduction's epilogue (one launch fewer per local step).  ``dbg``: stall-attribution buffers per
@@ -550,8 +550,10 @@ class HeaMfmaProgram:
                               None, None, ro, self.C, self.n_theta)
         else:
             cnt = self._zbuf("adamcnt", K, torch.int32)
+            f = fed if fed is not None else {}
             C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1],
-                              adam[0] + [cnt], adam[1], ro, self.C, self.n_theta)
+                              adam[0] + [cnt], adam[1], ro, self.C, self.n_theta, f.get("fed"),
+                              bool(f.get("wrap", False)), int(f.get("n_norms", 0)))
 
     def stamp_buffers(self) -> dict:
         """Zeroed stall-attribution buffers, one per pass launch (``fwd{j}``, ``adj{j}``), for the stamps build
@@ -562,7 +564,7 @@ class HeaMfmaProgram:
 
     def loss_and_grads(self, xang, y, wmask, params, spec, noise=None, keys=None, step: int = 0, out_loss=None,
                        out_correct=None, init: torch.Tensor | None = None, fused_opt=None, dbg=None,
-                       shared_frags=None) -> dict:
+                       shared_frags=None, fed_tail=None) -> dict:
         """One adjoint training step (same contract as ``HipProgram.loss_and_grads``).
         ``fused_opt`` = (BatchedOptimizer, active): with params updated in place (a contiguous fp32 tensor) and HIP
         Adam, the optimizer step runs in the gradient reduction's epilogue and the result says ``opt_done``;
@@ -586,9 +588,12 @@ class HeaMfmaProgram:
         want = K * (self.n_gradops + ro_rows) <= FUSED_ADAM_MAX_BLOCKS
         if want and fused_opt is not None and self.n_gradops > 0 and p.data_ptr() == params.data_ptr():
             adam = fused_opt[0].fused_adam(p, fused_opt[1])
+        fed = fed_tail if (adam is not None and fed_tail is not None) else None
         self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=adam, dbg=dbg,
-                   shared_frags=shared_frags)
+                   shared_frags=shared_frags, fed=fed)
         res = {"loss": loss, "grad": grad, "correct": correct, "expz": expz.reshape(K, B, self.C)}
         if adam is not None:
             res["opt_done"] = True
+        if fed is not None:
+            res["fed_done"] = True     # the round's FedAvg ran in the Adam epilogue (QfxFedTail)
         return res

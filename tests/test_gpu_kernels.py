@@ -619,3 +619,26 @@ def test_prologue_fragments_match_per_client_fragments(cuda, monkeypatch):
         outs.append(run_experiment(cfg, world=init_distributed(dev), device=dev, backend="hip"))
     assert torch.equal(outs[0]["params"], outs[1]["params"])
     assert torch.equal(torch.tensor(outs[0]["accuracies"]), torch.tensor(outs[1]["accuracies"]))
+
+
+@pytest.mark.parametrize("kw", [dict(local_epochs=2), dict(local_steps=1, weighting="uniform")])
+def test_fedavg_tail_in_adam_epilogue_is_bitwise(cuda, monkeypatch, kw):
+    """Plain FedAvg folded into the MFMA engine's fused Adam epilogue of the round's last local step (QfxFedTail:
+    the same fixed-point terms added with int64 atomics into the buffer head the prologue zeroed, metrics packed and
+    the single-rank round applied by the last client) gives bitwise the run with the separate FedAvg launch: global
+    parameters, accuracies and the round losses, eager and graph-captured rounds alike."""
+    from tests.test_fl import small_cfg
+    from qfedx_amd.api import run_experiment
+    from qfedx_amd.parallel.dist import init_distributed
+    outs = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("QFEDX_FED_TAIL", on)
+        cfg = small_cfg(num_rounds=4, n_qubits=12, n_layers=3, device="cuda", backend="hip", num_clients=6,
+                        state_dtype="mfma", **kw)
+        dev = torch.device("cuda", 0)
+        outs.append(run_experiment(cfg, world=init_distributed(dev), device=dev, backend="hip"))
+    assert torch.equal(outs[0]["params"], outs[1]["params"])
+    assert torch.equal(torch.tensor(outs[0]["accuracies"]), torch.tensor(outs[1]["accuracies"]))
+    l0 = [h.get("train_loss") for h in outs[0]["history"]]
+    l1 = [h.get("train_loss") for h in outs[1]["history"]]
+    assert l0 == l1
