@@ -451,7 +451,7 @@ void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<tor
   int64_t nz = 0;
   if (zero && zero->defined() && zero->numel() > 0) {
     need(*zero, torch::kInt64, "zero");
-    zp = zero->data_ptr<long long>();
+    zp = reinterpret_cast<long long*>(zero->data_ptr<int64_t>());
     nz = zero->numel();
   }
   // rows = false: params only gives the [K, P] shape (the first local step reads theta; CFed fused SGD)
