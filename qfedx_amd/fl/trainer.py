@@ -295,9 +295,8 @@ class VQCClientTrainer:
                                  float(spec.alpha), xbuf, ybuf, frag_job=fj,
                                  frag_bf16=bool(getattr(self.engine.hip, "bf16", False)),
                                  zero=ft["zero"] if ft is not None else None)
-        elif ft is not None:
-            ft = None                                  # (the tail needs the prologue's zeroed buffer head)
         else:
+            ft = None                                  # (the tail needs the prologue's zeroed buffer head)
             opt.init_round(params, theta.float())
         for s in range(steps):
             bi = idx_d[s]
