@@ -83,7 +83,8 @@ int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, f
                               const float* X, const long long* Y, const long long* lid, const long long* idx,
                               int steps, int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride,
                               long long* yo, const int* slot_tab, int n_slots, void* frags, int bf16, long long* zero,
-                              int nzero, hipStream_t st);
+                              int nzero, const void* up_host, void* up_dst, long up_nbytes, long long* up_ctr,
+                              long long* up_flag, hipStream_t st);
 int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx, int K,
                             int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride, long long* yo,
                             hipStream_t st);
@@ -405,7 +406,7 @@ void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<tor
                     c10::optional<torch::Tensor> v, c10::optional<torch::Tensor> t, torch::Tensor X, torch::Tensor Y,
                     torch::Tensor lid, torch::Tensor idx, int64_t mode, double alpha, torch::Tensor x_out,
                     torch::Tensor y_out, bool rows, c10::optional<std::vector<torch::Tensor>> frag_job, bool frag_bf16,
-                    c10::optional<torch::Tensor> zero) {
+                    c10::optional<torch::Tensor> zero, c10::optional<std::vector<torch::Tensor>> upload) {
   need(theta, torch::kFloat32, "theta");
   need(params, torch::kFloat32, "params");
   const int64_t K = params.size(0), P = params.size(1);
@@ -454,6 +455,28 @@ void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<tor
     zp = reinterpret_cast<long long*>(zero->data_ptr<int64_t>());
     nz = zero->numel();
   }
+  // upload = (src host_alloc uint8, dst device uint8, ctr int64 [2], flag host_alloc >= 8 bytes): the round's
+  // host_upload folded into this launch (lid and idx must be views of dst; the launcher checks)
+  const void* uh = nullptr;
+  void* ud = nullptr;
+  long un = 0;
+  long long *uc = nullptr, *uf = nullptr;
+  if (upload && !upload->empty()) {
+    if (upload->size() != 4) throw std::invalid_argument("round_prologue: upload = (src, dst, ctr, flag)");
+    const torch::Tensor &src = (*upload)[0], &dst = (*upload)[1], &ctr = (*upload)[2], &flag = (*upload)[3];
+    if (src.device().is_cuda() || !dst.device().is_cuda() || src.scalar_type() != torch::kUInt8 ||
+        dst.scalar_type() != torch::kUInt8 || !src.is_contiguous() || !dst.is_contiguous() ||
+        dst.numel() < src.numel() || src.numel() % 16)
+      throw std::invalid_argument("round_prologue: upload src (host_alloc) / dst (device) uint8, 16-byte multiple");
+    need(ctr, torch::kInt64, "upload ctr");
+    if (ctr.numel() < 2 || flag.device().is_cuda() || flag.numel() < 8 || flag.scalar_type() != torch::kUInt8)
+      throw std::invalid_argument("round_prologue: upload ctr [2] int64 / flag >= 8 bytes host_alloc");
+    uh = src.data_ptr();
+    ud = dst.data_ptr();
+    un = (long)src.numel();
+    uc = ptr<long long>(ctr);
+    uf = (long long*)flag.data_ptr();
+  }
   // rows = false: params only gives the [K, P] shape (the first local step reads theta; CFed fused SGD)
   check(qfx_launch_round_prologue(ptr<float>(theta), (int)K, (int)P, rows ? ptr<float>(params) : nullptr, ptr<float>(mt),
                                   ptr<float>(vt),
@@ -461,7 +484,7 @@ void round_prologue(torch::Tensor theta, torch::Tensor params, c10::optional<tor
                                   ptr<long long>(Y), ptr<long long>(lid), ptr<long long>(idx), (int)S, (int)B,
                                   (long)X.size(1), (int)F, (int)mode, (float)alpha, ptr<float>(x_out),
                                   (int)x_out.size(3), ptr<long long>(y_out), slot_tab, n_slots, frags,
-                                  frag_bf16 ? 1 : 0, zp, (int)nz, cur_stream()),
+                                  frag_bf16 ? 1 : 0, zp, (int)nz, uh, ud, un, uc, uf, cur_stream()),
         "qfx_round_prologue");
 }
 
@@ -658,7 +681,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("v"), pybind11::arg("t"), pybind11::arg("X"), pybind11::arg("Y"), pybind11::arg("lid"),
         pybind11::arg("idx"), pybind11::arg("mode"), pybind11::arg("alpha"), pybind11::arg("x_out"),
         pybind11::arg("y_out"), pybind11::arg("rows") = true, pybind11::arg("frag_job") = pybind11::none(),
-        pybind11::arg("frag_bf16") = false, pybind11::arg("zero") = pybind11::none());
+        pybind11::arg("frag_bf16") = false, pybind11::arg("zero") = pybind11::none(),
+        pybind11::arg("upload") = pybind11::none());
   m.def("amp_scratch", &amp_scratch);
   m.def("readout_noise", &readout_noise);
   m.def("philox_uniform", &philox_uniform);

@@ -56,6 +56,7 @@ struct QfxAdamArgs {
   const float* active;
   unsigned* cnt;
   float lr, b1, b2, eps;
+  int owned;                 // 1: every block steps the parameters it owns itself (no last-block hand-off)
 };
 
 // The round's FedAvg folded into hea_grad_reduce's Adam epilogue (a round's last local step, plain FedAvg: no DP, no

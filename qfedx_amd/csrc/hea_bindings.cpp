@@ -251,7 +251,8 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
   QfxAdamArgs ad{};
   if (adam && !adam->empty()) {
     const auto& a = *adam;
-    need(a.size() == 6 && hyper && hyper->size() == 4, "grad_reduce: adam = (m, v, t_in, t_out, active, cnt), hyper = (lr, b1, b2, eps)");
+    need(a.size() == 6 && hyper && (hyper->size() == 4 || hyper->size() == 5),
+         "grad_reduce: adam = (m, v, t_in, t_out, active, cnt), hyper = (lr, b1, b2, eps[, owned])");
     need(params.size(1) == p_stride && params.is_contiguous(), "grad_reduce: fused Adam needs contiguous [K, P] params");
     ad.m = dp<float>(a[0], torch::kFloat32, "m", K * p_stride);
     ad.v = dp<float>(a[1], torch::kFloat32, "v", K * p_stride);
@@ -260,6 +261,10 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
     ad.active = dp<float>(a[4], torch::kFloat32, "active", K);
     ad.cnt = dp<unsigned>(a[5], torch::kInt32, "cnt", K);
     ad.lr = (float)(*hyper)[0], ad.b1 = (float)(*hyper)[1], ad.b2 = (float)(*hyper)[2], ad.eps = (float)(*hyper)[3];
+    // owned: every block steps the parameters it forms (the caller checked that the gradient records and the
+    // readout block own every parameter exactly once); needs the fused readout block
+    ad.owned = hyper->size() == 5 && (*hyper)[4] != 0.0 ? 1 : 0;
+    need(!ad.owned || ro.rec, "grad_reduce: owned Adam needs the fused readout block");
     need(n_gradops > 0 || ro.rec, "grad_reduce: fused Adam needs at least one reduction block");
   }
   // fed = (buf int64 [P + 6 + n_norms], theta_g f32 [P], mask u8 [P], weights f64 [K], loss, correct, nvalid, act

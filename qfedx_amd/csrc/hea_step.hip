@@ -35,6 +35,22 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   // 8 groups of 32 lanes split the client's (sample, tile) rows; 4 independent loads in flight per lane; the
   // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
   const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
+  // Owned mode (ad.owned; launches with more blocks than CUs): the thread that forms a parameter's gradient also
+  // runs its Adam step and, with the FedAvg tail, adds its exact fixed-point term - every parameter is formed by
+  // exactly one (client, block) (the host checks the ownership map), so no block hands data to another and none
+  // needs the per-block release of the last-block epilogue below (an L2 writeback each: at 832 blocks it made the
+  // fused launch cost 33.6 us against 13 + 5.4 us for two launches).  The metric pack and the single-rank apply
+  // follow as their own one-block launch (hea_fed_pack_kernel).
+  int nsat = 0;
+  auto own_step = [&](int i, float gi, bool first) {
+    const long e = (long)k * p_stride + i;
+    qfx_adam_elem(params, gi, ad.m, ad.v, ad.t_in, ad.t_out, ad.active, k, e, first, ad.lr, ad.b1, ad.b2, ad.eps);
+    if (!ft.buf) return;
+    double d = (double)params[e] - (double)ft.theta_g[i];
+    if (ft.wrap && ft.mask[i]) d = qfx::wrap_pi(d);
+    const long long v = qfx::fixed_term(ft.weights[k] * d * 4294967296.0, nsat);
+    if (v) atomicAdd((unsigned long long*)&ft.buf[i], (unsigned long long)v);
+  };
   if (g == n_gradops) {
     // fused readout: the client's per-sample records summed in a fixed order - loss, hits, and the readout gradients
     // d/da_c = sum dl_c z_c, d/db_c = sum dl_c.  Thread t < GS * NV sums value q = t % NV of samples t / NV + GS i
@@ -52,9 +68,17 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     if (tid < NV) {
       float tot = 0.f;
       for (int j = 0; j < GS; ++j) tot += rs[j * NV + tid];
-      if (tid < 2 * ro.C)
+      if (tid < 2 * ro.C) {
         grad[(size_t)k * p_stride + ro.n_theta + tid] = tot;
-      else if (tid == 2 * ro.C)
+        if (ad.owned) {
+          // (thread 0 also writes the client's step counter and adds its FedAvg weight)
+          own_step(ro.n_theta + tid, tot, tid == 0);
+          if (tid == 0 && ft.buf) {
+            const long long v = qfx::fixed_term(ft.weights[k] * 4294967296.0, nsat);
+            if (v) atomicAdd((unsigned long long*)&ft.buf[p_stride], (unsigned long long)v);
+          }
+        }
+      } else if (tid == 2 * ro.C)
         ro.loss[k] = tot;
       else
         ro.correct[k] = tot;
@@ -90,22 +114,33 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     if (tid < nreal) {
       const double* p = pt + 8 * tid;
       const float* prm = params + (size_t)k * p_stride;
+      float gth, gph;
       if (inside) {
         // at the op input: d/dtheta = Im<lam|X|psi> = Im(n01 + n10);
         // d/dphi = Im<lam|RX^H Z RX|psi> = cos(theta) Im(n00 - n11) + sin(theta) Re(n01 - n10)
         const double th = prm[m[2 + tid]];
         const double ct = cos(th), st = sin(th);
-        grad[(size_t)k * p_stride + m[2 + tid]] = (float)(p[3] + p[5]);
-        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
+        gth = (float)(p[3] + p[5]);
+        gph = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
       } else {
         const double ph = prm[m[6 + tid]];
         const double cp = cos(ph), sp = sin(ph);
-        grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
-        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
+        gth = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
+        gph = (float)(p[1] - p[7]);
+      }
+      grad[(size_t)k * p_stride + m[2 + tid]] = gth;
+      grad[(size_t)k * p_stride + m[6 + tid]] = gph;
+      if (ad.owned) {               // (this thread read the angle it needed above: no other thread reads it)
+        own_step(m[2 + tid], gth, false);
+        own_step(m[6 + tid], gph, false);
       }
     }
   }
   if (!ad.m) return;
+  if (ad.owned) {
+    if (nsat && ft.buf) atomicAdd((unsigned long long*)&ft.buf[p_stride + 5], (unsigned long long)nsat);
+    return;
+  }
   __shared__ int last_s;
   // The block's gradient stores are complete in L2 after the barrier; ONE agent-scope release (thread 0) makes
   // them visible across XCDs before the arrival.  A release is an L2 writeback on this chip: issued by every
@@ -133,7 +168,6 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   if (!ft.buf) return;
   // ---- the round's FedAvg (QfxFedTail): client k's terms from the row this block just updated
   const double SC = 4294967296.0;
-  int nsat = 0;
   __syncthreads();                                     // the block's own Adam stores, visible to the block
   for (int e = tid; e < p_stride; e += 256) {
     double d = (double)params[(size_t)k * p_stride + e] - (double)ft.theta_g[e];
@@ -170,6 +204,21 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   for (long e = tid; e < (long)p_stride + 6 + ft.n_norms; e += 256)
     qfx::round_apply_elem(ft.buf, p_stride, ft.apply_theta, 1.0, ft.apply_out, 0, 1.0, ft.n_norms, e, wsum, ld);
 }
+
+// Owned mode's round epilogue (after the reduction launch: every client's terms are in buf): the metric pack and,
+// single rank, the apply - the last-block code of the epilogue above as a one-block launch.
+__global__ void __launch_bounds__(256) hea_fed_pack_kernel(QfxFedTail ft, int p_stride) {
+  qfx::round_pack_block(qfx::RoundPack{ft.buf, ft.loss, ft.correct, ft.nvalid, ft.act, ft.n_metrics, nullptr,
+                                       nullptr, 0},
+                        p_stride);
+  if (!ft.apply_theta) return;
+  __syncthreads();
+  const long long* buf = ft.buf;
+  auto ld = [buf](long i) { return buf[i]; };
+  const double wsum = (double)ld(p_stride) / 4294967296.0;
+  for (long e = threadIdx.x; e < (long)p_stride + 6 + ft.n_norms; e += 256)
+    qfx::round_apply_elem(ft.buf, p_stride, ft.apply_theta, 1.0, ft.apply_out, 0, 1.0, ft.n_norms, e, wsum, ld);
+}
 #endif  // !QFX_HEA_BF16
 
 }  // namespace HEA_NS
@@ -198,8 +247,11 @@ extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n
     if (!adam || !adam->m) return (int)hipErrorInvalidValue;   // the FedAvg tail runs in the Adam epilogue
     ftl = *fed;
   }
+  if (ad.owned && (!ad.m || !ro.rec)) return (int)hipErrorInvalidValue;   // owned mode: the readout block counts
   hipLaunchKernelGGL(HEA_NS::hea_grad_reduce_kernel, dim3(K, rows), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
                      gmeta, spc, params, grad, p_stride, ad, ro, ftl);
+  if (ad.owned && ftl.buf)
+    hipLaunchKernelGGL(HEA_NS::hea_fed_pack_kernel, dim3(1), dim3(256), 0, st, ftl, p_stride);
   return (int)hipGetLastError();
 }
 

@@ -818,6 +818,11 @@ __device__ __forceinline__ void gather_row(const BatchGather& g, long s) {
     for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = rng > 0.f ? ((xr[f] - mn) / rng) * pi_f : 0.f;
   } else if (g.mode == 0) {
     for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = g.alpha * xr[f];
+  } else if ((F & 3) == 0 && (g.x_stride & 3) == 0 && ((uintptr_t)g.X & 15) == 0 && ((uintptr_t)g.xo & 15) == 0) {
+    // raw copy of 16-byte aligned rows (the CNN's 784-pixel images): one 16-byte load per lane
+    const float4* src = (const float4*)xr;
+    float4* dst = (float4*)out;
+    for (int f = threadIdx.x; f < (F >> 2); f += blockDim.x) dst[f] = src[f];
   } else {
     for (int f = threadIdx.x; f < F; f += blockDim.x) out[f] = xr[f];
   }
@@ -837,14 +842,30 @@ struct FragJob {
   int bf16;
 };
 
-__global__ void __launch_bounds__(256) qfx_round_prologue_kernel(RoundInit ri, int chunks, BatchGather g, FragJob fj,
-                                                                 long gather_blocks, long long* zero, int nzero) {
+// The round's host upload folded into the prologue (otherwise the graph's first node, qfx_host_upload_kernel):
+// ``blocks`` trailing blocks copy the pinned tables into the device pack for the later launches, the gather blocks
+// read their slot and minibatch indices from the pinned copy itself (the launcher points BatchGather there), and the
+// last block of the launch to finish is the round's completion signal for the pinned buffer (ctr / flag exactly as
+// the upload kernel's).  Each gather block makes dependent host reads, so the trainer folds the upload only into
+// small prologues (the 8-client share: 256 gather blocks, 9.7 -> 8.1 us and one launch fewer; at 64 clients, 2,048
+// gather blocks, the merged launch took 35 us - profiles/r5_round_timelines_r5k.txt).
+struct UploadJob {
+  const uint4* src;        // device-mapped pinned buffer
+  uint4* dst;
+  long n16;
+  long long* ctr;          // [round count, arrivals]
+  long long* flag;         // coherent pinned word
+  int blocks;              // 0: no upload in this launch
+};
+
+__device__ __forceinline__ void prologue_block(const RoundInit& ri, int chunks, const BatchGather& g, const FragJob& fj,
+                                               long gather_blocks, long long* zero, int nzero, long blk) {
   const int init_blocks = ri.K * chunks;
-  if ((int)blockIdx.x < init_blocks) {
-    round_init_chunk(ri, blockIdx.x / chunks, blockIdx.x % chunks);
+  if (blk < init_blocks) {
+    round_init_chunk(ri, (int)(blk / chunks), (int)(blk % chunks));
     return;
   }
-  const long b = (long)blockIdx.x - init_blocks;
+  const long b = blk - init_blocks;
   if (b < gather_blocks) {
     gather_row(g, b);
     return;
@@ -861,27 +882,69 @@ __global__ void __launch_bounds__(256) qfx_round_prologue_kernel(RoundInit ri, i
     hea_frag::build<_Float16>(ri.theta, fj.slot_tab + slot * 9, threadIdx.x, out);
 }
 
+__global__ void __launch_bounds__(256) qfx_round_prologue_kernel(RoundInit ri, int chunks, BatchGather g, FragJob fj,
+                                                                 long gather_blocks, long long* zero, int nzero,
+                                                                 UploadJob up) {
+  const long work = (long)gridDim.x - up.blocks;
+  if ((long)blockIdx.x < work) {
+    prologue_block(ri, chunks, g, fj, gather_blocks, zero, nzero, blockIdx.x);
+  } else {
+    for (long i = ((long)blockIdx.x - work) * 256 + threadIdx.x; i < up.n16; i += (long)up.blocks * 256)
+      up.dst[i] = up.src[i];
+  }
+  if (!up.ctr) return;
+  // a block's pinned loads have returned once the stores they feed are issued (the copy, the gather rows)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long prev = atomicAdd((unsigned long long*)&up.ctr[1], 1ull);
+    if (prev == (unsigned long long)gridDim.x - 1) {
+      up.ctr[1] = 0;
+      const long long c = up.ctr[0] + 1;
+      up.ctr[0] = c;
+      __hip_atomic_store(up.flag, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 extern "C" int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, float* m, float* v, float* t,
                                          int nt, const float* X, const long long* Y, const long long* lid,
                                          const long long* idx, int steps, int B, long nmax, int F, int mode,
                                          float alpha, float* xo, int x_stride, long long* yo, const int* slot_tab,
                                          int n_slots, void* frags, int bf16, long long* zero, int nzero,
-                                         hipStream_t st) {
+                                         const void* up_host, void* up_dst, long up_nbytes, long long* up_ctr,
+                                         long long* up_flag, hipStream_t st) {
   if (K <= 0 || P <= 0) return 0;
   if (n_slots < 0 || (n_slots > 0 && (!slot_tab || !frags))) return (int)hipErrorInvalidValue;
+  UploadJob up{nullptr, nullptr, 0, nullptr, nullptr, 0};
+  if (up_nbytes > 0) {
+    if (up_nbytes % 16 || !up_dst || !up_host || (up_ctr == nullptr) != (up_flag == nullptr))
+      return (int)hipErrorInvalidValue;
+    void* dsrc = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&dsrc, const_cast<void*>(up_host), 0);
+    if (e != hipSuccess) return (int)e;
+    // the gather reads lid / idx from the pinned copy: both must lie inside the uploaded range
+    const char *d0 = (const char*)up_dst, *d1 = d0 + up_nbytes;
+    const char *l0 = (const char*)lid, *i0 = (const char*)idx;
+    const long lb = (long)K * 8, ib = (long)steps * K * B * 8;
+    if (l0 < d0 || l0 + lb > d1 || i0 < d0 || i0 + ib > d1) return (int)hipErrorInvalidValue;
+    lid = (const long long*)((const char*)dsrc + (l0 - d0));
+    idx = (const long long*)((const char*)dsrc + (i0 - d0));
+    const long n16 = up_nbytes / 16, ub = (n16 + 255) / 256;
+    up = UploadJob{(const uint4*)dsrc, (uint4*)up_dst, n16, up_ctr, up_flag, (int)(ub < 256 ? ub : 256)};
+  }
   // without client rows or moments to set, only the step counters need a block (chunk 0 of row 0)
   const bool rows = params || m || v;
   const int chunks = rows ? (P + SG_E - 1) / SG_E : (t ? 1 : 0);
   const int kinit = rows ? K : (t ? 1 : 0);
   const long gather = (long)steps * K * B;
   if (nzero < 0 || (nzero > 0 && !zero)) return (int)hipErrorInvalidValue;
-  const long blocks = (long)kinit * chunks + gather + n_slots + (nzero > 0 ? 1 : 0);
+  const long blocks = (long)kinit * chunks + gather + n_slots + (nzero > 0 ? 1 : 0) + up.blocks;
   if (blocks > 0x7fffffffL) return (int)hipErrorInvalidValue;
   if (blocks == 0) return 0;
   hipLaunchKernelGGL(qfx_round_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
                      RoundInit{theta, kinit, P, params, m, v, t, nt}, chunks,
                      BatchGather{X, Y, lid, idx, K, B, nmax, F, mode, alpha, xo, x_stride, yo},
-                     FragJob{slot_tab, n_slots, (uint4*)frags, bf16}, gather, zero, nzero);
+                     FragJob{slot_tab, n_slots, (uint4*)frags, bf16}, gather, zero, nzero, up);
   return (int)hipGetLastError();
 }
 

@@ -27,6 +27,9 @@ from .optim import BatchedOptimizer
 # The round prologue gathers every step's inputs up front below this buffer size.  The buffer lives in the round
 # graph's private pool and up to _GRAPH_LRU graphs stay cached, so the cap bounds that reserve too (1.5 GiB).
 UPFRONT_GATHER_BYTES = 1 << 28
+# gather rows (steps x clients x batch) up to which the round prologue also does the host upload: one launch fewer at
+# the 8-client share (256 rows, 9.7 -> 8.1 us); at 2,048 rows the gather's pinned index reads took 35 us
+FOLD_UPLOAD_MAX_ROWS = 512
 _GRAPH_LRU = 6
 
 
@@ -274,6 +277,14 @@ class VQCClientTrainer:
         # and encoded up front (trajectory replicas, T > 1, and rounds whose inputs pass UPFRONT_GATHER_BYTES
         # gather per step)
         upfront = fused and T == 1 and steps * K * BT * X.shape[-1] * 4 <= UPFRONT_GATHER_BYTES
+        # the round graph's host upload (_graphed): folded into the prologue launch while its gather is small (each
+        # gather block reads its indices from the pinned buffer itself: csrc/train_kernels.hip UploadJob), else its
+        # own copy kernel here, ahead of every reader of the uploaded tables
+        pend = self.__dict__.pop("_pending_upload", None)
+        if pend is not None and not (upfront and idx_d.is_contiguous() and steps * K * BT <= FOLD_UPLOAD_MAX_ROWS):
+            from ..ops._ext import ext
+            ext().host_upload(*pend)
+            pend = None
         if fused:
             from ..ops._ext import ext
             mode = 2 if spec.amplitude else (1 if spec.feature_scale == "minmax" else 0)
@@ -294,7 +305,8 @@ class VQCClientTrainer:
             ext().round_prologue(theta.float().contiguous(), params, m, v, t, X, Y, lid, idx_d.contiguous(), mode,
                                  float(spec.alpha), xbuf, ybuf, frag_job=fj,
                                  frag_bf16=bool(getattr(self.engine.hip, "bf16", False)),
-                                 zero=ft["zero"] if ft is not None else None)
+                                 zero=ft["zero"] if ft is not None else None,
+                                 upload=list(pend) if pend is not None else None)
         else:
             ft = None                                  # (the tail needs the prologue's zeroed buffer head)
             opt.init_round(params, theta.float())
@@ -410,8 +422,9 @@ class VQCClientTrainer:
         """Replay the whole round as ONE hipGraph (static shapes: #clients, steps, batch).
 
         Captured once per SHAPE, not per client set, in two variants that differ only in the pinned host buffer
-        their first node (a copy kernel) reads the round's packed tables from (client slots, minibatch indices,
-        loss weights, step masks, per-client keys): round r fills pinned buffer r % 2 - free once round r - 2's
+        their first node reads the round's packed tables from (client slots, minibatch indices, loss weights, step
+        masks, per-client keys; a copy kernel, or the round prologue itself when its gather is small): round r
+        fills pinned buffer r % 2 - free once round r - 2's
         replay has finished - and replays variant r % 2, so the host stays a round ahead with no upload launch
         of its own.  The captured launches gather every step's minibatches from the (static) client store by
         slot, so client sampling reuses the graph.  The global params are read in place when they are a float32
@@ -468,11 +481,12 @@ class VQCClientTrainer:
                     g = torch.cuda.CUDAGraph()
                     try:
                         with torch.cuda.graph(g):
-                            E.host_upload(ent["pin"][v][: up.nbytes], pack, ent["ctr"], ent["flag"])
+                            self._pending_upload = (ent["pin"][v][: up.nbytes], pack, ent["ctr"], ent["flag"])
                             out = body(v if ent["post_in_graph"] else None)
                             if ent["post_in_graph"]:
                                 post(v)
                     except Exception as exc:
+                        self.__dict__.pop("_pending_upload", None)
                         if not ent["post_in_graph"]:
                             raise
                         # the collective refused capture although the ranks agreed it could be captured
@@ -488,7 +502,7 @@ class VQCClientTrainer:
                         for v2 in range(2):
                             g = torch.cuda.CUDAGraph()
                             with torch.cuda.graph(g):
-                                E.host_upload(ent["pin"][v2][: up.nbytes], pack, ent["ctr"], ent["flag"])
+                                self._pending_upload = (ent["pin"][v2][: up.nbytes], pack, ent["ctr"], ent["flag"])
                                 out = body()
                             ent["graphs"].append(g)
                             ent["out"].append(out)
