@@ -749,7 +749,6 @@ constexpr int HID = 64, CMAXC = 16, HB = 64;
 constexpr int F1IN = C2 * Q2 * Q2;   // 1568 fc1 inputs
 constexpr int FC_KS = 7, FC_KC = F1IN / FC_KS, FC_T16 = FC_KC / 16;   // fc1 split: 224 inputs, 14 x 16 per chunk
 static_assert(FC_KC * FC_KS == F1IN && FC_T16 * 16 == FC_KC, "fc1 split");
-constexpr int FC_LA = 5;             // cnn_fc1_fwd: load steps in flight ahead of the MFMAs (3 x 16 B per lane each)
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));   // client parameter rows are only 4-B aligned
 constexpr int HG = (CMAXC * HID + CMAXC + 255) / 256;   // fc2 gradient entries per thread
 
@@ -935,24 +934,23 @@ __global__ void __launch_bounds__(256) cnn_fc1_fwd(const float* __restrict__ poo
   const f4u* bw = (const f4u*)(params + (size_t)k * P + off_w1 + (size_t)(wave * 16 + i) * F1IN + cb);
   const f4u zero = {0.f, 0.f, 0.f, 0.f};
   f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-  // loads run FC_LA steps of 16 inputs ahead of the MFMAs (fully unrolled: the arrays are registers): with one
-  // step ahead the 14 steps were 14 dependent global round trips per wave and the launch latency-bound (21.7 us)
-  f4u x0[FC_T16], x1[FC_T16], w[FC_T16];
-  auto load = [&](int T) {
-    x0[T] = ok0 ? a0[4 * T] : zero;
-    x1[T] = ok1 ? a1[4 * T] : zero;
-    w[T] = bw[4 * T];
-  };
-#pragma unroll
-  for (int T = 0; T < FC_LA; ++T) load(T);
+  f4u x0 = ok0 ? a0[0] : zero, x1 = ok1 ? a1[0] : zero, w = bw[0];
 #pragma unroll
   for (int T = 0; T < FC_T16; ++T) {
-    if (T + FC_LA < FC_T16) load(T + FC_LA);
+    f4u nx0 = zero, nx1 = zero, nw = zero;
+    if (T + 1 < FC_T16) {                         // 16 inputs ahead = 4 float4
+      nx0 = ok0 ? a0[4 * (T + 1)] : zero;
+      nx1 = ok1 ? a1[4 * (T + 1)] : zero;
+      nw = bw[4 * (T + 1)];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      acc0 = mfma(x0[T][u], w[T][u], acc0);
-      acc1 = mfma(x1[T][u], w[T][u], acc1);
+      acc0 = mfma(x0[u], w[u], acc0);
+      acc1 = mfma(x1[u], w[u], acc1);
     }
+    x0 = nx0;
+    x1 = nx1;
+    w = nw;
   }
   float* out = h1p + (((size_t)k * FC_KS + g) * B) * HID + wave * 16 + i;
 #pragma unroll
@@ -998,24 +996,23 @@ __global__ void __launch_bounds__(256) cnn_fc1_dgrad(const float* __restrict__ d
   auto wrow = [&](int T, int u) -> f4u {
     return okc ? *(const f4u*)(w + (size_t)(16 * T + 4 * kq + u) * F1IN) : zero;
   };
-  // W1 rows two steps ahead of the MFMAs (fully unrolled: registers); one step ahead left 4 dependent round trips
-  f4u wv[4][4];
+  f4u wv[4];
 #pragma unroll
-  for (int T = 0; T < 2; ++T)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) wv[T][u] = wrow(T, u);
+  for (int u = 0; u < 4; ++u) wv[u] = wrow(0, u);
 #pragma unroll
   for (int T = 0; T < 4; ++T) {
-    if (T + 2 < 4)
+    f4u nw[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) wv[T + 2][u] = wrow(T + 2, u);
+    for (int u = 0; u < 4; ++u) nw[u] = T + 1 < 4 ? wrow(T + 1, u) : zero;
 #pragma unroll
     for (int u = 0; u < 4; ++u)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        acc[0][q] = mfma(x0[T][u], wv[T][u][q], acc[0][q]);
-        acc[1][q] = mfma(x1[T][u], wv[T][u][q], acc[1][q]);
+        acc[0][q] = mfma(x0[T][u], wv[u][q], acc[0][q]);
+        acc[1][q] = mfma(x1[T][u], wv[u][q], acc[1][q]);
       }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) wv[u] = nw[u];
   }
   if (!okc) return;
 #pragma unroll

@@ -77,6 +77,8 @@ struct QfxFedTail {
   float* apply_theta;        // single rank: theta_g updated in place (nullptr: the all-reduce + apply follow)
   double* apply_out;         // [6 + n_norms] metrics / saturation / weight sum read back by the host
   int n_norms;
+  long long* terms;          // owned Adam mode: [K][P + 1] per-client terms (weight last), summed by the pack launch
+  int K;
 };
 
 // Per-client readout reduction in hea_grad_reduce (fused readout): one more block per client sums its samples' ro_rec

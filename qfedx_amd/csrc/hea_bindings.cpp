@@ -236,7 +236,8 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
                      int64_t K, torch::Tensor params, torch::Tensor grad, int64_t p_stride,
                      c10::optional<std::vector<torch::Tensor>> adam, c10::optional<std::vector<double>> hyper,
                      c10::optional<std::vector<torch::Tensor>> readout, int64_t ro_c, int64_t ro_ntheta,
-                     c10::optional<std::vector<torch::Tensor>> fed, bool fed_wrap, int64_t fed_n_norms) {
+                     c10::optional<std::vector<torch::Tensor>> fed, bool fed_wrap, int64_t fed_n_norms,
+                     c10::optional<torch::Tensor> fed_terms) {
   QfxReadoutRed ro{};
   if (readout && !readout->empty()) {
     const auto& r = *readout;
@@ -296,6 +297,12 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
       ft.apply_out = dp<double>(f[10], torch::kFloat64, "fed apply out", 6 + fed_n_norms);
       need(ft.apply_theta == ft.theta_g, "grad_reduce: the single-rank apply updates theta_g in place");
     }
+    // owned Adam mode: int64 [K, P + 1] per-client term rows, summed by the pack launch
+    if (ad.owned) {
+      need(fed_terms.has_value(), "grad_reduce: owned Adam with the FedAvg tail needs fed_terms [K, P + 1]");
+      ft.terms = dp<long long>(*fed_terms, torch::kInt64, "fed_terms", K * (p_stride + 1));
+      ft.K = (int)K;
+    }
   }
   check(qfx_hea_grad_reduce(dp<long long>(gslab, torch::kInt64, "gslab", K * spc * slab_tiles * n_gradops * 32),
                             (int)slab_tiles, (int)n_gradops, dp<int>(gmeta, torch::kInt32, "gmeta", n_gradops * 10),
@@ -321,7 +328,8 @@ void register_hea(pybind11::module& m) {
         pybind11::arg("params"), pybind11::arg("grad"), pybind11::arg("p_stride"),
         pybind11::arg("adam") = pybind11::none(), pybind11::arg("hyper") = pybind11::none(),
         pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_c") = 0, pybind11::arg("ro_ntheta") = 0,
-        pybind11::arg("fed") = pybind11::none(), pybind11::arg("fed_wrap") = false, pybind11::arg("fed_n_norms") = 0);
+        pybind11::arg("fed") = pybind11::none(), pybind11::arg("fed_wrap") = false, pybind11::arg("fed_n_norms") = 0,
+        pybind11::arg("fed_terms") = pybind11::none());
   m.def("hea_args_size", []() { return qfx_hea_args_size(); });
   m.attr("HEA_STAMP_ROWS") = HEA_STAMP_ROWS;
   // -1: release build (no device checks); 0: no failure since the last read; else the failing source line

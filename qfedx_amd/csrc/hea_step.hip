@@ -48,8 +48,8 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     if (!ft.buf) return;
     double d = (double)params[e] - (double)ft.theta_g[i];
     if (ft.wrap && ft.mask[i]) d = qfx::wrap_pi(d);
-    const long long v = qfx::fixed_term(ft.weights[k] * d * 4294967296.0, nsat);
-    if (v) atomicAdd((unsigned long long*)&ft.buf[i], (unsigned long long)v);
+    // (a row per client: 64 clients adding into the same ~100 entries with atomics serialised ~6 us)
+    ft.terms[(size_t)k * (p_stride + 1) + i] = qfx::fixed_term(ft.weights[k] * d * 4294967296.0, nsat);
   };
   if (g == n_gradops) {
     // fused readout: the client's per-sample records summed in a fixed order - loss, hits, and the readout gradients
@@ -73,10 +73,8 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
         if (ad.owned) {
           // (thread 0 also writes the client's step counter and adds its FedAvg weight)
           own_step(ro.n_theta + tid, tot, tid == 0);
-          if (tid == 0 && ft.buf) {
-            const long long v = qfx::fixed_term(ft.weights[k] * 4294967296.0, nsat);
-            if (v) atomicAdd((unsigned long long*)&ft.buf[p_stride], (unsigned long long)v);
-          }
+          if (tid == 0 && ft.buf)
+            ft.terms[(size_t)k * (p_stride + 1) + p_stride] = qfx::fixed_term(ft.weights[k] * 4294967296.0, nsat);
         }
       } else if (tid == 2 * ro.C)
         ro.loss[k] = tot;
@@ -205,9 +203,20 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     qfx::round_apply_elem(ft.buf, p_stride, ft.apply_theta, 1.0, ft.apply_out, 0, 1.0, ft.n_norms, e, wsum, ld);
 }
 
-// Owned mode's round epilogue (after the reduction launch: every client's terms are in buf): the metric pack and,
-// single rank, the apply - the last-block code of the epilogue above as a one-block launch.
+// Owned mode's round epilogue (after the reduction launch): the clients' term rows summed into the buffer head (int64,
+// exact in any order), the metric pack and, single rank, the apply - the last-block code of the epilogue above as a
+// one-block launch.
 __global__ void __launch_bounds__(256) hea_fed_pack_kernel(QfxFedTail ft, int p_stride) {
+  for (int e = threadIdx.x; e <= p_stride; e += 256) {
+    long long acc[4] = {0, 0, 0, 0};
+    int k = 0;
+    for (; k + 3 < ft.K; k += 4)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += ft.terms[(size_t)(k + u) * (p_stride + 1) + e];
+    for (; k < ft.K; ++k) acc[0] += ft.terms[(size_t)k * (p_stride + 1) + e];
+    ft.buf[e] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  }
+  __syncthreads();
   qfx::round_pack_block(qfx::RoundPack{ft.buf, ft.loss, ft.correct, ft.nvalid, ft.act, ft.n_metrics, nullptr,
                                        nullptr, 0},
                         p_stride);
@@ -247,7 +256,8 @@ extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n
     if (!adam || !adam->m) return (int)hipErrorInvalidValue;   // the FedAvg tail runs in the Adam epilogue
     ftl = *fed;
   }
-  if (ad.owned && (!ad.m || !ro.rec)) return (int)hipErrorInvalidValue;   // owned mode: the readout block counts
+  if (ad.owned && (!ad.m || !ro.rec || (ftl.buf && (!ftl.terms || ftl.K != K))))   // owned: the readout block
+    return (int)hipErrorInvalidValue;                                                // counts; term rows
   hipLaunchKernelGGL(HEA_NS::hea_grad_reduce_kernel, dim3(K, rows), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
                      gmeta, spc, params, grad, p_stride, ad, ro, ftl);
   if (ad.owned && ftl.buf)

@@ -560,9 +560,10 @@ class HeaMfmaProgram:
         else:
             cnt = self._zbuf("adamcnt", K, torch.int32)
             f = fed if fed is not None else {}
+            terms = self._buf("fedterms", K * (p.shape[1] + 1), torch.int64) if (len(adam[1]) == 5 and f) else None
             C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1],
                               adam[0] + [cnt], adam[1], ro, self.C, self.n_theta, f.get("fed"),
-                              bool(f.get("wrap", False)), int(f.get("n_norms", 0)))
+                              bool(f.get("wrap", False)), int(f.get("n_norms", 0)), terms)
 
     def stamp_buffers(self) -> dict:
         """Zeroed stall-attribution buffers, one per pass launch (``fwd{j}``, ``adj{j}``), for the stamps build
