@@ -56,7 +56,6 @@ struct QfxAdamArgs {
   const float* active;
   unsigned* cnt;
   float lr, b1, b2, eps;
-  int owned;                 // 1: every block steps the parameters it owns itself (no last-block hand-off)
 };
 
 // The round's FedAvg folded into hea_grad_reduce's Adam epilogue (a round's last local step, plain FedAvg: no DP, no
@@ -77,8 +76,6 @@ struct QfxFedTail {
   float* apply_theta;        // single rank: theta_g updated in place (nullptr: the all-reduce + apply follow)
   double* apply_out;         // [6 + n_norms] metrics / saturation / weight sum read back by the host
   int n_norms;
-  long long* terms;          // owned Adam mode: [K][P + 1] per-client terms (weight last), summed by the pack launch
-  int K;
 };
 
 // Per-client readout reduction in hea_grad_reduce (fused readout): one more block per client sums its samples' ro_rec

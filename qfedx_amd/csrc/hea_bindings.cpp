@@ -236,8 +236,7 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
                      int64_t K, torch::Tensor params, torch::Tensor grad, int64_t p_stride,
                      c10::optional<std::vector<torch::Tensor>> adam, c10::optional<std::vector<double>> hyper,
                      c10::optional<std::vector<torch::Tensor>> readout, int64_t ro_c, int64_t ro_ntheta,
-                     c10::optional<std::vector<torch::Tensor>> fed, bool fed_wrap, int64_t fed_n_norms,
-                     c10::optional<torch::Tensor> fed_terms) {
+                     c10::optional<std::vector<torch::Tensor>> fed, bool fed_wrap, int64_t fed_n_norms) {
   QfxReadoutRed ro{};
   if (readout && !readout->empty()) {
     const auto& r = *readout;
@@ -252,8 +251,7 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
   QfxAdamArgs ad{};
   if (adam && !adam->empty()) {
     const auto& a = *adam;
-    need(a.size() == 6 && hyper && (hyper->size() == 4 || hyper->size() == 5),
-         "grad_reduce: adam = (m, v, t_in, t_out, active, cnt), hyper = (lr, b1, b2, eps[, owned])");
+    need(a.size() == 6 && hyper && hyper->size() == 4, "grad_reduce: adam = (m, v, t_in, t_out, active, cnt), hyper = (lr, b1, b2, eps)");
     need(params.size(1) == p_stride && params.is_contiguous(), "grad_reduce: fused Adam needs contiguous [K, P] params");
     ad.m = dp<float>(a[0], torch::kFloat32, "m", K * p_stride);
     ad.v = dp<float>(a[1], torch::kFloat32, "v", K * p_stride);
@@ -262,10 +260,6 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
     ad.active = dp<float>(a[4], torch::kFloat32, "active", K);
     ad.cnt = dp<unsigned>(a[5], torch::kInt32, "cnt", K);
     ad.lr = (float)(*hyper)[0], ad.b1 = (float)(*hyper)[1], ad.b2 = (float)(*hyper)[2], ad.eps = (float)(*hyper)[3];
-    // owned: every block steps the parameters it forms (the caller checked that the gradient records and the
-    // readout block own every parameter exactly once); needs the fused readout block
-    ad.owned = hyper->size() == 5 && (*hyper)[4] != 0.0 ? 1 : 0;
-    need(!ad.owned || ro.rec, "grad_reduce: owned Adam needs the fused readout block");
     need(n_gradops > 0 || ro.rec, "grad_reduce: fused Adam needs at least one reduction block");
   }
   // fed = (buf int64 [P + 6 + n_norms], theta_g f32 [P], mask u8 [P], weights f64 [K], loss, correct, nvalid, act
@@ -297,12 +291,6 @@ void hea_grad_reduce(torch::Tensor gslab, int64_t slab_tiles, int64_t n_gradops,
       ft.apply_out = dp<double>(f[10], torch::kFloat64, "fed apply out", 6 + fed_n_norms);
       need(ft.apply_theta == ft.theta_g, "grad_reduce: the single-rank apply updates theta_g in place");
     }
-    // owned Adam mode: int64 [K, P + 1] per-client term rows, summed by the pack launch
-    if (ad.owned) {
-      need(fed_terms.has_value(), "grad_reduce: owned Adam with the FedAvg tail needs fed_terms [K, P + 1]");
-      ft.terms = dp<long long>(*fed_terms, torch::kInt64, "fed_terms", K * (p_stride + 1));
-      ft.K = (int)K;
-    }
   }
   check(qfx_hea_grad_reduce(dp<long long>(gslab, torch::kInt64, "gslab", K * spc * slab_tiles * n_gradops * 32),
                             (int)slab_tiles, (int)n_gradops, dp<int>(gmeta, torch::kInt32, "gmeta", n_gradops * 10),
@@ -328,8 +316,7 @@ void register_hea(pybind11::module& m) {
         pybind11::arg("params"), pybind11::arg("grad"), pybind11::arg("p_stride"),
         pybind11::arg("adam") = pybind11::none(), pybind11::arg("hyper") = pybind11::none(),
         pybind11::arg("readout") = pybind11::none(), pybind11::arg("ro_c") = 0, pybind11::arg("ro_ntheta") = 0,
-        pybind11::arg("fed") = pybind11::none(), pybind11::arg("fed_wrap") = false, pybind11::arg("fed_n_norms") = 0,
-        pybind11::arg("fed_terms") = pybind11::none());
+        pybind11::arg("fed") = pybind11::none(), pybind11::arg("fed_wrap") = false, pybind11::arg("fed_n_norms") = 0);
   m.def("hea_args_size", []() { return qfx_hea_args_size(); });
   m.attr("HEA_STAMP_ROWS") = HEA_STAMP_ROWS;
   // -1: release build (no device checks); 0: no failure since the last read; else the failing source line

@@ -35,51 +35,6 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   // 8 groups of 32 lanes split the client's (sample, tile) rows; 4 independent loads in flight per lane; the
   // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
   const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
-  // Owned mode (ad.owned; launches with more blocks than CUs): the thread that forms a parameter's gradient also
-  // runs its Adam step and, with the FedAvg tail, adds its exact fixed-point term - every parameter is formed by
-  // exactly one (client, block) (the host checks the ownership map), so no block hands data to another and none
-  // needs the per-block release of the last-block epilogue below (an L2 writeback each: at 832 blocks it made the
-  // fused launch cost 33.6 us against 13 + 5.4 us for two launches).  The metric pack and the single-rank apply
-  // follow as their own one-block launch (hea_fed_pack_kernel).
-  // An owning thread loads its angles' Adam operands (and FedAvg inputs) before the reduction, so their latency
-  // hides behind the slab loads; the step itself is qfx_adam_math, the element math of the separate launch.
-  int nsat = 0;
-  struct OwnOp {
-    float p, m, v, tg;
-    bool wr;
-  };
-  OwnOp o0{}, o1{};
-  float act = 0.f, tk = 0.f;
-  double wk = 0.0;
-  auto own_load = [&](int i, OwnOp& o) {
-    const long e = (long)k * p_stride + i;
-    o.p = params[e];
-    o.m = ad.m[e];
-    o.v = ad.v[e];
-    if (ft.buf) {
-      o.tg = ft.theta_g[i];
-      o.wr = ft.wrap && ft.mask[i];
-    }
-  };
-  auto own_client = [&]() {
-    act = ad.active[k];
-    tk = ad.t_in[k] + act;
-    if (ft.buf) wk = ft.weights[k];
-  };
-  auto own_step = [&](int i, float gi, OwnOp& o) {
-    const long e = (long)k * p_stride + i;
-    if (act != 0.f) {               // inactive rows keep parameters and moments (qfx_adam_elem)
-      qfx_adam_math(gi, tk, ad.lr, ad.b1, ad.b2, ad.eps, o.m, o.v, o.p);
-      ad.m[e] = o.m;
-      ad.v[e] = o.v;
-      params[e] = o.p;
-    }
-    if (!ft.buf) return;
-    double d = (double)o.p - (double)o.tg;
-    if (o.wr) d = qfx::wrap_pi(d);
-    // (a row per client: 64 clients adding into the same ~100 entries with atomics serialised ~6 us)
-    ft.terms[(size_t)k * (p_stride + 1) + i] = qfx::fixed_term(wk * d * 4294967296.0, nsat);
-  };
   if (g == n_gradops) {
     // fused readout: the client's per-sample records summed in a fixed order - loss, hits, and the readout gradients
     // d/da_c = sum dl_c z_c, d/db_c = sum dl_c.  Thread t < GS * NV sums value q = t % NV of samples t / NV + GS i
@@ -87,10 +42,6 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     // (A loop over q with a load and a tree per value serialised NV global round trips: this block was the
     // straggler of the 8-client reduction.)
     __shared__ float rs[256];
-    if (ad.owned && tid < 2 * ro.C) {
-      own_client();
-      own_load(ro.n_theta + tid, o0);
-    }
     const int NV = 2 * ro.C + 2, GS = 256 / NV;
     const float* rec = ro.rec + (size_t)k * spc * NV;
     float v = 0.f;
@@ -101,17 +52,9 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     if (tid < NV) {
       float tot = 0.f;
       for (int j = 0; j < GS; ++j) tot += rs[j * NV + tid];
-      if (tid < 2 * ro.C) {
+      if (tid < 2 * ro.C)
         grad[(size_t)k * p_stride + ro.n_theta + tid] = tot;
-        if (ad.owned) {
-          // (thread 0 also writes the client's step counter and its FedAvg weight term)
-          own_step(ro.n_theta + tid, tot, o0);
-          if (tid == 0) {
-            ad.t_out[k] = tk;
-            if (ft.buf) ft.terms[(size_t)k * (p_stride + 1) + p_stride] = qfx::fixed_term(wk * 4294967296.0, nsat);
-          }
-        }
-      } else if (tid == 2 * ro.C)
+      else if (tid == 2 * ro.C)
         ro.loss[k] = tot;
       else
         ro.correct[k] = tot;
@@ -121,11 +64,6 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     // m[1]: nreal in bits 0..3; bit 4 = cross matrix taken at the op INPUT (transposed BACK ops)
     const int nt = m[0], nreal = m[1] & 15, inside = (m[1] >> 4) & 1;
     const int R = spc * nt;
-    if (ad.owned && tid < nreal) {
-      own_client();
-      own_load(m[2 + tid], o0);
-      own_load(m[6 + tid], o1);
-    }
     __shared__ long long part[8][32];
     __shared__ double pt[32];
     long long acc[4] = {0, 0, 0, 0};
@@ -152,33 +90,22 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     if (tid < nreal) {
       const double* p = pt + 8 * tid;
       const float* prm = params + (size_t)k * p_stride;
-      float gth, gph;
       if (inside) {
         // at the op input: d/dtheta = Im<lam|X|psi> = Im(n01 + n10);
         // d/dphi = Im<lam|RX^H Z RX|psi> = cos(theta) Im(n00 - n11) + sin(theta) Re(n01 - n10)
         const double th = prm[m[2 + tid]];
         const double ct = cos(th), st = sin(th);
-        gth = (float)(p[3] + p[5]);
-        gph = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
+        grad[(size_t)k * p_stride + m[2 + tid]] = (float)(p[3] + p[5]);
+        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
       } else {
         const double ph = prm[m[6 + tid]];
         const double cp = cos(ph), sp = sin(ph);
-        gth = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
-        gph = (float)(p[1] - p[7]);
-      }
-      grad[(size_t)k * p_stride + m[2 + tid]] = gth;
-      grad[(size_t)k * p_stride + m[6 + tid]] = gph;
-      if (ad.owned) {               // (this thread read the angle it needed above: no other thread reads it)
-        own_step(m[2 + tid], gth, o0);
-        own_step(m[6 + tid], gph, o1);
+        grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
+        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
       }
     }
   }
   if (!ad.m) return;
-  if (ad.owned) {
-    if (nsat && ft.buf) atomicAdd((unsigned long long*)&ft.buf[p_stride + 5], (unsigned long long)nsat);
-    return;
-  }
   __shared__ int last_s;
   // The block's gradient stores are complete in L2 after the barrier; ONE agent-scope release (thread 0) makes
   // them visible across XCDs before the arrival.  A release is an L2 writeback on this chip: issued by every
@@ -206,6 +133,7 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   if (!ft.buf) return;
   // ---- the round's FedAvg (QfxFedTail): client k's terms from the row this block just updated
   const double SC = 4294967296.0;
+  int nsat = 0;
   __syncthreads();                                     // the block's own Adam stores, visible to the block
   for (int e = tid; e < p_stride; e += 256) {
     double d = (double)params[(size_t)k * p_stride + e] - (double)ft.theta_g[e];
@@ -242,47 +170,6 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   for (long e = tid; e < (long)p_stride + 6 + ft.n_norms; e += 256)
     qfx::round_apply_elem(ft.buf, p_stride, ft.apply_theta, 1.0, ft.apply_out, 0, 1.0, ft.n_norms, e, wsum, ld);
 }
-
-// Owned mode's round epilogue (after the reduction launch): the clients' term rows summed into the buffer head (int64,
-// exact in any order), the metric pack and, single rank, the apply - the last-block code of the epilogue above as a
-// one-block launch.
-// 1024 threads: G = 1024 / (P + 1) client groups per entry (the VQC's ~100-entry rows: 10 groups of ~7 clients, all
-// loads in flight at once; one thread walking 64 rows took 8.6 us), partial sums combined in LDS.
-constexpr int FP_NT = 1024;
-__global__ void __launch_bounds__(FP_NT) hea_fed_pack_kernel(QfxFedTail ft, int p_stride) {
-  __shared__ long long red[FP_NT];
-  const int E = p_stride + 1, t = threadIdx.x;
-  const int G = E <= FP_NT / 2 ? FP_NT / E : 1;
-  for (int e0 = 0; e0 < E; e0 += FP_NT / G) {
-    const int e = e0 + t % (FP_NT / G), grp = t / (FP_NT / G);
-    long long acc[4] = {0, 0, 0, 0};
-    if (e < E && grp < G) {
-      int k = grp;
-      for (; k + 3 * G < ft.K; k += 4 * G)
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc[u] += ft.terms[(size_t)(k + u * G) * E + e];
-      for (; k < ft.K; k += G) acc[0] += ft.terms[(size_t)k * E + e];
-    }
-    red[t] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
-    __syncthreads();
-    if (grp == 0 && e < E) {
-      long long v = 0;
-      for (int j = 0; j < G; ++j) v += red[j * (FP_NT / G) + t];
-      ft.buf[e] = v;
-    }
-    __syncthreads();
-  }
-  qfx::round_pack_block(qfx::RoundPack{ft.buf, ft.loss, ft.correct, ft.nvalid, ft.act, ft.n_metrics, nullptr,
-                                       nullptr, 0},
-                        p_stride);
-  if (!ft.apply_theta) return;
-  __syncthreads();
-  const long long* buf = ft.buf;
-  auto ld = [buf](long i) { return buf[i]; };
-  const double wsum = (double)ld(p_stride) / 4294967296.0;
-  for (long e = threadIdx.x; e < (long)p_stride + 6 + ft.n_norms; e += FP_NT)
-    qfx::round_apply_elem(ft.buf, p_stride, ft.apply_theta, 1.0, ft.apply_out, 0, 1.0, ft.n_norms, e, wsum, ld);
-}
 #endif  // !QFX_HEA_BF16
 
 }  // namespace HEA_NS
@@ -311,12 +198,8 @@ extern "C" int qfx_hea_grad_reduce(const long long* gslab, int slab_tiles, int n
     if (!adam || !adam->m) return (int)hipErrorInvalidValue;   // the FedAvg tail runs in the Adam epilogue
     ftl = *fed;
   }
-  if (ad.owned && (!ad.m || !ro.rec || (ftl.buf && (!ftl.terms || ftl.K != K))))   // owned: the readout block
-    return (int)hipErrorInvalidValue;                                                // counts; term rows
   hipLaunchKernelGGL(HEA_NS::hea_grad_reduce_kernel, dim3(K, rows), dim3(256), 0, st, gslab, slab_tiles, n_gradops,
                      gmeta, spc, params, grad, p_stride, ad, ro, ftl);
-  if (ad.owned && ftl.buf)
-    hipLaunchKernelGGL(HEA_NS::hea_fed_pack_kernel, dim3(1), dim3(HEA_NS::FP_NT), 0, st, ftl, p_stride);
   return (int)hipGetLastError();
 }
 

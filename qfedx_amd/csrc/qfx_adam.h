@@ -10,17 +10,6 @@
 
 // p[i] (row k, element i of P) with gradient gi; the row's first element also writes the step counter
 // t_out[k] = t_in[k] + active[k].  Rows with active[k] == 0 are left untouched.
-// The element math on values in registers (m, v, p in; updated in place) - what qfx_adam_elem does between its
-// loads and stores, so a caller that prefetched the operands gets bitwise the same update.
-__device__ __forceinline__ void qfx_adam_math(float gi, float tk, float lr, float b1, float b2, float eps, float& m,
-                                              float& v, float& p) {
-  m = __fmaf_rn(b1, m, (1.f - b1) * gi);
-  v = __fmaf_rn(b2, v, (1.f - b2) * gi * gi);
-  const float mh = m / (1.f - powf(b1, tk));
-  const float vh = v / (1.f - powf(b2, tk));
-  p = __fmaf_rn(-lr, mh / (sqrtf(vh) + eps), p);
-}
-
 __device__ __forceinline__ void qfx_adam_elem(float* __restrict__ p, float gi, float* __restrict__ m,
                                               float* __restrict__ v, const float* __restrict__ t_in,
                                               float* __restrict__ t_out, const float* __restrict__ active, int k,
@@ -29,9 +18,11 @@ __device__ __forceinline__ void qfx_adam_elem(float* __restrict__ p, float gi, f
   const float tk = t_in[k] + act;
   if (first) t_out[k] = tk;
   if (act == 0.f) return;
-  float mi = m[i], vi = v[i], pi = p[i];
-  qfx_adam_math(gi, tk, lr, b1, b2, eps, mi, vi, pi);
+  const float mi = __fmaf_rn(b1, m[i], (1.f - b1) * gi);
+  const float vi = __fmaf_rn(b2, v[i], (1.f - b2) * gi * gi);
   m[i] = mi;
   v[i] = vi;
-  p[i] = pi;
+  const float mh = mi / (1.f - powf(b1, tk));
+  const float vh = vi / (1.f - powf(b2, tk));
+  p[i] = __fmaf_rn(-lr, mh / (sqrtf(vh) + eps), p[i]);
 }

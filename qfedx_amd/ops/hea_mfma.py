@@ -62,7 +62,6 @@ _NODBG = torch.zeros(0, dtype=torch.int64)     # no stall-attribution buffer (st
 
 
 FUSED_ADAM_MAX_BLOCKS = 256   # hea_grad_reduce blocks (clients x gradient ops) up to which Adam is fused
-OWNED_ADAM = os.environ.get("QFEDX_OWNED_ADAM", "1") != "0"   # past it: the owned mode (A/B knob)
 
 
 class HeaMfmaProgram:
@@ -151,14 +150,6 @@ class HeaMfmaProgram:
             raise RuntimeError("a parameter has no owning pass")
         self.slot_tab = torch.from_numpy(slot_tab).to(self.device)
         self.gmeta = torch.tensor(gmeta, dtype=torch.int32).reshape(-1).to(self.device)
-        # every rotation angle formed by exactly one gradient record (theta and phi of its real qubits): the owned
-        # fused-Adam mode of hea_grad_reduce steps each angle in the thread that forms its gradient
-        own = np.zeros(self.n_theta, dtype=np.int64)
-        for m in np.asarray(gmeta, dtype=np.int64).reshape(-1, 10):
-            for j in range(int(m[1]) & 15):
-                own[m[2 + j]] += 1
-                own[m[6 + j]] += 1
-        self.owned_adam = bool(self.n_gradops > 0 and (own == 1).all())
         self.slab_tiles = max(1 << (self.n - p.t) for p in plan_a.passes)
         self.scale = float(1 << (self.n // 2))
         self.feature = _FEATURE[spec.feature_map.lower()]
@@ -560,10 +551,9 @@ class HeaMfmaProgram:
         else:
             cnt = self._zbuf("adamcnt", K, torch.int32)
             f = fed if fed is not None else {}
-            terms = self._buf("fedterms", K * (p.shape[1] + 1), torch.int64) if (len(adam[1]) == 5 and f) else None
             C.hea_grad_reduce(gslab, self.slab_tiles, self.n_gradops, self.gmeta, B, K, p, grad, p.shape[1],
                               adam[0] + [cnt], adam[1], ro, self.C, self.n_theta, f.get("fed"),
-                              bool(f.get("wrap", False)), int(f.get("n_norms", 0)), terms)
+                              bool(f.get("wrap", False)), int(f.get("n_norms", 0)))
 
     def stamp_buffers(self) -> dict:
         """Zeroed stall-attribution buffers, one per pass launch (``fwd{j}``, ``adj{j}``), for the stamps build
@@ -594,15 +584,10 @@ class HeaMfmaProgram:
         # with one agent-scope release (an L2 writeback here): at 16q x 64 clients (832 blocks) the fused launch took
         # 33.6 us against 13 + 5.4 us for the two launches; at the 8-client share (104 blocks) it saves a launch
         # (round 387 -> 382 us; profiles/r3_fused_adam_ab.txt).
-        # Past that (64 clients: 832 blocks) the owned mode steps every angle in the thread that forms its gradient (no
-        # hand-off, no release) when the ownership map is complete and the readout block exists (fused readout).
         ro_rows = 1 if self._fused_readout(noise) else 0
         want = K * (self.n_gradops + ro_rows) <= FUSED_ADAM_MAX_BLOCKS
-        owned = not want and ro_rows == 1 and self.owned_adam and OWNED_ADAM
-        if (want or owned) and fused_opt is not None and self.n_gradops > 0 and p.data_ptr() == params.data_ptr():
+        if want and fused_opt is not None and self.n_gradops > 0 and p.data_ptr() == params.data_ptr():
             adam = fused_opt[0].fused_adam(p, fused_opt[1])
-            if adam is not None and owned:
-                adam = (adam[0], adam[1] + [1.0])
         fed = fed_tail if (adam is not None and fed_tail is not None) else None
         self._step(x, p, yy, ww, K, B, loss, correct, grad, expz, noise, keys, step, adam=adam, dbg=dbg,
                    shared_frags=shared_frags, fed=fed)

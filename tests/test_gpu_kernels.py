@@ -518,22 +518,16 @@ def test_dp_client_norms_ride_in_round_buffer(cuda):
     assert all(0.0 <= h["clip_frac"] <= 1.0 for h in gpu["history"])
 
 
-@pytest.mark.parametrize("owned", [False, True])
-def test_fused_adam_in_grad_reduce_bitwise(cuda, monkeypatch, owned):
-    """MFMA engine: the Adam step fused into hea_grad_reduce gives bitwise the parameters, moments and step counters
-    of the separate qfx_adam launch, over several steps with clients that drop out (active 0: row untouched, counter
-    unchanged) - in the last-block mode (the client's last block updates its row) and in the owned mode (every thread
-    steps the angles whose gradient it forms; what launches with more blocks than CUs use)."""
+def test_fused_adam_in_grad_reduce_bitwise(cuda):
+    """MFMA engine: the Adam step fused into hea_grad_reduce (the client's last block updates its row) gives bitwise
+    the parameters, moments and step counters of the separate qfx_adam launch, over several steps with clients that
+    drop out (active 0: row untouched, counter unchanged)."""
     from qfedx_amd.fl.optim import BatchedOptimizer
     from qfedx_amd.models.vqc import VQCSpec
-    from qfedx_amd.ops import hea_mfma
     from qfedx_amd.ops.engine import VQCEngine
-    if owned:
-        monkeypatch.setattr(hea_mfma, "FUSED_ADAM_MAX_BLOCKS", 0)
     spec = VQCSpec(n_qubits=12, n_layers=2, n_classes=3)
     eng = VQCEngine(spec, cuda, "hip", "mfma")
     assert getattr(eng.hip, "fuses_optimizer", False)
-    assert eng.hip.owned_adam
     K, B = 5, 8
     g = torch.Generator().manual_seed(7)
     xs = [spec.encode_features(torch.rand(K, B, 12, generator=g)).to(cuda) for _ in range(3)]
@@ -628,19 +622,14 @@ def test_prologue_fragments_match_per_client_fragments(cuda, monkeypatch):
 
 
 @pytest.mark.parametrize("kw", [dict(local_epochs=2), dict(local_steps=1, weighting="uniform")])
-@pytest.mark.parametrize("owned", [False, True])
-def test_fedavg_tail_in_adam_epilogue_is_bitwise(cuda, monkeypatch, kw, owned):
+def test_fedavg_tail_in_adam_epilogue_is_bitwise(cuda, monkeypatch, kw):
     """Plain FedAvg folded into the MFMA engine's fused Adam epilogue of the round's last local step (QfxFedTail:
     the same fixed-point terms added with int64 atomics into the buffer head the prologue zeroed, metrics packed and
     the single-rank round applied by the last client) gives bitwise the run with the separate FedAvg launch: global
-    parameters, accuracies and the round losses, eager and graph-captured rounds alike.  ``owned``: the owned Adam
-    mode (terms added by the threads that step the angles, metric pack + apply as a one-block launch)."""
+    parameters, accuracies and the round losses, eager and graph-captured rounds alike."""
     from tests.test_fl import small_cfg
     from qfedx_amd.api import run_experiment
-    from qfedx_amd.ops import hea_mfma
     from qfedx_amd.parallel.dist import init_distributed
-    if owned:
-        monkeypatch.setattr(hea_mfma, "FUSED_ADAM_MAX_BLOCKS", 0)
     outs = []
     for on in ("1", "0"):
         monkeypatch.setenv("QFEDX_FED_TAIL", on)
