@@ -82,8 +82,7 @@ def main():
         p, fwd = ent[0], ent[1]
         out = prog._buf(f"psi{j}", N, torch.int32)
         psi_in = stored[j - 1] if j > 0 else empty
-        geom = prog._geom(p, j == 0, False, True, False, B, params.shape[1], S, xx.shape[1], K,
-                          pair=prog._paired(B))
+        geom = prog._geom(p, j == 0, False, True, False, B, params.shape[1], S, xx.shape[1], K)
         nb = 4 * N * ((j > 0) + 1)
         timeit(lambda: C.hea_pass(False, fwd[0], fwd[1], fwd[2], geom, prog.scale, psi_in, out, empty, empty, xx, params, fr, fempty,
                                   part if j == R else fempty, fempty, _NODBG), f"fwd{j}", nb)
