@@ -126,10 +126,14 @@ __device__ __forceinline__ void lds_barrier() { __asm__ volatile("s_waitcnt lgkm
 //   EPI     gradient epilogue (fixed-point packing, u64 LDS atomics)
 //   TAIL    after the op loop: last barrier, region reduction, tile store
 // Slots NPH - 2 / NPH - 1 hold the op count and the wave's total cycles.
-enum { PH_PRO = 0, PH_LOAD, PH_BAR, PH_SETUP, PH_BACK, PH_GRADL1, PH_APPLY, PH_OTHER, PH_EPI, PH_TAIL, NPH = 16 };
+//   GEN1 / GEN2  the first forward pass's layer-1 generation: factors + outer product (wave 0) and its barrier / the
+//           half-index tables and their barrier (LOAD then covers the quads)
+enum { PH_PRO = 0, PH_LOAD, PH_BAR, PH_SETUP, PH_BACK, PH_GRADL1, PH_APPLY, PH_OTHER, PH_EPI, PH_TAIL, PH_GEN1, PH_GEN2,
+       PH_COUNT, NPH = 16 };
+static_assert(PH_COUNT <= NPH - 2, "stamp row: phases + op count + total");
 constexpr int STAMP_WG = HEA_STAMP_ROWS / 16;   // workgroups stamped per pass (a.dbg: STAMP_WG x waves x NPH u64)
 struct Stamps {
-  unsigned long long acc[PH_TAIL + 1];
+  unsigned long long acc[PH_COUNT];
   unsigned long long t0, last;
   int nops;
   __device__ __forceinline__ static unsigned long long now() {
@@ -142,7 +146,7 @@ struct Stamps {
   __device__ __forceinline__ void init() {
     if constexpr (QFX_HEA_STAMPS) {
 #pragma unroll
-      for (int i = 0; i <= PH_TAIL; ++i) acc[i] = 0;
+      for (int i = 0; i < PH_COUNT; ++i) acc[i] = 0;
       nops = 0;
       t0 = last = now();
     }
@@ -160,7 +164,7 @@ struct Stamps {
       if (!dbg || bid >= STAMP_WG || lane != 0) return;
       long long* row = dbg + ((size_t)bid * nw + wave) * NPH;
 #pragma unroll
-      for (int i = 0; i <= PH_TAIL; ++i) row[i] = (long long)acc[i];
+      for (int i = 0; i < PH_COUNT; ++i) row[i] = (long long)acc[i];
       row[NPH - 2] = nops;
       row[NPH - 1] = (long long)(last - t0);
     }

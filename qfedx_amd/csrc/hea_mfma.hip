@@ -888,6 +888,7 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
       if (tid == 0) outer_s = make_float2(a.scale * f.x, a.scale * f.y);
     }
     lds_barrier();
+    st.mark(PH_GEN1);
     const int ta = a.t >> 1, tb = a.t - ta;
     constexpr int JMAX = TMAX - (TMAX >> 1);
     const bool lowt = tid < (1 << ta), hight = tid >= 256 && tid < 256 + (1 << tb);
@@ -909,6 +910,7 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
         tabB[i] = v;
     }
     lds_barrier();
+    st.mark(PH_GEN2);
     const uint32_t am = (1u << ta) - 1u;
     // quad q = tid + NT i holds LDS words 4q .. 4q+3 = amplitudes tau_e = (4q + e) ^ h, h = h(q >> 3);
     // the swizzle only flips bits < 5 and ta >= 4, so the four words share one high-half factor.  Table reads

@@ -7,6 +7,7 @@ of the first STAMP_WG workgroups of each pass launch sums s_memtime deltas per p
   BAR    op barriers, arrival -> release          SETUP  fragment registers, next-op staging, gradient-region flush
   BACK   BACK op bodies   GRADL1 cross-only op bodies   APPLY forward group ops   OTHER OBS / READOUT
   EPI    gradient epilogue (fixed point + u64 LDS atomics)                        TAIL   last barrier, reduction, store
+  GEN1   first forward pass: layer-1 factors (wave 0) + barrier   GEN2 half-index tables + barrier (LOAD: the quads)
 
 Each stamp costs ~40 cycles and drains the wave's LDS operations (s_waitcnt lgkmcnt(0)), so read SHARES, never the
 build's run time.  Prints one JSON line per pass (mean cycles per wave per phase, per-op means, shares) and a text
@@ -20,7 +21,7 @@ import sys
 os.environ["QFEDX_STAMPS"] = "1"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-PH = ["PRO", "LOAD", "BAR", "SETUP", "BACK", "GRADL1", "APPLY", "OTHER", "EPI", "TAIL"]
+PH = ["PRO", "LOAD", "BAR", "SETUP", "BACK", "GRADL1", "APPLY", "OTHER", "EPI", "TAIL", "GEN1", "GEN2"]
 
 
 def main():
