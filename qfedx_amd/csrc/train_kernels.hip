@@ -357,12 +357,14 @@ __device__ __forceinline__ long long secagg_masks(const SecAgg& sa, int k, long 
   return sa.masks[(size_t)k * (P + 1) + e];
 }
 
+template <bool PLAIN>
 __device__ __forceinline__ long long fedavg_term(float x, double tg, bool wr, int k, long e, const double* weights,
                                                  const double* norms, const uint32_t* keys, const float* dps, int dp,
                                                  float clip, float sigma, int& nsat, const SecAgg& sa, int sa_P) {
   const double SC = 4294967296.0;
   double d = (double)x - tg;
   if (wr) d = wrap_pi(d);
+  if constexpr (PLAIN) return fixed_term(weights[k] * d * SC, nsat);
   if (dp) {
     const double n = norms[k];
     const double sc = fmin(1.0, (double)clip / fmax(n, 1e-12));
@@ -455,6 +457,10 @@ __device__ __forceinline__ long long weight_sum_wave(const double* __restrict__ 
   return ws;
 }
 
+// PLAIN: no DP clip / noise and no SecAgg masks (the common round: the CFed and plain VQC reductions) - its own
+// instantiation, since the general one's DP / SecAgg paths held it at 123 VGPRs, one 1024-thread block per CU
+// (the CNN's 1,779 blocks then ran in seven rounds of latency-bound blocks: 34 us)
+template <bool PLAIN>
 __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
     const float* __restrict__ theta_k, const float* theta_g,     // theta_g may be fa.theta (applied in place)
     const unsigned char* __restrict__ angle_mask, const double* __restrict__ weights,
@@ -509,10 +515,12 @@ __global__ void __launch_bounds__(FA_E * FA_G) qfx_fedavg_reduce_kernel(
       for (int u = 0; u < FA_U; ++u) x[u] = theta_k[(size_t)(k + u * FA_G) * P + e];
 #pragma unroll
       for (int u = 0; u < FA_U; ++u)
-        acc += fedavg_term(x[u], tg, wr, k + u * FA_G, e, weights, norms, keys, dps, dp, clip, sigma, nsat, sa, P);
+        acc += fedavg_term<PLAIN>(x[u], tg, wr, k + u * FA_G, e, weights, norms, keys, dps, dp, clip, sigma, nsat, sa,
+                                  P);
     }
     for (; k < K; k += FA_G)
-      acc += fedavg_term(theta_k[(size_t)k * P + e], tg, wr, k, e, weights, norms, keys, dps, dp, clip, sigma, nsat, sa,
+      acc += fedavg_term<PLAIN>(theta_k[(size_t)k * P + e], tg, wr, k, e, weights, norms, keys, dps, dp, clip, sigma,
+                                nsat, sa,
                          P);
   }
   // saturated terms are counted (an integer: the count is exact in any order); the host raises on a nonzero
@@ -990,8 +998,12 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                    fa_n_norms < 0 || (fa_bits != 0) != (sa_seeds != nullptr)))
     return (int)hipErrorInvalidValue;
   const FusedApply fa{fa_theta, fa_out, fa_cnt, fa_bits, fa_n_norms, fa_ring_scale, 1.0};
-  hipLaunchKernelGGL(qfx_fedavg_reduce_kernel, dim3(blocks), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
-                     angle_mask, weights, norms, keys, dp ? dp_scale : nullptr, K, P, wrap, dp, clip, sigma, out, rp,
-                     sat, sa, fa);
+  if (!dp && !sa_seeds)
+    hipLaunchKernelGGL(qfx_fedavg_reduce_kernel<true>, dim3(blocks), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
+                       angle_mask, weights, norms, keys, nullptr, K, P, wrap, 0, clip, sigma, out, rp, sat, sa, fa);
+  else
+    hipLaunchKernelGGL(qfx_fedavg_reduce_kernel<false>, dim3(blocks), dim3(FA_E * FA_G), 0, st, theta_k, theta_g,
+                       angle_mask, weights, norms, keys, dp ? dp_scale : nullptr, K, P, wrap, dp, clip, sigma, out, rp,
+                       sat, sa, fa);
   return (int)hipGetLastError();
 }
