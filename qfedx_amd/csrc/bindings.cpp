@@ -85,6 +85,7 @@ int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, f
                               long long* yo, const int* slot_tab, int n_slots, void* frags, int bf16, long long* zero,
                               int nzero, const void* up_host, void* up_dst, long up_nbytes, long long* up_ctr,
                               long long* up_flag, hipStream_t st);
+int qfx_prologue_gather_lanes(int F);
 int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx, int K,
                             int B, long nmax, int F, int mode, float alpha, float* xo, int x_stride, long long* yo,
                             hipStream_t st);
@@ -694,6 +695,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam", &adam);
   m.def("sgdm", &sgdm);
   m.def("fedavg", &fedavg);
+  m.def("prologue_gather_lanes", [](int64_t F) { return qfx_prologue_gather_lanes((int)F); });
   m.def("jit_prepare", &jit_prepare, "generate + hiprtc-compile (or load cached) a circuit-specialised pass kernel",
         py::arg("blob"), py::arg("p"), py::arg("adjoint"), py::arg("cache_dir"), py::arg("include_dir"),
         py::arg("arch"), py::arg("bf16") = false);

@@ -838,6 +838,37 @@ __device__ __forceinline__ void gather_row(const BatchGather& g, long s) {
 
 __global__ void __launch_bounds__(256) qfx_batch_gather_kernel(BatchGather g) { gather_row(g, blockIdx.x); }
 
+// Row s gathered and encoded by tps lanes (a power of two <= 64: an aligned lane group inside one wave; lane l of it),
+// bitwise what gather_row computes (min / max are exact in any order).  The prologue packs 256 / tps rows into a block
+// for short rows (the VQC's n-qubit features): one 256-thread block per 16-float row had made 2,048 gather blocks of a
+// 64-client round.
+__device__ __forceinline__ void gather_row_lanes(const BatchGather& g, long s, int l, int tps) {
+  const long row = g.lid[(s / g.B) % g.K] * g.nmax + g.idx[s];
+  const int F = g.F;
+  const float* xr = g.X + row * F;
+  float* out = g.xo + s * (long)g.x_stride;
+  if (l == 0) g.yo[s] = g.Y[row];
+  if (g.mode == 1) {
+    float mn = INFINITY, mx = -INFINITY;
+    for (int f = l; f < F; f += tps) {
+      const float v = xr[f];
+      mn = fminf(mn, v);
+      mx = fmaxf(mx, v);
+    }
+    for (int o = tps >> 1; o > 0; o >>= 1) {
+      mn = fminf(mn, __shfl_xor(mn, o, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    }
+    const float rng = mx - mn;
+    const float pi_f = 3.14159265358979323846f;
+    for (int f = l; f < F; f += tps) out[f] = rng > 0.f ? ((xr[f] - mn) / rng) * pi_f : 0.f;
+  } else if (g.mode == 0) {
+    for (int f = l; f < F; f += tps) out[f] = g.alpha * xr[f];
+  } else {
+    for (int f = l; f < F; f += tps) out[f] = xr[f];
+  }
+}
+
 // Round prologue in ONE launch: blocks [0, K * chunks) initialise the client rows / optimizer state (as
 // qfx_round_init_kernel), the rest gather and encode the minibatches of EVERY local step of the round (as
 // qfx_batch_gather_kernel over steps * K * B rows).  Neither part reads what the other writes.
@@ -867,7 +898,8 @@ struct UploadJob {
 };
 
 __device__ __forceinline__ void prologue_block(const RoundInit& ri, int chunks, const BatchGather& g, const FragJob& fj,
-                                               long gather_blocks, long long* zero, int nzero, long blk) {
+                                               long gather_blocks, long gather_rows, int tps, long long* zero,
+                                               int nzero, long blk) {
   const int init_blocks = ri.K * chunks;
   if (blk < init_blocks) {
     round_init_chunk(ri, (int)(blk / chunks), (int)(blk % chunks));
@@ -875,7 +907,12 @@ __device__ __forceinline__ void prologue_block(const RoundInit& ri, int chunks, 
   }
   const long b = blk - init_blocks;
   if (b < gather_blocks) {
-    gather_row(g, b);
+    if (tps == 0) {
+      gather_row(g, b);
+    } else {
+      const long s = b * (256 / tps) + threadIdx.x / tps;
+      if (s < gather_rows) gather_row_lanes(g, s, threadIdx.x % tps, tps);
+    }
     return;
   }
   if (b == gather_blocks + fj.n_slots) {   // the all-reduce buffer head the FedAvg tail (hea_grad_reduce) adds into
@@ -891,11 +928,11 @@ __device__ __forceinline__ void prologue_block(const RoundInit& ri, int chunks, 
 }
 
 __global__ void __launch_bounds__(256) qfx_round_prologue_kernel(RoundInit ri, int chunks, BatchGather g, FragJob fj,
-                                                                 long gather_blocks, long long* zero, int nzero,
-                                                                 UploadJob up) {
+                                                                 long gather_blocks, long gather_rows, int tps,
+                                                                 long long* zero, int nzero, UploadJob up) {
   const long work = (long)gridDim.x - up.blocks;
   if ((long)blockIdx.x < work) {
-    prologue_block(ri, chunks, g, fj, gather_blocks, zero, nzero, blockIdx.x);
+    prologue_block(ri, chunks, g, fj, gather_blocks, gather_rows, tps, zero, nzero, blockIdx.x);
   } else {
     for (long i = ((long)blockIdx.x - work) * 256 + threadIdx.x; i < up.n16; i += (long)up.blocks * 256)
       up.dst[i] = up.src[i];
@@ -913,6 +950,8 @@ __global__ void __launch_bounds__(256) qfx_round_prologue_kernel(RoundInit ri, i
     }
   }
 }
+
+extern "C" int qfx_prologue_gather_lanes(int F);
 
 extern "C" int qfx_launch_round_prologue(const float* theta, int K, int P, float* params, float* m, float* v, float* t,
                                          int nt, const float* X, const long long* Y, const long long* lid,
@@ -944,7 +983,10 @@ extern "C" int qfx_launch_round_prologue(const float* theta, int K, int P, float
   const bool rows = params || m || v;
   const int chunks = rows ? (P + SG_E - 1) / SG_E : (t ? 1 : 0);
   const int kinit = rows ? K : (t ? 1 : 0);
-  const long gather = (long)steps * K * B;
+  const long gather_rows = (long)steps * K * B;
+  // short rows: tps lanes per row, 256 / tps rows per block (prologue_gather_lanes, shared with the trainer's gate)
+  const int tps = qfx_prologue_gather_lanes(F);
+  const long gather = tps ? (gather_rows + 256 / tps - 1) / (256 / tps) : gather_rows;
   if (nzero < 0 || (nzero > 0 && !zero)) return (int)hipErrorInvalidValue;
   const long blocks = (long)kinit * chunks + gather + n_slots + (nzero > 0 ? 1 : 0) + up.blocks;
   if (blocks > 0x7fffffffL) return (int)hipErrorInvalidValue;
@@ -952,8 +994,15 @@ extern "C" int qfx_launch_round_prologue(const float* theta, int K, int P, float
   hipLaunchKernelGGL(qfx_round_prologue_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
                      RoundInit{theta, kinit, P, params, m, v, t, nt}, chunks,
                      BatchGather{X, Y, lid, idx, K, B, nmax, F, mode, alpha, xo, x_stride, yo},
-                     FragJob{slot_tab, n_slots, (uint4*)frags, bf16}, gather, zero, nzero, up);
+                     FragJob{slot_tab, n_slots, (uint4*)frags, bf16}, gather, gather_rows, tps, zero, nzero, up);
   return (int)hipGetLastError();
+}
+
+extern "C" int qfx_prologue_gather_lanes(int F) {
+  if (F <= 0 || F > 64) return 0;
+  int t = 8;
+  while (t < F) t <<= 1;
+  return t;
 }
 
 extern "C" int qfx_launch_batch_gather(const float* X, const long long* Y, const long long* lid, const long long* idx,

@@ -11,9 +11,9 @@ fixes the step count for every client (benchmarks).
 """
 from __future__ import annotations
 
-import time
-
 import math
+import os
+import time
 
 import numpy as np
 from typing import Optional
@@ -27,9 +27,11 @@ from .optim import BatchedOptimizer
 # The round prologue gathers every step's inputs up front below this buffer size.  The buffer lives in the round
 # graph's private pool and up to _GRAPH_LRU graphs stay cached, so the cap bounds that reserve too (1.5 GiB).
 UPFRONT_GATHER_BYTES = 1 << 28
-# gather rows (steps x clients x batch) up to which the round prologue also does the host upload: one launch fewer at
-# the 8-client share (256 rows, 9.7 -> 8.1 us); at 2,048 rows the gather's pinned index reads took 35 us
-FOLD_UPLOAD_MAX_ROWS = 512
+# prologue gather blocks up to which the round prologue also does the host upload (its gather blocks read their indices
+# from the pinned buffer): one launch fewer at the 8-client share (9.7 -> 8.1 us); at 2,048 one-row blocks the pinned
+# index reads took 35 us.  Short rows are packed 16 to a block since (64 clients: 128 gather blocks).
+FOLD_UPLOAD_MAX_BLOCKS = 512
+FOLD_UPLOAD = os.environ.get("QFEDX_FOLD_UPLOAD", "1") != "0"     # (A/B knob)
 _GRAPH_LRU = 6
 
 
@@ -246,6 +248,14 @@ class VQCClientTrainer:
     def encode(self, X: torch.Tensor) -> torch.Tensor:
         return self.spec.encode_features(X)
 
+    @staticmethod
+    def _gather_blocks(rows: int, F: int) -> int:
+        """Gather blocks of the round prologue for ``rows`` rows of F features (csrc/train_kernels.hip: short rows are
+        packed 256 / tps to a block)."""
+        from ..ops._ext import ext
+        tps = int(ext().prologue_gather_lanes(int(F)))
+        return rows if tps == 0 else -(-rows // (256 // tps))
+
     def _body(self, X, Y, lid, theta, idx_d, wts_d, act_d, steps: int, round_num: int, method: str,
               traj_keys=None, ro_keys=None, tail=None):
         """Device work of one round (capturable): local steps of all clients.
@@ -281,7 +291,8 @@ class VQCClientTrainer:
         # gather block reads its indices from the pinned buffer itself: csrc/train_kernels.hip UploadJob), else its
         # own copy kernel here, ahead of every reader of the uploaded tables
         pend = self.__dict__.pop("_pending_upload", None)
-        if pend is not None and not (upfront and idx_d.is_contiguous() and steps * K * BT <= FOLD_UPLOAD_MAX_ROWS):
+        if pend is not None and not (upfront and idx_d.is_contiguous() and FOLD_UPLOAD
+                                     and self._gather_blocks(steps * K * BT, X.shape[-1]) <= FOLD_UPLOAD_MAX_BLOCKS):
             from ..ops._ext import ext
             ext().host_upload(*pend)
             pend = None
