@@ -99,12 +99,26 @@ __device__ __forceinline__ uint32_t pack_h2(float re, float im) {
   return __builtin_bit_cast(uint32_t, h);
 }
 
+// |amplitude|^2 of one packed word: one v_dot2_f32_f16 for fp16 (the fp16 products are exact in fp32) instead of two
+// converts, a multiply and an fma
+__device__ __forceinline__ float norm2_h2(uint32_t u);
+
 __device__ __forceinline__ float2 unpack_h2(uint32_t u) {
 #if QFX_HEA_BF16
   return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u));   // bf16 -> fp32 is a shift
 #else
   half2v h = __builtin_bit_cast(half2v, u);
   return make_float2((float)h.x, (float)h.y);
+#endif
+}
+
+__device__ __forceinline__ float norm2_h2(uint32_t u) {
+#if QFX_HEA_BF16
+  const float2 f = unpack_h2(u);
+  return f.x * f.x + f.y * f.y;
+#else
+  const half2v h = __builtin_bit_cast(half2v, u);
+  return __builtin_amdgcn_fdot2(h, h, 0.f, false);
 #endif
 }
 

@@ -722,8 +722,7 @@ __device__ __forceinline__ void readout_op(const uint32_t* psi_t, const PassArgs
     for (int c = 0; c < NC; ++c) sum[c] = 0.f;
 #pragma unroll
     for (int j = 0; j < CH; ++j) {
-      const float2 f = unpack_h2(v[j]);
-      const float p = f.x * f.x + f.y * f.y;
+      const float p = norm2_h2(v[j]);
 #pragma unroll
       for (int c = 0; c < NC; ++c) sum[c] += cs.mul(p, j, c);
     }
