@@ -491,7 +491,10 @@ class VQCClientTrainer:
                     up._fill(ent["pin"][v][: up.nbytes])
                     g = torch.cuda.CUDAGraph()
                     try:
-                        with torch.cuda.graph(g):
+                        # thread-local capture: the RCCL watchdog thread queries its work events at any time, and in
+                        # the global mode such a query during the capture aborted the process (hipErrorStreamCapture-
+                        # Unsupported, seen once in tests/test_gpu_rccl.py)
+                        with torch.cuda.graph(g, capture_error_mode="thread_local"):
                             self._pending_upload = (ent["pin"][v][: up.nbytes], pack, ent["ctr"], ent["flag"])
                             out = body(v if ent["post_in_graph"] else None)
                             if ent["post_in_graph"]:
@@ -512,7 +515,7 @@ class VQCClientTrainer:
                         ent["graphs"], ent["out"] = [], []
                         for v2 in range(2):
                             g = torch.cuda.CUDAGraph()
-                            with torch.cuda.graph(g):
+                            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                                 self._pending_upload = (ent["pin"][v2][: up.nbytes], pack, ent["ctr"], ent["flag"])
                                 out = body()
                             ent["graphs"].append(g)

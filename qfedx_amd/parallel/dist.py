@@ -272,7 +272,7 @@ def graph_allreduce_selfcheck(world: World) -> Optional[Callable[[], bool]]:
         torch.cuda.current_stream(dev).wait_stream(side)
         static = torch.zeros_like(x)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             dist.all_reduce(static)
     except Exception:
         return None
