@@ -122,3 +122,16 @@ def test_jit_cache_concurrent_writers(tmp_path):
     a = open(os.path.join(shared, key + ".co"), "rb").read()
     b = open(os.path.join(alone, key + ".co"), "rb").read()
     assert len(a) > 0 and a == b
+
+
+def test_prologue_gather_packing_and_upload_fold_gate():
+    """The round prologue gathers short rows (the VQC's n features) 256 / tps to a block, tps = the next power of two
+    >= n lanes (csrc/train_kernels.hip qfx_prologue_gather_lanes); rows past 64 floats keep one block each.  The
+    trainer's upload-fold gate counts those blocks (64 clients x 32 samples of 16 features: 128 blocks, folded; the
+    CNN's 4,096 784-pixel rows: 4,096 blocks, not folded)."""
+    from qfedx_amd.fl.trainer import FOLD_UPLOAD_MAX_BLOCKS, VQCClientTrainer
+    assert [C.prologue_gather_lanes(f) for f in (1, 8, 9, 16, 20, 64, 65, 784)] == [8, 8, 16, 16, 32, 64, 0, 0]
+    assert VQCClientTrainer._gather_blocks(2048, 16) == 128 <= FOLD_UPLOAD_MAX_BLOCKS
+    assert VQCClientTrainer._gather_blocks(256, 16) == 16
+    assert VQCClientTrainer._gather_blocks(2049, 20) == 257
+    assert VQCClientTrainer._gather_blocks(4096, 784) == 4096 > FOLD_UPLOAD_MAX_BLOCKS
