@@ -68,7 +68,7 @@ SUITE = {
     # distributed DP: each client adds sigma^2 C^2 / m, the SecAgg sum carries the accounted sigma C
     "vqc20q_ddp64_mfma": ("configs/baseline3_20q_dp_64clients.yaml",
                           ["model.state_dtype=mfma", "privacy.deterministic_noise=true",
-                           "privacy.noise_mode=distributed", "privacy.secure_agg=true"],
+                           "privacy.noise_mode=distributed", "privacy.secure_agg=true", "train.weighting=uniform"],
                           "client local-steps/sec (20-qubit VQC x 64 non-IID clients, distributed DP + SecAgg, "
                           "fp16 MFMA engine)", None),
     "vqc48q_mps64": ("configs/mps_48q_64clients.yaml", [],
@@ -138,8 +138,12 @@ def main():
         if cfg.privacy.dp:
             rec["dp"] = {"noise_mode": cfg.privacy.noise_mode, "noise_multiplier": cfg.privacy.noise_multiplier,
                          "clip_norm": cfg.privacy.clip_norm, "delta": cfg.privacy.delta,
-                         "rounds_accounted": len(runner.accountant.history) if hasattr(runner.accountant, "history")
-                         else None, "epsilon": round(float(runner.accountant.get_epsilon(cfg.privacy.delta)), 4),
+                         # accounted rounds = the sum of the history's step counts (the accountant merges equal
+                         # (q, sigma) rounds into one record); q next to epsilon.  Every round that ran is charged:
+                         # warm-up, timed and calibration rounds alike.
+                         "rounds_accounted": int(sum(h[2] for h in runner.accountant.history)),
+                         "sampling_rate_q": sorted({round(float(h[0]), 6) for h in runner.accountant.history}),
+                         "epsilon": round(float(runner.accountant.get_epsilon(cfg.privacy.delta)), 4),
                          "deterministic_noise": cfg.privacy.deterministic_noise}
         eng = getattr(runner.adapter, "engine", None)
         if kind == "vqc" and backend == "hip":

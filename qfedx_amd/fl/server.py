@@ -99,6 +99,12 @@ class FederatedRunner:
             # each client's share of the noise is too small to protect its update on its own: only the SecAgg sum
             # (which the server sees instead of the shares) carries the accounted sigma C
             raise ValueError("privacy.noise_mode=distributed needs privacy.secure_agg=true")
+        if p.dp and getattr(p, "noise_mode", "local") == "distributed" and t.weighting != "uniform":
+            # the shares are scaled by each client's FedAvg weight AFTER noising: the sum then carries noise std
+            # sigma C sqrt(sum w_k^2 / m) against a sensitivity of max_k w_k C, an effective multiplier of
+            # sigma RMS(w) / max(w) < sigma for unequal weights - the accountant would under-report epsilon
+            raise ValueError("privacy.noise_mode=distributed needs train.weighting=uniform (with sample weighting "
+                             "the aggregate noise falls below the accounted sigma)")
         self.secagg = None
         if p.secure_agg:
             # each client's DH secret comes from OS randomness on the rank hosting it; only public keys

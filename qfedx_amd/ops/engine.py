@@ -72,9 +72,12 @@ class VQCEngine:
                 raise ValueError("amplitude-encoded initial states need a dense 2^n vector (n <= 26 with mps)")
             self.prog = MPSProgram(ops, coef, spec.n_qubits, self.device, chi_max=mps_chi)
             self.hip = None
-            # the CNOT-chain VQC (<= 3 layers, exact at bond 8) runs on one HIP kernel per step on a GPU
+            # the CNOT-chain VQC (<= 3 layers, exact at bond 2^L) runs on one HIP kernel per step on a GPU - only
+            # when mps_chi admits the exact bond: with mps_chi < 2^L the einsum network truncates, and the same
+            # config must give the same (truncated) result on every device
             from ..quantum.mps_chain import eligible as chain_ok
-            if self.device.type == "cuda" and chain_ok(spec) and noise is None:
+            if (self.device.type == "cuda" and chain_ok(spec) and noise is None
+                    and int(mps_chi) >= (1 << spec.n_layers)):
                 from .mps_hip import MpsChainProgram
                 self.mps_hip = MpsChainProgram(spec, self.device)
         elif backend == "density":

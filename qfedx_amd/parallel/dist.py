@@ -70,9 +70,13 @@ def init_distributed(device: torch.device, backend: str = "auto", timeout_s: int
         # RCCL runs one rank per GPU: more local ranks than visible GPUs would put two ranks on one device (the
         # device map takes LOCAL_RANK modulo the count) and fail deep inside communicator setup.  device_count()
         # does not initialise the GPU.
+        # Only what the launcher actually set is checked: a multi-node srun / mpirun job that sets RANK and
+        # WORLD_SIZE but no LOCAL_* variables has no local-rank information to check against (the global RANK
+        # is not a local index there).
         ngpu = torch.cuda.device_count()
-        lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(ws)))
-        if local >= ngpu or lws > ngpu:
+        lws = int(os.environ["LOCAL_WORLD_SIZE"]) if "LOCAL_WORLD_SIZE" in os.environ else 0
+        lrank = int(os.environ["LOCAL_RANK"]) if "LOCAL_RANK" in os.environ else -1
+        if lrank >= ngpu or lws > ngpu:
             raise RuntimeError(f"dist_backend=nccl (RCCL) needs one GPU per rank: LOCAL_RANK={local} of "
                                f"{lws} local ranks, but {ngpu} GPU(s) visible; launch at most {ngpu} ranks per node "
                                "or use dist_backend=gloo")

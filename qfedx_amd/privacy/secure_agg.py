@@ -181,9 +181,23 @@ class SecureAggregator:
         """Every surviving participant keeps at least ``live_threshold`` live neighbours (public information: the
         participant set, the dropouts and the round-keyed graph, so every rank decides alike)."""
         parts = sorted({int(c) for c in participants})
-        cnt = self.live_counts(parts, dropped, round_num)
         t = self.live_threshold(len(parts))
+        self.check_threshold(len(parts))
+        cnt = self.live_counts(parts, dropped, round_num)
         return all(v >= t for v in cnt.values())
+
+    def check_threshold(self, num_participants: int) -> None:
+        """A ``min_live`` above the mask graph's degree (sparse degree, or K - 1 on the complete graph) fails every
+        round even with no dropout: the server would silently turn every round into an aborted no-op.  Raised
+        instead (a configuration error, not a privacy event)."""
+        if num_participants < 2:
+            return
+        deg = num_participants - 1
+        if self.graph == "sparse":
+            deg = min(deg, secagg_degree(num_participants))
+        if self.live_threshold(num_participants) > deg:
+            raise ValueError(f"privacy.secagg_min_live={self.min_live} exceeds the mask graph degree {deg} of a "
+                             f"{num_participants}-participant round ({self.graph} graph): every round would abort")
 
     def _require_ok(self, participants, dropped, round_num) -> None:
         if not self.round_ok(participants, dropped, round_num):

@@ -224,6 +224,20 @@ def test_rccl_refuses_more_ranks_than_gpus(monkeypatch):
     monkeypatch.setenv("LOCAL_RANK", "3")
     with pytest.raises(RuntimeError, match="one GPU per rank"):
         init_distributed(torch.device("cuda", 1), "nccl")
+    # a multi-node launcher that sets only RANK / WORLD_SIZE (no LOCAL_*) carries no local-rank
+    # information; the global rank must not be mistaken for a local index
+    import torch.distributed as tdist
+    monkeypatch.delenv("LOCAL_RANK")
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    monkeypatch.setenv("MASTER_PORT", "29999")
+    inits = []
+    monkeypatch.setattr(tdist, "is_initialized", lambda: False)
+    monkeypatch.setattr(tdist, "init_process_group", lambda **kw: inits.append(kw))
+    w = init_distributed(torch.device("cuda", 1), "nccl")
+    assert inits and inits[0]["rank"] == 3 and w.world_size == 4
+    monkeypatch.undo()
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
+    monkeypatch.setenv("WORLD_SIZE", "4")
     monkeypatch.setenv("RANK", "1")
     monkeypatch.setenv("LOCAL_RANK", "1")
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")          # rank 1 fits, but the node launched 4 ranks on 2 GPUs

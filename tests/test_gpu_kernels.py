@@ -630,13 +630,25 @@ def test_fedavg_tail_in_adam_epilogue_is_bitwise(cuda, monkeypatch, kw):
     from tests.test_fl import small_cfg
     from qfedx_amd.api import run_experiment
     from qfedx_amd.parallel.dist import init_distributed
+    from qfedx_amd.ops.hea_mfma import HeaMfmaProgram
+    orig = HeaMfmaProgram.loss_and_grads
+    fused = {"1": 0, "0": 0}
+    mode = ["1"]
+
+    def spy(self, *a, **k):          # the knob-on run must actually take the fused path
+        res = orig(self, *a, **k)
+        fused[mode[0]] += int(bool(res.get("fed_done")))
+        return res
+    monkeypatch.setattr(HeaMfmaProgram, "loss_and_grads", spy)
     outs = []
     for on in ("1", "0"):
+        mode[0] = on
         monkeypatch.setenv("QFEDX_FED_TAIL", on)
         cfg = small_cfg(num_rounds=4, n_qubits=12, n_layers=3, device="cuda", backend="hip", num_clients=6,
                         state_dtype="mfma", **kw)
         dev = torch.device("cuda", 0)
         outs.append(run_experiment(cfg, world=init_distributed(dev), device=dev, backend="hip"))
+    assert fused["1"] >= 1 and fused["0"] == 0, fused      # the fused FedAvg tail ran (graph replays skip Python)
     assert torch.equal(outs[0]["params"], outs[1]["params"])
     assert torch.equal(torch.tensor(outs[0]["accuracies"]), torch.tensor(outs[1]["accuracies"]))
     l0 = [h.get("train_loss") for h in outs[0]["history"]]

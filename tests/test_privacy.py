@@ -342,9 +342,12 @@ def test_distributed_dp_noise_scale_and_learning():
         noise_scale("other", 4)
     kw = dict(num_rounds=12, num_clients=32, samples_per_client=32, client_fraction=0.5, dp=True, noise_multiplier=1.0,
               clip_norm=1.0, deterministic_noise=True, noise_mode="distributed", n_qubits=6, n_layers=2,
-              test_samples=256, batch_size=16, learning_rate=0.05, local_steps=1)
+              test_samples=256, batch_size=16, learning_rate=0.05, local_steps=1, weighting="uniform")
     with pytest.raises(ValueError, match="secure_agg"):
         run_experiment(small_cfg(**kw))
+    # sample weighting scales the noised shares after noising: rejected
+    with pytest.raises(ValueError, match="weighting=uniform"):
+        run_experiment(small_cfg(secure_agg=True, **dict(kw, weighting="samples")))
     out = run_experiment(small_cfg(secure_agg=True, **kw))
     acc = out["accuracies"]
     assert acc[-1] > acc[0] + 0.05 and sum(acc[-3:]) > sum(acc[:3])
@@ -360,3 +363,36 @@ def test_distributed_dp_sum_carries_accounted_noise():
     for mode, want in (("local", m ** 0.5), ("distributed", 1.0)):
         out, _ = clip_and_noise(d, 1.0, 1.0, 7, 0, list(range(m)), scale_k=noise_scale(mode, m))
         assert abs(float(out.sum(0).std()) / want - 1.0) < 0.03
+
+
+def test_weighted_distributed_noise_would_under_noise():
+    """Why noise_mode=distributed needs uniform weights: with FedAvg weights w_k applied after each client adds
+    N(0, sigma^2 C^2 / m), the weighted sum's noise std is sigma C sqrt(sum w_k^2 / m) while one client's sensitivity
+    is max_k w_k C.  One client with 10x the samples among 16 gives an effective multiplier ~0.27 sigma."""
+    from qfedx_amd.privacy.dp import clip_and_noise, noise_scale
+    m, P = 16, 40000
+    n = torch.ones(m, dtype=torch.float64)
+    n[0] = 10.0
+    w = n / n.sum()
+    out, _ = clip_and_noise(torch.zeros(m, P, dtype=torch.float64), 1.0, 1.0, 11, 0, list(range(m)),
+                            scale_k=noise_scale("distributed", m))
+    eff = float((out * w[:, None]).sum(0).std()) / float(w.max())      # effective sigma (C = 1)
+    want = float((w.pow(2).sum() / m).sqrt() / w.max())
+    assert abs(eff / want - 1.0) < 0.03 and eff < 0.3                   # ~0.27 sigma: far below the accounted 1.0
+    uni = torch.full((m,), 1.0 / m, dtype=torch.float64)
+    eff_u = float((out * uni[:, None]).sum(0).std()) / float(uni.max())
+    assert abs(eff_u - 1.0) < 0.03                                       # uniform weights: exactly sigma
+
+
+def test_secagg_min_live_above_degree_raises():
+    """a min_live the mask graph can never satisfy is a configuration error, not a silent abort of every
+    round."""
+    from qfedx_amd.privacy.secure_agg import SecureAggregator, secagg_degree
+    sa = SecureAggregator(0, graph="full", min_live=4)
+    assert sa.round_ok(range(5), [], 0)                  # K - 1 = 4 live neighbours: fine
+    with pytest.raises(ValueError, match="degree"):
+        sa.round_ok(range(4), [], 0)                     # K - 1 = 3 < 4
+    K = 64
+    sp = SecureAggregator(0, graph="sparse", min_live=secagg_degree(K) + 1)
+    with pytest.raises(ValueError, match="degree"):
+        sp.round_ok(range(K), [], 0)
