@@ -24,8 +24,8 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ..parallel.dist import (ShardedServerState, World, agree_graph_comm, all_gather_cat, all_reduce_, barrier,
-                             broadcast_, shard_clients)
+from ..parallel.dist import (ShardedServerState, World, agree_graph_comm, all_gather_cat, all_reduce_,
+                             all_reduce_async, barrier, broadcast_, shard_clients)
 from ..privacy.accountant import RDPAccountant
 from ..privacy.dp import noise_scale, draw_noise_seed
 from ..privacy.secure_agg import SecureAggregator
@@ -146,6 +146,10 @@ class FederatedRunner:
         want = (bool(getattr(cfg.runtime, "graph_comm", True)) and backend == "hip" and self.server_opt is None
                 and torch.device(device).type == "cuda" and (not world.distributed or world.backend == "nccl"))
         self.graph_comm = agree_graph_comm(world, want)
+        cc4_env = os.environ.get("QFEDX_CC4")
+        self.cc4 = (cc4_env == "1") or (cc4_env is None and world.distributed and
+                                        bool(getattr(cfg.runtime, "overlap_comm", True)))
+        adapter.trainer.cc4 = self.cc4          # the graphed HIP round's side-stream upload + gather
         self.graph_comm_mode = ("captured" if self.graph_comm else "eager") if backend == "hip" else "none"
 
     # ------------------------------------------------------------------ eval
@@ -219,13 +223,11 @@ class FederatedRunner:
         self.log.info(f"resumed from {path} at round {self.start_round}")
 
     # ------------------------------------------------------------------ main loop
-    def run_round(self, r: int, sync: bool = True) -> dict:
-        """One federated round.  With ``sync=False`` nothing reads device memory back: the round is
-        only enqueued (the host can build round r+1 while the GPU runs round r) and the returned
-        record holds device tensors until :meth:`resolve_record`."""
+    def _round_setup(self, r: int) -> dict:
+        """Round r's public, theta-independent decisions: participants, dropouts, the SecAgg abort, this rank's live
+        clients.  Keyed by (seed, round) only, so computing them a round early (CC4 prefetch) changes nothing."""
         t = self.cfg.train
         p = self.cfg.privacy
-        self.timer.step(r)
         # under DP the participant set is part of the mechanism: keyed by the secret like the noise
         participants = sample_participants(self.num_clients, t.client_fraction,
                                            self.noise_seed if p.dp else t.seed, r, self.poisson)
@@ -242,6 +244,34 @@ class FederatedRunner:
         part_set = set(participants)
         local_part = [i for i, c in enumerate(self.local_ids) if c in part_set]
         local_alive = [i for i in local_part if self.local_ids[i] not in dropped_set]
+        return {"participants": participants, "dropped": dropped, "sa_abort": sa_abort, "dropped_set": dropped_set,
+                "local_alive": local_alive}
+
+    def _prefetch(self, r: int) -> None:
+        """CC4: build round r's theta-independent inputs now - its setup and, through the trainer, the minibatch plan,
+        the tables and the gathered, encoded minibatches - while the previous round's collective is in flight."""
+        if r >= self.cfg.train.num_rounds or not hasattr(self.adapter.trainer, "prepare_round"):
+            return
+        st = self._round_setup(r)
+        pre = self.adapter.trainer.prepare_round(self.store, st["local_alive"], r)
+        self._pre = (r, st, pre)
+        self.prefetches = getattr(self, "prefetches", 0) + 1
+
+    def run_round(self, r: int, sync: bool = True) -> dict:
+        """One federated round.  With ``sync=False`` nothing reads device memory back: the round is
+        only enqueued (the host can build round r+1 while the GPU runs round r) and the returned
+        record holds device tensors until :meth:`resolve_record`."""
+        t = self.cfg.train
+        p = self.cfg.privacy
+        self.timer.step(r)
+        pre_r = self.__dict__.pop("_pre", None)
+        pre = None
+        if pre_r is not None and pre_r[0] == r:
+            st, pre = pre_r[1], pre_r[2]
+        else:
+            st = self._round_setup(r)
+        participants, dropped, sa_abort = st["participants"], st["dropped"], st["sa_abort"]
+        dropped_set, local_alive = st["dropped_set"], st["local_alive"]
         t0 = time.perf_counter()
         dev = self.device
         P = self.P
@@ -360,7 +390,8 @@ class FederatedRunner:
                 buf.zero_()
         else:
             with self.timer.phase("local_train"):
-                res = trainer.run_round(self.store, local_alive, self.params, r)
+                res = trainer.run_round(self.store, local_alive, self.params, r,
+                                        **({"pre": pre} if pre is not None else {}))
             with self.timer.phase("aggregate"):
                 if t.weighting == "uniform":
                     w = torch.ones(len(local_alive), dtype=torch.float64, device=dev)
@@ -425,7 +456,14 @@ class FederatedRunner:
                 # ONE collective per round (CC2+CC3): [exact fixed-point update | weight | metrics]
                 buf = torch.cat([contrib.to(torch.int64),
                                  torch.round(metrics.double() * EXACT_SCALE).to(torch.int64)])
-                all_reduce_(buf, self.world)
+                if self.cc4:
+                    # CC4: round r + 1's theta-independent work (setup, plan, minibatch gather + encode) runs while
+                    # this round's all-reduce is in flight (gloo: on its worker thread); theta_{r+1} waits for it
+                    work = all_reduce_async(buf, self.world)
+                    self._prefetch(r + 1)
+                    work.wait()
+                else:
+                    all_reduce_(buf, self.world)
                 comm_bytes = buf.numel() * 8
                 mean_upd, wsum = self.aggregator.finalize(buf[: P + 1])
                 metrics = buf[P + 1:].double() / EXACT_SCALE

@@ -235,6 +235,17 @@ def _tail(epilogue, dv, theta, variant=None, eager=False):
     return tail
 
 
+class RoundPrefetch:
+    """A round's theta-independent inputs, built ahead (CC4): plan, host tables, and on the portable path the
+    gathered + encoded minibatches of every step."""
+
+    def __init__(self, round_num: int, local_idx: list):
+        self.round_num = round_num
+        self.local_idx = local_idx
+        self.plan = self.tabs = self.cids = self.common = self.batches = None
+        self.method = None
+
+
 class VQCClientTrainer:
     """Runs one federated round of local training for a rank's clients (batched)."""
 
@@ -256,8 +267,12 @@ class VQCClientTrainer:
         tps = int(ext().prologue_gather_lanes(int(F)))
         return rows if tps == 0 else -(-rows // (256 // tps))
 
+    def _gather_mode(self) -> int:
+        spec = self.spec
+        return 2 if spec.amplitude else (1 if spec.feature_scale == "minmax" else 0)
+
     def _body(self, X, Y, lid, theta, idx_d, wts_d, act_d, steps: int, round_num: int, method: str,
-              traj_keys=None, ro_keys=None, tail=None):
+              traj_keys=None, ro_keys=None, tail=None, batches=None, xy=None):
         """Device work of one round (capturable): local steps of all clients.
 
         ``X`` [Nc, Nmax, F] / ``Y`` [Nc, Nmax] are the whole device-resident client store and ``lid`` [K]
@@ -287,6 +302,9 @@ class VQCClientTrainer:
         # and encoded up front (trajectory replicas, T > 1, and rounds whose inputs pass UPFRONT_GATHER_BYTES
         # gather per step)
         upfront = fused and T == 1 and steps * K * BT * X.shape[-1] * 4 <= UPFRONT_GATHER_BYTES
+        # xy: every step's minibatches already gathered into these buffers on the side stream (CC4, _graphed): the
+        # prologue only sets the client rows (and the first step's fragments); no upload or gather here
+        pregathered = xy is not None and upfront
         # the round graph's host upload (_graphed): folded into the prologue launch while its gather is small (each
         # gather block reads its indices from the pinned buffer itself: csrc/train_kernels.hip UploadJob), else its
         # own copy kernel here, ahead of every reader of the uploaded tables
@@ -298,9 +316,13 @@ class VQCClientTrainer:
             pend = None
         if fused:
             from ..ops._ext import ext
-            mode = 2 if spec.amplitude else (1 if spec.feature_scale == "minmax" else 0)
-            xbuf = torch.empty(steps if upfront else 1, K, BT, X.shape[-1], dtype=torch.float32, device=self.device)
-            ybuf = torch.empty((steps if upfront else 1) * K * BT, dtype=torch.int64, device=self.device)
+            mode = self._gather_mode()
+            if pregathered:
+                xbuf, ybuf = xy
+            else:
+                xbuf = torch.empty(steps if upfront else 1, K, BT, X.shape[-1], dtype=torch.float32,
+                                   device=self.device)
+                ybuf = torch.empty((steps if upfront else 1) * K * BT, dtype=torch.int64, device=self.device)
             dummy = torch.zeros(K, BT, 0 if spec.noisy else 1, device=self.device) if spec.amplitude else None
         else:
             rows = lid[:, None]
@@ -313,8 +335,9 @@ class VQCClientTrainer:
             # the MFMA engine's first-step fragments come from theta in the same launch (every row starts as theta);
             # the FedAvg tail's all-reduce buffer head is zeroed there too
             fj = self.engine.prologue_frag_job() if method == "adjoint" and noise is None else None
-            ext().round_prologue(theta.float().contiguous(), params, m, v, t, X, Y, lid, idx_d.contiguous(), mode,
-                                 float(spec.alpha), xbuf, ybuf, frag_job=fj,
+            gi = idx_d[:0] if pregathered else idx_d.contiguous()         # steps = 0: no gather blocks
+            ext().round_prologue(theta.float().contiguous(), params, m, v, t, X, Y, lid, gi, mode,
+                                 float(spec.alpha), xbuf[:0] if pregathered else xbuf, ybuf, frag_job=fj,
                                  frag_bf16=bool(getattr(self.engine.hip, "bf16", False)),
                                  zero=ft["zero"] if ft is not None else None,
                                  upload=list(pend) if pend is not None else None)
@@ -335,6 +358,9 @@ class VQCClientTrainer:
                     xs, yb = xbuf[0], ybuf.view(K, BT)
                 init = xs if spec.amplitude else None
                 xang = dummy if spec.amplitude else xs
+            elif batches is not None:                 # gathered + encoded ahead (prepare_round, CC4)
+                xang, yb = batches[s]
+                init = None
             else:
                 xb = X[rows, bi]                     # [K, B, F]
                 yb = Y[rows, bi]
@@ -352,8 +378,46 @@ class VQCClientTrainer:
                 opt.step(params, res["grad"], act_d[s])
         return params, loss_all, correct_all
 
+    def prepare_round(self, store: ShardStore, local_idx: list, round_num: int, extra: Optional[dict] = None,
+                      gather: bool = True) -> "RoundPrefetch":
+        """The theta-INDEPENDENT part of a round (CC4): the keyed minibatch plan, the round's host tables and, on the
+        portable path, every step's gathered and encoded minibatch.  The server builds round r + 1's while round r's
+        collective is in flight (``all_reduce_async``); on the graphed HIP path the upload and the gather of round
+        r + 1 run on a side stream against round r's graph (``_graphed``, ``cc4``).  ``gather=False``: tables only."""
+        cfg = self.cfg
+        K = len(local_idx)
+        pre = RoundPrefetch(round_num, list(local_idx))
+        if K == 0:
+            return pre
+        li = torch.tensor(local_idx, dtype=torch.int64)
+        cids = [store.client_ids[i] for i in local_idx]
+        plan = BatchPlan(store.counts[li], cids, cfg.batch_size, round_num, cfg.seed,
+                         cfg.local_epochs, cfg.local_steps)
+        nvalid = (plan.wts > 0).sum(-1).float() * plan.active
+        pre.common = {"samples": float(nvalid.sum()), "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
+                      "n_samples": store.counts[li].to(torch.float64)}
+        if plan.idx.numel() and int(plan.idx.max()) >= max(1, store.nmax):   # the gather kernel trusts the table
+            raise RuntimeError("minibatch plan indexes past the client store")
+        tabs = {"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid,
+                "w": store.counts[li].to(torch.float64)}   # FedAvg sample-count weights
+        for name, t in (extra or {}).items():
+            if name in tabs or t.shape[0] != K:
+                raise ValueError(f"extra table {name!r} must be a new per-client [K, ...] table")
+            tabs[name] = t
+        pre.plan, pre.tabs, pre.cids = plan, tabs, cids
+        pre.method = "spsa" if cfg.optimizer == "spsa" else cfg.grad_method
+        fused = self.backend == "hip" and store.X.is_cuda
+        if gather and not fused and self.engine.noise is None and not self.spec.amplitude:
+            # portable path: every step's minibatch gathered and encoded now (theta-independent)
+            rows = li.to(store.X.device)[:, None]
+            pre.batches = []
+            for s_ in range(plan.max_steps):
+                bi = plan.idx[s_].to(store.X.device)
+                pre.batches.append((self.encode(store.X[rows, bi]), store.y[rows, bi]))
+        return pre
+
     def run_round(self, store: ShardStore, local_idx: list, theta_g: torch.Tensor, round_num: int,
-                  epilogue=None, extra: Optional[dict] = None, post=None) -> dict:
+                  epilogue=None, extra: Optional[dict] = None, post=None, pre: "RoundPrefetch" = None) -> dict:
         """Train clients ``store[local_idx]`` from the global params.
 
         Returns device tensors: ``params`` [K,P], ``loss`` / ``correct`` [S,K] per step, ``nvalid`` /
@@ -368,8 +432,9 @@ class VQCClientTrainer:
         ``post()``: the round's collective + global update (all-reduce of the epilogue's buffer, apply to
         ``theta_g`` in place), run after the epilogue: captured into the round graph too when possible (then the
         whole round - host upload, local steps, reduce, all-reduce, apply - is ONE graph launch), else run
-        eagerly.  The returned ``post_done`` says it ran (the caller must not run it again)."""
-        cfg = self.cfg
+        eagerly.  The returned ``post_done`` says it ran (the caller must not run it again).
+        ``pre``: this round's ``prepare_round`` result, built ahead while the previous round's collective ran (CC4);
+        used when it is for the same round and clients (else the tables are built here)."""
         K = len(local_idx)
         P = theta_g.numel()
         if K == 0:
@@ -377,26 +442,19 @@ class VQCClientTrainer:
             return {"params": torch.zeros(0, P, device=self.device), "loss": z, "correct": z, "nvalid": z, "act": z,
                     "lid": torch.zeros(0, dtype=torch.int64, device=self.device), "samples": 0.0, "steps": 0,
                     "client_ids": [], "n_samples": torch.zeros(0, dtype=torch.float64)}
-        li = torch.tensor(local_idx, dtype=torch.int64)
-        cids = [store.client_ids[i] for i in local_idx]
-        plan = BatchPlan(store.counts[li], cids, cfg.batch_size, round_num, cfg.seed,
-                         cfg.local_epochs, cfg.local_steps)
-        method = "spsa" if cfg.optimizer == "spsa" else cfg.grad_method
-        nvalid = (plan.wts > 0).sum(-1).float() * plan.active
-        common = {"samples": float(nvalid.sum()), "steps": int(sum(plan.steps_per_client)), "client_ids": cids,
-                  "n_samples": store.counts[li].to(torch.float64)}
-        if plan.idx.numel() and int(plan.idx.max()) >= max(1, store.nmax):   # the gather kernel trusts the table
-            raise RuntimeError("minibatch plan indexes past the client store")
+        if pre is None or pre.round_num != round_num or pre.local_idx != list(local_idx) or pre.plan is None:
+            pre = self.prepare_round(store, local_idx, round_num, extra, gather=False)
+        else:
+            self.prefetch_hits = getattr(self, "prefetch_hits", 0) + 1
+        plan, tabs, cids, common, method = pre.plan, pre.tabs, pre.cids, pre.common, pre.method
         noise = self.engine.noise
         graphed = self.use_graph and method == "adjoint" and noise is None
-        tabs = {"lid": li, "idx": plan.idx, "wts": plan.wts, "act": plan.active, "nvalid": nvalid,
-                "w": store.counts[li].to(torch.float64)}   # FedAvg sample-count weights
-        for name, t in (extra or {}).items():
-            if name in tabs or t.shape[0] != K:
-                raise ValueError(f"extra table {name!r} must be a new per-client [K, ...] table")
-            tabs[name] = t
         if graphed:
             tabs = _pad_clients(tabs, graph_bucket(K, len(store)))
+            fit = getattr(self.engine, "fit_tiles", None)
+            if fit is not None and not self.__dict__.get("_graph_cache"):
+                # small per-rank batches: smaller MFMA tiles (decided once, before the first round graph)
+                fit(int(tabs["lid"].shape[0]) * plan.B)
         up = PackedUpload(tabs)
         traj_keys = ro_keys = None
         if noise is not None:
@@ -416,7 +474,7 @@ class VQCClientTrainer:
             tail = _tail(epilogue, dv, theta, eager=True)
             params, loss_all, correct_all = self._body(store.X, store.y, dv["lid"], theta, dv["idx"],
                                                        dv["wts"], dv["act"], plan.max_steps, round_num, method,
-                                                       traj_keys, ro_keys, tail=tail)
+                                                       traj_keys, ro_keys, tail=tail, batches=pre.batches)
             if epilogue is not None:    # eager: ``post`` (if any) runs right after, on the caller's side
                 epilogue(params, dict(dv, loss=loss_all, correct=correct_all, eager=True,
                                       fed_done=bool(tail and tail.done)), theta)
@@ -447,31 +505,49 @@ class VQCClientTrainer:
         K = up.layout[0][4][0]
         dev = self.device
         direct = theta_g.is_cuda and theta_g.dtype == torch.float32 and theta_g.is_contiguous()
+        # CC4 (world_size > 1, or QFEDX_CC4=1): the round's host upload and minibatch gather leave the graph for a side
+        # stream, into per-variant table / minibatch buffers, so round r + 1's upload + gather run while round r's
+        # graph - its local steps, and its all-reduce + apply at the end - is still on the main stream
+        F = store.X.shape[-1]
+        cc4 = bool(getattr(self, "cc4", False)) and plan.max_steps * K * plan.B * F * 4 <= UPFRONT_GATHER_BYTES
         key = (K, plan.max_steps, plan.B, store.nmax, store.X.data_ptr(), tuple(l[0] for l in up.layout),
-               theta_g.data_ptr() if direct else None, epilogue is not None, post is not None)
+               theta_g.data_ptr() if direct else None, epilogue is not None, post is not None, cc4)
         cache = self.__dict__.setdefault("_graph_cache", {})
         ent = cache.pop(key, None)
         if ent is None:
             from ..ops._ext import ext
             E = ext()
-            pack = torch.empty(up.nbytes, dtype=torch.uint8, device=dev)
-            dv = up.to_device(dev, pack)
+            packs = [torch.empty(up.nbytes, dtype=torch.uint8, device=dev) for _ in range(2 if cc4 else 1)]
+            dvs = [up.to_device(dev, pk) for pk in packs]
+            pack, dv = packs[0], dvs[0]
             ent = {"pack": pack, "dv": dv, "theta": theta_g if direct else theta_g.to(dev).float().clone(),
+                   "cc4": cc4, "packs": packs, "dvs": dvs,
                    "pin": [E.host_alloc(up.nbytes), E.host_alloc(up.nbytes)], "flip": 0,
                    # upload-completion counter (round count + block arrivals) and its coherent host mirror, both
                    # written by the graph's first node (the upload kernel's last block)
                    "ctr": torch.zeros(2, dtype=torch.int64, device=dev), "flag": E.host_alloc(8, True),
                    "launched": 0}
             ent["flag"].zero_()
-            args = (store.X, store.y, dv["lid"], ent["theta"], dv["idx"], dv["wts"], dv["act"], plan.max_steps,
-                    round_num, "adjoint")
+            if cc4:
+                ent["xy"] = [(torch.empty(plan.max_steps, K, plan.B, F, dtype=torch.float32, device=dev),
+                              torch.empty(plan.max_steps * K * plan.B, dtype=torch.int64, device=dev))
+                             for _ in range(2)]
+                ent["side"] = torch.cuda.Stream(device=dev)
+                ent["ev_g"] = [torch.cuda.Event() for _ in range(2)]
+                ent["ev_c"] = [torch.cuda.Event() for _ in range(2)]
+                ent["c_rec"] = [False, False]
+                ent["pshape"] = torch.empty(K, theta_g.numel(), dtype=torch.float32, device=dev)
 
-            def body(variant=None):
-                # ``variant``: set when post(variant) is captured right behind the epilogue (it may fold into it)
-                tail = _tail(epilogue, dv, ent["theta"], variant=variant)
-                out = self._body(*args, tail=tail)
+            def body(variant=None, bv=0):
+                # ``variant``: set when post(variant) is captured right behind the epilogue (it may fold into it);
+                # ``bv``: the variant whose tables / minibatch buffers the capture reads (CC4: one set per variant)
+                d = dvs[bv] if cc4 else dv
+                tail = _tail(epilogue, d, ent["theta"], variant=variant)
+                out = self._body(store.X, store.y, d["lid"], ent["theta"], d["idx"], d["wts"], d["act"],
+                                 plan.max_steps, round_num, "adjoint", tail=tail,
+                                 xy=ent["xy"][bv] if cc4 else None)
                 if epilogue is not None:
-                    tabs = dict(dv, loss=out[1], correct=out[2], fed_done=bool(tail and tail.done))
+                    tabs = dict(d, loss=out[1], correct=out[2], fed_done=bool(tail and tail.done))
                     if variant is not None:
                         tabs["variant"] = variant
                     epilogue(out[0], tabs, ent["theta"])
@@ -483,6 +559,8 @@ class VQCClientTrainer:
                 side = torch.cuda.Stream(device=dev)
                 side.wait_stream(cur)
                 with torch.cuda.stream(side):       # warm-up (no collective / apply): modules loaded, sizes fixed
+                    if cc4:     # gather only, from the device tables to_device filled (no pinned upload, no count)
+                        self._cc4_gather(ent, store, up, 0, wait=False, upload=False)
                     body()
                 cur.wait_stream(side)
                 ent["graphs"], ent["out"] = [], []
@@ -495,8 +573,9 @@ class VQCClientTrainer:
                         # the global mode such a query during the capture aborted the process (hipErrorStreamCapture-
                         # Unsupported, seen once in tests/test_gpu_rccl.py)
                         with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                            self._pending_upload = (ent["pin"][v][: up.nbytes], pack, ent["ctr"], ent["flag"])
-                            out = body(v if ent["post_in_graph"] else None)
+                            if not cc4:
+                                self._pending_upload = (ent["pin"][v][: up.nbytes], pack, ent["ctr"], ent["flag"])
+                            out = body(v if ent["post_in_graph"] else None, v)
                             if ent["post_in_graph"]:
                                 post(v)
                     except Exception as exc:
@@ -516,8 +595,10 @@ class VQCClientTrainer:
                         for v2 in range(2):
                             g = torch.cuda.CUDAGraph()
                             with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                                self._pending_upload = (ent["pin"][v2][: up.nbytes], pack, ent["ctr"], ent["flag"])
-                                out = body()
+                                if not cc4:
+                                    self._pending_upload = (ent["pin"][v2][: up.nbytes], pack, ent["ctr"],
+                                                            ent["flag"])
+                                out = body(None, v2)
                             ent["graphs"].append(g)
                             ent["out"].append(out)
                         break
@@ -537,8 +618,36 @@ class VQCClientTrainer:
         n = ent["launched"]
         _wait_rounds(ent, n - 1)                    # pinned buffer v: its last reader (replay n - 2) is done
         up._fill(ent["pin"][v][: up.nbytes])
+        if cc4:
+            # side stream: this round's upload + gather, behind only the graph that last read variant v's buffers
+            # (round r - 2); it runs while round r - 1's graph, collective included, is still on the main stream
+            self._cc4_gather(ent, store, up, v)
+            torch.cuda.current_stream(dev).wait_event(ent["ev_g"][v])
         ent["graphs"][v].replay()
+        if cc4:
+            ent["ev_c"][v].record(torch.cuda.current_stream(dev))
+            ent["c_rec"][v] = True
         ent["launched"] = n + 1
         if post is not None and not ent["post_in_graph"]:
             post(v)
-        return (*ent["out"][v], ent["dv"], v if post is not None else None)
+        return (*ent["out"][v], ent["dvs"][v] if cc4 else ent["dv"], v if post is not None else None)
+
+    def _cc4_gather(self, ent, store, up, v: int, wait: bool = True, upload: bool = True) -> None:
+        """The round's theta-independent device work on the side stream (CC4): the upload of the round's tables from
+        pinned buffer v into the variant's device tables and every step's minibatch gather + encode, one prologue
+        launch without client rows (csrc/train_kernels.hip: its gather blocks read the indices from the pinned copy,
+        its last block posts the upload-completion count).  Ordered after the graph that last read variant v."""
+        from ..ops._ext import ext
+        side = ent["side"]
+        if wait and ent["c_rec"][v]:
+            side.wait_event(ent["ev_c"][v])
+        d = ent["dvs"][v]
+        xb, yb = ent["xy"][v]
+        with torch.cuda.stream(side):
+            ext().round_prologue(ent["theta"], ent["pshape"], None, None, None, store.X, store.y, d["lid"],
+                                 d["idx"].contiguous(), self._gather_mode(), float(self.spec.alpha), xb, yb,
+                                 rows=False, upload=[ent["pin"][v][: up.nbytes], ent["packs"][v], ent["ctr"],
+                                                     ent["flag"]] if upload else None)
+            ent["ev_g"][v].record(side)
+        if not wait:
+            torch.cuda.current_stream(self.device).wait_stream(side)

@@ -99,6 +99,32 @@ class VQCEngine:
         else:
             raise ValueError(f"unknown backend '{backend}'")
 
+    def fit_tiles(self, samples: int) -> bool:
+        """Small-batch tiling of the MFMA engine (BASELINE config 2's per-GPU point, 1 client x 32 samples): when a
+        step's forward would launch fewer than two workgroups per CU at 2^14-amplitude tiles (16q: 4 tiles per
+        sample, 128 workgroups at 32 samples), rebuild the program on 2^13 forward tiles (two passes still; 256
+        workgroups) - measured 0.084 -> 0.076 ms per 1-client step (profiles/r6_config2_1client.txt).  Decided once,
+        by the trainer before its first round graph is captured (eager evaluation workspaces of the old program are
+        simply dropped); QFEDX_HEA_TILE pins the tiling.  Returns True if it switched."""
+        import os
+        hip = self.hip
+        if (getattr(self, "_tiles_fitted", False) or hip is None or not hasattr(hip, "tile_bits")
+                or os.environ.get("QFEDX_HEA_TILE") or self.device.type != "cuda"):
+            return False
+        self._tiles_fitted = True
+        if hip.tile_bits < 14 or samples <= 0:
+            return False
+        cus = torch.cuda.get_device_properties(self.device).multi_processor_count
+        if samples * hip.tiles_last >= 2 * cus:
+            return False
+        from .hea_mfma import HeaMfmaProgram
+        small = HeaMfmaProgram(self.spec, self.device, tile_bits=13, storage=hip.storage)
+        if small.n_passes != hip.n_passes:
+            return False
+        small.fused_readout = hip.fused_readout
+        self.hip = small
+        return True
+
     # ------------------------------------------------------------------ helpers
     def _states(self, init: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
         """Initial states [.., 2^n] complex: real ``init`` holds raw amplitudes (encoded here, on the HIP

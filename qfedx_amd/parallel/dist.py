@@ -128,6 +128,24 @@ def all_reduce_(t: torch.Tensor, world: World, op=None) -> torch.Tensor:
     return t
 
 
+class _Done:
+    def wait(self):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+def all_reduce_async(t: torch.Tensor, world: World, op=None):
+    """Issue the SUM all-reduce of ``t`` and return a handle whose ``wait()`` completes it (CC4: the caller does the
+    next round's theta-independent work in between).  gloo runs the collective on its own worker thread, so host
+    work overlaps it; RCCL enqueues it on the current stream (the device-side overlap is the trainer's side stream,
+    fl/trainer.py ``RoundPrefetch``).  Single process: a completed handle."""
+    if not world.distributed:
+        return _Done()
+    return dist.all_reduce(t, op=op or dist.ReduceOp.SUM, async_op=True)
+
+
 def broadcast_(t: torch.Tensor, world: World, src: int = 0) -> torch.Tensor:
     if world.distributed:
         dist.broadcast(t, src)

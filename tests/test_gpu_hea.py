@@ -41,10 +41,14 @@ def _inputs(spec, K, B, seed=0):
                                                  (10, 3, 8, True, "ry"), (11, 2, 8, False, "rx"),
                                                  (12, 4, 9, True, "ry"), (9, 1, 8, True, "rz"),
                                                  (13, 3, 10, True, "ry"), (16, 3, 14, True, "ry"),
-                                                 (12, 1, 9, True, "ry"), (20, 1, 14, True, "rx")])
+                                                 (16, 3, 13, True, "ry"), (12, 1, 9, True, "ry"),
+                                                 (20, 1, 14, True, "rx")])
 def test_hea_vjp_matches_dense(cuda, n, L, tile, chain, feat):
     """L = 1 plans have identity forward passes (they only place layer-1 gradient tiles for the adjoint): the
-    forward reads out at its last applying pass and the later pass outputs alias it."""
+    forward reads out at its last applying pass and the later pass outputs alias it.  (16, 3, 13) is the small-batch
+    tiling (VQCEngine.fit_tiles).  Tolerances: ~3x the largest error measured on these shapes (<Z> 2.5e-4, gradients
+    1.7e-4 x scale: profiles/r6_hea_err_table.txt), so a dropped lo half of the gate split or an extra fp16 rounding
+    per op fails."""
     spec = VQCSpec(n, L, 3, feature_map=feat, entangler="chain" if chain else "none")
     prog = HeaMfmaProgram(spec, cuda, tile_bits=tile)
     K, B = 2, 3
@@ -52,9 +56,9 @@ def test_hea_vjp_matches_dense(cuda, n, L, tile, chain, feat):
     ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
     z, g = prog.vjp(x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda))
     torch.cuda.synchronize()
-    np.testing.assert_allclose(z.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
+    np.testing.assert_allclose(z.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=7.5e-4)
     scale = max(1.0, float(g_ref.abs().max()))
-    np.testing.assert_allclose(g.cpu().numpy(), g_ref.numpy(), atol=4e-3 * scale)
+    np.testing.assert_allclose(g.cpu().numpy(), g_ref.numpy(), atol=5e-4 * scale)
 
 
 @pytest.mark.parametrize("n,L,tile", [(10, 3, 14), (12, 4, 9), (13, 3, 10), (16, 3, 14)])
@@ -117,8 +121,8 @@ def test_hea_expz_eval_matches_dense_20q(cuda):
     x, params, wr = _inputs(spec, K, B, seed=5)
     ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
     z, gr = prog.vjp(x.to(cuda), params[:, : spec.n_theta].to(cuda), wr.to(cuda))
-    np.testing.assert_allclose(z.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
-    np.testing.assert_allclose(gr.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
+    np.testing.assert_allclose(z.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=7.5e-4)
+    np.testing.assert_allclose(gr.cpu().numpy(), g_ref.numpy(), atol=5e-4 * max(1.0, float(g_ref.abs().max())))
     z2 = prog.expz(x.to(cuda), params[:, : spec.n_theta].to(cuda))
     np.testing.assert_allclose(z2.cpu().numpy(), z.cpu().reshape(K, B, -1).numpy(), atol=1e-6)
 
@@ -256,3 +260,28 @@ def test_pair_ops_match_unpaired_kernels(cuda, monkeypatch, n, L, tile):
     ez_ref, g_ref = _dense(spec, x.double(), params.double(), wr.double())
     np.testing.assert_allclose(z1.cpu().reshape(K, B, -1).numpy(), ez_ref.numpy(), atol=3e-3)
     np.testing.assert_allclose(g1.cpu().numpy(), g_ref.numpy(), atol=4e-3 * max(1.0, float(g_ref.abs().max())))
+
+
+def test_small_batch_tiling_switches_once(cuda):
+    """BASELINE config 2's per-GPU point (1 client x 32 samples): the MFMA engine moves to 2^13 forward tiles when
+    2^14 tiles would give fewer than two workgroups per CU, keeps them (decided once), and a large batch keeps 2^14."""
+    import os
+    if os.environ.get("QFEDX_HEA_TILE"):
+        pytest.skip("QFEDX_HEA_TILE pins the tiling")
+    spec = VQCSpec(16, 3, 3)
+    small = VQCEngine(spec, cuda, "hip", "mfma")
+    assert small.hip.tile_bits == 14 and small.fit_tiles(32) and small.hip.tile_bits == 13
+    assert not small.fit_tiles(4096) and small.hip.tile_bits == 13
+    big = VQCEngine(spec, cuda, "hip", "mfma")
+    assert not big.fit_tiles(2048) and big.hip.tile_bits == 14
+    # the switched engine trains: loss and gradients against the fp32 VALU engine
+    g = torch.Generator().manual_seed(4)
+    x = spec.encode_features(torch.rand(1, 32, 16, generator=g)).to(cuda)
+    y = torch.randint(0, 3, (1, 32), generator=g).to(cuda)
+    w = torch.full((1, 32), 1.0 / 32, device=cuda)
+    p = spec.init_params(0)[None].to(cuda)
+    out = small.loss_and_grads(x, y, w, p)
+    ref = VQCEngine(spec, cuda, "hip").loss_and_grads(x, y, w, p)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out["loss"].cpu().numpy(), ref["loss"].cpu().numpy(), atol=1e-3)
+    np.testing.assert_allclose(out["grad"].cpu().numpy(), ref["grad"].cpu().numpy(), atol=1e-3)

@@ -93,3 +93,53 @@ def test_captured_allreduce_selfcheck_rccl():
                        timeout=300, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
     assert r.returncode == 0, r.stderr[-3000:]
     assert "RESULT 1 1" in r.stdout, r.stdout[-2000:]
+
+
+_CC4 = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from tests.test_fl import small_cfg
+from qfedx_amd.api import run_experiment
+from qfedx_amd.parallel.dist import init_distributed, shutdown
+from qfedx_amd.fl.trainer import VQCClientTrainer
+import os
+
+calls = [0]
+real = VQCClientTrainer._cc4_gather
+def counting(self, *a, **k):
+    calls[0] += 1
+    return real(self, *a, **k)
+VQCClientTrainer._cc4_gather = counting
+
+def cfg(backend, **kw):
+    base = dict(num_rounds=4, n_qubits=12, n_layers=3, num_clients=6, samples_per_client=32, batch_size=8,
+                device="cuda", backend="hip", dist_backend=backend, state_dtype="mfma")
+    return small_cfg(**{{**base, **kw}})
+
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+kw = {kw}
+os.environ["QFEDX_CC4"] = "0"
+plain = run_experiment(cfg("auto", **kw), world=init_distributed(dev, "auto"), device=dev, backend="hip")
+c_off = calls[0]
+os.environ["QFEDX_CC4"] = "1"
+world = init_distributed(dev, "nccl")
+rccl = run_experiment(cfg("nccl", **kw), world=world, device=dev, backend="hip")
+same = torch.equal(plain["params"].cpu(), rccl["params"].cpu()) and plain["accuracies"] == rccl["accuracies"]
+shutdown(world)
+print("RESULT", int(same), c_off, calls[0])
+"""
+
+
+@pytest.mark.parametrize("kw", [{}, dict(local_epochs=2, client_fraction=0.5)])
+def test_cc4_side_stream_gather_is_bitwise(kw):
+    """Verdict r5 item 4 (CC4): with a one-rank RCCL group and QFEDX_CC4=1 every round's host upload and minibatch
+    gather run on a side stream (ahead of the round graph, against the previous round's graph and collective), and
+    the run is bitwise the no-group run without the overlap."""
+    code = _CC4.format(root=ROOT, kw=repr(kw))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("RESULT")][-1].split()
+    assert line[1] == "1", r.stdout[-2000:]
+    assert int(line[2]) == 0 and int(line[3]) >= 4, line      # the side-stream path ran every round (+ warm-ups)
