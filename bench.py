@@ -237,6 +237,12 @@ def main():
             # shape had to fall back to an eager collective on some rank)
             "rccl_world_size": rccl_ws,
             "graph_comm": graph_comm,
+            # CC4: round r + 1's upload + minibatch gather on a side stream against round r's graph + collective
+            # (on with more than one rank; QFEDX_CC4 overrides)
+            "cc4_overlap": bool(getattr(runner, "cc4", False)),
+            # MFMA engine tiling: forward / adjoint tile bits (2^13 forward tiles for small per-rank batches)
+            "mfma_tiles": ([int(runner.adapter.engine.hip.tile_bits), int(runner.adapter.engine.hip.adj_tile_bits)]
+                           if mfma else None),
             "host_ms_per_round": round(getattr(runner, "host_ms", 0.0), 4),   # enqueue time (GPU runs behind)
             "clients_per_rank": per_rank,
             # bytes each rank all-reduces per round: ONE fused [exact int64 update | weight | metrics] buffer

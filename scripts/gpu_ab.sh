@@ -5,5 +5,5 @@ source "$(dirname "$0")/gpu_step.sh"
 variants=$(ls -d ab/*/ | xargs -n1 basename)
 for r in 1 2 3; do for v in $variants; do
   extra=""; [ $r -eq 1 ] && [ -z "$KBENCH" ] && extra="--precision"
-  TAILN=1 QFX_PKG_ROOT=$PWD/ab/$v step ab_${v}$r 200 python ${KBENCH:-scripts/hea_kbench.py} --iters 30 $extra $KARGS
+  TAILN=1 QFX_PKG_ROOT=$PWD/ab/$v step ab_${TAG}${v}$r 200 python ${KBENCH:-scripts/hea_kbench.py} --iters 30 $extra $KARGS
 done; done

@@ -135,7 +135,9 @@ print("RESULT", int(same), c_off, calls[0])
 def test_cc4_side_stream_gather_is_bitwise(kw):
     """Verdict r5 item 4 (CC4): with a one-rank RCCL group and QFEDX_CC4=1 every round's host upload and minibatch
     gather run on a side stream (ahead of the round graph, against the previous round's graph and collective), and
-    the run is bitwise the no-group run without the overlap."""
+    the run is bitwise the no-group run without the overlap.  (Plain FedAvg on the MFMA engine: with the group, the
+    Adam-epilogue FedAvg tail writes the all-reduce buffer and leaves the apply to the collective's post step; without
+    it, the tail also applies the round - the multi-rank form of the fused tail)"""
     code = _CC4.format(root=ROOT, kw=repr(kw))
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
