@@ -34,6 +34,7 @@ struct HeaPassArgs {
   int hrow[5];               // LDS swizzle: dword(tau) = tau ^ h(tau >> 5), h bit b = parity(hrow[b] & x)
   long long* dbg;            // stamps build only (QFX_HEA_STAMPS): per-wave phase cycles, [HEA_STAMP_ROWS][16]
   int in_rep;                // forward: shifted parameter rows per stored input sample (param-shift prefix reuse)
+  int nt_store;              // 1: pass-output tiles stored with the non-temporal hint (a pass's states exceed the MALL)
   // Fused readout (first adjoint pass, noiseless): every workgroup computes its sample's <Z>, cross entropy and
   // dL/d<Z> from the readout partials (part, ro_tps tiles) instead of reading wread; the tile-0 workgroup writes
   // ro_expz / ro_w [S][C] (the later passes' wread) and the per-sample reduction record ro_rec [S][2C + 2]

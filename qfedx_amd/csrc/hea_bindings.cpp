@@ -60,7 +60,7 @@ void check(int rc, const char* what) {
 
 // geom = [n, t, c, lo, hi, n_tiles, gen, load_lam, store_psi, store_lam, spc, C, n_theta, p_stride, feature,
 //         S, x_stride, n_slots, slab_tiles, K, H0..H4 (LDS swizzle rows), n_gradops, in_rep, bf16, n_regions,
-//         frag_shared]
+//         frag_shared, nt_store]
 // bf16: states and fragments in bf16 (hea_mfma_bf16.hip) instead of fp16.  dbg: the stall-attribution buffer of the
 // stamps build (int64 [HEA_STAMP_ROWS * 16]; empty otherwise)
 void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, torch::Tensor fo, std::vector<int64_t> geom, double scale,
@@ -69,7 +69,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, torch::Tensor
               torch::Tensor params, torch::Tensor frags, torch::Tensor wread, torch::Tensor part,
               torch::Tensor gslab, torch::Tensor dbg, c10::optional<std::vector<torch::Tensor>> readout,
               int64_t ro_tps) {
-  need(geom.size() == 30, "geometry vector must have 30 entries");
+  need(geom.size() == 31, "geometry vector must have 31 entries");
   const bool bf16 = geom[27] != 0;
   HeaPassArgs a{};
   a.n = (int)geom[0];
@@ -96,6 +96,7 @@ void hea_pass(bool adjoint, torch::Tensor ops, torch::Tensor fidx, torch::Tensor
   a.in_rep = (int)geom[26];
   a.n_regions = (int)geom[28];
   a.frag_shared = geom[29] != 0 ? 1 : 0;
+  a.nt_store = geom[30] != 0 ? 1 : 0;
   need(a.n_regions >= 0 && a.n_regions <= 2 * 32, "gradient regions per pass out of range");
   a.scale = (float)scale;
   a.dbg = dbg.defined() && dbg.numel() > 0 ? dp<long long>(dbg, torch::kInt64, "dbg", (int64_t)HEA_STAMP_ROWS * 16)

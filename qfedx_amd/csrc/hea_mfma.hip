@@ -23,29 +23,15 @@
 __device__ unsigned int qfx_check_word = 0;
 #endif
 
-// Static wave priority (bit 0: forward, bit 1: adjoint): waves NW/2 .. NW-1 of a workgroup share SIMDs with waves
-// 0 .. NW/2-1 and, younger, lose every VALU arbitration (stall table: their op bodies run 25-30% longer while the older
-// half waits for them at the op barrier).
-#ifndef QFX_HEA_PRIO
-#define QFX_HEA_PRIO 0
-#endif
 
 namespace HEA_NS {
 
-// Tile traffic with the non-temporal hint (QFX_HEA_NT bit 0: stores, bit 1: loads): a pass's 512 MB of tiles is read
-// once by a later pass and fits neither L2 nor the Infinity Cache.
-#ifndef QFX_HEA_NT
-#define QFX_HEA_NT 0
-#endif
-__device__ __forceinline__ uint4 tile_ld(const uint32_t* p) {
-  if constexpr (QFX_HEA_NT & 2) {
-    const u4v v = __builtin_nontemporal_load((const u4v*)p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-  }
-  return *(const uint4*)p;
-}
-__device__ __forceinline__ void tile_st(uint32_t* p, uint4 v) {
-  if constexpr (QFX_HEA_NT & 1) {
+// Pass-output tiles are stored with the non-temporal hint when a pass's states exceed the Infinity Cache (PassArgs::
+// nt_store, set by the host: 16q x 2048 samples = 512 MB per pass; the next pass reads them back from HBM anyway):
+// interleaved A/B, 64 clients 1.820 -> 1.784 ms per step; at 8 clients (64 MB, MALL-resident) the plain stores are
+// faster (profiles/r6_tile_nt_priority_ab.txt).  Non-temporal tile LOADS measured slower and are not used.
+__device__ __forceinline__ void tile_st(uint32_t* p, uint4 v, int nt) {
+  if (nt) {
     __builtin_nontemporal_store(u4v{v.x, v.y, v.z, v.w}, (u4v*)p);
     return;
   }
@@ -84,7 +70,7 @@ __device__ __forceinline__ void load_tile(const PassArgs& a, const uint32_t* src
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) v[i] = tile_ld(&src[mem_of(q, a, fixed)]);
+    if (q < (uint32_t)T) v[i] = *(const uint4*)&src[mem_of(q, a, fixed)];
   }
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
@@ -112,7 +98,7 @@ __device__ __forceinline__ void store_tile(const PassArgs& a, uint32_t* dst, con
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) tile_st(&dst[mem_of(q, a, fixed)], v[i]);
+    if (q < (uint32_t)T) tile_st(&dst[mem_of(q, a, fixed)], v[i], a.nt_store);
   }
 }
 
@@ -130,8 +116,8 @@ __device__ __forceinline__ void load_tile_il(const PassArgs& a, const uint32_t* 
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
     if (q < (uint32_t)T) {
-      v[i] = tile_ld(&psrc[mem_of(q, a, fixed)]);
-      l[i] = lsrc ? tile_ld(&lsrc[mem_of(q, a, fixed)]) : make_uint4(0u, 0u, 0u, 0u);
+      v[i] = *(const uint4*)&psrc[mem_of(q, a, fixed)];
+      l[i] = lsrc ? *(const uint4*)&lsrc[mem_of(q, a, fixed)] : make_uint4(0u, 0u, 0u, 0u);
     }
   }
 #pragma unroll
@@ -165,7 +151,7 @@ __device__ __forceinline__ void store_lam_il(const PassArgs& a, uint32_t* dst, c
 #pragma unroll
   for (int i = 0; i < MQ; ++i) {
     const uint32_t q = 4u * (tid + NT * i);
-    if (q < (uint32_t)T) tile_st(&dst[mem_of(q, a, fixed)], v[i]);
+    if (q < (uint32_t)T) tile_st(&dst[mem_of(q, a, fixed)], v[i], a.nt_store);
   }
 }
 
@@ -875,7 +861,6 @@ __device__ __forceinline__ void fwd_pass(const PassArgs& a, int bid) {
   const size_t N = (size_t)1 << a.n;
   const uint32_t fixed = tile_fixed(a, tile_id);
   const float* prm = a.params + (size_t)k * a.p_stride;
-  if ((QFX_HEA_PRIO & 1) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // (wave-uniform: a scalar branch)
   Stamps st;
   st.init();
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)
@@ -1068,7 +1053,6 @@ __device__ __forceinline__ void adj_pass(const PassArgs& a, int bid) {
   const int T = 1 << a.t;
   const size_t N = (size_t)1 << a.n;
   const uint32_t fixed = tile_fixed(a, tile_id);
-  if ((QFX_HEA_PRIO & 2) && wave >= NW / 2) __builtin_amdgcn_s_setprio(1);   // (wave-uniform: a scalar branch)
   Stamps st;
   st.init();
   const uint32_t h_q = swz(a, (uint32_t)tid >> 3);        // for quads 4 (tid + NT i)

@@ -61,6 +61,7 @@ _NO_KEYS = torch.zeros(0, dtype=torch.int64)
 _NODBG = torch.zeros(0, dtype=torch.int64)     # no stall-attribution buffer (stamps build only)
 
 
+NT_STORE_MIN_BYTES = 128 << 20   # pass states above which tiles are stored non-temporally (_nt_store)
 FUSED_ADAM_MAX_BLOCKS = 256   # hea_grad_reduce blocks (clients x gradient ops) up to which Adam is fused
 
 
@@ -202,7 +203,16 @@ class HeaMfmaProgram:
         return [self.n, p.t, p.c, p.lo, p.hi, 1 << (self.n - p.t), int(gen), int(load_lam), int(store_psi),
                 int(store_lam), B, self.C, self.n_theta, p_stride, self.feature, S, x_stride, self.n_slots,
                 self.slab_tiles, K] + [int(h) for h in p.H] + [self.n_gradops, int(in_rep), int(self.bf16),
-                                                                 int(n_regions), int(shared)]
+                                                                 int(n_regions), int(shared), int(self._nt_store(S))]
+
+    def _nt_store(self, S: int) -> bool:
+        """Non-temporal pass-output stores once a pass's states (S x 2^n x 4 bytes) outgrow half the 256 MB Infinity
+        Cache: 16q x 2048 samples (512 MB) 1.820 -> 1.784 ms per step, while 8 clients' 64 MB are re-read faster from
+        the cache with plain stores (profiles/r6_tile_nt_priority_ab.txt).  QFEDX_HEA_NT=0 / 1 overrides."""
+        env = os.environ.get("QFEDX_HEA_NT")
+        if env is not None:
+            return env == "1"
+        return S * (4 << self.n) > NT_STORE_MIN_BYTES
 
     def _frags(self, params: torch.Tensor, K: int, tag: str = "") -> torch.Tensor:
         fr = self._buf(f"{tag}frags", max(K * self.n_slots * 4 * 128 * 4, 1), torch.int32)
