@@ -239,7 +239,7 @@ def main():
             "graph_comm": graph_comm,
             # CC4: round r + 1's upload + minibatch gather on a side stream against round r's graph + collective
             # (on with more than one rank; QFEDX_CC4 overrides)
-            "cc4_overlap": bool(getattr(runner, "cc4", False)),
+            "cc4_overlap": bool(getattr(runner.adapter.trainer, "cc4", False)),
             # MFMA engine tiling: forward / adjoint tile bits (2^13 forward tiles for small per-rank batches)
             "mfma_tiles": ([int(runner.adapter.engine.hip.tile_bits), int(runner.adapter.engine.hip.adj_tile_bits)]
                            if mfma else None),

@@ -130,9 +130,12 @@ class RuntimeConfig:
     use_graphs: bool = True            # hipGraph capture of the local round (HIP backend)
     graph_comm: bool = True            # capture the round's all-reduce + apply into that graph (RCCL / no group)
     # CC4: with more than one rank, round r + 1's theta-independent inputs (setup, minibatch plan, tables, gather +
-    # encode; on the HIP graph path the upload + gather kernels on a side stream) are built while round r's
-    # collective is in flight.  Bitwise the same rounds; QFEDX_CC4=0 / 1 overrides (1 also at one rank, for tests)
+    # encode) are built while round r's collective is in flight (gloo: async all-reduce).  overlap_comm_device: the
+    # graphed HIP round's upload + gather on a side stream against the previous round's graph + collective - bitwise
+    # the same, but the cross-queue join costs +12-15 us per round at one RCCL rank against a ~5 us gather
+    # (profiles/r6_cc4_overlap.txt), so it is opt-in.  QFEDX_CC4=0 / 1 overrides both (1 also at one rank, for tests)
     overlap_comm: bool = True
+    overlap_comm_device: bool = False
     timer_every: int = 0               # time the GPU phases every N-th round (0: 16 on GPU, every round on CPU)
     log_client_norms: bool = False     # NON-PRIVATE debug diagnostic (DP rounds): every client's raw pre-clip update
                                        # norm reaches every rank in the round all-reduce (CC6) and clip fraction +

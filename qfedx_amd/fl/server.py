@@ -149,7 +149,9 @@ class FederatedRunner:
         cc4_env = os.environ.get("QFEDX_CC4")
         self.cc4 = (cc4_env == "1") or (cc4_env is None and world.distributed and
                                         bool(getattr(cfg.runtime, "overlap_comm", True)))
-        adapter.trainer.cc4 = self.cc4          # the graphed HIP round's side-stream upload + gather
+        # the graphed HIP round's side-stream upload + gather (opt-in: see RuntimeConfig.overlap_comm_device)
+        adapter.trainer.cc4 = (cc4_env == "1") or (cc4_env is None and world.distributed and
+                                                   bool(getattr(cfg.runtime, "overlap_comm_device", False)))
         self.graph_comm_mode = ("captured" if self.graph_comm else "eager") if backend == "hip" else "none"
 
     # ------------------------------------------------------------------ eval
