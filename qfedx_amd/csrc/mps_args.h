@@ -15,3 +15,22 @@ struct QfxMpsArgs {
   int x_stride, t_stride, spc, S, n, L, feature, C, qmax;
   int readout[QFX_MPS_RMAX];
 };
+
+// Launch arguments of the generic MPO-product MPS kernel (csrc/mps_mpo.hip; tables: quantum/mps_mpo.py).
+constexpr int QFX_MPO_DMAX = 16;       // max bond (4 two-qubit gates across any cut)
+constexpr int QFX_MPO_MAXPG = 64;      // max parametric rotations on one qubit
+
+struct QfxMpoArgs {
+  const float* ang;            // [S][G] gate angles (gate_angles of the lowered program)
+  const int* gkind;            // [G] gate kinds (quantum/circuit.py KIND)
+  const int* events;           // per-qubit event lists (mps_mpo.compile_mpo)
+  const int* sinfo;            // [n][8] (event offset, count, pass-through pairs, their count, rotations, 0, 0, 0)
+  const int* nbits;            // [n - 1] bond bits of every cut
+  const float* w;              // [S][C] dL/d<Z_c> (gradient mode) or nullptr
+  float* z;                    // [S][C]
+  float* dang;                 // [S][G] dL/d(angle) of RX / RY / RZ / P gates (gradient mode; others untouched)
+  float* rp;                   // scratch, complex [S][n][256]: right environments R_{q+1}
+  float* ro;                   // scratch, complex [S][qmax + 1][256]: RO_{q+1} (gradient mode)
+  int S, G, n, C, qmax;
+  int readout[QFX_MPS_RMAX];
+};

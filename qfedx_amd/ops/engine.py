@@ -196,6 +196,9 @@ class VQCEngine:
             return self._readout(z, readout_keys, step)
         if self.mps_hip is not None and init is None:
             return self._readout(self.mps_hip.expz(xang, theta), readout_keys, step)
+        if self.backend == "mps" and init is None:
+            z = self.prog.expz_rows(self._rows(xang, theta), self.spec.readout).reshape(K, B, -1).float()
+            return self._readout(z, readout_keys, step)
         psi = self.prog.run(self._rows(xang, theta), state=self._init_rows(init))
         z = self.prog.expz(psi, self.spec.readout).reshape(K, B, -1).float()
         return self._readout(z, readout_keys, step)

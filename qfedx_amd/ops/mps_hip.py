@@ -1,8 +1,11 @@
-"""HIP fast path of the MPS backend for the CNOT-chain VQC (csrc/mps_chain.hip; math: quantum/mps_chain.py).
+"""HIP paths of the MPS backend.
 
-``VQCEngine(backend="mps")`` routes <Z> and adjoint gradients here on a GPU when ``mps_chain.eligible(spec)`` (the
-angle-encoded RX/RZ + CNOT-chain ansatz with <= 3 layers: exact bond 2^L <= 8, any qubit count); the generic
-einsum-network MPS (``quantum/mps.py``) stays the path for every other circuit and on the CPU."""
+* ``MpsChainProgram`` (csrc/mps_chain.hip; math: quantum/mps_chain.py): ``VQCEngine(backend="mps")`` routes <Z> and
+  adjoint gradients here on a GPU when ``mps_chain.eligible(spec)`` (the angle-encoded RX/RZ + CNOT-chain ansatz with
+  <= 3 layers: exact bond 2^L <= 8, any qubit count).
+* ``MpsMpoProgram`` (csrc/mps_mpo.hip; tables: quantum/mps_mpo.py): any other lowered circuit whose MPO bonds stay
+  <= 16 without recompression - ``MPSProgram.expz_vjp`` / ``expz_rows`` use it on the GPU.
+The einsum-network MPS (``quantum/mps.py``) stays the path for truncating circuits and on the CPU."""
 from __future__ import annotations
 
 import torch
@@ -58,3 +61,65 @@ class MpsChainProgram:
         """d/dtheta of sum_{b, c} w[k, b, c] <Z_c>_{k, b}: [K, n_theta] (per-sample gradients summed over each
         client's samples in order)."""
         return self._run(xang, theta, w)[1].sum(1)
+
+
+class MpsMpoProgram:
+    """HIP contraction (csrc/mps_mpo.hip) of an ``MPSProgram`` that is never recompressed (``autograd_ok``) and
+    whose cuts carry at most 4 two-qubit gates (bond <= 16): any 1-qubit gate kinds, CX / CZ at any distance - the
+    ring / all-to-all / custom circuits the chain kernel does not cover.  One workgroup per sample builds each
+    qubit's tensor from its event list (``quantum/mps_mpo.py``) and runs the transfer-environment sweeps; the
+    gradient launch pulls dL/d<Z> back to every rotation angle.  Replaces the einsum network's ~10 small batched
+    GEMMs per gate (and their autograd tape) on the GPU; the CPU keeps the einsum network."""
+
+    def __init__(self, prog):
+        from ..quantum.mps_mpo import ROTATIONS, compile_mpo
+        self.n = prog.n
+        self.G = len(prog.ops_list)
+        self.device = prog.device
+        self.tab_host = compile_mpo(prog.ops_list, prog.n)
+        self.tab = {k: v.to(self.device) for k, v in self.tab_host.items()}
+        # dL/d(angle) is reported for the slot-carrying rotations, as MPSProgram.expz_vjp masks its AD gradient
+        self.mask = torch.tensor([s >= 0 and k in ROTATIONS for k, _, _, s in prog.ops_list], device=self.device)
+        self._ws = {}
+        self.launches = 0
+
+    @staticmethod
+    def eligible(prog) -> bool:
+        from ..quantum.mps_mpo import compile_mpo
+        if prog.device.type != "cuda" or prog.dtype != torch.complex64 or not prog.autograd_ok or prog.n < 2:
+            return False
+        try:
+            compile_mpo(prog.ops_list, prog.n)
+        except ValueError:
+            return False
+        return True
+
+    def _buf(self, name, numel):
+        t = self._ws.get(name)
+        if t is None or t.numel() < numel:
+            t = torch.empty(numel, dtype=torch.float32, device=self.device)
+            self._ws[name] = t
+        return t[:numel]
+
+    def run(self, ang: torch.Tensor, readout, w=None):
+        """ang [S, G] gate angles -> (<Z_c> [S, C], dL/d(angle) [S, G] masked to rotations, or None without w)."""
+        ro = [int(q) for q in readout]
+        if not 1 <= len(ro) <= 8:
+            raise ValueError("the MPO kernel reads out 1..8 qubits")
+        ang = ang.float().contiguous()
+        S = ang.shape[0]
+        if ang.shape[1] != self.G:
+            raise ValueError(f"angles [S, {ang.shape[1]}] for a {self.G}-gate program")
+        z = torch.empty(S, len(ro), dtype=torch.float32, device=self.device)
+        t, h = self.tab, self.tab_host
+        rp = self._buf("rp", S * self.n * 512)
+        self.launches += 1
+        if w is None:
+            ext().mps_mpo(ang, t["gkind"], t["events"], t["sinfo"], t["nbits"], h["sinfo"], h["nbits"], ro, _EMPTY,
+                          z, _EMPTY, rp, _EMPTY)
+            return z, None
+        dang = torch.zeros(S, self.G, dtype=torch.float32, device=self.device)
+        rob = self._buf("ro", S * (max(ro) + 1) * 512)
+        ext().mps_mpo(ang, t["gkind"], t["events"], t["sinfo"], t["nbits"], h["sinfo"], h["nbits"], ro,
+                      w.reshape(S, len(ro)).float().contiguous(), z, dang, rp, rob)
+        return z, torch.where(self.mask, dang, torch.zeros_like(dang))

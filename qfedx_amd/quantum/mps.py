@@ -352,12 +352,43 @@ class MPSProgram:
             return self.param_shift_grads(params, w, readout, init=init)
         return self.expz_vjp(params, readout)[1](w)
 
+    def hip_program(self):
+        """The HIP contraction of this program (``ops/mps_hip.MpsMpoProgram``: complex64 on a GPU, never
+        recompressed, bond <= 16), or None (einsum network)."""
+        if "_hip" not in self.__dict__:
+            self._hip = None
+            if self.device.type == "cuda":
+                from ..ops.mps_hip import MpsMpoProgram
+                if MpsMpoProgram.eligible(self):
+                    self._hip = MpsMpoProgram(self)
+        return self._hip
+
+    @torch.no_grad()
+    def expz_rows(self, params: torch.Tensor, readout) -> torch.Tensor:
+        """<Z_c> [B, C] of the program on parameter rows, from |0..0> (HIP kernel when ``hip_program``)."""
+        hip = self.hip_program()
+        if hip is not None:
+            return hip.run(self.angles(params), readout)[0].to(self.rdtype)
+        return self.expz(self.run(params), readout)
+
     def expz_vjp(self, params: torch.Tensor, readout):
         """One recorded forward: -> (<Z> [B, C] detached, back(w) -> dL/d(angle_g) [B, G]).  A training step
         computes dL/d<Z> from the returned readout and pulls it back through the same network, so the MPS
-        is contracted once per step (requires ``autograd_ok``: no QR/SVD in the graph)."""
+        is contracted once per step (requires ``autograd_ok``: no QR/SVD in the graph).  On a GPU with
+        ``hip_program``: the <Z> launch, and ``back`` is the gradient launch (csrc/mps_mpo.hip)."""
         if not self.autograd_ok:
             raise RuntimeError("expz_vjp needs a program whose raw MPO bond fits chi_max")
+        hip = self.hip_program()
+        if hip is not None:
+            with torch.no_grad():
+                ang = self.angles(params)
+                z = hip.run(ang, readout)[0]
+
+            def back_hip(w: torch.Tensor) -> torch.Tensor:
+                with torch.no_grad():
+                    return hip.run(ang, readout, w)[1].to(self.rdtype)
+
+            return z.to(self.rdtype), back_hip
         with torch.enable_grad():
             ang = self.angles(params).detach().requires_grad_(True)
             z = self.expz(self.run(params, ang=ang), readout)

@@ -73,6 +73,10 @@ class Simulator:
         v = self._rows(values)
         S = v.shape[0]
         init = None if initial_state is None else torch.as_tensor(initial_state).to(self.device, torch.complex64)
+        if self.backend == "mps" and init is None and self.prog.autograd_ok and self.prog.hip_program() is not None:
+            z, back = self.prog.expz_vjp(v, self.readout)        # HIP contraction (csrc/mps_mpo.hip)
+            g = slot_grads(back(w), torch.from_numpy(self.ops), torch.from_numpy(self.coef), self.n_slots).float()
+            return z.float(), g
         if self.backend == "mps":
             st = self.prog.run(v, state=init)
             return st, self.prog.expz(st, self.readout).float()
@@ -96,6 +100,10 @@ class Simulator:
             x = torch.zeros(S, 1, 1, device=self.device)
             return self.prog.vjp(x, v, w, init)
         from ..ops.statevec_torch import slot_grads
+        if self.backend == "mps" and init is None and self.prog.autograd_ok and self.prog.hip_program() is not None:
+            z, back = self.prog.expz_vjp(v, self.readout)        # HIP contraction (csrc/mps_mpo.hip)
+            g = slot_grads(back(w), torch.from_numpy(self.ops), torch.from_numpy(self.coef), self.n_slots).float()
+            return z.float(), g
         if self.backend == "mps":
             st = self.prog.run(v, state=init)
             z = self.prog.expz(st, self.readout).float()
