@@ -153,6 +153,11 @@ def main():
                 rec["dtype_note"] = ("BASELINE config 2 names bf16 state storage; the fp16 MFMA engine stores "
                                      "fp16 amplitudes (11-bit significand vs bf16's 8), so the substitution is more "
                                      "precise, not less: see max_abs_err_* against the fp32 engine")
+        if kind == "tinycnn" and backend == "hip":
+            from qfedx_amd.ops.cnn_hip import precision_check as cnn_precision
+            rec.update(cnn_precision(cfg.model.n_classes, device))   # untimed: kernels vs float64 autograd
+            rec["dtype"] = ("fp32 (conv2 forward as a 3-term fp16 split on v_mfma_f32_16x16x32_f16 with fp32 "
+                            "accumulation; every other product on v_mfma_f32_16x16x4_f32)")
         if t.grad_method == "param_shift" and eng is not None and hasattr(eng.hip, "shift_pass_counts"):
             # pass launches per sample of one gradient: naive shifted circuits vs prefix reuse + pi identity
             rec["param_shift"] = dict(eng.hip.shift_pass_counts(), reuse=bool(eng.ps_reuse))

@@ -154,11 +154,34 @@ __device__ __forceinline__ float relu_pool(f4 acc, float bias, int& arg) {
 //          w/2's last m-tile (window 48); the two halves are summed in fixed order afterwards.
 // --------------------------------------------------------------------------------------------
 constexpr int FSG = 4;             // samples per forward workgroup
-constexpr int CSF = 336;           // LDS stride of one padded 18x18 pool1 map (== 16 mod 32, see fwd_win)
-constexpr int W2F = 402;           // LDS stride of W2 reordered as w2f[o][tap*16 + ci] (== 18 mod 32)
 constexpr int IRF = 46;            // LDS row stride of a padded forward image (32 used): conv1's A reads of 4
                                    // windows x 2 rows x 2 taps average 1.19-way vs 2.24-way at stride 32
 static_assert(FSG * 2 == NW, "conv2 partial m-tile: one (sample, half) per wave");
+
+// conv2 runs on the fp16 matrix pipe at fp32-grade accuracy: every fp32 operand x is split into fp16 halves
+// hi = fp16(x), lo = fp16(x - hi) (22 significant bits) and each K = 32 slab takes three v_mfma_f32_16x16x32_f16
+// (hi.hi + hi.lo + lo.hi; lo.lo is below the split's own 2^-22) with fp32 accumulation - 48 MFMA cycles where the
+// fp32 pipe (v_mfma_f32_16x16x4_f32) needed 256.  W2 is scaled by 2^8 before the split (its 0.05-scale lo halves
+// would sit in fp16's subnormal range) and the accumulators by 2^-8 after (exact).  CPU emulation of the split on
+// TinyCNN conv2 (max |err| / max |y| against float64): 1.30e-6 vs 0.97e-6 for fp32 (3 x bf16: 6.9e-6).
+//   K ordered (tap, ci), 13 slabs of 2 taps x 16 channels (tap 25 is zero): lane group g = lane / 16 supplies
+//   k = 8 g .. 8 g + 7 = tap 2 slab + g / 2, channels 8 (g & 1) .. + 7 - one 16-byte chunk of a position record.
+constexpr int NPOS = P1P * P1P;    // positions of the zero-padded 18 x 18 pool1 map
+constexpr int PRQ = 4;             // 16-byte chunks per position record: hi ci 0-7 | hi ci 8-15 | lo ci 0-7 | lo 8-15
+constexpr int W2Q = 106;           // chunks per output channel of the split W2 image (26 taps x 4 + 2 pad: the 16
+                                   // lanes of a ds_read_b128 group land on distinct 16-byte bank slots)
+constexpr int NSL = 13;            // K slabs
+constexpr float SW2 = 256.f;       // W2 scale before the split (power of two, undone on the accumulators)
+
+// pool1 record chunk c of position pos sits at chunk c ^ h(pos): with the fwd_win row order the 16 rows of an
+// m-tile have distinct pos mod 16, and this XOR puts each 16-lane ds_read_b128 group on distinct bank slots
+// (exhaustive check over tiles, taps and lane groups: 1.08-way on average, from 2-way unswizzled)
+__device__ __forceinline__ int p1_chunk(int pos, int c) { return c ^ ((pos ^ (pos >> 1)) & 3); }
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f4 mfma_h(uint4 a, uint4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+}
 
 // conv2 (forward) m-tile slot (tile * 4 + j, slot 48 = the partial tile) -> pooled window wy * 7 + wx.  A 32-lane
 // half of an A read touches 4 windows x 4 positions of two channels CSF apart: with window origins o = 36 wy + 2 wx,
@@ -205,51 +228,66 @@ __device__ __forceinline__ void stage_w2(const float* __restrict__ w2g, float* d
 
 template <int NM>
 struct Fwd2Set {
-  float a[NM][4], b[2][4];
+  uint4 ah[NM], al[NM], bh[2], bl[2];
 };
 
+// conv2 over slabs [c0, c1) for NM m-tiles of one sample: apos = each m-tile row's window position (lane row i),
+// p1 = the sample's position records, w2 = lane column i's W2 chunks (+ 16 W2Q for the second n-tile)
 template <int NM>
-__device__ __forceinline__ void fwd_conv2(const float* sm, const int (&aoff)[NM], int boff, int r0, int r1,
-                                          f4 (&acc)[NM][2]) {
+__device__ __forceinline__ void fwd_conv2(const uint4* p1, const int (&apos)[NM], const uint4* w2, int g, int c0,
+                                          int c1, f4 (&acc)[NM][2]) {
+  const int tpar = g >> 1, ch = g & 1;
   pipelined<Fwd2Set<NM>>(
-      r0, r1,
-      [&](int r, Fwd2Set<NM>& st) {
-        const float* bp = sm + boff + r * 16;
+      c0, c1,
+      [&](int sl, Fwd2Set<NM>& st) {
+        const int tap = 2 * sl + tpar;
+        const uint4* bp = w2 + tap * PRQ + ch;
 #pragma unroll
-        for (int cq = 0; cq < 4; ++cq) {
-          st.b[0][cq] = bp[4 * cq];
-          st.b[1][cq] = bp[16 * W2F + 4 * cq];
+        for (int h = 0; h < 2; ++h) {
+          st.bh[h] = bp[h * 16 * W2Q];
+          st.bl[h] = bp[h * 16 * W2Q + 2];
         }
-        const int ro = tap_off(r);
+        const int ro = tap_off(min(tap, K1 - 1));   // tap 25 has zero weights: any in-range position
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          const float* ap = sm + (aoff[m] + ro);
-#pragma unroll
-          for (int cq = 0; cq < 4; ++cq) st.a[m][cq] = ap[4 * cq * CSF];
+          const int pos = apos[m] + ro;
+          const uint4* rec = p1 + pos * PRQ;
+          st.ah[m] = rec[p1_chunk(pos, ch)];
+          st.al[m] = rec[p1_chunk(pos, 2 + ch)];
         }
       },
       [&](const Fwd2Set<NM>& st) {
 #pragma unroll
-        for (int cq = 0; cq < 4; ++cq)
+        for (int m = 0; m < NM; ++m)
 #pragma unroll
-          for (int m = 0; m < NM; ++m)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) acc[m][h] = mfma(st.a[m][cq], st.b[h][cq], acc[m][h]);
+          for (int h = 0; h < 2; ++h) {
+            acc[m][h] = mfma_h(st.ah[m], st.bh[h], acc[m][h]);
+            acc[m][h] = mfma_h(st.ah[m], st.bl[h], acc[m][h]);
+            acc[m][h] = mfma_h(st.al[m], st.bh[h], acc[m][h]);
+          }
       });
 }
+
+// LDS of cnn_fwd (bytes, 16-byte aligned pieces): pool1 records | (images during conv1, then the split W2) | W1 |
+// b1 | b2 | window-48 partials
+constexpr int FWD_P1_B = FSG * NPOS * PRQ * 16;
+constexpr int FWD_U_B = (C2 * W2Q * 16 > FSG * IMGP * IRF * 4) ? C2 * W2Q * 16 : FSG * IMGP * IRF * 4;
+constexpr int FWD_LDS = FWD_P1_B + FWD_U_B + (C1 * K1P + C1 + C2 + FSG * 2 * C2 * 4) * 4;
+static_assert(FWD_LDS <= 160 * 1024, "cnn_fwd LDS");
 
 __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const float* __restrict__ params,
                                               int P, int B, int G, CnnOff off, float* __restrict__ pool1,
                                               uint8_t* __restrict__ am1, float* __restrict__ pool2,
                                               uint8_t* __restrict__ am2) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* w2f = sm;                          // [32][402]: w2f[o][tap*16 + ci] = W2[o][ci][tap]
-  float* w1s = w2f + C2 * W2F;              // [16][28]  (tap >= 25 zero)
-  float* b1s = w1s + C1 * K1P;              // [16]
-  float* b2s = b1s + C1;                    // [32]
-  float* img = b2s + C2;                    // [FSG][32*32] zero-padded images
-  float* p1s = img + FSG * IMGP * IRF;      // [FSG][16][CSF] zero-padded pool1
-  float* red = img;                         // [FSG][2 halves][32 o][4]: window-48 partials (images dead)
+  uint4* p1q = reinterpret_cast<uint4*>(sm);                          // [FSG][324][4] split pool1 records
+  char* ub = reinterpret_cast<char*>(sm) + FWD_P1_B;
+  float* img = reinterpret_cast<float*>(ub);                          // [FSG][32][46] zero-padded images (conv1)
+  uint4* w2q = reinterpret_cast<uint4*>(ub);                          // [32][106] split W2 chunks (conv2)
+  float* w1s = reinterpret_cast<float*>(ub + FWD_U_B);                // [16][28]  (tap >= 25 zero)
+  float* b1s = w1s + C1 * K1P;                                        // [16]
+  float* b2s = b1s + C1;                                              // [32]
+  float* red = b2s + C2;                                              // [FSG][2 halves][32 o][4]: window-48 partials
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -259,7 +297,15 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
   const float* prow = params + (size_t)k * P;
   const int i = lane & 15, kq = lane >> 4;
 
-  stage_w2(prow + off.w2, w2f, W2F, 1, 16, tid);   // w2f[o][tap*16 + ci]
+  // W2 loads are issued now and land in registers behind conv1; they are split into the image region once conv1
+  // has consumed the images
+  constexpr int NU2 = (C2 * K2 + NT - 1) / NT;
+  float w2v[NU2];
+#pragma unroll
+  for (int u = 0; u < NU2; ++u) {
+    const int e = tid + u * NT;
+    if (e < C2 * K2) w2v[u] = prow[off.w2 + e];
+  }
   for (int e = tid; e < C1 * K1P; e += NT) {
     const int o = e / K1P, kk = e - o * K1P;
     w1s[e] = kk < K1 ? prow[off.w1 + o * K1 + kk] : 0.f;
@@ -282,10 +328,11 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
       img[(e >> 10) * IMGP * IRF + (r >> 5) * IRF + (r & 31)] = v[u];
     }
   }
-  for (int e = tid; e < FSG * C1 * CSF; e += NT) p1s[e] = 0.f;
+  for (int e = tid; e < FSG * NPOS * PRQ; e += NT) p1q[e] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
 
-  // ---- conv1
+  // ---- conv1 (fp32 MFMA, K = 28): pooled outputs to global and, split, into the pool1 records
+  _Float16* p1h = reinterpret_cast<_Float16*>(p1q);
   {
     float bw[K1P / 4];
     int toff[K1P / 4];
@@ -298,18 +345,18 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
     const int nu = ns * 49;
     for (int u = wave; u < nu; u += 2 * NW) {
       const int u1 = u + NW < nu ? u + NW : u;
-      int ub[2];
+      int ubs[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int uu = h ? u1 : u, s = uu / 49, mt = uu - s * 49;
         const int w = mt * 4 + (i >> 2), pos = i & 3;
-        ub[h] = s * IMGP * IRF + (2 * (w / Q1) + (pos >> 1)) * IRF + 2 * (w % Q1) + (pos & 1);
+        ubs[h] = s * IMGP * IRF + (2 * (w / Q1) + (pos >> 1)) * IRF + 2 * (w % Q1) + (pos & 1);
       }
       float av[2][K1P / 4];
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int ks = 0; ks < K1P / 4; ++ks) av[h][ks] = img[ub[h] + toff[ks]];
+        for (int ks = 0; ks < K1P / 4; ++ks) av[h][ks] = img[ubs[h] + toff[ks]];
       f4 acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
       for (int ks = 0; ks < K1P / 4; ++ks)
@@ -326,23 +373,46 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
         const size_t so = ((size_t)k * B + s0 + s) * C1 * Q1 * Q1 + o * Q1 * Q1 + wo;
         pool1[so] = best;
         am1[so] = (uint8_t)arg;
-        p1s[s * C1 * CSF + o * CSF + (wo / Q1 + 2) * P1P + (wo % Q1) + 2] = best;
+        const int pos = (wo / Q1 + 2) * P1P + (wo % Q1) + 2;
+        const _Float16 hi = (_Float16)best, lo = (_Float16)(best - (float)hi);
+        _Float16* rec = p1h + (size_t)(s * NPOS + pos) * PRQ * 8 + (o & 7);
+        rec[8 * p1_chunk(pos, o >> 3)] = hi;
+        rec[8 * p1_chunk(pos, 2 + (o >> 3))] = lo;
       }
     }
+  }
+  __syncthreads();   // images consumed: the region takes the split W2
+
+  {
+    _Float16* w2h = reinterpret_cast<_Float16*>(w2q);
+#pragma unroll
+    for (int u = 0; u < NU2; ++u) {
+      const int e = tid + u * NT;
+      if (e < C2 * K2) {
+        const int o = e / K2, rem = e - o * K2, ci = rem / 25, tap = rem - ci * 25;
+        const float x = w2v[u] * SW2;
+        const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
+        _Float16* rec = w2h + (size_t)(o * W2Q + tap * PRQ) * 8 + (ci & 7);
+        rec[8 * (ci >> 3)] = hi;
+        rec[8 * (2 + (ci >> 3))] = lo;
+      }
+    }
+    if (tid < C2 * PRQ) w2q[(tid >> 2) * W2Q + (K1 * PRQ) + (tid & 3)] = make_uint4(0u, 0u, 0u, 0u);   // tap 25
   }
   __syncthreads();
 
   // ---- conv2: full m-tiles
-  const int boff = (int)(w2f - sm) + i * W2F + kq;
+  const uint4* w2l = w2q + i * W2Q;
+  constexpr float USC = 1.f / SW2;
 #pragma unroll 1
   for (int gq = 0; gq < 2; ++gq) {
     const int u = 6 * wave + 3 * gq, s = u / 12, mt0 = u - s * 12;
     if (s >= ns) break;
-    int aoff[3];
+    int apos[3];
 #pragma unroll
-    for (int m = 0; m < 3; ++m) aoff[m] = (int)(p1s - sm) + (s * C1 + kq) * CSF + fwd_q2((mt0 + m) * 16 + i);
+    for (int m = 0; m < 3; ++m) apos[m] = fwd_q2((mt0 + m) * 16 + i);
     f4 acc[3][2] = {};
-    fwd_conv2<3>(sm, aoff, boff, 0, 25, acc);
+    fwd_conv2<3>(p1q + s * NPOS * PRQ, apos, w2l, kq, 0, NSL, acc);
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
       const int wo = fwd_win((mt0 + m) * 4 + kq);
@@ -350,22 +420,22 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
       for (int h = 0; h < 2; ++h) {
         const int o = h * 16 + i;
         int arg;
-        const float best = relu_pool(acc[m][h], b2s[o], arg);
+        const float best = relu_pool(acc[m][h] * USC, b2s[o], arg);
         const size_t so = ((size_t)k * B + s0 + s) * C2 * Q2 * Q2 + o * Q2 * Q2 + wo;
         pool2[so] = best;
         am2[so] = (uint8_t)arg;
       }
     }
   }
-  // ---- conv2: window 48 (m-tile 12), half of the taps per wave
+  // ---- conv2: window 48 (m-tile 12), half of the slabs per wave
   {
     const int s = wave >> 1, half = wave & 1;
     f4 acc[1][2] = {};
     if (s < ns) {
-      const int aoff[1] = {(int)(p1s - sm) + (s * C1 + kq) * CSF + fwd_q2(12 * 16 + i)};
-      fwd_conv2<1>(sm, aoff, boff, half ? 13 : 0, half ? 25 : 13, acc);
+      const int apos[1] = {fwd_q2(12 * 16 + i)};
+      fwd_conv2<1>(p1q + s * NPOS * PRQ, apos, w2l, kq, half ? 7 : 0, half ? NSL : 7, acc);
     }
-    if (s < ns && kq == 0) {   // red aliases the images, dead since conv1
+    if (s < ns && kq == 0) {
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -377,7 +447,7 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
     const int s = tid / C2, o = tid - s * C2;
     f4 v;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = red[((s * 2) * C2 + o) * 4 + r] + red[((s * 2 + 1) * C2 + o) * 4 + r];
+    for (int r = 0; r < 4; ++r) v[r] = (red[((s * 2) * C2 + o) * 4 + r] + red[((s * 2 + 1) * C2 + o) * 4 + r]) * USC;
     int arg;
     const float best = relu_pool(v, b2s[o], arg);
     const size_t so = ((size_t)k * B + s0 + s) * C2 * Q2 * Q2 + o * Q2 * Q2 + fwd_win(Q2 * Q2 - 1);
@@ -1100,10 +1170,7 @@ __global__ void __launch_bounds__(256) cnn_eval_head(const float* __restrict__ h
   }
 }
 
-static_assert((C2 * W2F + C1 * K1P + C1 + C2 + FSG * IMGP * IRF + FSG * C1 * CSF) * 4 <= 160 * 1024, "cnn_fwd LDS");
-size_t fwd_lds() {
-  return (size_t)(C2 * W2F + C1 * K1P + C1 + C2 + FSG * IMGP * IRF + FSG * C1 * CSF) * 4;
-}
+size_t fwd_lds() { return (size_t)FWD_LDS; }
 size_t bwd_lds() {
   return (size_t)(C1 * W2R + (C2 + C1) * CS + 2 * C1 * DPS + 2 * IMGP * IMS + 256 + 256) * 4 + 2 * C1 * DPS;
 }

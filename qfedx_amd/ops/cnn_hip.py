@@ -130,3 +130,48 @@ class HipTinyCNN:
         part = self._buf("part", (K * G, C.cnn_partial_size()))
         C.cnn_backward(Xf, params, K, B, self.off_conv, pool1, am1, pool2, am2, dP2, part, grad, sk, hy)
         return {"loss": loss, "grad": grad if sgd is None else None, "correct": correct}
+
+
+def precision_check(num_classes: int, device, K: int = 16, B: int = 32, seed: int = 0) -> dict:
+    """Untimed evidence for the CFed kernels' arithmetic (bench_suite lines): logits and per-client gradients of
+    ``HipTinyCNN`` on K clients x B MNIST-like samples against float64 torch autograd, as max |error| / max |value|
+    (logits; each parameter tensor's gradient), and the same for float32 torch on the CPU - the fp32 yardstick."""
+    import torch.nn.functional as F
+    from ..models import tinycnn as tc
+    C = num_classes
+    g = torch.Generator().manual_seed(seed)
+    params = torch.stack([tc.init_flat(C, seed + k) for k in range(K)]) + 0.02 * torch.randn(K, tc.n_params(C),
+                                                                                              generator=g)
+    X = torch.rand(K, B, 1, 28, 28, generator=g)
+    X[X < 0.6] = 0.0
+    y = torch.randint(0, C, (K, B), generator=g)
+    w = torch.full((K, B), 1.0 / B)
+    mask = (torch.rand(K, B, 64, generator=g) >= 0.5).float() * 2.0
+
+    def ref(dtype):
+        p = params.to(dtype).clone().requires_grad_(True)
+        logits = tc.batched_forward(p, X.to(dtype), C, mask.to(dtype))
+        nll = F.cross_entropy(logits.reshape(-1, C), y.reshape(-1), reduction="none").reshape(K, B)
+        (nll * w.to(dtype)).sum().backward()
+        return logits.detach().double(), p.grad.double()
+
+    l64, g64 = ref(torch.float64)
+    l32, g32 = ref(torch.float32)
+    hip = HipTinyCNN(C, device)
+    dev = torch.device(device)
+    lh = hip.logits(params.to(dev), X.to(dev)).double().cpu()
+    # logits() runs without dropout; the gradient check uses the same dropout mask as the reference
+    lref = tc.batched_forward(params.double(), X.double(), C).detach()
+    r = hip.loss_and_grads(params.to(dev), X.to(dev), y.to(dev), w.to(dev), mask.to(dev))
+    gh = r["grad"].double().cpu()
+    bounds = tc.layer_boundaries(C)
+
+    def grad_err(gx):
+        return max(float((gx[:, a:b] - g64[:, a:b]).abs().max() / g64[:, a:b].abs().max().clamp_min(1e-30))
+                   for a, b in zip(bounds[:-1], bounds[1:]))
+
+    return {"max_rel_err_logits": float((lh - lref).abs().max() / lref.abs().max()),
+            "max_rel_err_grad": grad_err(gh),
+            "fp32_torch_max_rel_err_logits": float((l32 - l64).abs().max() / l64.abs().max()),
+            "fp32_torch_max_rel_err_grad": grad_err(g32),
+            "precision_ref": "float64 torch autograd", "precision_samples": K * B}
