@@ -204,28 +204,6 @@ __device__ __forceinline__ int fwd_q2(int row) {
   return (2 * (w / Q2) + (pos >> 1)) * P1P + 2 * (w % Q2) + (pos & 1);
 }
 
-// W2 [o][ci][tap] of one client row -> LDS at dst[o*so + ci*sc + tap*st]: all 25 loads of a thread are issued
-// before any store (a plain strided loop waits on each load in turn: one workgroup per CU hides nothing)
-// (PERM: channel o goes to column 4 (o % 8) + o / 8, the dgrad B layout of cnn_bwd)
-template <bool PERM = false>
-__device__ __forceinline__ void stage_w2(const float* __restrict__ w2g, float* dst, int so, int sc, int st, int tid) {
-  constexpr int NU = (C2 * K2 + NT - 1) / NT;
-  float v[NU];
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    const int e = tid + u * NT;
-    if (e < C2 * K2) v[u] = w2g[e];
-  }
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    const int e = tid + u * NT;
-    if (e < C2 * K2) {
-      const int o = e / K2, rem = e - o * K2, ci = rem / 25, r = rem - ci * 25;
-      dst[(PERM ? 4 * (o & 7) + (o >> 3) : o) * so + ci * sc + r * st] = v[u];
-    }
-  }
-}
-
 template <int NM>
 struct Fwd2Set {
   uint4 ah[NM], al[NM], bh[2], bl[2];
@@ -465,7 +443,9 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
 //   conv2 wgrad  D[o][(tap, ci)] = sum_p dC2[o][p] P1pad[ci][q(p) + off(tap)]    M=32  N=26x16 K=196
 //                n-tile = one tap (lane = ci), plus a 26th "ones" n-tile that yields db2
 //   conv2 dgrad  D[p][ci] = sum_{tap,o} dC2pad[o][rb(p) - off(tap)] W2[o][ci][tap] M=196 N=16    K=25x32
-//                K ordered (tap, o): the tap offset is wave-uniform, o runs over immediate offsets
+//                on the fp16 pipe like the forward conv2: one K = 32 slab per tap (k = o), dC2 staged as split
+//                channel-minor position records with a per-sample power-of-two scale, W2 as split (ci, tap)
+//                records scaled by 2^8; the wgrad rebuilds its dC2 operand from the same records (hi + lo)
 //   conv1 wgrad  D[o][tap] = sum_p dC1[o][p] img[p + off1(tap)]                    M=16  N=32    K=784
 //                tap 25 is a ones column (db1); taps 26..31 are discarded
 // Work split (MFMA count per SIMD balanced; waves w and w+4 share a SIMD): wave w<4 owns dgrad
@@ -477,7 +457,26 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
 constexpr int BS_MAX = 16;         // samples per backward workgroup, at most (bwd_bs)
 constexpr int CS = 338;            // LDS stride of one zero-padded 18x18 map (== 18 mod 32: channel-strided
                                    // ds_read_b32 lanes land on distinct banks)
-constexpr int W2R = 802;           // LDS stride of W2 reordered as w2r[ci][tap*32 + o]
+constexpr int DRQ = 8;             // 16-byte chunks per dC2 position record / split W2 (ci, tap) record:
+                                   // hi o 0-7 | hi o 8-15 | hi o 16-23 | hi o 24-31 | lo o 0-7 | ... | lo o 24-31
+constexpr int W2B = 202;           // chunks per input channel of the split W2 image (25 taps x 8 + 2 pad: the 16
+                                   // lanes of a ds_read_b128 group land on distinct 16-byte bank slots)
+// dC2 record chunk c of position pos sits at chunk c ^ (pos & 7): conflict-free b128 dgrad A reads for every m-tile,
+// tap and lane group (exhaustive check; 4.3-way on average unswizzled)
+__device__ __forceinline__ int dc_chunk(int pos, int c) { return c ^ (pos & 7); }
+// Power-of-two scale of one sample's dC2 for the fp16 split: the largest |value| lands in [2^14, 2^15)
+// (conv-stack gradients are ~1e-5..1e-3: unscaled, their fp16 halves would be subnormal)
+__device__ __forceinline__ float dc_scale(float m) {
+  if (!(m > 0.f)) return 1.f;
+  int e;
+  (void)frexpf(m, &e);
+  return ldexpf(1.f, 15 - e);
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
 constexpr int DPS = 198;           // LDS stride of the dP1 / argmax1 rows
 constexpr int IMS = 37;            // LDS row stride of the padded image
 constexpr int NT2 = 26;            // conv2 wgrad n-tiles (25 taps + ones)
@@ -505,13 +504,17 @@ struct WgradSet {
   float a, b[NJ];
 };
 
+// A = dC2[o][p] (o = the lane's row) rebuilt from the split records: hi + lo (22 bits), times the sample's 1 / scale
 template <int NJ>
-__device__ __forceinline__ void bwd_wgrad2(const float* sm, int aoff, const int (&boff)[7], f4 (&acc)[7], int kq) {
+__device__ __forceinline__ void bwd_wgrad2(const float* sm, const _Float16* dch, int o, float inv, const int (&boff)[7],
+                                           f4 (&acc)[7], int kq) {
   pipelined<WgradSet<NJ>>(
       0, H2 * H2 / 4,
       [&](int ks, WgradSet<NJ>& st) {
         const int q = q14(ks * 4 + kq);
-        st.a = sm[aoff + q];
+        const int pos = q + 2 * P1P + 2;
+        const _Float16* rec = dch + pos * DRQ * 8 + (o & 7);
+        st.a = ((float)rec[8 * dc_chunk(pos, o >> 3)] + (float)rec[8 * dc_chunk(pos, 4 + (o >> 3))]) * inv;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) st.b[j] = sm[boff[j] + q];
       },
@@ -521,34 +524,38 @@ __device__ __forceinline__ void bwd_wgrad2(const float* sm, int aoff, const int 
       });
 }
 
-// conv2 dgrad of NM m-tiles over taps [r0, r1): two accumulator chains per m-tile (even / odd o-quads)
+// conv2 dgrad of NM m-tiles over taps [r0, r1) on the fp16 pipe: one K = 32 slab per tap (k = o), A = the split dC2
+// records at the row's position minus the tap offset, B = the lane column's (ci) split W2 record of the tap
 template <int NM>
 struct DgradSet {
-  float a[NM][8], b[8];
+  uint4 ah[NM], al[NM], bh, bl;
 };
 
 template <int NM>
-__device__ __forceinline__ void bwd_dgrad2(const float* sm, const int (&aoff)[NM], int boff, int r0, int r1,
-                                           f4 (&acc)[NM][2]) {
+__device__ __forceinline__ void bwd_dgrad2(const uint4* dcr, const int (&apos)[NM], const uint4* w2, int g, int r0,
+                                           int r1, f4 (&acc)[NM]) {
   pipelined<DgradSet<NM>>(
       r0, r1,
       [&](int r, DgradSet<NM>& st) {
+        const uint4* bp = w2 + r * DRQ;
+        st.bh = bp[g];
+        st.bl = bp[4 + g];
         const int ro = tap_off(r);
-        const float* bp = sm + boff + r * 32;
-#pragma unroll
-        for (int oc = 0; oc < 8; ++oc) st.b[oc] = bp[4 * oc];
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          const float* ap = sm + (aoff[m] - ro);
-#pragma unroll
-          for (int oc = 0; oc < 8; ++oc) st.a[m][oc] = ap[oc * CS];   // channel oc + 8 kq (kq in aoff)
+          const int pos = apos[m] - ro;
+          const uint4* rec = dcr + pos * DRQ;
+          st.ah[m] = rec[dc_chunk(pos, g)];
+          st.al[m] = rec[dc_chunk(pos, 4 + g)];
         }
       },
       [&](const DgradSet<NM>& st) {
 #pragma unroll
-        for (int oc = 0; oc < 8; ++oc)
-#pragma unroll
-          for (int m = 0; m < NM; ++m) acc[m][oc & 1] = mfma(st.a[m][oc], st.b[oc], acc[m][oc & 1]);
+        for (int m = 0; m < NM; ++m) {
+          acc[m] = mfma_h(st.ah[m], st.bh, acc[m]);
+          acc[m] = mfma_h(st.ah[m], st.bl, acc[m]);
+          acc[m] = mfma_h(st.al[m], st.bh, acc[m]);
+        }
       });
 }
 
@@ -601,19 +608,31 @@ struct BwdStage {
       if (e < IMG * IMG) im[j] = X[sidx * IMG * IMG + e];
     }
   }
-  // unpool2 (+ReLU mask) into padded dc2, pool1 -> padded p1s, argmax1, image
-  __device__ __forceinline__ void store(float* dc2, float* p1s, uint8_t* a1s, float* img, int tid) const {
+  // max |dC2| of this thread's windows (the sample's split scale)
+  __device__ __forceinline__ float maxabs(int tid) const {
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < ND; ++j)
+      if (tid + j * NT < C2 * Q2 * Q2 && pl2[j] > 0.f) m = fmaxf(m, fabsf(dp2[j]));
+    return m;
+  }
+  // unpool2 (+ReLU mask) into the padded split dC2 records (values x scale), pool1 -> padded p1s, argmax1, image
+  __device__ __forceinline__ void store(_Float16* dch, float scale, float* p1s, uint8_t* a1s, float* img, int tid) const {
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       const int e = tid + j * NT;
       if (e < C2 * Q2 * Q2) {
         const int o = e / (Q2 * Q2), w = e - o * Q2 * Q2, wy = w / Q2, wx = w - wy * Q2;
-        const float v = pl2[j] > 0.f ? dp2[j] : 0.f;
-        float* d = dc2 + o * CS + (2 * wy + 2) * P1P + 2 * wx + 2;
-        d[0] = am2[j] == 0 ? v : 0.f;
-        d[1] = am2[j] == 1 ? v : 0.f;
-        d[P1P] = am2[j] == 2 ? v : 0.f;
-        d[P1P + 1] = am2[j] == 3 ? v : 0.f;
+        const float v = pl2[j] > 0.f ? dp2[j] * scale : 0.f;
+        const _Float16 hi = (_Float16)v, lo = (_Float16)(v - (float)hi), z = (_Float16)0.f;
+        const int p0 = (2 * wy + 2) * P1P + 2 * wx + 2;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int pos = p0 + (c >> 1) * P1P + (c & 1);
+          _Float16* rec = dch + pos * DRQ * 8 + (o & 7);
+          rec[8 * dc_chunk(pos, o >> 3)] = am2[j] == c ? hi : z;
+          rec[8 * dc_chunk(pos, 4 + (o >> 3))] = am2[j] == c ? lo : z;
+        }
       }
     }
 #pragma unroll
@@ -639,16 +658,18 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
                                               const uint8_t* __restrict__ am2, const float* __restrict__ dP2,
                                               int bs, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* w2r = sm;                          // [16][802]: w2r[ci][tap*32 + 4 (o % 8) + o / 8] = W2[o][ci][tap]
-  float* dc2 = w2r + C1 * W2R;              // [32][338] padded dL/d conv2-output (post-unpool, ReLU-masked)
-  float* p1s = dc2 + C2 * CS;               // [16][338] padded pool1 (conv2 input)
+  uint4* w2b = reinterpret_cast<uint4*>(sm);                // [16][202] split W2: w2b[ci][tap * 8 + chunk(o)]
+  uint4* dcr = w2b + C1 * W2B;                              // [324][8] split padded dL/d conv2-output records
+  _Float16* dch = reinterpret_cast<_Float16*>(dcr);
+  float* p1s = reinterpret_cast<float*>(dcr + NPOS * DRQ);   // [16][338] padded pool1 (conv2 input)
   // conv1 wgrad of sample s runs during sample s+1's conv2 work: its inputs are double buffered (index s & 1)
   float* dp1b = p1s + C1 * CS;              // [2][16][198] dL/d pool1, ReLU-masked
   float* imgb = dp1b + 2 * C1 * DPS;        // [2][32][37]  padded images
   float* ones = imgb + 2 * IMGP * IMS;      // [256]     1.0 (bias columns)
   float* red12 = ones + 256;                // [4][64]   m-tile 12 partials of waves 4..7
-  uint8_t* a1sb = reinterpret_cast<uint8_t*>(red12 + 256);   // [2][16][198] argmax of pool1
-  float* red = dc2;                         // [8 waves][2][256] conv1 wgrad partials (after the sample loop)
+  float* smax = red12 + 256;                // [8]       per-wave max |dC2| of the next staged sample
+  uint8_t* a1sb = reinterpret_cast<uint8_t*>(smax + 8);   // [2][16][198] argmax of pool1
+  float* red = reinterpret_cast<float*>(dcr);   // [8 waves][2][256] conv1 wgrad partials (after the sample loop)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform (SGPR): per-wave branches are scalar
   const int k = blockIdx.x / G, g = blockIdx.x - k * G;
@@ -657,15 +678,37 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
   const float* prow = params + (size_t)k * P;
   const int i = lane & 15, kq = lane >> 4;
 
-  stage_w2<true>(prow + off.w2, w2r, 1, W2R, 32, tid);
-  for (int e = tid; e < (C2 + C1) * CS; e += NT) dc2[e] = 0.f;   // dc2 and p1s are contiguous
+  {   // W2 [o][ci][tap], scaled by 2^8 and split into the dgrad B records
+    constexpr int NU = (C2 * K2 + NT - 1) / NT;
+    float v[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int e = tid + u * NT;
+      if (e < C2 * K2) v[u] = prow[off.w2 + e];
+    }
+    _Float16* w2h = reinterpret_cast<_Float16*>(w2b);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int e = tid + u * NT;
+      if (e < C2 * K2) {
+        const int o = e / K2, rem = e - o * K2, ci = rem / 25, tap = rem - ci * 25;
+        const float x = v[u] * SW2;
+        const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
+        _Float16* rec = w2h + (size_t)(ci * W2B + tap * DRQ) * 8 + (o & 7);
+        rec[8 * (o >> 3)] = hi;
+        rec[8 * (4 + (o >> 3))] = lo;
+      }
+    }
+  }
+  for (int e = tid; e < NPOS * DRQ; e += NT) dcr[e] = make_uint4(0u, 0u, 0u, 0u);
+  for (int e = tid; e < C1 * CS; e += NT) p1s[e] = 0.f;
   for (int e = tid; e < 2 * IMGP * IMS; e += NT) imgb[e] = 0.f;
   if (tid < 256) ones[tid] = 1.f;
 
   // conv2 wgrad tiles: m-tile (o rows) and 7 / 6 n-tiles (taps; n-tile 25 = ones -> db2)
   const int wmt = (wave >> 1) & 1;
   const int nt0 = wave < 4 ? (wave & 1) * 7 : 14 + (wave & 1) * 6;
-  const int waoff = (int)(dc2 - sm) + (wmt * 16 + i) * CS + 2 * P1P + 2;
+  const int wo_row = wmt * 16 + i;
   int wboff[7];
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
@@ -676,7 +719,13 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
 #pragma unroll
   for (int j = 0; j < 7; ++j) wacc[j] = f4{0.f, 0.f, 0.f, 0.f};
   f4 c1acc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-  const int dboff = (int)(w2r - sm) + i * W2R + kq;   // dgrad B: w2r[i][tap*32 + 4*oc + kq] = W2[oc + 8 kq][i][tap]
+  const uint4* dgw2 = w2b + i * W2B;                 // dgrad B: lane column ci = i
+  BwdStage st;
+  st.load((size_t)k * B + s0, X, pool1, am1, pool2, am2, dP2, tid);
+  {
+    const float m = wave_max(st.maxabs(tid));
+    if (lane == 0) smax[wave] = m;
+  }
   __syncthreads();
 
   // conv1 wgrad (dC1 = unpool1(dp1) on the fly; K = 784 split across the 8 waves) of one finished sample
@@ -704,43 +753,44 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
         });
   };
 
-  BwdStage st;
-  st.load((size_t)k * B + s0, X, pool1, am1, pool2, am2, dP2, tid);
   for (int s = 0; s < ns; ++s) {
     float* dp1 = dp1b + (s & 1) * C1 * DPS;
-    // ---- stage the sample loaded during the previous one; then issue the next sample's loads, which
-    //      complete behind this sample's MFMA work (one workgroup per CU: nothing else hides them)
-    st.store(dc2, p1s, a1sb + (s & 1) * C1 * DPS, imgb + (s & 1) * IMGP * IMS, tid);
+    // ---- stage the sample loaded during the previous one (dC2 split with its own power-of-two scale); then issue
+    //      the next sample's loads, which complete behind this sample's MFMA work (one workgroup per CU)
+    float mx = smax[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) mx = fmaxf(mx, smax[w]);
+    const float scale = dc_scale(mx), inv = 1.f / scale, dinv = inv * (1.f / SW2);
+    st.store(dch, scale, p1s, a1sb + (s & 1) * C1 * DPS, imgb + (s & 1) * IMGP * IMS, tid);
     if (s + 1 < ns) st.load((size_t)k * B + s0 + s + 1, X, pool1, am1, pool2, am2, dP2, tid);
     __syncthreads();   // staged sample visible; the previous sample's dp1 complete
 
     // ---- conv2 wgrad (accumulates over the workgroup's samples)
-    if (wave < 4) bwd_wgrad2<7>(sm, waoff, wboff, wacc, kq);
-    else bwd_wgrad2<6>(sm, waoff, wboff, wacc, kq);
+    if (wave < 4) bwd_wgrad2<7>(sm, dch, wo_row, inv, wboff, wacc, kq);
+    else bwd_wgrad2<6>(sm, dch, wo_row, inv, wboff, wacc, kq);
 
-    // ---- conv2 dgrad -> dp1
+    // ---- conv2 dgrad -> dp1 (fp16 pipe, 3-term split)
     if (wave < 4) {
       const int mt0 = 2 * wave;
-      const int aoff[2] = {(int)(dc2 - sm) + 8 * kq * CS + q14(dg_pix(mt0 * 16 + i)) + 4 * P1P + 4,
-                           (int)(dc2 - sm) + 8 * kq * CS + q14(dg_pix(mt0 * 16 + 16 + i)) + 4 * P1P + 4};
-      f4 acc[2][2] = {};
-      bwd_dgrad2<2>(sm, aoff, dboff, 0, 25, acc);
-      bwd_dp1_store(dp1, p1s, mt0, acc[0][0] + acc[0][1], i, kq);
-      bwd_dp1_store(dp1, p1s, mt0 + 1, acc[1][0] + acc[1][1], i, kq);
+      const int apos[2] = {q14(dg_pix(mt0 * 16 + i)) + 4 * P1P + 4, q14(dg_pix(mt0 * 16 + 16 + i)) + 4 * P1P + 4};
+      f4 acc[2] = {};
+      bwd_dgrad2<2>(dcr, apos, dgw2, kq, 0, 25, acc);
+      bwd_dp1_store(dp1, p1s, mt0, acc[0] * dinv, i, kq);
+      bwd_dp1_store(dp1, p1s, mt0 + 1, acc[1] * dinv, i, kq);
     } else {
       const int mt = 4 + wave;
-      const int aoff[1] = {(int)(dc2 - sm) + 8 * kq * CS + q14(dg_pix(mt * 16 + i)) + 4 * P1P + 4};
-      f4 acc[1][2] = {};
-      bwd_dgrad2<1>(sm, aoff, dboff, 0, 25, acc);
-      bwd_dp1_store(dp1, p1s, mt, acc[0][0] + acc[0][1], i, kq);
+      const int apos[1] = {q14(dg_pix(mt * 16 + i)) + 4 * P1P + 4};
+      f4 acc[1] = {};
+      bwd_dgrad2<1>(dcr, apos, dgw2, kq, 0, 25, acc);
+      bwd_dp1_store(dp1, p1s, mt, acc[0] * dinv, i, kq);
       // m-tile 12: rows 192..195 valid (rows past 195 read a clamped in-range row and are dropped)
       const int w4 = wave - 4;
-      const int aoff12[1] = {(int)(dc2 - sm) + 8 * kq * CS + q14(dg_pix(192 + i)) + 4 * P1P + 4};
-      f4 acc12[1][2] = {};
-      bwd_dgrad2<1>(sm, aoff12, dboff, w4 == 0 ? 0 : 1 + 6 * w4, 7 + 6 * w4, acc12);
+      const int apos12[1] = {q14(dg_pix(192 + i)) + 4 * P1P + 4};
+      f4 acc12[1] = {};
+      bwd_dgrad2<1>(dcr, apos12, dgw2, kq, w4 == 0 ? 0 : 1 + 6 * w4, 7 + 6 * w4, acc12);
       if (kq == 0) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) red12[w4 * 64 + r * 16 + i] = acc12[0][0][r] + acc12[0][1][r];
+        for (int r = 0; r < 4; ++r) red12[w4 * 64 + r * 16 + i] = acc12[0][r] * dinv;
       }
     }
 
@@ -753,6 +803,10 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
     const int r12 = tid >> 4, ci12 = tid & 15;
     const int p12 = dg_pix(192 + r12);
     const bool m12 = tid < 64 && p1s[ci12 * CS + q14(p12) + 2 * P1P + 2] > 0.f;
+    if (s + 1 < ns) {   // the next sample's split scale (its loads have landed behind this sample's work)
+      const float m = wave_max(st.maxabs(tid));
+      if (lane == 0) smax[wave] = m;
+    }
     __syncthreads();
     if (tid < 64) {
       const float v = ((red12[tid] + red12[64 + tid]) + red12[128 + tid]) + red12[192 + tid];
@@ -762,7 +816,7 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
   __syncthreads();   // the last sample's dp1 rows 192..195
   if (ns > 0) conv1_wgrad(dp1b + ((ns - 1) & 1) * C1 * DPS, a1sb + ((ns - 1) & 1) * C1 * DPS,
                           imgb + ((ns - 1) & 1) * IMGP * IMS);
-  __syncthreads();   // red aliases dc2
+  __syncthreads();   // red aliases the dC2 records
 
   // ---- write partials (fixed order: deterministic)
   float* out = part + (size_t)blockIdx.x * PART;
@@ -1171,9 +1225,11 @@ __global__ void __launch_bounds__(256) cnn_eval_head(const float* __restrict__ h
 }
 
 size_t fwd_lds() { return (size_t)FWD_LDS; }
-size_t bwd_lds() {
-  return (size_t)(C1 * W2R + (C2 + C1) * CS + 2 * C1 * DPS + 2 * IMGP * IMS + 256 + 256) * 4 + 2 * C1 * DPS;
-}
+constexpr int BWD_LDS = (C1 * W2B + NPOS * DRQ) * 16 + (C1 * CS + 2 * C1 * DPS + 2 * IMGP * IMS + 256 + 256 + 8) * 4 +
+                        2 * C1 * DPS;
+static_assert(BWD_LDS <= 160 * 1024, "cnn_bwd LDS");
+static_assert(NW * 2 * 256 * 4 <= NPOS * DRQ * 16, "conv1 wgrad partials alias the dC2 records");
+size_t bwd_lds() { return (size_t)BWD_LDS; }
 
 }  // namespace cnn
 }  // namespace qfx

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 6: CFed conv2 dgrad on the fp16 pipe too - CNN tests, flip diagnostics of both trees, interleaved cfed128
+# suite lines (base = split forward only, new = split forward + dgrad) and kernel traces.
+source "$(dirname "$0")/gpu_step.sh"
+step cnn_tests 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_cnn.py
+for v in base new; do
+  QFX_PKG_ROOT=$PWD/ab/$v TAILN=1 step diag_$v 200 python scripts/cnn_flip_diag.py
+done
+for r in 1 2 3; do for v in base new; do
+  (cd ab/$v && timeout -k 10 300 python bench_suite.py --config cfed128 --steps 50 --warmup 3 > ../../gpurun_out/cfab_${v}$r.log 2>&1) || { echo "cfab_${v}$r failed"; tail -5 gpurun_out/cfab_${v}$r.log; exit 1; }
+  grep '"metric"' gpurun_out/cfab_${v}$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], {k: d[k] for k in d if 'err' in k})"
+done; done
+for v in base new; do
+  mkdir -p gpurun_out/cfprof_$v
+  (cd ab/$v && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d ../../gpurun_out/cfprof_$v -o cf -- python3 bench_suite.py --config cfed128 --steps 10 --warmup 2 > ../../gpurun_out/cfprof_$v.log 2>&1) || { echo "cfprof_$v failed"; exit 1; }
+done
