@@ -455,8 +455,6 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
 // a sample costs two barriers; the next sample's global inputs load into registers meanwhile.
 // --------------------------------------------------------------------------------------------
 constexpr int BS_MAX = 16;         // samples per backward workgroup, at most (bwd_bs)
-constexpr int CS = 338;            // LDS stride of one zero-padded 18x18 map (== 18 mod 32: channel-strided
-                                   // ds_read_b32 lanes land on distinct banks)
 constexpr int DRQ = 8;             // 16-byte chunks per dC2 position record / split W2 (ci, tap) record:
                                    // hi o 0-7 | hi o 8-15 | hi o 16-23 | hi o 24-31 | lo o 0-7 | ... | lo o 24-31
 constexpr int W2B = 202;           // chunks per input channel of the split W2 image (25 taps x 8 + 2 pad: the 16
@@ -482,11 +480,10 @@ constexpr int IMS = 37;            // LDS row stride of the padded image
 constexpr int NT2 = 26;            // conv2 wgrad n-tiles (25 taps + ones)
 constexpr int PART = C2 * K2 + C2 + C1 * K1 + C1;
 
-// conv2 dgrad GEMM row (m-tile * 16 + row) -> dp1 pixel p = 14 y + x.  A 32-lane half of an A read touches 16 pixels
-// (lane i) of two channels 8 CS apart (o = oc + 8 kq; 8 CS == 16 mod 32): its banks are distinct iff the 16 pixels'
-// map offsets 18 y + x are distinct mod 16, i.e. (2 y + x) mod 16.  Tile t holds the t-th pixel (in row order) of
-// every residue class; rows 192..195 (partial m-tile 12) the four classes that have a 13th.  In plain row order
-// (16 consecutive pixels) every A read was 2-way (PMC: 29% of the kernel's LDS cycles were conflict cycles).
+// conv2 dgrad GEMM row (m-tile * 16 + row) -> dp1 pixel p = 14 y + x.  Tile t holds the t-th pixel (in row order) of
+// every residue class of (2 y + x) mod 16; rows 192..195 (partial m-tile 12) the four classes that have a 13th.  (Chosen
+// for the round-5 fp32 channel-strided image; with the split position records and dc_chunk's XOR the b128 A reads are
+// conflict-free in this order.)
 __constant__ uint8_t kDgPix[H2 * H2] = {
     0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 26, 27, 40, 41, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23,
     24, 25, 38, 39, 52, 53, 54, 55, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 50, 51, 64, 65, 66, 67, 68, 69, 42, 43,
@@ -498,30 +495,85 @@ __constant__ uint8_t kDgPix[H2 * H2] = {
 };
 __device__ __forceinline__ int dg_pix(int row) { return kDgPix[min(row, H2 * H2 - 1)]; }
 
-// conv2 wgrad over the 49 k-steps of one sample: acc[j] += A(o rows) x B(n-tile j)
-template <int NJ>
+// conv2 wgrad of one sample on the fp16 pipe: D[o][(tap, ci)] += sum_k dC2[o][p_k] P1[ci][p_k + off(tap)], K = the
+// 196 pool2-resolution positions in row order, padded to 7 slabs of 32 (pad rows read the zero corner record).
+// Both operands have K on their LDS rows (position records) and M / N on the record's columns, so they are fetched
+// with ds_read_b64_tr_b16: lane 4q + p of a 16-lane group addresses row q, columns 4p .. 4p + 3 of a 4 x 16 block,
+// and lane i receives column i of the 4 rows - the MFMA's 8 consecutive k of its column in two reads.
+typedef short v4s __attribute__((vector_size(8)));
+__device__ __forceinline__ uint2 lds_tr16(const void* p) {
+  const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)p);
+  return __builtin_bit_cast(uint2, v);
+}
+__device__ __forceinline__ uint4 cat2(uint2 a, uint2 b) { return make_uint4(a.x, a.y, b.x, b.y); }
+constexpr int WG_SL = 7;           // wgrad K slabs (224 rows >= 196 positions)
+
 struct WgradSet {
-  float a, b[NJ];
+  uint4 bh, bl;
 };
 
-// A = dC2[o][p] (o = the lane's row) rebuilt from the split records: hi + lo (22 bits), times the sample's 1 / scale
+// wgrad of one sample into acc[j] (n-tiles nt0 + j, NJ of them; n-tile 25 = the db2 ones column) for the o rows of
+// m-tile wmt.  qk = the lane's block row (lane & 15) >> 2, pc = its column quad lane & 3, g = lane >> 4.
 template <int NJ>
-__device__ __forceinline__ void bwd_wgrad2(const float* sm, const _Float16* dch, int o, float inv, const int (&boff)[7],
-                                           f4 (&acc)[7], int kq) {
-  pipelined<WgradSet<NJ>>(
-      0, H2 * H2 / 4,
-      [&](int ks, WgradSet<NJ>& st) {
-        const int q = q14(ks * 4 + kq);
-        const int pos = q + 2 * P1P + 2;
-        const _Float16* rec = dch + pos * DRQ * 8 + (o & 7);
-        st.a = ((float)rec[8 * dc_chunk(pos, o >> 3)] + (float)rec[8 * dc_chunk(pos, 4 + (o >> 3))]) * inv;
+__device__ __forceinline__ void bwd_wgrad2(const char* dcb, const char* p1b, int wmt, int nt0, int g, int qk, int pc,
+                                           f4 (&acc)[7]) {
+  const int cA = 2 * wmt + (pc >> 1), cB = pc >> 1, eo = 8 * (pc & 1);
+  const uint4 ones = make_uint4(0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u);
+#pragma unroll 1
+  for (int sl = 0; sl < WG_SL; ++sl) {
+    int q[2];   // the lane's two block rows: k = 32 sl + 8 g + 4 h + qk -> position offset q14 (-1: pad row)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) st.b[j] = sm[boff[j] + q];
-      },
-      [&](const WgradSet<NJ>& st) {
+    for (int h = 0; h < 2; ++h) {
+      const int k = 32 * sl + 8 * g + 4 * h + qk;
+      q[h] = k < H2 * H2 ? q14(k) : -1;
+    }
+    uint4 ah, al;
+    {
+      uint2 rh[2], rl[2];
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[j] = mfma(st.a, st.b[j], acc[j]);
-      });
+      for (int h = 0; h < 2; ++h) {
+        const int pos = q[h] < 0 ? 0 : q[h] + 2 * P1P + 2;
+        const char* rec = dcb + pos * DRQ * 16 + eo;
+        rh[h] = lds_tr16(rec + 16 * dc_chunk(pos, cA));
+        rl[h] = lds_tr16(rec + 16 * dc_chunk(pos, 4 + cA));
+      }
+      ah = cat2(rh[0], rh[1]);
+      al = cat2(rl[0], rl[1]);
+    }
+    auto load = [&](int j, WgradSet& st) {
+      const int nt = nt0 + j;
+      if (nt >= 25) return;   // wave-uniform: the ones column reads nothing
+      const int ro = tap_off(nt);
+      uint2 bh[2], bl[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pos = (q[h] < 0 ? 0 : q[h]) + ro;
+        const char* rec = p1b + pos * PRQ * 16 + eo;
+        bh[h] = lds_tr16(rec + 16 * p1_chunk(pos, cB));
+        bl[h] = lds_tr16(rec + 16 * p1_chunk(pos, 2 + cB));
+      }
+      st.bh = cat2(bh[0], bh[1]);
+      st.bl = cat2(bl[0], bl[1]);
+    };
+    // n-tiles one at a time, the next one's operands in flight (all of them at once would take 56 more VGPRs)
+    WgradSet cur, nxt;
+    load(0, cur);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      if (j + 1 < NJ) load(j + 1, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      if (nt0 + j >= 25) {
+        acc[j] = mfma_h(ah, ones, acc[j]);
+        acc[j] = mfma_h(al, ones, acc[j]);
+      } else {
+        acc[j] = mfma_h(ah, cur.bh, acc[j]);
+        acc[j] = mfma_h(ah, cur.bl, acc[j]);
+        acc[j] = mfma_h(al, cur.bh, acc[j]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      cur = nxt;
+    }
+  }
 }
 
 // conv2 dgrad of NM m-tiles over taps [r0, r1) on the fp16 pipe: one K = 32 slab per tap (k = o), A = the split dC2
@@ -566,11 +618,12 @@ struct C1Set {
 };
 
 // dP1 rows of a finished dgrad m-tile, ReLU-masked by pool1 > 0 (the conv1 ReLU derivative)
-__device__ __forceinline__ void bwd_dp1_store(float* dp1, const float* p1s, int mt, f4 acc, int i, int kq) {
+// (a1s bit 7 = pool1 > 0, set at staging)
+__device__ __forceinline__ void bwd_dp1_store(float* dp1, const uint8_t* a1s, int mt, f4 acc, int i, int kq) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int row = mt * 16 + 4 * kq + r, p = dg_pix(row);
-    if (row < H2 * H2) dp1[i * DPS + p] = p1s[i * CS + q14(p) + 2 * P1P + 2] > 0.f ? acc[r] : 0.f;
+    if (row < H2 * H2) dp1[i * DPS + p] = (a1s[i * DPS + p] & 0x80) ? acc[r] : 0.f;
   }
 }
 
@@ -616,8 +669,9 @@ struct BwdStage {
       if (tid + j * NT < C2 * Q2 * Q2 && pl2[j] > 0.f) m = fmaxf(m, fabsf(dp2[j]));
     return m;
   }
-  // unpool2 (+ReLU mask) into the padded split dC2 records (values x scale), pool1 -> padded p1s, argmax1, image
-  __device__ __forceinline__ void store(_Float16* dch, float scale, float* p1s, uint8_t* a1s, float* img, int tid) const {
+  // unpool2 (+ReLU mask) into the padded split dC2 records (values x scale), pool1 -> its padded split records,
+  // argmax1 (bit 7: pool1 > 0), image
+  __device__ __forceinline__ void store(_Float16* dch, float scale, _Float16* p1h, uint8_t* a1s, float* img, int tid) const {
 #pragma unroll
     for (int j = 0; j < ND; ++j) {
       const int e = tid + j * NT;
@@ -640,8 +694,12 @@ struct BwdStage {
       const int e = tid + j * NT;
       if (e < C1 * Q1 * Q1) {
         const int ci = e / (Q1 * Q1), r = e - ci * Q1 * Q1;
-        p1s[ci * CS + (r / Q1 + 2) * P1P + (r % Q1) + 2] = p1[j];
-        a1s[ci * DPS + r] = a1[j];
+        const int pos = (r / Q1 + 2) * P1P + (r % Q1) + 2;
+        const _Float16 hi = (_Float16)p1[j], lo = (_Float16)(p1[j] - (float)hi);
+        _Float16* rec = p1h + pos * PRQ * 8 + (ci & 7);
+        rec[8 * p1_chunk(pos, ci >> 3)] = hi;
+        rec[8 * p1_chunk(pos, 2 + (ci >> 3))] = lo;
+        a1s[ci * DPS + r] = (uint8_t)(a1[j] | (p1[j] > 0.f ? 0x80 : 0));
       }
     }
 #pragma unroll
@@ -661,12 +719,12 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
   uint4* w2b = reinterpret_cast<uint4*>(sm);                // [16][202] split W2: w2b[ci][tap * 8 + chunk(o)]
   uint4* dcr = w2b + C1 * W2B;                              // [324][8] split padded dL/d conv2-output records
   _Float16* dch = reinterpret_cast<_Float16*>(dcr);
-  float* p1s = reinterpret_cast<float*>(dcr + NPOS * DRQ);   // [16][338] padded pool1 (conv2 input)
+  uint4* p1r = dcr + NPOS * DRQ;                            // [324][4] split padded pool1 records (conv2 input)
+  _Float16* p1h = reinterpret_cast<_Float16*>(p1r);
   // conv1 wgrad of sample s runs during sample s+1's conv2 work: its inputs are double buffered (index s & 1)
-  float* dp1b = p1s + C1 * CS;              // [2][16][198] dL/d pool1, ReLU-masked
+  float* dp1b = reinterpret_cast<float*>(p1r + NPOS * PRQ);   // [2][16][198] dL/d pool1, ReLU-masked
   float* imgb = dp1b + 2 * C1 * DPS;        // [2][32][37]  padded images
-  float* ones = imgb + 2 * IMGP * IMS;      // [256]     1.0 (bias columns)
-  float* red12 = ones + 256;                // [4][64]   m-tile 12 partials of waves 4..7
+  float* red12 = imgb + 2 * IMGP * IMS;     // [4][64]   m-tile 12 partials of waves 4..7
   float* smax = red12 + 256;                // [8]       per-wave max |dC2| of the next staged sample
   uint8_t* a1sb = reinterpret_cast<uint8_t*>(smax + 8);   // [2][16][198] argmax of pool1
   float* red = reinterpret_cast<float*>(dcr);   // [8 waves][2][256] conv1 wgrad partials (after the sample loop)
@@ -701,20 +759,14 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
     }
   }
   for (int e = tid; e < NPOS * DRQ; e += NT) dcr[e] = make_uint4(0u, 0u, 0u, 0u);
-  for (int e = tid; e < C1 * CS; e += NT) p1s[e] = 0.f;
+  for (int e = tid; e < NPOS * PRQ; e += NT) p1r[e] = make_uint4(0u, 0u, 0u, 0u);
   for (int e = tid; e < 2 * IMGP * IMS; e += NT) imgb[e] = 0.f;
-  if (tid < 256) ones[tid] = 1.f;
 
   // conv2 wgrad tiles: m-tile (o rows) and 7 / 6 n-tiles (taps; n-tile 25 = ones -> db2)
   const int wmt = (wave >> 1) & 1;
   const int nt0 = wave < 4 ? (wave & 1) * 7 : 14 + (wave & 1) * 6;
-  const int wo_row = wmt * 16 + i;
-  int wboff[7];
-#pragma unroll
-  for (int j = 0; j < 7; ++j) {
-    const int nt = min(nt0 + j, NT2 - 1);
-    wboff[j] = nt < 25 ? (int)(p1s - sm) + i * CS + tap_off(nt) : (int)(ones - sm);
-  }
+  // the wgrad accumulators hold sum_s D_s x (the latest sample's dC2 scale): rescaled by a power of two per sample
+  float wscale = 1.f;
   f4 wacc[7];
 #pragma unroll
   for (int j = 0; j < 7; ++j) wacc[j] = f4{0.f, 0.f, 0.f, 0.f};
@@ -747,7 +799,7 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
           c.b1 = im[toff1];
         },
         [&](const C1Set& c) {
-          const float a = c.a1 == c.pos ? c.d : 0.f;
+          const float a = (c.a1 & 3) == c.pos ? c.d : 0.f;
           c1acc[0] = mfma(a, c.b0, c1acc[0]);
           c1acc[1] = mfma(a, one1 ? 1.f : c.b1, c1acc[1]);
         });
@@ -761,13 +813,20 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
 #pragma unroll
     for (int w = 1; w < NW; ++w) mx = fmaxf(mx, smax[w]);
     const float scale = dc_scale(mx), inv = 1.f / scale, dinv = inv * (1.f / SW2);
-    st.store(dch, scale, p1s, a1sb + (s & 1) * C1 * DPS, imgb + (s & 1) * IMGP * IMS, tid);
+    st.store(dch, scale, p1h, a1sb + (s & 1) * C1 * DPS, imgb + (s & 1) * IMGP * IMS, tid);
     if (s + 1 < ns) st.load((size_t)k * B + s0 + s + 1, X, pool1, am1, pool2, am2, dP2, tid);
     __syncthreads();   // staged sample visible; the previous sample's dp1 complete
 
-    // ---- conv2 wgrad (accumulates over the workgroup's samples)
-    if (wave < 4) bwd_wgrad2<7>(sm, dch, wo_row, inv, wboff, wacc, kq);
-    else bwd_wgrad2<6>(sm, dch, wo_row, inv, wboff, wacc, kq);
+    // ---- conv2 wgrad (accumulates over the workgroup's samples, fp16 pipe)
+    {
+      const float rs = scale / wscale;   // exact: both powers of two
+#pragma unroll
+      for (int j = 0; j < 7; ++j) wacc[j] *= rs;
+      wscale = scale;
+    }
+    const uint8_t* a1cur = a1sb + (s & 1) * C1 * DPS;
+    if (wave < 4) bwd_wgrad2<7>((const char*)dcr, (const char*)p1r, wmt, nt0, kq, i >> 2, i & 3, wacc);
+    else bwd_wgrad2<6>((const char*)dcr, (const char*)p1r, wmt, nt0, kq, i >> 2, i & 3, wacc);
 
     // ---- conv2 dgrad -> dp1 (fp16 pipe, 3-term split)
     if (wave < 4) {
@@ -775,14 +834,14 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
       const int apos[2] = {q14(dg_pix(mt0 * 16 + i)) + 4 * P1P + 4, q14(dg_pix(mt0 * 16 + 16 + i)) + 4 * P1P + 4};
       f4 acc[2] = {};
       bwd_dgrad2<2>(dcr, apos, dgw2, kq, 0, 25, acc);
-      bwd_dp1_store(dp1, p1s, mt0, acc[0] * dinv, i, kq);
-      bwd_dp1_store(dp1, p1s, mt0 + 1, acc[1] * dinv, i, kq);
+      bwd_dp1_store(dp1, a1cur, mt0, acc[0] * dinv, i, kq);
+      bwd_dp1_store(dp1, a1cur, mt0 + 1, acc[1] * dinv, i, kq);
     } else {
       const int mt = 4 + wave;
       const int apos[1] = {q14(dg_pix(mt * 16 + i)) + 4 * P1P + 4};
       f4 acc[1] = {};
       bwd_dgrad2<1>(dcr, apos, dgw2, kq, 0, 25, acc);
-      bwd_dp1_store(dp1, p1s, mt, acc[0] * dinv, i, kq);
+      bwd_dp1_store(dp1, a1cur, mt, acc[0] * dinv, i, kq);
       // m-tile 12: rows 192..195 valid (rows past 195 read a clamped in-range row and are dropped)
       const int w4 = wave - 4;
       const int apos12[1] = {q14(dg_pix(192 + i)) + 4 * P1P + 4};
@@ -799,10 +858,10 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
                            imgb + ((s - 1) & 1) * IMGP * IMS);
 
     // m-tile 12 partials in fixed wave order -> dp1 rows 192..195.  The ReLU mask is read before the barrier:
-    // after it the other waves may already restage p1s for the next sample.
+    // after it the other waves may already restage the pool1 records for the next sample.
     const int r12 = tid >> 4, ci12 = tid & 15;
     const int p12 = dg_pix(192 + r12);
-    const bool m12 = tid < 64 && p1s[ci12 * CS + q14(p12) + 2 * P1P + 2] > 0.f;
+    const bool m12 = tid < 64 && (a1cur[ci12 * DPS + p12] & 0x80);
     if (s + 1 < ns) {   // the next sample's split scale (its loads have landed behind this sample's work)
       const float m = wave_max(st.maxabs(tid));
       if (lane == 0) smax[wave] = m;
@@ -819,6 +878,11 @@ __global__ void __launch_bounds__(NT) cnn_bwd(const float* __restrict__ X, const
   __syncthreads();   // red aliases the dC2 records
 
   // ---- write partials (fixed order: deterministic)
+  {
+    const float us = 1.f / wscale;
+#pragma unroll
+    for (int j = 0; j < 7; ++j) wacc[j] *= us;
+  }
   float* out = part + (size_t)blockIdx.x * PART;
   const int nj = wave < 4 ? 7 : 6;
 #pragma unroll
@@ -1225,7 +1289,7 @@ __global__ void __launch_bounds__(256) cnn_eval_head(const float* __restrict__ h
 }
 
 size_t fwd_lds() { return (size_t)FWD_LDS; }
-constexpr int BWD_LDS = (C1 * W2B + NPOS * DRQ) * 16 + (C1 * CS + 2 * C1 * DPS + 2 * IMGP * IMS + 256 + 256 + 8) * 4 +
+constexpr int BWD_LDS = (C1 * W2B + NPOS * DRQ + NPOS * PRQ) * 16 + (2 * C1 * DPS + 2 * IMGP * IMS + 256 + 8) * 4 +
                         2 * C1 * DPS;
 static_assert(BWD_LDS <= 160 * 1024, "cnn_bwd LDS");
 static_assert(NW * 2 * 256 * 4 <= NPOS * DRQ * 16, "conv1 wgrad partials alias the dC2 records");

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 6: CFed conv2 dgrad on the fp16 pipe too - CNN tests, flip diagnostics of both trees, interleaved cfed128
-# suite lines (base = split forward only, new = split forward + dgrad) and kernel traces.
+# Round 6: CFed conv2 wgrad on the fp16 pipe (transposed LDS reads) - CNN tests, flip diagnostics of both trees,
+# interleaved cfed128 suite lines (base = split forward + dgrad, new = + split wgrad) and kernel traces.
 source "$(dirname "$0")/gpu_step.sh"
 step cnn_tests 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_cnn.py
 for v in base new; do
