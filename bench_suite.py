@@ -156,8 +156,8 @@ def main():
         if kind == "tinycnn" and backend == "hip":
             from qfedx_amd.ops.cnn_hip import precision_check as cnn_precision
             rec.update(cnn_precision(cfg.model.n_classes, device))   # untimed: kernels vs float64 autograd
-            rec["dtype"] = ("fp32 (conv2 forward and conv2 dgrad as a 3-term fp16 split on v_mfma_f32_16x16x32_f16 "
-                            "with fp32 accumulation; conv1, conv2 wgrad and the fc layers on v_mfma_f32_16x16x4_f32)")
+            rec["dtype"] = ("fp32 (conv2 forward, dgrad and wgrad as a 3-term fp16 split on v_mfma_f32_16x16x32_f16 "
+                            "with fp32 accumulation; conv1 and the fc layers on v_mfma_f32_16x16x4_f32)")
         if t.grad_method == "param_shift" and eng is not None and hasattr(eng.hip, "shift_pass_counts"):
             # pass launches per sample of one gradient: naive shifted circuits vs prefix reuse + pi identity
             rec["param_shift"] = dict(eng.hip.shift_pass_counts(), reuse=bool(eng.ps_reuse))
