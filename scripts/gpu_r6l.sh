@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 6: CFed conv2 wgrad on the fp16 pipe (transposed LDS reads) - CNN tests, flip diagnostics of both trees,
-# interleaved cfed128 suite lines (base = split forward + dgrad, new = + split wgrad) and kernel traces.
+# Round 6: CFed kernels, conflict-free staging lane orders (W2 and the per-sample records) - CNN tests, diagnostics,
+# interleaved cfed128 suite lines (base = HEAD, new = staging lane orders) and kernel traces.
 source "$(dirname "$0")/gpu_step.sh"
 step cnn_tests 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_cnn.py
 for v in base new; do
