@@ -174,17 +174,29 @@ class SecureAggregator:
         surv = [c for c in parts if c not in gone]
         if self.graph == "full" or secagg_degree(len(parts)) >= len(parts) - 1:
             return {c: len(surv) - 1 for c in surv}           # complete graph: every other survivor
-        nb = self._neighbor_map(tuple(parts), round_num)
-        return {c: sum(1 for j in nb[c] if j not in gone) for c in surv}
+        pt, nbm = self._neighbor_matrix(tuple(parts), round_num)
+        dead = np.zeros(int(pt.max()) + 1, dtype=bool)
+        idx = [d for d in gone if d <= int(pt.max())]
+        dead[idx] = True
+        live = (~dead[nbm]).sum(1)
+        return {int(c): int(n) for c, n, d in zip(pt, live, dead[pt]) if not d}
 
     def round_ok(self, participants: Iterable[int], dropped: Iterable[int], round_num: int) -> bool:
         """Every surviving participant keeps at least ``live_threshold`` live neighbours (public information: the
-        participant set, the dropouts and the round-keyed graph, so every rank decides alike)."""
+        participant set, the dropouts and the round-keyed graph, so every rank decides alike).  Decided once per
+        (participants, dropouts, round): the server asks, then ``round_tables`` asks again."""
         parts = sorted({int(c) for c in participants})
+        key = (tuple(parts), tuple(sorted({int(d) for d in dropped})), int(round_num))
+        memo = self.__dict__.setdefault("_ok_memo", {})
+        if key in memo:
+            return memo[key]
         t = self.live_threshold(len(parts))
         self.check_threshold(len(parts))
         cnt = self.live_counts(parts, dropped, round_num)
-        return all(v >= t for v in cnt.values())
+        ok = all(v >= t for v in cnt.values())
+        memo.clear()
+        memo[key] = ok
+        return ok
 
     def check_threshold(self, num_participants: int) -> None:
         """A ``min_live`` above the mask graph's degree (sparse degree, or K - 1 on the complete graph) fails every
@@ -219,17 +231,26 @@ class SecureAggregator:
             return [j for j in parts if j != client]
         return list(self._neighbor_map(parts, round_num)[client])
 
-    def _neighbor_map(self, parts: tuple, round_num: int) -> dict:
-        """client -> sorted sparse-graph neighbours for the sorted participant tuple ``parts`` (cached per round)."""
+    def _neighbor_matrix(self, parts: tuple, round_num: int):
+        """(participants [K], their sorted sparse-graph neighbours [K, 2h]) for the sorted participant tuple ``parts``:
+        the h predecessors and successors on the round's circle (cached per round; vectorised - the per-client
+        Python sets cost ~1 ms a round at 128 clients, on the host path of every SecAgg round)."""
         key = (parts, int(round_num))
         if self._nb[0] != key:
             K = len(parts)
-            order = [parts[i] for i in np_rng(GRAPH_KEY, "secagg_graph", int(round_num), K).permutation(K)]
-            pos = {c: i for i, c in enumerate(order)}
+            pt = np.asarray(parts, dtype=np.int64)
+            order = pt[np_rng(GRAPH_KEY, "secagg_graph", int(round_num), K).permutation(K)]
+            pos = np.zeros(int(pt.max()) + 1, dtype=np.int64)
+            pos[order] = np.arange(K)
             h = secagg_degree(K) // 2
-            self._nb = (key, {c: sorted({order[(pos[c] + d) % K] for d in range(1, h + 1)} |
-                                        {order[(pos[c] - d) % K] for d in range(1, h + 1)}) for c in parts})
+            d = np.concatenate([np.arange(1, h + 1), -np.arange(1, h + 1)])
+            self._nb = (key, (pt, np.sort(order[(pos[pt][:, None] + d[None, :]) % K], axis=1)))
         return self._nb[1]
+
+    def _neighbor_map(self, parts: tuple, round_num: int) -> dict:
+        """client -> sorted sparse-graph neighbours for the sorted participant tuple ``parts``."""
+        pt, nbm = self._neighbor_matrix(parts, round_num)
+        return {int(c): [int(j) for j in row] for c, row in zip(pt, nbm)}
 
     def table_width(self, num_clients: int) -> int:
         """Peer columns of ``round_tables``: every client (full graph) or the largest neighbourhood any round
@@ -271,8 +292,13 @@ class SecureAggregator:
         """uint64 [len(rows), num_clients] pair seeds s_{i,j} of clients ``rows`` (held here) with every client j
         (diagonal 0).  Pair seeds do not depend on the round, so they are derived once (modular exponentiations)
         and cached."""
+        rows = [int(i) for i in rows]
+        key = (tuple(rows), int(num_clients))
+        whole = self.__dict__.get("_seed_whole")
+        if whole is not None and whole[0] == key:
+            return whole[1]                                  # the same rows every round: one stacked copy
         cache = self.__dict__.setdefault("_seed_rows", {})
-        out = np.zeros((len(list(rows)), num_clients), dtype=np.uint64)
+        out = np.zeros((len(rows), num_clients), dtype=np.uint64)
         for r, i in enumerate(rows):
             i = int(i)
             row = cache.get(i)
@@ -281,6 +307,8 @@ class SecureAggregator:
                                dtype=np.uint64)
                 cache[i] = row
             out[r] = row
+        out.setflags(write=False)
+        self._seed_whole = (key, out)
         return out
 
     def round_tables(self, clients: list[int], participants: Iterable[int], dropped: Iterable[int],
@@ -321,14 +349,12 @@ class SecureAggregator:
         elif secagg_degree(K) >= K - 1:
             nb = np.where((pt[None, :] != cl[:, None]) & np.isin(cl, pt)[:, None], pt[None, :], -1)   # all others
         else:
-            # the round's circle (as _neighbor_map): h predecessors and successors of each client, vectorised
-            order = pt[np_rng(GRAPH_KEY, "secagg_graph", int(round_num), K).permutation(K)]
-            pos = np.zeros(max(int(pt.max()), int(cl.max(initial=0))) + 1, dtype=np.int64)
-            pos[order] = np.arange(K)
-            h = secagg_degree(K) // 2
-            d = np.concatenate([np.arange(1, h + 1), -np.arange(1, h + 1)])
-            nb = np.sort(order[(pos[cl][:, None] + d[None, :]) % K], axis=1)
-            nb = np.where(np.isin(cl, pt)[:, None], nb, -1)                  # non-participants mask nothing
+            # the round's circle (_neighbor_matrix, shared with round_ok): rows of this rank's clients
+            ptm, nbm = self._neighbor_matrix(tuple(int(c) for c in pt), round_num)
+            row = np.full(max(int(pt.max()), int(cl.max(initial=0))) + 1, -1, dtype=np.int64)
+            row[ptm] = np.arange(K)
+            r = row[cl]
+            nb = np.where((r >= 0)[:, None], nbm[np.maximum(r, 0)], -1)       # non-participants mask nothing
         if len(gone):
             nb = np.where(np.isin(nb, np.asarray(sorted(gone), dtype=np.int64)), -1, nb)
         # live neighbours first (ascending), -1 pads
