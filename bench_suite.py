@@ -125,6 +125,8 @@ def main():
                           if backend == "hip" else "fp32", "fp32"),   # the MFMA/bf16 engines exist only on HIP
             "data": "synthetic non-IID client shards, random init", "rounds_per_sec": round(args.steps / dt, 4),
             "samples_per_sec": round(value * t.batch_size, 1), "backend": backend,
+            # host time to build and enqueue a round (bench.timed_rounds): a round is host-bound when this nears ms_per_step
+            "host_ms_per_round": round(float(getattr(runner, "host_ms", 0.0)), 4),
             "test_acc_after": round(ev["test_acc"], 4),
             "config": {"name": cfg.name, "model": kind if kind != "vqc" else
                        f"vqc-{cfg.model.n_qubits}q-{cfg.model.n_layers}L",

@@ -119,8 +119,8 @@ def batched_forward(params: torch.Tensor, x: torch.Tensor, num_classes: int = 3,
 
 def dropout_keys(K_ids, seed: int, round_num: int) -> torch.Tensor:
     """Host int64 [K, 2] Philox keys of the clients' dropout streams in round ``round_num`` (step = stream)."""
-    from ..utils.seeding import philox_key
-    return torch.tensor([philox_key(seed, "dropout", round_num, int(c)) for c in K_ids], dtype=torch.int64)
+    from ..utils.seeding import philox_keys
+    return torch.tensor(philox_keys(seed, ("dropout", round_num), [int(c) for c in K_ids]), dtype=torch.int64)
 
 
 def dropout_masks(K_ids, B: int, seed: int, round_num: int, step: int, device, p: float = 0.5) -> torch.Tensor:

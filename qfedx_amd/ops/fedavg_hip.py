@@ -4,7 +4,7 @@ from __future__ import annotations
 import torch
 
 from ..utils.device import h2d
-from ..utils.seeding import philox_key
+from ..utils.seeding import philox_keys
 from ._ext import ext
 
 
@@ -24,7 +24,7 @@ _NO_PACK = {}
 
 def dp_noise_keys(client_ids, round_num, seed) -> torch.Tensor:
     """Host int32 [K, 2] Philox keys of the clients' DP noise in round ``round_num``."""
-    return torch.tensor([philox_key(seed, "dp_noise", round_num, int(c)) for c in client_ids],
+    return torch.tensor(philox_keys(seed, ("dp_noise", round_num), [int(c) for c in client_ids]),
                         dtype=torch.int64).reshape(-1, 2).to(torch.int32)
 
 

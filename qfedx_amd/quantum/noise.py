@@ -30,7 +30,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ..utils.seeding import philox_key, philox_uniform_rows
+from ..utils.seeding import philox_keys, philox_uniform_rows
 
 
 EXACT_ONLY = ("amplitude", "amplitude_damping", "amp")     # channels with no Pauli-trajectory realisation
@@ -102,7 +102,7 @@ class NoiseModel:
 
     def client_keys(self, purpose: str, round_num: int, client_ids, device) -> torch.Tensor:
         """int64 [K, 2] Philox key words per client for this round (rank-count invariant)."""
-        return torch.tensor([philox_key(self.seed, purpose, round_num, int(c)) for c in client_ids],
+        return torch.tensor(philox_keys(self.seed, (purpose, round_num), [int(c) for c in client_ids]),
                             dtype=torch.int64).to(device)
 
     # ---------------------------------------------------------------- gate noise

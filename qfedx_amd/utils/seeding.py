@@ -77,6 +77,25 @@ def philox_key(root: int, *keys: int | str) -> tuple[int, int]:
     return s & MASK32, (s >> 32) & MASK32
 
 
+def philox_keys(root: int, prefix: tuple, last: list) -> list[tuple[int, int]]:
+    """``[philox_key(root, *prefix, k) for k in last]`` (bitwise the same): the hash state of (root, *prefix) is built
+    once and copied per key - a round's per-client keys (128 clients) cost ~0.2 ms of host time per round otherwise."""
+    h0 = hashlib.blake2b(digest_size=8)
+    h0.update(int(root).to_bytes(8, "little", signed=False))
+    for k in prefix:
+        if isinstance(k, str):
+            k = PURPOSE[k] if k in PURPOSE else int.from_bytes(
+                hashlib.blake2b(k.encode(), digest_size=8).digest(), "little")
+        h0.update(int(k & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "little", signed=False))
+    out = []
+    for k in last:
+        h = h0.copy()
+        h.update(int(int(k) & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "little", signed=False))
+        s = int.from_bytes(h.digest(), "little")
+        out.append((s & MASK32, (s >> 32) & MASK32))
+    return out
+
+
 # ---------------------------------------------------------------------------
 # Philox4x32-10, vectorised in torch int64 (CPU oracle of csrc/philox.h)
 # ---------------------------------------------------------------------------
