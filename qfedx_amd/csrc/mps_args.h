@@ -14,6 +14,15 @@ struct QfxMpsArgs {
   float* ro;                   // scratch, complex [S][qmax + 1][64]: RO_{q+1} (gradient mode)
   int x_stride, t_stride, spc, S, n, L, feature, C, qmax;
   int readout[QFX_MPS_RMAX];
+  // fused readout (gradient mode, w == nullptr): logits a <Z> + b from theta[ro_off ..] (a) and [ro_off + C ..] (b),
+  // softmax cross entropy of label y with loss weight wts, dL/d<Z> = a dl formed in the kernel; per sample out:
+  // dl [S][C] (dL/dlogit), lossv / hitv [S] (y == nullptr: no fused readout)
+  const long long* y;
+  const float* wts;
+  int ro_off;
+  float* dl;
+  float* lossv;
+  float* hitv;
 };
 
 // Launch arguments of the generic MPO-product MPS kernel (csrc/mps_mpo.hip; tables: quantum/mps_mpo.py).

@@ -28,9 +28,12 @@ float* fp(const torch::Tensor& t, const char* name, int64_t numel) {
 
 // x [S, >= n] angles, theta [K, >= 2 n L] per-client rows (spc samples each), readout qubit list; w [S, C] (or an
 // empty tensor: <Z> only).  z [S, C] out; grad [S, 2 n L] out (gradient mode); rp / ro float32 scratch.
+// Fused readout (y defined, non-empty; w then empty): theta rows hold the readout a / b at ro_off / ro_off + C, y [S]
+// int64 labels, wts [S] loss weights; out dl [S, C] (dL/dlogit), lossv / hitv [S]; z [S, C] and grad as usual.
 void mps_chain(torch::Tensor x, torch::Tensor theta, int64_t spc, int64_t n, int64_t L, int64_t feature,
                std::vector<int64_t> readout, torch::Tensor w, torch::Tensor z, torch::Tensor grad, torch::Tensor rp,
-               torch::Tensor ro) {
+               torch::Tensor ro, c10::optional<torch::Tensor> y, c10::optional<torch::Tensor> wts, int64_t ro_off,
+               c10::optional<torch::Tensor> dl, c10::optional<torch::Tensor> lossv, c10::optional<torch::Tensor> hitv) {
   need(x.dim() == 2 && theta.dim() == 2, "x [S, F] and theta [K, P] expected");
   const int64_t S = x.size(0), C = (int64_t)readout.size();
   need(n >= 2 && L >= 1 && L <= 3 && x.size(1) >= n && theta.size(1) >= 2 * n * L, "shape / layer range");
@@ -43,10 +46,21 @@ void mps_chain(torch::Tensor x, torch::Tensor theta, int64_t spc, int64_t n, int
     a.readout[i] = (int)readout[i];
     qmax = std::max(qmax, (int)readout[i]);
   }
-  const bool gmode = w.defined() && w.numel() > 0;
+  const bool fused = y.has_value() && y->defined() && y->numel() > 0;
+  const bool gmode = (w.defined() && w.numel() > 0) || fused;
   a.x = fp(x, "x", S * x.size(1));
   a.theta = fp(theta, "theta", theta.numel());
-  a.w = gmode ? fp(w, "w", S * C) : nullptr;
+  a.w = (gmode && !fused) ? fp(w, "w", S * C) : nullptr;
+  if (fused) {
+    need(y->is_cuda() && y->is_contiguous() && y->scalar_type() == torch::kInt64 && y->numel() >= S, "y: int64 [S]");
+    need(ro_off >= 2 * n * L && ro_off + 2 * C <= theta.size(1), "readout a / b outside the theta rows");
+    a.y = reinterpret_cast<const long long*>(y->data_ptr<int64_t>());
+    a.wts = fp(*wts, "wts", S);
+    a.ro_off = (int)ro_off;
+    a.dl = fp(*dl, "dl", S * C);
+    a.lossv = fp(*lossv, "lossv", S);
+    a.hitv = fp(*hitv, "hitv", S);
+  }
   a.z = fp(z, "z", S * C);
   a.grad = gmode ? fp(grad, "grad", S * 2 * n * L) : nullptr;
   a.rp = fp(rp, "rp", S * n * 64 * 2);
@@ -123,7 +137,9 @@ void mps_mpo(torch::Tensor ang, torch::Tensor gkind, torch::Tensor events, torch
 void register_mps(pybind11::module& m) {
   m.def("mps_chain", &mps_chain, pybind11::arg("x"), pybind11::arg("theta"), pybind11::arg("spc"), pybind11::arg("n"),
         pybind11::arg("L"), pybind11::arg("feature"), pybind11::arg("readout"), pybind11::arg("w"), pybind11::arg("z"),
-        pybind11::arg("grad"), pybind11::arg("rp"), pybind11::arg("ro"));
+        pybind11::arg("grad"), pybind11::arg("rp"), pybind11::arg("ro"), pybind11::arg("y") = pybind11::none(),
+        pybind11::arg("wts") = pybind11::none(), pybind11::arg("ro_off") = 0, pybind11::arg("dl") = pybind11::none(),
+        pybind11::arg("lossv") = pybind11::none(), pybind11::arg("hitv") = pybind11::none());
   m.def("mps_mpo", &mps_mpo, pybind11::arg("ang"), pybind11::arg("gkind"), pybind11::arg("events"),
         pybind11::arg("sinfo"), pybind11::arg("nbits"), pybind11::arg("sinfo_host"), pybind11::arg("nbits_host"),
         pybind11::arg("readout"), pybind11::arg("w"), pybind11::arg("z"),

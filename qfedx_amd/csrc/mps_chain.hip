@@ -18,6 +18,7 @@
 #include <cstdint>
 
 #include "mps_args.h"
+#include "qfx_readout.h"
 
 namespace qfx_mps {
 
@@ -144,13 +145,14 @@ __global__ void __launch_bounds__(64 * WPB) mps_chain_kernel(MpsArgs g) {
   float2* A1 = As[wave][1];
   float2* R = E1[wave];
   float2* rp = reinterpret_cast<float2*>(g.rp) + (size_t)s * n * 64;
-  const bool grad = g.w != nullptr;
+  const bool fused = g.y != nullptr;                 // gradient mode, dL/d<Z> formed from the kernel's own <Z>
+  const bool grad = g.w != nullptr || fused;
   float wq[RMAX];
   int rq[RMAX];
 #pragma unroll
   for (int i = 0; i < RMAX; ++i) {
     rq[i] = i < g.C ? g.readout[i] : -1;
-    wq[i] = (grad && i < g.C) ? g.w[(size_t)s * g.C + i] : 0.f;
+    wq[i] = (grad && !fused && i < g.C) ? g.w[(size_t)s * g.C + i] : 0.f;
   }
   auto wof = [&](int q) {                  // weight of Z_q in O (0 off the readout)
     float v = 0.f;
@@ -214,11 +216,132 @@ __global__ void __launch_bounds__(64 * WPB) mps_chain_kernel(MpsArgs g) {
   float2* LO = E2[wave];
   float2* Rq = E3[wave];
   float2* ROq = E4[wave];
+  // RO_{q+1} of the readout cuts (gradient mode), written by the RO sweep below
+  float2* ros = reinterpret_cast<float2*>(g.ro) + (size_t)s * (g.qmax + 1) * 64;
   float zc[RMAX];
+  // left sweep over columns [0, qend): <Z> of the readout qubits into zc, and with gm the gradient terms
+  auto left = [&](int qend, bool gm) {
 #pragma unroll
   for (int i = 0; i < RMAX; ++i) zc[i] = 0.f;
-  // RO sweep (grad mode): RO_{q+1} for q <= qmax, right to left, from RO_{qmax+1} = 0
-  float2* ros = reinterpret_cast<float2*>(g.ro) + (size_t)s * (g.qmax + 1) * 64;
+  if (lane == 0) {
+      Lp[0] = make_float2(1.f, 0.f);
+      LO[0] = make_float2(0.f, 0.f);
+    }
+    wave_lds();
+    float* gout = grad ? g.grad + (size_t)s * 2 * n * g.L : nullptr;
+    for (int q = 0; q < qend; ++q) {
+      const int Dl = q == 0 ? 1 : D, Dr = q == n - 1 ? 1 : D;
+      Col c;
+      build_col(g, th, xs[q], q, x_, y_, c);
+      put_col(c, Dl, Dr);
+      Rq[lane] = rp[(size_t)q * 64 + lane];
+      ROq[lane] = (gm && q <= g.qmax) ? ros[(size_t)q * 64 + lane] : make_float2(0.f, 0.f);
+      // U1[a'][s][b] = sum_a conj(A[a,s,b]) Lp[a][a'],  U2 the same with LO   (lane (a', b))
+      float2* u1 = U1[wave][0];
+      float2* u2 = U2[wave][0];
+      if (x_ < Dl && y_ < Dr) {
+        float2 p0 = make_float2(0.f, 0.f), p1 = p0, o0 = p0, o1 = p0;
+        for (int a = 0; a < Dl; ++a) {
+          const float2 l = Lp[a * 8 + x_], lo = LO[a * 8 + x_];
+          const float2 a0 = A0[a * 8 + y_], a1 = A1[a * 8 + y_];
+          p0 = cadd(p0, cjmul(a0, l));
+          p1 = cadd(p1, cjmul(a1, l));
+          o0 = cadd(o0, cjmul(a0, lo));
+          o1 = cadd(o1, cjmul(a1, lo));
+        }
+        u1[x_ * 8 + y_] = p0;
+        u1[64 + x_ * 8 + y_] = p1;
+        u2[x_ * 8 + y_] = o0;
+        u2[64 + x_ * 8 + y_] = o1;
+      }
+      wave_lds();
+      const float wz = wof(q);
+      // readout: <Z_q> = sum_{a',s,b,b'} z_s U1[a',s,b] A[a',s,b'] Rp[b][b']
+      bool isro = false;
+  #pragma unroll
+      for (int i = 0; i < RMAX; ++i) isro |= rq[i] == q;
+      if (isro) {
+        float t = 0.f;
+        if (x_ < Dl && y_ < Dr) {
+          float2 y0 = make_float2(0.f, 0.f), y1 = y0;
+          for (int bp = 0; bp < Dr; ++bp) {
+            const float2 r = Rq[y_ * 8 + bp];
+            y0 = cadd(y0, cmul(A0[x_ * 8 + bp], r));
+            y1 = cadd(y1, cmul(A1[x_ * 8 + bp], r));
+          }
+          t = cmul(u1[x_ * 8 + y_], y0).x - cmul(u1[64 + x_ * 8 + y_], y1).x;
+        }
+        t = wave_sum(t);
+  #pragma unroll
+        for (int i = 0; i < RMAX; ++i)
+          if (rq[i] == q) zc[i] = t;
+      }
+      if (gm) {
+        // Ybar[a'][s][b'] = sum_b U1[a',s,b] (RO[b][b'] + wz z_s Rp[b][b']) + U2[a',s,b] Rp[b][b']   (lane (a', b'))
+        float2 g0 = make_float2(0.f, 0.f), g1 = g0;
+        if (x_ < Dl && y_ < Dr) {
+          for (int b = 0; b < Dr; ++b) {
+            const float2 r = Rq[b * 8 + y_], ro = ROq[b * 8 + y_];
+            const float2 k0 = cadd(ro, csc(r, wz)), k1 = cadd(ro, csc(r, -wz));
+            g0 = cadd(g0, cadd(cmul(u1[x_ * 8 + b], k0), cmul(u2[x_ * 8 + b], r)));
+            g1 = cadd(g1, cadd(cmul(u1[64 + x_ * 8 + b], k1), cmul(u2[64 + x_ * 8 + b], r)));
+          }
+        }
+        float part[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (x_ < Dl && y_ < Dr) reverse_col(g, c, q, x_, y_, g0, g1, part);
+  #pragma unroll
+        for (int l = 0; l < 3; ++l) {
+          if (l >= g.L) break;
+          const float dt = wave_sum(part[2 * l]), dp = wave_sum(part[2 * l + 1]);
+          if (lane == 0) {
+            gout[2 * (l * n + q)] = dt * inv_norm;      // (reverse_col already returns 2 Re)
+            gout[2 * (l * n + q) + 1] = dp * inv_norm;
+          }
+        }
+      }
+      // Lp_{q+1}[b][b'] = sum_{a',s} U1[a',s,b] A[a',s,b'];  LO_{q+1} = sum (U2 + wz z_s U1) A   (lane (b, b'))
+      float2 nl = make_float2(0.f, 0.f), no = nl;
+      if (x_ < Dr && y_ < Dr) {
+        for (int ap = 0; ap < Dl; ++ap) {
+          const float2 a0 = A0[ap * 8 + y_], a1 = A1[ap * 8 + y_];
+          const float2 p0 = u1[ap * 8 + x_], p1 = u1[64 + ap * 8 + x_];
+          nl = cadd(nl, cadd(cmul(p0, a0), cmul(p1, a1)));
+          if (gm) {
+            const float2 o0 = cadd(u2[ap * 8 + x_], csc(p0, wz)), o1 = cadd(u2[64 + ap * 8 + x_], csc(p1, -wz));
+            no = cadd(no, cadd(cmul(o0, a0), cmul(o1, a1)));
+          }
+        }
+      }
+      wave_lds();
+      Lp[lane] = nl;
+      LO[lane] = no;
+      wave_lds();
+    }
+  };
+  if (fused) {
+    // <Z> first (left sweep up to the last readout qubit), then the sample's logits a <Z> + b, softmax cross
+    // entropy (qfx_readout.h, the HEA engine's fused readout) and dL/d<Z>_c = a_c dl_c for the gradient sweeps
+    left(g.qmax + 1, false);
+    float* wsh = reinterpret_cast<float*>(E3[wave]);
+    if (lane == 0) {
+      const float* prm = g.theta + (size_t)(s / g.spc) * g.t_stride + g.ro_off;
+      float zz[qfx_ro::RO_CMAX], dl[qfx_ro::RO_CMAX], loss, hit;
+#pragma unroll
+      for (int i = 0; i < qfx_ro::RO_CMAX; ++i) zz[i] = i < g.C ? zc[i] * inv_norm : 0.f;
+      qfx_ro::ce_sample(zz, prm, prm + g.C, g.C, (int)g.y[s], g.wts[s], dl, loss, hit);
+      for (int i = 0; i < g.C; ++i) {
+        g.z[(size_t)s * g.C + i] = zz[i];
+        g.dl[(size_t)s * g.C + i] = dl[i];
+        wsh[i] = prm[i] * dl[i];
+      }
+      g.lossv[s] = loss;
+      g.hitv[s] = hit;
+    }
+    wave_lds();
+#pragma unroll
+    for (int i = 0; i < RMAX; ++i) wq[i] = i < g.C ? wsh[i] : 0.f;
+    wave_lds();
+  }
   if (grad) {
     ROq[lane] = make_float2(0.f, 0.f);
     wave_lds();
@@ -240,102 +363,8 @@ __global__ void __launch_bounds__(64 * WPB) mps_chain_kernel(MpsArgs g) {
       wave_lds();
     }
   }
-  if (lane == 0) {
-    Lp[0] = make_float2(1.f, 0.f);
-    LO[0] = make_float2(0.f, 0.f);
-  }
-  wave_lds();
-  const int qend = grad ? n : g.qmax + 1;
-  float* gout = grad ? g.grad + (size_t)s * 2 * n * g.L : nullptr;
-  for (int q = 0; q < qend; ++q) {
-    const int Dl = q == 0 ? 1 : D, Dr = q == n - 1 ? 1 : D;
-    Col c;
-    build_col(g, th, xs[q], q, x_, y_, c);
-    put_col(c, Dl, Dr);
-    Rq[lane] = rp[(size_t)q * 64 + lane];
-    ROq[lane] = (grad && q <= g.qmax) ? ros[(size_t)q * 64 + lane] : make_float2(0.f, 0.f);
-    // U1[a'][s][b] = sum_a conj(A[a,s,b]) Lp[a][a'],  U2 the same with LO   (lane (a', b))
-    float2* u1 = U1[wave][0];
-    float2* u2 = U2[wave][0];
-    if (x_ < Dl && y_ < Dr) {
-      float2 p0 = make_float2(0.f, 0.f), p1 = p0, o0 = p0, o1 = p0;
-      for (int a = 0; a < Dl; ++a) {
-        const float2 l = Lp[a * 8 + x_], lo = LO[a * 8 + x_];
-        const float2 a0 = A0[a * 8 + y_], a1 = A1[a * 8 + y_];
-        p0 = cadd(p0, cjmul(a0, l));
-        p1 = cadd(p1, cjmul(a1, l));
-        o0 = cadd(o0, cjmul(a0, lo));
-        o1 = cadd(o1, cjmul(a1, lo));
-      }
-      u1[x_ * 8 + y_] = p0;
-      u1[64 + x_ * 8 + y_] = p1;
-      u2[x_ * 8 + y_] = o0;
-      u2[64 + x_ * 8 + y_] = o1;
-    }
-    wave_lds();
-    const float wz = wof(q);
-    // readout: <Z_q> = sum_{a',s,b,b'} z_s U1[a',s,b] A[a',s,b'] Rp[b][b']
-    bool isro = false;
-#pragma unroll
-    for (int i = 0; i < RMAX; ++i) isro |= rq[i] == q;
-    if (isro) {
-      float t = 0.f;
-      if (x_ < Dl && y_ < Dr) {
-        float2 y0 = make_float2(0.f, 0.f), y1 = y0;
-        for (int bp = 0; bp < Dr; ++bp) {
-          const float2 r = Rq[y_ * 8 + bp];
-          y0 = cadd(y0, cmul(A0[x_ * 8 + bp], r));
-          y1 = cadd(y1, cmul(A1[x_ * 8 + bp], r));
-        }
-        t = cmul(u1[x_ * 8 + y_], y0).x - cmul(u1[64 + x_ * 8 + y_], y1).x;
-      }
-      t = wave_sum(t);
-#pragma unroll
-      for (int i = 0; i < RMAX; ++i)
-        if (rq[i] == q) zc[i] = t;
-    }
-    if (grad) {
-      // Ybar[a'][s][b'] = sum_b U1[a',s,b] (RO[b][b'] + wz z_s Rp[b][b']) + U2[a',s,b] Rp[b][b']   (lane (a', b'))
-      float2 g0 = make_float2(0.f, 0.f), g1 = g0;
-      if (x_ < Dl && y_ < Dr) {
-        for (int b = 0; b < Dr; ++b) {
-          const float2 r = Rq[b * 8 + y_], ro = ROq[b * 8 + y_];
-          const float2 k0 = cadd(ro, csc(r, wz)), k1 = cadd(ro, csc(r, -wz));
-          g0 = cadd(g0, cadd(cmul(u1[x_ * 8 + b], k0), cmul(u2[x_ * 8 + b], r)));
-          g1 = cadd(g1, cadd(cmul(u1[64 + x_ * 8 + b], k1), cmul(u2[64 + x_ * 8 + b], r)));
-        }
-      }
-      float part[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (x_ < Dl && y_ < Dr) reverse_col(g, c, q, x_, y_, g0, g1, part);
-#pragma unroll
-      for (int l = 0; l < 3; ++l) {
-        if (l >= g.L) break;
-        const float dt = wave_sum(part[2 * l]), dp = wave_sum(part[2 * l + 1]);
-        if (lane == 0) {
-          gout[2 * (l * n + q)] = dt * inv_norm;      // (reverse_col already returns 2 Re)
-          gout[2 * (l * n + q) + 1] = dp * inv_norm;
-        }
-      }
-    }
-    // Lp_{q+1}[b][b'] = sum_{a',s} U1[a',s,b] A[a',s,b'];  LO_{q+1} = sum (U2 + wz z_s U1) A   (lane (b, b'))
-    float2 nl = make_float2(0.f, 0.f), no = nl;
-    if (x_ < Dr && y_ < Dr) {
-      for (int ap = 0; ap < Dl; ++ap) {
-        const float2 a0 = A0[ap * 8 + y_], a1 = A1[ap * 8 + y_];
-        const float2 p0 = u1[ap * 8 + x_], p1 = u1[64 + ap * 8 + x_];
-        nl = cadd(nl, cadd(cmul(p0, a0), cmul(p1, a1)));
-        if (grad) {
-          const float2 o0 = cadd(u2[ap * 8 + x_], csc(p0, wz)), o1 = cadd(u2[64 + ap * 8 + x_], csc(p1, -wz));
-          no = cadd(no, cadd(cmul(o0, a0), cmul(o1, a1)));
-        }
-      }
-    }
-    wave_lds();
-    Lp[lane] = nl;
-    LO[lane] = no;
-    wave_lds();
-  }
-  if (lane == 0) {
+  left(grad ? n : g.qmax + 1, grad);
+  if (lane == 0 && !fused) {
 #pragma unroll
     for (int i = 0; i < RMAX; ++i)
       if (i < g.C) g.z[(size_t)s * g.C + i] = zc[i] * inv_norm;

@@ -54,6 +54,9 @@ class VQCEngine:
                  noise=None, mps_chi: int = 64):
         self.spec = spec
         self.mps_hip = None
+        # noiseless MPS-chain training steps fuse the readout cross entropy into the gradient launch (MpsChainProgram.
+        # train); False runs the <Z> launch, the torch readout and the gradient launch (tests compare the two)
+        self.fused_mps_readout = True
         self.noise = noise          # quantum.noise.NoiseModel or None
         self.device = torch.device(device)
         self.backend = backend
@@ -260,6 +263,12 @@ class VQCEngine:
         P = spec.n_theta
         with torch.no_grad():
             rows = psi = None
+            if (method == "adjoint" and self.mps_hip is not None and init is None and self.noise is None
+                    and self.fused_mps_readout):
+                # one HIP launch (csrc/mps_chain.hip): <Z>, the readout cross entropy and dL/d<Z> in the kernel, then
+                # the gradient sweeps
+                loss, grad, correct, expz = self.mps_hip.train(xang, params, y, wmask)
+                return {"loss": loss, "grad": grad, "correct": correct, "expz": expz}
             if method == "adjoint" and self.mps_hip is not None and init is None:
                 # HIP column contraction (csrc/mps_chain.hip): <Z>, then the gradient sweep with dL/d<Z>
                 expz = self._readout(self.mps_hip.expz(xang, th), readout_keys, step)

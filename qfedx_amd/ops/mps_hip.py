@@ -57,6 +57,32 @@ class MpsChainProgram:
         return self._run(xang, theta)[0]
 
     @torch.no_grad()
+    def train(self, xang: torch.Tensor, params: torch.Tensor, y: torch.Tensor, wmask: torch.Tensor):
+        """One launch for a noiseless training step: <Z>, the logits a <Z> + b, the weighted softmax cross entropy and
+        dL/d<Z> per sample in the kernel (qfx_readout.h, as the MFMA engine's fused readout), then the gradient sweeps
+        - the separate <Z> launch, its right sweep and the torch readout ops are gone.  params [K, n_theta + 2C]
+        (theta | a | b) -> (loss [K], grad [K, n_theta + 2C], correct [K], expz [K, B, C]), ``ce_readout``'s
+        definitions."""
+        K, B, F = xang.shape
+        S = K * B
+        C = self.C
+        x = xang.reshape(S, F).float().contiguous()
+        p = params.float().contiguous()
+        z = torch.empty(S, C, dtype=torch.float32, device=self.device)
+        dl = torch.empty(S, C, dtype=torch.float32, device=self.device)
+        lossv = torch.empty(S, dtype=torch.float32, device=self.device)
+        hitv = torch.empty(S, dtype=torch.float32, device=self.device)
+        g = torch.empty(S, 2 * self.n * self.L, dtype=torch.float32, device=self.device)
+        rp = self._buf("rp", S * self.n * 128)
+        ro = self._buf("ro", S * (max(self.readout) + 1) * 128)
+        ext().mps_chain(x, p, B, self.n, self.L, self.feature, self.readout, _EMPTY, z, g, rp, ro,
+                        y.reshape(S).long().contiguous(), wmask.reshape(S).float().contiguous(), self.n_theta, dl,
+                        lossv, hitv)
+        zk, dlk = z.view(K, B, C), dl.view(K, B, C)
+        grad = torch.cat([g.view(K, B, -1).sum(1), (dlk * zk).sum(1), dlk.sum(1)], -1)
+        return lossv.view(K, B).sum(1), grad, hitv.view(K, B).sum(1), zk
+
+    @torch.no_grad()
     def grads(self, xang: torch.Tensor, theta: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         """d/dtheta of sum_{b, c} w[k, b, c] <Z_c>_{k, b}: [K, n_theta] (per-sample gradients summed over each
         client's samples in order)."""

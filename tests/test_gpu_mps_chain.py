@@ -74,3 +74,35 @@ def test_48_qubits_match_torch_mps_and_train(cuda):
                            spec.readout, "ry", w[0].double().cpu().numpy())
     np.testing.assert_allclose(z1[0].cpu().numpy(), zo, atol=2e-5)
     np.testing.assert_allclose(g1[0].cpu().numpy(), go.sum(0), atol=5e-5)
+
+
+def test_fused_readout_train_matches_two_launch_step(cuda):
+    """The one-launch training step (readout cross entropy and dL/d<Z> in the kernel) against the <Z> launch + torch
+    readout + gradient launch: same loss, gradients (readout a / b included), hits and <Z>, at fp32 rounding."""
+    from qfedx_amd.ops.engine import VQCEngine
+    spec = VQCSpec(24, 3, 3, readout_scale=3.0)
+    g = torch.Generator().manual_seed(5)
+    K, B = 3, 8
+    xang = spec.encode_features(torch.rand(K, B, 24, generator=g)).to(cuda)
+    params = (torch.stack([spec.init_params(k) for k in range(K)]) + 0.2 * torch.randn(K, spec.n_params,
+                                                                                      generator=g)).to(cuda)
+    y = torch.randint(0, 3, (K, B), generator=g).to(cuda)
+    wm = torch.rand(K, B, generator=g).to(cuda)
+    eng = VQCEngine(spec, cuda, "mps")
+    assert eng.mps_hip is not None and eng.fused_mps_readout
+    calls = [0]
+    real = eng.mps_hip.train
+
+    def spy(*a, **k):
+        calls[0] += 1
+        return real(*a, **k)
+    eng.mps_hip.train = spy
+    fused = eng.loss_and_grads(xang, y, wm, params)
+    eng.fused_mps_readout = False
+    ref = eng.loss_and_grads(xang, y, wm, params)
+    torch.cuda.synchronize()
+    assert calls[0] == 1
+    np.testing.assert_allclose(fused["loss"].cpu().numpy(), ref["loss"].cpu().numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(fused["grad"].cpu().numpy(), ref["grad"].cpu().numpy(), atol=1e-5)
+    np.testing.assert_allclose(fused["expz"].cpu().numpy(), ref["expz"].cpu().numpy(), atol=1e-6)
+    assert torch.equal(fused["correct"].cpu(), ref["correct"].cpu())
