@@ -168,7 +168,9 @@ static_assert(FSG * 2 == NW, "conv2 partial m-tile: one (sample, half) per wave"
 //   k = 8 g .. 8 g + 7 = tap 2 slab + g / 2, channels 8 (g & 1) .. + 7 - one 16-byte chunk of a position record.
 constexpr int NPOS = P1P * P1P;    // positions of the zero-padded 18 x 18 pool1 map
 constexpr int PRQ = 4;             // 16-byte chunks per position record: hi ci 0-7 | hi ci 8-15 | lo ci 0-7 | lo 8-15
-constexpr int W2Q = 106;           // chunks per output channel of the split W2 image (26 taps x 4 + 2 pad: the 16
+constexpr int W2T = 5;             // chunks per tap record of the split W2 image (4 + 1 pad: the staging stores of a
+                                   // wave's consecutive taps spread over 8 bank groups instead of 2 - 6.5-way, not 12-way)
+constexpr int W2Q = 130;           // chunks per output channel of the split W2 image (26 taps x 5: the 16
                                    // lanes of a ds_read_b128 group land on distinct 16-byte bank slots)
 constexpr int NSL = 13;            // K slabs
 constexpr float SW2 = 256.f;       // W2 scale before the split (power of two, undone on the accumulators)
@@ -219,7 +221,7 @@ __device__ __forceinline__ void fwd_conv2(const uint4* p1, const int (&apos)[NM]
       c0, c1,
       [&](int sl, Fwd2Set<NM>& st) {
         const int tap = 2 * sl + tpar;
-        const uint4* bp = w2 + tap * PRQ + ch;
+        const uint4* bp = w2 + tap * W2T + ch;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           st.bh[h] = bp[h * 16 * W2Q];
@@ -370,12 +372,12 @@ __global__ void __launch_bounds__(NT) cnn_fwd(const float* __restrict__ X, const
         const int o = e / K2, rem = e - o * K2, ci = rem / 25, tap = rem - ci * 25;
         const float x = w2v[u] * SW2;
         const _Float16 hi = (_Float16)x, lo = (_Float16)(x - (float)hi);
-        _Float16* rec = w2h + (size_t)(o * W2Q + tap * PRQ) * 8 + (ci & 7);
+        _Float16* rec = w2h + (size_t)(o * W2Q + tap * W2T) * 8 + (ci & 7);
         rec[8 * (ci >> 3)] = hi;
         rec[8 * (2 + (ci >> 3))] = lo;
       }
     }
-    if (tid < C2 * PRQ) w2q[(tid >> 2) * W2Q + (K1 * PRQ) + (tid & 3)] = make_uint4(0u, 0u, 0u, 0u);   // tap 25
+    if (tid < C2 * PRQ) w2q[(tid >> 2) * W2Q + (K1 * W2T) + (tid & 3)] = make_uint4(0u, 0u, 0u, 0u);   // tap 25
   }
   __syncthreads();
 

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 6: CFed kernels, conflict-free staging lane orders (W2 and the per-sample records) - CNN tests, diagnostics,
-# interleaved cfed128 suite lines (base = HEAD, new = staging lane orders) and kernel traces.
+# Round 6: CFed forward W2 tap records padded to 5 chunks (staging stores 12-way -> 6.5-way) - CNN tests, diagnostics,
+# interleaved cfed128 suite lines (base = HEAD, new = padded W2 records) and kernel traces.
 source "$(dirname "$0")/gpu_step.sh"
 step cnn_tests 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_cnn.py
 for v in base new; do
