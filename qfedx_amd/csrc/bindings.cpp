@@ -96,7 +96,7 @@ int qfx_launch_fedavg(const float* theta_k, const float* theta_g, const unsigned
                       const uint32_t* sa_seeds, const int* sa_sign, const int* sa_round, int sa_n, double sa_scale,
                       int sa_bits, long long* sa_masks, const int* norm_cid, float* fa_theta, double* fa_out,
                       unsigned* fa_cnt, int fa_bits, double fa_ring_scale, int fa_n_norms, const float* dp_scale,
-                      hipStream_t st);
+                      int sa_pairsym, hipStream_t st);
 }
 
 namespace qfx_runtime {
@@ -500,7 +500,7 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
             int64_t sa_bits, c10::optional<torch::Tensor> sa_masks, c10::optional<torch::Tensor> norm_cid,
             c10::optional<torch::Tensor> fa_theta, c10::optional<torch::Tensor> fa_out,
             c10::optional<torch::Tensor> fa_cnt, int64_t fa_bits, double fa_scale, int64_t fa_n_norms,
-            c10::optional<torch::Tensor> dp_scale) {
+            c10::optional<torch::Tensor> dp_scale, bool sa_pairsym) {
   need(theta_k, torch::kFloat32, "theta_k");
   need(sat, torch::kInt64, "sat");
   if (sat.numel() < 1) throw std::invalid_argument("fedavg: sat counter missing");
@@ -537,6 +537,9 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
     if (sa_seeds->numel() < (int64_t)K * sa_n * 2 || sa_round->numel() < 1)
       throw std::invalid_argument("fedavg: SecAgg table sizes");
     if (sa_bits < 2 || sa_bits > 62 || !(sa_scale > 0)) throw std::invalid_argument("fedavg: SecAgg bits / scale");
+    // pair-symmetric mask generation: the caller vouches that row k is client k and every client is a row
+    if (sa_pairsym && (sa_n != K || K > 128 || sa_sign->size(0) != K))
+      throw std::invalid_argument("fedavg: pair-symmetric SecAgg masks need a square [K, K] table, K <= 128");
     if (!sa_masks.has_value()) throw std::invalid_argument("fedavg: SecAgg needs a [K, P + 1] mask workspace");
     need(*sa_masks, torch::kInt64, "sa_masks");
     if (sa_masks->numel() < (int64_t)K * (P + 1)) throw std::invalid_argument("fedavg: SecAgg mask workspace size");
@@ -576,7 +579,7 @@ void fedavg(torch::Tensor theta_k, torch::Tensor theta_g, torch::Tensor angle_ma
                           sa ? ptr<long long>(*sa_masks) : nullptr, nc ? ptr<int>(*norm_cid) : nullptr,
                           fa ? ptr<float>(*fa_theta) : nullptr, fa ? ptr<double>(*fa_out) : nullptr,
                           fa ? ptr<unsigned>(*fa_cnt) : nullptr, (int)fa_bits, fa_scale, (int)fa_n_norms,
-                          ds ? ptr<float>(*dp_scale) : nullptr, cur_stream()),
+                          ds ? ptr<float>(*dp_scale) : nullptr, sa_pairsym ? 1 : 0, cur_stream()),
         "qfx_fedavg");
 }
 

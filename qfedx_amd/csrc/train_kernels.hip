@@ -353,6 +353,131 @@ __global__ void __launch_bounds__(256) qfx_secagg_mask_kernel(SecAgg sa, int P) 
     if (e0 + i <= P) row[e0 + i] = a[i];
 }
 
+// The same masks when the table is square (full graph, row k = client k, every client local: one rank): a pair's
+// stream is the same Philox stream for both of its clients (one shared seed, opposite signs), so it is generated
+// once and added to both rows - half the generator calls of the per-client kernel, bitwise the same integer sums.
+// A workgroup (4 waves) owns SaPs<EPB>::NB consecutive Philox blocks; wave w owns blocks w + 4 t (t < NT) of every
+// row.  Its lanes walk the pairs in round-robin order (circle method: the K/2 pairs of a round are disjoint), so
+// within a wave no two lanes touch one accumulator and no other wave touches it at all: plain LDS adds, no atomics.
+// Each (block, row) keeps a + and a - accumulator ([NB][2][EPB][K] int64, K x 512 bytes; rows innermost, so the
+// lanes' distinct rows spread over the banks): a lane adds its mask words to the one its sign selects (one 64-bit
+// add per word; the difference is taken at the end).  A lane's pair (rows, signs, key words - per lane, so the key
+// schedule is VALU work here) serves NT generator calls, run as NT interleaved Philox chains (one round key per
+// round for all of them: the ILP that 2 waves per SIMD need), with the next pair's table loads in flight.
+template <int EPB> struct SaPs {
+  static constexpr int NT = 8 / EPB;                   // generator calls per lane and pair
+  static constexpr int NB = 4 * NT;                    // Philox blocks per workgroup
+};
+template <int NT>
+__device__ __forceinline__ void philox_multi(u32x4 (&c)[NT], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      uint32_t hi0, lo0, hi1, lo1;
+      mulhilo32(0xD2511F53u, c[t].x, hi0, lo0);
+      mulhilo32(0xCD9E8D57u, c[t].z, hi1, lo1);
+      c[t] = {hi1 ^ c[t].y ^ k0, lo1, hi0 ^ c[t].w ^ k1, lo0};
+    }
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+}
+template <int EPB>
+__global__ void __launch_bounds__(256) qfx_secagg_pairsym_kernel(SecAgg sa, int K, int P) {
+  constexpr int NT = SaPs<EPB>::NT, NB = SaPs<EPB>::NB;
+  extern __shared__ long long sacc[];                  // [NB][2][EPB][K]
+  const int tid = threadIdx.x, slot = tid & 63, bl = tid >> 6;
+  const long base = (long)blockIdx.x * NB;             // first Philox block of the workgroup
+  for (int e = tid; e < NB * K * 2 * EPB; e += 256) sacc[e] = 0;
+  __syncthreads();
+  const int Kp = K + (K & 1), R = Kp - 1, half = Kp >> 1;
+  const int nq = (half + 63) >> 6, nit = R * nq;       // lane iterations: (round, pair slot + 64 q)
+  const uint32_t rnd = (uint32_t)sa.round[0];
+  int nlive = 0;                                       // this wave's blocks that hold elements <= P (a prefix)
+#pragma unroll
+  for (int t = 0; t < NT; ++t) nlive += (long)EPB * (base + bl + 4 * t) <= P;
+  struct Pair { int k, j, sk, sj; uint32_t k0, k1; };
+  auto fetch = [&](int it) {
+    Pair q{0, 0, 0, 0, 0u, 0u};
+    if (it >= nit) return q;
+    const int r = it / nq, i = slot + 64 * (it - r * nq);
+    if (i >= half) return q;
+    int a = r, b = Kp - 1;                             // i == 0: the fixed player
+    if (i > 0) {
+      a = r + i;
+      if (a >= R) a -= R;
+      b = r - i;
+      if (b < 0) b += R;
+    }
+    if (a >= K || b >= K) return q;                    // the odd-K bye
+    q.k = min(a, b);
+    q.j = max(a, b);
+    q.sk = sa.sign[(size_t)q.k * sa.N + q.j];
+    q.sj = sa.sign[(size_t)q.j * sa.N + q.k];
+    const uint32_t* key = sa.seeds + ((size_t)q.k * sa.N + q.j) * 2;
+    q.k0 = key[0];
+    q.k1 = key[1];
+    return q;
+  };
+  const uint64_t wm = (uint64_t)sa.mask;
+  Pair nx = fetch(0);
+  for (int it = 0; it < nit; ++it) {
+    const Pair cu = nx;
+    nx = fetch(it + 1);
+    if ((cu.sk | cu.sj) == 0) continue;
+    // accumulator slots: element index of (row, sign half) within a block's [2][EPB][K] plane.  Every slot this
+    // lane updates is read before the generator runs (the LDS latency hides behind it) and written after, a zero
+    // sign adding 0 (the slot is this lane's in this round either way)
+    const int ok = (cu.sk < 0) * EPB * K + cu.k, oj = (cu.sj < 0) * EPB * K + cu.j;
+    const uint64_t zk = cu.sk ? ~0ull : 0ull, zj = cu.sj ? ~0ull : 0ull;
+    long long vk[NT][EPB], vj[NT][EPB];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const long long* row = sacc + (size_t)(bl + 4 * t) * K * 2 * EPB;
+#pragma unroll
+      for (int e = 0; e < EPB; ++e) {
+        vk[t][e] = row[ok + e * K];
+        vj[t][e] = row[oj + e * K];
+      }
+    }
+    u32x4 o[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const long blk = base + bl + 4 * t;
+      o[t] = {(uint32_t)blk, (uint32_t)((uint64_t)blk >> 32), rnd, 0x5ECu};
+    }
+    philox_multi<NT>(o, cu.k0, cu.k1);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (t >= nlive) break;
+      uint64_t m[EPB];
+      if constexpr (EPB == 2) {
+        m[0] = ((uint64_t)o[t].y << 32 | o[t].x) & wm;
+        m[1] = ((uint64_t)o[t].w << 32 | o[t].z) & wm;
+      } else {
+        m[0] = o[t].x & wm;
+        m[1] = o[t].y & wm;
+        m[2] = o[t].z & wm;
+        m[3] = o[t].w & wm;
+      }
+      long long* row = sacc + (size_t)(bl + 4 * t) * K * 2 * EPB;
+#pragma unroll
+      for (int e = 0; e < EPB; ++e) {
+        row[ok + e * K] = vk[t][e] + (long long)(m[e] & zk);
+        row[oj + e * K] = vj[t][e] + (long long)(m[e] & zj);
+      }
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < K * NB * EPB; idx += 256) {   // row k: NB EPB consecutive elements
+    const int k = idx / (NB * EPB), rest = idx % (NB * EPB);
+    const long el = (long)EPB * base + rest;
+    const long long* a = sacc + ((size_t)(rest / EPB) * 2 * EPB + rest % EPB) * K + k;
+    if (el <= P) sa.masks[(size_t)k * (P + 1) + el] = a[0] - a[(size_t)EPB * K];
+  }
+}
+
 __device__ __forceinline__ long long secagg_masks(const SecAgg& sa, int k, long e, int P) {
   return sa.masks[(size_t)k * (P + 1) + e];
 }
@@ -1023,7 +1148,7 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
                                  const int* sa_round, int sa_n, double sa_scale, int sa_bits, long long* sa_masks,
                                  const int* norm_cid, float* fa_theta, double* fa_out, unsigned* fa_cnt,
                                  int fa_bits, double fa_ring_scale, int fa_n_norms, const float* dp_scale,
-                                 hipStream_t st) {
+                                 int sa_pairsym, hipStream_t st) {
   if (dp) {   // clipping needs the per-client norms; without DP they are not computed
     const int nc = (P + NORM_CHUNK - 1) / NORM_CHUNK;
     double* partial = norms + K;   // scratch tail of the norms buffer: K * nc doubles
@@ -1037,8 +1162,19 @@ extern "C" int qfx_launch_fedavg(const float* theta_k, const float* theta_g, con
   if (sa_seeds) {
     if (!sa_masks) return (int)hipErrorInvalidValue;
     const long nblk = (P + 1 + epb - 1) / epb;
-    hipLaunchKernelGGL(qfx_secagg_mask_kernel, dim3((unsigned)((nblk + 255) / 256), (unsigned)K), dim3(256), 0,
-                       st, sa, P);
+    if (sa_pairsym) {   // square table (host-checked: N == K <= 128, row k = client k)
+      const size_t lds = (size_t)K * 512;             // [NB][2][EPB][K] int64 (NB x EPB = 32)
+      if (K > 128) return (int)hipErrorInvalidValue;
+      if (epb == 2)
+        hipLaunchKernelGGL(qfx_secagg_pairsym_kernel<2>, dim3((unsigned)((nblk + SaPs<2>::NB - 1) / SaPs<2>::NB)),
+                           dim3(256), lds, st, sa, K, P);
+      else
+        hipLaunchKernelGGL(qfx_secagg_pairsym_kernel<4>, dim3((unsigned)((nblk + SaPs<4>::NB - 1) / SaPs<4>::NB)),
+                           dim3(256), lds, st, sa, K, P);
+    } else {
+      hipLaunchKernelGGL(qfx_secagg_mask_kernel, dim3((unsigned)((nblk + 255) / 256), (unsigned)K), dim3(256), 0,
+                         st, sa, P);
+    }
   }
   const unsigned blocks = (unsigned)((P + FA_E - 1) / FA_E) + (pack_buf ? 1u : 0u);
   // the fused apply reads the whole [P + 6 + n_norms] buffer this launch writes: it needs the pack block and the

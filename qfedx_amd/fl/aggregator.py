@@ -111,7 +111,13 @@ class Aggregator:
                     seeds, sign = self.secagg.round_tables(client_ids, parts, dropped or [], n_all, round_num)
                     secagg_tabs = (h2d(seeds, self.device), h2d(sign, self.device),
                                    h2d(torch.tensor([round_num], dtype=torch.int32), self.device))
-                sa = (*secagg_tabs, self.secagg.scale, self.secagg.bits)
+                # a square full-graph table (row k = client k, all clients here) lets the kernel generate each
+                # pair's mask stream once for both clients
+                ids = [int(c) for c in client_ids]
+                pairsym = (getattr(self.secagg, "graph", "full") == "full" and ids == list(range(len(ids)))
+                           and secagg_tabs[1].dim() == 2 and tuple(secagg_tabs[1].shape) == (len(ids), len(ids))
+                           and len(ids) <= 128)
+                sa = (*secagg_tabs, self.secagg.scale, self.secagg.bits, pairsym)
             out, norms, sat = fedavg_hip.fused_local_reduce(
                 theta_k, theta_g, weights, self._mask_u8, client_ids, round_num, self.seed,
                 wrap=self.wrap, dp=self.dp, clip_norm=self.clip_norm,

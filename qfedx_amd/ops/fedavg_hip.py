@@ -1,6 +1,8 @@
 """Python entry points of the fused aggregation / optimizer kernels (``csrc/train_kernels.hip``)."""
 from __future__ import annotations
 
+import os
+
 import torch
 
 from ..utils.device import h2d
@@ -20,6 +22,7 @@ def sgdm_step(params, grads, buf, t_in, t_out, active, lr, mu, keep_state: bool 
 
 _NO_KEYS = {}
 _NO_PACK = {}
+_PAIRSYM = os.environ.get("QFEDX_SECAGG_PAIRSYM", "1") != "0"   # A/B knob: per-client mask generation
 
 
 def dp_noise_keys(client_ids, round_num, seed) -> torch.Tensor:
@@ -41,9 +44,11 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
     block of the same launch packs the round metrics into its tail (what ``round_pack`` does on its own).
     ``sat``: int64 [1] device counter that receives the number of fixed-point terms clamped at 2^53 (with
     ``pack``: ``buf[P + 5]``, zeroed by ``round_apply``; else a fresh zero counter).
-    ``secagg`` = (seeds int32 [K, N, 2], sign int32 [K, N], round int32 [1] device tensors, scale, bits): the
-    [P + 1] head holds SecAgg ring elements instead, each client's term masked in the kernel
-    (``SecureAggregator.round_tables``).  ``norm_cid`` (device int32 [K] global client ids; needs ``pack`` and
+    ``secagg`` = (seeds int32 [K, N, 2], sign int32 [K, N], round int32 [1] device tensors, scale, bits[,
+    pairsym]): the [P + 1] head holds SecAgg ring elements instead, each client's term masked in the kernel
+    (``SecureAggregator.round_tables``).  ``pairsym``: the table is square (full graph, row k = client k, every
+    client a row) - each pair's mask stream is generated once for both of its clients (``QFEDX_SECAGG_PAIRSYM=0``
+    turns it off; bitwise the same masks).  ``norm_cid`` (device int32 [K] global client ids; needs ``pack`` and
     DP): the pack block scatters the clients' pre-clip norms into ``buf[P + 6 + id]`` (CC6).
     ``apply`` = (theta [P] float32, outs float64 [6 + n_norms], counter int32 [1] zeroed, bits, ring scale,
     n_norms): single-rank rounds (no collective between reduce and apply) - the launch's last block also does
@@ -80,5 +85,6 @@ def fused_local_reduce(theta_k, theta_g, weights, angle_mask, client_ids, round_
                     int(secagg[4]), torch.empty(K * (P + 1), dtype=torch.int64, device=dev))
                    if secagg is not None else (None, None, None, 1.0, 48, None)),
                  norm_cid, *(apply if apply is not None else (None, None, None, 0, 1.0, 0)),
-                 dp_scale.float().contiguous() if (dp and dp_scale is not None) else None)
+                 dp_scale.float().contiguous() if (dp and dp_scale is not None) else None,
+                 bool(secagg is not None and len(secagg) > 5 and secagg[5] and _PAIRSYM))
     return out, (norms[:K] if dp else None), sat

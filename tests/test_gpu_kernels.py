@@ -447,6 +447,45 @@ def test_secagg_sparse_graph_in_fused_reduce_match_host_protocol(cuda):
     assert torch.equal(b.cpu() & m, a & m)
 
 
+@pytest.mark.parametrize("K,bits,P", [(6, 48, 301), (7, 32, 301), (128, 48, 1037), (127, 32, 515)])
+def test_secagg_pair_symmetric_masks_are_bitwise(cuda, K, bits, P):
+    """Square full-graph table (one rank holds every client, row k = client k): the pair-symmetric mask kernel
+    generates each pair's stream once for both clients.  Its masked local sum is bitwise the per-client kernel's and
+    (small K) the host protocol's, with non-participants and dropped clients in the table, odd K (the round-robin
+    bye) and P + 1 not a multiple of a workgroup's 8 Philox blocks."""
+    from qfedx_amd.fl.aggregator import Aggregator
+    from qfedx_amd.ops import fedavg_hip
+    from qfedx_amd.privacy.secure_agg import SecureAggregator
+    from qfedx_amd.utils.device import h2d
+    g = torch.Generator().manual_seed(K)
+    tk = torch.randn(K, P, generator=g) * 0.3
+    tg = torch.randn(P, generator=g)
+    w = torch.rand(K, generator=g).double() * 40 + 1
+    ids = list(range(K))
+    participants = [c for c in ids if c % 5 != 4]        # clients 4, 9, ... sit the round out
+    dropped = [1, K - 2]
+    sa = SecureAggregator(321, bits=bits, scale=2.0 ** 24 if bits > 32 else 2.0 ** 16)
+    kw = dict(dp=False, seed=5, secure_agg=True, secagg=sa, num_clients=K)
+    gpu = Aggregator(P, torch.zeros(P), cuda, "hip", wrap=False, **kw)
+    seeds, sign = sa.round_tables(ids, participants, dropped, K, 3)
+    tabs = (h2d(seeds, cuda), h2d(sign, cuda), h2d(torch.tensor([3], dtype=torch.int32), cuda))
+    outs = []
+    for pairsym in (False, True):
+        out, _, _ = fedavg_hip.fused_local_reduce(
+            tk.to(cuda), tg.to(cuda), w.to(cuda), torch.zeros(P, dtype=torch.uint8, device=cuda), ids, 3, 5,
+            wrap=False, dp=False, clip_norm=1.0, noise_multiplier=0.0, secagg=(*tabs, sa.scale, sa.bits, pairsym))
+        outs.append(out.cpu())
+    m = (1 << sa.bits) - 1
+    assert torch.equal(outs[0], outs[1])
+    b = gpu.local_reduce(tk.to(cuda), tg.to(cuda), w.to(cuda), 3, ids, participants=participants, dropped=dropped)
+    assert torch.equal(b.cpu(), outs[1])                 # the aggregator takes the pair-symmetric path itself
+    if K <= 8:                                           # every client participates and survives: host protocol
+        cpu = Aggregator(P, torch.zeros(P), "cpu", "torch", wrap=False, **kw)
+        a = cpu.local_reduce(tk, tg, w, 3, ids, participants=ids, dropped=[])
+        b = gpu.local_reduce(tk.to(cuda), tg.to(cuda), w.to(cuda), 3, ids, participants=ids, dropped=[])
+        assert torch.equal(b.cpu() & m, a & m)
+
+
 @pytest.mark.parametrize("dp,bits", [(False, 48), (True, 48), (False, 32), (True, 32)])
 def test_secagg_masks_in_fused_reduce_match_host_protocol(cuda, dp, bits):
     """SecAgg on the device (K18): the fused FedAvg kernel masks every local client's ring element with the pairwise
