@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
                                                               float* __restrict__ params,
                                                               float* __restrict__ grad, int p_stride, QfxAdamArgs ad,
                                                               QfxReadoutRed ro, QfxFedTail ft) {
-  // 8 groups of 32 lanes split the client's (sample, tile) rows; 4 independent loads in flight per lane; the
+  // 8 groups of 32 lanes split the client's (sample, tile) rows; 16 independent loads in flight per lane; the
   // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
   const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
   if (g == n_gradops) {
@@ -66,20 +66,24 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     const int R = spc * nt;
     __shared__ long long part[8][32];
     __shared__ double pt[32];
-    long long acc[4] = {0, 0, 0, 0};
     auto row = [&](int r) -> long long {
       const int s = k * spc + r / nt, t = r % nt;
       return gslab[(((size_t)s * slab_tiles + t) * n_gradops + g) * 32 + lane];
     };
+    // RU rows per lane in flight: the slab rows come from other XCDs' passes (an L2 miss each), and a 4-deep chain
+    // made the 8-client reduction 8 dependent round trips long
+    constexpr int RU = 16;
+    long long tot = 0;
     int r = grp;
-    for (; r + 24 < R; r += 32) {
-      acc[0] += row(r);
-      acc[1] += row(r + 8);
-      acc[2] += row(r + 16);
-      acc[3] += row(r + 24);
+    for (; r + 8 * (RU - 1) < R; r += 8 * RU) {
+      long long v[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) v[u] = row(r + 8 * u);
+#pragma unroll
+      for (int u = 0; u < RU; ++u) tot += v[u];
     }
-    for (; r < R; r += 8) acc[0] += row(r);
-    part[grp][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    for (; r < R; r += 8) tot += row(r);
+    part[grp][lane] = tot;
     __syncthreads();
     if (tid < 32) {
       long long v = 0;
