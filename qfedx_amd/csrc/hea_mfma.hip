@@ -1364,9 +1364,14 @@ extern "C" int HEA_EXT(qfx_hea_pass)(int adjoint, const HEA_NS::PassArgs* args, 
 
 
 // Debug build: synchronise the stream and return (and clear) the first failed device-check line, 0 if none;
-// -1 in the release build (no checks compiled).
+// -1 in the release build (no checks compiled).  A launch recorded into a graph under capture is not checked here
+// (a synchronise would invalidate the capture): its checks fire when the graph replays and are read at the next
+// eager launch's check.
 extern "C" int HEA_EXT(qfx_hea_check_status)(hipStream_t st) {
 #if QFX_CHECKS_ON
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return -2;
+  if (cs != hipStreamCaptureStatusNone) return 0;
   if (hipStreamSynchronize(st) != hipSuccess) return -2;
   unsigned int v = 0, z = 0;
   if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(qfx_check_word), sizeof(v)) != hipSuccess) return -2;
