@@ -363,7 +363,8 @@ __global__ void __launch_bounds__(256) qfx_secagg_mask_kernel(SecAgg sa, int P) 
 // lanes' distinct rows spread over the banks): a lane adds its mask words to the one its sign selects (one 64-bit
 // add per word; the difference is taken at the end).  A lane's pair (rows, signs, key words - per lane, so the key
 // schedule is VALU work here) serves NT generator calls, run as NT interleaved Philox chains (one round key per
-// round for all of them: the ILP that 2 waves per SIMD need), with the next pair's table loads in flight.
+// round for all of them: the ILP that 2 waves per SIMD need), with the next pair's table loads in flight and its
+// LDS slots read before the generator runs (profiles/r6_secagg_pairsym_ab.txt: each of these steps measured).
 template <int EPB> struct SaPs {
   static constexpr int NT = 8 / EPB;                   // generator calls per lane and pair
   static constexpr int NB = 4 * NT;                    // Philox blocks per workgroup
