@@ -20,12 +20,12 @@ __global__ void __launch_bounds__(256) hea_frag_kernel(const float* __restrict__
 // the op's tiles, then per real qubit j (slots 8j + 4y + 2x + comp = n_j[y][x].(re, im))
 //   d/dtheta = Im(e^{-i phi} n10 + e^{i phi} n01),   d/dphi = Im(n00 - n11).
 //
-// Optional Adam epilogue (ad.m != nullptr; the local optimizer step fused into this launch): the last of a client's
-// gridDim.y blocks to finish - arrival counter ad.cnt[k], reset by that block - updates the client's parameter row
-// from the complete gradient row, with the element update of qfx_adam_kernel (qfx_adam.h): bitwise the separate
-// launch.  The arrivals are the n_gradops gradient-record blocks PLUS, with the fused readout, the g == n_gradops
-// block that writes the readout-parameter gradients: the Adam step must wait for all gridDim.y = n_gradops + 1 of
-// them (the launcher sizes the grid so).  Every block has read its parameters before it arrives.
+// Optional Adam epilogue (ad.m != nullptr; the local optimizer step fused into this launch): Adam is elementwise,
+// and every parameter's gradient is formed by exactly one block (its gradient op's, or the readout block's for the
+// readout parameters; the host checks the cover, HeaMfmaProgram.grad_cover_exact), so each block updates the
+// parameters it owns right after forming their gradients, with the element update of qfx_adam_kernel (qfx_adam.h):
+// bitwise the separate launch, and no per-client hand-off.  A block reads only its own op's parameters (before it
+// updates them).  Block (k, 0) writes the client's step counter.
 #if !QFX_HEA_BF16
 __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* __restrict__ gslab, int slab_tiles,
                                                               int n_gradops, const int* __restrict__ gmeta, int spc,
@@ -35,6 +35,19 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
   // 8 groups of 32 lanes split the client's (sample, tile) rows; 16 independent loads in flight per lane; the
   // int64 sums are exact, so the group split and the LDS combine do not change a bit of the result
   const int k = blockIdx.x, g = blockIdx.y, tid = threadIdx.x, lane = tid & 31, grp = tid >> 5;
+  // fused Adam of one owned parameter i (row k) from its gradient, then - the round's last local step - the
+  // client's exact FedAvg term of it into the round buffer
+  const double SC = 4294967296.0;
+  int nsat = 0;
+  auto owned_step = [&](int i, float gi) {
+    const long e = (long)k * p_stride + i;
+    qfx_adam_elem(params, gi, ad.m, ad.v, ad.t_in, ad.t_out, ad.active, k, e, false, ad.lr, ad.b1, ad.b2, ad.eps);
+    if (!ft.buf) return;
+    double d = (double)params[e] - (double)ft.theta_g[i];
+    if (ft.wrap && ft.mask[i]) d = qfx::wrap_pi(d);
+    const long long v = qfx::fixed_term(ft.weights[k] * d * SC, nsat);
+    if (v) atomicAdd((unsigned long long*)&ft.buf[i], (unsigned long long)v);
+  };
   if (g == n_gradops) {
     // fused readout: the client's per-sample records summed in a fixed order - loss, hits, and the readout gradients
     // d/da_c = sum dl_c z_c, d/db_c = sum dl_c.  Thread t < GS * NV sums value q = t % NV of samples t / NV + GS i
@@ -52,9 +65,10 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     if (tid < NV) {
       float tot = 0.f;
       for (int j = 0; j < GS; ++j) tot += rs[j * NV + tid];
-      if (tid < 2 * ro.C)
+      if (tid < 2 * ro.C) {
         grad[(size_t)k * p_stride + ro.n_theta + tid] = tot;
-      else if (tid == 2 * ro.C)
+        if (ad.m) owned_step(ro.n_theta + tid, tot);
+      } else if (tid == 2 * ro.C)
         ro.loss[k] = tot;
       else
         ro.correct[k] = tot;
@@ -94,67 +108,48 @@ __global__ void __launch_bounds__(256) hea_grad_reduce_kernel(const long long* _
     if (tid < nreal) {
       const double* p = pt + 8 * tid;
       const float* prm = params + (size_t)k * p_stride;
+      float gth, gph;
       if (inside) {
         // at the op input: d/dtheta = Im<lam|X|psi> = Im(n01 + n10);
         // d/dphi = Im<lam|RX^H Z RX|psi> = cos(theta) Im(n00 - n11) + sin(theta) Re(n01 - n10)
         const double th = prm[m[2 + tid]];
         const double ct = cos(th), st = sin(th);
-        grad[(size_t)k * p_stride + m[2 + tid]] = (float)(p[3] + p[5]);
-        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
+        gth = (float)(p[3] + p[5]);
+        gph = (float)(ct * (p[1] - p[7]) + st * (p[2] - p[4]));
       } else {
         const double ph = prm[m[6 + tid]];
         const double cp = cos(ph), sp = sin(ph);
-        grad[(size_t)k * p_stride + m[2 + tid]] = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
-        grad[(size_t)k * p_stride + m[6 + tid]] = (float)(p[1] - p[7]);
+        gth = (float)((cp * p[5] - sp * p[4]) + (cp * p[3] + sp * p[2]));
+        gph = (float)(p[1] - p[7]);
+      }
+      grad[(size_t)k * p_stride + m[2 + tid]] = gth;
+      grad[(size_t)k * p_stride + m[6 + tid]] = gph;
+      if (ad.m) {
+        owned_step(m[2 + tid], gth);
+        owned_step(m[6 + tid], gph);
       }
     }
   }
   if (!ad.m) return;
-  __shared__ int last_s;
-  // The block's gradient stores are complete in L2 after the barrier; ONE agent-scope release (thread 0) makes
-  // them visible across XCDs before the arrival.  A release is an L2 writeback on this chip: issued by every
-  // thread it made the launch 7x slower (16q x 64 clients: 13 -> 98 us).
+  if (g == 0 && tid == 0) {
+    ad.t_out[k] = ad.t_in[k] + ad.active[k];          // the client's step counter (qfx_adam_elem's `first`)
+    if (ft.buf) {
+      const long long v = qfx::fixed_term(ft.weights[k] * SC, nsat);
+      if (v) atomicAdd((unsigned long long*)&ft.buf[p_stride], (unsigned long long)v);
+    }
+  }
+  if (!ft.buf) return;
+  // ---- the round's FedAvg (QfxFedTail): every block added its owned parameters' terms above; the last block of
+  // the launch packs the metrics and (single rank) applies the round
+  if (nsat) atomicAdd((unsigned long long*)&ft.buf[p_stride + 5], (unsigned long long)nsat);   // saturated terms
+  __shared__ int flast_s;
+  // The block's stores and atomics are complete in L2 after the barrier; ONE agent-scope release (thread 0) makes
+  // them visible across XCDs before the arrival (issued by every thread, a release - an L2 writeback here - made
+  // the launch 7x slower: 16q x 64 clients, 13 -> 98 us).
   __syncthreads();
   if (tid == 0) {
     __threadfence();
-    const unsigned prev = atomicAdd(&ad.cnt[k], 1u);
-    last_s = prev == (unsigned)(gridDim.y - 1);
-    if (last_s) ad.cnt[k] = 0u;                       // ready for the next launch
-  }
-  __syncthreads();
-  if (!last_s) return;
-  if (tid == 0) {                                     // consumer side: one agent-scope acquire, drained
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  for (int i = tid; i < p_stride; i += 256) {
-    const long e = (long)k * p_stride + i;
-    // device-coherent load: other blocks (other CUs) wrote these entries
-    const float gi = __hip_atomic_load(&grad[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    qfx_adam_elem(params, gi, ad.m, ad.v, ad.t_in, ad.t_out, ad.active, k, e, i == 0, ad.lr, ad.b1, ad.b2, ad.eps);
-  }
-  if (!ft.buf) return;
-  // ---- the round's FedAvg (QfxFedTail): client k's terms from the row this block just updated
-  const double SC = 4294967296.0;
-  int nsat = 0;
-  __syncthreads();                                     // the block's own Adam stores, visible to the block
-  for (int e = tid; e < p_stride; e += 256) {
-    double d = (double)params[(size_t)k * p_stride + e] - (double)ft.theta_g[e];
-    if (ft.wrap && ft.mask[e]) d = qfx::wrap_pi(d);
-    const long long v = qfx::fixed_term(ft.weights[k] * d * SC, nsat);
-    if (v) atomicAdd((unsigned long long*)&ft.buf[e], (unsigned long long)v);
-  }
-  if (tid == 0) {
-    const long long v = qfx::fixed_term(ft.weights[k] * SC, nsat);
-    if (v) atomicAdd((unsigned long long*)&ft.buf[p_stride], (unsigned long long)v);
-  }
-  if (nsat) atomicAdd((unsigned long long*)&ft.buf[p_stride + 5], (unsigned long long)nsat);   // saturated terms
-  __shared__ int flast_s;
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();                                   // this client's terms published before its arrival
-    flast_s = atomicAdd(ft.cnt, 1u) == gridDim.x - 1;
+    flast_s = atomicAdd(ft.cnt, 1u) == gridDim.x * gridDim.y - 1;
     if (flast_s) *ft.cnt = 0u;
   }
   __syncthreads();

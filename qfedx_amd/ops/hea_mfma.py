@@ -116,6 +116,13 @@ class HeaMfmaProgram:
         J = len(progs_f)
         progs_a = pass_programs(plan_a, gmeta)
         self.n_gradops = len(gmeta)
+        # the fused Adam epilogue of hea_grad_reduce updates each parameter in the block that formed its gradient:
+        # it needs every theta parameter owned by exactly one gradient record (else the separate Adam launch runs)
+        owned = []
+        for row in gmeta:
+            nr = int(row[1]) & 15
+            owned += [int(v) for v in row[2:2 + nr]] + [int(v) for v in row[6:6 + nr]]
+        self.grad_cover_exact = sorted(owned) == list(range(self.n_theta))
         if self.fwd_last < J - 1:
             pr, fr_ops, ar = progs_f[self.fwd_last]
             fr_ops = np.concatenate([fr_ops, obs_table(fplan, pr, OP_READOUT)[None]], 0)
@@ -595,7 +602,9 @@ class HeaMfmaProgram:
         # 33.6 us against 13 + 5.4 us for the two launches; at the 8-client share (104 blocks) it saves a launch
         # (round 387 -> 382 us; profiles/r3_fused_adam_ab.txt).
         ro_rows = 1 if self._fused_readout(noise) else 0
-        want = K * (self.n_gradops + ro_rows) <= FUSED_ADAM_MAX_BLOCKS
+        # (the readout parameters are owned by the fused readout block, and the row must hold nothing else)
+        want = (K * (self.n_gradops + ro_rows) <= FUSED_ADAM_MAX_BLOCKS and ro_rows == 1 and self.grad_cover_exact
+                and p.shape[1] == self.n_theta + 2 * self.C)
         if want and fused_opt is not None and self.n_gradops > 0 and p.data_ptr() == params.data_ptr():
             adam = fused_opt[0].fused_adam(p, fused_opt[1])
         fed = fed_tail if (adam is not None and fed_tail is not None) else None
