@@ -47,8 +47,8 @@ struct HeaPassArgs {
   float* ro_rec;
 };
 
-// Launch arguments of a fused Adam epilogue (m == nullptr: none).  cnt: one zero-initialised arrival counter per
-// client (the client's last block resets it).
+// Launch arguments of a fused Adam epilogue (m == nullptr: none); each gradient block steps the parameters it owns.
+// cnt: per-client counters of the earlier last-block epilogue, unused since round 6 (kept zero).
 struct QfxAdamArgs {
   float* m;
   float* v;
@@ -60,11 +60,11 @@ struct QfxAdamArgs {
 };
 
 // The round's FedAvg folded into hea_grad_reduce's Adam epilogue (a round's last local step, plain FedAvg: no DP, no
-// SecAgg; buf == nullptr: none).  The last block of client k, right after its Adam step, adds the client's exact
-// fixed-point terms round(2^32 w_k wrap(theta_k - theta_g)) and weight round(2^32 w_k) into the all-reduce buffer head
-// with int64 atomics (integer sums: any arrival order gives the same bits, as the FedAvg reduce's own sums), which the
-// round prologue zeroed; the last of the K client epilogues packs the round metrics and, on a single rank, applies
-// the round to theta_g (the FedAvg launch's FusedApply).
+// SecAgg; buf == nullptr: none).  Each block, right after the Adam step of the parameters it owns, adds client k's
+// exact fixed-point terms round(2^32 w_k wrap(theta_k - theta_g)) of them (block (k, 0) also the weight
+// round(2^32 w_k)) into the all-reduce buffer head with int64 atomics (integer sums: any arrival order gives the same
+// bits, as the FedAvg reduce's own sums), which the round prologue zeroed; the last block of the launch packs the
+// round metrics and, on a single rank, applies the round to theta_g (the FedAvg launch's FusedApply).
 struct QfxFedTail {
   long long* buf;            // [P + 6 + n_norms] all-reduce buffer
   const float* theta_g;      // [P]
