@@ -73,7 +73,7 @@ struct QfxFedTail {
   int wrap;
   const float *loss, *correct, *nvalid, *act;   // round metric tables (n_metrics entries each)
   int n_metrics;
-  unsigned* cnt;             // zero-initialised arrival counter of the client epilogues (the last one resets it)
+  unsigned* cnt;             // zero-initialised arrival counter of the launch's blocks (the last one resets it)
   float* apply_theta;        // single rank: theta_g updated in place (nullptr: the all-reduce + apply follow)
   double* apply_out;         // [6 + n_norms] metrics / saturation / weight sum read back by the host
   int n_norms;
